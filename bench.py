@@ -1,0 +1,254 @@
+#!/usr/bin/env python
+"""Benchmark: denoised frames/sec of MDGen's forward-sim denoising on MI355X.
+
+Workload (BASELINE.json configs[1]): tetrapeptide forward simulation, num_frames T=1000,
+crop L=4, default model (5 layers, C=384, 16 heads, IPA prepend), bf16 GEMM/attention
+operands, synthetic seed-derived weights and inputs (no checkpoint/dataset offline).
+
+One bench "step" = one sim_inference rollout window: Sampler.sample_ode('euler', 50) over
+B trajectories of T frames = 49 Euler denoising steps (each a full forward + Euler update)
+plus the window's conditioning precompute, through the drop-in engine call
+(HipEngine.sample_euler: input staging + one hipGraph replay + output copy).
+value = frames denoised per second = ranks * B * T * 49 * steps / max-over-ranks time.
+
+Multi-GPU: inference does not shard (temporal attention couples all T frames of a
+trajectory), so N ranks run N independent replicas of the window ("replicas only",
+scaling "weak"); no collective on the data path.
+
+Extra fields: "roofline" for the dominant kernel (live HIP-event timing on the stream the
+kernel runs on), "cpu_baseline" (the oracle restatement timed on this host's cores).
+"""
+import argparse
+import ctypes
+import json
+import math
+import os
+import sys
+import time
+
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+PEAK_TFLOPS = {"bf16": 2500.0, "f32": 157.3}   # MI355X dense MFMA (MI355X_MICROARCH.md:42-43)
+PEAK_HBM_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10, help="timed rollout windows")
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=8, help="trajectories per GPU")
+    ap.add_argument("--frames", type=int, default=1000)
+    ap.add_argument("--crop", type=int, default=4)
+    ap.add_argument("--num-steps", type=int, default=50, help="ODE grid points (49 Euler steps)")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-graph", action="store_true")
+    return ap.parse_args()
+
+
+def make_model(T, L, seed=0):
+    import argparse as ap_
+
+    from mdgen_finetune_amd import synthetic
+    from mdgen_finetune_amd.model.latent_model import LatentMDGenModel
+
+    args = ap_.Namespace(embed_dim=384, mha_heads=16, num_layers=5, ipa_heads=4, ipa_head_dim=32, ipa_qk=8,
+                         ipa_v=8, dropout=0.0, no_rope=False, prepend_ipa=True, abs_pos_emb=True, crop=L,
+                         num_frames=T, time_multiplier=100.0, sim_condition=True, tps_condition=False)
+    m = LatentMDGenModel(args, 21).eval()
+    synthetic.fill_module_(m, seed)
+    return m
+
+
+def inputs(B, T, L, seed, device):
+    from mdgen_finetune_amd import synthetic
+    from mdgen_finetune_amd.rigid_utils import Rigid, Rotation
+
+    inp = synthetic.make_inputs(seed, B, T, L, 21)
+    g = lambda k: torch.from_numpy(inp[k]).to(device)  # noqa: E731
+    kw = dict(mask=g("mask"), start_frames=Rigid(Rotation(rot_mats=g("rots")), g("trans")), x_cond=g("x_cond"),
+              x_cond_mask=g("x_cond_mask"), aatype=g("aatype"))
+    return g("x"), kw, inp
+
+
+def time_kernel(fn, iters=20):
+    """Average device time of fn() (launches on the current stream) via HIP events."""
+    s = torch.cuda.current_stream()
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(iters):
+        fn()
+    e1.record(s)
+    e1.synchronize()
+    return e0.elapsed_time(e1) / iters * 1e-3
+
+
+def roofline(eng, st, dtype, B, T, L):
+    """Dominant kernel = the temporal flash attention (largest share of the step in the rocprof
+    summary, profiles/).  Algorithmic FLOPs per launch = 4*B*L*H*T*(T+1)*D (QK^T and PV over
+    T+1 keys incl. the bias row, unpadded head_dim D=24)."""
+    from mdgen_finetune_amd import _lib
+
+    lib = eng.lib
+    ws = st.ws.data_ptr()
+    H, D = eng.H, eng.D
+    # workspace offsets (mirror of ws_layout in capi.hip)
+    cs = 2 if dtype == "bf16" else 4
+    a256 = lambda x: (x + 255) // 256 * 256  # noqa: E731
+    N = B * T * L
+    off_qkv_t = a256(N * 3 * H * 32 * cs)
+    off_o = off_qkv_t + a256(3 * B * L * H * T * 32 * cs)
+    off_kb = off_o + a256(N * eng.C * cs) + a256(N * eng.F * cs)
+    kvb = st.kvb[0][1]
+    s = _lib.stream_handle()
+
+    def launch():
+        _lib.check(lib.mdg_attn_temporal(eng.mdg_dtype, B, T, L, H, D, ws + off_qkv_t, ws + off_kb, kvb.data_ptr(),
+                                         ws + off_o, s), "attn_temporal")
+
+    sec = time_kernel(launch, 50)
+    flops = 4.0 * B * L * H * T * (T + 1) * D
+    achieved = flops / sec / 1e12
+    traffic = None
+    prof = os.path.join(REPO, "profiles", "traffic_attn_temporal.json")
+    if os.path.exists(prof):
+        try:
+            traffic = json.load(open(prof)).get(f"B{B}_T{T}_L{L}_{dtype}")
+        except Exception:
+            traffic = None
+    return {"kernel": "attn_temporal_kernel", "bound": "mfma", "achieved": round(achieved, 2),
+            "peak": PEAK_TFLOPS[dtype], "unit": "TFLOP/s", "frac": round(achieved / PEAK_TFLOPS[dtype], 4),
+            "traffic": traffic, "avg_launch_us": round(sec * 1e6, 2), "flops_per_launch": flops}
+
+
+def cpu_baseline(T, L, seconds):
+    """The oracle (oracle/mdgen_oracle.py, fp32 PyTorch-CPU restatement pinned to the
+    reference) timed on this host: forward + Euler update at B=1 T=1000 L=4, repeated until
+    `seconds` of CPU work."""
+    from mdgen_finetune_amd import synthetic
+    from oracle import mdgen_oracle as O
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    threads = max(1, min(threads, os.cpu_count() or 1))
+    torch.set_num_threads(threads)
+    c = O.Cfg(crop=L)
+    P = O.seeded_params(c, 0)
+    inp = synthetic.make_inputs(1, 1, T, L, 21)
+    f = lambda k: torch.from_numpy(inp[k])  # noqa: E731
+    kw = dict(mask=f("mask"), rots=f("rots"), trans=f("trans"), x_cond=f("x_cond"), x_cond_mask=f("x_cond_mask"),
+              aatype=f("aatype"))
+    x = f("x")
+    dt = float(torch.linspace(0, 1, 50)[1])
+    with torch.no_grad():
+        O.forward(P, c, x, torch.zeros(1), **kw)  # warm
+        n, t0 = 0, time.perf_counter()
+        while True:
+            v = O.forward(P, c, x, torch.zeros(1), **kw)
+            x = x + dt * v
+            n += 1
+            el = time.perf_counter() - t0
+            if el >= seconds or n >= 50:
+                break
+    cpu = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": round(T * n / el, 1), "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": f"{n} denoising steps (oracle forward + Euler update), B=1 T={T} L={L}, fp32, "
+                      f"{el:.1f} s on {threads} threads of {cpu}"}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=dev)
+    from mdgen_finetune_amd.engine import get_engine
+
+    B, T, L = a.batch, a.frames, a.crop
+    m = make_model(T, L).to(dev)
+    m.hip_dtype = a.dtype
+    eng = get_engine(m)
+    zs, kw, _ = inputs(B, T, L, seed=100 + rank, device=dev)
+
+    def window():
+        return eng.sample_euler(zs, num_steps=a.num_steps, use_graph=not a.no_graph, **kw)
+
+    with torch.no_grad():
+        for _ in range(max(1, a.warmup)):
+            ys = window()
+        torch.cuda.synchronize()
+        assert torch.isfinite(ys[-1]).all(), "non-finite samples"
+
+        def barrier():
+            if world > 1:
+                torch.distributed.barrier()
+
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            ys = window()
+        torch.cuda.synchronize()
+        barrier()
+        el = time.perf_counter() - t0
+        if world > 1:
+            tt = torch.tensor([el], device=dev, dtype=torch.float64)
+            torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
+            el = tt.item()
+        n_euler = a.num_steps - 1
+        frames = world * B * T * n_euler * a.steps
+        value = frames / el
+        st = eng._state(B, T, L)
+        roof = roofline(eng, st, a.dtype, B, T, L) if rank == 0 else None
+
+    out = None
+    if rank == 0:
+        cpu = None if (a.no_cpu_baseline or world > 1) else cpu_baseline(T, L, a.cpu_seconds)
+        out = {
+            "metric": "denoised frames/sec, 1000-frame x crop4 forward-sim step, 1/2/4/8 MI355X",
+            "value": round(value, 1),
+            "unit": "frames/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(el / a.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": a.dtype,
+            "data": "synthetic (seed-derived weights and tetrapeptide latents/frames; no checkpoint offline)",
+            "config": {"workload": f"sim_inference rollout window: Euler ODE {n_euler} denoising steps x "
+                                   f"B={B} trajectories x T={T} frames x L={L} residues (+ per-window "
+                                   "conditioning), per GPU",
+                       "model": "LatentMDGenModel default (5 layers, C=384, 16 heads, IPA prepend, abs pos emb)",
+                       "global_batch": B * world, "seq_len": T, "crop": L, "denoise_steps_per_step": n_euler,
+                       "parallelism": f"replicas{world}", "hipgraph": not a.no_graph},
+            "us_per_denoise_step": round(el / a.steps / n_euler * 1e6, 2),
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,163 @@
+/*
+ * mdgen_hip.h — C ABI of libmdgen_hip.so, the MI355X (gfx950) denoising hot path of MDGen.
+ *
+ * Replaces, on the device, the reference's eager-PyTorch forward of one flow-matching
+ * denoising step and the Euler update around it:
+ *   LatentMDGenModel.forward        src/mdgen/model/latent_model.py:216-269
+ *   LatentMDGenLayer.forward        src/mdgen/model/latent_model.py:456-493
+ *   AttentionWithRoPE / MultiheadAttention (rope + bias_kv path)
+ *                                   latent_model.py:329-338, src/mdgen/model/mha.py:161-407
+ *   FinalLayer                      src/mdgen/model/layers.py:58-75
+ *   torchdiffeq Euler step used by Sampler.sample_ode('euler')
+ *                                   src/mdgen/transport/integrators.py:95-114
+ * The reference is pure Python, so there is no reference FFI to mirror; the Python-side
+ * drop-in (mdgen_finetune_amd.model.latent_model.LatentMDGenModel.forward and
+ * mdgen_finetune_amd.transport.Sampler.sample_ode) binds these entry points with ctypes
+ * (INTEGRATION.md shows the binding).
+ *
+ * Contract (every entry point):
+ *   - all tensor arguments are CALLER-OWNED DEVICE pointers, contiguous row-major;
+ *   - `stream` is a hipStream_t (passed as void*); calls are asynchronous and stream-ordered;
+ *   - no allocation, no host synchronisation, no globals: calls are reentrant and
+ *     hipGraph-capturable;
+ *   - return 0 on success, else an MDG_E_* code or a hipError_t (launch failure);
+ *     mdg_last_error_string() (thread-local) describes the last failure.
+ * Token order is n = (b*T + t)*L + l (the reference's [B,T,L,C] layout flattened).
+ */
+#ifndef MDGEN_HIP_H
+#define MDGEN_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MDG_ABI_VERSION 1
+#define MDG_MAX_LAYERS 16
+#define MDG_DP 32 /* padded head dim of every attention operand buffer (head_dim <= 31) */
+
+typedef enum { MDG_F32 = 0, MDG_BF16 = 1 } mdg_dtype;
+
+enum {
+  MDG_OK = 0,
+  MDG_E_SHAPE = 1001, /* unsupported / inconsistent dimensions */
+  MDG_E_DTYPE = 1002, /* unknown dtype enum */
+  MDG_E_ARG = 1003,   /* null pointer or bad enum */
+};
+
+/* GEMM building block: out = epilogue( prologue(A) . W^T + bias ) */
+enum { MDG_A_PLAIN = 0, MDG_A_LNMOD = 1 };
+enum { MDG_EPI_STORE = 0, MDG_EPI_GATE_RES = 1, MDG_EPI_QKV = 2 };
+enum { MDG_ACT_NONE = 0, MDG_ACT_GELU = 1, MDG_ACT_SILU = 2 };
+enum { MDG_QKV_SPATIAL = 0, MDG_QKV_TEMPORAL = 1 };
+
+typedef struct {
+  int32_t B, T, L;    /* batch, frames (num_frames), residues (crop) */
+  int32_t C, H, D, F; /* embed_dim, mha_heads, head_dim = C/H, ffn dim (4C) */
+  int32_t latent;     /* latent channels: 21 (sim), 28 (tps) */
+  int32_t num_layers;
+  int32_t dtype;      /* mdg_dtype of the packed GEMM / attention operands */
+} mdg_dims;
+
+typedef struct {
+  const void* wqkv[2];  /* CT [3C][C], rows q|k|v (nn.Linear layout); [0]=mha_l, [1]=mha_t */
+  const float* bqkv[2]; /* [3C] */
+  const void* wo[2];    /* CT [C][C] out_proj */
+  const float* bo[2];   /* [C] */
+  const float* kvb[2];  /* [H][2][32]: bias_k RoPE-rotated at position S (=L or T), bias_v;
+                           bias_v[D] = 1 (the softmax row sum rides in the pad column) */
+  const void* w1;       /* CT [F][C] fc1 */
+  const float* b1;      /* [F] */
+  const void* w2;       /* CT [C][F] fc2 */
+  const float* b2;      /* [C] */
+} mdg_layer_weights;
+
+typedef struct {
+  mdg_dims dims;
+  const float* w_l2e;   /* latent_to_emb.weight [C][latent] */
+  const float* w_final; /* emb_to_latent.linear.weight [latent][C] */
+  const float* b_final; /* [latent] */
+  const float* rope_l;  /* [L+1][D/2] cos, then [L+1][D/2] sin (spatial) */
+  const float* rope_t;  /* [T+1][D/2] cos, then [T+1][D/2] sin (temporal) */
+  mdg_layer_weights layers[MDG_MAX_LAYERS];
+} mdg_model;
+
+typedef struct {
+  const float* x_in;       /* [N][latent] noisy latents x_t */
+  float* x_out;            /* [N][latent] x_t + dt * v (may alias x_in); null = skip */
+  float* v_out;            /* [N][latent] velocity v; null = skip */
+  const float* base;       /* [N][C] step-invariant embedding (cond_to_emb + mask_to_emb +
+                              pos_embed + biases), from mdg_embed once per window */
+  const float* ipa;        /* [B][L][C] IPA prepend for this step's t (null = none) */
+  const float* mods;       /* [num_layers][B][9C] adaLN chunks for this step's t */
+  const float* mods_final; /* [B][2C] FinalLayer adaLN (shift, scale) */
+  float dt;                /* t_{i+1} - t_i */
+  float* h;                /* [N][C] fp32 residual-stream scratch */
+} mdg_step_io;
+
+typedef struct {
+  int32_t dtype, a_mode, epi, act;
+  int32_t M, N, K;
+  const void* A; int32_t lda; /* PLAIN: CT [M][lda]; LNMOD: fp32 [M][lda], K == row length */
+  const void* W; int32_t ldw; /* CT [N][ldw] */
+  const float* bias;          /* [N] or null */
+  /* LNMOD prologue: y = LN(a; eps) (*ln_w + ln_b); y = y*(1+scale) + shift with
+     shift = mods[(m / rows_per_mod)*mod_stride + shift_off + k] (mods may be null) */
+  const float* mods; int32_t mod_stride, rows_per_mod, shift_off, scale_off;
+  const float* ln_w; const float* ln_b; float ln_eps;
+  /* STORE */
+  void* out; int32_t ldo, out_f32;
+  /* GATE_RES: resid[m][n] += gate[(m/rows_per_mod)*mod_stride + gate_off + n] * v
+     (gate null: += v) */
+  float* resid; int32_t ldr; const float* gate; int32_t gate_off;
+  /* QKV: N == 3*H*D; q scaled by qscale; RoPE on q,k at pos l (spatial) or t (temporal) */
+  int32_t qkv_layout; void* qkv_out; int32_t H, D, T, L; float qscale;
+  const float* rope; int32_t rope_rows; /* cos [rope_rows][D/2] then sin; null = no RoPE */
+} mdg_gemm_desc;
+
+int mdg_abi_version(void);
+const char* mdg_last_error_string(void);
+
+/* Workspace (attention operand buffers, hidden activations, key-padding bias). */
+size_t mdg_workspace_bytes(const mdg_dims* d);
+int mdg_workspace_init(const mdg_dims* d, void* ws, void* stream);
+/* key-padding additive bias for the temporal attention from mask [B,T,L] (0 -> -inf) */
+int mdg_prepare_mask(const mdg_dims* d, const float* mask, void* ws, void* stream);
+
+/* out[n][c] = sum_j x[n][j] W[c][j] + bias[c] + base[n][c] + pos[l][c]
+               + emb[idx[n]][c] + ipa[b*L + l][c]   (every term but x.W optional)
+   latent_to_emb / cond_to_emb + mask_to_emb + pos_embed (latent_model.py:242-250) */
+int mdg_embed(int32_t N, int32_t T, int32_t L, int32_t C, int32_t K, const float* x,
+              const float* W, const float* bias, const float* base, const float* pos,
+              const float* emb, const int64_t* idx, const float* ipa, float* out, void* stream);
+
+/* One LatentMDGenLayer (latent_model.py:456-493) on the residual h [N][C], in place. */
+int mdg_layer_fwd(const mdg_dims* d, const mdg_layer_weights* w, const float* rope_l,
+                  const float* rope_t, const float* mods, const float* mask, float* h, void* ws,
+                  void* stream);
+
+/* FinalLayer (layers.py:58-75) + Euler update (integrators.py:106-113). */
+int mdg_final_euler(int32_t N, int32_t rows_per_b, int32_t C, int32_t latent,
+                    const float* w_final, const float* b_final, const float* mods_final,
+                    const float* h, const float* x_in, float dt, float* x_out, float* v_out,
+                    void* stream);
+
+/* Whole denoising step: embed -> num_layers x layer -> FinalLayer -> Euler. */
+int mdg_denoise_step(const mdg_model* m, const mdg_step_io* io, const float* mask, void* ws,
+                     void* stream);
+
+/* Building blocks (exposed for unit tests and for the conditioning precompute). */
+int mdg_gemm(const mdg_gemm_desc* g, void* stream);
+int mdg_attn_spatial(int32_t dtype, int32_t n_frames, int32_t L, int32_t H, int32_t D,
+                     const void* qkv, const float* kvb, const float* mask, void* out,
+                     void* stream);
+int mdg_attn_temporal(int32_t dtype, int32_t B, int32_t T, int32_t L, int32_t H, int32_t D,
+                      const void* qkv_t, const float* kbias, const float* kvb, void* out,
+                      void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MDGEN_HIP_H */

@@ -1,0 +1,122 @@
+"""ctypes binding of libmdgen_hip.so (C ABI declared in include/mdgen_hip.h).
+
+The library is built in-tree (mdgen_finetune_amd/libmdgen_hip.so, see csrc/Makefile) and
+loaded after torch, so it binds to the HIP runtime torch already loaded (same SONAME
+libamdhip64.so.7).  There is no fallback: if the library is missing or a call fails, a
+RuntimeError is raised.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (must be imported before the HIP library is loaded)
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libmdgen_hip.so")
+
+MDG_F32, MDG_BF16 = 0, 1
+MDG_A_PLAIN, MDG_A_LNMOD = 0, 1
+MDG_EPI_STORE, MDG_EPI_GATE_RES, MDG_EPI_QKV = 0, 1, 2
+MDG_ACT_NONE, MDG_ACT_GELU, MDG_ACT_SILU = 0, 1, 2
+MDG_QKV_SPATIAL, MDG_QKV_TEMPORAL = 0, 1
+MDG_MAX_LAYERS = 16
+MDG_DP = 32
+
+_vp = ctypes.c_void_p
+_i32 = ctypes.c_int32
+_f32 = ctypes.c_float
+
+
+class MdgDims(ctypes.Structure):
+    _fields_ = [(n, _i32) for n in ("B", "T", "L", "C", "H", "D", "F", "latent", "num_layers", "dtype")]
+
+
+class MdgLayerWeights(ctypes.Structure):
+    _fields_ = [("wqkv", _vp * 2), ("bqkv", _vp * 2), ("wo", _vp * 2), ("bo", _vp * 2),
+                ("kvb", _vp * 2), ("w1", _vp), ("b1", _vp), ("w2", _vp), ("b2", _vp)]
+
+
+class MdgModel(ctypes.Structure):
+    _fields_ = [("dims", MdgDims), ("w_l2e", _vp), ("w_final", _vp), ("b_final", _vp),
+                ("rope_l", _vp), ("rope_t", _vp), ("layers", MdgLayerWeights * MDG_MAX_LAYERS)]
+
+
+class MdgStepIO(ctypes.Structure):
+    _fields_ = [("x_in", _vp), ("x_out", _vp), ("v_out", _vp), ("base", _vp), ("ipa", _vp),
+                ("mods", _vp), ("mods_final", _vp), ("dt", _f32), ("h", _vp)]
+
+
+class MdgGemmDesc(ctypes.Structure):
+    _fields_ = [
+        ("dtype", _i32), ("a_mode", _i32), ("epi", _i32), ("act", _i32),
+        ("M", _i32), ("N", _i32), ("K", _i32),
+        ("A", _vp), ("lda", _i32), ("W", _vp), ("ldw", _i32), ("bias", _vp),
+        ("mods", _vp), ("mod_stride", _i32), ("rows_per_mod", _i32), ("shift_off", _i32),
+        ("scale_off", _i32),
+        ("ln_w", _vp), ("ln_b", _vp), ("ln_eps", _f32),
+        ("out", _vp), ("ldo", _i32), ("out_f32", _i32),
+        ("resid", _vp), ("ldr", _i32), ("gate", _vp), ("gate_off", _i32),
+        ("qkv_layout", _i32), ("qkv_out", _vp), ("H", _i32), ("D", _i32), ("T", _i32), ("L", _i32),
+        ("qscale", _f32), ("rope", _vp), ("rope_rows", _i32),
+    ]
+
+
+# (name, restype, argtypes) of every exported entry point — the test suite checks that the
+# built library exports exactly these and that include/mdgen_hip.h declares them.
+SIGNATURES = [
+    ("mdg_abi_version", _i32, []),
+    ("mdg_last_error_string", ctypes.c_char_p, []),
+    ("mdg_workspace_bytes", ctypes.c_size_t, [ctypes.POINTER(MdgDims)]),
+    ("mdg_workspace_init", _i32, [ctypes.POINTER(MdgDims), _vp, _vp]),
+    ("mdg_prepare_mask", _i32, [ctypes.POINTER(MdgDims), _vp, _vp, _vp]),
+    ("mdg_embed", _i32, [_i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    ("mdg_layer_fwd", _i32, [ctypes.POINTER(MdgDims), ctypes.POINTER(MdgLayerWeights), _vp, _vp, _vp,
+                             _vp, _vp, _vp, _vp]),
+    ("mdg_final_euler", _i32, [_i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _vp]),
+    ("mdg_denoise_step", _i32, [ctypes.POINTER(MdgModel), ctypes.POINTER(MdgStepIO), _vp, _vp, _vp]),
+    ("mdg_gemm", _i32, [ctypes.POINTER(MdgGemmDesc), _vp]),
+    ("mdg_attn_spatial", _i32, [_i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
+    ("mdg_attn_temporal", _i32, [_i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
+]
+
+ABI_VERSION = 1
+_LIB = None
+
+
+def load():
+    """Load (once) and return the ctypes library; raise if it is missing or mismatched."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            f"{LIB_PATH} not found: build it with `make -C mdgen_finetune_amd/csrc` or "
+            "`python -c 'import __graft_entry__ as g; g.build()'` (there is no non-HIP fallback)")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, res, args in SIGNATURES:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    v = lib.mdg_abi_version()
+    if v != ABI_VERSION:
+        raise RuntimeError(f"libmdgen_hip ABI {v} != expected {ABI_VERSION}; rebuild")
+    _LIB = lib
+    return lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = load().mdg_last_error_string().decode(errors="replace")
+        raise RuntimeError(f"{what} failed (code {rc}): {msg}")
+
+
+def ptr(t) -> int | None:
+    """Device pointer of a tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream_handle(stream=None) -> int:
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return s.cuda_stream

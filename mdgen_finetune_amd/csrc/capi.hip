@@ -1,0 +1,305 @@
+// extern "C" entry points of libmdgen_hip.so (declared in include/mdgen_hip.h).
+// Argument validation happens here, on the host, before any launch: a kernel is never
+// started on shapes it does not support.
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+
+#include "../../include/mdgen_hip.h"
+#include "common.h"
+
+namespace mdg {
+int gemm_pick_bn(const mdg_gemm_desc& p);
+size_t gemm_smem_bytes(const mdg_gemm_desc& p, int bn);
+hipError_t gemm_launch(const mdg_gemm_desc& p, int bn, hipStream_t s);
+hipError_t attn_temporal_launch(int dtype, int B, int T, int L, int H, int D, const void* qkv_t,
+                                const float* kbias, const float* kvb, void* out, hipStream_t s);
+hipError_t attn_spatial_launch(int dtype, int nf, int L, int H, int D, const void* qkv,
+                               const float* kvb, const float* mask, void* out, hipStream_t s);
+hipError_t embed_launch(int N, int T, int L, int C, int K, const float* x, const float* W,
+                        const float* bias, const float* base, const float* pos, const float* emb,
+                        const int64_t* idx, const float* ipa, float* out, hipStream_t s);
+hipError_t final_euler_launch(int N, int rows_per_b, int C, int lat, const float* Wf,
+                              const float* bf, const float* mods, const float* h,
+                              const float* x_in, float dt, float* x_out, float* v_out,
+                              hipStream_t s);
+hipError_t mask_bias_launch(int B, int T, int L, const float* mask, float* kbias, hipStream_t s);
+hipError_t set_vpad_launch(int dtype, void* v, size_t rows, int D, hipStream_t s);
+}  // namespace mdg
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+int hip_check(hipError_t e, const char* what) {
+  if (e == hipSuccess) return MDG_OK;
+  return fail((int)e, "%s: %s", what, hipGetErrorString(e));
+}
+
+size_t ct_size(int dtype) { return dtype == MDG_BF16 ? 2 : 4; }
+size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+struct WsLayout {
+  size_t qkv_s, qkv_t, o, hid, kbias, total;
+};
+
+WsLayout ws_layout(const mdg_dims& d) {
+  const size_t cs = ct_size(d.dtype);
+  const size_t N = (size_t)d.B * d.T * d.L;
+  WsLayout w;
+  size_t off = 0;
+  w.qkv_s = off; off += align256(N * 3 * d.H * MDG_DP * cs);
+  w.qkv_t = off; off += align256(3ull * d.B * d.L * d.H * d.T * MDG_DP * cs);
+  w.o = off;     off += align256(N * d.C * cs);
+  w.hid = off;   off += align256(N * d.F * cs);
+  w.kbias = off; off += align256((size_t)d.B * d.L * d.T * sizeof(float));
+  w.total = off;
+  return w;
+}
+
+int check_dims(const mdg_dims* d) {
+  if (!d) return fail(MDG_E_ARG, "null dims");
+  if (d->dtype != MDG_F32 && d->dtype != MDG_BF16) return fail(MDG_E_DTYPE, "dtype %d", d->dtype);
+  if (d->B <= 0 || d->T <= 0 || d->L <= 0 || d->H <= 0)
+    return fail(MDG_E_SHAPE, "B,T,L,H must be positive (%d,%d,%d,%d)", d->B, d->T, d->L, d->H);
+  if (d->C != d->H * d->D) return fail(MDG_E_SHAPE, "C (%d) != H*D (%d*%d)", d->C, d->H, d->D);
+  if (d->D % 4 || d->D >= MDG_DP)
+    return fail(MDG_E_SHAPE, "head_dim %d unsupported (multiple of 4, < %d)", d->D, MDG_DP);
+  if (d->C % 64 || d->C > 512) return fail(MDG_E_SHAPE, "embed_dim %d unsupported (64k, <= 512)", d->C);
+  if (d->F % 64) return fail(MDG_E_SHAPE, "ffn dim %d not a multiple of 64", d->F);
+  if (d->latent <= 0 || d->latent > 64) return fail(MDG_E_SHAPE, "latent %d unsupported", d->latent);
+  if (d->num_layers < 0 || d->num_layers > MDG_MAX_LAYERS) return fail(MDG_E_SHAPE, "num_layers %d", d->num_layers);
+  if ((long long)d->B * d->T * d->L >= (1ll << 31) / d->F) return fail(MDG_E_SHAPE, "problem too large");
+  if (d->dtype == MDG_F32 && d->C > 384)
+    return fail(MDG_E_SHAPE, "f32 path: embed_dim %d > 384 exceeds the LDS-resident LN block", d->C);
+  return MDG_OK;
+}
+
+bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+}  // namespace
+
+extern "C" {
+
+int mdg_abi_version(void) { return MDG_ABI_VERSION; }
+
+const char* mdg_last_error_string(void) { return g_err.c_str(); }
+
+size_t mdg_workspace_bytes(const mdg_dims* d) {
+  if (check_dims(d)) return 0;
+  return ws_layout(*d).total;
+}
+
+int mdg_workspace_init(const mdg_dims* d, void* ws, void* stream) {
+  if (int e = check_dims(d)) return e;
+  if (!ws) return fail(MDG_E_ARG, "null workspace");
+  const WsLayout w = ws_layout(*d);
+  hipStream_t s = (hipStream_t)stream;
+  if (int e = hip_check(hipMemsetAsync(ws, 0, w.total, s), "workspace memset")) return e;
+  const size_t vrows = (size_t)d->B * d->L * d->H * d->T;
+  char* v = (char*)ws + w.qkv_t + 2 * vrows * MDG_DP * ct_size(d->dtype);
+  return hip_check(mdg::set_vpad_launch(d->dtype, v, vrows, d->D, s), "set_vpad");
+}
+
+int mdg_prepare_mask(const mdg_dims* d, const float* mask, void* ws, void* stream) {
+  if (int e = check_dims(d)) return e;
+  if (!mask || !ws) return fail(MDG_E_ARG, "null mask/workspace");
+  const WsLayout w = ws_layout(*d);
+  return hip_check(mdg::mask_bias_launch(d->B, d->T, d->L, mask, (float*)((char*)ws + w.kbias),
+                                         (hipStream_t)stream),
+                   "mask_bias");
+}
+
+int mdg_gemm(const mdg_gemm_desc* g, void* stream) {
+  if (!g) return fail(MDG_E_ARG, "null gemm desc");
+  if (g->dtype != MDG_F32 && g->dtype != MDG_BF16) return fail(MDG_E_DTYPE, "dtype %d", g->dtype);
+  if (!g->A || !g->W) return fail(MDG_E_ARG, "gemm: null A or W");
+  if (g->M <= 0 || g->N <= 0 || g->K <= 0 || g->K % 64)
+    return fail(MDG_E_SHAPE, "gemm: M,N,K = %d,%d,%d (K must be a multiple of 64)", g->M, g->N, g->K);
+  const size_t cs = ct_size(g->dtype);
+  if (g->ldw < g->K || (g->ldw * cs) % 16 || !aligned16(g->W))
+    return fail(MDG_E_SHAPE, "gemm: W must be 16-B aligned with ldw >= K and ldw*size %% 16 == 0");
+  if (g->a_mode == MDG_A_LNMOD) {
+    if (g->K > 512 || g->lda < g->K) return fail(MDG_E_SHAPE, "gemm LNMOD: K=%d lda=%d", g->K, g->lda);
+    if (g->mods && g->rows_per_mod <= 0) return fail(MDG_E_ARG, "gemm: rows_per_mod");
+    if ((g->ln_w == nullptr) != (g->ln_b == nullptr)) return fail(MDG_E_ARG, "gemm: ln_w/ln_b");
+  } else if (g->a_mode == MDG_A_PLAIN) {
+    if (g->lda < g->K || (g->lda * cs) % 16 || !aligned16(g->A))
+      return fail(MDG_E_SHAPE, "gemm PLAIN: A must be 16-B aligned, lda >= K");
+  } else {
+    return fail(MDG_E_ARG, "gemm: a_mode %d", g->a_mode);
+  }
+  switch (g->epi) {
+    case MDG_EPI_STORE:
+      if (!g->out || g->ldo < g->N || g->ldo % 4) return fail(MDG_E_ARG, "gemm STORE: out/ldo");
+      break;
+    case MDG_EPI_GATE_RES:
+      if (!g->resid || g->ldr < g->N || g->ldr % 4) return fail(MDG_E_ARG, "gemm GATE_RES: resid/ldr");
+      if (g->gate && g->rows_per_mod <= 0) return fail(MDG_E_ARG, "gemm: rows_per_mod");
+      break;
+    case MDG_EPI_QKV:
+      if (!g->qkv_out || g->D <= 0 || g->D % 4 || g->D >= MDG_DP || g->N != 3 * g->H * g->D)
+        return fail(MDG_E_SHAPE, "gemm QKV: N=%d H=%d D=%d", g->N, g->H, g->D);
+      if (g->T <= 0 || g->L <= 0 || g->M % (g->T * g->L))
+        return fail(MDG_E_SHAPE, "gemm QKV: M=%d not a multiple of T*L", g->M);
+      if (g->rope && g->rope_rows < (g->qkv_layout == MDG_QKV_SPATIAL ? g->L : g->T))
+        return fail(MDG_E_SHAPE, "gemm QKV: rope table too short");
+      break;
+    default:
+      return fail(MDG_E_ARG, "gemm: epi %d", g->epi);
+  }
+  const int bn = mdg::gemm_pick_bn(*g);
+  if (!bn) return fail(MDG_E_SHAPE, "gemm: no tile fits N=%d (D=%d)", g->N, g->D);
+  if (mdg::gemm_smem_bytes(*g, bn) > 160 * 1024)
+    return fail(MDG_E_SHAPE, "gemm: K=%d needs more LDS than a CU has", g->K);
+  return hip_check(mdg::gemm_launch(*g, bn, (hipStream_t)stream), "gemm launch");
+}
+
+int mdg_attn_spatial(int32_t dtype, int32_t n_frames, int32_t L, int32_t H, int32_t D,
+                     const void* qkv, const float* kvb, const float* mask, void* out,
+                     void* stream) {
+  if (dtype != MDG_F32 && dtype != MDG_BF16) return fail(MDG_E_DTYPE, "dtype %d", dtype);
+  if (!qkv || !kvb || !out) return fail(MDG_E_ARG, "attn_spatial: null pointer");
+  if (n_frames <= 0 || L <= 0 || H <= 0 || D <= 0 || D % 4 || D >= MDG_DP)
+    return fail(MDG_E_SHAPE, "attn_spatial: nf=%d L=%d H=%d D=%d", n_frames, L, H, D);
+  return hip_check(mdg::attn_spatial_launch(dtype, n_frames, L, H, D, qkv, kvb, mask, out,
+                                            (hipStream_t)stream),
+                   "attn_spatial");
+}
+
+int mdg_attn_temporal(int32_t dtype, int32_t B, int32_t T, int32_t L, int32_t H, int32_t D,
+                      const void* qkv_t, const float* kbias, const float* kvb, void* out,
+                      void* stream) {
+  if (dtype != MDG_F32 && dtype != MDG_BF16) return fail(MDG_E_DTYPE, "dtype %d", dtype);
+  if (!qkv_t || !kbias || !kvb || !out) return fail(MDG_E_ARG, "attn_temporal: null pointer");
+  if (B <= 0 || T <= 0 || L <= 0 || H <= 0 || D <= 0 || D % 4 || D >= MDG_DP)
+    return fail(MDG_E_SHAPE, "attn_temporal: B=%d T=%d L=%d H=%d D=%d", B, T, L, H, D);
+  if (H > 65535 || B * L > 65535) return fail(MDG_E_SHAPE, "attn_temporal: grid too large");
+  return hip_check(mdg::attn_temporal_launch(dtype, B, T, L, H, D, qkv_t, kbias, kvb, out,
+                                             (hipStream_t)stream),
+                   "attn_temporal");
+}
+
+int mdg_embed(int32_t N, int32_t T, int32_t L, int32_t C, int32_t K, const float* x,
+              const float* W, const float* bias, const float* base, const float* pos,
+              const float* emb, const int64_t* idx, const float* ipa, float* out, void* stream) {
+  if (!x || !W || !out) return fail(MDG_E_ARG, "embed: null x/W/out");
+  if (N <= 0 || T <= 0 || L <= 0 || C <= 0 || K <= 0 || K > 64 || N % (T * L))
+    return fail(MDG_E_SHAPE, "embed: N=%d T=%d L=%d C=%d K=%d", N, T, L, C, K);
+  if ((emb == nullptr) != (idx == nullptr)) return fail(MDG_E_ARG, "embed: emb/idx");
+  return hip_check(mdg::embed_launch(N, T, L, C, K, x, W, bias, base, pos, emb, idx, ipa, out,
+                                     (hipStream_t)stream),
+                   "embed");
+}
+
+int mdg_final_euler(int32_t N, int32_t rows_per_b, int32_t C, int32_t latent,
+                    const float* w_final, const float* b_final, const float* mods_final,
+                    const float* h, const float* x_in, float dt, float* x_out, float* v_out,
+                    void* stream) {
+  if (!w_final || !b_final || !mods_final || !h) return fail(MDG_E_ARG, "final_euler: null pointer");
+  if (x_out && !x_in) return fail(MDG_E_ARG, "final_euler: x_out without x_in");
+  if (N <= 0 || rows_per_b <= 0 || C % 64 || C > 512 || latent <= 0 || latent > 64)
+    return fail(MDG_E_SHAPE, "final_euler: N=%d C=%d latent=%d", N, C, latent);
+  return hip_check(mdg::final_euler_launch(N, rows_per_b, C, latent, w_final, b_final, mods_final,
+                                           h, x_in, dt, x_out, v_out, (hipStream_t)stream),
+                   "final_euler");
+}
+
+int mdg_layer_fwd(const mdg_dims* d, const mdg_layer_weights* w, const float* rope_l,
+                  const float* rope_t, const float* mods, const float* mask, float* h, void* ws,
+                  void* stream) {
+  if (int e = check_dims(d)) return e;
+  if (!w || !mods || !h || !ws) return fail(MDG_E_ARG, "layer_fwd: null pointer");
+  const WsLayout lay = ws_layout(*d);
+  char* wsb = (char*)ws;
+  const int B = d->B, T = d->T, L = d->L, C = d->C, H = d->H, D = d->D, F = d->F;
+  const int N = B * T * L;
+  const float qs = 1.0f / sqrtf((float)D);
+  void* qkv_s = wsb + lay.qkv_s;
+  void* qkv_t = wsb + lay.qkv_t;
+  void* o = wsb + lay.o;
+  void* hid = wsb + lay.hid;
+  const float* kbias = (const float*)(wsb + lay.kbias);
+
+  mdg_gemm_desc g;
+  memset(&g, 0, sizeof(g));
+  g.dtype = d->dtype;
+  g.M = N;
+  g.mods = mods;
+  g.mod_stride = 9 * C;
+  g.rows_per_mod = T * L;
+  g.ln_eps = 1e-6f;
+  g.H = H; g.D = D; g.T = T; g.L = L;
+
+  // ---- spatial attention: x += gate_l * mha_l(mod(LN x))      (latent_model.py:466-472)
+  mdg_gemm_desc q = g;
+  q.a_mode = MDG_A_LNMOD; q.epi = MDG_EPI_QKV;
+  q.N = 3 * C; q.K = C; q.A = h; q.lda = C; q.W = w->wqkv[0]; q.ldw = C; q.bias = w->bqkv[0];
+  q.shift_off = 0; q.scale_off = C;
+  q.qkv_layout = MDG_QKV_SPATIAL; q.qkv_out = qkv_s; q.qscale = qs;
+  q.rope = rope_l; q.rope_rows = L + 1;
+  if (int e = mdg_gemm(&q, stream)) return e;
+  if (int e = mdg_attn_spatial(d->dtype, B * T, L, H, D, qkv_s, w->kvb[0], mask, o, stream)) return e;
+  mdg_gemm_desc r = g;
+  r.a_mode = MDG_A_PLAIN; r.epi = MDG_EPI_GATE_RES;
+  r.N = C; r.K = C; r.A = o; r.lda = C; r.W = w->wo[0]; r.ldw = C; r.bias = w->bo[0];
+  r.resid = h; r.ldr = C; r.gate = mods; r.gate_off = 2 * C;
+  if (int e = mdg_gemm(&r, stream)) return e;
+
+  // ---- temporal attention: x += gate_t * mha_t(mod(LN x))     (latent_model.py:474-486)
+  q.W = w->wqkv[1]; q.bias = w->bqkv[1];
+  q.shift_off = 3 * C; q.scale_off = 4 * C;
+  q.qkv_layout = MDG_QKV_TEMPORAL; q.qkv_out = qkv_t; q.qscale = qs * 1.4426950408889634f;
+  q.rope = rope_t; q.rope_rows = T + 1;
+  if (int e = mdg_gemm(&q, stream)) return e;
+  if (int e = mdg_attn_temporal(d->dtype, B, T, L, H, D, qkv_t, kbias, w->kvb[1], o, stream)) return e;
+  r.W = w->wo[1]; r.bias = w->bo[1]; r.gate_off = 5 * C;
+  if (int e = mdg_gemm(&r, stream)) return e;
+
+  // ---- MLP: x += gate_m * fc2(gelu(fc1(mod(LN x))))           (latent_model.py:488-491)
+  mdg_gemm_desc f1 = g;
+  f1.a_mode = MDG_A_LNMOD; f1.epi = MDG_EPI_STORE; f1.act = MDG_ACT_GELU;
+  f1.N = F; f1.K = C; f1.A = h; f1.lda = C; f1.W = w->w1; f1.ldw = C; f1.bias = w->b1;
+  f1.shift_off = 6 * C; f1.scale_off = 7 * C; f1.out = hid; f1.ldo = F;
+  if (int e = mdg_gemm(&f1, stream)) return e;
+  mdg_gemm_desc f2 = g;
+  f2.a_mode = MDG_A_PLAIN; f2.epi = MDG_EPI_GATE_RES;
+  f2.N = C; f2.K = F; f2.A = hid; f2.lda = F; f2.W = w->w2; f2.ldw = F; f2.bias = w->b2;
+  f2.resid = h; f2.ldr = C; f2.gate = mods; f2.gate_off = 8 * C;
+  return mdg_gemm(&f2, stream);
+}
+
+int mdg_denoise_step(const mdg_model* m, const mdg_step_io* io, const float* mask, void* ws,
+                     void* stream) {
+  if (!m || !io) return fail(MDG_E_ARG, "denoise_step: null model/io");
+  const mdg_dims* d = &m->dims;
+  if (int e = check_dims(d)) return e;
+  if (!io->x_in || !io->base || !io->mods || !io->mods_final || !io->h)
+    return fail(MDG_E_ARG, "denoise_step: null io pointer");
+  const int N = d->B * d->T * d->L;
+  if (int e = mdg_embed(N, d->T, d->L, d->C, d->latent, io->x_in, m->w_l2e, nullptr, io->base,
+                        nullptr, nullptr, nullptr, io->ipa, io->h, stream))
+    return e;
+  const size_t mstride = (size_t)d->B * 9 * d->C;
+  for (int i = 0; i < d->num_layers; ++i)
+    if (int e = mdg_layer_fwd(d, &m->layers[i], m->rope_l, m->rope_t, io->mods + i * mstride, mask,
+                              io->h, ws, stream))
+      return e;
+  return mdg_final_euler(N, d->T * d->L, d->C, d->latent, m->w_final, m->b_final, io->mods_final,
+                         io->h, io->x_in, io->dt, io->x_out, io->v_out, stream);
+}
+
+}  // extern "C"

@@ -1,0 +1,110 @@
+// Shared device helpers for the MDGen denoiser kernels (gfx950 / CDNA4 only).
+//
+// Compute-type convention: every kernel is templated on CT, the operand type fed to the
+// matrix cores — `float` (exact-f32 MFMA v_mfma_f32_16x16x4_f32: the fp32 parity path) or
+// `__bf16` (v_mfma_f32_16x16x32_bf16: the performance path).  Accumulation, softmax,
+// LayerNorm statistics and the residual stream are always fp32.
+//
+// Fragment convention (one 16x16 output tile, K = 32 per step): lane l holds 8 consecutive
+// K-elements  [8*(l>>4), 8*(l>>4)+8)  of row (l & 15) for both the A and the B operand.
+// For bf16 that is exactly the 16x16x32 operand map; for f32 the 8 elements feed 8
+// consecutive 16x16x4 MFMAs (MFMA j reads element j of every lane, i.e. k = 8g + j for lane
+// group g), which sums the same 32 products.  The C/D map is the same for both:
+//   row = 4*(l>>4) + i (i = register 0..3), col = l & 15.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <type_traits>
+
+typedef __bf16 bf16_t;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(8))) float f32x8;
+
+template <typename CT> struct V8;
+template <> struct V8<bf16_t> { using T = bf16x8; };
+template <> struct V8<float> { using T = f32x8; };
+
+template <typename CT> __device__ __forceinline__ constexpr bool is_bf16() {
+  return std::is_same<CT, bf16_t>::value;
+}
+
+// 8 consecutive CT elements from a 16-byte aligned address (LDS or global).
+template <typename CT>
+__device__ __forceinline__ typename V8<CT>::T ld8(const CT* p) {
+  if constexpr (is_bf16<CT>()) {
+    return *reinterpret_cast<const bf16x8*>(p);
+  } else {
+    const float4 a = reinterpret_cast<const float4*>(p)[0];
+    const float4 b = reinterpret_cast<const float4*>(p)[1];
+    f32x8 r;
+    r[0] = a.x; r[1] = a.y; r[2] = a.z; r[3] = a.w;
+    r[4] = b.x; r[5] = b.y; r[6] = b.z; r[7] = b.w;
+    return r;
+  }
+}
+
+template <typename CT>
+__device__ __forceinline__ typename V8<CT>::T zero8() {
+  typename V8<CT>::T r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (CT)0.0f;
+  return r;
+}
+
+// acc += A(16x32) * B(32x16) in the fragment convention above.
+template <typename CT>
+__device__ __forceinline__ void mma_k32(f32x4& acc, const typename V8<CT>::T& a,
+                                        const typename V8<CT>::T& b) {
+  if constexpr (is_bf16<CT>()) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], b[j], acc, 0, 0, 0);
+  }
+}
+
+// Store 4 fp32 values as 4 CT (8 B for bf16, 16 B for f32); p must be aligned accordingly.
+template <typename CT>
+__device__ __forceinline__ void st4(CT* p, float a, float b, float c, float d) {
+  if constexpr (is_bf16<CT>()) {
+    bf16x4 v;
+    v[0] = (bf16_t)a; v[1] = (bf16_t)b; v[2] = (bf16_t)c; v[3] = (bf16_t)d;
+    *reinterpret_cast<bf16x4*>(p) = v;
+  } else {
+    *reinterpret_cast<float4*>(p) = make_float4(a, b, c, d);
+  }
+}
+
+template <typename CT>
+__device__ __forceinline__ float4 ld4f(const CT* p) {
+  if constexpr (is_bf16<CT>()) {
+    const bf16x4 v = *reinterpret_cast<const bf16x4*>(p);
+    return make_float4((float)v[0], (float)v[1], (float)v[2], (float)v[3]);
+  } else {
+    return *reinterpret_cast<const float4*>(p);
+  }
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+__device__ __forceinline__ float gelu_erf(float x) {
+  // exact-erf GELU (reference layers.py:78-85)
+  return x * 0.5f * (1.0f + erff(x * 0.70710678118654752440f));
+}
+
+__device__ __forceinline__ float silu(float x) { return x / (1.0f + expf(-x)); }
+
+static inline int cdiv(int a, int b) { return (a + b - 1) / b; }

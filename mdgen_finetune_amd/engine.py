@@ -1,0 +1,391 @@
+"""HIP execution engine for LatentMDGenModel (the MI355X hot path).
+
+Responsibilities
+  * pack the module's parameters once (re-packed when any parameter changes) into the
+    operand layout of libmdgen_hip.so: fused [3C][C] QKV weights per attention, CT (bf16 or
+    f32) GEMM operands, fp32 biases, RoPE tables and the RoPE-rotated bias_k / bias_v rows;
+  * per (B, T, L): workspace (attention operand buffers, hidden activations), residual
+    stream, and the mdg_model struct of device pointers;
+  * conditioning precompute, x-independent and therefore done for ALL Euler steps of a
+    window at once: t-embedding, every adaLN modulation, IPA prepend, the
+    step-invariant token embedding (cond_to_emb + mask_to_emb + pos_embed + biases);
+  * the Euler loop: ``sample_euler`` runs num_steps-1 ``mdg_denoise_step`` calls
+    (Sampler.sample_ode('euler'), transport.py:407-450 + integrators.py:95-114), optionally
+    captured with the conditioning precompute into ONE hipGraph and replayed.
+
+The conditioning precompute currently uses eager PyTorch ops on the GPU (t-embedding MLP,
+the adaLN GEMVs, the 5 IPA layers on B*L tokens: < 0.5% of a window's FLOPs); every
+token-wise op of the 49 denoising steps runs in libmdgen_hip.so.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+
+import torch
+import torch.nn.functional as F
+
+from . import _lib
+from .rigid_utils import frames_to_tensors
+
+_DTYPES = {"bf16": (_lib.MDG_BF16, torch.bfloat16), "f32": (_lib.MDG_F32, torch.float32)}
+
+
+def get_engine(model):
+    dt = getattr(model, "hip_dtype", "bf16")
+    eng = model._engine
+    if eng is None or eng.dtype_name != dt:
+        eng = HipEngine(model, dt)
+        model._engine = eng
+    return eng
+
+
+class _ShapeState:
+    pass
+
+
+class HipEngine:
+    def __init__(self, model, dtype="bf16"):
+        if dtype not in _DTYPES:
+            raise ValueError(f"hip_dtype must be one of {list(_DTYPES)}")
+        self.model = model
+        self.lib = _lib.load()
+        self.dtype_name = dtype
+        self.mdg_dtype, self.ct = _DTYPES[dtype]
+        a = model.args
+        self.C, self.H = a.embed_dim, a.mha_heads
+        self.D = self.C // self.H
+        self.F = 4 * self.C
+        self.nl = a.num_layers
+        self.lat = model.latent_dim
+        self.rope = not a.no_rope
+        self._pack_key = None
+        self._packed = None
+        self._states = {}
+        self._graphs = {}
+
+    # ------------------------------------------------------------------ packing
+    def _param_key(self):
+        return tuple((p.data_ptr(), p._version) for p in self.model.parameters())
+
+    def _pack(self):
+        key = self._param_key()
+        if key == self._pack_key:
+            return self._packed
+        m, ct = self.model, self.ct
+        dev = m.device
+        if dev.type != "cuda":
+            raise RuntimeError("the HIP backend needs the model on a ROCm device (model.cuda())")
+        with torch.no_grad():
+            P = {"layers": []}
+            for layer in m.layers:
+                d = {}
+                for i, mha in enumerate((layer.mha_l.attn, layer.mha_t.attn)):
+                    d[f"wqkv{i}"] = torch.cat([mha.q_proj.weight, mha.k_proj.weight, mha.v_proj.weight]).to(ct).contiguous()
+                    d[f"bqkv{i}"] = torch.cat([mha.q_proj.bias, mha.k_proj.bias, mha.v_proj.bias]).float().contiguous()
+                    d[f"wo{i}"] = mha.out_proj.weight.to(ct).contiguous()
+                    d[f"bo{i}"] = mha.out_proj.bias.float().contiguous()
+                    d[f"bias_k{i}"] = mha.bias_k.detach().float().reshape(-1)
+                    d[f"bias_v{i}"] = mha.bias_v.detach().float().reshape(-1)
+                d["w1"] = layer.fc1.weight.to(ct).contiguous()
+                d["b1"] = layer.fc1.bias.float().contiguous()
+                d["w2"] = layer.fc2.weight.to(ct).contiguous()
+                d["b2"] = layer.fc2.bias.float().contiguous()
+                P["layers"].append(d)
+            P["w_l2e"] = m.latent_to_emb.weight.float().contiguous()
+            P["b_l2e"] = m.latent_to_emb.bias.float().contiguous()
+            P["w_c2e"] = m.cond_to_emb.weight.float().contiguous()
+            P["b_base"] = (m.cond_to_emb.bias + m.latent_to_emb.bias).float().contiguous()
+            P["w_final"] = m.emb_to_latent.linear.weight.float().contiguous()
+            P["b_final"] = m.emb_to_latent.linear.bias.float().contiguous()
+            P["inv_freq"] = m.layers[0].mha_l.attn.rot_emb.inv_freq if self.rope else None
+        self._packed, self._pack_key = P, key
+        self._states.clear()
+        self._graphs.clear()
+        return P
+
+    def _rope_table(self, n_rows):
+        """cos | sin tables [n_rows][D/2] exactly as fair-esm builds them (fp32 outer product of
+        positions and inv_freq, then cos/sin; computed on the CPU like the reference)."""
+        inv = self._packed["inv_freq"].detach().float().cpu()
+        pos = torch.arange(n_rows).type_as(inv)
+        freqs = torch.einsum("i,j->ij", pos, inv)
+        return torch.cat([freqs.cos().reshape(-1), freqs.sin().reshape(-1)]).to(self.model.device)
+
+    def _kvb(self, bias_k, bias_v, S, table, n_rows):
+        """[H][2][32]: bias_k rotated at position S (the appended row's index), bias_v with 1.0
+        in pad column D (the temporal kernel's softmax row sum)."""
+        H, D, half = self.H, self.D, self.D // 2
+        kb = bias_k.reshape(H, D)
+        if table is not None:
+            cos = table[: n_rows * half].reshape(n_rows, half)[S]
+            sin = table[n_rows * half:].reshape(n_rows, half)[S]
+            c2, s2 = torch.cat([cos, cos]), torch.cat([sin, sin])
+            rot = torch.cat([-kb[:, half:], kb[:, :half]], -1)
+            kb = kb * c2 + rot * s2
+        out = torch.zeros(H, 2, _lib.MDG_DP, device=bias_k.device, dtype=torch.float32)
+        out[:, 0, :D] = kb
+        out[:, 1, :D] = bias_v.reshape(H, D)
+        out[:, 1, D] = 1.0
+        return out.contiguous()
+
+    def _state(self, B, T, L):
+        P = self._pack()
+        key = (B, T, L)
+        st = self._states.get(key)
+        if st is not None:
+            return st
+        lib, dev = self.lib, self.model.device
+        st = _ShapeState()
+        st.B, st.T, st.L, st.N = B, T, L, B * T * L
+        st.dims = _lib.MdgDims(B=B, T=T, L=L, C=self.C, H=self.H, D=self.D, F=self.F, latent=self.lat,
+                               num_layers=self.nl, dtype=self.mdg_dtype)
+        nbytes = lib.mdg_workspace_bytes(ctypes.byref(st.dims))
+        if nbytes == 0:
+            _lib.check(1001, f"workspace for B={B} T={T} L={L}")
+        st.ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        _lib.check(lib.mdg_workspace_init(ctypes.byref(st.dims), st.ws.data_ptr(), _lib.stream_handle()),
+                   "mdg_workspace_init")
+        st.h = torch.empty(st.N, self.C, device=dev)
+        st.base = torch.empty(st.N, self.C, device=dev)
+        st.rope_l = self._rope_table(L + 1) if self.rope else None
+        st.rope_t = self._rope_table(T + 1) if self.rope else None
+        st.kvb = []
+        mstruct = _lib.MdgModel()
+        mstruct.dims = st.dims
+        mstruct.w_l2e = P["w_l2e"].data_ptr()
+        mstruct.w_final = P["w_final"].data_ptr()
+        mstruct.b_final = P["b_final"].data_ptr()
+        mstruct.rope_l = _lib.ptr(st.rope_l)
+        mstruct.rope_t = _lib.ptr(st.rope_t)
+        for i, d in enumerate(P["layers"]):
+            kl = self._kvb(d["bias_k0"], d["bias_v0"], L, st.rope_l, L + 1)
+            kt = self._kvb(d["bias_k1"], d["bias_v1"], T, st.rope_t, T + 1)
+            st.kvb.append((kl, kt))
+            lw = mstruct.layers[i]
+            for j in range(2):
+                lw.wqkv[j] = d[f"wqkv{j}"].data_ptr()
+                lw.bqkv[j] = d[f"bqkv{j}"].data_ptr()
+                lw.wo[j] = d[f"wo{j}"].data_ptr()
+                lw.bo[j] = d[f"bo{j}"].data_ptr()
+            lw.kvb[0], lw.kvb[1] = kl.data_ptr(), kt.data_ptr()
+            lw.w1, lw.b1 = d["w1"].data_ptr(), d["b1"].data_ptr()
+            lw.w2, lw.b2 = d["w2"].data_ptr(), d["b2"].data_ptr()
+        st.model_struct = mstruct
+        self._states[key] = st
+        return st
+
+    # ------------------------------------------------------------------ conditioning
+    def conditioning(self, t_sb, mask, rots, trans, erots, etrans, aatype):
+        """x-independent conditioning for S time points at once.
+        t_sb [S, B] -> mods [S][nl][B][9C], mods_final [S][B][2C], ipa [S][B][L][C] (or None)."""
+        m = self.model
+        S, B = t_sb.shape
+        C = self.C
+        c = m.embed_time(t_sb.reshape(-1))                                    # [S*B, C]
+        sc = F.silu(c)
+        mods = torch.stack([F.linear(sc, l.adaLN_modulation[1].weight, l.adaLN_modulation[1].bias)
+                            for l in m.layers], 1)                             # [S*B, nl, 9C]
+        mods = mods.reshape(S, B, self.nl, 9 * C).permute(0, 2, 1, 3).contiguous()
+        fl = m.emb_to_latent.adaLN_modulation[1]
+        mods_f = F.linear(sc, fl.weight, fl.bias).reshape(S, B, 2 * C).contiguous()
+        ipa = None
+        if m.args.prepend_ipa:
+            L = mask.shape[-1]
+            mask_b = mask[:, 0].repeat(S, 1)                                  # [S*B, L]
+            rep = lambda z: None if z is None else z.repeat(S, *([1] * (z.dim() - 1)))  # noqa: E731
+            aa = rep(aatype)
+            ipa = self._run_ipa(c, mask_b, rep(rots), rep(trans), rep(erots), rep(etrans), aa)
+            ipa = ipa.reshape(S, B, L, C).contiguous()
+        return mods, mods_f, ipa
+
+    def _run_ipa(self, c, mask_b, rots, trans, erots, etrans, aatype):
+        m = self.model
+        B, L = mask_b.shape
+        use_aa = aatype is not None and hasattr(m, "aatype_to_emb")
+        if not m.tps:
+            x = torch.zeros(B, L, self.C, device=mask_b.device)
+            if use_aa:
+                x = x + m.aatype_to_emb(aatype)
+            for layer in m.ipa_layers:
+                x = layer(x, c, mask_b, rots, trans)
+            return x
+        x_f = m.latent_to_emb_f(self._rel7[0].repeat(B // self._rel7[0].shape[0], 1, 1))
+        x_r = m.latent_to_emb_r(self._rel7[1].repeat(B // self._rel7[1].shape[0], 1, 1))
+        if use_aa:
+            x_f = x_f + m.aatype_to_emb(aatype)
+            x_r = x_r + m.aatype_to_emb(aatype)
+        for layer in m.ipa_layers:
+            x_r = layer(x_r, c, mask_b, rots, trans)
+            x_f = layer(x_f, c, mask_b, erots, etrans)
+        return x_r + x_f
+
+    def _prepare_tps(self, rots, trans, erots, etrans):
+        # relative frames use an eigen-solve on the host (rot_to_quat); done once per window,
+        # outside any captured graph.
+        from .model.latent_model import relative_tensor7
+
+        if self.model.tps:
+            self._rel7 = (relative_tensor7(rots, trans, erots, etrans), relative_tensor7(erots, etrans, rots, trans))
+        else:
+            self._rel7 = None
+
+    def _base(self, st, x_cond, x_cond_mask):
+        """Step-invariant embedding: cond_to_emb(x_cond) + mask_to_emb + pos_embed + both biases
+        (latent_model.py:242-250 without the x-dependent latent_to_emb(x))."""
+        m, P, s = self.model, self._packed, _lib.stream_handle()
+        pos = m.pos_embed[0].contiguous() if m.args.abs_pos_emb else None
+        if x_cond is not None:
+            xc = x_cond.float().contiguous()
+            idx = x_cond_mask.to(torch.int64).contiguous()
+            _lib.check(self.lib.mdg_embed(st.N, st.T, st.L, self.C, self.lat, xc.data_ptr(), P["w_c2e"].data_ptr(),
+                                          P["b_base"].data_ptr(), None, _lib.ptr(pos),
+                                          m.mask_to_emb.weight.data_ptr(), idx.data_ptr(), None,
+                                          st.base.data_ptr(), s), "mdg_embed(cond)")
+        else:
+            b = P["b_l2e"].reshape(1, 1, 1, -1)
+            if pos is not None:
+                b = b + pos.reshape(1, 1, st.L, -1)
+            st.base.copy_(b.expand(st.B, st.T, st.L, self.C).reshape(st.N, self.C))
+        if getattr(m.args, "abs_time_emb", False):
+            st.base.add_(m.time_embed[0, :st.T].reshape(1, st.T, 1, self.C).expand(st.B, st.T, st.L, self.C)
+                         .reshape(st.N, self.C))
+
+    # ------------------------------------------------------------------ inputs
+    def _inputs(self, x, mask, start_frames, end_frames, aatype):
+        if not x.is_cuda:
+            raise RuntimeError("HIP backend: inputs must be ROCm device tensors (no CPU fallback)")
+        B, T, L, lat = x.shape
+        if lat != self.lat:
+            raise ValueError(f"latent dim {lat} != model latent {self.lat}")
+        if self.model.args.abs_pos_emb and L != self.model.args.crop:
+            raise ValueError(f"abs_pos_emb needs L == crop ({L} vs {self.model.args.crop})")
+        mask = mask.to(x.device, torch.float32).contiguous()
+        rots, trans = frames_to_tensors(start_frames, x.device)
+        erots, etrans = frames_to_tensors(end_frames, x.device) if self.model.tps else (None, None)
+        if self.model.args.prepend_ipa and rots is None:
+            raise ValueError("prepend_ipa needs start_frames")
+        aa = None if aatype is None else aatype.to(x.device)
+        return B, T, L, mask, rots, trans, erots, etrans, aa
+
+    def _step_io(self, st, x_in, x_out, v_out, ipa, mods, mods_f, dt):
+        io = _lib.MdgStepIO()
+        io.x_in, io.x_out, io.v_out = x_in, x_out, v_out
+        io.base, io.ipa = st.base.data_ptr(), ipa
+        io.mods, io.mods_final = mods, mods_f
+        io.dt = dt
+        io.h = st.h.data_ptr()
+        return io
+
+    # ------------------------------------------------------------------ one forward
+    @torch.no_grad()
+    def forward(self, x, t, mask, start_frames, end_frames, x_cond, x_cond_mask, aatype):
+        B, T, L, mask, rots, trans, erots, etrans, aa = self._inputs(x, mask, start_frames, end_frames, aatype)
+        st = self._state(B, T, L)
+        self._prepare_tps(rots, trans, erots, etrans)
+        tb = t.to(x.device).float().reshape(1, B) if t.dim() else t.to(x.device).float().expand(1, B)
+        mods, mods_f, ipa = self.conditioning(tb, mask, rots, trans, erots, etrans, aa)
+        self._base(st, x_cond, x_cond_mask)
+        xin = x.float().contiguous()
+        v = torch.empty_like(xin)
+        s = _lib.stream_handle()
+        _lib.check(self.lib.mdg_prepare_mask(ctypes.byref(st.dims), mask.data_ptr(), st.ws.data_ptr(), s),
+                   "mdg_prepare_mask")
+        io = self._step_io(st, xin.data_ptr(), None, v.data_ptr(), _lib.ptr(ipa), mods.data_ptr(),
+                           mods_f.data_ptr(), 0.0)
+        _lib.check(self.lib.mdg_denoise_step(ctypes.byref(st.model_struct), ctypes.byref(io), mask.data_ptr(),
+                                             st.ws.data_ptr(), s), "mdg_denoise_step")
+        return v
+
+    # ------------------------------------------------------------------ Euler sampling
+    @torch.no_grad()
+    def sample_euler(self, zs, num_steps=50, mask=None, start_frames=None, end_frames=None, x_cond=None,
+                     x_cond_mask=None, aatype=None, use_graph=True):
+        """All num_steps states of the fixed-grid Euler ODE solve from t=0 to t=1
+        (the tensor ``Sampler.sample_ode('euler')(zs, model)`` returns)."""
+        B, T, L, mask, rots, trans, erots, etrans, aa = self._inputs(zs, mask, start_frames, end_frames, aatype)
+        st = self._state(B, T, L)
+        self._prepare_tps(rots, trans, erots, etrans)
+        key = (B, T, L, num_steps)
+        gs = self._graphs.get(key) if use_graph else None
+        if gs is None:
+            gs = self._build_sampler(st, num_steps, key if use_graph else None)
+        # stage inputs into the static buffers the (captured) program reads
+        gs.states[0].copy_(zs)
+        gs.mask.copy_(mask)
+        self._copy_opt(gs, "rots", rots)
+        self._copy_opt(gs, "trans", trans)
+        self._copy_opt(gs, "erots", erots)
+        self._copy_opt(gs, "etrans", etrans)
+        self._copy_opt(gs, "aatype", aa)
+        if self._rel7 is not None:  # TPS relative frames: static copies the graph reads
+            self._copy_opt(gs, "rel7f", self._rel7[0])
+            self._copy_opt(gs, "rel7r", self._rel7[1])
+            self._rel7 = (gs.rel7f, gs.rel7r)
+        gs.has_cond = x_cond is not None
+        if gs.has_cond:
+            self._copy_opt(gs, "x_cond", x_cond.float())
+            self._copy_opt(gs, "x_cond_mask", x_cond_mask.to(torch.int64))
+        if gs.graph is not None and gs.graph_has_cond == gs.has_cond:
+            gs.graph.replay()
+        else:
+            self._run_sampler(gs, st)
+            if use_graph and gs.graph is None:
+                self._capture(gs, st)
+        return gs.states.clone()
+
+    def _copy_opt(self, gs, name, val):
+        if val is None:
+            setattr(gs, name, None)
+            return
+        buf = getattr(gs, name, None)
+        if buf is None or buf.shape != val.shape or buf.dtype != val.dtype:
+            buf = torch.empty_like(val)
+            setattr(gs, name, buf)
+            gs.graph = None  # static buffers changed: recapture
+        buf.copy_(val)
+
+    def _build_sampler(self, st, num_steps, key):
+        gs = _ShapeState()
+        dev = self.model.device
+        ts = torch.linspace(0, 1, num_steps)  # CPU fp32, as the reference's ode (integrators.py:85)
+        gs.S = num_steps - 1
+        gs.t_sb = ts[:-1].reshape(-1, 1).expand(gs.S, st.B).contiguous().to(dev)
+        gs.dts = [float(ts[i + 1] - ts[i]) for i in range(gs.S)]
+        gs.states = torch.empty(num_steps, st.B, st.T, st.L, self.lat, device=dev)
+        gs.mask = torch.empty(st.B, st.T, st.L, device=dev)
+        gs.graph = None
+        gs.graph_has_cond = None
+        if key is not None:
+            self._graphs[key] = gs
+        return gs
+
+    def _run_sampler(self, gs, st):
+        """The whole window: conditioning for all steps, base embedding, mask bias, S steps."""
+        s = _lib.stream_handle()
+        mods, mods_f, ipa = self.conditioning(gs.t_sb, gs.mask, gs.rots, gs.trans, getattr(gs, "erots", None),
+                                              getattr(gs, "etrans", None), getattr(gs, "aatype", None))
+        gs.cond = (mods, mods_f, ipa)  # keep alive (graph-pool memory during capture)
+        self._base(st, gs.x_cond if gs.has_cond else None, gs.x_cond_mask if gs.has_cond else None)
+        _lib.check(self.lib.mdg_prepare_mask(ctypes.byref(st.dims), gs.mask.data_ptr(), st.ws.data_ptr(), s),
+                   "mdg_prepare_mask")
+        C, B = self.C, st.B
+        ios = []
+        for i in range(gs.S):
+            io = self._step_io(st, gs.states[i].data_ptr(), gs.states[i + 1].data_ptr(), None,
+                               None if ipa is None else ipa[i].data_ptr(), mods[i].data_ptr(),
+                               mods_f[i].data_ptr(), gs.dts[i])
+            ios.append(io)
+            _lib.check(self.lib.mdg_denoise_step(ctypes.byref(st.model_struct), ctypes.byref(io),
+                                                 gs.mask.data_ptr(), st.ws.data_ptr(), s), "mdg_denoise_step")
+        gs.ios = ios
+        del C, B
+
+    def _capture(self, gs, st):
+        g = torch.cuda.CUDAGraph()
+        torch.cuda.synchronize()
+        with torch.cuda.graph(g):
+            self._run_sampler(gs, st)
+        gs.graph = g
+        gs.graph_has_cond = gs.has_cond
+        g.replay()  # the capture did not execute; produce this call's result

@@ -1,0 +1,197 @@
+"""Parameter containers (and their eager forwards) with the reference's module names, so
+``state_dict()`` keys match a reference checkpoint exactly.
+
+Reference: src/mdgen/model/layers.py (modulate 14-15, TimestepEmbedder 17-55, FinalLayer
+58-75, gelu 78-85), src/mdgen/model/mha.py (MultiheadAttention 67-159: parameter layout
+only), fair-esm RotaryEmbedding (buffer ``inv_freq``), src/mdgen/model/ipa.py:34-90
+(InvariantPointAttention parameters).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+
+def modulate(x, shift, scale):
+    return x * (1 + scale.unsqueeze(1)) + shift.unsqueeze(1)
+
+
+def gelu(x):
+    return x * 0.5 * (1.0 + torch.erf(x / math.sqrt(2.0)))
+
+
+def timestep_embedding(t, dim=256, max_period=10000):
+    half = dim // 2
+    freqs = torch.exp(-math.log(max_period) * torch.arange(0, half, dtype=torch.float32) / half).to(t.device)
+    args = t[:, None].float() * freqs[None]
+    emb = torch.cat([torch.cos(args), torch.sin(args)], dim=-1)
+    if dim % 2:
+        emb = torch.cat([emb, torch.zeros_like(emb[:, :1])], dim=-1)
+    return emb
+
+
+class TimestepEmbedder(nn.Module):
+    def __init__(self, hidden_size, frequency_embedding_size=256):
+        super().__init__()
+        self.mlp = nn.Sequential(nn.Linear(frequency_embedding_size, hidden_size, bias=True), nn.SiLU(),
+                                 nn.Linear(hidden_size, hidden_size, bias=True))
+        self.frequency_embedding_size = frequency_embedding_size
+
+    def forward(self, t):
+        return self.mlp(timestep_embedding(t, self.frequency_embedding_size))
+
+
+class FinalLayer(nn.Module):
+    def __init__(self, hidden_size, out_channels):
+        super().__init__()
+        self.norm_final = nn.LayerNorm(hidden_size, elementwise_affine=False, eps=1e-6)
+        self.linear = nn.Linear(hidden_size, out_channels, bias=True)
+        self.adaLN_modulation = nn.Sequential(nn.SiLU(), nn.Linear(hidden_size, 2 * hidden_size, bias=True))
+
+    def forward(self, x, c):
+        shift, scale = self.adaLN_modulation(c).chunk(2, dim=-1)
+        return self.linear(modulate(self.norm_final(x), shift, scale))
+
+
+class RotaryEmbedding(nn.Module):
+    """fair-esm 1.0.2 RotaryEmbedding: only the ``inv_freq`` buffer is state."""
+
+    def __init__(self, dim):
+        super().__init__()
+        self.register_buffer("inv_freq", 1.0 / (10000 ** (torch.arange(0, dim, 2).float() / dim)))
+
+    def tables(self, n, device):
+        """cos, sin [n, dim/2] for positions 0..n-1 (the table is built from k's length)."""
+        pos = torch.arange(n, device=self.inv_freq.device).type_as(self.inv_freq)
+        freqs = torch.einsum("i,j->ij", pos, self.inv_freq)
+        return freqs.cos().to(device), freqs.sin().to(device)
+
+
+def apply_rope(x, cos, sin):
+    n, h = x.shape[-2], x.shape[-1] // 2
+    c = torch.cat([cos[:n], cos[:n]], -1)
+    s = torch.cat([sin[:n], sin[:n]], -1)
+    rot = torch.cat((-x[..., h:], x[..., :h]), dim=-1)
+    return x * c + rot * s
+
+
+class MultiheadAttention(nn.Module):
+    """Parameter layout of the reference fairseq/ESM MultiheadAttention (mha.py:67-159) with
+    add_bias_kv and rotary embeddings; ``forward`` is the eager rope path (mha.py:161-407)
+    for batch-first input [N, S, C] and key validity [N, S]."""
+
+    def __init__(self, embed_dim, num_heads, add_bias_kv=True, use_rotary_embeddings=True, dropout=0.0):
+        super().__init__()
+        self.embed_dim, self.num_heads = embed_dim, num_heads
+        self.head_dim = embed_dim // num_heads
+        self.scaling = self.head_dim ** -0.5
+        self.dropout = dropout
+        self.k_proj = nn.Linear(embed_dim, embed_dim)
+        self.v_proj = nn.Linear(embed_dim, embed_dim)
+        self.q_proj = nn.Linear(embed_dim, embed_dim)
+        self.out_proj = nn.Linear(embed_dim, embed_dim)
+        if add_bias_kv:
+            self.bias_k = nn.Parameter(torch.empty(1, 1, embed_dim))
+            self.bias_v = nn.Parameter(torch.empty(1, 1, embed_dim))
+        else:
+            self.bias_k = self.bias_v = None
+        g = 1 / math.sqrt(2)
+        for lin in (self.k_proj, self.v_proj, self.q_proj):
+            nn.init.xavier_uniform_(lin.weight, gain=g)
+        nn.init.xavier_uniform_(self.out_proj.weight)
+        nn.init.constant_(self.out_proj.bias, 0.0)
+        if add_bias_kv:
+            nn.init.xavier_normal_(self.bias_k)
+            nn.init.xavier_normal_(self.bias_v)
+        self.rot_emb = RotaryEmbedding(self.head_dim) if use_rotary_embeddings else None
+
+    def forward(self, x, valid):
+        N, S, C = x.shape
+        H, d = self.num_heads, self.head_dim
+        q = self.q_proj(x) * self.scaling
+        k, v = self.k_proj(x), self.v_proj(x)
+        kvalid = valid.bool()
+        if self.bias_k is not None:
+            k = torch.cat([k, self.bias_k.expand(N, 1, C)], 1)
+            v = torch.cat([v, self.bias_v.expand(N, 1, C)], 1)
+            kvalid = torch.cat([kvalid, torch.ones(N, 1, dtype=torch.bool, device=x.device)], 1)
+        Sk = k.shape[1]
+        q = q.reshape(N, S, H, d).transpose(1, 2)
+        k = k.reshape(N, Sk, H, d).transpose(1, 2)
+        v = v.reshape(N, Sk, H, d).transpose(1, 2)
+        if self.rot_emb is not None:
+            cos, sin = self.rot_emb.tables(Sk, x.device)
+            q, k = apply_rope(q, cos, sin), apply_rope(k, cos, sin)
+        w = q @ k.transpose(-1, -2)
+        w = w.masked_fill(~kvalid[:, None, None, :], float("-inf"))
+        w = torch.softmax(w, dim=-1, dtype=torch.float32)
+        w = F.dropout(w, p=self.dropout, training=self.training)
+        o = (w @ v).transpose(1, 2).reshape(N, S, C)
+        return self.out_proj(o)
+
+
+class AttentionWithRoPE(nn.Module):
+    """latent_model.py:329-338 (key_padding_mask = 1 - mask)."""
+
+    def __init__(self, *args, **kwargs):
+        super().__init__()
+        self.attn = MultiheadAttention(*args, **kwargs)
+
+    def forward(self, x, mask):
+        return self.attn(x, mask)
+
+
+class InvariantPointAttention(nn.Module):
+    """Parameters of ipa.py:34-90 (c_z = 0) and the eager forward of ipa.py:92-255."""
+
+    def __init__(self, c_s, c_z, c_hidden, no_heads, no_qk_points, no_v_points, inf=1e5, eps=1e-8, dropout=0.0):
+        super().__init__()
+        assert c_z == 0
+        self.c_s, self.c_hidden, self.no_heads = c_s, c_hidden, no_heads
+        self.no_qk_points, self.no_v_points = no_qk_points, no_v_points
+        self.inf, self.eps = inf, eps
+        hc = c_hidden * no_heads
+        self.linear_q = nn.Linear(c_s, hc)
+        self.linear_kv = nn.Linear(c_s, 2 * hc)
+        self.linear_q_points = nn.Linear(c_s, no_heads * no_qk_points * 3)
+        self.linear_kv_points = nn.Linear(c_s, no_heads * (no_qk_points + no_v_points) * 3)
+        self.head_weights = nn.Parameter(torch.full((no_heads,), 0.541324854612918))
+        self.linear_out = nn.Linear(no_heads * (c_hidden + no_v_points * 4), c_s)
+        nn.init.zeros_(self.linear_out.weight)
+        nn.init.zeros_(self.linear_out.bias)
+
+    def forward(self, s, rots, trans, mask):
+        B, L, _ = s.shape
+        H, c, Pq, Pv = self.no_heads, self.c_hidden, self.no_qk_points, self.no_v_points
+        q = self.linear_q(s).reshape(B, L, H, c)
+        kv = self.linear_kv(s).reshape(B, L, H, 2 * c)
+        k, v = kv[..., :c], kv[..., c:]
+
+        def points(lin, n):
+            raw = lin(s)
+            pts = torch.stack(torch.split(raw, n, dim=-1), dim=-1)
+            r = rots[:, :, None]
+            x, y, z = pts.unbind(-1)
+            rp = torch.stack([r[..., i, 0] * x + r[..., i, 1] * y + r[..., i, 2] * z for i in range(3)], -1)
+            return rp + trans[:, :, None]
+
+        q_pts = points(self.linear_q_points, H * Pq).reshape(B, L, H, Pq, 3)
+        kv_pts = points(self.linear_kv_points, H * (Pq + Pv)).reshape(B, L, H, Pq + Pv, 3)
+        k_pts, v_pts = kv_pts[..., :Pq, :], kv_pts[..., Pq:, :]
+        a = torch.einsum("bihc,bjhc->bhij", q, k) * math.sqrt(1.0 / (3 * c))
+        d2 = ((q_pts[:, :, None] - k_pts[:, None, :]) ** 2).sum(-1)
+        hw = F.softplus(self.head_weights) * math.sqrt(1.0 / (3 * (Pq * 9.0 / 2)))
+        pt = (d2 * hw[:, None]).sum(-1) * (-0.5)
+        sq = self.inf * (mask[:, :, None] * mask[:, None, :] - 1)
+        a = torch.softmax(a + pt.permute(0, 3, 1, 2) + sq[:, None], dim=-1)
+        o = torch.einsum("bhij,bjhc->bihc", a, v).reshape(B, L, H * c)
+        opt = torch.einsum("bhij,bjhpx->bihpx", a, v_pts) - trans[:, :, None, None]
+        r = rots[:, :, None, None]
+        x, y, z = opt.unbind(-1)
+        opt = torch.stack([r[..., 0, i] * x + r[..., 1, i] * y + r[..., 2, i] * z for i in range(3)], -1)
+        nrm = torch.sqrt((opt ** 2).sum(-1) + self.eps).reshape(B, L, H * Pv)
+        opt = opt.reshape(B, L, H * Pv, 3)
+        return self.linear_out(torch.cat([o, opt[..., 0], opt[..., 1], opt[..., 2], nrm], -1))

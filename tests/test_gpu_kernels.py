@@ -1,0 +1,248 @@
+"""Per-kernel numerics of libmdgen_hip.so against plain PyTorch fp32 references of the same op
+(called through the C ABI: mdg_gemm / mdg_attn_temporal / mdg_attn_spatial / mdg_embed /
+mdg_final_euler)."""
+import ctypes
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    from mdgen_finetune_amd import _lib
+
+    return _lib.load()
+
+
+def _s():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _tol(dt):
+    return (2e-5, 2e-5) if dt == "f32" else (2e-2, 2e-2)
+
+
+CT = {"f32": torch.float32, "bf16": torch.bfloat16}
+ENUM = {"f32": 0, "bf16": 1}
+
+
+def _desc(**kw):
+    from mdgen_finetune_amd import _lib
+
+    d = _lib.MdgGemmDesc()
+    for k, v in kw.items():
+        setattr(d, k, v)
+    return d
+
+
+def _ln_mod(a, mods, rows_per, sh_off, sc_off, C, eps=1e-6):
+    y = torch.nn.functional.layer_norm(a, (a.shape[-1],), eps=eps)
+    b = torch.arange(a.shape[0], device=a.device) // rows_per
+    m = mods[b]
+    return y * (1 + m[:, sc_off:sc_off + C]) + m[:, sh_off:sh_off + C]
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+@pytest.mark.parametrize("M,N,K,act", [(200, 384, 384, 0), (64, 1536, 384, 1), (130, 192, 1536, 2), (7, 64, 64, 0)])
+def test_gemm_plain_store(lib, dt, M, N, K, act):
+    from mdgen_finetune_amd import _lib
+
+    g = torch.Generator(device="cuda").manual_seed(M + N)
+    A = torch.randn(M, K, device="cuda", generator=g).to(CT[dt])
+    W = (torch.randn(N, K, device="cuda", generator=g) / math.sqrt(K)).to(CT[dt])
+    bias = torch.randn(N, device="cuda", generator=g)
+    out = torch.empty(M, N, device="cuda")
+    d = _desc(dtype=ENUM[dt], a_mode=0, epi=0, act=act, M=M, N=N, K=K, A=A.data_ptr(), lda=K, W=W.data_ptr(),
+              ldw=K, bias=bias.data_ptr(), out=out.data_ptr(), ldo=N, out_f32=1)
+    _lib.check(lib.mdg_gemm(ctypes.byref(d), _s()), "mdg_gemm")
+    ref = A.float() @ W.float().T + bias
+    ref = {0: ref, 1: ref * 0.5 * (1 + torch.erf(ref / math.sqrt(2))), 2: torch.nn.functional.silu(ref)}[act]
+    rtol, atol = _tol(dt)
+    torch.testing.assert_close(out, ref, rtol=rtol, atol=atol)
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+def test_gemm_lnmod_gate_res(lib, dt):
+    from mdgen_finetune_amd import _lib
+
+    M, C, TL = 300, 384, 100
+    g = torch.Generator(device="cuda").manual_seed(3)
+    A = torch.randn(M, C, device="cuda", generator=g) * 3 + 1
+    W = (torch.randn(C, C, device="cuda", generator=g) / math.sqrt(C)).to(CT[dt])
+    bias = torch.randn(C, device="cuda", generator=g)
+    mods = torch.randn(3, 9 * C, device="cuda", generator=g) * 0.5
+    resid = torch.randn(M, C, device="cuda", generator=g)
+    r0 = resid.clone()
+    d = _desc(dtype=ENUM[dt], a_mode=1, epi=1, M=M, N=C, K=C, A=A.data_ptr(), lda=C, W=W.data_ptr(), ldw=C,
+              bias=bias.data_ptr(), mods=mods.data_ptr(), mod_stride=9 * C, rows_per_mod=TL, shift_off=3 * C,
+              scale_off=4 * C, ln_eps=1e-6, resid=resid.data_ptr(), ldr=C, gate=mods.data_ptr(), gate_off=5 * C)
+    _lib.check(lib.mdg_gemm(ctypes.byref(d), _s()), "mdg_gemm")
+    y = _ln_mod(A, mods, TL, 3 * C, 4 * C, C).to(CT[dt]).float()
+    b = torch.arange(M, device="cuda") // TL
+    ref = r0 + mods[b, 5 * C:6 * C] * (y @ W.float().T + bias)
+    rtol, atol = _tol(dt)
+    torch.testing.assert_close(resid, ref, rtol=rtol, atol=atol * 10)
+
+
+def _rope_ref(x, pos, inv_freq):
+    # x [..., D] at integer positions pos [...]
+    half = x.shape[-1] // 2
+    f = pos[..., None].float() * inv_freq
+    c, s = torch.cat([f.cos(), f.cos()], -1), torch.cat([f.sin(), f.sin()], -1)
+    rot = torch.cat([-x[..., half:], x[..., :half]], -1)
+    return x * c + rot * s
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+@pytest.mark.parametrize("layout", [0, 1])
+def test_gemm_qkv_rope_layouts(lib, dt, layout):
+    from mdgen_finetune_amd import _lib
+
+    B, T, L, H, D = 2, 37, 4, 16, 24
+    C, M = H * D, B * T * L
+    g = torch.Generator(device="cuda").manual_seed(5 + layout)
+    A = torch.randn(M, C, device="cuda", generator=g)
+    W = (torch.randn(3 * C, C, device="cuda", generator=g) / math.sqrt(C)).to(CT[dt])
+    bias = torch.randn(3 * C, device="cuda", generator=g)
+    mods = torch.randn(B, 9 * C, device="cuda", generator=g) * 0.3
+    inv = 1.0 / (10000 ** (torch.arange(0, D, 2).float() / D))
+    S = (L if layout == 0 else T) + 1
+    f = torch.arange(S).float()[:, None] * inv
+    table = torch.cat([f.cos().reshape(-1), f.sin().reshape(-1)]).cuda()
+    qs = 0.2
+    if layout == 0:
+        out = torch.zeros(M, 3, H, 32, device="cuda", dtype=CT[dt])
+    else:
+        out = torch.zeros(3, B * L, H, T, 32, device="cuda", dtype=CT[dt])
+    d = _desc(dtype=ENUM[dt], a_mode=1, epi=2, M=M, N=3 * C, K=C, A=A.data_ptr(), lda=C, W=W.data_ptr(), ldw=C,
+              bias=bias.data_ptr(), mods=mods.data_ptr(), mod_stride=9 * C, rows_per_mod=T * L, shift_off=0,
+              scale_off=C, ln_eps=1e-6, qkv_layout=layout, qkv_out=out.data_ptr(), H=H, D=D, T=T, L=L, qscale=qs,
+              rope=table.data_ptr(), rope_rows=S)
+    _lib.check(lib.mdg_gemm(ctypes.byref(d), _s()), "mdg_gemm")
+    y = _ln_mod(A, mods, T * L, 0, C, C).to(CT[dt]).float()
+    p = (y @ W.float().T + bias).reshape(B, T, L, 3, H, D)
+    pos = (torch.arange(L) if layout == 0 else torch.arange(T)).cuda()
+    posb = pos.reshape(1, 1, L, 1) if layout == 0 else pos.reshape(1, T, 1, 1)
+    posb = posb.expand(B, T, L, H)
+    q = _rope_ref(p[..., 0, :, :] * qs, posb, inv.cuda())
+    k = _rope_ref(p[..., 1, :, :], posb, inv.cuda())
+    v = p[..., 2, :, :]
+    ref = torch.stack([q, k, v], 3)                               # [B,T,L,3,H,D]
+    if layout == 0:
+        got = out.float().reshape(B, T, L, 3, H, 32)
+    else:
+        got = out.float().reshape(3, B, L, H, T, 32).permute(1, 4, 2, 0, 3, 5)
+    rtol, atol = _tol(dt)
+    torch.testing.assert_close(got[..., :D], ref, rtol=rtol, atol=atol * 5)
+    assert torch.all(got[..., D:] == 0)
+
+
+def _attn_ref(q, k, v, kb, vb, keyvalid, base2):
+    # q [N,S,D], k/v [N,S,D], bias row kb/vb [D]; keyvalid [N,S]
+    N, S, D = q.shape
+    kk = torch.cat([k, kb.expand(N, 1, D)], 1)
+    vv = torch.cat([v, vb.expand(N, 1, D)], 1)
+    s = q @ kk.transpose(1, 2)
+    if base2:
+        s = s * math.log(2.0)
+    valid = torch.cat([keyvalid, torch.ones(N, 1, dtype=torch.bool, device=q.device)], 1)
+    s = s.masked_fill(~valid[:, None, :], float("-inf"))
+    return torch.softmax(s, -1) @ vv
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+@pytest.mark.parametrize("T", [1, 63, 64, 129, 1000])
+def test_attn_temporal(lib, dt, T):
+    from mdgen_finetune_amd import _lib
+
+    B, L, H, D = 1, 3, 4, 24
+    BL = B * L
+    g = torch.Generator(device="cuda").manual_seed(T)
+    qkv = torch.zeros(3, BL, H, T, 32, device="cuda")
+    qkv[..., :D] = torch.randn(3, BL, H, T, D, device="cuda", generator=g)
+    qkv[2, ..., D] = 1.0
+    qkv = qkv.to(CT[dt])
+    mask = torch.ones(B, T, L, device="cuda")
+    if T > 3:
+        mask[:, T // 3: T // 2, 1] = 0          # a padded run of keys in sequence 1
+        mask[:, :, 2] = 0                        # every key of sequence 2 padded: bias row only
+    kvb = torch.zeros(H, 2, 32, device="cuda")
+    kvb[:, :, :D] = torch.randn(H, 2, D, device="cuda", generator=g)
+    kvb[:, 1, D] = 1.0
+    kbias = torch.where(mask.permute(0, 2, 1).reshape(BL, T) != 0, 0.0, float("-inf")).contiguous()
+    out = torch.zeros(B * T * L, H * D, device="cuda", dtype=CT[dt])
+    _lib.check(lib.mdg_attn_temporal(ENUM[dt], B, T, L, H, D, qkv.data_ptr(), kbias.data_ptr(), kvb.data_ptr(),
+                                     out.data_ptr(), _s()), "attn_temporal")
+    qf = qkv.float()
+    got = out.float().reshape(B, T, L, H, D)
+    for h in range(H):
+        ref = _attn_ref(qf[0, :, h, :, :D], qf[1, :, h, :, :D], qf[2, :, h, :, :D], kvb[h, 0, :D], kvb[h, 1, :D],
+                        mask.permute(0, 2, 1).reshape(BL, T) != 0, base2=True)  # [BL, T, D]
+        rtol, atol = _tol(dt)
+        torch.testing.assert_close(got[0, :, :, h].permute(1, 0, 2), ref, rtol=rtol * 2, atol=atol * 2)
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+def test_attn_spatial(lib, dt):
+    from mdgen_finetune_amd import _lib
+
+    NF, L, H, D = 50, 5, 16, 24
+    g = torch.Generator(device="cuda").manual_seed(1)
+    qkv = torch.zeros(NF * L, 3, H, 32, device="cuda")
+    qkv[..., :D] = torch.randn(NF * L, 3, H, D, device="cuda", generator=g)
+    qkv = qkv.to(CT[dt])
+    mask = torch.ones(NF, L, device="cuda")
+    mask[::3, 2] = 0
+    mask[1::7, :] = 0
+    kvb = torch.zeros(H, 2, 32, device="cuda")
+    kvb[:, :, :D] = torch.randn(H, 2, D, device="cuda", generator=g)
+    out = torch.zeros(NF * L, H * D, device="cuda", dtype=CT[dt])
+    _lib.check(lib.mdg_attn_spatial(ENUM[dt], NF, L, H, D, qkv.data_ptr(), kvb.data_ptr(), mask.data_ptr(),
+                                    out.data_ptr(), _s()), "attn_spatial")
+    qf = qkv.float().reshape(NF, L, 3, H, 32)
+    got = out.float().reshape(NF, L, H, D)
+    for h in range(H):
+        ref = _attn_ref(qf[:, :, 0, h, :D], qf[:, :, 1, h, :D], qf[:, :, 2, h, :D], kvb[h, 0, :D], kvb[h, 1, :D],
+                        mask != 0, base2=False)
+        rtol, atol = _tol(dt)
+        torch.testing.assert_close(got[:, :, h], ref, rtol=rtol * 2, atol=atol * 2)
+
+
+def test_embed_and_final_euler(lib):
+    from mdgen_finetune_amd import _lib
+
+    B, T, L, C, K = 2, 10, 4, 384, 21
+    N = B * T * L
+    g = torch.Generator(device="cuda").manual_seed(2)
+    x = torch.randn(N, K, device="cuda", generator=g)
+    W = torch.randn(C, K, device="cuda", generator=g)
+    bias = torch.randn(C, device="cuda", generator=g)
+    pos = torch.randn(L, C, device="cuda", generator=g)
+    emb = torch.randn(2, C, device="cuda", generator=g)
+    idx = torch.randint(0, 2, (N,), device="cuda", generator=g)
+    ipa = torch.randn(B * L, C, device="cuda", generator=g)
+    out = torch.empty(N, C, device="cuda")
+    _lib.check(lib.mdg_embed(N, T, L, C, K, x.data_ptr(), W.data_ptr(), bias.data_ptr(), None, pos.data_ptr(),
+                             emb.data_ptr(), idx.data_ptr(), ipa.data_ptr(), out.data_ptr(), _s()), "embed")
+    n = torch.arange(N, device="cuda")
+    ref = x @ W.T + bias + pos[n % L] + emb[idx] + ipa[(n // (T * L)) * L + n % L]
+    torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-4)
+
+    Wf = torch.randn(K, C, device="cuda", generator=g) / 20
+    bf = torch.randn(K, device="cuda", generator=g)
+    mods = torch.randn(B, 2 * C, device="cuda", generator=g) * 0.3
+    xin = torch.randn(N, K, device="cuda", generator=g)
+    xo = torch.empty_like(xin)
+    vo = torch.empty_like(xin)
+    _lib.check(lib.mdg_final_euler(N, T * L, C, K, Wf.data_ptr(), bf.data_ptr(), mods.data_ptr(), out.data_ptr(),
+                                   xin.data_ptr(), 0.25, xo.data_ptr(), vo.data_ptr(), _s()), "final_euler")
+    b = n // (T * L)
+    y = torch.nn.functional.layer_norm(out, (C,), eps=1e-6) * (1 + mods[b, C:]) + mods[b, :C]
+    vref = y @ Wf.T + bf
+    torch.testing.assert_close(vo, vref, rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(xo, xin + 0.25 * vo, rtol=0, atol=1e-6)
