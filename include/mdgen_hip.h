@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define MDG_ABI_VERSION 1
+#define MDG_ABI_VERSION 2
 #define MDG_MAX_LAYERS 16
 #define MDG_DP 32 /* padded head dim of every attention operand buffer (head_dim <= 31) */
 
@@ -49,7 +49,7 @@ enum {
 
 /* GEMM building block: out = epilogue( prologue(A) . W^T + bias ) */
 enum { MDG_A_PLAIN = 0, MDG_A_LNMOD = 1 };
-enum { MDG_EPI_STORE = 0, MDG_EPI_GATE_RES = 1, MDG_EPI_QKV = 2 };
+enum { MDG_EPI_STORE = 0, MDG_EPI_GATE_RES = 1, MDG_EPI_QKV = 2, MDG_EPI_EULER = 3 };
 enum { MDG_ACT_NONE = 0, MDG_ACT_GELU = 1, MDG_ACT_SILU = 2 };
 enum { MDG_QKV_SPATIAL = 0, MDG_QKV_TEMPORAL = 1 };
 
@@ -62,12 +62,15 @@ typedef struct {
 } mdg_dims;
 
 typedef struct {
-  const void* wqkv[2];  /* CT [3C][C], rows q|k|v (nn.Linear layout); [0]=mha_l, [1]=mha_t */
-  const float* bqkv[2]; /* [3C] */
+  const void* wqkv[2];  /* CT [3C][C], rows q|k|v (nn.Linear layout); [0]=mha_l, [1]=mha_t.
+                           With RoPE, each q and k head's D rows are PAIR-INTERLEAVED:
+                           row 2i = dim i, row 2i+1 = dim i + D/2 (v rows natural). */
+  const float* bqkv[2]; /* [3C], same row order */
   const void* wo[2];    /* CT [C][C] out_proj */
   const float* bo[2];   /* [C] */
-  const float* kvb[2];  /* [H][2][32]: bias_k RoPE-rotated at position S (=L or T), bias_v;
-                           bias_v[D] = 1 (the softmax row sum rides in the pad column) */
+  const float* kvb[2];  /* [H][2][32]: bias_k RoPE-rotated at position S (=L or T) in the
+                           interleaved order, bias_v natural order with bias_v[D] = 1 (the
+                           softmax row sum rides in the pad column) */
   const void* w1;       /* CT [F][C] fc1 */
   const float* b1;      /* [F] */
   const void* w2;       /* CT [C][F] fc2 */
@@ -76,9 +79,9 @@ typedef struct {
 
 typedef struct {
   mdg_dims dims;
-  const float* w_l2e;   /* latent_to_emb.weight [C][latent] */
-  const float* w_final; /* emb_to_latent.linear.weight [latent][C] */
-  const float* b_final; /* [latent] */
+  const float* w_l2e_t; /* latent_to_emb.weight TRANSPOSED: [latent][C] fp32 */
+  const void* w_final;  /* emb_to_latent.linear.weight, CT [round_up(latent,32)][C], pad rows 0 */
+  const float* b_final; /* [round_up(latent,32)], pad 0 */
   const float* rope_l;  /* [L+1][D/2] cos, then [L+1][D/2] sin (spatial) */
   const float* rope_t;  /* [T+1][D/2] cos, then [T+1][D/2] sin (temporal) */
   mdg_layer_weights layers[MDG_MAX_LAYERS];
@@ -115,6 +118,8 @@ typedef struct {
   /* QKV: N == 3*H*D; q scaled by qscale; RoPE on q,k at pos l (spatial) or t (temporal) */
   int32_t qkv_layout; void* qkv_out; int32_t H, D, T, L; float qscale;
   const float* rope; int32_t rope_rows; /* cos [rope_rows][D/2] then sin; null = no RoPE */
+  /* EULER: x_out (= out, row stride ldo) = x_in + dt * v, v_out = v, for columns < n_valid */
+  const float* x_in; float* v_out; float dt; int32_t n_valid;
 } mdg_gemm_desc;
 
 int mdg_abi_version(void);
@@ -126,11 +131,12 @@ int mdg_workspace_init(const mdg_dims* d, void* ws, void* stream);
 /* key-padding additive bias for the temporal attention from mask [B,T,L] (0 -> -inf) */
 int mdg_prepare_mask(const mdg_dims* d, const float* mask, void* ws, void* stream);
 
-/* out[n][c] = sum_j x[n][j] W[c][j] + bias[c] + base[n][c] + pos[l][c]
-               + emb[idx[n]][c] + ipa[b*L + l][c]   (every term but x.W optional)
+/* out[n][c] = sum_j x[n][j] Wt[j][c] + bias[c] + base[n][c] + pos[l][c]
+               + emb[idx[n]][c] + ipa[b*L + l][c]   (every term but x.Wt optional;
+               Wt is the nn.Linear weight transposed, [K][C], so channel reads coalesce)
    latent_to_emb / cond_to_emb + mask_to_emb + pos_embed (latent_model.py:242-250) */
 int mdg_embed(int32_t N, int32_t T, int32_t L, int32_t C, int32_t K, const float* x,
-              const float* W, const float* bias, const float* base, const float* pos,
+              const float* Wt, const float* bias, const float* base, const float* pos,
               const float* emb, const int64_t* idx, const float* ipa, float* out, void* stream);
 
 /* One LatentMDGenLayer (latent_model.py:456-493) on the residual h [N][C], in place. */
@@ -138,9 +144,10 @@ int mdg_layer_fwd(const mdg_dims* d, const mdg_layer_weights* w, const float* ro
                   const float* rope_t, const float* mods, const float* mask, float* h, void* ws,
                   void* stream);
 
-/* FinalLayer (layers.py:58-75) + Euler update (integrators.py:106-113). */
-int mdg_final_euler(int32_t N, int32_t rows_per_b, int32_t C, int32_t latent,
-                    const float* w_final, const float* b_final, const float* mods_final,
+/* FinalLayer (layers.py:58-75) + Euler update (integrators.py:106-113) as one LN-prologue
+   GEMM; w_final / b_final padded as in mdg_model.  dtype selects the operand type. */
+int mdg_final_euler(int32_t dtype, int32_t N, int32_t rows_per_b, int32_t C, int32_t latent,
+                    const void* w_final, const float* b_final, const float* mods_final,
                     const float* h, const float* x_in, float dt, float* x_out, float* v_out,
                     void* stream);
 

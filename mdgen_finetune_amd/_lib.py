@@ -16,7 +16,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libmdgen_hi
 
 MDG_F32, MDG_BF16 = 0, 1
 MDG_A_PLAIN, MDG_A_LNMOD = 0, 1
-MDG_EPI_STORE, MDG_EPI_GATE_RES, MDG_EPI_QKV = 0, 1, 2
+MDG_EPI_STORE, MDG_EPI_GATE_RES, MDG_EPI_QKV, MDG_EPI_EULER = 0, 1, 2, 3
 MDG_ACT_NONE, MDG_ACT_GELU, MDG_ACT_SILU = 0, 1, 2
 MDG_QKV_SPATIAL, MDG_QKV_TEMPORAL = 0, 1
 MDG_MAX_LAYERS = 16
@@ -37,7 +37,7 @@ class MdgLayerWeights(ctypes.Structure):
 
 
 class MdgModel(ctypes.Structure):
-    _fields_ = [("dims", MdgDims), ("w_l2e", _vp), ("w_final", _vp), ("b_final", _vp),
+    _fields_ = [("dims", MdgDims), ("w_l2e_t", _vp), ("w_final", _vp), ("b_final", _vp),
                 ("rope_l", _vp), ("rope_t", _vp), ("layers", MdgLayerWeights * MDG_MAX_LAYERS)]
 
 
@@ -58,6 +58,7 @@ class MdgGemmDesc(ctypes.Structure):
         ("resid", _vp), ("ldr", _i32), ("gate", _vp), ("gate_off", _i32),
         ("qkv_layout", _i32), ("qkv_out", _vp), ("H", _i32), ("D", _i32), ("T", _i32), ("L", _i32),
         ("qscale", _f32), ("rope", _vp), ("rope_rows", _i32),
+        ("x_in", _vp), ("v_out", _vp), ("dt", _f32), ("n_valid", _i32),
     ]
 
 
@@ -72,14 +73,14 @@ SIGNATURES = [
     ("mdg_embed", _i32, [_i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     ("mdg_layer_fwd", _i32, [ctypes.POINTER(MdgDims), ctypes.POINTER(MdgLayerWeights), _vp, _vp, _vp,
                              _vp, _vp, _vp, _vp]),
-    ("mdg_final_euler", _i32, [_i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _vp]),
+    ("mdg_final_euler", _i32, [_i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _vp]),
     ("mdg_denoise_step", _i32, [ctypes.POINTER(MdgModel), ctypes.POINTER(MdgStepIO), _vp, _vp, _vp]),
     ("mdg_gemm", _i32, [ctypes.POINTER(MdgGemmDesc), _vp]),
     ("mdg_attn_spatial", _i32, [_i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
     ("mdg_attn_temporal", _i32, [_i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
 ]
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 _LIB = None
 
 

@@ -11,9 +11,12 @@
 #include "common.h"
 
 namespace mdg {
-int gemm_pick_bn(const mdg_gemm_desc& p);
-size_t gemm_smem_bytes(const mdg_gemm_desc& p, int bn);
-hipError_t gemm_launch(const mdg_gemm_desc& p, int bn, hipStream_t s);
+struct GemmPlan {
+  int bm, bn;
+  size_t smem;
+};
+GemmPlan gemm_plan(const mdg_gemm_desc& p);
+hipError_t gemm_launch(const mdg_gemm_desc& p, const GemmPlan& g, hipStream_t s);
 hipError_t attn_temporal_launch(int dtype, int B, int T, int L, int H, int D, const void* qkv_t,
                                 const float* kbias, const float* kvb, void* out, hipStream_t s);
 hipError_t attn_spatial_launch(int dtype, int nf, int L, int H, int D, const void* qkv,
@@ -21,10 +24,6 @@ hipError_t attn_spatial_launch(int dtype, int nf, int L, int H, int D, const voi
 hipError_t embed_launch(int N, int T, int L, int C, int K, const float* x, const float* W,
                         const float* bias, const float* base, const float* pos, const float* emb,
                         const int64_t* idx, const float* ipa, float* out, hipStream_t s);
-hipError_t final_euler_launch(int N, int rows_per_b, int C, int lat, const float* Wf,
-                              const float* bf, const float* mods, const float* h,
-                              const float* x_in, float dt, float* x_out, float* v_out,
-                              hipStream_t s);
 hipError_t mask_bias_launch(int B, int T, int L, const float* mask, float* kbias, hipStream_t s);
 hipError_t set_vpad_launch(int dtype, void* v, size_t rows, int D, hipStream_t s);
 }  // namespace mdg
@@ -158,14 +157,19 @@ int mdg_gemm(const mdg_gemm_desc* g, void* stream) {
       if (g->rope && g->rope_rows < (g->qkv_layout == MDG_QKV_SPATIAL ? g->L : g->T))
         return fail(MDG_E_SHAPE, "gemm QKV: rope table too short");
       break;
+    case MDG_EPI_EULER:
+      if (g->n_valid <= 0 || g->n_valid > g->N || g->ldo < g->n_valid)
+        return fail(MDG_E_SHAPE, "gemm EULER: n_valid=%d N=%d ldo=%d", g->n_valid, g->N, g->ldo);
+      if (g->out && !g->x_in) return fail(MDG_E_ARG, "gemm EULER: x_out without x_in");
+      break;
     default:
       return fail(MDG_E_ARG, "gemm: epi %d", g->epi);
   }
-  const int bn = mdg::gemm_pick_bn(*g);
-  if (!bn) return fail(MDG_E_SHAPE, "gemm: no tile fits N=%d (D=%d)", g->N, g->D);
-  if (mdg::gemm_smem_bytes(*g, bn) > 160 * 1024)
-    return fail(MDG_E_SHAPE, "gemm: K=%d needs more LDS than a CU has", g->K);
-  return hip_check(mdg::gemm_launch(*g, bn, (hipStream_t)stream), "gemm launch");
+  const mdg::GemmPlan plan = mdg::gemm_plan(*g);
+  if (!plan.bn) return fail(MDG_E_SHAPE, "gemm: no tile fits N=%d", g->N);
+  if (plan.smem > 160 * 1024)
+    return fail(MDG_E_SHAPE, "gemm: K=%d needs %zu B of LDS (> 160 KiB)", g->K, plan.smem);
+  return hip_check(mdg::gemm_launch(*g, plan, (hipStream_t)stream), "gemm launch");
 }
 
 int mdg_attn_spatial(int32_t dtype, int32_t n_frames, int32_t L, int32_t H, int32_t D,
@@ -194,28 +198,35 @@ int mdg_attn_temporal(int32_t dtype, int32_t B, int32_t T, int32_t L, int32_t H,
 }
 
 int mdg_embed(int32_t N, int32_t T, int32_t L, int32_t C, int32_t K, const float* x,
-              const float* W, const float* bias, const float* base, const float* pos,
+              const float* Wt, const float* bias, const float* base, const float* pos,
               const float* emb, const int64_t* idx, const float* ipa, float* out, void* stream) {
-  if (!x || !W || !out) return fail(MDG_E_ARG, "embed: null x/W/out");
+  if (!x || !Wt || !out) return fail(MDG_E_ARG, "embed: null x/Wt/out");
   if (N <= 0 || T <= 0 || L <= 0 || C <= 0 || K <= 0 || K > 64 || N % (T * L))
     return fail(MDG_E_SHAPE, "embed: N=%d T=%d L=%d C=%d K=%d", N, T, L, C, K);
   if ((emb == nullptr) != (idx == nullptr)) return fail(MDG_E_ARG, "embed: emb/idx");
-  return hip_check(mdg::embed_launch(N, T, L, C, K, x, W, bias, base, pos, emb, idx, ipa, out,
+  return hip_check(mdg::embed_launch(N, T, L, C, K, x, Wt, bias, base, pos, emb, idx, ipa, out,
                                      (hipStream_t)stream),
                    "embed");
 }
 
-int mdg_final_euler(int32_t N, int32_t rows_per_b, int32_t C, int32_t latent,
-                    const float* w_final, const float* b_final, const float* mods_final,
+int mdg_final_euler(int32_t dtype, int32_t N, int32_t rows_per_b, int32_t C, int32_t latent,
+                    const void* w_final, const float* b_final, const float* mods_final,
                     const float* h, const float* x_in, float dt, float* x_out, float* v_out,
                     void* stream) {
   if (!w_final || !b_final || !mods_final || !h) return fail(MDG_E_ARG, "final_euler: null pointer");
-  if (x_out && !x_in) return fail(MDG_E_ARG, "final_euler: x_out without x_in");
-  if (N <= 0 || rows_per_b <= 0 || C % 64 || C > 512 || latent <= 0 || latent > 64)
-    return fail(MDG_E_SHAPE, "final_euler: N=%d C=%d latent=%d", N, C, latent);
-  return hip_check(mdg::final_euler_launch(N, rows_per_b, C, latent, w_final, b_final, mods_final,
-                                           h, x_in, dt, x_out, v_out, (hipStream_t)stream),
-                   "final_euler");
+  if (N <= 0 || rows_per_b <= 0 || latent <= 0 || latent > 64)
+    return fail(MDG_E_SHAPE, "final_euler: N=%d latent=%d", N, latent);
+  mdg_gemm_desc g;
+  memset(&g, 0, sizeof(g));
+  g.dtype = dtype;
+  g.a_mode = MDG_A_LNMOD;
+  g.epi = MDG_EPI_EULER;
+  g.M = N; g.N = (latent + 31) / 32 * 32; g.K = C;
+  g.A = h; g.lda = C; g.W = w_final; g.ldw = C; g.bias = b_final;
+  g.mods = mods_final; g.mod_stride = 2 * C; g.rows_per_mod = rows_per_b; g.shift_off = 0; g.scale_off = C;
+  g.ln_eps = 1e-6f;
+  g.out = x_out; g.ldo = latent; g.x_in = x_in; g.v_out = v_out; g.dt = dt; g.n_valid = latent;
+  return mdg_gemm(&g, stream);
 }
 
 int mdg_layer_fwd(const mdg_dims* d, const mdg_layer_weights* w, const float* rope_l,
@@ -290,7 +301,7 @@ int mdg_denoise_step(const mdg_model* m, const mdg_step_io* io, const float* mas
   if (!io->x_in || !io->base || !io->mods || !io->mods_final || !io->h)
     return fail(MDG_E_ARG, "denoise_step: null io pointer");
   const int N = d->B * d->T * d->L;
-  if (int e = mdg_embed(N, d->T, d->L, d->C, d->latent, io->x_in, m->w_l2e, nullptr, io->base,
+  if (int e = mdg_embed(N, d->T, d->L, d->C, d->latent, io->x_in, m->w_l2e_t, nullptr, io->base,
                         nullptr, nullptr, nullptr, io->ipa, io->h, stream))
     return e;
   const size_t mstride = (size_t)d->B * 9 * d->C;
@@ -298,7 +309,7 @@ int mdg_denoise_step(const mdg_model* m, const mdg_step_io* io, const float* mas
     if (int e = mdg_layer_fwd(d, &m->layers[i], m->rope_l, m->rope_t, io->mods + i * mstride, mask,
                               io->h, ws, stream))
       return e;
-  return mdg_final_euler(N, d->T * d->L, d->C, d->latent, m->w_final, m->b_final, io->mods_final,
+  return mdg_final_euler(d->dtype, N, d->T * d->L, d->C, d->latent, m->w_final, m->b_final, io->mods_final,
                          io->h, io->x_in, io->dt, io->x_out, io->v_out, stream);
 }
 

@@ -22,6 +22,7 @@ typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 typedef __attribute__((ext_vector_type(8))) float f32x8;
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
 
 template <typename CT> struct V8;
 template <> struct V8<bf16_t> { using T = bf16x8; };

@@ -1,18 +1,18 @@
-// Small kernels around the block stack: token embedding, FinalLayer + Euler update,
-// key-padding bias, workspace pad initialisation.
+// Small kernels around the block stack: token embedding, key-padding bias, workspace pad
+// initialisation.  (FinalLayer + Euler runs as the EULER epilogue of the GEMM, gemm.hip.)
 #include "../../include/mdgen_hip.h"
 #include "common.h"
 
 namespace mdg {
 
-// out[n][c] = sum_j x[n][j] W[c][j] + bias[c] + base[n][c] + pos[l][c] + emb[idx[n]][c]
+// out[n][c] = sum_j x[n][j] Wt[j][c] + bias[c] + base[n][c] + pos[l][c] + emb[idx[n]][c]
 //             + ipa[b*L + l][c]
 // latent_to_emb / cond_to_emb (nn.Linear, K = 21 or 28) + pos_embed + mask_to_emb
 // (latent_model.py:242-250) + the IPA prepend broadcast over frames (latent_model.py:255).
 // K is tiny, so this is a bandwidth kernel: 8 tokens per block share the x rows in LDS.
 __global__ __launch_bounds__(256) void embed_kernel(int N, int T, int L, int C, int K,
                                                     const float* __restrict__ x,
-                                                    const float* __restrict__ W,
+                                                    const float* __restrict__ Wt,
                                                     const float* __restrict__ bias,
                                                     const float* __restrict__ base,
                                                     const float* __restrict__ pos,
@@ -33,7 +33,7 @@ __global__ __launch_bounds__(256) void embed_kernel(int N, int T, int L, int C, 
 #pragma unroll
     for (int r = 0; r < TOK; ++r) acc[r] = 0.f;
     for (int j = 0; j < K; ++j) {
-      const float w = W[(size_t)c * K + j];
+      const float w = Wt[(size_t)j * C + c];  // coalesced across the block's channels
 #pragma unroll
       for (int r = 0; r < TOK; ++r) acc[r] += xs[r][j] * w;
     }
@@ -49,66 +49,6 @@ __global__ __launch_bounds__(256) void embed_kernel(int N, int T, int L, int C, 
       if (emb) v += emb[(size_t)idx[n] * C + c];
       if (ipa) v += ipa[((size_t)(n / (T * L)) * L + l) * C + c];
       out[(size_t)n * C + c] = v;
-    }
-  }
-}
-
-// FinalLayer (layers.py:58-75): v = Linear(LN(h)*(1+scale) + shift), then the Euler update
-// x_out = x_in + dt * v (torchdiffeq fixed-grid Euler, integrators.py:106-113) with the
-// multiply and add rounded separately, as the reference computes dy then y + dy.
-// One wave per token; the [latent][C] weight lives in LDS.
-__global__ __launch_bounds__(256) void final_euler_kernel(int N, int rows_per_b, int C, int lat,
-                                                          const float* __restrict__ Wf,
-                                                          const float* __restrict__ bf,
-                                                          const float* __restrict__ mods,
-                                                          const float* __restrict__ h,
-                                                          const float* __restrict__ x_in,
-                                                          float dt, float* x_out, float* v_out) {
-  extern __shared__ __attribute__((aligned(16))) float Ws[];
-  for (int i = threadIdx.x; i < lat * C; i += 256) Ws[i] = Wf[i];
-  __syncthreads();
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int nper = C >> 6;
-  const float invC = 1.0f / (float)C;
-  for (int n = blockIdx.x * 4 + wave; n < N; n += gridDim.x * 4) {
-    const float* hr = h + (size_t)n * C;
-    float v[8];
-    float s = 0.f;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      v[e] = (e < nper) ? hr[lane + 64 * e] : 0.f;
-      s += v[e];
-    }
-    const float mean = wave_sum(s) * invC;
-    float ss = 0.f;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float d = v[e] - mean;
-      ss += (e < nper) ? d * d : 0.f;
-    }
-    const float rstd = 1.0f / sqrtf(wave_sum(ss) * invC + 1e-6f);
-    const float* mr = mods + (size_t)(n / rows_per_b) * 2 * C;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      if (e < nper) {
-        const int k = lane + 64 * e;
-        v[e] = (v[e] - mean) * rstd * (1.0f + mr[C + k]) + mr[k];
-      }
-    }
-    float mine = 0.f;
-    for (int o = 0; o < lat; ++o) {
-      float part = 0.f;
-#pragma unroll
-      for (int e = 0; e < 8; ++e)
-        if (e < nper) part += v[e] * Ws[o * C + lane + 64 * e];
-      part = wave_sum(part);
-      if (lane == o) mine = part;
-    }
-    if (lane < lat) {
-      const float vv = mine + bf[lane];
-      const size_t off = (size_t)n * lat + lane;
-      if (v_out) v_out[off] = vv;
-      if (x_out) x_out[off] = __fadd_rn(x_in[off], __fmul_rn(dt, vv));
     }
   }
 }
@@ -130,30 +70,11 @@ __global__ void set_vpad_kernel(CT* v, size_t rows, int D) {
   if (i < rows) v[i * MDG_DP + D] = (CT)1.0f;
 }
 
-hipError_t embed_launch(int N, int T, int L, int C, int K, const float* x, const float* W,
+hipError_t embed_launch(int N, int T, int L, int C, int K, const float* x, const float* Wt,
                         const float* bias, const float* base, const float* pos, const float* emb,
                         const int64_t* idx, const float* ipa, float* out, hipStream_t s) {
-  hipLaunchKernelGGL(embed_kernel, dim3((N + 7) / 8), dim3(256), 0, s, N, T, L, C, K, x, W, bias,
+  hipLaunchKernelGGL(embed_kernel, dim3((N + 7) / 8), dim3(256), 0, s, N, T, L, C, K, x, Wt, bias,
                      base, pos, emb, idx, ipa, out);
-  return hipGetLastError();
-}
-
-hipError_t final_euler_launch(int N, int rows_per_b, int C, int lat, const float* Wf,
-                              const float* bf, const float* mods, const float* h,
-                              const float* x_in, float dt, float* x_out, float* v_out,
-                              hipStream_t s) {
-  const size_t smem = (size_t)lat * C * sizeof(float);
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&final_euler_kernel),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (e != hipSuccess) return e;
-    attr_set = true;
-  }
-  int grid = (N + 3) / 4;
-  if (grid > 1024) grid = 1024;
-  hipLaunchKernelGGL(final_euler_kernel, dim3(grid), dim3(256), smem, s, N, rows_per_b, C, lat,
-                     Wf, bf, mods, h, x_in, dt, x_out, v_out);
   return hipGetLastError();
 }
 

@@ -78,11 +78,16 @@ class HipEngine:
             raise RuntimeError("the HIP backend needs the model on a ROCm device (model.cuda())")
         with torch.no_grad():
             P = {"layers": []}
+            perm = self._pair_perm() if self.rope else None
             for layer in m.layers:
                 d = {}
                 for i, mha in enumerate((layer.mha_l.attn, layer.mha_t.attn)):
-                    d[f"wqkv{i}"] = torch.cat([mha.q_proj.weight, mha.k_proj.weight, mha.v_proj.weight]).to(ct).contiguous()
-                    d[f"bqkv{i}"] = torch.cat([mha.q_proj.bias, mha.k_proj.bias, mha.v_proj.bias]).float().contiguous()
+                    wq, wk = mha.q_proj.weight, mha.k_proj.weight
+                    bq, bk = mha.q_proj.bias, mha.k_proj.bias
+                    if perm is not None:  # pair-interleave q/k head rows (RoPE partner in lane^1)
+                        wq, wk, bq, bk = wq[perm], wk[perm], bq[perm], bk[perm]
+                    d[f"wqkv{i}"] = torch.cat([wq, wk, mha.v_proj.weight]).to(ct).contiguous()
+                    d[f"bqkv{i}"] = torch.cat([bq, bk, mha.v_proj.bias]).float().contiguous()
                     d[f"wo{i}"] = mha.out_proj.weight.to(ct).contiguous()
                     d[f"bo{i}"] = mha.out_proj.bias.float().contiguous()
                     d[f"bias_k{i}"] = mha.bias_k.detach().float().reshape(-1)
@@ -92,17 +97,30 @@ class HipEngine:
                 d["w2"] = layer.fc2.weight.to(ct).contiguous()
                 d["b2"] = layer.fc2.bias.float().contiguous()
                 P["layers"].append(d)
-            P["w_l2e"] = m.latent_to_emb.weight.float().contiguous()
+            P["w_l2e_t"] = m.latent_to_emb.weight.float().t().contiguous()      # [latent][C]
             P["b_l2e"] = m.latent_to_emb.bias.float().contiguous()
-            P["w_c2e"] = m.cond_to_emb.weight.float().contiguous()
+            P["w_c2e_t"] = m.cond_to_emb.weight.float().t().contiguous()
             P["b_base"] = (m.cond_to_emb.bias + m.latent_to_emb.bias).float().contiguous()
-            P["w_final"] = m.emb_to_latent.linear.weight.float().contiguous()
-            P["b_final"] = m.emb_to_latent.linear.bias.float().contiguous()
+            lp = (self.lat + 31) // 32 * 32                                       # padded to the GEMM tile
+            wf = torch.zeros(lp, self.C, device=dev)
+            wf[: self.lat] = m.emb_to_latent.linear.weight.float()
+            bf = torch.zeros(lp, device=dev)
+            bf[: self.lat] = m.emb_to_latent.linear.bias.float()
+            P["w_final"] = wf.to(ct).contiguous()
+            P["b_final"] = bf
             P["inv_freq"] = m.layers[0].mha_l.attn.rot_emb.inv_freq if self.rope else None
         self._packed, self._pack_key = P, key
         self._states.clear()
         self._graphs.clear()
         return P
+
+    def _pair_perm(self):
+        """Row permutation of a [C] q/k projection: within each head, new row 2i = dim i and
+        2i+1 = dim i + D/2 (the fair-esm rotate-half partner), see gemm.hip QKV epilogue."""
+        D, half = self.D, self.D // 2
+        idx = torch.arange(D)
+        within = torch.where(idx % 2 == 0, idx // 2, idx // 2 + half)
+        return (torch.arange(self.H)[:, None] * D + within[None]).reshape(-1).to(self.model.device)
 
     def _rope_table(self, n_rows):
         """cos | sin tables [n_rows][D/2] exactly as fair-esm builds them (fp32 outer product of
@@ -123,6 +141,8 @@ class HipEngine:
             c2, s2 = torch.cat([cos, cos]), torch.cat([sin, sin])
             rot = torch.cat([-kb[:, half:], kb[:, :half]], -1)
             kb = kb * c2 + rot * s2
+        if table is not None:  # same pair-interleaved order as the packed k rows
+            kb = kb.reshape(-1)[self._pair_perm()].reshape(H, D)
         out = torch.zeros(H, 2, _lib.MDG_DP, device=bias_k.device, dtype=torch.float32)
         out[:, 0, :D] = kb
         out[:, 1, :D] = bias_v.reshape(H, D)
@@ -153,7 +173,7 @@ class HipEngine:
         st.kvb = []
         mstruct = _lib.MdgModel()
         mstruct.dims = st.dims
-        mstruct.w_l2e = P["w_l2e"].data_ptr()
+        mstruct.w_l2e_t = P["w_l2e_t"].data_ptr()
         mstruct.w_final = P["w_final"].data_ptr()
         mstruct.b_final = P["b_final"].data_ptr()
         mstruct.rope_l = _lib.ptr(st.rope_l)
@@ -226,7 +246,12 @@ class HipEngine:
         from .model.latent_model import relative_tensor7
 
         if self.model.tps:
-            self._rel7 = (relative_tensor7(rots, trans, erots, etrans), relative_tensor7(erots, etrans, rots, trans))
+            ov = getattr(self, "rel7_override", None)
+            if ov is not None:  # test hook: inject the reference's own 7-vectors (eigh sign)
+                self._rel7 = tuple(t.to(rots.device, torch.float32) for t in ov)
+            else:
+                self._rel7 = (relative_tensor7(rots, trans, erots, etrans),
+                              relative_tensor7(erots, etrans, rots, trans))
         else:
             self._rel7 = None
 
@@ -238,7 +263,7 @@ class HipEngine:
         if x_cond is not None:
             xc = x_cond.float().contiguous()
             idx = x_cond_mask.to(torch.int64).contiguous()
-            _lib.check(self.lib.mdg_embed(st.N, st.T, st.L, self.C, self.lat, xc.data_ptr(), P["w_c2e"].data_ptr(),
+            _lib.check(self.lib.mdg_embed(st.N, st.T, st.L, self.C, self.lat, xc.data_ptr(), P["w_c2e_t"].data_ptr(),
                                           P["b_base"].data_ptr(), None, _lib.ptr(pos),
                                           m.mask_to_emb.weight.data_ptr(), idx.data_ptr(), None,
                                           st.base.data_ptr(), s), "mdg_embed(cond)")

@@ -247,13 +247,31 @@ class LatentMDGenModel(nn.Module):
 
 
 def relative_tensor7(rots_a, trans_a, rots_b, trans_b):
-    """a.invert().compose(b).to_tensor_7() (rigid_utils.py:1031-1087, 1143-1155) for the TPS
-    branch (latent_model.py:198-199)."""
-    ra_inv = rots_a.transpose(-1, -2)
-    t_inv = -1 * torch.einsum("...ij,...j->...i", ra_inv, trans_a)
-    rot = ra_inv @ rots_b
-    tr = torch.einsum("...ij,...j->...i", ra_inv, trans_b) + t_inv
-    return torch.cat([rot_to_quat(rot), tr], -1)
+    """a.invert().compose(b).to_tensor_7() for the TPS branch (latent_model.py:198-199), in
+    the reference's exact operation order (Rigid.invert 1075-1087, Rigid.compose 1031-1045,
+    rot_matmul 24-57, rot_vec_mul 64-86, to_tensor_7 1143-1155) on the HOST in fp32.
+
+    The quaternion comes from an eigenvector (rot_to_quat, rigid_utils.py:191-210) whose sign
+    flips under 1-ulp changes of the composed rotation for a sizeable fraction of residues, and
+    latent_to_emb_f/_r are linear in it — so this x-independent, once-per-window precompute must
+    reproduce the reference's arithmetic bit for bit; it is not done on the device."""
+    dev = rots_a.device
+    ra, ta, rb, tb = (z.detach().float().cpu() for z in (rots_a, trans_a, rots_b, trans_b))
+    ra_inv = ra.transpose(-1, -2)
+
+    def rvm(r, t):
+        x, y, z = torch.unbind(t, dim=-1)
+        return torch.stack([r[..., i, 0] * x + r[..., i, 1] * y + r[..., i, 2] * z for i in range(3)], dim=-1)
+
+    def rmm(a, b):
+        rows = [torch.stack([a[..., i, 0] * b[..., 0, j] + a[..., i, 1] * b[..., 1, j] + a[..., i, 2] * b[..., 2, j]
+                             for j in range(3)], dim=-1) for i in range(3)]
+        return torch.stack(rows, dim=-2)
+
+    t_inv = -1 * rvm(ra_inv, ta)
+    rot = rmm(ra_inv, rb)
+    tr = rvm(ra_inv, tb) + t_inv
+    return torch.cat([rot_to_quat(rot), tr], -1).to(dev)
 
 
 __all__ = ["LatentMDGenModel", "LatentMDGenLayer", "IPALayer", "Rotation", "F"]

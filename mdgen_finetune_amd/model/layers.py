@@ -23,9 +23,17 @@ def gelu(x):
     return x * 0.5 * (1.0 + torch.erf(x / math.sqrt(2.0)))
 
 
-def timestep_embedding(t, dim=256, max_period=10000):
+def timestep_freqs(dim=256, max_period=10000):
+    """exp(-ln(max_period) * i / half), computed on the CPU exactly as layers.py:42-44 does."""
     half = dim // 2
-    freqs = torch.exp(-math.log(max_period) * torch.arange(0, half, dtype=torch.float32) / half).to(t.device)
+    return torch.exp(-math.log(max_period) * torch.arange(start=0, end=half, dtype=torch.float32) / half)
+
+
+def timestep_embedding(t, dim=256, max_period=10000, freqs=None):
+    half = dim // 2
+    if freqs is None:
+        freqs = timestep_freqs(dim, max_period)
+    freqs = freqs.to(t.device)
     args = t[:, None].float() * freqs[None]
     emb = torch.cat([torch.cos(args), torch.sin(args)], dim=-1)
     if dim % 2:
@@ -39,9 +47,11 @@ class TimestepEmbedder(nn.Module):
         self.mlp = nn.Sequential(nn.Linear(frequency_embedding_size, hidden_size, bias=True), nn.SiLU(),
                                  nn.Linear(hidden_size, hidden_size, bias=True))
         self.frequency_embedding_size = frequency_embedding_size
+        # device-resident copy (not in state_dict) so graph capture never copies host->device
+        self.register_buffer("freqs", timestep_freqs(frequency_embedding_size), persistent=False)
 
     def forward(self, t):
-        return self.mlp(timestep_embedding(t, self.frequency_embedding_size))
+        return self.mlp(timestep_embedding(t, self.frequency_embedding_size, freqs=self.freqs))
 
 
 class FinalLayer(nn.Module):

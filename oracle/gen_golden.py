@@ -133,6 +133,11 @@ def forward_case(name, flags, latent_dim, B, T, L, seed, tps=False, n_pad=0, eul
     for h in hooks:
         h.remove()
     out = {"v": v, "ipa": cap["ipa"]}
+    if tps:  # the relative-frame 7-vectors the TPS branch embeds (latent_model.py:198-199); their
+        # quaternion half comes from an eigen-solve whose sign depends on the LAPACK build, so
+        # parity on another host injects these exact values
+        out["rel7_f"] = kw["start_frames"].invert().compose(kw["end_frames"]).to_tensor_7()
+        out["rel7_r"] = kw["end_frames"].invert().compose(kw["start_frames"]).to_tensor_7()
     for i, o in enumerate(layer_out):
         out[f"layer{i}"] = o
     if euler:

@@ -119,8 +119,14 @@ def test_gemm_qkv_rope_layouts(lib, dt, layout):
         out = torch.zeros(M, 3, H, 32, device="cuda", dtype=CT[dt])
     else:
         out = torch.zeros(3, B * L, H, T, 32, device="cuda", dtype=CT[dt])
-    d = _desc(dtype=ENUM[dt], a_mode=1, epi=2, M=M, N=3 * C, K=C, A=A.data_ptr(), lda=C, W=W.data_ptr(), ldw=C,
-              bias=bias.data_ptr(), mods=mods.data_ptr(), mod_stride=9 * C, rows_per_mod=T * L, shift_off=0,
+    # the kernel contract: q/k head rows pair-interleaved (row 2i = dim i, 2i+1 = dim i + D/2)
+    idx = torch.arange(D)
+    within = torch.where(idx % 2 == 0, idx // 2, idx // 2 + D // 2)
+    perm = (torch.arange(H)[:, None] * D + within[None]).reshape(-1).cuda()
+    full = torch.cat([perm, perm + C, torch.arange(2 * C, 3 * C, device="cuda")])
+    Wi, bi = W[full].contiguous(), bias[full].contiguous()
+    d = _desc(dtype=ENUM[dt], a_mode=1, epi=2, M=M, N=3 * C, K=C, A=A.data_ptr(), lda=C, W=Wi.data_ptr(), ldw=C,
+              bias=bi.data_ptr(), mods=mods.data_ptr(), mod_stride=9 * C, rows_per_mod=T * L, shift_off=0,
               scale_off=C, ln_eps=1e-6, qkv_layout=layout, qkv_out=out.data_ptr(), H=H, D=D, T=T, L=L, qscale=qs,
               rope=table.data_ptr(), rope_rows=S)
     _lib.check(lib.mdg_gemm(ctypes.byref(d), _s()), "mdg_gemm")
@@ -132,6 +138,7 @@ def test_gemm_qkv_rope_layouts(lib, dt, layout):
     q = _rope_ref(p[..., 0, :, :] * qs, posb, inv.cuda())
     k = _rope_ref(p[..., 1, :, :], posb, inv.cuda())
     v = p[..., 2, :, :]
+    q, k = q[..., within.cuda()], k[..., within.cuda()]           # stored interleaved
     ref = torch.stack([q, k, v], 3)                               # [B,T,L,3,H,D]
     if layout == 0:
         got = out.float().reshape(B, T, L, 3, H, 32)
@@ -213,7 +220,7 @@ def test_attn_spatial(lib, dt):
         torch.testing.assert_close(got[:, :, h], ref, rtol=rtol * 2, atol=atol * 2)
 
 
-def test_embed_and_final_euler(lib):
+def test_embed(lib):
     from mdgen_finetune_amd import _lib
 
     B, T, L, C, K = 2, 10, 4, 384, 21
@@ -227,22 +234,39 @@ def test_embed_and_final_euler(lib):
     idx = torch.randint(0, 2, (N,), device="cuda", generator=g)
     ipa = torch.randn(B * L, C, device="cuda", generator=g)
     out = torch.empty(N, C, device="cuda")
-    _lib.check(lib.mdg_embed(N, T, L, C, K, x.data_ptr(), W.data_ptr(), bias.data_ptr(), None, pos.data_ptr(),
+    Wt = W.t().contiguous()
+    _lib.check(lib.mdg_embed(N, T, L, C, K, x.data_ptr(), Wt.data_ptr(), bias.data_ptr(), None, pos.data_ptr(),
                              emb.data_ptr(), idx.data_ptr(), ipa.data_ptr(), out.data_ptr(), _s()), "embed")
     n = torch.arange(N, device="cuda")
     ref = x @ W.T + bias + pos[n % L] + emb[idx] + ipa[(n // (T * L)) * L + n % L]
     torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-4)
 
-    Wf = torch.randn(K, C, device="cuda", generator=g) / 20
-    bf = torch.randn(K, device="cuda", generator=g)
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+def test_final_euler_gemm(lib, dt):
+    from mdgen_finetune_amd import _lib
+
+    B, T, L, C, K = 2, 10, 4, 384, 21
+    N = B * T * L
+    g = torch.Generator(device="cuda").manual_seed(4)
+    h = torch.randn(N, C, device="cuda", generator=g) * 2
+    Wf = torch.zeros(32, C, device="cuda")
+    Wf[:K] = torch.randn(K, C, device="cuda", generator=g) / 20
+    bf = torch.zeros(32, device="cuda")
+    bf[:K] = torch.randn(K, device="cuda", generator=g)
     mods = torch.randn(B, 2 * C, device="cuda", generator=g) * 0.3
     xin = torch.randn(N, K, device="cuda", generator=g)
     xo = torch.empty_like(xin)
     vo = torch.empty_like(xin)
-    _lib.check(lib.mdg_final_euler(N, T * L, C, K, Wf.data_ptr(), bf.data_ptr(), mods.data_ptr(), out.data_ptr(),
-                                   xin.data_ptr(), 0.25, xo.data_ptr(), vo.data_ptr(), _s()), "final_euler")
+    Wc = Wf.to(CT[dt]).contiguous()
+    _lib.check(lib.mdg_final_euler(ENUM[dt], N, T * L, C, K, Wc.data_ptr(), bf.data_ptr(), mods.data_ptr(),
+                                   h.data_ptr(), xin.data_ptr(), 0.25, xo.data_ptr(), vo.data_ptr(), _s()),
+               "final_euler")
+    n = torch.arange(N, device="cuda")
     b = n // (T * L)
-    y = torch.nn.functional.layer_norm(out, (C,), eps=1e-6) * (1 + mods[b, C:]) + mods[b, :C]
-    vref = y @ Wf.T + bf
-    torch.testing.assert_close(vo, vref, rtol=1e-5, atol=1e-4)
+    y = torch.nn.functional.layer_norm(h, (C,), eps=1e-6) * (1 + mods[b, C:]) + mods[b, :C]
+    vref = y.to(CT[dt]).float() @ Wc.float()[:K].T + bf[:K]
+    rtol, atol = _tol(dt)
+    torch.testing.assert_close(vo, vref, rtol=rtol, atol=atol * 10)
     torch.testing.assert_close(xo, xin + 0.25 * vo, rtol=0, atol=1e-6)

@@ -1,0 +1,61 @@
+"""Standalone GEMM timing on the GPU: libmdgen_hip mdg_gemm vs torch (hipBLASLt) on the
+block's shapes.  Usage: python tools/gemm_bench.py"""
+import ctypes
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from mdgen_finetune_amd import _lib  # noqa: E402
+
+lib = _lib.load()
+
+
+def tm(fn, it=20):
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(it):
+        fn()
+    e1.record()
+    e1.synchronize()
+    return e0.elapsed_time(e1) / it * 1e3  # us
+
+
+def run(M, N, K, a_mode, epi, dt="bf16"):
+    ct = torch.bfloat16 if dt == "bf16" else torch.float32
+    A = torch.randn(M, K, device="cuda").to(ct if a_mode == 0 else torch.float32)
+    W = torch.randn(N, K, device="cuda").to(ct)
+    bias = torch.randn(N, device="cuda")
+    out = torch.empty(M, N, device="cuda", dtype=ct)
+    resid = torch.zeros(M, N, device="cuda")
+    mods = torch.randn(8, 9 * K, device="cuda") * 0.1
+    d = _lib.MdgGemmDesc()
+    d.dtype = 1 if dt == "bf16" else 0
+    d.a_mode, d.epi, d.M, d.N, d.K = a_mode, epi, M, N, K
+    d.A, d.lda, d.W, d.ldw, d.bias = A.data_ptr(), K, W.data_ptr(), K, bias.data_ptr()
+    d.mods, d.mod_stride, d.rows_per_mod, d.shift_off, d.scale_off, d.ln_eps = mods.data_ptr(), 9 * K, 4000, 0, K, 1e-6
+    d.out, d.ldo, d.resid, d.ldr = out.data_ptr(), N, resid.data_ptr(), N
+    s = torch.cuda.current_stream().cuda_stream
+
+    def f():
+        _lib.check(lib.mdg_gemm(ctypes.byref(d), s), "gemm")
+
+    us = tm(f)
+    Ab = A.to(ct)
+    ref = tm(lambda: torch.matmul(Ab, W.t()))
+    fl = 2.0 * M * N * K
+    print(f"M={M:6d} N={N:5d} K={K:5d} amode={a_mode} epi={epi} {dt}: mdg {us:8.1f} us ({fl/us/1e6:7.1f} TF/s)   "
+          f"torch.matmul {ref:8.1f} us ({fl/ref/1e6:7.1f} TF/s)", flush=True)
+
+
+if __name__ == "__main__":
+    for B in (8, 1):
+        M = B * 4000
+        run(M, 384, 384, 0, 1)      # out-proj gate-res
+        run(M, 384, 1536, 0, 1)     # fc2
+        run(M, 1152, 384, 1, 0)     # qkv-like LNMOD store
+        run(M, 1536, 384, 1, 0)     # fc1-like
+        run(M, 1536, 384, 0, 0)     # plain store, same shape
