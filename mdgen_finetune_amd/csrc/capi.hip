@@ -12,8 +12,9 @@
 
 namespace mdg {
 struct GemmPlan {
-  int bm, bn;
+  int cfg;
   size_t smem;
+  int bm, bn;
 };
 GemmPlan gemm_plan(const mdg_gemm_desc& p);
 hipError_t gemm_launch(const mdg_gemm_desc& p, const GemmPlan& g, hipStream_t s);
@@ -166,7 +167,7 @@ int mdg_gemm(const mdg_gemm_desc* g, void* stream) {
       return fail(MDG_E_ARG, "gemm: epi %d", g->epi);
   }
   const mdg::GemmPlan plan = mdg::gemm_plan(*g);
-  if (!plan.bn) return fail(MDG_E_SHAPE, "gemm: no tile fits N=%d", g->N);
+  if (plan.cfg < 0) return fail(MDG_E_SHAPE, "gemm: no tile fits N=%d", g->N);
   if (plan.smem > 160 * 1024)
     return fail(MDG_E_SHAPE, "gemm: K=%d needs %zu B of LDS (> 160 KiB)", g->K, plan.smem);
   return hip_check(mdg::gemm_launch(*g, plan, (hipStream_t)stream), "gemm launch");
