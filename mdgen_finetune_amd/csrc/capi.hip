@@ -26,6 +26,9 @@ hipError_t embed_launch(int N, int T, int L, int C, int K, const float* x, const
                         const float* bias, const float* base, const float* pos, const float* emb,
                         const int64_t* idx, const float* ipa, float* out, hipStream_t s);
 hipError_t mask_bias_launch(int B, int T, int L, const float* mask, float* kbias, hipStream_t s);
+hipError_t ln_mod_launch(int dtype, int M, int C, const float* h, const float* mods, int mod_stride,
+                         int rows_per_mod, int shift_off, int scale_off, float eps, void* xn,
+                         hipStream_t s);
 hipError_t set_vpad_launch(int dtype, void* v, size_t rows, int D, hipStream_t s);
 }  // namespace mdg
 
@@ -53,7 +56,7 @@ size_t ct_size(int dtype) { return dtype == MDG_BF16 ? 2 : 4; }
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 struct WsLayout {
-  size_t qkv_s, qkv_t, o, hid, kbias, total;
+  size_t qkv_s, qkv_t, o, hid, xn, kbias, total;
 };
 
 WsLayout ws_layout(const mdg_dims& d) {
@@ -65,6 +68,7 @@ WsLayout ws_layout(const mdg_dims& d) {
   w.qkv_t = off; off += align256(3ull * d.B * d.L * d.H * d.T * MDG_DP * cs);
   w.o = off;     off += align256(N * d.C * cs);
   w.hid = off;   off += align256(N * d.F * cs);
+  w.xn = off;    off += align256(N * d.C * cs);
   w.kbias = off; off += align256((size_t)d.B * d.L * d.T * sizeof(float));
   w.total = off;
   return w;
@@ -246,34 +250,43 @@ int mdg_layer_fwd(const mdg_dims* d, const mdg_layer_weights* w, const float* ro
   void* hid = wsb + lay.hid;
   const float* kbias = (const float*)(wsb + lay.kbias);
 
+  void* xn = wsb + lay.xn;
+  hipStream_t s = (hipStream_t)stream;
+  const int TL = T * L, ms = 9 * C;
+  // LN + adaLN modulate into the CT activation buffer (latent_model.py:467/475/489)
+  auto ln = [&](int shift_off, int scale_off) -> int {
+    return hip_check(mdg::ln_mod_launch(d->dtype, N, C, h, mods, ms, TL, shift_off, scale_off, 1e-6f, xn, s),
+                     "ln_mod");
+  };
+
   mdg_gemm_desc g;
   memset(&g, 0, sizeof(g));
   g.dtype = d->dtype;
   g.M = N;
+  g.a_mode = MDG_A_PLAIN;
   g.mods = mods;
-  g.mod_stride = 9 * C;
-  g.rows_per_mod = T * L;
-  g.ln_eps = 1e-6f;
+  g.mod_stride = ms;
+  g.rows_per_mod = TL;
   g.H = H; g.D = D; g.T = T; g.L = L;
 
   // ---- spatial attention: x += gate_l * mha_l(mod(LN x))      (latent_model.py:466-472)
+  if (int e = ln(0, C)) return e;
   mdg_gemm_desc q = g;
-  q.a_mode = MDG_A_LNMOD; q.epi = MDG_EPI_QKV;
-  q.N = 3 * C; q.K = C; q.A = h; q.lda = C; q.W = w->wqkv[0]; q.ldw = C; q.bias = w->bqkv[0];
-  q.shift_off = 0; q.scale_off = C;
+  q.epi = MDG_EPI_QKV;
+  q.N = 3 * C; q.K = C; q.A = xn; q.lda = C; q.W = w->wqkv[0]; q.ldw = C; q.bias = w->bqkv[0];
   q.qkv_layout = MDG_QKV_SPATIAL; q.qkv_out = qkv_s; q.qscale = qs;
   q.rope = rope_l; q.rope_rows = L + 1;
   if (int e = mdg_gemm(&q, stream)) return e;
   if (int e = mdg_attn_spatial(d->dtype, B * T, L, H, D, qkv_s, w->kvb[0], mask, o, stream)) return e;
   mdg_gemm_desc r = g;
-  r.a_mode = MDG_A_PLAIN; r.epi = MDG_EPI_GATE_RES;
+  r.epi = MDG_EPI_GATE_RES;
   r.N = C; r.K = C; r.A = o; r.lda = C; r.W = w->wo[0]; r.ldw = C; r.bias = w->bo[0];
   r.resid = h; r.ldr = C; r.gate = mods; r.gate_off = 2 * C;
   if (int e = mdg_gemm(&r, stream)) return e;
 
   // ---- temporal attention: x += gate_t * mha_t(mod(LN x))     (latent_model.py:474-486)
+  if (int e = ln(3 * C, 4 * C)) return e;
   q.W = w->wqkv[1]; q.bias = w->bqkv[1];
-  q.shift_off = 3 * C; q.scale_off = 4 * C;
   q.qkv_layout = MDG_QKV_TEMPORAL; q.qkv_out = qkv_t; q.qscale = qs * 1.4426950408889634f;
   q.rope = rope_t; q.rope_rows = T + 1;
   if (int e = mdg_gemm(&q, stream)) return e;
@@ -282,13 +295,14 @@ int mdg_layer_fwd(const mdg_dims* d, const mdg_layer_weights* w, const float* ro
   if (int e = mdg_gemm(&r, stream)) return e;
 
   // ---- MLP: x += gate_m * fc2(gelu(fc1(mod(LN x))))           (latent_model.py:488-491)
+  if (int e = ln(6 * C, 7 * C)) return e;
   mdg_gemm_desc f1 = g;
-  f1.a_mode = MDG_A_LNMOD; f1.epi = MDG_EPI_STORE; f1.act = MDG_ACT_GELU;
-  f1.N = F; f1.K = C; f1.A = h; f1.lda = C; f1.W = w->w1; f1.ldw = C; f1.bias = w->b1;
-  f1.shift_off = 6 * C; f1.scale_off = 7 * C; f1.out = hid; f1.ldo = F;
+  f1.epi = MDG_EPI_STORE; f1.act = MDG_ACT_GELU;
+  f1.N = F; f1.K = C; f1.A = xn; f1.lda = C; f1.W = w->w1; f1.ldw = C; f1.bias = w->b1;
+  f1.out = hid; f1.ldo = F;
   if (int e = mdg_gemm(&f1, stream)) return e;
   mdg_gemm_desc f2 = g;
-  f2.a_mode = MDG_A_PLAIN; f2.epi = MDG_EPI_GATE_RES;
+  f2.epi = MDG_EPI_GATE_RES;
   f2.N = C; f2.K = F; f2.A = hid; f2.lda = F; f2.W = w->w2; f2.ldw = F; f2.bias = w->b2;
   f2.resid = h; f2.ldr = C; f2.gate = mods; f2.gate_off = 8 * C;
   return mdg_gemm(&f2, stream);
@@ -310,8 +324,22 @@ int mdg_denoise_step(const mdg_model* m, const mdg_step_io* io, const float* mas
     if (int e = mdg_layer_fwd(d, &m->layers[i], m->rope_l, m->rope_t, io->mods + i * mstride, mask,
                               io->h, ws, stream))
       return e;
-  return mdg_final_euler(d->dtype, N, d->T * d->L, d->C, d->latent, m->w_final, m->b_final, io->mods_final,
-                         io->h, io->x_in, io->dt, io->x_out, io->v_out, stream);
+  // FinalLayer: LN + modulate (layers.py:73) into xn, then the EULER-epilogue GEMM
+  const WsLayout lay = ws_layout(*d);
+  void* xn = (char*)ws + lay.xn;
+  if (int e = hip_check(mdg::ln_mod_launch(d->dtype, N, d->C, io->h, io->mods_final, 2 * d->C, d->T * d->L, 0,
+                                           d->C, 1e-6f, xn, (hipStream_t)stream), "ln_mod(final)"))
+    return e;
+  mdg_gemm_desc g;
+  memset(&g, 0, sizeof(g));
+  g.dtype = d->dtype;
+  g.a_mode = MDG_A_PLAIN;
+  g.epi = MDG_EPI_EULER;
+  g.M = N; g.N = (d->latent + 31) / 32 * 32; g.K = d->C;
+  g.A = xn; g.lda = d->C; g.W = m->w_final; g.ldw = d->C; g.bias = m->b_final;
+  g.out = io->x_out; g.ldo = d->latent; g.x_in = io->x_in; g.v_out = io->v_out; g.dt = io->dt;
+  g.n_valid = d->latent;
+  return mdg_gemm(&g, stream);
 }
 
 }  // extern "C"

@@ -106,6 +106,20 @@ __device__ __forceinline__ float gelu_erf(float x) {
   return x * 0.5f * (1.0f + erff(x * 0.70710678118654752440f));
 }
 
+// exact-erf GELU via erfc(a) = t*poly(t)*exp(-a^2), t = 1/(1 + p a)  (Abramowitz & Stegun
+// 7.1.26, |error| <= 1.5e-7 absolute on erf): 1 rcp + 1 exp + 6 FMAs instead of the
+// multi-range ocml erff.  Used where the result is rounded to bf16.
+__device__ __forceinline__ float gelu_fast(float x) {
+  const float a = fabsf(x) * 0.70710678118654752440f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, a, 1.0f));
+  float q = fmaf(1.061405429f, t, -1.453152027f);
+  q = fmaf(q, t, 1.421413741f);
+  q = fmaf(q, t, -0.284496736f);
+  q = fmaf(q, t, 0.254829592f);
+  q *= t * __builtin_amdgcn_exp2f(-a * a * 1.4426950408889634f);  // erfc(|x|/sqrt2)
+  return x >= 0.f ? x * (1.0f - 0.5f * q) : x * (0.5f * q);
+}
+
 __device__ __forceinline__ float silu(float x) { return x / (1.0f + expf(-x)); }
 
 static inline int cdiv(int a, int b) { return (a + b - 1) / b; }

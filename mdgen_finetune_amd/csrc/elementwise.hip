@@ -1,5 +1,5 @@
-// Small kernels around the block stack: token embedding, key-padding bias, workspace pad
-// initialisation.  (FinalLayer + Euler runs as the EULER epilogue of the GEMM, gemm.hip.)
+// Small kernels around the block stack: token embedding, LayerNorm + adaLN modulate,
+// key-padding bias, workspace pad initialisation.  (FinalLayer + Euler runs as the EULER epilogue of the GEMM, gemm.hip.)
 #include "../../include/mdgen_hip.h"
 #include "common.h"
 
@@ -9,7 +9,8 @@ namespace mdg {
 //             + ipa[b*L + l][c]
 // latent_to_emb / cond_to_emb (nn.Linear, K = 21 or 28) + pos_embed + mask_to_emb
 // (latent_model.py:242-250) + the IPA prepend broadcast over frames (latent_model.py:255).
-// K is tiny, so this is a bandwidth kernel: 8 tokens per block share the x rows in LDS.
+// K is tiny, so this is a bandwidth kernel: one thread per (token, 4 channels), float4
+// accesses; the x row is re-read from L1 by the C/4 threads of a token.
 __global__ __launch_bounds__(256) void embed_kernel(int N, int T, int L, int C, int K,
                                                     const float* __restrict__ x,
                                                     const float* __restrict__ Wt,
@@ -20,35 +21,98 @@ __global__ __launch_bounds__(256) void embed_kernel(int N, int T, int L, int C, 
                                                     const int64_t* __restrict__ idx,
                                                     const float* __restrict__ ipa,
                                                     float* __restrict__ out) {
-  constexpr int TOK = 8;
-  __shared__ float xs[TOK][64];
-  const int n0 = blockIdx.x * TOK;
-  for (int i = threadIdx.x; i < TOK * K; i += 256) {
-    const int r = i / K, j = i % K, n = n0 + r;
-    xs[r][j] = (n < N) ? x[(size_t)n * K + j] : 0.f;
-  }
-  __syncthreads();
-  for (int c = threadIdx.x; c < C; c += 256) {
-    float acc[TOK];
-#pragma unroll
-    for (int r = 0; r < TOK; ++r) acc[r] = 0.f;
+  const int C4 = C >> 2;
+  const long total = (long)N * C4;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const int n = (int)(i / C4), c = (int)(i - (long)n * C4) * 4;
+    const float* xr = x + (size_t)n * K;
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int j = 0; j < K; ++j) {
-      const float w = Wt[(size_t)j * C + c];  // coalesced across the block's channels
-#pragma unroll
-      for (int r = 0; r < TOK; ++r) acc[r] += xs[r][j] * w;
+      const float xv = xr[j];
+      const float4 w = *reinterpret_cast<const float4*>(Wt + (size_t)j * C + c);
+      a.x += xv * w.x; a.y += xv * w.y; a.z += xv * w.z; a.w += xv * w.w;
     }
+    const int l = n % L;
+    if (bias) { const float4 t = *reinterpret_cast<const float4*>(bias + c); a.x += t.x; a.y += t.y; a.z += t.z; a.w += t.w; }
+    if (base) { const float4 t = *reinterpret_cast<const float4*>(base + (size_t)n * C + c); a.x += t.x; a.y += t.y; a.z += t.z; a.w += t.w; }
+    if (pos) { const float4 t = *reinterpret_cast<const float4*>(pos + (size_t)l * C + c); a.x += t.x; a.y += t.y; a.z += t.z; a.w += t.w; }
+    if (emb) { const float4 t = *reinterpret_cast<const float4*>(emb + (size_t)idx[n] * C + c); a.x += t.x; a.y += t.y; a.z += t.z; a.w += t.w; }
+    if (ipa) { const float4 t = *reinterpret_cast<const float4*>(ipa + ((size_t)(n / (T * L)) * L + l) * C + c); a.x += t.x; a.y += t.y; a.z += t.z; a.w += t.w; }
+    *reinterpret_cast<float4*>(out + (size_t)n * C + c) = a;
+  }
+}
+
+// xn[m][k] = CT( LN(h[m])[k] * (1 + scale[b][k]) + shift[b][k] ),  b = m / rows_per_mod
+// The no-affine LayerNorm (eps 1e-6) + adaLN modulate in front of every projection of the
+// block (latent_model.py:467/475/489, FinalLayer layers.py:73, modulate layers.py:14-15).
+// One wave per row: each lane holds W consecutive channels of every 64W-channel chunk
+// (W = 2 when C % 128 == 0: 256-B bf16 stores per wave instruction), two wave reductions
+// (mean, then the centred sum of squares, as torch's two-pass LayerNorm).
+template <typename CT, int W>
+__global__ __launch_bounds__(256) void ln_mod_kernel(int M, int C, const float* __restrict__ h,
+                                                     const float* __restrict__ mods, int mod_stride,
+                                                     int rows_per_mod, int shift_off, int scale_off,
+                                                     float eps, CT* __restrict__ xn) {
+  constexpr int E = 8 / W;  // C <= 512
+  const int lane = threadIdx.x & 63;
+  const int m = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (m >= M) return;
+  const int nE = C / (64 * W);
+  const float* hr = h + (size_t)m * C;
+  const float* mr = mods + (size_t)(m / rows_per_mod) * mod_stride;
+  float v[E][W], sc[E][W], sh[E][W];
 #pragma unroll
-    for (int r = 0; r < TOK; ++r) {
-      const int n = n0 + r;
-      if (n >= N) break;
-      float v = acc[r];
-      if (bias) v += bias[c];
-      if (base) v += base[(size_t)n * C + c];
-      const int l = n % L;
-      if (pos) v += pos[(size_t)l * C + c];
-      if (emb) v += emb[(size_t)idx[n] * C + c];
-      if (ipa) v += ipa[((size_t)(n / (T * L)) * L + l) * C + c];
-      out[(size_t)n * C + c] = v;
+  for (int e = 0; e < E; ++e) {
+    const int k = W * lane + 64 * W * e;
+    if (e < nE) {
+      if constexpr (W == 2) {
+        const float2 a = *reinterpret_cast<const float2*>(hr + k);
+        const float2 b = *reinterpret_cast<const float2*>(mr + scale_off + k);
+        const float2 c = *reinterpret_cast<const float2*>(mr + shift_off + k);
+        v[e][0] = a.x; v[e][1] = a.y; sc[e][0] = b.x; sc[e][1] = b.y; sh[e][0] = c.x; sh[e][1] = c.y;
+      } else {
+        v[e][0] = hr[k]; sc[e][0] = mr[scale_off + k]; sh[e][0] = mr[shift_off + k];
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < W; ++j) v[e][j] = sc[e][j] = sh[e][j] = 0.f;
+    }
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int e = 0; e < E; ++e)
+#pragma unroll
+    for (int j = 0; j < W; ++j) s += v[e][j];
+  const float mean = wave_sum(s) / (float)C;
+  float ss = 0.f;
+#pragma unroll
+  for (int e = 0; e < E; ++e)
+    if (e < nE)
+#pragma unroll
+      for (int j = 0; j < W; ++j) {
+        const float a = v[e][j] - mean;
+        ss += a * a;
+      }
+  const float rs = 1.0f / sqrtf(wave_sum(ss) / (float)C + eps);
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    if (e < nE) {
+      const int k = W * lane + 64 * W * e;
+      float y[W];
+#pragma unroll
+      for (int j = 0; j < W; ++j) y[j] = (v[e][j] - mean) * rs * (1.0f + sc[e][j]) + sh[e][j];
+      CT* o = xn + (size_t)m * C + k;
+      if constexpr (W == 2 && is_bf16<CT>()) {
+        typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+        bf16x2 pr;
+        pr[0] = (bf16_t)y[0];
+        pr[1] = (bf16_t)y[1];
+        *reinterpret_cast<bf16x2*>(o) = pr;
+      } else if constexpr (W == 2) {
+        *reinterpret_cast<float2*>(o) = make_float2(y[0], y[1]);
+      } else {
+        o[0] = (CT)y[0];
+      }
     }
   }
 }
@@ -73,8 +137,28 @@ __global__ void set_vpad_kernel(CT* v, size_t rows, int D) {
 hipError_t embed_launch(int N, int T, int L, int C, int K, const float* x, const float* Wt,
                         const float* bias, const float* base, const float* pos, const float* emb,
                         const int64_t* idx, const float* ipa, float* out, hipStream_t s) {
-  hipLaunchKernelGGL(embed_kernel, dim3((N + 7) / 8), dim3(256), 0, s, N, T, L, C, K, x, Wt, bias,
+  const long total = (long)N * (C / 4);
+  long grid = (total + 255) / 256;
+  if (grid > 4096) grid = 4096;
+  hipLaunchKernelGGL(embed_kernel, dim3((unsigned)grid), dim3(256), 0, s, N, T, L, C, K, x, Wt, bias,
                      base, pos, emb, idx, ipa, out);
+  return hipGetLastError();
+}
+
+hipError_t ln_mod_launch(int dtype, int M, int C, const float* h, const float* mods, int mod_stride,
+                         int rows_per_mod, int shift_off, int scale_off, float eps, void* xn,
+                         hipStream_t s) {
+  dim3 grid((M + 3) / 4);
+#define MDG_LN(CTT, W)                                                                        \
+  hipLaunchKernelGGL((ln_mod_kernel<CTT, W>), grid, dim3(256), 0, s, M, C, h, mods, mod_stride, \
+                     rows_per_mod, shift_off, scale_off, eps, (CTT*)xn)
+  const bool w2 = (C % 128) == 0;
+  if (dtype == MDG_BF16) {
+    if (w2) MDG_LN(bf16_t, 2); else MDG_LN(bf16_t, 1);
+  } else {
+    if (w2) MDG_LN(float, 2); else MDG_LN(float, 1);
+  }
+#undef MDG_LN
   return hipGetLastError();
 }
 

@@ -35,6 +35,8 @@
 #include "../../include/mdgen_hip.h"
 #include "common.h"
 
+#include <stdlib.h>
+
 namespace mdg {
 
 constexpr int kThreads = 512;
@@ -45,6 +47,77 @@ __device__ __forceinline__ int fdiv(int a, int d, float inv) {
   const int r = a - q * d;
   q += (r >= d) - (r < 0);
   return q;
+}
+
+// Epilogue of 4 consecutive output columns n..n+3 of row m (v = the fp32 accumulators).
+template <typename CT, int EPI>
+__device__ __forceinline__ void epi4(const mdg_gemm_desc& p, int m, int n, float4 v, float invD, float invL,
+                                     float invT) {
+  const int M = p.M;
+  if (p.bias) {
+    const float4 bb = *reinterpret_cast<const float4*>(p.bias + n);
+    v.x += bb.x; v.y += bb.y; v.z += bb.z; v.w += bb.w;
+  }
+  if constexpr (EPI == MDG_EPI_STORE) {
+    if (p.act == MDG_ACT_GELU) {
+      v.x = gelu_erf(v.x); v.y = gelu_erf(v.y); v.z = gelu_erf(v.z); v.w = gelu_erf(v.w);
+    } else if (p.act == MDG_ACT_SILU) {
+      v.x = silu(v.x); v.y = silu(v.y); v.z = silu(v.z); v.w = silu(v.w);
+    }
+    if (p.out_f32) *reinterpret_cast<float4*>(reinterpret_cast<float*>(p.out) + (size_t)m * p.ldo + n) = v;
+    else st4<CT>(reinterpret_cast<CT*>(p.out) + (size_t)m * p.ldo + n, v.x, v.y, v.z, v.w);
+  } else if constexpr (EPI == MDG_EPI_GATE_RES) {
+    float4* R = reinterpret_cast<float4*>(p.resid + (size_t)m * p.ldr + n);
+    float4 hv = *R;
+    if (p.gate) {
+      const float4 g = *reinterpret_cast<const float4*>(
+          p.gate + (size_t)(m / p.rows_per_mod) * p.mod_stride + p.gate_off + n);
+      hv.x += g.x * v.x; hv.y += g.y * v.y; hv.z += g.z * v.z; hv.w += g.w * v.w;
+    } else {
+      hv.x += v.x; hv.y += v.y; hv.z += v.z; hv.w += v.w;
+    }
+    *R = hv;
+  } else if constexpr (EPI == MDG_EPI_QKV) {
+    // 4 columns = 2 rotate-half pairs of one head (D % 4 == 0, pair-interleaved rows)
+    const int Cm = p.N / 3, D = p.D;
+    const int which = (n >= Cm) + (n >= 2 * Cm), w = n - which * Cm;
+    const int head = fdiv(w, D, invD), cp = w - head * D;
+    if (which == 0) {
+      v.x *= p.qscale; v.y *= p.qscale; v.z *= p.qscale; v.w *= p.qscale;
+    }
+    const int ml = fdiv(m, p.L, invL), l = m - ml * p.L;  // m = ml*L + l
+    const int mt = fdiv(ml, p.T, invT), t = ml - mt * p.T;  // ml = b*T + t
+    if (p.rope && which < 2) {
+      const int half = D >> 1, pi = cp >> 1;
+      const int pos = (p.qkv_layout == MDG_QKV_SPATIAL) ? l : t;
+      const float* cs = p.rope + (size_t)pos * half + pi;
+      const float* sn = p.rope + (size_t)p.rope_rows * half + (size_t)pos * half + pi;
+      const float c0 = cs[0], s0 = sn[0], c1 = cs[1], s1 = sn[1];
+      const float x0 = v.x * c0 - v.y * s0, y0 = v.y * c0 + v.x * s0;
+      const float x1 = v.z * c1 - v.w * s1, y1 = v.w * c1 + v.z * s1;
+      v.x = x0; v.y = y0; v.z = x1; v.w = y1;
+    }
+    CT* dst;
+    if (p.qkv_layout == MDG_QKV_SPATIAL) {
+      dst = reinterpret_cast<CT*>(p.qkv_out) + ((size_t)(m * 3 + which) * p.H + head) * MDG_DP + cp;
+    } else {
+      const int BL = (M / (p.T * p.L)) * p.L, seq = mt * p.L + l;
+      dst = reinterpret_cast<CT*>(p.qkv_out) + (size_t)which * BL * p.H * p.T * MDG_DP +
+            ((size_t)(seq * p.H + head) * p.T + t) * MDG_DP + cp;
+    }
+    st4<CT>(dst, v.x, v.y, v.z, v.w);
+  } else {  // EULER
+    const size_t rowoff = (size_t)m * p.ldo;
+    const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      if (n + e < p.n_valid) {
+        if (p.v_out) p.v_out[rowoff + n + e] = vv[e];
+        float* xo = reinterpret_cast<float*>(p.out);
+        if (xo) xo[rowoff + n + e] = __fadd_rn(p.x_in[rowoff + n + e], __fmul_rn(p.dt, vv[e]));
+      }
+    }
+  }
 }
 
 template <typename CT, int BM, int BN, int WM, int AMODE, int EPI>
@@ -298,72 +371,8 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(const mdg_gemm_desc p) {
         const int rb = idx / C4, c = (idx % C4) * 4;
         const int m = m0 + pass * BAND + rb;
         if (m >= M) continue;
-        const int n = n0 + c;
-        float4 v = *reinterpret_cast<const float4*>(stage + rb * LDS_ST + c);
-        if (p.bias) {
-          const float4 bb = *reinterpret_cast<const float4*>(p.bias + n);
-          v.x += bb.x; v.y += bb.y; v.z += bb.z; v.w += bb.w;
-        }
-        if constexpr (EPI == MDG_EPI_STORE) {
-          if (p.act == MDG_ACT_GELU) {
-            v.x = gelu_erf(v.x); v.y = gelu_erf(v.y); v.z = gelu_erf(v.z); v.w = gelu_erf(v.w);
-          } else if (p.act == MDG_ACT_SILU) {
-            v.x = silu(v.x); v.y = silu(v.y); v.z = silu(v.z); v.w = silu(v.w);
-          }
-          if (p.out_f32) *reinterpret_cast<float4*>(reinterpret_cast<float*>(p.out) + (size_t)m * p.ldo + n) = v;
-          else st4<CT>(reinterpret_cast<CT*>(p.out) + (size_t)m * p.ldo + n, v.x, v.y, v.z, v.w);
-        } else if constexpr (EPI == MDG_EPI_GATE_RES) {
-          float4* R = reinterpret_cast<float4*>(p.resid + (size_t)m * p.ldr + n);
-          float4 hv = *R;
-          if (p.gate) {
-            const float4 g = *reinterpret_cast<const float4*>(
-                p.gate + (size_t)(m / p.rows_per_mod) * p.mod_stride + p.gate_off + n);
-            hv.x += g.x * v.x; hv.y += g.y * v.y; hv.z += g.z * v.z; hv.w += g.w * v.w;
-          } else {
-            hv.x += v.x; hv.y += v.y; hv.z += v.z; hv.w += v.w;
-          }
-          *R = hv;
-        } else if constexpr (EPI == MDG_EPI_QKV) {
-          // 4 columns = 2 rotate-half pairs of one head (D % 4 == 0, pair-interleaved rows)
-          const int Cm = p.N / 3, D = p.D;
-          const int which = (n >= Cm) + (n >= 2 * Cm), w = n - which * Cm;
-          const int head = fdiv(w, D, invD), cp = w - head * D;
-          if (which == 0) {
-            v.x *= p.qscale; v.y *= p.qscale; v.z *= p.qscale; v.w *= p.qscale;
-          }
-          const int ml = fdiv(m, p.L, invL), l = m - ml * p.L;  // m = ml*L + l
-          const int mt = fdiv(ml, p.T, invT), t = ml - mt * p.T;  // ml = b*T + t
-          if (p.rope && which < 2) {
-            const int half = D >> 1, pi = cp >> 1;
-            const int pos = (p.qkv_layout == MDG_QKV_SPATIAL) ? l : t;
-            const float* cs = p.rope + (size_t)pos * half + pi;
-            const float* sn = p.rope + (size_t)p.rope_rows * half + (size_t)pos * half + pi;
-            const float c0 = cs[0], s0 = sn[0], c1 = cs[1], s1 = sn[1];
-            const float x0 = v.x * c0 - v.y * s0, y0 = v.y * c0 + v.x * s0;
-            const float x1 = v.z * c1 - v.w * s1, y1 = v.w * c1 + v.z * s1;
-            v.x = x0; v.y = y0; v.z = x1; v.w = y1;
-          }
-          CT* dst;
-          if (p.qkv_layout == MDG_QKV_SPATIAL) {
-            dst = reinterpret_cast<CT*>(p.qkv_out) + ((size_t)(m * 3 + which) * p.H + head) * MDG_DP + cp;
-          } else {
-            const int BL = (M / (p.T * p.L)) * p.L, seq = mt * p.L + l;
-            dst = reinterpret_cast<CT*>(p.qkv_out) + (size_t)which * BL * p.H * p.T * MDG_DP +
-                  ((size_t)(seq * p.H + head) * p.T + t) * MDG_DP + cp;
-          }
-          st4<CT>(dst, v.x, v.y, v.z, v.w);
-        } else {  // EULER
-          const size_t rowoff = (size_t)m * p.ldo;
-          const float vv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            if (n + e < p.n_valid) {
-              if (p.v_out) p.v_out[rowoff + n + e] = vv[e];
-              float* xo = reinterpret_cast<float*>(p.out);
-              if (xo) xo[rowoff + n + e] = __fadd_rn(p.x_in[rowoff + n + e], __fmul_rn(p.dt, vv[e]));
-            }
-          }
-        }
+        const float4 v = *reinterpret_cast<const float4*>(stage + rb * LDS_ST + c);
+        epi4<CT, EPI>(p, m, n0 + c, v, invD, invL, invT);
       }
       __syncthreads();
     }
@@ -374,6 +383,381 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(const mdg_gemm_desc p) {
   }
 #undef MDG_LOAD_TILES
 #undef MDG_STORE_TILES
+}
+
+// ---------------------------------------------------------------------------------------
+// bf16 streamed-A GEMM for the block's big projections (qkv, out_proj, fc1, fc2 at
+// M = B*T*L rows): 128x128 block tile, 4 waves as 2x2 with 64x64 wave tiles (4x4
+// accumulators of v_mfma_f32_16x16x32_bf16, 8 fragment reads per 16 MFMAs), K-step 64.
+//   staging : global_load_lds (16 B/lane, no VGPR round trip) into two LDS stages; the
+//             image is lane-linear per wave instruction (8 rows x 128 B), so the
+//             ds_read_b128 bank swizzle (16-B chunk c of row r stored at c ^ ((r>>1)&7))
+//             is applied to the per-lane GLOBAL source address and undone on the read.
+//             With 16 fragment rows of one lane group on 8 row pairs the read is
+//             conflict-free for all four ds_read_b128 lane groups.
+//   schedule: one barrier per K-step — wait for stage k, barrier, issue stage k+1's
+//             loads, MFMAs on stage k; two blocks per CU hide each other's barriers.
+//   order   : XCD-aware bijective remap of the 1-D grid so the N tiles of one M tile run on
+//             the same XCD (its L2 serves the A panel re-reads; W stays L2-resident).
+//   epilogue: accumulators -> fp32 LDS image of the whole tile -> epi4 on 4-column chunks
+//             with full-row coalesced accesses.
+constexpr int kB4Threads = 256;
+constexpr int kB4Tile = 128;
+
+__host__ __device__ constexpr size_t b4_smem_bytes() {
+  return (2 * 2 * kB4Tile * 64 * 2) > (kB4Tile * (kB4Tile + 4) * 4) ? (2 * 2 * kB4Tile * 64 * 2)
+                                                                     : (kB4Tile * (kB4Tile + 4) * 4);
+}
+
+// Epilogue of one BM x 128 output tile staged in LDS as fp32 [BM][132] (NT threads).
+template <int EPI, int NT, int BM>
+__device__ __forceinline__ void epi_tile(const mdg_gemm_desc& p, const float* __restrict__ stage, int m0, int n0,
+                                         int tid) {
+  constexpr int LDS_ST = 128 + 4;
+  const int M = p.M;
+  // Thread -> (4-column chunk c, rows r0 + RS*u): the chunk is fixed per thread, so every
+  // per-column operand (bias, head/which/pair of the QKV scatter) is loaded once, and the
+  // per-row global operands (residual, gate, RoPE table) of 8 rows are gathered before any
+  // of them is consumed — no load -> store -> load latency chain.
+  constexpr int U = 8;
+  const int c = (tid & 31) * 4, n = n0 + c, r0 = tid >> 5;
+  constexpr int RS = NT / 32, RPT = BM / RS;  // row stride, rows per thread
+  float4 bb = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (p.bias) bb = *reinterpret_cast<const float4*>(p.bias + n);
+  if constexpr (EPI == MDG_EPI_STORE) {
+#pragma unroll
+    for (int u0 = 0; u0 < RPT; u0 += U) {
+      float4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        v[u] = *reinterpret_cast<const float4*>(stage + (r0 + RS * (u0 + u)) * LDS_ST + c);
+        v[u].x += bb.x; v[u].y += bb.y; v[u].z += bb.z; v[u].w += bb.w;
+        if (p.act == MDG_ACT_GELU) {
+          v[u].x = gelu_fast(v[u].x); v[u].y = gelu_fast(v[u].y); v[u].z = gelu_fast(v[u].z); v[u].w = gelu_fast(v[u].w);
+        } else if (p.act == MDG_ACT_SILU) {
+          v[u].x = silu(v[u].x); v[u].y = silu(v[u].y); v[u].z = silu(v[u].z); v[u].w = silu(v[u].w);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int m = m0 + r0 + RS * (u0 + u);
+        if (m >= M) break;
+        if (p.out_f32) *reinterpret_cast<float4*>(reinterpret_cast<float*>(p.out) + (size_t)m * p.ldo + n) = v[u];
+        else st4<bf16_t>(reinterpret_cast<bf16_t*>(p.out) + (size_t)m * p.ldo + n, v[u].x, v[u].y, v[u].z, v[u].w);
+      }
+    }
+  } else if constexpr (EPI == MDG_EPI_GATE_RES) {
+    const float inv_rpm = 1.0f / (float)p.rows_per_mod;
+#pragma unroll
+    for (int u0 = 0; u0 < RPT; u0 += U) {
+      float4 hv[U], g[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int m = min(m0 + r0 + RS * (u0 + u), M - 1);
+        hv[u] = *reinterpret_cast<const float4*>(p.resid + (size_t)m * p.ldr + n);
+        g[u] = make_float4(1.f, 1.f, 1.f, 1.f);
+        if (p.gate)
+          g[u] = *reinterpret_cast<const float4*>(p.gate + (size_t)fdiv(m, p.rows_per_mod, inv_rpm) * p.mod_stride +
+                                                  p.gate_off + n);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int m = m0 + r0 + RS * (u0 + u);
+        if (m >= M) break;
+        float4 v = *reinterpret_cast<const float4*>(stage + (r0 + RS * (u0 + u)) * LDS_ST + c);
+        v.x += bb.x; v.y += bb.y; v.z += bb.z; v.w += bb.w;
+        float4 h = hv[u];
+        if (p.gate) {
+          h.x += g[u].x * v.x; h.y += g[u].y * v.y; h.z += g[u].z * v.z; h.w += g[u].w * v.w;
+        } else {
+          h.x += v.x; h.y += v.y; h.z += v.z; h.w += v.w;
+        }
+        *reinterpret_cast<float4*>(p.resid + (size_t)m * p.ldr + n) = h;
+      }
+    }
+  } else if constexpr (EPI == MDG_EPI_QKV) {
+    const int Cm = p.N / 3, D = p.D, half = D >> 1;
+    const int which = (n >= Cm) + (n >= 2 * Cm), w = n - which * Cm;
+    const int head = w / D, cp = w - head * D, pi = cp >> 1;
+    const float sc = (which == 0) ? p.qscale : 1.0f;
+    const bool rope = p.rope && which < 2, spatial = p.qkv_layout == MDG_QKV_SPATIAL;
+    const float invL = 1.0f / (float)p.L, invT = 1.0f / (float)p.T;
+    const int BL = (M / (p.T * p.L)) * p.L;
+    bf16_t* qo = reinterpret_cast<bf16_t*>(p.qkv_out);
+    const size_t colS = (size_t)(which * p.H + head) * MDG_DP + cp;          // spatial: + m*3*H*DP
+    const size_t colT = (size_t)which * BL * p.H * p.T * MDG_DP + (size_t)head * p.T * MDG_DP + cp;
+#pragma unroll
+    for (int u0 = 0; u0 < RPT; u0 += U) {
+      float2 cs[U], sn[U];
+      int pos[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int m = min(m0 + r0 + RS * (u0 + u), M - 1);
+        const int ml = fdiv(m, p.L, invL), l = m - ml * p.L;
+        const int t = ml - fdiv(ml, p.T, invT) * p.T;
+        pos[u] = spatial ? l : t;
+        cs[u] = sn[u] = make_float2(0.f, 0.f);
+        if (rope) {
+          cs[u] = *reinterpret_cast<const float2*>(p.rope + (size_t)pos[u] * half + pi);
+          sn[u] = *reinterpret_cast<const float2*>(p.rope + (size_t)(p.rope_rows + pos[u]) * half + pi);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int m = m0 + r0 + RS * (u0 + u);
+        if (m >= M) break;
+        float4 v = *reinterpret_cast<const float4*>(stage + (r0 + RS * (u0 + u)) * LDS_ST + c);
+        v.x = (v.x + bb.x) * sc; v.y = (v.y + bb.y) * sc; v.z = (v.z + bb.z) * sc; v.w = (v.w + bb.w) * sc;
+        if (rope) {
+          const float x0 = v.x * cs[u].x - v.y * sn[u].x, y0 = v.y * cs[u].x + v.x * sn[u].x;
+          const float x1 = v.z * cs[u].y - v.w * sn[u].y, y1 = v.w * cs[u].y + v.z * sn[u].y;
+          v.x = x0; v.y = y0; v.z = x1; v.w = y1;
+        }
+        size_t off;
+        if (spatial) {
+          off = (size_t)m * 3 * p.H * MDG_DP + colS;
+        } else {
+          const int ml = fdiv(m, p.L, invL), l = m - ml * p.L;
+          const int b = fdiv(ml, p.T, invT), t = ml - b * p.T;
+          off = colT + ((size_t)(b * p.L + l) * p.H * p.T + t) * MDG_DP;
+        }
+        st4<bf16_t>(qo + off, v.x, v.y, v.z, v.w);
+      }
+    }
+  } else {
+    const float invD = 1.0f / (float)(p.D > 0 ? p.D : 1);
+    const float invL = 1.0f / (float)(p.L > 0 ? p.L : 1);
+    const float invT = 1.0f / (float)(p.T > 0 ? p.T : 1);
+    for (int u = 0; u < RPT; ++u) {
+      const int m = m0 + r0 + RS * u;
+      if (m >= M) break;
+      float4 v = *reinterpret_cast<const float4*>(stage + (r0 + RS * u) * LDS_ST + c);
+      epi4<bf16_t, EPI>(p, m, n, v, invD, invL, invT);
+    }
+  }
+}
+
+template <int EPI>
+__global__ __launch_bounds__(kB4Threads) void gemm_bf16_b4_kernel(const mdg_gemm_desc p) {
+  constexpr int BM = kB4Tile, BN = kB4Tile, BK = 64, TILE = BM * BK, LDS_ST = BN + 4;
+  typedef __attribute__((address_space(3))) void* lds_ptr_t;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  bf16_t* lds = reinterpret_cast<bf16_t*>(smem);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int M = p.M, K = p.K;
+  const int n_tiles = p.N / BN, m_tiles = (M + BM - 1) / BM, nwg = n_tiles * m_tiles;
+  const int xcd = blockIdx.x & 7, loc = blockIdx.x >> 3, q = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + loc;
+  const int mt = wg / n_tiles, nt = wg - mt * n_tiles;
+  const int m0 = mt * BM, n0 = nt * BN;
+
+  // per-lane source rows of this wave's 4 A and 4 B load instructions (rows 32*wave + 8*i + lane/8)
+  const bf16_t* A = reinterpret_cast<const bf16_t*>(p.A);
+  const bf16_t* W = reinterpret_cast<const bf16_t*>(p.W);
+  const int lrow = 32 * wave + (lane >> 3);
+  const bf16_t* asrc[4];
+  const bf16_t* bsrc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = lrow + 8 * i;
+    const int ch = ((lane & 7) ^ ((row >> 1) & 7)) * 8;
+    asrc[i] = A + (size_t)min(m0 + row, M - 1) * p.lda + ch;
+    bsrc[i] = W + (size_t)(n0 + row) * p.ldw + ch;
+  }
+
+#define MDG_B4_LOAD(stage_, k0_)                                                                   \
+  {                                                                                                \
+    bf16_t* sa = lds + (stage_) * 2 * TILE + (32 * wave) * BK;                                     \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                                \
+      __builtin_amdgcn_global_load_lds((const void*)(asrc[i] + (k0_)), (lds_ptr_t)(sa + 8 * i * BK), 16, 0, 0); \
+      __builtin_amdgcn_global_load_lds((const void*)(bsrc[i] + (k0_)), (lds_ptr_t)(sa + TILE + 8 * i * BK), 16, 0, 0); \
+    }                                                                                              \
+  }
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  MDG_B4_LOAD(0, 0);
+  const int nk = K / BK;
+  const int swz = (lr >> 1) & 7;  // ((row >> 1) & 7) of every fragment row this lane reads
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (kt + 1 < nk) MDG_B4_LOAD(cur ^ 1, (kt + 1) * BK);
+    const bf16_t* As = lds + cur * 2 * TILE;
+    const bf16_t* Bs = As + TILE;
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 32) {
+      const int ch = (((kk >> 3) + lg) ^ swz) * 8;
+      bf16x8 a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = *reinterpret_cast<const bf16x8*>(As + (wm * 64 + i * 16 + lr) * BK + ch);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = *reinterpret_cast<const bf16x8*>(Bs + (wn * 64 + j * 16 + lr) * BK + ch);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+  }
+#undef MDG_B4_LOAD
+
+  // ------------------------------------------------------------------ epilogue
+  __syncthreads();  // every wave is done reading the last stage
+  float* stage = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        stage[(wm * 64 + i * 16 + lg * 4 + r) * LDS_ST + wn * 64 + j * 16 + lr] = acc[i][j][r];
+  __syncthreads();
+  epi_tile<EPI, kB4Threads, BM>(p, stage, m0, n0, tid);
+}
+
+template <int EPI>
+static hipError_t launch_b4(const mdg_gemm_desc& p, hipStream_t s) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_bf16_b4_kernel<EPI>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)b4_smem_bytes());
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  const int nwg = (p.N / kB4Tile) * ((p.M + kB4Tile - 1) / kB4Tile);
+  hipLaunchKernelGGL((gemm_bf16_b4_kernel<EPI>), dim3(nwg), dim3(kB4Threads), b4_smem_bytes(), s, p);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// Large-M variant: 256x128 block tile, 8 waves as 4x2 (64x64 wave tiles), K-step 64, a
+// 3-stage global_load_lds ring with two stages in flight across the (raw) barriers: per
+// K-step a wave waits with a COUNTED vmcnt for the stage it is about to read (leaving the
+// next stage's 6 loads outstanding), passes the barrier, issues the stage two ahead into
+// the buffer every wave finished reading one step earlier, then runs 32 MFMAs.  One block
+// per CU (144 KiB of LDS); the 256-row tile halves the L2->LDS bytes per FLOP of 128x128.
+constexpr int kB8Threads = 512;
+constexpr int kB8M = 256;
+constexpr size_t kB8Smem = 3ull * (kB8M + 128) * 64 * 2;  // 147456 B (the fp32 epilogue image, 135168 B, fits)
+
+template <int EPI>
+__global__ __launch_bounds__(kB8Threads) void gemm_bf16_b8_kernel(const mdg_gemm_desc p) {
+  constexpr int BM = kB8M, BN = 128, BK = 64, ATILE = BM * BK, STAGE = (BM + BN) * BK, LDS_ST = BN + 4;
+  typedef __attribute__((address_space(3))) void* lds_ptr_t;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  bf16_t* lds = reinterpret_cast<bf16_t*>(smem);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int M = p.M, K = p.K;
+  const int n_tiles = p.N / BN, m_tiles = (M + BM - 1) / BM, nwg = n_tiles * m_tiles;
+  const int xcd = blockIdx.x & 7, loc = blockIdx.x >> 3, q = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + loc;
+  const int mt = wg / n_tiles, nt = wg - mt * n_tiles;
+  const int m0 = mt * BM, n0 = nt * BN;
+
+  const bf16_t* A = reinterpret_cast<const bf16_t*>(p.A);
+  const bf16_t* W = reinterpret_cast<const bf16_t*>(p.W);
+  // A: 4 wave-instructions (rows 32*wave + 8i + lane/8); B: 2 (rows 16*wave + 8i + lane/8)
+  const bf16_t* asrc[4];
+  const bf16_t* bsrc[2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = 32 * wave + 8 * i + (lane >> 3);
+    asrc[i] = A + (size_t)min(m0 + row, M - 1) * p.lda + ((lane & 7) ^ ((row >> 1) & 7)) * 8;
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = 16 * wave + 8 * i + (lane >> 3);
+    bsrc[i] = W + (size_t)(n0 + row) * p.ldw + ((lane & 7) ^ ((row >> 1) & 7)) * 8;
+  }
+
+#define MDG_B8_LOAD(stage_, k0_)                                                                   \
+  {                                                                                                \
+    bf16_t* sa = lds + (stage_) * STAGE;                                                           \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i)                                                  \
+      __builtin_amdgcn_global_load_lds((const void*)(asrc[i] + (k0_)),                             \
+                                       (lds_ptr_t)(sa + (32 * wave + 8 * i) * BK), 16, 0, 0);       \
+    _Pragma("unroll") for (int i = 0; i < 2; ++i)                                                  \
+      __builtin_amdgcn_global_load_lds((const void*)(bsrc[i] + (k0_)),                             \
+                                       (lds_ptr_t)(sa + ATILE + (16 * wave + 8 * i) * BK), 16, 0, 0); \
+  }
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = K / BK;
+  MDG_B8_LOAD(0, 0);
+  if (nk > 1) MDG_B8_LOAD(1, BK);
+  const int swz = (lr >> 1) & 7;
+  int cur = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    // stage kt landed (this wave's loads) -> barrier (every wave's loads, and every wave
+    // finished reading stage kt-1, whose buffer the loads below overwrite)
+    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (kt + 2 < nk) {
+      const int nb = (cur == 0) ? 2 : cur - 1;  // (kt + 2) % 3
+      MDG_B8_LOAD(nb, (kt + 2) * BK);
+    }
+    const bf16_t* As = lds + cur * STAGE;
+    const bf16_t* Bs = As + ATILE;
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 32) {
+      const int ch = (((kk >> 3) + lg) ^ swz) * 8;
+      bf16x8 a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = *reinterpret_cast<const bf16x8*>(As + (wm * 64 + i * 16 + lr) * BK + ch);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = *reinterpret_cast<const bf16x8*>(Bs + (wn * 64 + j * 16 + lr) * BK + ch);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    cur = (cur == 2) ? 0 : cur + 1;
+  }
+#undef MDG_B8_LOAD
+
+  __syncthreads();
+  float* stage = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        stage[(wm * 64 + i * 16 + lg * 4 + r) * LDS_ST + wn * 64 + j * 16 + lr] = acc[i][j][r];
+  __syncthreads();
+  epi_tile<EPI, kB8Threads, BM>(p, stage, m0, n0, tid);
+}
+
+template <int EPI>
+static hipError_t launch_b8(const mdg_gemm_desc& p, hipStream_t s) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_bf16_b8_kernel<EPI>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)kB8Smem);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  const int nwg = (p.N / 128) * ((p.M + kB8M - 1) / kB8M);
+  hipLaunchKernelGGL((gemm_bf16_b8_kernel<EPI>), dim3(nwg), dim3(kB8Threads), kB8Smem, s, p);
+  return hipGetLastError();
 }
 
 template <typename CT, int BM, int BN, int WM, int AMODE>
@@ -392,6 +776,8 @@ static bool stage_fits() {
                                              : 2ull * BM * LDT * sizeof(CT) + 2ull * BN * LDT * sizeof(CT);
   return stage <= room;
 }
+
+constexpr int kCfgB4 = 100, kCfgB8 = 101;
 
 struct GemmPlan {
   int cfg;  // index into the config table below; -1 = unsupported
@@ -459,7 +845,25 @@ GemmPlan gemm_plan(const mdg_gemm_desc& p) {
   const bool big = p.M >= 128 * 128;
   int cfg = -1;
   if (bf && ln) cfg = (p.N % 128 == 0) ? (big ? 0 : 2) : (p.N % 32 == 0 ? (big ? 1 : 3) : -1);
-  else if (bf) cfg = (p.N == 384) ? (big ? 4 : 6) : (p.N % 128 == 0 ? (big ? 5 : 7) : (p.N % 32 == 0 ? 8 : -1));
+  else if (bf && p.N % kB4Tile == 0 && p.K % 64 == 0 && p.lda % 8 == 0 && p.ldw % 8 == 0) {
+    // MDG_GEMM_TILE=256 selects the 256x128 3-stage kernel (tuning knob; the 128x128 kernel at
+    // two blocks per CU measures faster on the block's K = 384 / 1536 shapes)
+    static const int forced = [] {
+      const char* e = getenv("MDG_GEMM_TILE");
+      return e ? atoi(e) : 0;
+    }();
+    if (forced == 256) {
+      g.cfg = kCfgB8;  // 256x128, 3-stage glds ring
+      g.smem = kB8Smem;
+      g.bm = kB8M;
+    } else {
+      g.cfg = kCfgB4;  // 128x128 glds kernel
+      g.smem = b4_smem_bytes();
+      g.bm = kB4Tile;
+    }
+    g.bn = 128;
+    return g;
+  } else if (bf) cfg = (p.N == 384) ? (big ? 4 : 6) : (p.N % 128 == 0 ? (big ? 5 : 7) : (p.N % 32 == 0 ? 8 : -1));
   else if (ln) cfg = (p.N % 32 == 0) ? 9 : -1;
   else cfg = (p.N % 96 == 0) ? 10 : (p.N % 128 == 0 ? 11 : (p.N % 32 == 0 ? 12 : -1));
   if (cfg < 0) return g;
@@ -477,6 +881,22 @@ GemmPlan gemm_plan(const mdg_gemm_desc& p) {
 }
 
 hipError_t gemm_launch(const mdg_gemm_desc& p, const GemmPlan& g, hipStream_t s) {
+  if (g.cfg == kCfgB8) {
+    switch (p.epi) {
+      case MDG_EPI_STORE: return launch_b8<MDG_EPI_STORE>(p, s);
+      case MDG_EPI_GATE_RES: return launch_b8<MDG_EPI_GATE_RES>(p, s);
+      case MDG_EPI_QKV: return launch_b8<MDG_EPI_QKV>(p, s);
+      default: return launch_b8<MDG_EPI_EULER>(p, s);
+    }
+  }
+  if (g.cfg == kCfgB4) {
+    switch (p.epi) {
+      case MDG_EPI_STORE: return launch_b4<MDG_EPI_STORE>(p, s);
+      case MDG_EPI_GATE_RES: return launch_b4<MDG_EPI_GATE_RES>(p, s);
+      case MDG_EPI_QKV: return launch_b4<MDG_EPI_QKV>(p, s);
+      default: return launch_b4<MDG_EPI_EULER>(p, s);
+    }
+  }
 #define MDG_LAUNCH_CASE(id, CT, AM, BM, BN, WM) \
   case id:                                    \
     return dispatch_epi<CT, BM, BN, WM, AM>(p, s);

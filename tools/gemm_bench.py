@@ -24,7 +24,7 @@ def tm(fn, it=20):
     return e0.elapsed_time(e1) / it * 1e3  # us
 
 
-def run(M, N, K, a_mode, epi, dt="bf16"):
+def run(M, N, K, a_mode, epi, dt="bf16", act=0):
     ct = torch.bfloat16 if dt == "bf16" else torch.float32
     A = torch.randn(M, K, device="cuda").to(ct if a_mode == 0 else torch.float32)
     W = torch.randn(N, K, device="cuda").to(ct)
@@ -34,7 +34,7 @@ def run(M, N, K, a_mode, epi, dt="bf16"):
     mods = torch.randn(8, 9 * K, device="cuda") * 0.1
     d = _lib.MdgGemmDesc()
     d.dtype = 1 if dt == "bf16" else 0
-    d.a_mode, d.epi, d.M, d.N, d.K = a_mode, epi, M, N, K
+    d.a_mode, d.epi, d.M, d.N, d.K, d.act = a_mode, epi, M, N, K, act
     d.A, d.lda, d.W, d.ldw, d.bias = A.data_ptr(), K, W.data_ptr(), K, bias.data_ptr()
     d.mods, d.mod_stride, d.rows_per_mod, d.shift_off, d.scale_off, d.ln_eps = mods.data_ptr(), 9 * K, 4000, 0, K, 1e-6
     d.out, d.ldo, d.resid, d.ldr = out.data_ptr(), N, resid.data_ptr(), N
@@ -47,15 +47,21 @@ def run(M, N, K, a_mode, epi, dt="bf16"):
     Ab = A.to(ct)
     ref = tm(lambda: torch.matmul(Ab, W.t()))
     fl = 2.0 * M * N * K
-    print(f"M={M:6d} N={N:5d} K={K:5d} amode={a_mode} epi={epi} {dt}: mdg {us:8.1f} us ({fl/us/1e6:7.1f} TF/s)   "
+    print(f"M={M:6d} N={N:5d} K={K:5d} amode={a_mode} epi={epi} act={act} {dt}: mdg {us:8.1f} us ({fl/us/1e6:7.1f} TF/s)   "
           f"torch.matmul {ref:8.1f} us ({fl/ref/1e6:7.1f} TF/s)", flush=True)
 
 
 if __name__ == "__main__":
+    import sys as _s
+    if len(_s.argv) > 1 and _s.argv[1] == "ksweep":
+        for K in (64, 128, 256, 384, 768, 1536):
+            run(32000, 1536, K, 0, 0)
+        run(32000, 1536, 384, 0, 0, act=1)
+        _s.exit(0)
     for B in (8, 1):
         M = B * 4000
         run(M, 384, 384, 0, 1)      # out-proj gate-res
-        run(M, 384, 1536, 0, 1)     # fc2
-        run(M, 1152, 384, 1, 0)     # qkv-like LNMOD store
-        run(M, 1536, 384, 1, 0)     # fc1-like
-        run(M, 1536, 384, 0, 0)     # plain store, same shape
+        run(M, 384, 1536, 0, 1)     # fc2 gate-res
+        run(M, 1152, 384, 0, 0)     # qkv-shaped plain store
+        run(M, 1536, 384, 0, 0)     # fc1-shaped plain store
+        run(M, 1536, 384, 0, 0, act=1)  # fc1 with GELU
