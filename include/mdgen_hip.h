@@ -160,6 +160,8 @@ int mdg_gemm(const mdg_gemm_desc* g, void* stream);
 int mdg_attn_spatial(int32_t dtype, int32_t n_frames, int32_t L, int32_t H, int32_t D,
                      const void* qkv, const float* kvb, const float* mask, void* out,
                      void* stream);
+/* qkv_t: CT [3][B*L][H][T][32] (q | k | v planes), head dim in columns < D, k and v rows
+   with 1.0 in pad column D (mdg_workspace_init sets it), other pad columns 0. */
 int mdg_attn_temporal(int32_t dtype, int32_t B, int32_t T, int32_t L, int32_t H, int32_t D,
                       const void* qkv_t, const float* kbias, const float* kvb, void* out,
                       void* stream);

@@ -15,7 +15,8 @@
 //    O^T = V^T P^T (the key permutation of that operand is matched by the V^T fragment read,
 //    ds_read_b64_tr_b16 of a row-major V tile).  The softmax denominator comes out of the
 //    same MFMAs: V's pad column D holds 1.0, so O^T row D = sum_k p_k.  Scores are in
-//    log2 units (q was pre-scaled by log2 e) and exponentiated with v_exp_f32.
+//    log2 units (q was pre-scaled by log2 e) and exponentiated with v_exp_f32; the running
+//    max subtraction also rides in the MFMA (K pad column D = 1.0, Q pad element = -offset).
 //  * attn_spatial: L+1 keys per query (L = crop = 4): one thread per (token, head), fp32
 //    online softmax on the VALU — no MFMA shape fits 4x5 scores.
 #include "../../include/mdgen_hip.h"
@@ -55,22 +56,32 @@ __global__ __launch_bounds__(256) void attn_temporal_kernel(const CT* __restrict
     qf[qg] = (q < T) ? ld8<CT>(Qg + (size_t)q * DP + 8 * lg) : zero8<CT>();
   }
 
-  // virtual bias key (p = exp2(0) = 1 at the initial max)
+  // virtual bias key first.  The running softmax offset mt (per query, exactly representable
+  // in CT) rides in the MFMA: K's pad column D holds 1.0 and Q's pad element D holds -mt, so
+  // S^T = K Q^T comes out of the matrix cores already as score - mt and the common case
+  // needs one v_exp_f32 per score and nothing else.  mt is only raised (rare path below)
+  // when a score exceeds it by more than kGrow (log2 units), so p <= 2^kGrow.
+  constexpr float kGrow = 8.0f;
+  const int padg = D >> 3, pade = D & 7;  // lane group / element of the pad column
   const float* kvh = kvb + head * 2 * DP;
-  float mrun[2];
+  float mt[2];
   f32x4 o[2][2];  // [d-tile][q-group]: O^T[d = 16dt + 4lg + i][q = lr]
 #pragma unroll
   for (int qg = 0; qg < 2; ++qg) {
-    float s = 0.f;
+    float sb = 0.f;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) s += (float)qf[qg][j] * kvh[8 * lg + j];
-    s += __shfl_xor(s, 16, 64);
-    s += __shfl_xor(s, 32, 64);
-    mrun[qg] = s;
+    for (int j = 0; j < 8; ++j) sb += (float)qf[qg][j] * kvh[8 * lg + j];
+    sb += __shfl_xor(sb, 16, 64);
+    sb += __shfl_xor(sb, 32, 64);
+    mt[qg] = (float)(CT)sb;
+    const float pb = __builtin_amdgcn_exp2f(sb - mt[qg]);
 #pragma unroll
     for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) o[dt][qg][i] = kvh[DP + dt * 16 + lg * 4 + i];
+      for (int i = 0; i < 4; ++i) o[dt][qg][i] = pb * kvh[DP + dt * 16 + lg * 4 + i];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (lg == padg && j == pade) qf[qg][j] = (CT)(-mt[qg]);
   }
 
   uint4 kreg[PIECES], vreg[PIECES];
@@ -137,27 +148,44 @@ __global__ __launch_bounds__(256) void attn_temporal_kernel(const CT* __restrict
           s[kt][1][i] += bb;
         }
     }
+    float mx[2];
 #pragma unroll
     for (int qg = 0; qg < 2; ++qg) {
-      float mx = s[0][qg][0];
+      float m = s[0][qg][0];
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) mx = fmaxf(mx, s[kt][qg][i]);
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mn = fmaxf(mrun[qg], mx);
-      const float alpha = __builtin_amdgcn_exp2f(mrun[qg] - mn);
-      mrun[qg] = mn;
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) o[dt][qg][i] *= alpha;
-#pragma unroll
-      for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) s[kt][qg][i] = __builtin_amdgcn_exp2f(s[kt][qg][i] - mn);
+        for (int i = 0; i < 4; ++i) m = fmaxf(m, s[kt][qg][i]);
+      m = fmaxf(m, __shfl_xor(m, 16, 64));
+      mx[qg] = fmaxf(m, __shfl_xor(m, 32, 64));
     }
+    if (__builtin_expect(__any(mx[0] > kGrow || mx[1] > kGrow), 0)) {
+      // raise the offset of the queries that outgrew it: rescale O, shift this chunk's scores
+#pragma unroll
+      for (int qg = 0; qg < 2; ++qg) {
+        const float nm = (mx[qg] > kGrow) ? (float)(CT)(mt[qg] + mx[qg]) : mt[qg];
+        const float delta = nm - mt[qg];
+        const float alpha = __builtin_amdgcn_exp2f(-delta);
+        mt[qg] = nm;
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) o[dt][qg][i] *= alpha;
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) s[kt][qg][i] -= delta;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (lg == padg && j == pade) qf[qg][j] = (CT)(-nm);
+      }
+    }
+#pragma unroll
+    for (int qg = 0; qg < 2; ++qg)
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) s[kt][qg][i] = __builtin_amdgcn_exp2f(s[kt][qg][i]);
 #pragma unroll
     for (int kh = 0; kh < 2; ++kh) {
       typename V8<CT>::T pf[2];

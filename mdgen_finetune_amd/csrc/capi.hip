@@ -113,9 +113,10 @@ int mdg_workspace_init(const mdg_dims* d, void* ws, void* stream) {
   const WsLayout w = ws_layout(*d);
   hipStream_t s = (hipStream_t)stream;
   if (int e = hip_check(hipMemsetAsync(ws, 0, w.total, s), "workspace memset")) return e;
+  // 1.0 in pad column D of every temporal K row (softmax offset) and V row (row sum)
   const size_t vrows = (size_t)d->B * d->L * d->H * d->T;
-  char* v = (char*)ws + w.qkv_t + 2 * vrows * MDG_DP * ct_size(d->dtype);
-  return hip_check(mdg::set_vpad_launch(d->dtype, v, vrows, d->D, s), "set_vpad");
+  char* k = (char*)ws + w.qkv_t + vrows * MDG_DP * ct_size(d->dtype);
+  return hip_check(mdg::set_vpad_launch(d->dtype, k, 2 * vrows, d->D, s), "set_vpad");
 }
 
 int mdg_prepare_mask(const mdg_dims* d, const float* mask, void* ws, void* stream) {

@@ -404,10 +404,6 @@ __global__ __launch_bounds__(kThreads) void gemm_kernel(const mdg_gemm_desc p) {
 constexpr int kB4Threads = 256;
 constexpr int kB4Tile = 128;
 
-__host__ __device__ constexpr size_t b4_smem_bytes() {
-  return (2 * 2 * kB4Tile * 64 * 2) > (kB4Tile * (kB4Tile + 4) * 4) ? (2 * 2 * kB4Tile * 64 * 2)
-                                                                     : (kB4Tile * (kB4Tile + 4) * 4);
-}
 
 // Epilogue of one BM x 128 output tile staged in LDS as fp32 [BM][132] (NT threads).
 template <int EPI, int NT, int BM>
@@ -537,9 +533,13 @@ __device__ __forceinline__ void epi_tile(const mdg_gemm_desc& p, const float* __
   }
 }
 
-template <int EPI>
+template <int EPI, int BK>
 __global__ __launch_bounds__(kB4Threads) void gemm_bf16_b4_kernel(const mdg_gemm_desc p) {
-  constexpr int BM = kB4Tile, BN = kB4Tile, BK = 64, TILE = BM * BK, LDS_ST = BN + 4;
+  constexpr int BM = kB4Tile, BN = kB4Tile, TILE = BM * BK, LDS_ST = BN + 4;
+  constexpr int CPR = BK / 8;      // 16-B chunks per tile row
+  constexpr int RPI = 64 / CPR;    // rows per glds wave-instruction (1 KiB)
+  constexpr int NLD = 32 / RPI;    // glds per operand per wave (a wave fills 32 rows)
+  static_assert(BK == 32 || BK == 64, "BK");
   typedef __attribute__((address_space(3))) void* lds_ptr_t;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   bf16_t* lds = reinterpret_cast<bf16_t*>(smem);
@@ -554,16 +554,18 @@ __global__ __launch_bounds__(kB4Threads) void gemm_bf16_b4_kernel(const mdg_gemm
   const int mt = wg / n_tiles, nt = wg - mt * n_tiles;
   const int m0 = mt * BM, n0 = nt * BN;
 
-  // per-lane source rows of this wave's 4 A and 4 B load instructions (rows 32*wave + 8*i + lane/8)
+  // chunk swizzle of tile row r: 128-B rows (BK 64) pair up in a 256-B bank row -> c ^ ((r>>1)&7);
+  // 64-B rows (BK 32) come four to a bank row -> c ^ ((-(r>>2))&3).  Both make the 16 fragment
+  // rows of each ds_read_b128 lane group land on 16 distinct 16-B bank slots.
+  auto swz_of = [](int r) { return BK == 64 ? ((r >> 1) & 7) : ((-(r >> 2)) & 3); };
   const bf16_t* A = reinterpret_cast<const bf16_t*>(p.A);
   const bf16_t* W = reinterpret_cast<const bf16_t*>(p.W);
-  const int lrow = 32 * wave + (lane >> 3);
-  const bf16_t* asrc[4];
-  const bf16_t* bsrc[4];
+  const bf16_t* asrc[NLD];
+  const bf16_t* bsrc[NLD];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int row = lrow + 8 * i;
-    const int ch = ((lane & 7) ^ ((row >> 1) & 7)) * 8;
+  for (int i = 0; i < NLD; ++i) {
+    const int row = 32 * wave + RPI * i + lane / CPR;
+    const int ch = ((lane % CPR) ^ swz_of(row)) * 8;
     asrc[i] = A + (size_t)min(m0 + row, M - 1) * p.lda + ch;
     bsrc[i] = W + (size_t)(n0 + row) * p.ldw + ch;
   }
@@ -571,9 +573,9 @@ __global__ __launch_bounds__(kB4Threads) void gemm_bf16_b4_kernel(const mdg_gemm
 #define MDG_B4_LOAD(stage_, k0_)                                                                   \
   {                                                                                                \
     bf16_t* sa = lds + (stage_) * 2 * TILE + (32 * wave) * BK;                                     \
-    _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                                \
-      __builtin_amdgcn_global_load_lds((const void*)(asrc[i] + (k0_)), (lds_ptr_t)(sa + 8 * i * BK), 16, 0, 0); \
-      __builtin_amdgcn_global_load_lds((const void*)(bsrc[i] + (k0_)), (lds_ptr_t)(sa + TILE + 8 * i * BK), 16, 0, 0); \
+    _Pragma("unroll") for (int i = 0; i < NLD; ++i) {                                              \
+      __builtin_amdgcn_global_load_lds((const void*)(asrc[i] + (k0_)), (lds_ptr_t)(sa + RPI * i * BK), 16, 0, 0); \
+      __builtin_amdgcn_global_load_lds((const void*)(bsrc[i] + (k0_)), (lds_ptr_t)(sa + TILE + RPI * i * BK), 16, 0, 0); \
     }                                                                                              \
   }
 
@@ -585,7 +587,7 @@ __global__ __launch_bounds__(kB4Threads) void gemm_bf16_b4_kernel(const mdg_gemm
 
   MDG_B4_LOAD(0, 0);
   const int nk = K / BK;
-  const int swz = (lr >> 1) & 7;  // ((row >> 1) & 7) of every fragment row this lane reads
+  const int swz = swz_of(lr);  // every fragment row this lane reads is lr mod 16
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -610,30 +612,44 @@ __global__ __launch_bounds__(kB4Threads) void gemm_bf16_b4_kernel(const mdg_gemm
 #undef MDG_B4_LOAD
 
   // ------------------------------------------------------------------ epilogue
-  __syncthreads();  // every wave is done reading the last stage
+  // BK 64: the whole tile is staged at once (67.5 KiB, two blocks per CU);
+  // BK 32: two 64-row bands (33.8 KiB of LDS in all, four blocks per CU).
+  constexpr int BANDS = (BK == 64) ? 1 : 2, BROWS = BM / BANDS;
   float* stage = reinterpret_cast<float*>(smem);
+  __syncthreads();  // every wave is done reading the last stage
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int band = 0; band < BANDS; ++band) {
+    if (BANDS == 1 || wm == band) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        stage[(wm * 64 + i * 16 + lg * 4 + r) * LDS_ST + wn * 64 + j * 16 + lr] = acc[i][j][r];
-  __syncthreads();
-  epi_tile<EPI, kB4Threads, BM>(p, stage, m0, n0, tid);
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            stage[((BANDS == 1 ? wm * 64 : 0) + i * 16 + lg * 4 + r) * LDS_ST + wn * 64 + j * 16 + lr] = acc[i][j][r];
+    }
+    __syncthreads();
+    epi_tile<EPI, kB4Threads, BROWS>(p, stage, m0 + band * BROWS, n0, tid);
+    if (band + 1 < BANDS) __syncthreads();
+  }
 }
 
-template <int EPI>
+template <int BK>
+__host__ __device__ constexpr size_t b4_smem() {
+  return BK == 64 ? (size_t)kB4Tile * (kB4Tile + 4) * 4 : (size_t)(kB4Tile / 2) * (kB4Tile + 4) * 4;
+}
+
+template <int EPI, int BK>
 static hipError_t launch_b4(const mdg_gemm_desc& p, hipStream_t s) {
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_bf16_b4_kernel<EPI>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)b4_smem_bytes());
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_bf16_b4_kernel<EPI, BK>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)b4_smem<BK>());
     if (e != hipSuccess) return e;
     attr_set = true;
   }
   const int nwg = (p.N / kB4Tile) * ((p.M + kB4Tile - 1) / kB4Tile);
-  hipLaunchKernelGGL((gemm_bf16_b4_kernel<EPI>), dim3(nwg), dim3(kB4Threads), b4_smem_bytes(), s, p);
+  hipLaunchKernelGGL((gemm_bf16_b4_kernel<EPI, BK>), dim3(nwg), dim3(kB4Threads), b4_smem<BK>(), s, p);
   return hipGetLastError();
 }
 
@@ -777,7 +793,7 @@ static bool stage_fits() {
   return stage <= room;
 }
 
-constexpr int kCfgB4 = 100, kCfgB8 = 101;
+constexpr int kCfgB4 = 100, kCfgB8 = 101, kCfgB4K32 = 102;
 
 struct GemmPlan {
   int cfg;  // index into the config table below; -1 = unsupported
@@ -846,8 +862,8 @@ GemmPlan gemm_plan(const mdg_gemm_desc& p) {
   int cfg = -1;
   if (bf && ln) cfg = (p.N % 128 == 0) ? (big ? 0 : 2) : (p.N % 32 == 0 ? (big ? 1 : 3) : -1);
   else if (bf && p.N % kB4Tile == 0 && p.K % 64 == 0 && p.lda % 8 == 0 && p.ldw % 8 == 0) {
-    // MDG_GEMM_TILE=256 selects the 256x128 3-stage kernel (tuning knob; the 128x128 kernel at
-    // two blocks per CU measures faster on the block's K = 384 / 1536 shapes)
+    // MDG_GEMM_TILE=256 / 64 select the 256x128 3-stage kernel / the 128x128 K-step-64 kernel
+    // (tuning knob); default: 128x128 with K-step 32 at four blocks per CU
     static const int forced = [] {
       const char* e = getenv("MDG_GEMM_TILE");
       return e ? atoi(e) : 0;
@@ -856,9 +872,13 @@ GemmPlan gemm_plan(const mdg_gemm_desc& p) {
       g.cfg = kCfgB8;  // 256x128, 3-stage glds ring
       g.smem = kB8Smem;
       g.bm = kB8M;
+    } else if (forced == 64) {
+      g.cfg = kCfgB4;  // 128x128, K-step 64, two blocks per CU
+      g.smem = b4_smem<64>();
+      g.bm = kB4Tile;
     } else {
-      g.cfg = kCfgB4;  // 128x128 glds kernel
-      g.smem = b4_smem_bytes();
+      g.cfg = kCfgB4K32;  // 128x128, K-step 32, four blocks per CU
+      g.smem = b4_smem<32>();
       g.bm = kB4Tile;
     }
     g.bn = 128;
@@ -889,12 +909,13 @@ hipError_t gemm_launch(const mdg_gemm_desc& p, const GemmPlan& g, hipStream_t s)
       default: return launch_b8<MDG_EPI_EULER>(p, s);
     }
   }
-  if (g.cfg == kCfgB4) {
+  if (g.cfg == kCfgB4 || g.cfg == kCfgB4K32) {
+    const bool k64 = g.cfg == kCfgB4;
     switch (p.epi) {
-      case MDG_EPI_STORE: return launch_b4<MDG_EPI_STORE>(p, s);
-      case MDG_EPI_GATE_RES: return launch_b4<MDG_EPI_GATE_RES>(p, s);
-      case MDG_EPI_QKV: return launch_b4<MDG_EPI_QKV>(p, s);
-      default: return launch_b4<MDG_EPI_EULER>(p, s);
+      case MDG_EPI_STORE: return k64 ? launch_b4<MDG_EPI_STORE, 64>(p, s) : launch_b4<MDG_EPI_STORE, 32>(p, s);
+      case MDG_EPI_GATE_RES: return k64 ? launch_b4<MDG_EPI_GATE_RES, 64>(p, s) : launch_b4<MDG_EPI_GATE_RES, 32>(p, s);
+      case MDG_EPI_QKV: return k64 ? launch_b4<MDG_EPI_QKV, 64>(p, s) : launch_b4<MDG_EPI_QKV, 32>(p, s);
+      default: return k64 ? launch_b4<MDG_EPI_EULER, 64>(p, s) : launch_b4<MDG_EPI_EULER, 32>(p, s);
     }
   }
 #define MDG_LAUNCH_CASE(id, CT, AM, BM, BN, WM) \

@@ -172,7 +172,7 @@ def test_attn_temporal(lib, dt, T):
     g = torch.Generator(device="cuda").manual_seed(T)
     qkv = torch.zeros(3, BL, H, T, 32, device="cuda")
     qkv[..., :D] = torch.randn(3, BL, H, T, D, device="cuda", generator=g)
-    qkv[2, ..., D] = 1.0
+    qkv[1:, ..., D] = 1.0                       # k / v pad column D (softmax offset / row sum)
     qkv = qkv.to(CT[dt])
     mask = torch.ones(B, T, L, device="cuda")
     if T > 3:
