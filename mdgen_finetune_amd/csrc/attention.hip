@@ -252,6 +252,227 @@ __global__ __launch_bounds__(256) void attn_temporal_kernel(const CT* __restrict
   }
 }
 
+// bf16 temporal attention on 32x32x16 MFMAs.  A block = 8 waves x 32 queries of one
+// (sequence, head); K/V stream through LDS in 128-key chunks (register-staged double
+// buffer, one barrier per chunk), each chunk processed as two 64-key sub-chunks:
+//   S^T (2 tiles of 32 keys x 32 queries) = K Q^T   — lane l holds 16 keys of query l&31
+//     (rows (reg&3) + 8(reg>>2) + 4(l>>5)); K is the A operand read by ds_read_b128 from an
+//     image whose 16-B chunk c of key row k sits at c ^ ((k>>3)&3) (conflict-free for the
+//     four ds_read_b128 lane groups), Q the B operand held in registers;
+//   P = exp2(S^T) converted pairwise to bf16 IS the B operand of O^T = V^T P (the
+//     accumulator-as-operand map: element j of k-step s is key 16s + 8(j>>2) + 4h + (j&3)),
+//     and the matching V^T fragment is two ds_read_b64_tr_b16 of the plain [key][32] image;
+//   the softmax offset rides in the QK MFMA (K pad column D = 1, Q pad element = -mt) and is
+//   raised only when a score outgrows it by kGrow, so the common path is one v_exp_f32 per
+//   score plus a local max for the growth test; the row sum is O^T row D (V pad column = 1).
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+
+// One 64-key sub-chunk of the bf16 temporal attention (K / V images of its 64 rows at Kc /
+// Vc, key-padding bias at kbsub): S^T = K Q^T (4 MFMAs), growth test / rare offset raise,
+// P = exp2(S^T) -> bf16 B operand, O^T += V^T P (4 MFMAs with tr-read V^T fragments).
+__device__ __forceinline__ void ta_subchunk(const bf16_t* Kc, const bf16_t* Vc, const float* kbsub, bool masked,
+                                            int r, int h, int grow, int gcol, int padS, int padH, int padJ,
+                                            bf16x8 (&qf)[2], float& mt, f32x16& o) {
+  constexpr int DP = MDG_DP;
+  constexpr float kGrow = 8.0f;
+  typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+  f32x16 sacc[2];
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt) {
+    const int row = kt * 32 + r;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) sacc[kt][i] = 0.f;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const bf16x8 kf = *reinterpret_cast<const bf16x8*>(Kc + row * DP + (((2 * s2 + h) ^ ((row >> 3) & 3)) * 8));
+      sacc[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s2], sacc[kt], 0, 0, 0);
+    }
+  }
+  if (masked) {
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sacc[kt][i] += kbsub[kt * 32 + (i & 3) + 8 * (i >> 2) + 4 * h];
+  }
+  float lm = sacc[0][0];
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) lm = fmaxf(lm, sacc[kt][i]);
+  if (__builtin_expect(__any(lm > kGrow), 0)) {
+    const float mx = fmaxf(lm, __shfl_xor(lm, 32, 64));
+    const float nm = (mx > kGrow) ? (float)(bf16_t)(mt + mx) : mt;
+    const float delta = nm - mt;
+    const float alpha = __builtin_amdgcn_exp2f(-delta);
+    mt = nm;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) o[i] *= alpha;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sacc[kt][i] -= delta;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (s2 == padS && h == padH && j == padJ) qf[s2][j] = (bf16_t)(-nm);
+  }
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt) {
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      bf16x8 pf;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) pf[j] = (bf16_t)__builtin_amdgcn_exp2f(sacc[kt][8 * s2 + j]);
+      const bf16_t* vb = Vc + (kt * 32 + 16 * s2 + grow) * DP + gcol;
+      const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(vb));
+      const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(vb + 8 * DP));
+      bf16x8 vf;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        vf[j] = lo[j];
+        vf[4 + j] = hi[j];
+      }
+      o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, o, 0, 0, 0);
+    }
+  }
+}
+
+// Bias key + offset setup shared by both bf16 temporal kernels: Q fragments (B operand,
+// d = 16s + 8h + j), mt = bf16(score of the bias key), O^T = exp2(score_b - mt) * bias_v,
+// Q pad element = -mt.
+__device__ __forceinline__ void ta_setup(const bf16_t* Qg, const float* kvh, int q, int T, int D, int r, int h,
+                                         bf16x8 (&qf)[2], float& mt, f32x16& o) {
+  constexpr int DP = MDG_DP;
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2)
+    qf[s2] = (q < T) ? *reinterpret_cast<const bf16x8*>(Qg + (size_t)q * DP + 16 * s2 + 8 * h) : zero8<bf16_t>();
+  float sb = 0.f;
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sb += (float)qf[s2][j] * kvh[16 * s2 + 8 * h + j];
+  sb += __shfl_xor(sb, 32, 64);
+  mt = (float)(bf16_t)sb;
+  const float pb = __builtin_amdgcn_exp2f(sb - mt);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) o[i] = pb * kvh[DP + (i & 3) + 8 * (i >> 2) + 4 * h];
+  const int padS = D >> 4, padH = (D >> 3) & 1, padJ = D & 7;
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (s2 == padS && h == padH && j == padJ) qf[s2][j] = (bf16_t)(-mt);
+}
+
+// O = O^T / row sum (O^T row D), stored as O[token][head*D + d]
+__device__ __forceinline__ void ta_store(const f32x16& o, bf16_t* out, int q, int T, int L, int H, int D, int seq,
+                                         int head, int h) {
+  const int hD = (D >> 2) & 1, regD = (D & 3) + 4 * (D >> 3);
+  float mine = 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+    if (i == regD) mine = o[i];
+  const float other = __shfl_xor(mine, 32, 64);
+  const float inv = 1.0f / ((h == hD) ? mine : other);
+  if (q < T) {
+    const int C = H * D, b = seq / L, l = seq % L;
+    bf16_t* orow = out + ((size_t)(b * T + q) * L + l) * C + head * D;
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const int d0 = 8 * g4 + 4 * h;
+      if (d0 < D)
+        st4<bf16_t>(orow + d0, o[4 * g4] * inv, o[4 * g4 + 1] * inv, o[4 * g4 + 2] * inv, o[4 * g4 + 3] * inv);
+    }
+  }
+}
+
+constexpr int kTW = 8;    // waves per block
+constexpr int kTKC = 128; // keys per LDS chunk
+
+__global__ __launch_bounds__(kTW * 64) void attn_temporal_bf16_kernel(const bf16_t* __restrict__ qkv,
+                                                                    const float* __restrict__ kbias,
+                                                                    const float* __restrict__ kvb,
+                                                                    bf16_t* __restrict__ out, int T, int L,
+                                                                    int H, int D, int BL) {
+  constexpr int DP = MDG_DP, KC = kTKC, NTH = kTW * 64;
+  static_assert(KC * DP / 8 == NTH, "one 16-B K piece and one V piece per thread per chunk");
+  __shared__ __attribute__((aligned(16))) bf16_t Ks[2][KC * DP];
+  __shared__ __attribute__((aligned(16))) bf16_t Vs[2][KC * DP];
+  __shared__ float kbs[2][KC];
+  __shared__ int kflag[2][2];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int seq = blockIdx.z, head = blockIdx.y;
+  const int q0 = blockIdx.x * (kTW * 32) + wave * 32;
+  const size_t plane = (size_t)BL * H * T * DP;
+  const bf16_t* Qg = qkv + ((size_t)seq * H + head) * T * DP;
+  const bf16_t* Kg = Qg + plane;
+  const bf16_t* Vg = Qg + 2 * plane;
+  const float* kb = kbias + (size_t)seq * T;
+
+  const int q = q0 + r;
+  bf16x8 qf[2];
+  float mt;
+  f32x16 o;
+  ta_setup(Qg, kvb + head * 2 * DP, q, T, D, r, h, qf, mt, o);
+  const int padS = D >> 4, padH = (D >> 3) & 1, padJ = D & 7;  // Q element holding -mt
+
+  // chunk staging: thread -> key row tid/4, 16-B piece tid%4 of K and of V
+  const int srow = tid >> 2, spc = tid & 3;
+  u32x4 kreg, vreg;
+  float kbreg = 0.f;
+#define MDG_TA_GLOAD(c_)                                                                      \
+  {                                                                                           \
+    const int key = (c_) * KC + srow;                                                         \
+    kreg = vreg = u32x4{0u, 0u, 0u, 0u};                                                      \
+    if (key < T) {                                                                            \
+      kreg = *reinterpret_cast<const u32x4*>(Kg + (size_t)key * DP + spc * 8);                \
+      vreg = *reinterpret_cast<const u32x4*>(Vg + (size_t)key * DP + spc * 8);                \
+    }                                                                                         \
+    if (tid < KC) {                                                                           \
+      const int kk = (c_) * KC + tid;                                                         \
+      kbreg = (kk < T) ? kb[kk] : -INFINITY;                                                  \
+    }                                                                                         \
+  }
+#define MDG_TA_LSTORE(buf)                                                                    \
+  {                                                                                           \
+    *reinterpret_cast<u32x4*>(&Ks[buf][srow * DP + ((spc ^ ((srow >> 3) & 3)) * 8)]) = kreg;  \
+    *reinterpret_cast<u32x4*>(&Vs[buf][srow * DP + spc * 8]) = vreg;                          \
+    if (tid < KC) {                                                                           \
+      kbs[buf][tid] = kbreg;                                                                  \
+      const bool any = __any(kbreg != 0.f);                                                   \
+      if (lane == 0) kflag[buf][wave] = any ? 1 : 0;                                          \
+    }                                                                                         \
+  }
+
+  const int nchunks = (T + KC - 1) / KC;
+  MDG_TA_GLOAD(0);
+  MDG_TA_LSTORE(0);
+  __syncthreads();
+  // V^T tr-read lane geometry: 16-lane group g reads keys (+4h + i>>2), columns 16(g&1) + 4(i&3)
+  const int gi = lane & 15, gcol = 16 * ((lane >> 4) & 1) + 4 * (gi & 3), grow = 4 * h + (gi >> 2);
+  for (int c = 0; c < nchunks; ++c) {
+    const int cur = c & 1;
+    if (c + 1 < nchunks) MDG_TA_GLOAD(c + 1);
+    const bool masked = (kflag[cur][0] | kflag[cur][1]) != 0;
+    const bf16_t* Kc = Ks[cur];
+    const bf16_t* Vc = Vs[cur];
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub)
+      ta_subchunk(Kc + sub * 64 * DP, Vc + sub * 64 * DP, kbs[cur] + sub * 64, masked, r, h, grow, gcol, padS, padH,
+                  padJ, qf, mt, o);
+    if (c + 1 < nchunks) MDG_TA_LSTORE(cur ^ 1);
+    __syncthreads();
+  }
+#undef MDG_TA_GLOAD
+#undef MDG_TA_LSTORE
+
+  ta_store(o, out, q, T, L, H, D, seq, head, h);
+}
+
+
 template <typename CT>
 __global__ __launch_bounds__(256) void attn_spatial_kernel(const CT* __restrict__ qkv,
                                                            const float* __restrict__ kvb,
@@ -311,6 +532,12 @@ __global__ __launch_bounds__(256) void attn_spatial_kernel(const CT* __restrict_
 
 hipError_t attn_temporal_launch(int dtype, int B, int T, int L, int H, int D, const void* qkv_t,
                                 const float* kbias, const float* kvb, void* out, hipStream_t s) {
+  if (dtype == MDG_BF16) {
+    dim3 grid((T + kTW * 32 - 1) / (kTW * 32), H, B * L);
+    hipLaunchKernelGGL(attn_temporal_bf16_kernel, grid, dim3(kTW * 64), 0, s, (const bf16_t*)qkv_t, kbias,
+                       kvb, (bf16_t*)out, T, L, H, D, B * L);
+    return hipGetLastError();
+  }
   dim3 grid((T + 127) / 128, H, B * L);
   if (dtype == MDG_BF16)
     hipLaunchKernelGGL(attn_temporal_kernel<bf16_t>, grid, dim3(256), 0, s,

@@ -45,73 +45,100 @@ __global__ __launch_bounds__(256) void embed_kernel(int N, int T, int L, int C, 
 // xn[m][k] = CT( LN(h[m])[k] * (1 + scale[b][k]) + shift[b][k] ),  b = m / rows_per_mod
 // The no-affine LayerNorm (eps 1e-6) + adaLN modulate in front of every projection of the
 // block (latent_model.py:467/475/489, FinalLayer layers.py:73, modulate layers.py:14-15).
-// One wave per row: each lane holds W consecutive channels of every 64W-channel chunk
-// (W = 2 when C % 128 == 0: 256-B bf16 stores per wave instruction), two wave reductions
-// (mean, then the centred sum of squares, as torch's two-pass LayerNorm).
+// One wave per R = 4 consecutive rows (their 4 x C/64 loads in flight together; the shift /
+// scale rows loaded once when the 4 rows share a batch entry).  Each lane holds W
+// consecutive channels of every 64W-channel chunk (W = 2 when C % 128 == 0: 256-B bf16
+// stores per wave instruction); two wave reductions per row (mean, then the centred sum of
+// squares, as torch's two-pass LayerNorm).
 template <typename CT, int W>
 __global__ __launch_bounds__(256) void ln_mod_kernel(int M, int C, const float* __restrict__ h,
                                                      const float* __restrict__ mods, int mod_stride,
                                                      int rows_per_mod, int shift_off, int scale_off,
                                                      float eps, CT* __restrict__ xn) {
-  constexpr int E = 8 / W;  // C <= 512
+  constexpr int E = 8 / W, R = 4;  // C <= 512
   const int lane = threadIdx.x & 63;
-  const int m = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (m >= M) return;
+  const int m0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * R;
+  if (m0 >= M) return;
   const int nE = C / (64 * W);
-  const float* hr = h + (size_t)m * C;
-  const float* mr = mods + (size_t)(m / rows_per_mod) * mod_stride;
-  float v[E][W], sc[E][W], sh[E][W];
+  float v[R][E][W], sc[E][W], sh[E][W];
+  const int b0 = m0 / rows_per_mod;
+  const bool shared = (min(m0 + R - 1, M - 1) / rows_per_mod) == b0;
 #pragma unroll
-  for (int e = 0; e < E; ++e) {
-    const int k = W * lane + 64 * W * e;
-    if (e < nE) {
-      if constexpr (W == 2) {
-        const float2 a = *reinterpret_cast<const float2*>(hr + k);
-        const float2 b = *reinterpret_cast<const float2*>(mr + scale_off + k);
-        const float2 c = *reinterpret_cast<const float2*>(mr + shift_off + k);
-        v[e][0] = a.x; v[e][1] = a.y; sc[e][0] = b.x; sc[e][1] = b.y; sh[e][0] = c.x; sh[e][1] = c.y;
+  for (int r = 0; r < R; ++r) {
+    const float* hr = h + (size_t)min(m0 + r, M - 1) * C;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int k = W * lane + 64 * W * e;
+      if (e < nE) {
+        if constexpr (W == 2) {
+          const float2 a = *reinterpret_cast<const float2*>(hr + k);
+          v[r][e][0] = a.x; v[r][e][1] = a.y;
+        } else {
+          v[r][e][0] = hr[k];
+        }
       } else {
-        v[e][0] = hr[k]; sc[e][0] = mr[scale_off + k]; sh[e][0] = mr[shift_off + k];
-      }
-    } else {
 #pragma unroll
-      for (int j = 0; j < W; ++j) v[e][j] = sc[e][j] = sh[e][j] = 0.f;
+        for (int j = 0; j < W; ++j) v[r][e][j] = 0.f;
+      }
     }
   }
-  float s = 0.f;
+  auto load_mods = [&](int b) {
+    const float* mr = mods + (size_t)b * mod_stride;
 #pragma unroll
-  for (int e = 0; e < E; ++e)
-#pragma unroll
-    for (int j = 0; j < W; ++j) s += v[e][j];
-  const float mean = wave_sum(s) / (float)C;
-  float ss = 0.f;
-#pragma unroll
-  for (int e = 0; e < E; ++e)
-    if (e < nE)
-#pragma unroll
-      for (int j = 0; j < W; ++j) {
-        const float a = v[e][j] - mean;
-        ss += a * a;
-      }
-  const float rs = 1.0f / sqrtf(wave_sum(ss) / (float)C + eps);
-#pragma unroll
-  for (int e = 0; e < E; ++e) {
-    if (e < nE) {
+    for (int e = 0; e < E; ++e) {
       const int k = W * lane + 64 * W * e;
-      float y[W];
+      if (e < nE) {
+        if constexpr (W == 2) {
+          const float2 x = *reinterpret_cast<const float2*>(mr + scale_off + k);
+          const float2 y = *reinterpret_cast<const float2*>(mr + shift_off + k);
+          sc[e][0] = x.x; sc[e][1] = x.y; sh[e][0] = y.x; sh[e][1] = y.y;
+        } else {
+          sc[e][0] = mr[scale_off + k]; sh[e][0] = mr[shift_off + k];
+        }
+      }
+    }
+  };
+  if (shared) load_mods(b0);
 #pragma unroll
-      for (int j = 0; j < W; ++j) y[j] = (v[e][j] - mean) * rs * (1.0f + sc[e][j]) + sh[e][j];
-      CT* o = xn + (size_t)m * C + k;
-      if constexpr (W == 2 && is_bf16<CT>()) {
-        typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
-        bf16x2 pr;
-        pr[0] = (bf16_t)y[0];
-        pr[1] = (bf16_t)y[1];
-        *reinterpret_cast<bf16x2*>(o) = pr;
-      } else if constexpr (W == 2) {
-        *reinterpret_cast<float2*>(o) = make_float2(y[0], y[1]);
-      } else {
-        o[0] = (CT)y[0];
+  for (int r = 0; r < R; ++r) {
+    const int m = m0 + r;
+    if (m >= M) break;
+    if (!shared) load_mods(m / rows_per_mod);
+    float s = 0.f;
+#pragma unroll
+    for (int e = 0; e < E; ++e)
+#pragma unroll
+      for (int j = 0; j < W; ++j) s += v[r][e][j];
+    const float mean = wave_sum(s) / (float)C;
+    float ss = 0.f;
+#pragma unroll
+    for (int e = 0; e < E; ++e)
+      if (e < nE)
+#pragma unroll
+        for (int j = 0; j < W; ++j) {
+          const float a = v[r][e][j] - mean;
+          ss += a * a;
+        }
+    const float rs = 1.0f / sqrtf(wave_sum(ss) / (float)C + eps);
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      if (e < nE) {
+        const int k = W * lane + 64 * W * e;
+        float y[W];
+#pragma unroll
+        for (int j = 0; j < W; ++j) y[j] = (v[r][e][j] - mean) * rs * (1.0f + sc[e][j]) + sh[e][j];
+        CT* o = xn + (size_t)m * C + k;
+        if constexpr (W == 2 && is_bf16<CT>()) {
+          typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+          bf16x2 pr;
+          pr[0] = (bf16_t)y[0];
+          pr[1] = (bf16_t)y[1];
+          *reinterpret_cast<bf16x2*>(o) = pr;
+        } else if constexpr (W == 2) {
+          *reinterpret_cast<float2*>(o) = make_float2(y[0], y[1]);
+        } else {
+          o[0] = (CT)y[0];
+        }
       }
     }
   }
@@ -148,7 +175,7 @@ hipError_t embed_launch(int N, int T, int L, int C, int K, const float* x, const
 hipError_t ln_mod_launch(int dtype, int M, int C, const float* h, const float* mods, int mod_stride,
                          int rows_per_mod, int shift_off, int scale_off, float eps, void* xn,
                          hipStream_t s) {
-  dim3 grid((M + 3) / 4);
+  dim3 grid((M + 15) / 16);
 #define MDG_LN(CTT, W)                                                                        \
   hipLaunchKernelGGL((ln_mod_kernel<CTT, W>), grid, dim3(256), 0, s, M, C, h, mods, mod_stride, \
                      rows_per_mod, shift_off, scale_off, eps, (CTT*)xn)
