@@ -15,8 +15,9 @@ Multi-GPU: inference does not shard (temporal attention couples all T frames of 
 trajectory), so N ranks run N independent replicas of the window ("replicas only",
 scaling "weak"); no collective on the data path.
 
-Extra fields: "roofline" for the dominant kernel (live HIP-event timing on the stream the
-kernel runs on), "cpu_baseline" (the oracle restatement timed on this host's cores).
+Extra fields: "roofline" for the dominant kernel (the temporal q|k|v projection GEMM; live
+HIP-event timing on the stream the kernel runs on), "roofline_attn_temporal" for the next
+one, "cpu_baseline" (the oracle restatement timed on this host's cores).
 """
 import argparse
 import ctypes
@@ -90,42 +91,59 @@ def time_kernel(fn, iters=20):
     return e0.elapsed_time(e1) / iters * 1e-3
 
 
+def _traffic(kernel, B, T, L, dtype):
+    """HBM bytes per launch from the committed PMC pass (profiles/traffic_r01.json, FETCH_SIZE x2
+    + WRITE_SIZE per the gfx950 correction of MI355X_MICROARCH.md §HBM), or None."""
+    prof = os.path.join(REPO, "profiles", "traffic_r01.json")
+    try:
+        return json.load(open(prof))[kernel].get(f"B{B}_T{T}_L{L}_{dtype}")
+    except Exception:
+        return None
+
+
 def roofline(eng, st, dtype, B, T, L):
-    """Dominant kernel = the temporal flash attention (largest share of the step in the rocprof
-    summary, profiles/).  Algorithmic FLOPs per launch = 4*B*L*H*T*(T+1)*D (QK^T and PV over
-    T+1 keys incl. the bias row, unpadded head_dim D=24)."""
+    """Roofline of the two kernels that dominate the step (rocprof summary in profiles/):
+    the temporal q|k|v projection GEMM (2 per layer with the spatial one; 2*M*N*K FLOPs,
+    M = B*T*L, N = 3C, K = C) and the temporal flash attention (4*B*L*H*T*(T+1)*D FLOPs: QK^T
+    and PV over T+1 keys incl. the bias row, unpadded head_dim D).  Both launched exactly as
+    in the step (same workspace buffers, layer-0 weights) and timed with HIP events on the
+    stream they run on."""
     from mdgen_finetune_amd import _lib
 
-    lib = eng.lib
+    lib, P = eng.lib, eng._packed
     ws = st.ws.data_ptr()
-    H, D = eng.H, eng.D
-    # workspace offsets (mirror of ws_layout in capi.hip)
-    cs = 2 if dtype == "bf16" else 4
-    a256 = lambda x: (x + 255) // 256 * 256  # noqa: E731
+    off = _lib.workspace_offsets(st.dims)
+    H, D, C = eng.H, eng.D, eng.C
     N = B * T * L
-    off_qkv_t = a256(N * 3 * H * 32 * cs)
-    off_o = off_qkv_t + a256(3 * B * L * H * T * 32 * cs)
-    off_kb = off_o + a256(N * eng.C * cs) + a256(N * eng.F * cs)
-    kvb = st.kvb[0][1]
     s = _lib.stream_handle()
+    kvb = st.kvb[0][1]
 
-    def launch():
-        _lib.check(lib.mdg_attn_temporal(eng.mdg_dtype, B, T, L, H, D, ws + off_qkv_t, ws + off_kb, kvb.data_ptr(),
-                                         ws + off_o, s), "attn_temporal")
+    def attn():
+        _lib.check(lib.mdg_attn_temporal(eng.mdg_dtype, B, T, L, H, D, ws + off["qkv_t"], ws + off["kbias"],
+                                         kvb.data_ptr(), ws + off["o"], s), "attn_temporal")
 
-    sec = time_kernel(launch, 50)
-    flops = 4.0 * B * L * H * T * (T + 1) * D
-    achieved = flops / sec / 1e12
-    traffic = None
-    prof = os.path.join(REPO, "profiles", "traffic_attn_temporal.json")
-    if os.path.exists(prof):
-        try:
-            traffic = json.load(open(prof)).get(f"B{B}_T{T}_L{L}_{dtype}")
-        except Exception:
-            traffic = None
-    return {"kernel": "attn_temporal_kernel", "bound": "mfma", "achieved": round(achieved, 2),
-            "peak": PEAK_TFLOPS[dtype], "unit": "TFLOP/s", "frac": round(achieved / PEAK_TFLOPS[dtype], 4),
-            "traffic": traffic, "avg_launch_us": round(sec * 1e6, 2), "flops_per_launch": flops}
+    g = _lib.MdgGemmDesc()
+    g.dtype, g.a_mode, g.epi, g.M, g.N, g.K = eng.mdg_dtype, _lib.MDG_A_PLAIN, _lib.MDG_EPI_QKV, N, 3 * C, C
+    g.A, g.lda = ws + off["xn"], C
+    g.W, g.ldw, g.bias = P["layers"][0]["wqkv1"].data_ptr(), C, P["layers"][0]["bqkv1"].data_ptr()
+    g.qkv_layout, g.qkv_out, g.H, g.D, g.T, g.L = _lib.MDG_QKV_TEMPORAL, ws + off["qkv_t"], H, D, T, L
+    g.qscale = D ** -0.5 * math.log2(math.e)
+    g.rope, g.rope_rows = _lib.ptr(st.rope_t), T + 1
+
+    def gemm():
+        _lib.check(lib.mdg_gemm(ctypes.byref(g), s), "qkv gemm")
+
+    out = []
+    for name, fn, flops in (("gemm_qkv_temporal", gemm, 2.0 * N * 3 * C * C),
+                            ("attn_temporal", attn, 4.0 * B * L * H * T * (T + 1) * D)):
+        sec = time_kernel(fn, 50)
+        ach = flops / sec / 1e12
+        out.append({"kernel": name, "bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_TFLOPS[dtype],
+                    "unit": "TFLOP/s", "frac": round(ach / PEAK_TFLOPS[dtype], 4),
+                    "traffic": _traffic(name, B, T, L, dtype), "avg_launch_us": round(sec * 1e6, 2),
+                    "flops_per_launch": flops})
+    gemm()  # leave the temporal q|k|v of layer 0 in place (the attention launches above read it)
+    return out[0], out[1]
 
 
 def cpu_baseline(T, L, seconds):
@@ -217,7 +235,7 @@ def main():
         frames = world * B * T * n_euler * a.steps
         value = frames / el
         st = eng._state(B, T, L)
-        roof = roofline(eng, st, a.dtype, B, T, L) if rank == 0 else None
+        roof, roof2 = roofline(eng, st, a.dtype, B, T, L) if rank == 0 else (None, None)
 
     out = None
     if rank == 0:
@@ -243,6 +261,7 @@ def main():
                        "parallelism": f"replicas{world}", "hipgraph": not a.no_graph},
             "us_per_denoise_step": round(el / a.steps / n_euler * 1e6, 2),
             "roofline": roof,
+            "roofline_attn_temporal": roof2,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

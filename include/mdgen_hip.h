@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define MDG_ABI_VERSION 2
+#define MDG_ABI_VERSION 3
 #define MDG_MAX_LAYERS 16
 #define MDG_DP 32 /* padded head dim of every attention operand buffer (head_dim <= 31) */
 
@@ -127,6 +127,10 @@ const char* mdg_last_error_string(void);
 
 /* Workspace (attention operand buffers, hidden activations, key-padding bias). */
 size_t mdg_workspace_bytes(const mdg_dims* d);
+/* Byte offsets of the workspace regions, in this order: qkv_s (spatial q|k|v), qkv_t
+   (temporal q|k|v planes), o (attention output), hid (MLP hidden), xn (LayerNorm+modulate
+   output), kbias (temporal key-padding bias).  For profiling / tests; 0 on success. */
+int mdg_workspace_offsets(const mdg_dims* d, size_t offsets[6]);
 int mdg_workspace_init(const mdg_dims* d, void* ws, void* stream);
 /* key-padding additive bias for the temporal attention from mask [B,T,L] (0 -> -inf) */
 int mdg_prepare_mask(const mdg_dims* d, const float* mask, void* ws, void* stream);

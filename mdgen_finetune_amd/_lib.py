@@ -68,6 +68,7 @@ SIGNATURES = [
     ("mdg_abi_version", _i32, []),
     ("mdg_last_error_string", ctypes.c_char_p, []),
     ("mdg_workspace_bytes", ctypes.c_size_t, [ctypes.POINTER(MdgDims)]),
+    ("mdg_workspace_offsets", _i32, [ctypes.POINTER(MdgDims), ctypes.POINTER(ctypes.c_size_t)]),
     ("mdg_workspace_init", _i32, [ctypes.POINTER(MdgDims), _vp, _vp]),
     ("mdg_prepare_mask", _i32, [ctypes.POINTER(MdgDims), _vp, _vp, _vp]),
     ("mdg_embed", _i32, [_i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
@@ -80,7 +81,7 @@ SIGNATURES = [
     ("mdg_attn_temporal", _i32, [_i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
 ]
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 _LIB = None
 
 
@@ -116,6 +117,16 @@ def ptr(t) -> int | None:
     if t is None:
         return None
     return t.data_ptr()
+
+
+WS_REGIONS = ("qkv_s", "qkv_t", "o", "hid", "xn", "kbias")
+
+
+def workspace_offsets(dims) -> dict:
+    """Byte offsets of the workspace regions (mdg_workspace_offsets)."""
+    arr = (ctypes.c_size_t * 6)()
+    check(load().mdg_workspace_offsets(ctypes.byref(dims), arr), "mdg_workspace_offsets")
+    return dict(zip(WS_REGIONS, list(arr)))
 
 
 def stream_handle(stream=None) -> int:

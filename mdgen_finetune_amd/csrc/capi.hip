@@ -107,6 +107,15 @@ size_t mdg_workspace_bytes(const mdg_dims* d) {
   return ws_layout(*d).total;
 }
 
+int mdg_workspace_offsets(const mdg_dims* d, size_t offsets[6]) {
+  if (int e = check_dims(d)) return e;
+  if (!offsets) return fail(MDG_E_ARG, "null offsets");
+  const WsLayout w = ws_layout(*d);
+  offsets[0] = w.qkv_s; offsets[1] = w.qkv_t; offsets[2] = w.o;
+  offsets[3] = w.hid; offsets[4] = w.xn; offsets[5] = w.kbias;
+  return 0;
+}
+
 int mdg_workspace_init(const mdg_dims* d, void* ws, void* stream) {
   if (int e = check_dims(d)) return e;
   if (!ws) return fail(MDG_E_ARG, "null workspace");

@@ -75,3 +75,7 @@ def test_shape_validation_without_gpu():
     bad = _lib.MdgDims(B=1, T=10, L=4, C=384, H=12, D=32, F=1536, latent=21, num_layers=5, dtype=1)
     assert lib.mdg_workspace_bytes(ctypes.byref(bad)) == 0
     assert b"head_dim" in lib.mdg_last_error_string()
+    offs = _lib.workspace_offsets(d)
+    vals = [offs[k] for k in _lib.WS_REGIONS]
+    assert vals == sorted(vals) and vals[0] == 0 and all(v % 256 == 0 for v in vals)
+    assert offs["kbias"] < lib.mdg_workspace_bytes(ctypes.byref(d))

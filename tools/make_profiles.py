@@ -1,0 +1,58 @@
+"""Copy the judged rocprof summaries from gpurun_out/ into profiles/ (tracked) for round RR:
+  profiles/rRR_kernel_stats.csv   rocprofv3 --kernel-trace --stats of `bench.py --steps 3`
+  profiles/rRR_summary.md         per-kernel table (calls, avg us, share)
+  profiles/traffic_rRR.json       HBM bytes per launch of the bench roofline kernels from the
+                                  FETCH_SIZE / WRITE_SIZE passes (tools/roof_pmc.sh): KiB
+                                  counters x 1024, FETCH_SIZE doubled (gfx950: FETCH_SIZE
+                                  reports half the bytes of 16-B/lane streaming reads,
+                                  MI355X_MICROARCH.md §HBM); mean of the last 50 dispatches
+                                  (the roofline timing loop).
+Usage: python tools/make_profiles.py RR [B T L]"""
+import collections
+import csv
+import json
+import os
+import shutil
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+rr = sys.argv[1]
+B, T, L = (int(a) for a in sys.argv[2:5]) if len(sys.argv) > 4 else (8, 1000, 4)
+out = os.path.join(REPO, "profiles")
+os.makedirs(out, exist_ok=True)
+
+stats = os.path.join(REPO, "gpurun_out", "prof", "run_kernel_stats.csv")
+if os.path.exists(stats):
+    shutil.copy(stats, os.path.join(out, f"r{rr}_kernel_stats.csv"))
+    rows = list(csv.DictReader(open(stats)))
+    lines = [f"# r{rr}: rocprofv3 --kernel-trace --stats, `python bench.py --steps 3 --warmup 1 --no-cpu-baseline`",
+             "", "| kernel | calls | avg us | total % |", "|---|---|---|---|"]
+    for r in rows[:20]:
+        lines.append(f"| `{r['Name'][:90]}` | {r['Calls']} | {float(r['AverageNs']) / 1e3:.1f} | "
+                     f"{float(r['Percentage']):.2f} |")
+    open(os.path.join(out, f"r{rr}_summary.md"), "w").write("\n".join(lines) + "\n")
+
+KMAP = {"gemm_bf16_b4_kernel<2": "gemm_qkv_temporal", "attn_temporal_bf16": "attn_temporal"}
+res = collections.defaultdict(dict)
+for cname, scale in (("FETCH_SIZE", 2 * 1024), ("WRITE_SIZE", 1024)):
+    p = os.path.join(REPO, "gpurun_out", "pmc_roof", f"{cname}_counter_collection.csv")
+    if not os.path.exists(p):
+        continue
+    shutil.copy(p, os.path.join(out, f"r{rr}_pmc_{cname}.csv"))
+    by = collections.defaultdict(list)
+    for r in csv.DictReader(open(p)):
+        for pat, name in KMAP.items():
+            if pat in r["Kernel_Name"]:
+                by[name].append((int(r["Dispatch_Id"]), float(r["Counter_Value"])))
+    for name, v in by.items():
+        v.sort()
+        last = [x[1] for x in v[-50:]]
+        res[name][cname] = sum(last) / len(last) * scale
+traffic = {}
+for name, d in res.items():
+    if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
+        traffic[name] = {f"B{B}_T{T}_L{L}_bf16": round(d["FETCH_SIZE"] + d["WRITE_SIZE"]),
+                         "read_bytes": round(d["FETCH_SIZE"]), "write_bytes": round(d["WRITE_SIZE"])}
+if traffic:
+    json.dump(traffic, open(os.path.join(out, f"traffic_r{rr}.json"), "w"), indent=1)
+print(json.dumps(traffic, indent=1))
