@@ -404,8 +404,13 @@ __global__ __launch_bounds__(kTW * 64) void attn_temporal_bf16_kernel(const bf16
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
-  const int seq = blockIdx.z, head = blockIdx.y;
-  const int q0 = blockIdx.x * (kTW * 32) + wave * 32;
+  // XCD-aware order (bijective remap of the 1-D grid): the query blocks of one (sequence,
+  // head) are consecutive on one XCD, so its K / V are fetched into that XCD's L2 once
+  const int nqb = (T + kTW * 32 - 1) / (kTW * 32), nwg = nqb * H * BL;
+  const int xcd = blockIdx.x & 7, loc = blockIdx.x >> 3, qq = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (qq + 1) : r8 * (qq + 1) + (xcd - r8) * qq) + loc;
+  const int qb = wg % nqb, head = (wg / nqb) % H, seq = wg / (nqb * H);
+  const int q0 = qb * (kTW * 32) + wave * 32;
   const size_t plane = (size_t)BL * H * T * DP;
   const bf16_t* Qg = qkv + ((size_t)seq * H + head) * T * DP;
   const bf16_t* Kg = Qg + plane;
@@ -533,7 +538,7 @@ __global__ __launch_bounds__(256) void attn_spatial_kernel(const CT* __restrict_
 hipError_t attn_temporal_launch(int dtype, int B, int T, int L, int H, int D, const void* qkv_t,
                                 const float* kbias, const float* kvb, void* out, hipStream_t s) {
   if (dtype == MDG_BF16) {
-    dim3 grid((T + kTW * 32 - 1) / (kTW * 32), H, B * L);
+    dim3 grid((unsigned)((T + kTW * 32 - 1) / (kTW * 32) * H * B * L));
     hipLaunchKernelGGL(attn_temporal_bf16_kernel, grid, dim3(kTW * 64), 0, s, (const bf16_t*)qkv_t, kbias,
                        kvb, (bf16_t*)out, T, L, H, D, B * L);
     return hipGetLastError();
