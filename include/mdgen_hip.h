@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define MDG_ABI_VERSION 3
+#define MDG_ABI_VERSION 4
 #define MDG_MAX_LAYERS 16
 #define MDG_DP 32 /* padded head dim of every attention operand buffer (head_dim <= 31) */
 
@@ -120,6 +120,11 @@ typedef struct {
   const float* rope; int32_t rope_rows; /* cos [rope_rows][D/2] then sin; null = no RoPE */
   /* EULER: x_out (= out, row stride ldo) = x_in + dt * v, v_out = v, for columns < n_valid */
   const float* x_in; float* v_out; float dt; int32_t n_valid;
+  /* GATE_RES + LayerNorm (optional, bf16, N in {128, 256, 384, 512}): with xn_out set, the
+     updated residual rows are also normalised (no-affine LN, eps ln_eps) and modulated for
+     the NEXT projection: xn_out[m][n] = CT(LN(resid[m])[n] * (1 + xs) + xh) with
+     xh = xn_mods[(m/rows_per_mod)*xn_mod_stride + xn_shift_off + n], xs likewise. */
+  void* xn_out; const float* xn_mods; int32_t xn_mod_stride, xn_shift_off, xn_scale_off;
 } mdg_gemm_desc;
 
 int mdg_abi_version(void);
@@ -138,7 +143,8 @@ int mdg_prepare_mask(const mdg_dims* d, const float* mask, void* ws, void* strea
 /* out[n][c] = sum_j x[n][j] Wt[j][c] + bias[c] + base[n][c] + pos[l][c]
                + emb[idx[n]][c] + ipa[b*L + l][c]   (every term but x.Wt optional;
                Wt is the nn.Linear weight transposed, [K][C], so channel reads coalesce)
-   latent_to_emb / cond_to_emb + mask_to_emb + pos_embed (latent_model.py:242-250) */
+   latent_to_emb / cond_to_emb + mask_to_emb + pos_embed (latent_model.py:242-250).
+   K <= 32, C % 4 == 0, C <= 512. */
 int mdg_embed(int32_t N, int32_t T, int32_t L, int32_t C, int32_t K, const float* x,
               const float* Wt, const float* bias, const float* base, const float* pos,
               const float* emb, const int64_t* idx, const float* ipa, float* out, void* stream);
@@ -161,6 +167,7 @@ int mdg_denoise_step(const mdg_model* m, const mdg_step_io* io, const float* mas
 
 /* Building blocks (exposed for unit tests and for the conditioning precompute). */
 int mdg_gemm(const mdg_gemm_desc* g, void* stream);
+/* qkv: CT [n_frames*L][3][H][D] (unpadded q | k | v rows of each token) */
 int mdg_attn_spatial(int32_t dtype, int32_t n_frames, int32_t L, int32_t H, int32_t D,
                      const void* qkv, const float* kvb, const float* mask, void* out,
                      void* stream);

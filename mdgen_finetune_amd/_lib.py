@@ -59,6 +59,7 @@ class MdgGemmDesc(ctypes.Structure):
         ("qkv_layout", _i32), ("qkv_out", _vp), ("H", _i32), ("D", _i32), ("T", _i32), ("L", _i32),
         ("qscale", _f32), ("rope", _vp), ("rope_rows", _i32),
         ("x_in", _vp), ("v_out", _vp), ("dt", _f32), ("n_valid", _i32),
+        ("xn_out", _vp), ("xn_mods", _vp), ("xn_mod_stride", _i32), ("xn_shift_off", _i32), ("xn_scale_off", _i32),
     ]
 
 
@@ -81,7 +82,7 @@ SIGNATURES = [
     ("mdg_attn_temporal", _i32, [_i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
 ]
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 _LIB = None
 
 

@@ -478,6 +478,8 @@ __global__ __launch_bounds__(kTW * 64) void attn_temporal_bf16_kernel(const bf16
 }
 
 
+// Spatial attention over the L residues of one frame (+ the bias key): q|k|v come unpadded,
+// [token][3][H][D] (no MFMA reads them), so each (token, head) thread reads D-element rows.
 template <typename CT>
 __global__ __launch_bounds__(256) void attn_spatial_kernel(const CT* __restrict__ qkv,
                                                            const float* __restrict__ kvb,
@@ -488,12 +490,12 @@ __global__ __launch_bounds__(256) void attn_spatial_kernel(const CT* __restrict_
   const int idx = blockIdx.x * 256 + threadIdx.x;
   if (idx >= nf * L * H) return;
   const int h = idx % H, tok = idx / H, f = tok / L;
-  const size_t tstride = 3ull * H * DP;
+  const size_t tstride = 3ull * H * D;
   float q[DP];
-  const CT* qp = qkv + (size_t)tok * tstride + h * DP;
+  const CT* qp = qkv + (size_t)tok * tstride + h * D;
 #pragma unroll
   for (int d = 0; d < DP; d += 4) {
-    const float4 v = ld4f<CT>(qp + d);
+    const float4 v = (d < D) ? ld4f<CT>(qp + d) : make_float4(0.f, 0.f, 0.f, 0.f);
     q[d] = v.x; q[d + 1] = v.y; q[d + 2] = v.z; q[d + 3] = v.w;
   }
   const float* kbh = kvb + h * 2 * DP;
@@ -507,24 +509,28 @@ __global__ __launch_bounds__(256) void attn_spatial_kernel(const CT* __restrict_
   for (int j = 0; j < L; ++j) {
     const int kt = f * L + j;
     if (mask && mask[kt] == 0.f) continue;
-    const CT* kp = qkv + (size_t)kt * tstride + (size_t)H * DP + h * DP;
-    const CT* vp = kp + (size_t)H * DP;
+    const CT* kp = qkv + (size_t)kt * tstride + (size_t)H * D + h * D;
+    const CT* vp = kp + (size_t)H * D;
     float sc = 0.f;
 #pragma unroll
     for (int d = 0; d < DP; d += 4) {
-      const float4 kv = ld4f<CT>(kp + d);
-      sc += q[d] * kv.x + q[d + 1] * kv.y + q[d + 2] * kv.z + q[d + 3] * kv.w;
+      if (d < D) {
+        const float4 kv = ld4f<CT>(kp + d);
+        sc += q[d] * kv.x + q[d + 1] * kv.y + q[d + 2] * kv.z + q[d + 3] * kv.w;
+      }
     }
     const float mn = fmaxf(m, sc);
     const float a = expf(m - mn), pj = expf(sc - mn);
     lsum = lsum * a + pj;
 #pragma unroll
     for (int d = 0; d < DP; d += 4) {
-      const float4 vv = ld4f<CT>(vp + d);
-      acc[d] = acc[d] * a + pj * vv.x;
-      acc[d + 1] = acc[d + 1] * a + pj * vv.y;
-      acc[d + 2] = acc[d + 2] * a + pj * vv.z;
-      acc[d + 3] = acc[d + 3] * a + pj * vv.w;
+      if (d < D) {
+        const float4 vv = ld4f<CT>(vp + d);
+        acc[d] = acc[d] * a + pj * vv.x;
+        acc[d + 1] = acc[d + 1] * a + pj * vv.y;
+        acc[d + 2] = acc[d + 2] * a + pj * vv.z;
+        acc[d + 3] = acc[d + 3] * a + pj * vv.w;
+      }
     }
     m = mn;
   }
@@ -533,6 +539,103 @@ __global__ __launch_bounds__(256) void attn_spatial_kernel(const CT* __restrict_
 #pragma unroll
   for (int d = 0; d < DP; d += 4)
     if (d < D) st4<CT>(op + d, acc[d] * inv, acc[d + 1] * inv, acc[d + 2] * inv, acc[d + 3] * inv);
+}
+
+// broadcast lane I of every quad (DPP quad_perm(I,I,I,I))
+template <int I>
+__device__ __forceinline__ float quad_bcast(float x) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), I | (I << 2) | (I << 4) | (I << 6), 0xF, 0xF, true));
+}
+template <int I, int DM>
+__device__ __forceinline__ void qscore(const float (&q)[DM], const float (&k)[DM], float kvalid, float (&sc)[4],
+                                       float (&valid)[4]) {
+  float s = 0.f;
+#pragma unroll
+  for (int d = 0; d < DM; ++d) s += q[d] * quad_bcast<I>(k[d]);
+  sc[I] = s;
+  valid[I] = quad_bcast<I>(kvalid);
+}
+template <int I, int DM>
+__device__ __forceinline__ void qpv(const float (&p)[4], const float (&v)[DM], float (&acc)[DM]) {
+#pragma unroll
+  for (int d = 0; d < DM; ++d) acc[d] += p[I] * quad_bcast<I>(v[d]);
+}
+
+// L == 4 (tetrapeptide crop) fast path: one lane per (frame, head, residue), a quad of lanes
+// per (frame, head).  Each lane loads only its own residue's q / k / v rows; the other three
+// residues' k and v reach it by DPP quad broadcasts (no LDS, no redundant loads: the
+// q|k|v buffer is read from HBM exactly once).  fp32 softmax over the 4 keys + the bias key.
+template <typename CT, int DM>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void attn_spatial_quad_kernel(const CT* __restrict__ qkv,
+                                                                const float* __restrict__ kvb,
+                                                                const float* __restrict__ mask,
+                                                                CT* __restrict__ out, int nf, int H, int D) {
+  constexpr int DP = MDG_DP;  // kvb row stride
+  const int idx = blockIdx.x * 256 + threadIdx.x;   // ((f * H + h) * 4 + j); nf*H*4 % 64 == 0 not assumed
+  const int total = nf * H * 4;
+  const bool live = idx < total;
+  const int j = idx & 3, fh = (live ? idx : total - 1) >> 2, h = fh % H, f = fh / H;
+  const int tok = f * 4 + j;
+  const size_t tstride = 3ull * H * D;
+  const CT* base = qkv + (size_t)tok * tstride + h * D;
+  float q[DM], k[DM], v[DM];  // DM = head_dim rounded up to 8 (24 for the default model)
+  // 16-B loads (8 bf16): D % 8 == 0 is checked by the launcher for this kernel
+#pragma unroll
+  for (int d = 0; d < DM; d += 8) {
+    typename V8<CT>::T a = zero8<CT>(), b = a, c = a;
+    if (d < D) {
+      a = ld8<CT>(base + d);
+      b = ld8<CT>(base + (size_t)H * D + d);
+      c = ld8<CT>(base + 2ull * H * D + d);
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      q[d + e] = (float)a[e];
+      k[d + e] = (float)b[e];
+      v[d + e] = (float)c[e];
+    }
+  }
+  const float kvalid = (!mask || mask[tok] != 0.f) ? 1.f : 0.f;
+  const float* kbh = kvb + h * 2 * DP;
+  // bias key first (never masked)
+  float sb = 0.f;
+#pragma unroll
+  for (int d = 0; d < DM; ++d) sb += q[d] * kbh[d];
+  float sc[4], valid[4];
+  qscore<0, DM>(q, k, kvalid, sc, valid);
+  qscore<1, DM>(q, k, kvalid, sc, valid);
+  qscore<2, DM>(q, k, kvalid, sc, valid);
+  qscore<3, DM>(q, k, kvalid, sc, valid);
+  float m = sb;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if (valid[i] != 0.f) m = fmaxf(m, sc[i]);
+  const float pb = expf(sb - m);
+  float lsum = pb, p[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    p[i] = (valid[i] != 0.f) ? expf(sc[i] - m) : 0.f;
+    lsum += p[i];
+  }
+  float acc[DM];
+#pragma unroll
+  for (int d = 0; d < DM; ++d) acc[d] = pb * kbh[DP + d];
+  qpv<0, DM>(p, v, acc);
+  qpv<1, DM>(p, v, acc);
+  qpv<2, DM>(p, v, acc);
+  qpv<3, DM>(p, v, acc);
+  if (!live) return;
+  const float inv = 1.0f / lsum;
+  CT* op = out + (size_t)tok * H * D + h * D;
+#pragma unroll
+  for (int d = 0; d < DM; d += 8) {
+    if (d < D) {
+      typename V8<CT>::T o8;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o8[e] = (CT)(acc[d + e] * inv);
+      *reinterpret_cast<typename V8<CT>::T*>(op + d) = o8;
+    }
+  }
 }
 
 hipError_t attn_temporal_launch(int dtype, int B, int T, int L, int H, int D, const void* qkv_t,
@@ -555,6 +658,19 @@ hipError_t attn_temporal_launch(int dtype, int B, int T, int L, int H, int D, co
 
 hipError_t attn_spatial_launch(int dtype, int nf, int L, int H, int D, const void* qkv,
                                const float* kvb, const float* mask, void* out, hipStream_t s) {
+  if (L == 4 && D % 8 == 0) {
+    dim3 grid((unsigned)(((size_t)nf * H * 4 + 255) / 256));
+#define MDG_QUAD(CTT, DM)                                                                                  \
+  hipLaunchKernelGGL((attn_spatial_quad_kernel<CTT, DM>), grid, dim3(256), 0, s, (const CTT*)qkv, kvb, mask, \
+                     (CTT*)out, nf, H, D)
+    if (dtype == MDG_BF16) {
+      if (D <= 16) MDG_QUAD(bf16_t, 16); else if (D <= 24) MDG_QUAD(bf16_t, 24); else MDG_QUAD(bf16_t, 32);
+    } else {
+      if (D <= 16) MDG_QUAD(float, 16); else if (D <= 24) MDG_QUAD(float, 24); else MDG_QUAD(float, 32);
+    }
+#undef MDG_QUAD
+    return hipGetLastError();
+  }
   const int total = nf * L * H;
   dim3 grid((total + 255) / 256);
   if (dtype == MDG_BF16)

@@ -64,7 +64,7 @@ WsLayout ws_layout(const mdg_dims& d) {
   const size_t N = (size_t)d.B * d.T * d.L;
   WsLayout w;
   size_t off = 0;
-  w.qkv_s = off; off += align256(N * 3 * d.H * MDG_DP * cs);
+  w.qkv_s = off; off += align256(N * 3 * d.H * d.D * cs);
   w.qkv_t = off; off += align256(3ull * d.B * d.L * d.H * d.T * MDG_DP * cs);
   w.o = off;     off += align256(N * d.C * cs);
   w.hid = off;   off += align256(N * d.F * cs);
@@ -163,6 +163,11 @@ int mdg_gemm(const mdg_gemm_desc* g, void* stream) {
     case MDG_EPI_GATE_RES:
       if (!g->resid || g->ldr < g->N || g->ldr % 4) return fail(MDG_E_ARG, "gemm GATE_RES: resid/ldr");
       if (g->gate && g->rows_per_mod <= 0) return fail(MDG_E_ARG, "gemm: rows_per_mod");
+      if (g->xn_out) {
+        if (g->dtype != MDG_BF16 || g->a_mode != MDG_A_PLAIN || !g->xn_mods || g->rows_per_mod <= 0 ||
+            !(g->N == 128 || g->N == 256 || g->N == 384 || g->N == 512) || g->ldr % 2)
+          return fail(MDG_E_SHAPE, "gemm GATE_RES+LN: bf16 PLAIN, N in {128,256,384,512}, xn_mods, rows_per_mod");
+      }
       break;
     case MDG_EPI_QKV:
       if (!g->qkv_out || g->D <= 0 || g->D % 4 || g->D >= MDG_DP || g->N != 3 * g->H * g->D)
@@ -216,7 +221,7 @@ int mdg_embed(int32_t N, int32_t T, int32_t L, int32_t C, int32_t K, const float
               const float* Wt, const float* bias, const float* base, const float* pos,
               const float* emb, const int64_t* idx, const float* ipa, float* out, void* stream) {
   if (!x || !Wt || !out) return fail(MDG_E_ARG, "embed: null x/Wt/out");
-  if (N <= 0 || T <= 0 || L <= 0 || C <= 0 || K <= 0 || K > 64 || N % (T * L))
+  if (N <= 0 || T <= 0 || L <= 0 || C <= 0 || C % 4 || C > 512 || K <= 0 || K > 32 || N % (T * L))
     return fail(MDG_E_SHAPE, "embed: N=%d T=%d L=%d C=%d K=%d", N, T, L, C, K);
   if ((emb == nullptr) != (idx == nullptr)) return fail(MDG_E_ARG, "embed: emb/idx");
   return hip_check(mdg::embed_launch(N, T, L, C, K, x, Wt, bias, base, pos, emb, idx, ipa, out,
@@ -244,11 +249,19 @@ int mdg_final_euler(int32_t dtype, int32_t N, int32_t rows_per_b, int32_t C, int
   return mdg_gemm(&g, stream);
 }
 
-int mdg_layer_fwd(const mdg_dims* d, const mdg_layer_weights* w, const float* rope_l,
-                  const float* rope_t, const float* mods, const float* mask, float* h, void* ws,
-                  void* stream) {
-  if (int e = check_dims(d)) return e;
-  if (!w || !mods || !h || !ws) return fail(MDG_E_ARG, "layer_fwd: null pointer");
+// Where the layer's LayerNorm+modulate inputs come from.  `xn_ready`: the caller already put
+// LN_spatial(h) in the xn workspace (the previous layer's fused fc2 epilogue).  `next_mods`:
+// the fc2 epilogue also produces the NEXT consumer's LN input (next layer's spatial LN, or the
+// FinalLayer's) with shift/scale at next_shift/next_scale of rows of stride next_stride.
+struct LnHandoff {
+  bool xn_ready;
+  const float* next_mods;
+  int next_stride, next_shift, next_scale;
+};
+
+static int layer_fwd_impl(const mdg_dims* d, const mdg_layer_weights* w, const float* rope_l, const float* rope_t,
+                          const float* mods, const float* mask, float* h, void* ws, void* stream,
+                          const LnHandoff& ho) {
   const WsLayout lay = ws_layout(*d);
   char* wsb = (char*)ws;
   const int B = d->B, T = d->T, L = d->L, C = d->C, H = d->H, D = d->D, F = d->F;
@@ -264,6 +277,9 @@ int mdg_layer_fwd(const mdg_dims* d, const mdg_layer_weights* w, const float* ro
   hipStream_t s = (hipStream_t)stream;
   const int TL = T * L, ms = 9 * C;
   // LN + adaLN modulate into the CT activation buffer (latent_model.py:467/475/489)
+  // fused hand-off: the bf16 path with C in {128..512} produces each LN input inside the
+  // preceding gated-residual GEMM (gemm_rowln_kernel); otherwise a stand-alone ln_mod pass
+  const bool fuse = d->dtype == MDG_BF16 && (C == 128 || C == 256 || C == 384 || C == 512);
   auto ln = [&](int shift_off, int scale_off) -> int {
     return hip_check(mdg::ln_mod_launch(d->dtype, N, C, h, mods, ms, TL, shift_off, scale_off, 1e-6f, xn, s),
                      "ln_mod");
@@ -280,7 +296,8 @@ int mdg_layer_fwd(const mdg_dims* d, const mdg_layer_weights* w, const float* ro
   g.H = H; g.D = D; g.T = T; g.L = L;
 
   // ---- spatial attention: x += gate_l * mha_l(mod(LN x))      (latent_model.py:466-472)
-  if (int e = ln(0, C)) return e;
+  if (!(fuse && ho.xn_ready))
+    if (int e = ln(0, C)) return e;
   mdg_gemm_desc q = g;
   q.epi = MDG_EPI_QKV;
   q.N = 3 * C; q.K = C; q.A = xn; q.lda = C; q.W = w->wqkv[0]; q.ldw = C; q.bias = w->bqkv[0];
@@ -292,20 +309,29 @@ int mdg_layer_fwd(const mdg_dims* d, const mdg_layer_weights* w, const float* ro
   r.epi = MDG_EPI_GATE_RES;
   r.N = C; r.K = C; r.A = o; r.lda = C; r.W = w->wo[0]; r.ldw = C; r.bias = w->bo[0];
   r.resid = h; r.ldr = C; r.gate = mods; r.gate_off = 2 * C;
+  if (fuse) {  // + LN_temporal(h) -> xn
+    r.xn_out = xn; r.xn_mods = mods; r.xn_mod_stride = ms; r.xn_shift_off = 3 * C; r.xn_scale_off = 4 * C;
+    r.ln_eps = 1e-6f;
+  }
   if (int e = mdg_gemm(&r, stream)) return e;
 
   // ---- temporal attention: x += gate_t * mha_t(mod(LN x))     (latent_model.py:474-486)
-  if (int e = ln(3 * C, 4 * C)) return e;
+  if (!fuse)
+    if (int e = ln(3 * C, 4 * C)) return e;
   q.W = w->wqkv[1]; q.bias = w->bqkv[1];
   q.qkv_layout = MDG_QKV_TEMPORAL; q.qkv_out = qkv_t; q.qscale = qs * 1.4426950408889634f;
   q.rope = rope_t; q.rope_rows = T + 1;
   if (int e = mdg_gemm(&q, stream)) return e;
   if (int e = mdg_attn_temporal(d->dtype, B, T, L, H, D, qkv_t, kbias, w->kvb[1], o, stream)) return e;
   r.W = w->wo[1]; r.bias = w->bo[1]; r.gate_off = 5 * C;
+  if (fuse) {  // + LN_mlp(h) -> xn
+    r.xn_shift_off = 6 * C; r.xn_scale_off = 7 * C;
+  }
   if (int e = mdg_gemm(&r, stream)) return e;
 
   // ---- MLP: x += gate_m * fc2(gelu(fc1(mod(LN x))))           (latent_model.py:488-491)
-  if (int e = ln(6 * C, 7 * C)) return e;
+  if (!fuse)
+    if (int e = ln(6 * C, 7 * C)) return e;
   mdg_gemm_desc f1 = g;
   f1.epi = MDG_EPI_STORE; f1.act = MDG_ACT_GELU;
   f1.N = F; f1.K = C; f1.A = xn; f1.lda = C; f1.W = w->w1; f1.ldw = C; f1.bias = w->b1;
@@ -315,7 +341,19 @@ int mdg_layer_fwd(const mdg_dims* d, const mdg_layer_weights* w, const float* ro
   f2.epi = MDG_EPI_GATE_RES;
   f2.N = C; f2.K = F; f2.A = hid; f2.lda = F; f2.W = w->w2; f2.ldw = F; f2.bias = w->b2;
   f2.resid = h; f2.ldr = C; f2.gate = mods; f2.gate_off = 8 * C;
+  if (fuse && ho.next_mods) {  // + the next consumer's LN(h) -> xn
+    f2.xn_out = xn; f2.xn_mods = ho.next_mods; f2.xn_mod_stride = ho.next_stride;
+    f2.xn_shift_off = ho.next_shift; f2.xn_scale_off = ho.next_scale; f2.ln_eps = 1e-6f;
+  }
   return mdg_gemm(&f2, stream);
+}
+
+int mdg_layer_fwd(const mdg_dims* d, const mdg_layer_weights* w, const float* rope_l,
+                  const float* rope_t, const float* mods, const float* mask, float* h, void* ws,
+                  void* stream) {
+  if (int e = check_dims(d)) return e;
+  if (!w || !mods || !h || !ws) return fail(MDG_E_ARG, "layer_fwd: null pointer");
+  return layer_fwd_impl(d, w, rope_l, rope_t, mods, mask, h, ws, stream, LnHandoff{false, nullptr, 0, 0, 0});
 }
 
 int mdg_denoise_step(const mdg_model* m, const mdg_step_io* io, const float* mask, void* ws,
@@ -330,16 +368,28 @@ int mdg_denoise_step(const mdg_model* m, const mdg_step_io* io, const float* mas
                         nullptr, nullptr, nullptr, io->ipa, io->h, stream))
     return e;
   const size_t mstride = (size_t)d->B * 9 * d->C;
-  for (int i = 0; i < d->num_layers; ++i)
-    if (int e = mdg_layer_fwd(d, &m->layers[i], m->rope_l, m->rope_t, io->mods + i * mstride, mask,
-                              io->h, ws, stream))
-      return e;
-  // FinalLayer: LN + modulate (layers.py:73) into xn, then the EULER-epilogue GEMM
   const WsLayout lay = ws_layout(*d);
   void* xn = (char*)ws + lay.xn;
-  if (int e = hip_check(mdg::ln_mod_launch(d->dtype, N, d->C, io->h, io->mods_final, 2 * d->C, d->T * d->L, 0,
-                                           d->C, 1e-6f, xn, (hipStream_t)stream), "ln_mod(final)"))
-    return e;
+  const int C = d->C;
+  const bool fuse = d->dtype == MDG_BF16 && (C == 128 || C == 256 || C == 384 || C == 512);
+  if (fuse)  // layer 0's spatial LN input; later ones come out of the fused fc2 epilogues
+    if (int e = hip_check(mdg::ln_mod_launch(d->dtype, N, C, io->h, io->mods, 9 * C, d->T * d->L, 0, C, 1e-6f, xn,
+                                             (hipStream_t)stream), "ln_mod(layer 0)"))
+      return e;
+  for (int i = 0; i < d->num_layers; ++i) {
+    const bool last = i + 1 == d->num_layers;
+    const LnHandoff ho{fuse, last ? io->mods_final : io->mods + (i + 1) * mstride, last ? 2 * C : 9 * C, 0, C};
+    if (!m->layers[i].wqkv[0]) return fail(MDG_E_ARG, "denoise_step: layer %d weights missing", i);
+    if (int e = layer_fwd_impl(d, &m->layers[i], m->rope_l, m->rope_t, io->mods + i * mstride, mask, io->h, ws,
+                               stream, ho))
+      return e;
+  }
+  // FinalLayer: LN + modulate (layers.py:73) into xn (already there on the fused path), then
+  // the EULER-epilogue GEMM
+  if (!fuse)
+    if (int e = hip_check(mdg::ln_mod_launch(d->dtype, N, C, io->h, io->mods_final, 2 * C, d->T * d->L, 0, C, 1e-6f,
+                                             xn, (hipStream_t)stream), "ln_mod(final)"))
+      return e;
   mdg_gemm_desc g;
   memset(&g, 0, sizeof(g));
   g.dtype = d->dtype;

@@ -9,9 +9,13 @@ namespace mdg {
 //             + ipa[b*L + l][c]
 // latent_to_emb / cond_to_emb (nn.Linear, K = 21 or 28) + pos_embed + mask_to_emb
 // (latent_model.py:242-250) + the IPA prepend broadcast over frames (latent_model.py:255).
-// K is tiny, so this is a bandwidth kernel: one thread per (token, 4 channels), float4
-// accesses; the x row is re-read from L1 by the C/4 threads of a token.
-__global__ __launch_bounds__(256) void embed_kernel(int N, int T, int L, int C, int K,
+// HBM-bound (base read + out write dominate).  Thread (c4, g) of a C/4 x 4 block keeps its
+// 4-channel column of W (K x float4) in registers for the whole block and sweeps tokens
+// g, g+4, ... of a 64-token tile whose x rows are staged in LDS (broadcast reads), so global
+// traffic is one coalesced float4 per optional term per output quad.
+constexpr int kEmbedKMax = 32, kEmbedTile = 64;
+
+__global__ __launch_bounds__(512) void embed_kernel(int N, int T, int L, int C, int K,
                                                     const float* __restrict__ x,
                                                     const float* __restrict__ Wt,
                                                     const float* __restrict__ bias,
@@ -21,24 +25,60 @@ __global__ __launch_bounds__(256) void embed_kernel(int N, int T, int L, int C, 
                                                     const int64_t* __restrict__ idx,
                                                     const float* __restrict__ ipa,
                                                     float* __restrict__ out) {
-  const int C4 = C >> 2;
-  const long total = (long)N * C4;
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-    const int n = (int)(i / C4), c = (int)(i - (long)n * C4) * 4;
-    const float* xr = x + (size_t)n * K;
-    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int j = 0; j < K; ++j) {
-      const float xv = xr[j];
-      const float4 w = *reinterpret_cast<const float4*>(Wt + (size_t)j * C + c);
-      a.x += xv * w.x; a.y += xv * w.y; a.z += xv * w.z; a.w += xv * w.w;
+  __shared__ float xs[kEmbedTile * kEmbedKMax];
+  const int C4 = C >> 2, tid = threadIdx.x;
+  const int c4 = tid % C4, g = tid / C4, c = c4 * 4;
+  float4 w[kEmbedKMax];
+#pragma unroll
+  for (int j = 0; j < kEmbedKMax; ++j)
+    w[j] = (j < K) ? *reinterpret_cast<const float4*>(Wt + (size_t)j * C + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+  const float4 bb = bias ? *reinterpret_cast<const float4*>(bias + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int n0 = blockIdx.x * kEmbedTile; n0 < N; n0 += gridDim.x * kEmbedTile) {
+    const int nt = min(kEmbedTile, N - n0);
+    __syncthreads();
+    for (int i = tid; i < nt * K; i += blockDim.x) xs[(i / K) * kEmbedKMax + (i % K)] = x[(size_t)n0 * K + i];
+    __syncthreads();
+    // 4 tokens per pass (rows g, g+4, g+8, g+12 of the tile): their global operands are all
+    // issued before any is consumed
+    for (int r0 = g; r0 < nt; r0 += 16) {
+      float4 a[4], t0[4], t1[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int r = min(r0 + 4 * u, nt - 1), n = n0 + r, l = n % L;
+        t0[u] = base ? *reinterpret_cast<const float4*>(base + (size_t)n * C + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+        t1[u] = ipa ? *reinterpret_cast<const float4*>(ipa + ((size_t)(n / (T * L)) * L + l) * C + c)
+                    : make_float4(0.f, 0.f, 0.f, 0.f);
+        if (pos) {
+          const float4 t = *reinterpret_cast<const float4*>(pos + (size_t)l * C + c);
+          t1[u].x += t.x; t1[u].y += t.y; t1[u].z += t.z; t1[u].w += t.w;
+        }
+        if (emb) {
+          const float4 t = *reinterpret_cast<const float4*>(emb + (size_t)idx[n] * C + c);
+          t1[u].x += t.x; t1[u].y += t.y; t1[u].z += t.z; t1[u].w += t.w;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float* xr = xs + min(r0 + 4 * u, nt - 1) * kEmbedKMax;
+        a[u] = bb;
+#pragma unroll
+        for (int j = 0; j < kEmbedKMax; ++j) {
+          if (j < K) {
+            const float xv = xr[j];
+            a[u].x += xv * w[j].x; a[u].y += xv * w[j].y; a[u].z += xv * w[j].z; a[u].w += xv * w[j].w;
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int r = r0 + 4 * u;
+        if (r < nt) {
+          float4 v = a[u];
+          v.x += t0[u].x + t1[u].x; v.y += t0[u].y + t1[u].y; v.z += t0[u].z + t1[u].z; v.w += t0[u].w + t1[u].w;
+          *reinterpret_cast<float4*>(out + (size_t)(n0 + r) * C + c) = v;
+        }
+      }
     }
-    const int l = n % L;
-    if (bias) { const float4 t = *reinterpret_cast<const float4*>(bias + c); a.x += t.x; a.y += t.y; a.z += t.z; a.w += t.w; }
-    if (base) { const float4 t = *reinterpret_cast<const float4*>(base + (size_t)n * C + c); a.x += t.x; a.y += t.y; a.z += t.z; a.w += t.w; }
-    if (pos) { const float4 t = *reinterpret_cast<const float4*>(pos + (size_t)l * C + c); a.x += t.x; a.y += t.y; a.z += t.z; a.w += t.w; }
-    if (emb) { const float4 t = *reinterpret_cast<const float4*>(emb + (size_t)idx[n] * C + c); a.x += t.x; a.y += t.y; a.z += t.z; a.w += t.w; }
-    if (ipa) { const float4 t = *reinterpret_cast<const float4*>(ipa + ((size_t)(n / (T * L)) * L + l) * C + c); a.x += t.x; a.y += t.y; a.z += t.z; a.w += t.w; }
-    *reinterpret_cast<float4*>(out + (size_t)n * C + c) = a;
   }
 }
 
@@ -164,11 +204,11 @@ __global__ void set_vpad_kernel(CT* v, size_t rows, int D) {
 hipError_t embed_launch(int N, int T, int L, int C, int K, const float* x, const float* Wt,
                         const float* bias, const float* base, const float* pos, const float* emb,
                         const int64_t* idx, const float* ipa, float* out, hipStream_t s) {
-  const long total = (long)N * (C / 4);
-  long grid = (total + 255) / 256;
-  if (grid > 4096) grid = 4096;
-  hipLaunchKernelGGL(embed_kernel, dim3((unsigned)grid), dim3(256), 0, s, N, T, L, C, K, x, Wt, bias,
-                     base, pos, emb, idx, ipa, out);
+  if (K > kEmbedKMax || C % 4 || C > 512) return hipErrorInvalidValue;
+  const int tiles = (N + kEmbedTile - 1) / kEmbedTile;
+  const int grid = tiles < 2048 ? tiles : 2048;
+  hipLaunchKernelGGL(embed_kernel, dim3(grid), dim3(C), 0, s, N, T, L, C, K, x, Wt, bias, base, pos, emb, idx,
+                     ipa, out);
   return hipGetLastError();
 }
 

@@ -99,7 +99,7 @@ __device__ __forceinline__ void epi4(const mdg_gemm_desc& p, int m, int n, float
     }
     CT* dst;
     if (p.qkv_layout == MDG_QKV_SPATIAL) {
-      dst = reinterpret_cast<CT*>(p.qkv_out) + ((size_t)(m * 3 + which) * p.H + head) * MDG_DP + cp;
+      dst = reinterpret_cast<CT*>(p.qkv_out) + ((size_t)(m * 3 + which) * p.H + head) * D + cp;
     } else {
       const int BL = (M / (p.T * p.L)) * p.L, seq = mt * p.L + l;
       dst = reinterpret_cast<CT*>(p.qkv_out) + (size_t)which * BL * p.H * p.T * MDG_DP +
@@ -480,7 +480,7 @@ __device__ __forceinline__ void epi_tile(const mdg_gemm_desc& p, const float* __
     const float invL = 1.0f / (float)p.L, invT = 1.0f / (float)p.T;
     const int BL = (M / (p.T * p.L)) * p.L;
     bf16_t* qo = reinterpret_cast<bf16_t*>(p.qkv_out);
-    const size_t colS = (size_t)(which * p.H + head) * MDG_DP + cp;          // spatial: + m*3*H*DP
+    const size_t colS = (size_t)(which * p.H + head) * D + cp;               // spatial: + m*3*H*D
     const size_t colT = (size_t)which * BL * p.H * p.T * MDG_DP + (size_t)head * p.T * MDG_DP + cp;
 #pragma unroll
     for (int u0 = 0; u0 < RPT; u0 += U) {
@@ -511,7 +511,7 @@ __device__ __forceinline__ void epi_tile(const mdg_gemm_desc& p, const float* __
         }
         size_t off;
         if (spatial) {
-          off = (size_t)m * 3 * p.H * MDG_DP + colS;
+          off = (size_t)m * 3 * p.H * D + colS;
         } else {
           const int ml = fdiv(m, p.L, invL), l = m - ml * p.L;
           const int b = fdiv(ml, p.T, invT), t = ml - b * p.T;
@@ -776,6 +776,231 @@ static hipError_t launch_b8(const mdg_gemm_desc& p, hipStream_t s) {
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------------------
+// Full-row gated residual + LayerNorm: out_proj / fc2 whose epilogue also produces the next
+// projection's normalised, modulated bf16 input, so the stand-alone LN pass (and its 49 MB
+// re-read of h) disappears.  Block = 128 rows x all NCOL output columns (the whole row is in
+// the block, so the LN statistics are exact), 8 waves as 2 x 4 with 64 x NCOL/4 wave tiles,
+// K-step 32, a 4-stage global_load_lds ring with counted vmcnt (one block per CU: the ring
+// depth, not a second block, hides the load latency).  Epilogue in four 32-row bands: the
+// accumulators are staged in LDS, then each wave owns 4 rows: gather h and gate of its rows,
+// h += gate * (acc + bias) (stored), two wave reductions, xn = LN(h)*(1+scale)+shift (bf16).
+constexpr int kRowThreads = 512;
+constexpr int kRowStages = 4;
+
+template <int NCOL>
+__host__ __device__ constexpr size_t rowln_smem() {
+  return (size_t)kRowStages * (128 + NCOL) * 32 * 2;
+}
+
+template <int NCOL>
+__global__ __launch_bounds__(kRowThreads) void gemm_rowln_kernel(const mdg_gemm_desc p) {
+  constexpr int BM = 128, BK = 32, WTN = NCOL / 4, NT = WTN / 16, ATILE = BM * BK, STAGE = (BM + NCOL) * BK;
+  constexpr int LDS_ST = NCOL + 4, NE = NCOL / 128;  // float2 column pairs per lane per row
+  constexpr int WLD = NCOL / 128;                    // W glds instructions per wave per stage
+  static_assert(NCOL % 128 == 0 && NCOL <= 512, "NCOL");
+  static_assert(32 * LDS_ST * 4 <= kRowStages * STAGE * 2, "band stage fits the ring");
+  typedef __attribute__((address_space(3))) void* lds_ptr_t;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  bf16_t* lds = reinterpret_cast<bf16_t*>(smem);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int M = p.M, K = p.K;
+  // XCD-aware order of the row tiles (neighbouring tiles share nothing but W, which every
+  // XCD's L2 holds anyway; the remap keeps consecutive tiles on one XCD for the h / gate rows)
+  const int nwg = (M + BM - 1) / BM;
+  const int xcd = blockIdx.x & 7, loc = blockIdx.x >> 3, q = nwg >> 3, r8 = nwg & 7;
+  const int m0 = ((xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + loc) * BM;
+
+  // 64-B tile rows: chunk c of row r at c ^ ((-(r >> 2)) & 3)
+  const bf16_t* A = reinterpret_cast<const bf16_t*>(p.A);
+  const bf16_t* W = reinterpret_cast<const bf16_t*>(p.W);
+  const int arow = 16 * wave + (lane >> 2);
+  const bf16_t* asrc = A + (size_t)min(m0 + arow, M - 1) * p.lda + (((lane & 3) ^ ((-(arow >> 2)) & 3)) * 8);
+  const bf16_t* bsrc[WLD];
+#pragma unroll
+  for (int i = 0; i < WLD; ++i) {
+    const int row = 16 * (wave * WLD + i) + (lane >> 2);
+    bsrc[i] = W + (size_t)row * p.ldw + (((lane & 3) ^ ((-(row >> 2)) & 3)) * 8);
+  }
+#define MDG_ROW_LOAD(stage_, k0_)                                                                   \
+  {                                                                                                 \
+    bf16_t* sa = lds + (stage_) * STAGE;                                                            \
+    __builtin_amdgcn_global_load_lds((const void*)(asrc + (k0_)), (lds_ptr_t)(sa + 16 * wave * BK), 16, 0, 0); \
+    _Pragma("unroll") for (int i = 0; i < WLD; ++i)                                                 \
+      __builtin_amdgcn_global_load_lds((const void*)(bsrc[i] + (k0_)),                              \
+                                       (lds_ptr_t)(sa + ATILE + 16 * (wave * WLD + i) * BK), 16, 0, 0); \
+  }
+
+  f32x4 acc[4][NT];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = K / BK;
+#pragma unroll
+  for (int s0 = 0; s0 < kRowStages - 1; ++s0)
+    if (s0 < nk) MDG_ROW_LOAD(s0, s0 * BK);
+  const int swz = (-(lr >> 2)) & 3;
+  for (int kt = 0; kt < nk; ++kt) {
+    // stage kt landed: leave the (up to 2) younger stages' loads in flight
+    const int younger = min(kRowStages - 2, nk - 1 - kt);
+    if (younger >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (1 + WLD)) : "memory");
+    else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(1 + WLD) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (kt + kRowStages - 1 < nk) MDG_ROW_LOAD((kt + kRowStages - 1) % kRowStages, (kt + kRowStages - 1) * BK);
+    const bf16_t* As = lds + (kt % kRowStages) * STAGE;
+    const bf16_t* Bs = As + ATILE;
+    const int ch = (lg ^ swz) * 8;
+    bf16x8 a[4], b[NT];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[i] = *reinterpret_cast<const bf16x8*>(As + (wm * 64 + i * 16 + lr) * BK + ch);
+#pragma unroll
+    for (int j = 0; j < NT; ++j) b[j] = *reinterpret_cast<const bf16x8*>(Bs + (wn * WTN + j * 16 + lr) * BK + ch);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+  }
+#undef MDG_ROW_LOAD
+
+  // ------------------------------------------------------------------ epilogue
+  float* stage = reinterpret_cast<float*>(smem);
+  const float inv_rpm = 1.0f / (float)p.rows_per_mod, invN = 1.0f / (float)NCOL;
+  float2 bb[NE];
+#pragma unroll
+  for (int e = 0; e < NE; ++e)
+    bb[e] = p.bias ? *reinterpret_cast<const float2*>(p.bias + 2 * lane + 128 * e) : make_float2(0.f, 0.f);
+  __syncthreads();  // all waves are done with the ring
+#pragma unroll 1
+  for (int band = 0; band < 4; ++band) {
+    if (wm == (band >> 1)) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {  // compile-time acc index; the band selects 2 of the 4
+        if ((i >> 1) != (band & 1)) continue;
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            stage[((i & 1) * 16 + lg * 4 + r) * LDS_ST + wn * WTN + j * 16 + lr] = acc[i][j][r];
+      }
+    }
+    __syncthreads();
+    // wave -> rows 4*wave .. 4*wave+3 of the band; every global operand of the 4 rows is
+    // gathered before use and the 4 rows' reductions run interleaved (independent chains)
+    float2 hv[4][NE], gv[4][NE];
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int m = min(m0 + band * 32 + wave * 4 + rr, M - 1);
+      const float* hr = p.resid + (size_t)m * p.ldr;
+      const float* gr = p.gate ? p.gate + (size_t)fdiv(m, p.rows_per_mod, inv_rpm) * p.mod_stride + p.gate_off : nullptr;
+#pragma unroll
+      for (int e = 0; e < NE; ++e) {
+        const int k = 2 * lane + 128 * e;
+        hv[rr][e] = *reinterpret_cast<const float2*>(hr + k);
+        gv[rr][e] = gr ? *reinterpret_cast<const float2*>(gr + k) : make_float2(1.f, 1.f);
+      }
+    }
+    const int mb0 = min(m0 + band * 32 + wave * 4, M - 1), mb3 = min(mb0 + 3, M - 1);
+    const int b0 = fdiv(mb0, p.rows_per_mod, inv_rpm);
+    const bool one_b = fdiv(mb3, p.rows_per_mod, inv_rpm) == b0;  // the 4 rows share a batch entry
+    float2 xs[NE], xh[NE];
+    if (p.xn_out) {
+      const float* mr = p.xn_mods + (size_t)b0 * p.xn_mod_stride;
+#pragma unroll
+      for (int e = 0; e < NE; ++e) {
+        const int k = 2 * lane + 128 * e;
+        xs[e] = *reinterpret_cast<const float2*>(mr + p.xn_scale_off + k);
+        xh[e] = *reinterpret_cast<const float2*>(mr + p.xn_shift_off + k);
+      }
+    }
+    float sum[4];
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const float* srow = stage + (wave * 4 + rr) * LDS_ST;
+      float s = 0.f;
+#pragma unroll
+      for (int e = 0; e < NE; ++e) {
+        const float2 v = *reinterpret_cast<const float2*>(srow + 2 * lane + 128 * e);
+        hv[rr][e].x += gv[rr][e].x * (v.x + bb[e].x);
+        hv[rr][e].y += gv[rr][e].y * (v.y + bb[e].y);
+        s += hv[rr][e].x + hv[rr][e].y;
+      }
+      sum[rr] = s;
+      const int m = m0 + band * 32 + wave * 4 + rr;
+      if (m < M) {
+#pragma unroll
+        for (int e = 0; e < NE; ++e) *reinterpret_cast<float2*>(p.resid + (size_t)m * p.ldr + 2 * lane + 128 * e) = hv[rr][e];
+      }
+    }
+    if (p.xn_out) {
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) sum[rr] += __shfl_xor(sum[rr], o, 64);
+      float ss[4];
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        sum[rr] *= invN;  // mean
+        float t = 0.f;
+#pragma unroll
+        for (int e = 0; e < NE; ++e) {
+          const float a0 = hv[rr][e].x - sum[rr], a1 = hv[rr][e].y - sum[rr];
+          t += a0 * a0 + a1 * a1;
+        }
+        ss[rr] = t;
+      }
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) ss[rr] += __shfl_xor(ss[rr], o, 64);
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int m = m0 + band * 32 + wave * 4 + rr;
+        if (m >= M) continue;
+        const float rs = 1.0f / sqrtf(ss[rr] * invN + p.ln_eps);
+        if (!one_b) {  // rows straddle a batch boundary: this row's own shift / scale
+          const float* mr = p.xn_mods + (size_t)fdiv(m, p.rows_per_mod, inv_rpm) * p.xn_mod_stride;
+#pragma unroll
+          for (int e = 0; e < NE; ++e) {
+            const int k = 2 * lane + 128 * e;
+            xs[e] = *reinterpret_cast<const float2*>(mr + p.xn_scale_off + k);
+            xh[e] = *reinterpret_cast<const float2*>(mr + p.xn_shift_off + k);
+          }
+        }
+#pragma unroll
+        for (int e = 0; e < NE; ++e) {
+          const int k = 2 * lane + 128 * e;
+          typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+          bf16x2 pr;
+          pr[0] = (bf16_t)((hv[rr][e].x - sum[rr]) * rs * (1.0f + xs[e].x) + xh[e].x);
+          pr[1] = (bf16_t)((hv[rr][e].y - sum[rr]) * rs * (1.0f + xs[e].y) + xh[e].y);
+          *reinterpret_cast<bf16x2*>(reinterpret_cast<bf16_t*>(p.xn_out) + (size_t)m * NCOL + k) = pr;
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+template <int NCOL>
+static hipError_t launch_rowln(const mdg_gemm_desc& p, hipStream_t s) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_rowln_kernel<NCOL>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)rowln_smem<NCOL>());
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((gemm_rowln_kernel<NCOL>), dim3((p.M + 127) / 128), dim3(kRowThreads), rowln_smem<NCOL>(), s, p);
+  return hipGetLastError();
+}
+
 template <typename CT, int BM, int BN, int WM, int AMODE>
 static size_t smem_bytes(int K) {
   constexpr int BK = 64, VEC = 16 / sizeof(CT), LDT = BK + VEC;
@@ -793,7 +1018,7 @@ static bool stage_fits() {
   return stage <= room;
 }
 
-constexpr int kCfgB4 = 100, kCfgB8 = 101, kCfgB4K32 = 102;
+constexpr int kCfgB4 = 100, kCfgB8 = 101, kCfgB4K32 = 102, kCfgRow = 103;
 
 struct GemmPlan {
   int cfg;  // index into the config table below; -1 = unsupported
@@ -861,7 +1086,15 @@ GemmPlan gemm_plan(const mdg_gemm_desc& p) {
   const bool big = p.M >= 128 * 128;
   int cfg = -1;
   if (bf && ln) cfg = (p.N % 128 == 0) ? (big ? 0 : 2) : (p.N % 32 == 0 ? (big ? 1 : 3) : -1);
-  else if (bf && p.N % kB4Tile == 0 && p.K % 64 == 0 && p.lda % 8 == 0 && p.ldw % 8 == 0) {
+  else if (bf && p.epi == MDG_EPI_GATE_RES && p.xn_out && p.K % 64 == 0 && p.lda % 8 == 0 && p.ldw % 8 == 0 &&
+           (p.N == 128 || p.N == 256 || p.N == 384 || p.N == 512)) {
+    g.cfg = kCfgRow;  // full-row gated residual + LayerNorm
+    g.smem = p.N == 128 ? rowln_smem<128>() : p.N == 256 ? rowln_smem<256>() : p.N == 384 ? rowln_smem<384>()
+                                                                                        : rowln_smem<512>();
+    g.bm = 128;
+    g.bn = p.N;
+    return g;
+  } else if (bf && p.N % kB4Tile == 0 && p.K % 64 == 0 && p.lda % 8 == 0 && p.ldw % 8 == 0) {
     // MDG_GEMM_TILE=256 / 64 select the 256x128 3-stage kernel / the 128x128 K-step-64 kernel
     // (tuning knob); default: 128x128 with K-step 32 at four blocks per CU
     static const int forced = [] {
@@ -901,6 +1134,14 @@ GemmPlan gemm_plan(const mdg_gemm_desc& p) {
 }
 
 hipError_t gemm_launch(const mdg_gemm_desc& p, const GemmPlan& g, hipStream_t s) {
+  if (g.cfg == kCfgRow) {
+    switch (p.N) {
+      case 128: return launch_rowln<128>(p, s);
+      case 256: return launch_rowln<256>(p, s);
+      case 384: return launch_rowln<384>(p, s);
+      default: return launch_rowln<512>(p, s);
+    }
+  }
   if (g.cfg == kCfgB8) {
     switch (p.epi) {
       case MDG_EPI_STORE: return launch_b8<MDG_EPI_STORE>(p, s);

@@ -89,6 +89,34 @@ def test_gemm_lnmod_gate_res(lib, dt):
     torch.testing.assert_close(resid, ref, rtol=rtol, atol=atol * 10)
 
 
+@pytest.mark.parametrize("N,K,M", [(384, 384, 300), (384, 1536, 4000), (128, 256, 257), (512, 512, 130)])
+def test_gemm_gate_res_fused_layernorm(lib, N, K, M):
+    """bf16 full-row gated residual + next-LN epilogue (gemm_rowln_kernel): h and xn vs torch."""
+    from mdgen_finetune_amd import _lib
+
+    TL = 100
+    g = torch.Generator(device="cuda").manual_seed(N + K + M)
+    A = torch.randn(M, K, device="cuda", generator=g).to(torch.bfloat16)
+    W = (torch.randn(N, K, device="cuda", generator=g) / math.sqrt(K)).to(torch.bfloat16)
+    bias = torch.randn(N, device="cuda", generator=g)
+    nb = (M + TL - 1) // TL
+    mods = torch.randn(nb, 9 * N, device="cuda", generator=g) * 0.5
+    nmods = torch.randn(nb, 2 * N, device="cuda", generator=g) * 0.5
+    resid = torch.randn(M, N, device="cuda", generator=g) * 2
+    r0 = resid.clone()
+    xn = torch.zeros(M, N, device="cuda", dtype=torch.bfloat16)
+    d = _desc(dtype=1, a_mode=0, epi=1, M=M, N=N, K=K, A=A.data_ptr(), lda=K, W=W.data_ptr(), ldw=K,
+              bias=bias.data_ptr(), mods=mods.data_ptr(), mod_stride=9 * N, rows_per_mod=TL, resid=resid.data_ptr(),
+              ldr=N, gate=mods.data_ptr(), gate_off=8 * N, ln_eps=1e-6, xn_out=xn.data_ptr(), xn_mods=nmods.data_ptr(),
+              xn_mod_stride=2 * N, xn_shift_off=0, xn_scale_off=N)
+    _lib.check(lib.mdg_gemm(ctypes.byref(d), _s()), "mdg_gemm")
+    b = torch.arange(M, device="cuda") // TL
+    href = r0 + mods[b, 8 * N:9 * N] * (A.float() @ W.float().T + bias)
+    torch.testing.assert_close(resid, href, rtol=2e-3, atol=2e-3)
+    xref = _ln_mod(resid, nmods, TL, 0, N, N)  # LN of the kernel's own h: isolates the epilogue LN
+    torch.testing.assert_close(xn.float(), xref, rtol=2e-2, atol=2e-2)
+
+
 def _rope_ref(x, pos, inv_freq):
     # x [..., D] at integer positions pos [...]
     half = x.shape[-1] // 2
@@ -116,7 +144,7 @@ def test_gemm_qkv_rope_layouts(lib, dt, layout):
     table = torch.cat([f.cos().reshape(-1), f.sin().reshape(-1)]).cuda()
     qs = 0.2
     if layout == 0:
-        out = torch.zeros(M, 3, H, 32, device="cuda", dtype=CT[dt])
+        out = torch.zeros(M, 3, H, D, device="cuda", dtype=CT[dt])     # unpadded spatial layout
     else:
         out = torch.zeros(3, B * L, H, T, 32, device="cuda", dtype=CT[dt])
     # the kernel contract: q/k head rows pair-interleaved (row 2i = dim i, 2i+1 = dim i + D/2)
@@ -141,7 +169,7 @@ def test_gemm_qkv_rope_layouts(lib, dt, layout):
     q, k = q[..., within.cuda()], k[..., within.cuda()]           # stored interleaved
     ref = torch.stack([q, k, v], 3)                               # [B,T,L,3,H,D]
     if layout == 0:
-        got = out.float().reshape(B, T, L, 3, H, 32)
+        got = out.float().reshape(B, T, L, 3, H, D)
     else:
         got = out.float().reshape(3, B, L, H, T, 32).permute(1, 4, 2, 0, 3, 5)
     rtol, atol = _tol(dt)
@@ -195,14 +223,13 @@ def test_attn_temporal(lib, dt, T):
 
 
 @pytest.mark.parametrize("dt", ["f32", "bf16"])
-def test_attn_spatial(lib, dt):
+@pytest.mark.parametrize("L,D", [(5, 24), (4, 24), (4, 16)])   # L == 4: DPP quad kernel
+def test_attn_spatial(lib, dt, L, D):
     from mdgen_finetune_amd import _lib
 
-    NF, L, H, D = 50, 5, 16, 24
+    NF, H = 50, 16
     g = torch.Generator(device="cuda").manual_seed(1)
-    qkv = torch.zeros(NF * L, 3, H, 32, device="cuda")
-    qkv[..., :D] = torch.randn(NF * L, 3, H, D, device="cuda", generator=g)
-    qkv = qkv.to(CT[dt])
+    qkv = torch.randn(NF * L, 3, H, D, device="cuda", generator=g).to(CT[dt])   # unpadded [token][3][H][D]
     mask = torch.ones(NF, L, device="cuda")
     mask[::3, 2] = 0
     mask[1::7, :] = 0
@@ -211,7 +238,7 @@ def test_attn_spatial(lib, dt):
     out = torch.zeros(NF * L, H * D, device="cuda", dtype=CT[dt])
     _lib.check(lib.mdg_attn_spatial(ENUM[dt], NF, L, H, D, qkv.data_ptr(), kvb.data_ptr(), mask.data_ptr(),
                                     out.data_ptr(), _s()), "attn_spatial")
-    qf = qkv.float().reshape(NF, L, 3, H, 32)
+    qf = qkv.float().reshape(NF, L, 3, H, D)
     got = out.float().reshape(NF, L, H, D)
     for h in range(H):
         ref = _attn_ref(qf[:, :, 0, h, :D], qf[:, :, 1, h, :D], qf[:, :, 2, h, :D], kvb[h, 0, :D], kvb[h, 1, :D],
