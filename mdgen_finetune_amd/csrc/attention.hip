@@ -566,7 +566,7 @@ __device__ __forceinline__ void qpv(const float (&p)[4], const float (&v)[DM], f
 // residues' k and v reach it by DPP quad broadcasts (no LDS, no redundant loads: the
 // q|k|v buffer is read from HBM exactly once).  fp32 softmax over the 4 keys + the bias key.
 template <typename CT, int DM>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void attn_spatial_quad_kernel(const CT* __restrict__ qkv,
+__global__ __launch_bounds__(256) void attn_spatial_quad_kernel(const CT* __restrict__ qkv,
                                                                 const float* __restrict__ kvb,
                                                                 const float* __restrict__ mask,
                                                                 CT* __restrict__ out, int nf, int H, int D) {
