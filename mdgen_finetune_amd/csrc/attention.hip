@@ -22,6 +22,8 @@
 #include "../../include/mdgen_hip.h"
 #include "common.h"
 
+#include <stdlib.h>
+
 namespace mdg {
 
 
@@ -387,9 +389,8 @@ __device__ __forceinline__ void ta_store(const f32x16& o, bf16_t* out, int q, in
   }
 }
 
-constexpr int kTW = 8;    // waves per block
-constexpr int kTKC = 128; // keys per LDS chunk
 
+template <int kTW, int kTKC>  // waves per block, keys per LDS chunk
 __global__ __launch_bounds__(kTW * 64) void attn_temporal_bf16_kernel(const bf16_t* __restrict__ qkv,
                                                                     const float* __restrict__ kbias,
                                                                     const float* __restrict__ kvb,
@@ -400,7 +401,7 @@ __global__ __launch_bounds__(kTW * 64) void attn_temporal_bf16_kernel(const bf16
   __shared__ __attribute__((aligned(16))) bf16_t Ks[2][KC * DP];
   __shared__ __attribute__((aligned(16))) bf16_t Vs[2][KC * DP];
   __shared__ float kbs[2][KC];
-  __shared__ int kflag[2][2];
+  __shared__ int kflag[2][KC / 64];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
@@ -461,11 +462,14 @@ __global__ __launch_bounds__(kTW * 64) void attn_temporal_bf16_kernel(const bf16
   for (int c = 0; c < nchunks; ++c) {
     const int cur = c & 1;
     if (c + 1 < nchunks) MDG_TA_GLOAD(c + 1);
-    const bool masked = (kflag[cur][0] | kflag[cur][1]) != 0;
+    int mflag = 0;
+#pragma unroll
+    for (int f = 0; f < KC / 64; ++f) mflag |= kflag[cur][f];
+    const bool masked = mflag != 0;
     const bf16_t* Kc = Ks[cur];
     const bf16_t* Vc = Vs[cur];
 #pragma unroll
-    for (int sub = 0; sub < 2; ++sub)
+    for (int sub = 0; sub < KC / 64; ++sub)
       ta_subchunk(Kc + sub * 64 * DP, Vc + sub * 64 * DP, kbs[cur] + sub * 64, masked, r, h, grow, gcol, padS, padH,
                   padJ, qf, mt, o);
     if (c + 1 < nchunks) MDG_TA_LSTORE(cur ^ 1);
@@ -641,9 +645,20 @@ __global__ __launch_bounds__(256) void attn_spatial_quad_kernel(const CT* __rest
 hipError_t attn_temporal_launch(int dtype, int B, int T, int L, int H, int D, const void* qkv_t,
                                 const float* kbias, const float* kvb, void* out, hipStream_t s) {
   if (dtype == MDG_BF16) {
-    dim3 grid((unsigned)((T + kTW * 32 - 1) / (kTW * 32) * H * B * L));
-    hipLaunchKernelGGL(attn_temporal_bf16_kernel, grid, dim3(kTW * 64), 0, s, (const bf16_t*)qkv_t, kbias,
-                       kvb, (bf16_t*)out, T, L, H, D, B * L);
+    // MDG_ATTN_WAVES=4 selects 4-wave blocks with 64-key chunks (tuning knob; default 8 / 128)
+    static const int waves = [] {
+      const char* e = getenv("MDG_ATTN_WAVES");
+      return e ? atoi(e) : 8;
+    }();
+    if (waves == 4) {
+      dim3 grid((unsigned)((T + 127) / 128 * H * B * L));
+      hipLaunchKernelGGL((attn_temporal_bf16_kernel<4, 64>), grid, dim3(256), 0, s, (const bf16_t*)qkv_t, kbias, kvb,
+                         (bf16_t*)out, T, L, H, D, B * L);
+    } else {
+      dim3 grid((unsigned)((T + 255) / 256 * H * B * L));
+      hipLaunchKernelGGL((attn_temporal_bf16_kernel<8, 128>), grid, dim3(512), 0, s, (const bf16_t*)qkv_t, kbias, kvb,
+                         (bf16_t*)out, T, L, H, D, B * L);
+    }
     return hipGetLastError();
   }
   dim3 grid((T + 127) / 128, H, B * L);
