@@ -359,6 +359,72 @@ class HipEngine:
                 self._capture(gs, st)
         return gs.states.clone()
 
+    # ------------------------------------------------------------------ adaptive solvers
+    @torch.no_grad()
+    def velocity_field(self, x_like, mask=None, start_frames=None, end_frames=None, x_cond=None, x_cond_mask=None,
+                       aatype=None, use_graph=True):
+        """f(t, y) -> v = model(y, ones(B)·t, **kw) for an adaptive solver (dopri5): t is a
+        device scalar, y a [B,T,L,latent] device tensor.  Everything but (t, y) is staged once;
+        each evaluation is ONE hipGraph replay of [conditioning at t (t-embedding, adaLN, IPA
+        prepend), base embedding, mask bias, mdg_denoise_step] reading t and y from static
+        buffers, so no host sync happens inside an evaluation."""
+        B, T, L, mask, rots, trans, erots, etrans, aa = self._inputs(x_like, mask, start_frames, end_frames, aatype)
+        st = self._state(B, T, L)
+        self._prepare_tps(rots, trans, erots, etrans)
+        dev = self.model.device
+        vs = _ShapeState()
+        vs.x = torch.empty(B, T, L, self.lat, device=dev)
+        vs.v = torch.empty_like(vs.x)
+        vs.t = torch.zeros(1, B, device=dev)
+        vs.mask = mask.clone()
+        vs.graph = None
+        for name, val in (("rots", rots), ("trans", trans), ("erots", erots), ("etrans", etrans), ("aatype", aa)):
+            self._copy_opt(vs, name, val)
+        if self._rel7 is not None:
+            self._copy_opt(vs, "rel7f", self._rel7[0])
+            self._copy_opt(vs, "rel7r", self._rel7[1])
+            vs.rel7 = (vs.rel7f, vs.rel7r)
+        else:
+            vs.rel7 = None
+        vs.has_cond = x_cond is not None
+        if vs.has_cond:
+            self._copy_opt(vs, "x_cond", x_cond.float())
+            self._copy_opt(vs, "x_cond_mask", x_cond_mask.to(torch.int64))
+        vs.graph = None
+
+        def program():
+            s = _lib.stream_handle()
+            self._rel7 = vs.rel7
+            mods, mods_f, ipa = self.conditioning(vs.t, vs.mask, vs.rots, vs.trans, getattr(vs, "erots", None),
+                                                  getattr(vs, "etrans", None), getattr(vs, "aatype", None))
+            vs.cond = (mods, mods_f, ipa)
+            self._base(st, vs.x_cond if vs.has_cond else None, vs.x_cond_mask if vs.has_cond else None)
+            _lib.check(self.lib.mdg_prepare_mask(ctypes.byref(st.dims), vs.mask.data_ptr(), st.ws.data_ptr(), s),
+                       "mdg_prepare_mask")
+            vs.io = self._step_io(st, vs.x.data_ptr(), None, vs.v.data_ptr(),
+                                  None if ipa is None else ipa[0].data_ptr(), mods[0].data_ptr(),
+                                  mods_f[0].data_ptr(), 0.0)
+            _lib.check(self.lib.mdg_denoise_step(ctypes.byref(st.model_struct), ctypes.byref(vs.io),
+                                                 vs.mask.data_ptr(), st.ws.data_ptr(), s), "mdg_denoise_step")
+
+        def f(t, y):
+            vs.x.copy_(y)
+            vs.t.copy_(torch.as_tensor(t, device=dev).float().reshape(1, 1).expand(1, B))
+            if vs.graph is not None:
+                vs.graph.replay()
+            else:
+                program()
+                if use_graph:
+                    g = torch.cuda.CUDAGraph()
+                    torch.cuda.synchronize()
+                    with torch.cuda.graph(g):
+                        program()
+                    vs.graph = g
+            return vs.v.clone()
+
+        f.state = vs
+        return f
+
     def _copy_opt(self, gs, name, val):
         if val is None:
             setattr(gs, name, None)

@@ -142,15 +142,39 @@ class Sampler:
         self.drift = transport.get_drift()
 
     def sample_ode(self, *, sampling_method="dopri5", num_steps=50, atol=1e-6, rtol=1e-3, reverse=False):
-        if sampling_method != "euler":
-            raise NotImplementedError(
-                f"sampling_method={sampling_method!r}: only the fixed-grid 'euler' solver is built "
-                "(dopri5 is the next row of SURVEY §8f); pass --sampling_method euler")
+        """transport.py:407-450 + integrators.py:74-114: 'euler' (fixed grid of num_steps points)
+        or 'dopri5' (adaptive, num_steps saved points; integrators.odeint_dopri5)."""
+        if sampling_method not in ("euler", "dopri5"):
+            raise NotImplementedError(f"sampling_method={sampling_method!r}: the reference offers "
+                                      "'dopri5' and 'euler' (parsing.py:102)")
         t0, t1 = self.transport.check_interval(self.transport.train_eps, self.transport.sample_eps,
                                                sde=False, eval=True, reverse=reverse)
         drift = self.drift
         if reverse:
             drift = lambda x, t, model, **kw: self.drift(x, th.ones_like(t) * (1 - t), model, **kw)  # noqa: E731
+
+        if sampling_method == "dopri5":
+            def _sample_dopri5(x, model, **model_kwargs):
+                hip = None if (reverse or model_kwargs) else _hip_model_of(model)
+                if hip is not None:  # each evaluation = one hipGraph replay (HipEngine.velocity_field)
+                    m, kw = hip
+                    from ..engine import get_engine
+
+                    mask = kw.get("mask")
+                    if mask is not None and mask.dim() == 2:
+                        mask = mask.repeat(x.shape[0], 1, 1)
+                    fn = get_engine(m).velocity_field(
+                        x, mask=mask, start_frames=kw.get("start_frames"), end_frames=kw.get("end_frames"),
+                        x_cond=kw.get("x_cond"), x_cond_mask=kw.get("x_cond_mask"), aatype=kw.get("aatype"))
+                else:
+                    def fn(t, y):  # integrators.py:98-101
+                        return drift(y, th.ones(y.size(0)).to(y.device) * t, model, **model_kwargs)
+                from .integrators import odeint_dopri5
+
+                ts = th.linspace(t0, t1, num_steps).to(x.device)
+                return odeint_dopri5(fn, x, ts, rtol=rtol, atol=atol)
+
+            return _sample_dopri5
 
         def _sample(x, model, **model_kwargs):
             hip = None if (reverse or model_kwargs or (t0, t1) != (0, 1)) else _hip_model_of(model)

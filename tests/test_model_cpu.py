@@ -103,8 +103,3 @@ def test_unsupported_flags_raise():
             LatentMDGenModel(a, 21)
 
 
-def test_dopri5_is_refused_loudly():
-    from mdgen_finetune_amd.transport import Sampler, create_transport
-
-    with pytest.raises(NotImplementedError):
-        Sampler(create_transport(None, "GVP")).sample_ode(sampling_method="dopri5")
