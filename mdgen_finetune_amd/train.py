@@ -1,0 +1,219 @@
+"""Data-parallel trainer: the drop-in for the reference's ``src/train.py`` (a Lightning
+``Trainer.fit`` over ``NewMDGenWrapper``), rebuilt as one process per GPU.
+
+    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \
+        -m mdgen_finetune_amd.train --sim_condition --prepend_ipa --abs_pos_emb \
+        --num_frames 1000 --crop 4 --batch_size 8 --synthetic
+
+Per optimizer step (train.py:46-60 + wrapper.py:78-173 semantics):
+  * each rank draws its own ``batch_size`` items (DistributedSampler shard of the epoch's
+    permutation) and computes the GVP flow-matching loss (wrapper.general_step);
+  * backward through ``DistributedDataParallel``: gradients are averaged over ranks by
+    bucketed all-reduces that RCCL runs over xGMI while backward is still producing the
+    earlier layers' gradients (``bucket_cap_mb``; static graph, buckets as grad views);
+  * ``accumulate_grad`` micro-batches per step (the non-final ones under ``no_sync``, loss
+    divided by the count as Lightning does);
+  * global grad-norm clip (``grad_clip``, Lightning's default 'norm' algorithm), Adam/AdamW,
+    then the EMA update (on_before_zero_grad);
+  * every ``print_freq`` steps the logs are gathered from all ranks (wrapper.py:22-44) and
+    rank 0 prints their means; every ``ckpt_freq`` epochs rank 0 writes a Lightning-layout
+    checkpoint to MODEL_DIR (checkpoint.py).
+Resuming (``--ckpt``) restores weights, optimizer, EMA, epoch and step.
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import time
+from collections import defaultdict
+
+import numpy as np
+import torch
+import torch.distributed as dist
+from torch.nn.parallel import DistributedDataParallel as DDP
+
+from .checkpoint import load_checkpoint, model_state_dict, save_checkpoint
+from .data import SyntheticMDDataset, collate
+from .parsing import parse_train_args
+from .wrapper import NewMDGenWrapper
+
+
+def gather_log(log, world_size):
+    """wrapper.py:22-29."""
+    if world_size == 1:
+        return log
+    out = [None] * world_size
+    dist.all_gather_object(out, log)
+    merged = defaultdict(list)
+    for lg in out:
+        for k, v in lg.items():
+            merged[k].extend(v)
+    return dict(merged)
+
+
+def get_log_mean(log):
+    """wrapper.py:31-43 (numeric entries only)."""
+    out = {}
+    for k, v in log.items():
+        try:
+            out[k] = float(np.nanmean(v))
+        except (TypeError, ValueError):
+            pass
+    return out
+
+
+def setup_distributed():
+    """Rank/world from the torch.distributed.run environment; RCCL on GPUs, gloo on CPU."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    use_cuda = torch.cuda.is_available()
+    device = torch.device("cuda", local) if use_cuda else torch.device("cpu")
+    if use_cuda:
+        torch.cuda.set_device(device)
+    if world > 1 and not dist.is_initialized():
+        dist.init_process_group("nccl" if use_cuda else "gloo", rank=rank, world_size=world,
+                                **({"device_id": device} if use_cuda else {}))
+    return rank, world, device
+
+
+class Trainer:
+    def __init__(self, args, rank=0, world=1, device=None, dataset=None):
+        self.args, self.rank, self.world = args, rank, world
+        self.device = device or torch.device("cpu")
+        torch.manual_seed(args.seed)  # identical initial weights on every rank
+        self.wrapper = NewMDGenWrapper(args).to(self.device)
+        self.wrapper.model.backend = "torch"  # autograd path (HIP backward: DESIGN.md §7)
+        torch.manual_seed(args.seed + 1 + 1000 * rank)  # independent (t, x0) draws per rank
+        self.model = self.wrapper.model
+        if world > 1:
+            self.model = DDP(self.wrapper.model, device_ids=[self.device.index] if self.device.type == "cuda" else None,
+                             bucket_cap_mb=args.bucket_cap_mb, gradient_as_bucket_view=True, static_graph=True)
+        self.optimizer = self.wrapper.configure_optimizers()
+        self.epoch, self.global_step = 0, 0
+        if dataset is None:
+            if not args.synthetic:
+                raise NotImplementedError("only --synthetic data is available offline (the reference's "
+                                          "MDGenDataset needs the gs://mdgen-public trajectories)")
+            dataset = SyntheticMDDataset(args.num_frames, args.crop, size=args.synthetic_size, seed=args.seed)
+        self.dataset = dataset
+        self.sampler = torch.utils.data.DistributedSampler(dataset, num_replicas=world, rank=rank, shuffle=True,
+                                                           seed=args.seed, drop_last=True)
+        self.loader = torch.utils.data.DataLoader(dataset, batch_size=args.batch_size, sampler=self.sampler,
+                                                  num_workers=0, collate_fn=collate, drop_last=True)
+        if args.ckpt:
+            self.resume(args.ckpt)
+
+    # ------------------------------------------------------------------ checkpoint
+    def resume(self, path):
+        ck = load_checkpoint(path, map_location=self.device)
+        self.wrapper.model.load_state_dict(model_state_dict(ck))
+        if ck.get("optimizer_states"):
+            self.optimizer.load_state_dict(ck["optimizer_states"][0])
+        if self.wrapper.ema is not None and "ema" in ck:
+            self.wrapper.ema.load_state_dict(ck["ema"])
+            self.wrapper.ema.to(self.device)
+        self.epoch, self.global_step = int(ck["epoch"]) + 1, int(ck["global_step"])
+
+    def save(self):
+        if self.rank != 0:
+            return None
+        path = os.path.join(self.args.model_dir, f"epoch={self.epoch}-step={self.global_step}.ckpt")
+        save_checkpoint(path, self.wrapper, self.optimizer, self.epoch, self.global_step)
+        return path
+
+    # ------------------------------------------------------------------ one optimizer step
+    def _to_device(self, batch):
+        return {k: (v.to(self.device, non_blocking=True) if torch.is_tensor(v) else v) for k, v in batch.items()}
+
+    def step(self, micro_batches):
+        """One optimizer step over ``len(micro_batches)`` accumulated micro-batches; returns the
+        mean loss (rank-local) and the global grad norm before clipping."""
+        a = self.args
+        n = len(micro_batches)
+        self.wrapper.train()
+        losses = []
+        autocast = (torch.autocast(self.device.type, dtype=torch.bfloat16) if a.precision.startswith("bf16")
+                    else torch.autocast(self.device.type, enabled=False))
+        for i, batch in enumerate(micro_batches):
+            batch = self._to_device(batch)
+            sync = (i == n - 1) or self.world == 1
+            ctx = self.model.no_sync() if (not sync and isinstance(self.model, DDP)) else _null()
+            with ctx:
+                with autocast:
+                    loss = self.wrapper.general_step(batch, "train", model=self.model)
+                (loss / n).backward()
+            losses.append(loss.detach())
+        gnorm = torch.nn.utils.clip_grad_norm_(self.wrapper.model.parameters(), a.grad_clip) if a.grad_clip else None
+        self.optimizer.step()
+        self.wrapper.on_before_zero_grad()
+        self.optimizer.zero_grad(set_to_none=True)
+        self.global_step += 1
+        return torch.stack(losses).mean(), gnorm
+
+    def print_log(self, prefix="iter"):
+        """wrapper.py:132-165."""
+        w = self.wrapper
+        log = {k: v for k, v in w._log.items() if k.startswith(prefix + "_")}
+        log = gather_log(log, self.world)
+        mean = get_log_mean(log)
+        mean.update(epoch=self.epoch, trainer_step=self.global_step, iter_step=w.iter_step,
+                    lr=self.optimizer.param_groups[0]["lr"])
+        if self.rank == 0:
+            print(json.dumps(mean), flush=True)
+        for k in list(w._log):
+            if k.startswith(prefix + "_"):
+                del w._log[k]
+        return mean
+
+    def fit(self):
+        a = self.args
+        acc = max(1, a.accumulate_grad)
+        while self.epoch < a.epochs:
+            self.sampler.set_epoch(self.epoch)
+            pending = []
+            for bi, batch in enumerate(self.loader):
+                if a.train_batches is not None and bi >= a.train_batches:
+                    break
+                pending.append(batch)
+                if len(pending) < acc:
+                    continue
+                self.step(pending)
+                pending = []
+                if self.global_step % a.print_freq == 0:
+                    self.print_log("iter")
+                if a.max_steps is not None and self.global_step >= a.max_steps:
+                    self.save()
+                    return
+            self.print_log("train")
+            if (self.epoch + 1) % a.ckpt_freq == 0:
+                self.save()
+            self.epoch += 1
+
+
+class _null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        return False
+
+
+def main(argv=None):
+    args = parse_train_args(argv)
+    rank, world, device = setup_distributed()
+    if device.type == "cuda":
+        torch.set_float32_matmul_precision("medium")  # train.py:13
+    tr = Trainer(args, rank, world, device)
+    t0 = time.time()
+    tr.fit()
+    if rank == 0:
+        print(json.dumps({"done": True, "steps": tr.global_step, "wall_s": round(time.time() - t0, 2)}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:])

@@ -222,8 +222,49 @@ def state_dict_case(name, flags, latent_dim, tps):
     save(name, dict(name=name, flags=flags, latent_dim=latent_dim, tps=tps), {}, {"keys": keys, "shapes": shapes})
 
 
+def prep_batch_case(name, B, T, L, seed):
+    """wrapper.py:283-365 on a synthetic trajectory batch.  The offsets come from the
+    reference's own get_offsets (utils.py:7-14) on its Rigid/Rotation (rot_to_quat via eigh);
+    the remaining glue (sign fix 309, masks 311-350, x_cond 362) is evaluated with the same
+    tensor expressions as the reference (wrapper.py is not importable: it needs Lightning)."""
+    from mdgen.rigid_utils import Rigid, Rotation
+    from mdgen.utils import get_offsets
+    from mdgen_finetune_amd.data import SyntheticMDDataset, collate
+
+    ds = SyntheticMDDataset(T, L, size=B, seed=seed, n_pad=1)
+    batch = collate([ds[i] for i in range(B)])
+    batch["torsion_mask"][0, 0, 3] = 1.0
+    inp = {k: batch[k].numpy() for k in ("torsions", "torsion_mask", "trans", "rots", "seqres", "mask")}
+    rigids = Rigid(trans=batch["trans"], rots=Rotation(rot_mats=batch["rots"]))
+    out = {}
+    for tps in (False, True):
+        offsets = get_offsets(rigids[:, 0:1], rigids)
+        offsets[..., :4] *= torch.where(offsets[:, :, :, 0:1] < 0, -1, 1)
+        frame_loss_mask = batch["mask"].unsqueeze(-1).expand(-1, -1, 7)
+        torsion_loss_mask = batch["torsion_mask"].unsqueeze(-1).expand(-1, -1, -1, 2).reshape(B, L, 14)
+        if tps:
+            offsets_r = get_offsets(rigids[:, -1:], rigids)
+            offsets_r[..., :4] *= torch.where(offsets_r[:, :, :, 0:1] < 0, -1, 1)
+            offsets = torch.cat([offsets, offsets_r], -1)
+            frame_loss_mask = torch.cat([frame_loss_mask, frame_loss_mask], -1)
+        latents = torch.cat([offsets, batch["torsions"].view(B, T, L, 14)], -1)
+        loss_mask = torch.cat([frame_loss_mask, torsion_loss_mask], -1).unsqueeze(1).expand(-1, T, -1, -1)
+        cond_mask = torch.zeros(B, T, L, dtype=int)
+        cond_mask[:, 0] = 1
+        if tps:
+            cond_mask[:, -1] = 1
+        sfx = "_tps" if tps else ""
+        out["latents" + sfx] = latents
+        out["loss_mask" + sfx] = loss_mask
+        out["cond_mask" + sfx] = cond_mask
+    save(name, dict(name=name, B=B, T=T, L=L, seed=seed), inp, out)
+
+
 def main():
     torch.set_num_threads(8)
+    if sys.argv[1:] == ["prep_batch"]:
+        prep_batch_case("prep_batch", B=2, T=12, L=5, seed=51)
+        return
     state_dict_case("state_dict_sim", [], 21, False)
     state_dict_case("state_dict_tps", [], 28, True)
     forward_case("small_sim_T1", SMALL, 21, B=2, T=1, L=4, seed=11, intermediates=True)
@@ -235,6 +276,7 @@ def main():
     forward_case("full_tps_T100", [], 28, B=1, T=100, L=4, seed=23, tps=True)
     loss_case("small_loss", SMALL, B=3, T=8, L=4, seed=31)
     mha_case("mha_rope_biaskv", seed=41)
+    prep_batch_case("prep_batch", B=2, T=12, L=5, seed=51)
 
 
 if __name__ == "__main__":

@@ -1,0 +1,179 @@
+"""Training path on the CPU: prep_batch against the reference's golden offsets, the
+single-process trainer (steps, EMA, checkpoint round trip in the Lightning layout), and the
+data-parallel path at world_size 2 over gloo (DDP's bucketed all-reduce must equal the mean of
+the ranks' local gradients; replicas stay bit-identical after the optimizer step)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+SMALL = ["--synthetic", "--sim_condition", "--prepend_ipa", "--abs_pos_emb", "--num_frames", "8", "--crop", "4",
+         "--embed_dim", "32", "--mha_heads", "4", "--num_layers", "2", "--ipa_heads", "2", "--ipa_head_dim", "8",
+         "--ipa_qk", "4", "--ipa_v", "4", "--batch_size", "2", "--synthetic_size", "8", "--print_freq", "1000"]
+
+
+def _args(extra=(), tmp=None):
+    from mdgen_finetune_amd.parsing import parse_train_args
+
+    argv = list(SMALL) + list(extra)
+    if tmp is not None:
+        argv += ["--model_dir", str(tmp)]
+    return parse_train_args(argv)
+
+
+def _batch(args, B=2, seed=0):
+    from mdgen_finetune_amd.data import SyntheticMDDataset, collate
+
+    ds = SyntheticMDDataset(args.num_frames, args.crop, size=B, seed=seed)
+    return collate([ds[i] for i in range(B)])
+
+
+def test_prep_batch_matches_reference_golden(golden):
+    """Offsets/sign fix/cond mask/x_cond vs the reference's get_offsets (utils.py:7-14) and the
+    prep_batch glue (wrapper.py:283-365) — tests/golden/prep_batch.npz, oracle/gen_golden.py."""
+    from mdgen_finetune_amd.wrapper import NewMDGenWrapper
+
+    d, cfg = golden("prep_batch")
+    for tps in (False, True):
+        extra = ["--tps_condition"] if tps else []
+        a = _args(extra)
+        a.sim_condition = not tps
+        w = NewMDGenWrapper(a)
+        batch = {k[3:]: torch.from_numpy(d[k]) for k in d.files if k.startswith("in_")}
+        p = w.prep_batch(batch)
+        sfx = "_tps" if tps else ""
+        np.testing.assert_allclose(p["latents"].numpy(), d["out_latents" + sfx], rtol=0, atol=2e-6)
+        np.testing.assert_array_equal(p["loss_mask"].numpy(), d["out_loss_mask" + sfx])
+        np.testing.assert_array_equal(p["model_kwargs"]["x_cond_mask"].numpy(), d["out_cond_mask" + sfx])
+
+
+def test_trainer_steps_ema_and_checkpoint_roundtrip(tmp_path):
+    from mdgen_finetune_amd.checkpoint import load_checkpoint, load_from_checkpoint
+    from mdgen_finetune_amd.train import Trainer
+
+    a = _args(["--ema", "--ema_decay", "0.9", "--max_steps", "3", "--epochs", "1"], tmp_path)
+    tr = Trainer(a)
+    w0 = {k: v.clone() for k, v in tr.wrapper.model.state_dict().items()}
+    tr.fit()
+    assert tr.global_step == 3
+    changed = [k for k, v in tr.wrapper.model.state_dict().items() if not torch.equal(v, w0[k])]
+    assert len(changed) > 10
+    ema = tr.wrapper.ema.state_dict()["params"]
+    k = "layers.0.mha_t.attn.q_proj.weight"
+    assert not torch.equal(ema[k], tr.wrapper.model.state_dict()[k])
+    files = sorted(os.listdir(tmp_path))
+    assert files and files[-1].endswith(".ckpt")
+    ck = load_checkpoint(os.path.join(tmp_path, files[-1]))
+    assert set(ck) >= {"state_dict", "hyper_parameters", "optimizer_states", "ema", "epoch", "global_step"}
+    assert all(key.startswith("model.") for key in ck["state_dict"])
+    w2 = load_from_checkpoint(os.path.join(tmp_path, files[-1]))
+    for key, v in tr.wrapper.model.state_dict().items():
+        assert torch.equal(v, w2.model.state_dict()[key]), key
+    assert torch.equal(w2.ema.state_dict()["params"][k], ema[k])
+    # resume continues the step counter and the optimizer state
+    a2 = _args(["--ema", "--max_steps", "4", "--epochs", "2", "--ckpt", os.path.join(tmp_path, files[-1])], tmp_path)
+    tr2 = Trainer(a2)
+    assert tr2.global_step == 3 and len(tr2.optimizer.state) > 0
+    tr2.fit()
+    assert tr2.global_step == 4
+
+
+def test_loss_decreases_on_fixed_batch():
+    from mdgen_finetune_amd.train import Trainer
+
+    a = _args(["--lr", "1e-3"])
+    tr = Trainer(a)
+    b = _batch(a)
+    torch.manual_seed(0)
+    first = [tr.step([b])[0].item() for _ in range(3)]
+    for _ in range(30):
+        tr.step([b])
+    last = [tr.step([b])[0].item() for _ in range(3)]
+    assert np.mean(last) < np.mean(first)
+
+
+def test_grad_accumulation_equals_big_batch():
+    """accumulate_grad=2 over two halves == one step over the whole batch (same noise)."""
+    from mdgen_finetune_amd.train import Trainer
+
+    a = _args(["--grad_clip", "0"])
+    b = _batch(a, B=4)
+    halves = [{k: (v[:2] if torch.is_tensor(v) else v[:2]) for k, v in b.items()},
+              {k: (v[2:] if torch.is_tensor(v) else v[2:]) for k, v in b.items()}]
+    grads = []
+    for mb in ([b], halves):
+        tr = Trainer(a)
+        noise = torch.Generator().manual_seed(5)
+        x0 = torch.randn(4, 8, 4, 21, generator=noise)
+        t = torch.rand(4, generator=noise)
+        it = iter([(t[:2], x0[:2]), (t[2:], x0[2:])] if len(mb) == 2 else [(t, x0)])
+        tr.wrapper.transport.sample = lambda x1, it=it: (lambda tx: (tx[0], tx[1], x1))(next(it))
+        seen = []
+        orig = tr.optimizer.step
+        tr.optimizer.step = lambda *a_, **k_: (seen.append(torch.cat([p.grad.flatten().clone() for p in
+                                                                      tr.wrapper.model.parameters()
+                                                                      if p.grad is not None])), orig())[1]
+        tr.step(mb)
+        grads.append(seen[0])
+    torch.testing.assert_close(grads[0], grads[1], rtol=1e-5, atol=1e-6)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _ddp_worker(rank, world, port, out):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from mdgen_finetune_amd.train import Trainer, setup_distributed
+
+    r, w, dev = setup_distributed()
+    a = _args(["--grad_clip", "0", "--bucket_cap_mb", "1"])
+    tr = Trainer(a, r, w, dev)
+    b = _batch(a, B=2, seed=100 + rank)
+    # local gradient without communication, from the same (t, x0) draw
+    g = torch.Generator().manual_seed(7 + rank)
+    x0, t = torch.randn(2, 8, 4, 21, generator=g), torch.rand(2, generator=g)
+    tr.wrapper.transport.sample = lambda x1: (t, x0, x1)
+    prep = tr.wrapper.prep_batch(b)
+    loss = tr.wrapper.transport.training_losses(tr.wrapper.model, prep["latents"], mask=prep["loss_mask"],
+                                                model_kwargs=prep["model_kwargs"])["loss"].mean()
+    local = torch.autograd.grad(loss, [p for p in tr.wrapper.model.parameters()], allow_unused=True)
+    local = torch.cat([(x if x is not None else torch.zeros_like(p)).flatten()
+                       for x, p in zip(local, tr.wrapper.model.parameters())])
+    ref = local.clone()
+    dist.all_reduce(ref)
+    ref /= w
+    # the DDP path (bucketed all-reduce during backward)
+    loss = tr.wrapper.general_step(b, model=tr.model)
+    loss.backward()
+    ddp = torch.cat([(p.grad if p.grad is not None else torch.zeros_like(p)).flatten()
+                     for p in tr.wrapper.model.parameters()])
+    tr.optimizer.step()
+    params = torch.cat([p.detach().flatten() for p in tr.wrapper.model.parameters()])
+    gathered = [torch.zeros_like(params) for _ in range(w)]
+    dist.all_gather(gathered, params)
+    out[rank] = (float((ddp - ref).abs().max()), float(ref.abs().max()),
+                 float((gathered[0] - gathered[1]).abs().max()), float((local - ref).abs().max()))
+    dist.destroy_process_group()
+
+
+def test_ddp_world2_gloo_allreduce_matches_local_mean():
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_ddp_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    for r in range(2):
+        err, scale, drift, spread = out[r]
+        assert err <= 1e-6 * max(1.0, scale), (r, err, scale)
+        assert drift == 0.0
+        assert spread > 0.0  # the ranks really had different data
