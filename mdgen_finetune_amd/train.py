@@ -127,6 +127,7 @@ class Trainer:
     def _to_device(self, batch):
         return {k: (v.to(self.device, non_blocking=True) if torch.is_tensor(v) else v) for k, v in batch.items()}
 
+    @torch.enable_grad()
     def step(self, micro_batches):
         """One optimizer step over ``len(micro_batches)`` accumulated micro-batches; returns the
         mean loss (rank-local) and the global grad norm before clipping."""
