@@ -137,7 +137,9 @@ size_t mdg_workspace_bytes(const mdg_dims* d);
    output), kbias (temporal key-padding bias).  For profiling / tests; 0 on success. */
 int mdg_workspace_offsets(const mdg_dims* d, size_t offsets[6]);
 int mdg_workspace_init(const mdg_dims* d, void* ws, void* stream);
-/* key-padding additive bias for the temporal attention from mask [B,T,L] (0 -> -inf) */
+/* key-padding additive biases from mask [B,T,L] (0 -> -inf): the temporal one ([B*L][T],
+   region kbias) and the spatial one ([B*T][L], after kbias; used when L >= 16, where the
+   spatial attention runs on the MFMA temporal kernel with one sequence per frame) */
 int mdg_prepare_mask(const mdg_dims* d, const float* mask, void* ws, void* stream);
 
 /* out[n][c] = sum_j x[n][j] Wt[j][c] + bias[c] + base[n][c] + pos[l][c]

@@ -25,7 +25,7 @@ hipError_t attn_spatial_launch(int dtype, int nf, int L, int H, int D, const voi
 hipError_t embed_launch(int N, int T, int L, int C, int K, const float* x, const float* W,
                         const float* bias, const float* base, const float* pos, const float* emb,
                         const int64_t* idx, const float* ipa, float* out, hipStream_t s);
-hipError_t mask_bias_launch(int B, int T, int L, const float* mask, float* kbias, hipStream_t s);
+hipError_t mask_bias_launch(int B, int T, int L, const float* mask, float* kbias, float* kbias_s, hipStream_t s);
 hipError_t ln_mod_launch(int dtype, int M, int C, const float* h, const float* mods, int mod_stride,
                          int rows_per_mod, int shift_off, int scale_off, float eps, void* xn,
                          hipStream_t s);
@@ -55,8 +55,11 @@ int hip_check(hipError_t e, const char* what) {
 size_t ct_size(int dtype) { return dtype == MDG_BF16 ? 2 : 4; }
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
+// residue counts from which the spatial attention runs on the MFMA (temporal) kernel
+constexpr int kSpatialMfmaMinL = 16;
+
 struct WsLayout {
-  size_t qkv_s, qkv_t, o, hid, xn, kbias, total;
+  size_t qkv_s, qkv_t, o, hid, xn, kbias, kbias_s, total;
 };
 
 WsLayout ws_layout(const mdg_dims& d) {
@@ -70,6 +73,7 @@ WsLayout ws_layout(const mdg_dims& d) {
   w.hid = off;   off += align256(N * d.F * cs);
   w.xn = off;    off += align256(N * d.C * cs);
   w.kbias = off; off += align256((size_t)d.B * d.L * d.T * sizeof(float));
+  w.kbias_s = off; off += align256(N * sizeof(float));
   w.total = off;
   return w;
 }
@@ -133,7 +137,7 @@ int mdg_prepare_mask(const mdg_dims* d, const float* mask, void* ws, void* strea
   if (!mask || !ws) return fail(MDG_E_ARG, "null mask/workspace");
   const WsLayout w = ws_layout(*d);
   return hip_check(mdg::mask_bias_launch(d->B, d->T, d->L, mask, (float*)((char*)ws + w.kbias),
-                                         (hipStream_t)stream),
+                                         (float*)((char*)ws + w.kbias_s), (hipStream_t)stream),
                    "mask_bias");
 }
 
@@ -301,10 +305,21 @@ static int layer_fwd_impl(const mdg_dims* d, const mdg_layer_weights* w, const f
   mdg_gemm_desc q = g;
   q.epi = MDG_EPI_QKV;
   q.N = 3 * C; q.K = C; q.A = xn; q.lda = C; q.W = w->wqkv[0]; q.ldw = C; q.bias = w->bqkv[0];
-  q.qkv_layout = MDG_QKV_SPATIAL; q.qkv_out = qkv_s; q.qscale = qs;
   q.rope = rope_l; q.rope_rows = L + 1;
-  if (int e = mdg_gemm(&q, stream)) return e;
-  if (int e = mdg_attn_spatial(d->dtype, B * T, L, H, D, qkv_s, w->kvb[0], mask, o, stream)) return e;
+  if (L >= kSpatialMfmaMinL && (size_t)B * T <= 65535) {
+    // long residue axis (ATLAS crop 256): every frame is one attention sequence of L tokens;
+    // the temporal MFMA kernel runs it with (B', T', L') = (B*T, L, 1) — same token order
+    q.qkv_layout = MDG_QKV_TEMPORAL; q.qkv_out = qkv_t; q.qscale = qs * 1.4426950408889634f;
+    q.T = L; q.L = 1;
+    if (int e = mdg_gemm(&q, stream)) return e;
+    q.T = T; q.L = L;
+    const float* kbias_s = (const float*)(wsb + lay.kbias_s);
+    if (int e = mdg_attn_temporal(d->dtype, B * T, L, 1, H, D, qkv_t, kbias_s, w->kvb[0], o, stream)) return e;
+  } else {
+    q.qkv_layout = MDG_QKV_SPATIAL; q.qkv_out = qkv_s; q.qscale = qs;
+    if (int e = mdg_gemm(&q, stream)) return e;
+    if (int e = mdg_attn_spatial(d->dtype, B * T, L, H, D, qkv_s, w->kvb[0], mask, o, stream)) return e;
+  }
   mdg_gemm_desc r = g;
   r.epi = MDG_EPI_GATE_RES;
   r.N = C; r.K = C; r.A = o; r.lda = C; r.W = w->wo[0]; r.ldw = C; r.bias = w->bo[0];

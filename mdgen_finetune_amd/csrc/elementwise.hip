@@ -187,11 +187,13 @@ __global__ __launch_bounds__(256) void ln_mod_kernel(int M, int C, const float* 
 // kbias[b*L + l][t] = 0 where mask[b][t][l] != 0 else -inf  (key_padding_mask = 1 - mask,
 // latent_model.py:336, masked_fill(-inf) mha.py:370-376)
 __global__ void mask_bias_kernel(int B, int T, int L, const float* __restrict__ mask,
-                                 float* __restrict__ kbias) {
+                                 float* __restrict__ kbias, float* __restrict__ kbias_s) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= B * T * L) return;
   const int l = i % L, t = (i / L) % T, b = i / (T * L);
-  kbias[((size_t)b * L + l) * T + t] = (mask[i] != 0.f) ? 0.f : -INFINITY;
+  const float v = (mask[i] != 0.f) ? 0.f : -INFINITY;
+  kbias[((size_t)b * L + l) * T + t] = v;  // temporal sequences (b, l) over t
+  kbias_s[i] = v;                          // spatial sequences (b, t) over l
 }
 
 // 1.0 in pad column D of every temporal V row (softmax row sum rides in it).
@@ -229,9 +231,10 @@ hipError_t ln_mod_launch(int dtype, int M, int C, const float* h, const float* m
   return hipGetLastError();
 }
 
-hipError_t mask_bias_launch(int B, int T, int L, const float* mask, float* kbias, hipStream_t s) {
+hipError_t mask_bias_launch(int B, int T, int L, const float* mask, float* kbias, float* kbias_s,
+                            hipStream_t s) {
   const int n = B * T * L;
-  hipLaunchKernelGGL(mask_bias_kernel, dim3((n + 255) / 256), dim3(256), 0, s, B, T, L, mask, kbias);
+  hipLaunchKernelGGL(mask_bias_kernel, dim3((n + 255) / 256), dim3(256), 0, s, B, T, L, mask, kbias, kbias_s);
   return hipGetLastError();
 }
 

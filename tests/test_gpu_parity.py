@@ -209,3 +209,21 @@ def test_dopri5_solve_matches_cpu_solve(dtype):
     st = Dopri5Stats()
     I.odeint_dopri5(f, zs.cuda(), torch.linspace(0, 1, 50), stats=st)
     assert st.accepted > 0
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("T,L,n_pad", [(16, 256, 51), (40, 24, 3), (8, 16, 0)])
+def test_long_residue_axis_atlas_matches_oracle(T, L, n_pad, dtype):
+    """ATLAS shape (BASELINE config 5: crop 256, ~20% padded residues): L >= 16 routes the
+    spatial attention through the MFMA kernel with one sequence per frame (capi.hip
+    kSpatialMfmaMinL); T is cut so the CPU oracle finishes in seconds."""
+    inp, ref, cfg = _oracle_full(T, seed=17, B=1, n_pad=n_pad, L=L)
+    m, _ = build_model(cfg, "cuda", T=T)
+    m.hip_dtype = dtype
+    from mdgen_finetune_amd.rigid_utils import Rigid, Rotation
+
+    g = lambda k: torch.from_numpy(inp[k]).cuda()  # noqa: E731
+    with torch.no_grad():
+        v = m(g("x"), g("t"), g("mask"), start_frames=Rigid(Rotation(rot_mats=g("rots")), g("trans")),
+              x_cond=g("x_cond"), x_cond_mask=g("x_cond_mask"), aatype=g("aatype"))
+    _check(v, ref, dtype)
