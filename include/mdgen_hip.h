@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define MDG_ABI_VERSION 4
+#define MDG_ABI_VERSION 5
 #define MDG_MAX_LAYERS 16
 #define MDG_DP 32 /* padded head dim of every attention operand buffer (head_dim <= 31) */
 
@@ -178,6 +178,25 @@ int mdg_attn_spatial(int32_t dtype, int32_t n_frames, int32_t L, int32_t H, int3
 int mdg_attn_temporal(int32_t dtype, int32_t B, int32_t T, int32_t L, int32_t H, int32_t D,
                       const void* qkv_t, const float* kbias, const float* kvb, void* out,
                       void* stream);
+
+/* Batch preparation (NewMDGenWrapper.prep_batch, wrapper.py:283-365 with get_offsets,
+   utils.py:7-14, and rot_to_quat, rigid_utils.py:191-210), per token (b, t, l):
+     latents[n] = [ q, t of frame0^-1 . frame(n) (q sign-fixed to real part >= 0)
+                    | TPS: the same relative to frame T-1 | torsions[n] (7 x (cos, sin)) ]
+     x_cond[n]  = latents[n] where the token's frame is conditioned, else 0 (null = skip)
+     cond_mask[n] = 1 / 0 (int64, null = skip)
+   rots [B,T,L,3,3], trans [B,T,L,3], torsions [B,T,L,7,2] (null = zeros) fp32;
+   latent must be 21 (sim) or 28 (MDG_PREP_TPS).  cond_interval > 0 also conditions every
+   cond_interval-th frame (--cond_interval). */
+enum {
+  MDG_PREP_TPS = 1,          /* --tps_condition: offsets to the last frame appended */
+  MDG_PREP_NO_OFFSETS = 2,   /* --no_offsets: absolute 7-vector instead of offsets to frame 0 */
+  MDG_PREP_COND_FIRST = 4,   /* condition frame 0 (--sim_condition, --tps_condition) */
+  MDG_PREP_COND_LAST = 8,    /* condition frame T-1 (--tps_condition) */
+};
+int mdg_prep_latents(int32_t B, int32_t T, int32_t L, int32_t latent, int32_t flags, int32_t cond_interval,
+                     const float* rots, const float* trans, const float* torsions, float* latents,
+                     float* x_cond, int64_t* cond_mask, void* stream);
 
 #ifdef __cplusplus
 }

@@ -19,6 +19,7 @@ MDG_A_PLAIN, MDG_A_LNMOD = 0, 1
 MDG_EPI_STORE, MDG_EPI_GATE_RES, MDG_EPI_QKV, MDG_EPI_EULER = 0, 1, 2, 3
 MDG_ACT_NONE, MDG_ACT_GELU, MDG_ACT_SILU = 0, 1, 2
 MDG_QKV_SPATIAL, MDG_QKV_TEMPORAL = 0, 1
+MDG_PREP_TPS, MDG_PREP_NO_OFFSETS, MDG_PREP_COND_FIRST, MDG_PREP_COND_LAST = 1, 2, 4, 8
 MDG_MAX_LAYERS = 16
 MDG_DP = 32
 
@@ -80,9 +81,10 @@ SIGNATURES = [
     ("mdg_gemm", _i32, [ctypes.POINTER(MdgGemmDesc), _vp]),
     ("mdg_attn_spatial", _i32, [_i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
     ("mdg_attn_temporal", _i32, [_i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
+    ("mdg_prep_latents", _i32, [_i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
 ]
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 _LIB = None
 
 

@@ -30,6 +30,9 @@ hipError_t ln_mod_launch(int dtype, int M, int C, const float* h, const float* m
                          int rows_per_mod, int shift_off, int scale_off, float eps, void* xn,
                          hipStream_t s);
 hipError_t set_vpad_launch(int dtype, void* v, size_t rows, int D, hipStream_t s);
+hipError_t prep_latents_launch(int B, int T, int L, int lat, int tps, int no_offsets, int cond_mode,
+                               int cond_interval, const float* rots, const float* trans, const float* torsions,
+                               float* latents, float* x_cond, int64_t* cond_mask, hipStream_t s);
 }  // namespace mdg
 
 namespace {
@@ -415,6 +418,22 @@ int mdg_denoise_step(const mdg_model* m, const mdg_step_io* io, const float* mas
   g.out = io->x_out; g.ldo = d->latent; g.x_in = io->x_in; g.v_out = io->v_out; g.dt = io->dt;
   g.n_valid = d->latent;
   return mdg_gemm(&g, stream);
+}
+
+int mdg_prep_latents(int32_t B, int32_t T, int32_t L, int32_t latent, int32_t flags, int32_t cond_interval,
+                     const float* rots, const float* trans, const float* torsions, float* latents,
+                     float* x_cond, int64_t* cond_mask, void* stream) {
+  if (!rots || !trans || !latents) return fail(MDG_E_ARG, "prep_latents: null rots/trans/latents");
+  if (B <= 0 || T <= 0 || L <= 0) return fail(MDG_E_SHAPE, "prep_latents: B,T,L = %d,%d,%d", B, T, L);
+  const int tps = (flags & MDG_PREP_TPS) ? 1 : 0;
+  if (latent != (tps ? 28 : 21))
+    return fail(MDG_E_SHAPE, "prep_latents: latent %d != %d (offsets + 14 torsion channels)", latent, tps ? 28 : 21);
+  if (flags & ~(MDG_PREP_TPS | MDG_PREP_NO_OFFSETS | MDG_PREP_COND_FIRST | MDG_PREP_COND_LAST) || cond_interval < 0)
+    return fail(MDG_E_ARG, "prep_latents: flags 0x%x / cond_interval %d", flags, cond_interval);
+  return hip_check(mdg::prep_latents_launch(B, T, L, latent, tps, (flags & MDG_PREP_NO_OFFSETS) ? 1 : 0, flags,
+                                            cond_interval, rots, trans, torsions, latents, x_cond, cond_mask,
+                                            (hipStream_t)stream),
+                   "prep_latents");
 }
 
 }  // extern "C"

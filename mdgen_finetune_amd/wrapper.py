@@ -41,6 +41,30 @@ def get_offsets(ref_frame: Rigid, rigids: Rigid) -> torch.Tensor:
     return ref_frame.invert().compose(rigids).to_tensor_7()
 
 
+def prep_latents_hip(rots, trans, torsions, tps=False, no_offsets=False, cond_first=True, cond_last=False,
+                     cond_interval=0):
+    """latents / x_cond / cond_mask of prep_batch in one HIP launch (mdg_prep_latents): the
+    relative frames, quaternions (eigenvector of K, sign-fixed) and torsions per token."""
+    from . import _lib
+
+    lib = _lib.load()
+    B, T, L = trans.shape[:3]
+    lat = 28 if tps else 21
+    rots = rots.float().contiguous()
+    trans = trans.float().contiguous()
+    tors = torsions.float().contiguous() if torsions is not None else None
+    dev = trans.device
+    latents = torch.empty(B, T, L, lat, device=dev)
+    x_cond = torch.empty_like(latents)
+    cond = torch.empty(B, T, L, dtype=torch.int64, device=dev)
+    flags = ((_lib.MDG_PREP_TPS if tps else 0) | (_lib.MDG_PREP_NO_OFFSETS if no_offsets else 0)
+             | (_lib.MDG_PREP_COND_FIRST if cond_first else 0) | (_lib.MDG_PREP_COND_LAST if cond_last else 0))
+    _lib.check(lib.mdg_prep_latents(B, T, L, lat, flags, int(cond_interval or 0), rots.data_ptr(), trans.data_ptr(),
+                                    _lib.ptr(tors), latents.data_ptr(), x_cond.data_ptr(), cond.data_ptr(),
+                                    _lib.stream_handle()), "mdg_prep_latents")
+    return latents, x_cond, cond
+
+
 def fix_quat_sign_(offsets: torch.Tensor) -> torch.Tensor:
     """wrapper.py:309: make the quaternion's real part non-negative (in place on [..., :4])."""
     offsets[..., :4] *= torch.where(offsets[..., 0:1] < 0, -1, 1)
@@ -85,20 +109,16 @@ class NewMDGenWrapper(nn.Module):
 
     # ------------------------------------------------------------------ batch preparation
     def prep_batch(self, batch):
-        """wrapper.py:283-365."""
+        """wrapper.py:283-365.  On a ROCm device the offsets / quaternions / latents / x_cond
+        come from one HIP launch (mdg_prep_latents) instead of the reference's per-frame CPU
+        eigen-solve; CPU tensors take the eager path below."""
         a = self.args
         rigids = Rigid(Rotation(rot_mats=batch["rots"]), batch["trans"])  # B, T, L
         B, T, L = rigids.shape
-        if a.no_offsets:
-            offsets = rigids.to_tensor_7()
-        else:
-            offsets = get_offsets(rigids[:, 0:1], rigids)
-        fix_quat_sign_(offsets)
+        tps = bool(a.tps_condition or a.inpainting or a.dynamic_mpnn)
         frame_loss_mask = batch["mask"].unsqueeze(-1).expand(-1, -1, 7)
         torsion_loss_mask = batch["torsion_mask"].unsqueeze(-1).expand(-1, -1, -1, 2).reshape(B, L, 14)
-        if a.tps_condition or a.inpainting or a.dynamic_mpnn:
-            offsets_r = fix_quat_sign_(get_offsets(rigids[:, -1:], rigids))
-            offsets = torch.cat([offsets, offsets_r], -1)
+        if tps:
             frame_loss_mask = torch.cat([frame_loss_mask, frame_loss_mask], -1)
         tors = batch["torsions"].reshape(B, T, L, 14)
         if a.no_torsion:
@@ -107,23 +127,35 @@ class NewMDGenWrapper(nn.Module):
             tors = batch["torsions"].clone()
             tors[:, :, DESIGN_IDX] = 0
             tors = tors.reshape(B, T, L, 14)
-        latents = torch.cat([offsets, tors.to(offsets.dtype)], -1)
+        simple_cond = not (a.inpainting or a.dynamic_mpnn or a.mpnn)
+        if batch["trans"].is_cuda and simple_cond:
+            latents, x_cond, cond_mask = prep_latents_hip(
+                batch["rots"], batch["trans"], tors, tps=tps, no_offsets=bool(a.no_offsets),
+                cond_first=bool(a.sim_condition or a.tps_condition), cond_last=bool(a.tps_condition),
+                cond_interval=a.cond_interval or 0)
+        else:
+            offsets = rigids.to_tensor_7() if a.no_offsets else get_offsets(rigids[:, 0:1], rigids)
+            fix_quat_sign_(offsets)
+            if tps:
+                offsets_r = fix_quat_sign_(get_offsets(rigids[:, -1:], rigids))
+                offsets = torch.cat([offsets, offsets_r], -1)
+            latents = torch.cat([offsets, tors.to(offsets.dtype)], -1)
+            cond_mask = torch.zeros(B, T, L, dtype=torch.int64, device=offsets.device)
+            if a.sim_condition:
+                cond_mask[:, 0] = 1
+            if a.tps_condition:
+                cond_mask[:, 0] = 1
+                cond_mask[:, -1] = 1
+            if a.cond_interval:
+                cond_mask[:, ::a.cond_interval] = 1
+            if a.inpainting or a.dynamic_mpnn or a.mpnn:
+                cond_mask[:, :, COND_IDX] = 1
+            x_cond = torch.where(cond_mask.unsqueeze(-1).bool(), latents, 0.0)
         if a.supervise_all_torsions:
             torsion_loss_mask = torch.ones_like(torsion_loss_mask)
         elif a.supervise_no_torsions:
             torsion_loss_mask = torch.zeros_like(torsion_loss_mask)
         loss_mask = torch.cat([frame_loss_mask, torsion_loss_mask], -1).unsqueeze(1).expand(-1, T, -1, -1)
-
-        cond_mask = torch.zeros(B, T, L, dtype=torch.int64, device=offsets.device)
-        if a.sim_condition:
-            cond_mask[:, 0] = 1
-        if a.tps_condition:
-            cond_mask[:, 0] = 1
-            cond_mask[:, -1] = 1
-        if a.cond_interval:
-            cond_mask[:, ::a.cond_interval] = 1
-        if a.inpainting or a.dynamic_mpnn or a.mpnn:
-            cond_mask[:, :, COND_IDX] = 1
         aatype_mask = torch.ones_like(batch["seqres"])
         if a.design:
             aatype_mask[:, DESIGN_IDX] = 0
@@ -136,7 +168,7 @@ class NewMDGenWrapper(nn.Module):
                 "end_frames": rigids[:, -1],
                 "mask": batch["mask"].unsqueeze(1).expand(-1, T, -1),
                 "aatype": torch.where(aatype_mask.bool(), batch["seqres"], 20),
-                "x_cond": torch.where(cond_mask.unsqueeze(-1).bool(), latents, 0.0),
+                "x_cond": x_cond,
                 "x_cond_mask": cond_mask,
             },
         }
