@@ -135,11 +135,13 @@ class MultiheadAttention(nn.Module):
         if self.rot_emb is not None:
             cos, sin = self.rot_emb.tables(Sk, x.device)
             q, k = apply_rope(q, cos, sin), apply_rope(k, cos, sin)
-        w = q @ k.transpose(-1, -2)
-        w = w.masked_fill(~kvalid[:, None, None, :], float("-inf"))
-        w = torch.softmax(w, dim=-1, dtype=torch.float32)
-        w = F.dropout(w, p=self.dropout, training=self.training)
-        o = (w @ v).transpose(1, 2).reshape(N, S, C)
+        # softmax(q k^T masked) v (mha.py:359-389) as one fused SDPA call: the [N,H,S,Sk] score
+        # tensor of the reference is never materialised (forward or backward)
+        bias = torch.zeros(N, 1, 1, Sk, dtype=q.dtype, device=x.device).masked_fill(
+            ~kvalid[:, None, None, :], float("-inf"))
+        o = F.scaled_dot_product_attention(q, k, v, attn_mask=bias, scale=1.0,
+                                           dropout_p=self.dropout if self.training else 0.0)
+        o = o.transpose(1, 2).reshape(N, S, C)
         return self.out_proj(o)
 
 
