@@ -8,7 +8,9 @@ operands, synthetic seed-derived weights and inputs (no checkpoint/dataset offli
 One bench "step" = one sim_inference rollout window: Sampler.sample_ode('euler', 50) over
 B trajectories of T frames = 49 Euler denoising steps (each a full forward + Euler update)
 plus the window's conditioning precompute, through the drop-in engine call
-(HipEngine.sample_euler: input staging + one hipGraph replay + output copy).
+(HipEngine.sample_euler: input staging + one hipGraph replay + output copy).  Default
+B=16 trajectories per GPU, run as 2 concurrent 8-trajectory chains ("lanes": parallel
+branches of the one hipGraph, engine._run_lanes).
 value = frames denoised per second = ranks * B * T * 49 * steps / max-over-ranks time.
 
 Multi-GPU: inference does not shard (temporal attention couples all T frames of a
@@ -41,7 +43,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10, help="timed rollout windows")
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=8, help="trajectories per GPU")
+    ap.add_argument("--batch", type=int, default=16, help="trajectories per GPU")
     ap.add_argument("--frames", type=int, default=1000)
     ap.add_argument("--crop", type=int, default=4)
     ap.add_argument("--num-steps", type=int, default=50, help="ODE grid points (49 Euler steps)")
@@ -49,6 +51,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--lanes", type=int, default=2, help="concurrent sub-batch chains per window (streams)")
     return ap.parse_args()
 
 
@@ -204,6 +207,7 @@ def main():
     m = make_model(T, L).to(dev)
     m.hip_dtype = a.dtype
     eng = get_engine(m)
+    eng.lanes = a.lanes
     zs, kw, _ = inputs(B, T, L, seed=100 + rank, device=dev)
 
     def window():
@@ -258,7 +262,8 @@ def main():
                                    "conditioning), per GPU",
                        "model": "LatentMDGenModel default (5 layers, C=384, 16 heads, IPA prepend, abs pos emb)",
                        "global_batch": B * world, "seq_len": T, "crop": L, "denoise_steps_per_step": n_euler,
-                       "parallelism": f"replicas{world}", "hipgraph": not a.no_graph},
+                       "parallelism": f"replicas{world}", "hipgraph": not a.no_graph,
+                       "lanes": a.lanes},
             "us_per_denoise_step": round(el / a.steps / n_euler * 1e6, 2),
             "roofline": roof,
             "roofline_attn_temporal": roof2,

@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 
 import torch
 import torch.nn.functional as F
@@ -63,6 +64,9 @@ class HipEngine:
         self._packed = None
         self._states = {}
         self._graphs = {}
+        self._lane_streams = []
+        # concurrent sub-batch chains per Euler window (MDG_LANES, default 1 = one chain)
+        self.lanes = int(os.environ.get("MDG_LANES", "1"))
 
     # ------------------------------------------------------------------ packing
     def _param_key(self):
@@ -149,9 +153,9 @@ class HipEngine:
         out[:, 1, D] = 1.0
         return out.contiguous()
 
-    def _state(self, B, T, L):
+    def _state(self, B, T, L, lane=0):
         P = self._pack()
-        key = (B, T, L)
+        key = (B, T, L, lane)
         st = self._states.get(key)
         if st is not None:
             return st
@@ -293,10 +297,10 @@ class HipEngine:
         aa = None if aatype is None else aatype.to(x.device)
         return B, T, L, mask, rots, trans, erots, etrans, aa
 
-    def _step_io(self, st, x_in, x_out, v_out, ipa, mods, mods_f, dt):
+    def _step_io(self, st, x_in, x_out, v_out, ipa, mods, mods_f, dt, base=None):
         io = _lib.MdgStepIO()
         io.x_in, io.x_out, io.v_out = x_in, x_out, v_out
-        io.base, io.ipa = st.base.data_ptr(), ipa
+        io.base, io.ipa = st.base.data_ptr() if base is None else base, ipa
         io.mods, io.mods_final = mods, mods_f
         io.dt = dt
         io.h = st.h.data_ptr()
@@ -460,7 +464,10 @@ class HipEngine:
         self._base(st, gs.x_cond if gs.has_cond else None, gs.x_cond_mask if gs.has_cond else None)
         _lib.check(self.lib.mdg_prepare_mask(ctypes.byref(st.dims), gs.mask.data_ptr(), st.ws.data_ptr(), s),
                    "mdg_prepare_mask")
-        C, B = self.C, st.B
+        nlanes = self.lanes if (self.lanes > 1 and st.B % self.lanes == 0) else 1
+        if nlanes > 1:
+            self._run_lanes(gs, st, mods, mods_f, ipa, nlanes)
+            return
         ios = []
         for i in range(gs.S):
             io = self._step_io(st, gs.states[i].data_ptr(), gs.states[i + 1].data_ptr(), None,
@@ -470,7 +477,40 @@ class HipEngine:
             _lib.check(self.lib.mdg_denoise_step(ctypes.byref(st.model_struct), ctypes.byref(io),
                                                  gs.mask.data_ptr(), st.ws.data_ptr(), s), "mdg_denoise_step")
         gs.ios = ios
-        del C, B
+
+    def _run_lanes(self, gs, st, mods, mods_f, ipa, nlanes):
+        """The window's S denoising steps as ``nlanes`` independent sub-batch chains, each on its
+        own HIP stream (fork/join around them; inside a capture they become parallel graph
+        branches).  Trajectories never interact inside a step, so the chains only share the
+        read-only weights / conditioning; running them concurrently lets one chain's VALU-bound
+        attention co-reside with the other's MFMA/HBM-bound GEMMs and fills each kernel's tail."""
+        main = torch.cuda.current_stream()
+        Bl = st.B // nlanes
+        rows = Bl * st.T * st.L
+        if len(self._lane_streams) < nlanes:
+            self._lane_streams += [torch.cuda.Stream() for _ in range(nlanes - len(self._lane_streams))]
+        lane_mods = [mods[:, :, k * Bl:(k + 1) * Bl].contiguous() for k in range(nlanes)]  # [S][nl][Bl][9C]
+        gs.lane_keep = lane_mods
+        gs.ios = []
+        for k in range(nlanes):
+            ls = self._state(Bl, st.T, st.L, lane=1 + k)
+            strm = self._lane_streams[k]
+            strm.wait_stream(main)
+            with torch.cuda.stream(strm):
+                sk = strm.cuda_stream
+                mask_k = gs.mask[k * Bl:(k + 1) * Bl]
+                _lib.check(self.lib.mdg_prepare_mask(ctypes.byref(ls.dims), mask_k.data_ptr(), ls.ws.data_ptr(), sk),
+                           "mdg_prepare_mask(lane)")
+                base_k = st.base.data_ptr() + k * rows * self.C * 4
+                for i in range(gs.S):
+                    io = self._step_io(ls, gs.states[i, k * Bl].data_ptr(), gs.states[i + 1, k * Bl].data_ptr(), None,
+                                       None if ipa is None else ipa[i, k * Bl].data_ptr(), lane_mods[k][i].data_ptr(),
+                                       mods_f[i, k * Bl].data_ptr(), gs.dts[i], base=base_k)
+                    gs.ios.append(io)
+                    _lib.check(self.lib.mdg_denoise_step(ctypes.byref(ls.model_struct), ctypes.byref(io),
+                                                         mask_k.data_ptr(), ls.ws.data_ptr(), sk), "mdg_denoise_step")
+        for k in range(nlanes):
+            main.wait_stream(self._lane_streams[k])
 
     def _capture(self, gs, st):
         g = torch.cuda.CUDAGraph()

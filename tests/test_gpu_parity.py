@@ -227,3 +227,28 @@ def test_long_residue_axis_atlas_matches_oracle(T, L, n_pad, dtype):
         v = m(g("x"), g("t"), g("mask"), start_frames=Rigid(Rotation(rot_mats=g("rots")), g("trans")),
               x_cond=g("x_cond"), x_cond_mask=g("x_cond_mask"), aatype=g("aatype"))
     _check(v, ref, dtype)
+
+
+def test_concurrent_lanes_equal_single_chain():
+    """engine.lanes = 2: the window's steps as two concurrent sub-batch chains on two streams
+    (parallel graph branches) give exactly the single-chain result, eager and captured."""
+    from mdgen_finetune_amd.engine import get_engine
+    from mdgen_finetune_amd.rigid_utils import Rigid, Rotation
+
+    inp, _, cfg = _oracle_full(64, seed=3, B=4)
+    m, _ = build_model(cfg, "cuda", T=64)
+    m.hip_dtype = "bf16"
+    eng = get_engine(m)
+    g = lambda k: torch.from_numpy(inp[k]).cuda()  # noqa: E731
+    kw = dict(mask=g("mask"), start_frames=Rigid(Rotation(rot_mats=g("rots")), g("trans")), x_cond=g("x_cond"),
+              x_cond_mask=g("x_cond_mask"), aatype=g("aatype"))
+    eng.lanes = 1
+    ref = eng.sample_euler(g("x"), num_steps=6, use_graph=False, **kw)
+    eng.lanes = 2
+    eng._graphs.clear()
+    got_eager = eng.sample_euler(g("x"), num_steps=6, use_graph=False, **kw)
+    got_graph = eng.sample_euler(g("x"), num_steps=6, use_graph=True, **kw)
+    got_replay = eng.sample_euler(g("x"), num_steps=6, use_graph=True, **kw)
+    eng.lanes = 1
+    assert torch.equal(got_eager, ref)
+    assert torch.equal(got_graph, ref) and torch.equal(got_replay, ref)
