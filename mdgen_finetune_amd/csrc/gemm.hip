@@ -786,26 +786,36 @@ static hipError_t launch_b8(const mdg_gemm_desc& p, hipStream_t s) {
 // accumulators are staged in LDS, then each wave owns 4 rows: gather h and gate of its rows,
 // h += gate * (acc + bias) (stored), two wave reductions, xn = LN(h)*(1+scale)+shift (bf16).
 constexpr int kRowThreads = 512;
-constexpr int kRowStages = 4;
 
-template <int NCOL>
+// BM 128: 8 waves as 2 x 4, 4-stage ring, one block per CU.  BM 64 (row tiles of 64, twice
+// the blocks): 8 waves as 1 x 8, 2-stage ring, two blocks per CU, so one block's HBM-bound
+// epilogue (h read/write, xn write) overlaps the other's MFMA main loop.
+template <int BM> struct RowCfg;
+template <> struct RowCfg<128> { static constexpr int WMW = 2, STAGES = 4; };
+template <> struct RowCfg<64> { static constexpr int WMW = 1, STAGES = 2; };
+
+template <int NCOL, int BM>
 __host__ __device__ constexpr size_t rowln_smem() {
-  return (size_t)kRowStages * (128 + NCOL) * 32 * 2;
+  return (size_t)RowCfg<BM>::STAGES * (BM + NCOL) * 32 * 2;
 }
 
-template <int NCOL>
-__global__ __launch_bounds__(kRowThreads) void gemm_rowln_kernel(const mdg_gemm_desc p) {
-  constexpr int BM = 128, BK = 32, WTN = NCOL / 4, NT = WTN / 16, ATILE = BM * BK, STAGE = (BM + NCOL) * BK;
+template <int NCOL, int BM>
+__global__ __launch_bounds__(kRowThreads, BM == 64 ? 4 : 1) void gemm_rowln_kernel(const mdg_gemm_desc p) {
+  constexpr int kRowStages = RowCfg<BM>::STAGES, WMW = RowCfg<BM>::WMW, WNW = 8 / WMW;
+  constexpr int BK = 32, WTN = NCOL / WNW, NT = WTN / 16, ATILE = BM * BK, STAGE = (BM + NCOL) * BK;
   constexpr int LDS_ST = NCOL + 4, NE = NCOL / 128;  // float2 column pairs per lane per row
   constexpr int WLD = NCOL / 128;                    // W glds instructions per wave per stage
-  static_assert(NCOL % 128 == 0 && NCOL <= 512, "NCOL");
+  constexpr int ALD_WAVES = BM / 16;                 // waves that stage A (one 16-row glds each)
+  constexpr int RG = (BM == 64 && NCOL > 256) ? 2 : 4;  // epilogue rows per wave processed together
+  static_assert(NCOL % 128 == 0 && NCOL <= 512 && WTN % 16 == 0, "NCOL");
   static_assert(32 * LDS_ST * 4 <= kRowStages * STAGE * 2, "band stage fits the ring");
   typedef __attribute__((address_space(3))) void* lds_ptr_t;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   bf16_t* lds = reinterpret_cast<bf16_t*>(smem);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 2, wn = wave & 3;
+  const int wm = wave / WNW, wn = wave % WNW;
+  const bool has_a = wave < ALD_WAVES;
   const int lr = lane & 15, lg = lane >> 4;
   const int M = p.M, K = p.K;
   // XCD-aware order of the row tiles (neighbouring tiles share nothing but W, which every
@@ -828,7 +838,8 @@ __global__ __launch_bounds__(kRowThreads) void gemm_rowln_kernel(const mdg_gemm_
 #define MDG_ROW_LOAD(stage_, k0_)                                                                   \
   {                                                                                                 \
     bf16_t* sa = lds + (stage_) * STAGE;                                                            \
-    __builtin_amdgcn_global_load_lds((const void*)(asrc + (k0_)), (lds_ptr_t)(sa + 16 * wave * BK), 16, 0, 0); \
+    if (has_a)                                                                                      \
+      __builtin_amdgcn_global_load_lds((const void*)(asrc + (k0_)), (lds_ptr_t)(sa + 16 * wave * BK), 16, 0, 0); \
     _Pragma("unroll") for (int i = 0; i < WLD; ++i)                                                 \
       __builtin_amdgcn_global_load_lds((const void*)(bsrc[i] + (k0_)),                              \
                                        (lds_ptr_t)(sa + ATILE + 16 * (wave * WLD + i) * BK), 16, 0, 0); \
@@ -848,9 +859,15 @@ __global__ __launch_bounds__(kRowThreads) void gemm_rowln_kernel(const mdg_gemm_
   for (int kt = 0; kt < nk; ++kt) {
     // stage kt landed: leave the (up to 2) younger stages' loads in flight
     const int younger = min(kRowStages - 2, nk - 1 - kt);
-    if (younger >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (1 + WLD)) : "memory");
-    else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(1 + WLD) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (has_a) {
+      if (younger >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (1 + WLD)) : "memory");
+      else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(1 + WLD) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      if (younger >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * WLD) : "memory");
+      else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WLD) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (kt + kRowStages - 1 < nk) MDG_ROW_LOAD((kt + kRowStages - 1) % kRowStages, (kt + kRowStages - 1) * BK);
@@ -878,7 +895,7 @@ __global__ __launch_bounds__(kRowThreads) void gemm_rowln_kernel(const mdg_gemm_
     bb[e] = p.bias ? *reinterpret_cast<const float2*>(p.bias + 2 * lane + 128 * e) : make_float2(0.f, 0.f);
   __syncthreads();  // all waves are done with the ring
 #pragma unroll 1
-  for (int band = 0; band < 4; ++band) {
+  for (int band = 0; band < BM / 32; ++band) {
     if (wm == (band >> 1)) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {  // compile-time acc index; the band selects 2 of the 4
@@ -893,94 +910,98 @@ __global__ __launch_bounds__(kRowThreads) void gemm_rowln_kernel(const mdg_gemm_
     __syncthreads();
     // wave -> rows 4*wave .. 4*wave+3 of the band; every global operand of the 4 rows is
     // gathered before use and the 4 rows' reductions run interleaved (independent chains)
-    float2 hv[4][NE], gv[4][NE];
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-      const int m = min(m0 + band * 32 + wave * 4 + rr, M - 1);
-      const float* hr = p.resid + (size_t)m * p.ldr;
-      const float* gr = p.gate ? p.gate + (size_t)fdiv(m, p.rows_per_mod, inv_rpm) * p.mod_stride + p.gate_off : nullptr;
-#pragma unroll
-      for (int e = 0; e < NE; ++e) {
-        const int k = 2 * lane + 128 * e;
-        hv[rr][e] = *reinterpret_cast<const float2*>(hr + k);
-        gv[rr][e] = gr ? *reinterpret_cast<const float2*>(gr + k) : make_float2(1.f, 1.f);
-      }
-    }
-    const int mb0 = min(m0 + band * 32 + wave * 4, M - 1), mb3 = min(mb0 + 3, M - 1);
-    const int b0 = fdiv(mb0, p.rows_per_mod, inv_rpm);
-    const bool one_b = fdiv(mb3, p.rows_per_mod, inv_rpm) == b0;  // the 4 rows share a batch entry
-    float2 xs[NE], xh[NE];
-    if (p.xn_out) {
-      const float* mr = p.xn_mods + (size_t)b0 * p.xn_mod_stride;
-#pragma unroll
-      for (int e = 0; e < NE; ++e) {
-        const int k = 2 * lane + 128 * e;
-        xs[e] = *reinterpret_cast<const float2*>(mr + p.xn_scale_off + k);
-        xh[e] = *reinterpret_cast<const float2*>(mr + p.xn_shift_off + k);
-      }
-    }
-    float sum[4];
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-      const float* srow = stage + (wave * 4 + rr) * LDS_ST;
-      float s = 0.f;
-#pragma unroll
-      for (int e = 0; e < NE; ++e) {
-        const float2 v = *reinterpret_cast<const float2*>(srow + 2 * lane + 128 * e);
-        hv[rr][e].x += gv[rr][e].x * (v.x + bb[e].x);
-        hv[rr][e].y += gv[rr][e].y * (v.y + bb[e].y);
-        s += hv[rr][e].x + hv[rr][e].y;
-      }
-      sum[rr] = s;
-      const int m = m0 + band * 32 + wave * 4 + rr;
-      if (m < M) {
-#pragma unroll
-        for (int e = 0; e < NE; ++e) *reinterpret_cast<float2*>(p.resid + (size_t)m * p.ldr + 2 * lane + 128 * e) = hv[rr][e];
-      }
-    }
-    if (p.xn_out) {
-#pragma unroll
-      for (int o = 32; o >= 1; o >>= 1)
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) sum[rr] += __shfl_xor(sum[rr], o, 64);
-      float ss[4];
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        sum[rr] *= invN;  // mean
-        float t = 0.f;
-#pragma unroll
-        for (int e = 0; e < NE; ++e) {
-          const float a0 = hv[rr][e].x - sum[rr], a1 = hv[rr][e].y - sum[rr];
-          t += a0 * a0 + a1 * a1;
-        }
-        ss[rr] = t;
-      }
-#pragma unroll
-      for (int o = 32; o >= 1; o >>= 1)
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) ss[rr] += __shfl_xor(ss[rr], o, 64);
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        const int m = m0 + band * 32 + wave * 4 + rr;
-        if (m >= M) continue;
-        const float rs = 1.0f / sqrtf(ss[rr] * invN + p.ln_eps);
-        if (!one_b) {  // rows straddle a batch boundary: this row's own shift / scale
-          const float* mr = p.xn_mods + (size_t)fdiv(m, p.rows_per_mod, inv_rpm) * p.xn_mod_stride;
-#pragma unroll
-          for (int e = 0; e < NE; ++e) {
-            const int k = 2 * lane + 128 * e;
-            xs[e] = *reinterpret_cast<const float2*>(mr + p.xn_scale_off + k);
-            xh[e] = *reinterpret_cast<const float2*>(mr + p.xn_shift_off + k);
-          }
-        }
-#pragma unroll
+    // rows of this wave in groups of RG (fewer live registers at BM 64, two blocks per CU)
+#pragma unroll 1
+    for (int g0 = 0; g0 < 4; g0 += RG) {
+      float2 hv[RG][NE], gv[RG][NE];
+  #pragma unroll
+      for (int rr = 0; rr < RG; ++rr) {
+        const int m = min(m0 + band * 32 + wave * 4 + g0 + rr, M - 1);
+        const float* hr = p.resid + (size_t)m * p.ldr;
+        const float* gr = p.gate ? p.gate + (size_t)fdiv(m, p.rows_per_mod, inv_rpm) * p.mod_stride + p.gate_off : nullptr;
+  #pragma unroll
         for (int e = 0; e < NE; ++e) {
           const int k = 2 * lane + 128 * e;
-          typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
-          bf16x2 pr;
-          pr[0] = (bf16_t)((hv[rr][e].x - sum[rr]) * rs * (1.0f + xs[e].x) + xh[e].x);
-          pr[1] = (bf16_t)((hv[rr][e].y - sum[rr]) * rs * (1.0f + xs[e].y) + xh[e].y);
-          *reinterpret_cast<bf16x2*>(reinterpret_cast<bf16_t*>(p.xn_out) + (size_t)m * NCOL + k) = pr;
+          hv[rr][e] = *reinterpret_cast<const float2*>(hr + k);
+          gv[rr][e] = gr ? *reinterpret_cast<const float2*>(gr + k) : make_float2(1.f, 1.f);
+        }
+      }
+      const int mb0 = min(m0 + band * 32 + wave * 4 + g0, M - 1), mb3 = min(mb0 + RG - 1, M - 1);
+      const int b0 = fdiv(mb0, p.rows_per_mod, inv_rpm);
+      const bool one_b = fdiv(mb3, p.rows_per_mod, inv_rpm) == b0;  // the 4 rows share a batch entry
+      float2 xs[NE], xh[NE];
+      if (p.xn_out) {
+        const float* mr = p.xn_mods + (size_t)b0 * p.xn_mod_stride;
+  #pragma unroll
+        for (int e = 0; e < NE; ++e) {
+          const int k = 2 * lane + 128 * e;
+          xs[e] = *reinterpret_cast<const float2*>(mr + p.xn_scale_off + k);
+          xh[e] = *reinterpret_cast<const float2*>(mr + p.xn_shift_off + k);
+        }
+      }
+      float sum[RG];
+  #pragma unroll
+      for (int rr = 0; rr < RG; ++rr) {
+        const float* srow = stage + (wave * 4 + g0 + rr) * LDS_ST;
+        float s = 0.f;
+  #pragma unroll
+        for (int e = 0; e < NE; ++e) {
+          const float2 v = *reinterpret_cast<const float2*>(srow + 2 * lane + 128 * e);
+          hv[rr][e].x += gv[rr][e].x * (v.x + bb[e].x);
+          hv[rr][e].y += gv[rr][e].y * (v.y + bb[e].y);
+          s += hv[rr][e].x + hv[rr][e].y;
+        }
+        sum[rr] = s;
+        const int m = m0 + band * 32 + wave * 4 + g0 + rr;
+        if (m < M) {
+  #pragma unroll
+          for (int e = 0; e < NE; ++e) *reinterpret_cast<float2*>(p.resid + (size_t)m * p.ldr + 2 * lane + 128 * e) = hv[rr][e];
+        }
+      }
+      if (p.xn_out) {
+  #pragma unroll
+        for (int o = 32; o >= 1; o >>= 1)
+  #pragma unroll
+          for (int rr = 0; rr < RG; ++rr) sum[rr] += __shfl_xor(sum[rr], o, 64);
+        float ss[RG];
+  #pragma unroll
+        for (int rr = 0; rr < RG; ++rr) {
+          sum[rr] *= invN;  // mean
+          float t = 0.f;
+  #pragma unroll
+          for (int e = 0; e < NE; ++e) {
+            const float a0 = hv[rr][e].x - sum[rr], a1 = hv[rr][e].y - sum[rr];
+            t += a0 * a0 + a1 * a1;
+          }
+          ss[rr] = t;
+        }
+  #pragma unroll
+        for (int o = 32; o >= 1; o >>= 1)
+  #pragma unroll
+          for (int rr = 0; rr < RG; ++rr) ss[rr] += __shfl_xor(ss[rr], o, 64);
+  #pragma unroll
+        for (int rr = 0; rr < RG; ++rr) {
+          const int m = m0 + band * 32 + wave * 4 + g0 + rr;
+          if (m >= M) continue;
+          const float rs = 1.0f / sqrtf(ss[rr] * invN + p.ln_eps);
+          if (!one_b) {  // rows straddle a batch boundary: this row's own shift / scale
+            const float* mr = p.xn_mods + (size_t)fdiv(m, p.rows_per_mod, inv_rpm) * p.xn_mod_stride;
+  #pragma unroll
+            for (int e = 0; e < NE; ++e) {
+              const int k = 2 * lane + 128 * e;
+              xs[e] = *reinterpret_cast<const float2*>(mr + p.xn_scale_off + k);
+              xh[e] = *reinterpret_cast<const float2*>(mr + p.xn_shift_off + k);
+            }
+          }
+  #pragma unroll
+          for (int e = 0; e < NE; ++e) {
+            const int k = 2 * lane + 128 * e;
+            typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+            bf16x2 pr;
+            pr[0] = (bf16_t)((hv[rr][e].x - sum[rr]) * rs * (1.0f + xs[e].x) + xh[e].x);
+            pr[1] = (bf16_t)((hv[rr][e].y - sum[rr]) * rs * (1.0f + xs[e].y) + xh[e].y);
+            *reinterpret_cast<bf16x2*>(reinterpret_cast<bf16_t*>(p.xn_out) + (size_t)m * NCOL + k) = pr;
+          }
         }
       }
     }
@@ -988,17 +1009,29 @@ __global__ __launch_bounds__(kRowThreads) void gemm_rowln_kernel(const mdg_gemm_
   }
 }
 
-template <int NCOL>
+template <int NCOL, int BM>
 static hipError_t launch_rowln(const mdg_gemm_desc& p, hipStream_t s) {
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_rowln_kernel<NCOL>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)rowln_smem<NCOL>());
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_rowln_kernel<NCOL, BM>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)rowln_smem<NCOL, BM>());
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  hipLaunchKernelGGL((gemm_rowln_kernel<NCOL>), dim3((p.M + 127) / 128), dim3(kRowThreads), rowln_smem<NCOL>(), s, p);
+  hipLaunchKernelGGL((gemm_rowln_kernel<NCOL, BM>), dim3((p.M + BM - 1) / BM), dim3(kRowThreads),
+                     (rowln_smem<NCOL, BM>()), s, p);
   return hipGetLastError();
+}
+
+// row-tile height of the fused gated-residual + LN GEMM (MDG_ROWLN_BM=64 knob; default 128:
+// measured at M = 32000 / 64000, 64-row tiles at two blocks per CU tie on out_proj and lose
+// 20 % on fc2 — the extra W re-reads from L2 outweigh the epilogue / main-loop overlap)
+static int rowln_bm() {
+  static const int bm = [] {
+    const char* e = getenv("MDG_ROWLN_BM");
+    return (e && atoi(e) == 64) ? 64 : 128;
+  }();
+  return bm;
 }
 
 template <typename CT, int BM, int BN, int WM, int AMODE>
@@ -1089,9 +1122,11 @@ GemmPlan gemm_plan(const mdg_gemm_desc& p) {
   else if (bf && p.epi == MDG_EPI_GATE_RES && p.xn_out && p.K % 64 == 0 && p.lda % 8 == 0 && p.ldw % 8 == 0 &&
            (p.N == 128 || p.N == 256 || p.N == 384 || p.N == 512)) {
     g.cfg = kCfgRow;  // full-row gated residual + LayerNorm
-    g.smem = p.N == 128 ? rowln_smem<128>() : p.N == 256 ? rowln_smem<256>() : p.N == 384 ? rowln_smem<384>()
-                                                                                        : rowln_smem<512>();
-    g.bm = 128;
+    const bool b64 = rowln_bm() == 64 && p.N <= 384;
+#define MDG_ROWSM(n) (b64 ? rowln_smem<n, 64>() : rowln_smem<n, 128>())
+    g.smem = p.N == 128 ? MDG_ROWSM(128) : p.N == 256 ? MDG_ROWSM(256) : p.N == 384 ? MDG_ROWSM(384) : MDG_ROWSM(512);
+#undef MDG_ROWSM
+    g.bm = b64 ? 64 : 128;
     g.bn = p.N;
     return g;
   } else if (bf && p.N % kB4Tile == 0 && p.K % 64 == 0 && p.lda % 8 == 0 && p.ldw % 8 == 0) {
@@ -1135,11 +1170,19 @@ GemmPlan gemm_plan(const mdg_gemm_desc& p) {
 
 hipError_t gemm_launch(const mdg_gemm_desc& p, const GemmPlan& g, hipStream_t s) {
   if (g.cfg == kCfgRow) {
+    if (g.bm == 64) {
+      switch (p.N) {
+        case 128: return launch_rowln<128, 64>(p, s);
+        case 256: return launch_rowln<256, 64>(p, s);
+        case 384: return launch_rowln<384, 64>(p, s);
+        default: return launch_rowln<512, 64>(p, s);
+      }
+    }
     switch (p.N) {
-      case 128: return launch_rowln<128>(p, s);
-      case 256: return launch_rowln<256>(p, s);
-      case 384: return launch_rowln<384>(p, s);
-      default: return launch_rowln<512>(p, s);
+      case 128: return launch_rowln<128, 128>(p, s);
+      case 256: return launch_rowln<256, 128>(p, s);
+      case 384: return launch_rowln<384, 128>(p, s);
+      default: return launch_rowln<512, 128>(p, s);
     }
   }
   if (g.cfg == kCfgB8) {

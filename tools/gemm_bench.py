@@ -24,20 +24,25 @@ def tm(fn, it=20):
     return e0.elapsed_time(e1) / it * 1e3  # us
 
 
-def run(M, N, K, a_mode, epi, dt="bf16", act=0):
+def run(M, N, K, a_mode, epi, dt="bf16", act=0, rowln=False):
     ct = torch.bfloat16 if dt == "bf16" else torch.float32
     A = torch.randn(M, K, device="cuda").to(ct if a_mode == 0 else torch.float32)
     W = torch.randn(N, K, device="cuda").to(ct)
     bias = torch.randn(N, device="cuda")
     out = torch.empty(M, N, device="cuda", dtype=ct)
     resid = torch.zeros(M, N, device="cuda")
-    mods = torch.randn(8, 9 * K, device="cuda") * 0.1
+    mods = torch.randn(M // 4000 + 1, 9 * K, device="cuda") * 0.1
     d = _lib.MdgGemmDesc()
     d.dtype = 1 if dt == "bf16" else 0
     d.a_mode, d.epi, d.M, d.N, d.K, d.act = a_mode, epi, M, N, K, act
     d.A, d.lda, d.W, d.ldw, d.bias = A.data_ptr(), K, W.data_ptr(), K, bias.data_ptr()
     d.mods, d.mod_stride, d.rows_per_mod, d.shift_off, d.scale_off, d.ln_eps = mods.data_ptr(), 9 * K, 4000, 0, K, 1e-6
     d.out, d.ldo, d.resid, d.ldr = out.data_ptr(), N, resid.data_ptr(), N
+    if rowln:  # + LayerNorm of the updated rows into a bf16 xn (gemm_rowln_kernel)
+        xn = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+        d.gate, d.gate_off, d.rows_per_mod, d.mod_stride = mods.data_ptr(), 0, 4000, 9 * K
+        d.xn_out, d.xn_mods, d.xn_mod_stride, d.xn_shift_off, d.xn_scale_off = (xn.data_ptr(), mods.data_ptr(),
+                                                                              9 * K, 0, N)
     s = torch.cuda.current_stream().cuda_stream
 
     def f():
@@ -53,6 +58,11 @@ def run(M, N, K, a_mode, epi, dt="bf16", act=0):
 
 if __name__ == "__main__":
     import sys as _s
+    if len(_s.argv) > 1 and _s.argv[1] == "rowln":  # fused gated residual + LN (out_proj / fc2)
+        for M in (32000, 64000):
+            for K in (384, 1536):
+                run(M, 384, K, 0, 1, rowln=True)
+        _s.exit(0)
     if len(_s.argv) > 1 and _s.argv[1] == "ksweep":
         for K in (64, 128, 384):
             run(32000, 1536, K, 0, 0)
