@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define MDG_ABI_VERSION 5
+#define MDG_ABI_VERSION 6
 #define MDG_MAX_LAYERS 16
 #define MDG_DP 32 /* padded head dim of every attention operand buffer (head_dim <= 31) */
 
@@ -197,6 +197,21 @@ enum {
 int mdg_prep_latents(int32_t B, int32_t T, int32_t L, int32_t latent, int32_t flags, int32_t cond_interval,
                      const float* rots, const float* trans, const float* torsions, float* latents,
                      float* x_cond, int64_t* cond_mask, void* stream);
+
+/* Denoised latents -> atom14 coordinates (NewMDGenWrapper.inference, wrapper.py:480-505, with
+   frames_torsions_to_atom14, geometry.py:62-81 / 218-317), per token n = (b, t, l):
+     frame  = ref[b, l] o (normalised quaternion, translation) of samples[n][0:7]
+     alpha  = samples[n][tors_off .. tors_off+14) as 7 (sin, cos) pairs (unit-normalised if renorm)
+     atom14[n][a] = frame . group_frame(aatype, alpha)[group(a)] . lit(aatype, a)  (0 if absent)
+   samples [B,T,L,latent] fp32; ref_rots [B,L,3,3], ref_trans [B,L,3]; aatype [B,T,L] int64;
+   tables (residue_constants.npz, device copies): default_frames [21][8][4][4] f32,
+   group_idx [21][14] int32, atom_mask [21][14] f32, lit [21][14][3] f32.
+   out: atom14 [B,T,L,14,3]; out_rots [B,T,L,3,3] / out_trans [B,T,L,3] (null = skip). */
+int mdg_latents_to_atom14(int32_t B, int32_t T, int32_t L, int32_t latent, int32_t tors_off, int32_t renorm,
+                          const float* samples, const float* ref_rots, const float* ref_trans,
+                          const int64_t* aatype, const float* default_frames, const int32_t* group_idx,
+                          const float* atom_mask, const float* lit, float* atom14, float* out_rots,
+                          float* out_trans, void* stream);
 
 #ifdef __cplusplus
 }

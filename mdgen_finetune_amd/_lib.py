@@ -82,9 +82,10 @@ SIGNATURES = [
     ("mdg_attn_spatial", _i32, [_i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
     ("mdg_attn_temporal", _i32, [_i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
     ("mdg_prep_latents", _i32, [_i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    ("mdg_latents_to_atom14", _i32, [_i32, _i32, _i32, _i32, _i32, _i32] + [_vp] * 12),
 ]
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 _LIB = None
 
 

@@ -33,6 +33,11 @@ hipError_t set_vpad_launch(int dtype, void* v, size_t rows, int D, hipStream_t s
 hipError_t prep_latents_launch(int B, int T, int L, int lat, int tps, int no_offsets, int cond_mode,
                                int cond_interval, const float* rots, const float* trans, const float* torsions,
                                float* latents, float* x_cond, int64_t* cond_mask, hipStream_t s);
+hipError_t latents_to_atom14_launch(int B, int T, int L, int lat, int tors_off, int renorm, const float* samples,
+                                    const float* ref_rots, const float* ref_trans, const int64_t* aatype,
+                                    const float* default_frames, const int* group_idx, const float* atom_mask,
+                                    const float* lit, float* atom14, float* out_rots, float* out_trans,
+                                    hipStream_t s);
 }  // namespace mdg
 
 namespace {
@@ -434,6 +439,22 @@ int mdg_prep_latents(int32_t B, int32_t T, int32_t L, int32_t latent, int32_t fl
                                             cond_interval, rots, trans, torsions, latents, x_cond, cond_mask,
                                             (hipStream_t)stream),
                    "prep_latents");
+}
+
+int mdg_latents_to_atom14(int32_t B, int32_t T, int32_t L, int32_t latent, int32_t tors_off, int32_t renorm,
+                          const float* samples, const float* ref_rots, const float* ref_trans,
+                          const int64_t* aatype, const float* default_frames, const int32_t* group_idx,
+                          const float* atom_mask, const float* lit, float* atom14, float* out_rots,
+                          float* out_trans, void* stream) {
+  if (!samples || !ref_rots || !ref_trans || !aatype || !default_frames || !group_idx || !atom_mask || !lit || !atom14)
+    return fail(MDG_E_ARG, "latents_to_atom14: null pointer");
+  if ((out_rots == nullptr) != (out_trans == nullptr)) return fail(MDG_E_ARG, "latents_to_atom14: out_rots/out_trans");
+  if (B <= 0 || T <= 0 || L <= 0 || tors_off < 7 || latent < tors_off + 14)
+    return fail(MDG_E_SHAPE, "latents_to_atom14: B,T,L=%d,%d,%d latent=%d tors_off=%d", B, T, L, latent, tors_off);
+  return hip_check(mdg::latents_to_atom14_launch(B, T, L, latent, tors_off, renorm ? 1 : 0, samples, ref_rots,
+                                                 ref_trans, aatype, default_frames, group_idx, atom_mask, lit,
+                                                 atom14, out_rots, out_trans, (hipStream_t)stream),
+                   "latents_to_atom14");
 }
 
 }  // extern "C"

@@ -139,4 +139,143 @@ hipError_t prep_latents_launch(int B, int T, int L, int lat, int tps, int no_off
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------------------
+// Denoised latents -> atom14 coordinates (wrapper.py:480-505 + geometry.py:62-81, 218-317),
+// one thread per token: the offset quaternion (normalised) and translation composed onto the
+// token's frame-0 rigid, the 7 torsions normalised to unit (sin, cos), the 8 rigid-group
+// frames of the residue type (default frame o torsion rotation, chi2..4 chained onto chi1),
+// then each of the 14 atoms = its group's frame applied to the literature position.
+__device__ __forceinline__ void mat3_mul(const float (&a)[3][3], const float (&b)[3][3], float (&c)[3][3]) {
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) c[i][j] = a[i][0] * b[0][j] + a[i][1] * b[1][j] + a[i][2] * b[2][j];
+}
+
+__global__ void latents_to_atom14_kernel(int B, int T, int L, int lat, int tors_off, int renorm,
+                                         const float* __restrict__ samples, const float* __restrict__ ref_rots,
+                                         const float* __restrict__ ref_trans, const int64_t* __restrict__ aatype,
+                                         const float* __restrict__ default_frames, const int* __restrict__ group_idx,
+                                         const float* __restrict__ atom_mask, const float* __restrict__ lit,
+                                         float* __restrict__ atom14, float* __restrict__ out_rots,
+                                         float* __restrict__ out_trans) {
+  const size_t n = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= (size_t)B * T * L) return;
+  const int l = (int)(n % L);
+  const int b = (int)(n / ((size_t)T * L));
+  const float* x = samples + n * lat;
+  // Rigid.from_tensor_7(offsets, normalize_quats=True) (rigid_utils.py:155-189 quat -> rot)
+  float qa = x[0], qb = x[1], qc = x[2], qd = x[3];
+  const float qn = sqrtf(qa * qa + qb * qb + qc * qc + qd * qd);
+  qa /= qn; qb /= qn; qc /= qn; qd /= qn;
+  const float rr[3][3] = {
+      {qa * qa + qb * qb - qc * qc - qd * qd, 2.f * (qb * qc - qa * qd), 2.f * (qb * qd + qa * qc)},
+      {2.f * (qb * qc + qa * qd), qa * qa - qb * qb + qc * qc - qd * qd, 2.f * (qc * qd - qa * qb)},
+      {2.f * (qb * qd - qa * qc), 2.f * (qc * qd + qa * qb), qa * qa - qb * qb - qc * qc + qd * qd}};
+  // frame = frame0 o rel
+  const size_t bl = (size_t)b * L + l;
+  float r0[3][3], t0[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) r0[i][j] = ref_rots[bl * 9 + i * 3 + j];
+    t0[i] = ref_trans[bl * 3 + i];
+  }
+  float R[3][3], Tt[3];
+  mat3_mul(r0, rr, R);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) Tt[i] = r0[i][0] * x[4] + r0[i][1] * x[5] + r0[i][2] * x[6] + t0[i];
+  if (out_rots) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) out_rots[n * 9 + i * 3 + j] = R[i][j];
+      out_trans[n * 3 + i] = Tt[i];
+    }
+  }
+  int aa = (int)aatype[n];
+  aa = aa < 0 ? 0 : (aa > 20 ? 20 : aa);
+  // 8 group frames relative to the backbone: default_r o rot_x(alpha)   (geometry.py:283-301)
+  float gR[8][3][3], gT[8][3];
+#pragma unroll
+  for (int g = 0; g < 8; ++g) {
+    float sa = 0.f, ca = 1.f;  // backbone group: identity rotation (bb_rot = (0, 1))
+    if (g > 0) {
+      sa = x[tors_off + 2 * (g - 1)];
+      ca = x[tors_off + 2 * (g - 1) + 1];
+      if (renorm) {
+        const float nn = sqrtf(sa * sa + ca * ca);
+        sa /= nn;
+        ca /= nn;
+      }
+    }
+    const float* d = default_frames + ((size_t)aa * 8 + g) * 16;
+    // D_R . [[1,0,0],[0,c,-s],[0,s,c]]
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const float d0 = d[i * 4 + 0], d1 = d[i * 4 + 1], d2 = d[i * 4 + 2];
+      gR[g][i][0] = d0;
+      gR[g][i][1] = d1 * ca + d2 * sa;
+      gR[g][i][2] = -d1 * sa + d2 * ca;
+      gT[g][i] = d[i * 4 + 3];
+    }
+  }
+#pragma unroll
+  for (int g = 5; g < 8; ++g) {  // chi2..chi4 chained onto the previous chi frame
+    float nr[3][3], nt[3];
+    mat3_mul(gR[g - 1], gR[g], nr);
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+      nt[i] = gR[g - 1][i][0] * gT[g][0] + gR[g - 1][i][1] * gT[g][1] + gR[g - 1][i][2] * gT[g][2] + gT[g - 1][i];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) gR[g][i][j] = nr[i][j];
+      gT[g][i] = nt[i];
+    }
+  }
+  float* out = atom14 + n * 42;
+  for (int a = 0; a < 14; ++a) {
+    const int g = group_idx[aa * 14 + a];
+    const float m = atom_mask[aa * 14 + a];
+    const float* p = lit + ((size_t)aa * 14 + a) * 3;
+    float lr[3][3], lt[3];
+    // select the group frame without dynamic register indexing
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      lt[i] = gT[0][i];
+#pragma unroll
+      for (int j = 0; j < 3; ++j) lr[i][j] = gR[0][i][j];
+    }
+#pragma unroll
+    for (int gg = 1; gg < 8; ++gg)
+      if (g == gg) {
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          lt[i] = gT[gg][i];
+#pragma unroll
+          for (int j = 0; j < 3; ++j) lr[i][j] = gR[gg][i][j];
+        }
+      }
+    // local = group frame . lit ; global = frame . local
+    float loc[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) loc[i] = lr[i][0] * p[0] + lr[i][1] * p[1] + lr[i][2] * p[2] + lt[i];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) out[a * 3 + i] = (R[i][0] * loc[0] + R[i][1] * loc[1] + R[i][2] * loc[2] + Tt[i]) * m;
+  }
+}
+
+hipError_t latents_to_atom14_launch(int B, int T, int L, int lat, int tors_off, int renorm, const float* samples,
+                                    const float* ref_rots, const float* ref_trans, const int64_t* aatype,
+                                    const float* default_frames, const int* group_idx, const float* atom_mask,
+                                    const float* lit, float* atom14, float* out_rots, float* out_trans,
+                                    hipStream_t s) {
+  const size_t N = (size_t)B * T * L;
+  hipLaunchKernelGGL(latents_to_atom14_kernel, dim3((unsigned)((N + 127) / 128)), dim3(128), 0, s, B, T, L, lat,
+                     tors_off, renorm, samples, ref_rots, ref_trans, aatype, default_frames, group_idx, atom_mask,
+                     lit, atom14, out_rots, out_trans);
+  return hipGetLastError();
+}
+
 }  // namespace mdg

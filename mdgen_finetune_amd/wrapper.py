@@ -214,18 +214,26 @@ class NewMDGenWrapper(nn.Module):
 
     @torch.no_grad()
     def inference(self, batch, zs0=None):
-        """wrapper.py:436-508 up to (not including) atom14 reconstruction: returns
-        (frames Rigid [B,T,L], torsions [B,T,L,7,2] unit-normalised, samples)."""
+        """wrapper.py:436-508: (atom14 [B,T,L,14,3], aatype [B,T,L]).  On a ROCm device the
+        offsets -> frames -> 8 group frames -> 14 atoms reconstruction is one HIP launch
+        (mdg_latents_to_atom14); CPU tensors take the torch restatement (geometry.py)."""
+        from . import geometry as G
+
         samples, prep = self.sample_latents(batch, zs0)
         B, T, L, _ = samples.shape
-        offsets = samples[..., :7]
-        torsions = samples[..., 14:28] if (self.args.tps_condition or self.args.inpainting) else samples[..., 7:21]
-        rel = Rigid.from_tensor_7(offsets, normalize_quats=True)
-        frames = rel if self.args.no_offsets else prep["rigids"][:, 0:1].compose(rel)
-        torsions = torsions.reshape(B, T, L, 7, 2)
-        if not self.args.oracle:
-            torsions = torsions / torch.linalg.norm(torsions, dim=-1, keepdim=True)
-        return frames, torsions, samples
+        r0 = prep["rigids"][:, 0]
+        ref_rots, ref_trans = r0.get_rots().get_rot_mats(), r0.get_trans()
+        aa = batch["seqres"][:, None].expand(B, T, L)
+        tps = bool(self.args.tps_condition or self.args.inpainting)
+        if self.args.no_offsets:
+            raise NotImplementedError("--no_offsets rollout reconstruction is outside this build")
+        if samples.is_cuda:
+            atom14 = G.latents_to_atom14_hip(samples, ref_rots, ref_trans, aa, tps=tps, renorm=not self.args.oracle)
+        else:
+            rots, trans, tors = G.latents_to_frames_torsions(samples, ref_rots, ref_trans, tps=tps,
+                                                             renorm=not self.args.oracle)
+            atom14 = G.frames_torsions_to_atom14(rots, trans, tors, aa)
+        return atom14, aa
 
     # ------------------------------------------------------------------ optimizer / EMA / ckpt
     def configure_optimizers(self, params=None):

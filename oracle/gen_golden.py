@@ -260,8 +260,50 @@ def prep_batch_case(name, B, T, L, seed):
     save(name, dict(name=name, B=B, T=T, L=L, seed=seed), inp, out)
 
 
+def geometry_case(name, B, T, L, seed):
+    """Rollout geometry through the reference's own functions: wrapper.py:480-505 (offsets ->
+    frames composed on frame 0 via Rigid.from_tensor_7(normalize_quats=True), torsion
+    normalisation) + geometry.frames_torsions_to_atom14, atom14_to_frames, atom14_to_atom37,
+    atom37_to_torsions, and utils.atom14_to_pdb's multi-model PDB text."""
+    import tempfile
+
+    from mdgen.geometry import atom14_to_atom37, atom14_to_frames, atom37_to_torsions, frames_torsions_to_atom14
+    from mdgen.rigid_utils import Rigid, Rotation
+    from mdgen.utils import atom14_to_pdb
+    from mdgen_finetune_amd.data import SyntheticMDDataset
+
+    rng = np.random.default_rng(seed)
+    ds = SyntheticMDDataset(1, L, size=B, seed=seed)
+    rots0 = torch.stack([ds[i]["rots"][0] for i in range(B)])      # [B,L,3,3]
+    trans0 = torch.stack([ds[i]["trans"][0] for i in range(B)])    # [B,L,3]
+    samples = torch.from_numpy(rng.standard_normal((B, T, L, 21)).astype(np.float32))
+    samples[..., 4:7] *= 3.0
+    aatype = torch.from_numpy(rng.integers(0, 20, (B, L)).astype(np.int64))
+    ref = Rigid(trans=trans0[:, None], rots=Rotation(rot_mats=rots0[:, None]))
+    frames = ref.compose(Rigid.from_tensor_7(samples[..., :7], normalize_quats=True))
+    tors = samples[..., 7:21].reshape(B, T, L, 7, 2)
+    tors = tors / torch.linalg.norm(tors, dim=-1, keepdims=True)
+    atom14 = frames_torsions_to_atom14(frames, tors.view(B, T, L, 7, 2), aatype[:, None].expand(B, T, L))
+    last = atom14[:, -1]                                           # [B,L,14,3]
+    fr = atom14_to_frames(last)
+    atom37 = torch.from_numpy(np.asarray(atom14_to_atom37(last[0].numpy(), aatype[0].numpy()))).float()
+    tors37, tmask = atom37_to_torsions(atom37, aatype[0])
+    with tempfile.TemporaryDirectory() as tmp:
+        path = os.path.join(tmp, "x.pdb")
+        atom14_to_pdb(atom14[0].numpy(), aatype[0].numpy(), path)
+        pdb = open(path).read()
+    inp = dict(samples=samples.numpy(), rots0=rots0.numpy(), trans0=trans0.numpy(), aatype=aatype.numpy())
+    out = dict(atom14=atom14, frame_rots=frames.get_rots().get_rot_mats(), frame_trans=frames.get_trans(),
+               last_rots=fr.get_rots().get_rot_mats(), last_trans=fr.get_trans(), atom37=atom37,
+               torsions=tors37, torsion_mask=tmask, pdb=np.array(pdb))
+    save(name, dict(name=name, B=B, T=T, L=L, seed=seed), inp, out)
+
+
 def main():
     torch.set_num_threads(8)
+    if sys.argv[1:] == ["geometry"]:
+        geometry_case("geometry", B=2, T=5, L=6, seed=61)
+        return
     if sys.argv[1:] == ["prep_batch"]:
         prep_batch_case("prep_batch", B=2, T=12, L=5, seed=51)
         return
@@ -277,6 +319,7 @@ def main():
     loss_case("small_loss", SMALL, B=3, T=8, L=4, seed=31)
     mha_case("mha_rope_biaskv", seed=41)
     prep_batch_case("prep_batch", B=2, T=12, L=5, seed=51)
+    geometry_case("geometry", B=2, T=5, L=6, seed=61)
 
 
 if __name__ == "__main__":
