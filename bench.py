@@ -17,9 +17,11 @@ Multi-GPU: inference does not shard (temporal attention couples all T frames of 
 trajectory), so N ranks run N independent replicas of the window ("replicas only",
 scaling "weak"); no collective on the data path.
 
-Extra fields: "roofline" for the dominant kernel (the temporal q|k|v projection GEMM; live
-HIP-event timing on the stream the kernel runs on), "roofline_attn_temporal" for the next
-one, "cpu_baseline" (the oracle restatement timed on this host's cores).
+Extra fields: "roofline" for the dominant kernel (gemm_rowln_kernel, the gated-residual +
+LayerNorm-epilogue GEMM, 30 % of the step per profiles/; quoted on its largest launch, fc2;
+live HIP-event timing on the stream the kernel runs on), "roofline_more" for the next two
+(temporal q|k|v GEMM, temporal attention), "cpu_baseline" (the oracle restatement timed on
+this host's cores).
 """
 import argparse
 import ctypes
@@ -97,7 +99,7 @@ def time_kernel(fn, iters=20):
 def _traffic(kernel, B, T, L, dtype):
     """HBM bytes per launch from the committed PMC pass (profiles/traffic_r01.json, FETCH_SIZE x2
     + WRITE_SIZE per the gfx950 correction of MI355X_MICROARCH.md §HBM), or None."""
-    prof = os.path.join(REPO, "profiles", "traffic_r01.json")
+    prof = os.path.join(REPO, "profiles", "traffic_r01.json")  # this round's PMC passes
     try:
         return json.load(open(prof))[kernel].get(f"B{B}_T{T}_L{L}_{dtype}")
     except Exception:
@@ -105,12 +107,13 @@ def _traffic(kernel, B, T, L, dtype):
 
 
 def roofline(eng, st, dtype, B, T, L):
-    """Roofline of the two kernels that dominate the step (rocprof summary in profiles/):
-    the temporal q|k|v projection GEMM (2 per layer with the spatial one; 2*M*N*K FLOPs,
-    M = B*T*L, N = 3C, K = C) and the temporal flash attention (4*B*L*H*T*(T+1)*D FLOPs: QK^T
-    and PV over T+1 keys incl. the bias row, unpadded head_dim D).  Both launched exactly as
-    in the step (same workspace buffers, layer-0 weights) and timed with HIP events on the
-    stream they run on."""
+    """Rooflines of the launches that dominate the step, at the shape they run with in the
+    timed region (B = one lane's trajectories), launched exactly as in the step (same
+    workspace buffers, layer-0 weights) and timed with HIP events on their stream:
+      * attn_temporal — the largest launch type per step (profiles/r01_summary.md):
+        4*B*L*H*T*(T+1)*D FLOPs (QK^T and PV over T+1 keys incl. the bias row, unpadded D);
+      * gemm_qkv_temporal — 2*M*N*K with M = B*T*L, N = 3C, K = C (+ RoPE/scatter epilogue);
+      * gemm_fc2_rowln — fc2 with the gated residual + LayerNorm epilogue, 2*M*C*4C."""
     from mdgen_finetune_amd import _lib
 
     lib, P = eng.lib, eng._packed
@@ -136,17 +139,32 @@ def roofline(eng, st, dtype, B, T, L):
     def gemm():
         _lib.check(lib.mdg_gemm(ctypes.byref(g), s), "qkv gemm")
 
-    out = []
-    for name, fn, flops in (("gemm_qkv_temporal", gemm, 2.0 * N * 3 * C * C),
+    # fc2 + gated residual + LN of the next consumer (its own scratch residual / mods)
+    mods = torch.zeros(B, 9 * C, device=st.h.device)
+    h_scratch = torch.zeros_like(st.h)
+    f = _lib.MdgGemmDesc()
+    f.dtype, f.a_mode, f.epi, f.M, f.N, f.K = eng.mdg_dtype, _lib.MDG_A_PLAIN, _lib.MDG_EPI_GATE_RES, N, C, 4 * C
+    f.A, f.lda = ws + off["hid"], 4 * C
+    f.W, f.ldw, f.bias = P["layers"][0]["w2"].data_ptr(), 4 * C, P["layers"][0]["b2"].data_ptr()
+    f.resid, f.ldr, f.gate, f.gate_off = h_scratch.data_ptr(), C, mods.data_ptr(), 8 * C
+    f.mod_stride, f.rows_per_mod = 9 * C, T * L
+    f.xn_out, f.xn_mods, f.xn_mod_stride, f.xn_shift_off, f.xn_scale_off = ws + off["xn"], mods.data_ptr(), 9 * C, 0, C
+    f.ln_eps = 1e-6
+
+    def fc2():
+        _lib.check(lib.mdg_gemm(ctypes.byref(f), s), "fc2 rowln gemm")
+
+    out = {}
+    for name, fn, flops in (("gemm_fc2_rowln", fc2, 2.0 * N * C * 4 * C),
+                            ("gemm_qkv_temporal", gemm, 2.0 * N * 3 * C * C),
                             ("attn_temporal", attn, 4.0 * B * L * H * T * (T + 1) * D)):
         sec = time_kernel(fn, 50)
         ach = flops / sec / 1e12
-        out.append({"kernel": name, "bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_TFLOPS[dtype],
-                    "unit": "TFLOP/s", "frac": round(ach / PEAK_TFLOPS[dtype], 4),
-                    "traffic": _traffic(name, B, T, L, dtype), "avg_launch_us": round(sec * 1e6, 2),
-                    "flops_per_launch": flops})
-    gemm()  # leave the temporal q|k|v of layer 0 in place (the attention launches above read it)
-    return out[0], out[1]
+        out[name] = {"kernel": name, "bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_TFLOPS[dtype],
+                     "unit": "TFLOP/s", "frac": round(ach / PEAK_TFLOPS[dtype], 4),
+                     "traffic": _traffic(name, B, T, L, dtype), "avg_launch_us": round(sec * 1e6, 2),
+                     "flops_per_launch": flops, "shape": f"B={B} T={T} L={L}"}
+    return out
 
 
 def cpu_baseline(T, L, seconds):
@@ -238,8 +256,11 @@ def main():
         n_euler = a.num_steps - 1
         frames = world * B * T * n_euler * a.steps
         value = frames / el
-        st = eng._state(B, T, L)
-        roof, roof2 = roofline(eng, st, a.dtype, B, T, L) if rank == 0 else (None, None)
+        # roofline launches at the shape the timed region runs them with (one lane's batch)
+        nl = a.lanes if (a.lanes > 1 and B % a.lanes == 0) else 1
+        Bl = B // nl
+        st = eng._state(Bl, T, L, lane=1 if nl > 1 else 0)
+        roofs = roofline(eng, st, a.dtype, Bl, T, L) if rank == 0 else None
 
     out = None
     if rank == 0:
@@ -265,8 +286,8 @@ def main():
                        "parallelism": f"replicas{world}", "hipgraph": not a.no_graph,
                        "lanes": a.lanes},
             "us_per_denoise_step": round(el / a.steps / n_euler * 1e6, 2),
-            "roofline": roof,
-            "roofline_attn_temporal": roof2,
+            "roofline": roofs["gemm_fc2_rowln"] if roofs else None,
+            "roofline_more": [roofs["gemm_qkv_temporal"], roofs["attn_temporal"]] if roofs else None,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define MDG_ABI_VERSION 6
+#define MDG_ABI_VERSION 7
 #define MDG_MAX_LAYERS 16
 #define MDG_DP 32 /* padded head dim of every attention operand buffer (head_dim <= 31) */
 
@@ -49,7 +49,7 @@ enum {
 
 /* GEMM building block: out = epilogue( prologue(A) . W^T + bias ) */
 enum { MDG_A_PLAIN = 0, MDG_A_LNMOD = 1 };
-enum { MDG_EPI_STORE = 0, MDG_EPI_GATE_RES = 1, MDG_EPI_QKV = 2, MDG_EPI_EULER = 3 };
+enum { MDG_EPI_STORE = 0, MDG_EPI_GATE_RES = 1, MDG_EPI_QKV = 2, MDG_EPI_EULER = 3, MDG_EPI_ATTN_SPATIAL = 4 };
 enum { MDG_ACT_NONE = 0, MDG_ACT_GELU = 1, MDG_ACT_SILU = 2 };
 enum { MDG_QKV_SPATIAL = 0, MDG_QKV_TEMPORAL = 1 };
 
@@ -125,6 +125,13 @@ typedef struct {
      the NEXT projection: xn_out[m][n] = CT(LN(resid[m])[n] * (1 + xs) + xh) with
      xh = xn_mods[(m/rows_per_mod)*xn_mod_stride + xn_shift_off + n], xs likewise. */
   void* xn_out; const float* xn_mods; int32_t xn_mod_stride, xn_shift_off, xn_scale_off;
+  /* ATTN_SPATIAL (bf16, PLAIN, L == 4, D == 24, H even, N == 3*H*D, M % 4 == 0): the spatial
+     q|k|v projection (W, bias packed as for QKV; qscale; rope = the spatial table, rope_rows
+     >= L) fused with the 4-residue attention of each frame (latent_model.py:466-470,
+     mha.py:255-397): out (CT [M][ldo], ldo >= H*D) = softmax over the bias key (kvb, as in
+     mdg_layer_weights) and the frame's residues with key_mask != 0 (null = all) of q.k, times
+     v.  q|k|v are never written. */
+  const float* kvb; const float* key_mask;
 } mdg_gemm_desc;
 
 int mdg_abi_version(void);

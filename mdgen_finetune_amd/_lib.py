@@ -16,7 +16,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libmdgen_hi
 
 MDG_F32, MDG_BF16 = 0, 1
 MDG_A_PLAIN, MDG_A_LNMOD = 0, 1
-MDG_EPI_STORE, MDG_EPI_GATE_RES, MDG_EPI_QKV, MDG_EPI_EULER = 0, 1, 2, 3
+MDG_EPI_STORE, MDG_EPI_GATE_RES, MDG_EPI_QKV, MDG_EPI_EULER, MDG_EPI_ATTN_SPATIAL = 0, 1, 2, 3, 4
 MDG_ACT_NONE, MDG_ACT_GELU, MDG_ACT_SILU = 0, 1, 2
 MDG_QKV_SPATIAL, MDG_QKV_TEMPORAL = 0, 1
 MDG_PREP_TPS, MDG_PREP_NO_OFFSETS, MDG_PREP_COND_FIRST, MDG_PREP_COND_LAST = 1, 2, 4, 8
@@ -61,6 +61,7 @@ class MdgGemmDesc(ctypes.Structure):
         ("qscale", _f32), ("rope", _vp), ("rope_rows", _i32),
         ("x_in", _vp), ("v_out", _vp), ("dt", _f32), ("n_valid", _i32),
         ("xn_out", _vp), ("xn_mods", _vp), ("xn_mod_stride", _i32), ("xn_shift_off", _i32), ("xn_scale_off", _i32),
+        ("kvb", _vp), ("key_mask", _vp),
     ]
 
 
@@ -85,7 +86,7 @@ SIGNATURES = [
     ("mdg_latents_to_atom14", _i32, [_i32, _i32, _i32, _i32, _i32, _i32] + [_vp] * 12),
 ]
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 _LIB = None
 
 

@@ -66,6 +66,16 @@ size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 // residue counts from which the spatial attention runs on the MFMA (temporal) kernel
 constexpr int kSpatialMfmaMinL = 16;
 
+// bf16 tetrapeptide path: spatial q|k|v projection + attention as one launch
+// (MDG_EPI_ATTN_SPATIAL); MDG_FUSE_SPATIAL=0 selects the two-launch path (A/B knob)
+bool fuse_spatial_attn(const mdg_dims& d) {
+  static const bool on = [] {
+    const char* e = getenv("MDG_FUSE_SPATIAL");
+    return !(e && e[0] == '0');
+  }();
+  return on && d.dtype == MDG_BF16 && d.L == 4 && d.D == 24 && d.H % 2 == 0;
+}
+
 struct WsLayout {
   size_t qkv_s, qkv_t, o, hid, xn, kbias, kbias_s, total;
 };
@@ -188,6 +198,14 @@ int mdg_gemm(const mdg_gemm_desc* g, void* stream) {
         return fail(MDG_E_SHAPE, "gemm QKV: M=%d not a multiple of T*L", g->M);
       if (g->rope && g->rope_rows < (g->qkv_layout == MDG_QKV_SPATIAL ? g->L : g->T))
         return fail(MDG_E_SHAPE, "gemm QKV: rope table too short");
+      break;
+    case MDG_EPI_ATTN_SPATIAL:
+      if (g->dtype != MDG_BF16 || g->a_mode != MDG_A_PLAIN || g->L != 4 || g->D != 24 || g->H <= 0 || g->H % 2 ||
+          g->N != 3 * g->H * g->D || g->M % 4 || g->K % 32 || g->lda % 8 || g->ldw % 8)
+        return fail(MDG_E_SHAPE, "gemm ATTN_SPATIAL: bf16 PLAIN, L=4, D=24, even H, N=3HD, M%%4==0 (M=%d N=%d H=%d D=%d L=%d)",
+                    g->M, g->N, g->H, g->D, g->L);
+      if (!g->out || g->ldo < g->H * g->D || g->ldo % 4 || !g->kvb) return fail(MDG_E_ARG, "gemm ATTN_SPATIAL: out/ldo/kvb");
+      if (g->rope && g->rope_rows < g->L) return fail(MDG_E_SHAPE, "gemm ATTN_SPATIAL: rope table too short");
       break;
     case MDG_EPI_EULER:
       if (g->n_valid <= 0 || g->n_valid > g->N || g->ldo < g->n_valid)
@@ -323,6 +341,11 @@ static int layer_fwd_impl(const mdg_dims* d, const mdg_layer_weights* w, const f
     q.T = T; q.L = L;
     const float* kbias_s = (const float*)(wsb + lay.kbias_s);
     if (int e = mdg_attn_temporal(d->dtype, B * T, L, 1, H, D, qkv_t, kbias_s, w->kvb[0], o, stream)) return e;
+  } else if (fuse_spatial_attn(*d)) {
+    // q|k|v of the 4 residues stay on chip: projection + attention -> o in one launch
+    q.epi = MDG_EPI_ATTN_SPATIAL; q.qscale = qs;
+    q.out = o; q.ldo = C; q.kvb = w->kvb[0]; q.key_mask = mask;
+    if (int e = mdg_gemm(&q, stream)) return e;
   } else {
     q.qkv_layout = MDG_QKV_SPATIAL; q.qkv_out = qkv_s; q.qscale = qs;
     if (int e = mdg_gemm(&q, stream)) return e;
@@ -341,6 +364,7 @@ static int layer_fwd_impl(const mdg_dims* d, const mdg_layer_weights* w, const f
   // ---- temporal attention: x += gate_t * mha_t(mod(LN x))     (latent_model.py:474-486)
   if (!fuse)
     if (int e = ln(3 * C, 4 * C)) return e;
+  q.epi = MDG_EPI_QKV;  // (the spatial launch above may have been the fused ATTN_SPATIAL form)
   q.W = w->wqkv[1]; q.bias = w->bqkv[1];
   q.qkv_layout = MDG_QKV_TEMPORAL; q.qkv_out = qkv_t; q.qscale = qs * 1.4426950408889634f;
   q.rope = rope_t; q.rope_rows = T + 1;

@@ -1034,6 +1034,196 @@ static int rowln_bm() {
   return bm;
 }
 
+// ---------------------------------------------------------------------------------------
+// Spatial q|k|v projection fused with the 4-residue spatial attention (MDG_EPI_ATTN_SPATIAL;
+// latent_model.py:466-470 -> mha.py:161-407 with S = L = 4 keys + the bias_k / bias_v row).
+// A 128-row tile is 32 whole frames; its 144 output columns are the q | k | v rows of one
+// head PAIR (2 x 3 x 24), gathered from the standard packed [3C][C] weight by the loader, so
+// the tile holds every operand the pair's attention needs and q|k|v never reaches HBM: the
+// epilogue computes softmax(q k^T) v per (frame, head) and writes only o [N][C] (bf16).
+//   main loop: 4 waves; wave w owns rows {16w..16w+15} of each 64-row band (frag i = band)
+//              and all 9 16-column fragments; K-step 32, double-buffered global_load_lds into
+//              a chunk-swizzled image (as gemm_bf16_b4_kernel).
+//   epilogue : per band, acc + bias (q also * qscale) -> fp32 LDS [64][148]; then one lane per
+//              (frame, head, half of the head dim, residue): RoPE at position l, partial q.k
+//              over its 12 dims (the other residues' k / v by DPP quad broadcast, the other
+//              half's partial sums by one lane-xor-4 swap), fp32 softmax over the bias key +
+//              the unmasked residues, o = P.V, 3 x 8-B bf16 stores.
+// Requires bf16, L == 4, D == 24, H even; the unfused QKV GEMM + attn_spatial path covers
+// everything else.
+constexpr int kSpaThreads = 256;
+constexpr int kSpaBN = 144;                                   // 2 heads x q|k|v x 24
+constexpr int kSpaLdsSt = kSpaBN + 4;                         // fp32 epilogue row stride
+constexpr size_t kSpaSmem = (size_t)64 * kSpaLdsSt * 4;       // 37888 B (>= 2 x (128+144) x 32 x 2)
+static_assert(2 * (128 + kSpaBN) * 32 * 2 <= kSpaSmem, "ring fits the epilogue stage");
+
+template <int I>
+__device__ __forceinline__ float quad_bc(float x) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), I | (I << 2) | (I << 4) | (I << 6), 0xF, 0xF, true));
+}
+
+__global__ __launch_bounds__(kSpaThreads) void gemm_qkv_attn_spatial_kernel(const mdg_gemm_desc p) {
+  constexpr int D = 24, HP = 2, BM = 128, BN = kSpaBN, BK = 32, NF = BN / 16, HD = HP * D;
+  constexpr int ATILE = BM * BK, STAGE = (BM + BN) * BK, LDS_ST = kSpaLdsSt;
+  typedef __attribute__((address_space(3))) void* lds_ptr_t;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  bf16_t* lds = reinterpret_cast<bf16_t*>(smem);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int M = p.M, K = p.K, C = p.H * D;
+  const int n_tiles = p.H / HP, m_tiles = (M + BM - 1) / BM, nwg = n_tiles * m_tiles;
+  const int xcd = blockIdx.x & 7, loc = blockIdx.x >> 3, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+  const int mt = wg / n_tiles, pair = wg - mt * n_tiles;
+  const int m0 = mt * BM;
+  // tile column r -> packed weight row: segment r / 48 (q, k, v), head pair `pair`
+  auto wrow = [&](int r) { return (r / HD) * C + pair * HD + (r % HD); };
+
+  auto swz_of = [](int r) { return (-(r >> 2)) & 3; };
+  const bf16_t* A = reinterpret_cast<const bf16_t*>(p.A);
+  const bf16_t* W = reinterpret_cast<const bf16_t*>(p.W);
+  // glds instruction i stages 16 tile rows (64 B each); A: i = wave, wave + 4; B: i = wave,
+  // wave + 4, and wave 0 also i = 8
+  const bf16_t* asrc[2];
+  const bf16_t* bsrc[3];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int row = 16 * (wave + 4 * u) + (lane >> 2);
+    asrc[u] = A + (size_t)min(m0 + row, M - 1) * p.lda + (((lane & 3) ^ swz_of(row)) * 8);
+  }
+#pragma unroll
+  for (int u = 0; u < 3; ++u) {
+    const int row = min(16 * (wave + 4 * u) + (lane >> 2), BN - 1);
+    bsrc[u] = W + (size_t)wrow(row) * p.ldw + (((lane & 3) ^ swz_of(row)) * 8);
+  }
+#define MDG_SPA_LOAD(stage_, k0_)                                                                    \
+  {                                                                                                  \
+    bf16_t* sa = lds + (stage_) * STAGE;                                                             \
+    _Pragma("unroll") for (int u = 0; u < 2; ++u)                                                    \
+      __builtin_amdgcn_global_load_lds((const void*)(asrc[u] + (k0_)), (lds_ptr_t)(sa + 16 * (wave + 4 * u) * BK), 16, 0, 0); \
+    _Pragma("unroll") for (int u = 0; u < 2; ++u)                                                    \
+      __builtin_amdgcn_global_load_lds((const void*)(bsrc[u] + (k0_)),                               \
+                                       (lds_ptr_t)(sa + ATILE + 16 * (wave + 4 * u) * BK), 16, 0, 0); \
+    if (wave == 0)                                                                                   \
+      __builtin_amdgcn_global_load_lds((const void*)(bsrc[2] + (k0_)), (lds_ptr_t)(sa + ATILE + 16 * 8 * BK), 16, 0, 0); \
+  }
+
+  f32x4 acc[2][NF];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < NF; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  MDG_SPA_LOAD(0, 0);
+  const int nk = K / BK;
+  const int ch = (lg ^ swz_of(lr)) * 8;  // fragment rows are lr mod 16
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (kt + 1 < nk) MDG_SPA_LOAD(cur ^ 1, (kt + 1) * BK);
+    const bf16_t* As = lds + cur * STAGE;
+    const bf16_t* Bs = As + ATILE;
+    bf16x8 a[2], b[NF];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) a[i] = *reinterpret_cast<const bf16x8*>(As + (i * 64 + 16 * wave + lr) * BK + ch);
+#pragma unroll
+    for (int j = 0; j < NF; ++j) b[j] = *reinterpret_cast<const bf16x8*>(Bs + (j * 16 + lr) * BK + ch);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < NF; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+  }
+#undef MDG_SPA_LOAD
+
+  // ------------------------------------------------------------------ epilogue
+  float bcol[NF], scol[NF];
+#pragma unroll
+  for (int j = 0; j < NF; ++j) {
+    const int r = j * 16 + lr;
+    bcol[j] = p.bias ? p.bias[wrow(r)] : 0.f;
+    scol[j] = (r < HD) ? p.qscale : 1.0f;  // q = (x Wq + bq) * D^-1/2   (mha.py:263)
+  }
+  // attention lane map: residue jr (quad lanes), half dh of the head dim, head hh, frame f
+  const int jr = tid & 3, dh = (tid >> 2) & 1, hh = (tid >> 3) & 1, f = tid >> 4;
+  const int gh = pair * HP + hh, c0 = dh * 12;  // global head; first of the lane's 12 dims
+  const float* kbh = p.kvb + (size_t)gh * 2 * MDG_DP;
+  float* stage = reinterpret_cast<float*>(smem);
+  __syncthreads();  // every wave is done reading the ring
+#pragma unroll
+  for (int band = 0; band < 2; ++band) {
+#pragma unroll
+    for (int j = 0; j < NF; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        stage[(16 * wave + lg * 4 + r) * LDS_ST + j * 16 + lr] = (acc[band][j][r] + bcol[j]) * scol[j];
+    __syncthreads();
+    const int row = f * 4 + jr, m = m0 + band * 64 + row;
+    const float* srow = stage + row * LDS_ST + hh * D + c0;
+    float q[12], k[12], v[12];
+#pragma unroll
+    for (int c = 0; c < 12; c += 4) {
+      const float4 a4 = *reinterpret_cast<const float4*>(srow + c);
+      const float4 b4 = *reinterpret_cast<const float4*>(srow + HD + c);
+      const float4 v4 = *reinterpret_cast<const float4*>(srow + 2 * HD + c);
+      q[c] = a4.x; q[c + 1] = a4.y; q[c + 2] = a4.z; q[c + 3] = a4.w;
+      k[c] = b4.x; k[c + 1] = b4.y; k[c + 2] = b4.z; k[c + 3] = b4.w;
+      v[c] = v4.x; v[c + 1] = v4.y; v[c + 2] = v4.z; v[c + 3] = v4.w;
+    }
+    if (p.rope) {  // fair-esm rotate-half on the pair-interleaved columns, position l = jr
+      constexpr int half = D / 2;
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        const int pi = dh * 6 + i;
+        const float cs = p.rope[jr * half + pi], sn = p.rope[(p.rope_rows + jr) * half + pi];
+        const float q0 = q[2 * i], q1 = q[2 * i + 1], k0 = k[2 * i], k1 = k[2 * i + 1];
+        q[2 * i] = q0 * cs - q1 * sn; q[2 * i + 1] = q1 * cs + q0 * sn;
+        k[2 * i] = k0 * cs - k1 * sn; k[2 * i + 1] = k1 * cs + k0 * sn;
+      }
+    }
+    const float kvalid = (!p.key_mask || p.key_mask[min(m, M - 1)] != 0.f) ? 1.f : 0.f;
+    float sb = 0.f, s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+#pragma unroll
+    for (int c = 0; c < 12; ++c) {
+      sb += q[c] * kbh[c0 + c];
+      s0 += q[c] * quad_bc<0>(k[c]);
+      s1 += q[c] * quad_bc<1>(k[c]);
+      s2 += q[c] * quad_bc<2>(k[c]);
+      s3 += q[c] * quad_bc<3>(k[c]);
+    }
+    sb += __shfl_xor(sb, 4, 64); s0 += __shfl_xor(s0, 4, 64); s1 += __shfl_xor(s1, 4, 64);
+    s2 += __shfl_xor(s2, 4, 64); s3 += __shfl_xor(s3, 4, 64);
+    const float v0 = quad_bc<0>(kvalid), v1 = quad_bc<1>(kvalid), v2 = quad_bc<2>(kvalid), v3 = quad_bc<3>(kvalid);
+    float mx = sb;  // the bias key is never masked (mha.py:273-280)
+    if (v0 != 0.f) mx = fmaxf(mx, s0);
+    if (v1 != 0.f) mx = fmaxf(mx, s1);
+    if (v2 != 0.f) mx = fmaxf(mx, s2);
+    if (v3 != 0.f) mx = fmaxf(mx, s3);
+    const float pb = expf(sb - mx);
+    const float p0 = v0 != 0.f ? expf(s0 - mx) : 0.f, p1 = v1 != 0.f ? expf(s1 - mx) : 0.f;
+    const float p2 = v2 != 0.f ? expf(s2 - mx) : 0.f, p3 = v3 != 0.f ? expf(s3 - mx) : 0.f;
+    const float inv = 1.0f / (pb + p0 + p1 + p2 + p3);
+    float o[12];
+#pragma unroll
+    for (int c = 0; c < 12; ++c)
+      o[c] = (pb * kbh[MDG_DP + c0 + c] + p0 * quad_bc<0>(v[c]) + p1 * quad_bc<1>(v[c]) + p2 * quad_bc<2>(v[c]) +
+              p3 * quad_bc<3>(v[c])) * inv;
+    if (m < M) {
+      bf16_t* op = reinterpret_cast<bf16_t*>(p.out) + (size_t)m * p.ldo + gh * D + c0;
+#pragma unroll
+      for (int c = 0; c < 12; c += 4) st4<bf16_t>(op + c, o[c], o[c + 1], o[c + 2], o[c + 3]);
+    }
+    if (band == 0) __syncthreads();  // band 1 overwrites the stage
+  }
+}
+
+static hipError_t launch_spatial(const mdg_gemm_desc& p, hipStream_t s) {
+  const int nwg = (p.H / 2) * ((p.M + 127) / 128);
+  hipLaunchKernelGGL(gemm_qkv_attn_spatial_kernel, dim3(nwg), dim3(kSpaThreads), kSpaSmem, s, p);
+  return hipGetLastError();
+}
+
 template <typename CT, int BM, int BN, int WM, int AMODE>
 static size_t smem_bytes(int K) {
   constexpr int BK = 64, VEC = 16 / sizeof(CT), LDT = BK + VEC;
@@ -1051,7 +1241,7 @@ static bool stage_fits() {
   return stage <= room;
 }
 
-constexpr int kCfgB4 = 100, kCfgB8 = 101, kCfgB4K32 = 102, kCfgRow = 103;
+constexpr int kCfgB4 = 100, kCfgB8 = 101, kCfgB4K32 = 102, kCfgRow = 103, kCfgSpa = 104;
 
 struct GemmPlan {
   int cfg;  // index into the config table below; -1 = unsupported
@@ -1118,6 +1308,13 @@ GemmPlan gemm_plan(const mdg_gemm_desc& p) {
   const bool bf = p.dtype == MDG_BF16, ln = p.a_mode == MDG_A_LNMOD;
   const bool big = p.M >= 128 * 128;
   int cfg = -1;
+  if (p.epi == MDG_EPI_ATTN_SPATIAL) {  // validated by mdg_gemm: bf16 PLAIN, L 4, D 24, H even
+    g.cfg = kCfgSpa;
+    g.smem = kSpaSmem;
+    g.bm = 128;
+    g.bn = kSpaBN;
+    return g;
+  }
   if (bf && ln) cfg = (p.N % 128 == 0) ? (big ? 0 : 2) : (p.N % 32 == 0 ? (big ? 1 : 3) : -1);
   else if (bf && p.epi == MDG_EPI_GATE_RES && p.xn_out && p.K % 64 == 0 && p.lda % 8 == 0 && p.ldw % 8 == 0 &&
            (p.N == 128 || p.N == 256 || p.N == 384 || p.N == 512)) {
@@ -1169,6 +1366,7 @@ GemmPlan gemm_plan(const mdg_gemm_desc& p) {
 }
 
 hipError_t gemm_launch(const mdg_gemm_desc& p, const GemmPlan& g, hipStream_t s) {
+  if (g.cfg == kCfgSpa) return launch_spatial(p, s);
   if (g.cfg == kCfgRow) {
     if (g.bm == 64) {
       switch (p.N) {

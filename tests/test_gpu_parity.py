@@ -125,18 +125,20 @@ def test_full_size_T1000_matches_oracle(dtype):
     _check(v, ref, dtype)
 
 
-def test_padded_residues_T300_matches_oracle():
-    """Key-padding mask through both attentions at a T that is not a tile multiple."""
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_padded_residues_T300_matches_oracle(dtype):
+    """Key-padding mask through both attentions at a T that is not a tile multiple (bf16: the
+    fused spatial projection + attention kernel with padded residues)."""
     inp, ref, cfg = _oracle_full(300, seed=9, B=2, n_pad=1)
     m, _ = build_model(cfg, "cuda", T=300)
-    m.hip_dtype = "f32"
+    m.hip_dtype = dtype
     from mdgen_finetune_amd.rigid_utils import Rigid, Rotation
 
     g = lambda k: torch.from_numpy(inp[k]).cuda()  # noqa: E731
     with torch.no_grad():
         v = m(g("x"), g("t"), g("mask"), start_frames=Rigid(Rotation(rot_mats=g("rots")), g("trans")),
               x_cond=g("x_cond"), x_cond_mask=g("x_cond_mask"), aatype=g("aatype"))
-    _check(v, ref, "f32")
+    _check(v, ref, dtype)
 
 
 def test_batch_rows_independent_and_graph_equals_eager():

@@ -32,7 +32,9 @@ if os.path.exists(stats):
                      f"{float(r['Percentage']):.2f} |")
     open(os.path.join(out, f"r{rr}_summary.md"), "w").write("\n".join(lines) + "\n")
 
-KMAP = {"gemm_bf16_b4_kernel<2": "gemm_qkv_temporal", "attn_temporal_bf16": "attn_temporal"}
+# the rowln family's last 50 dispatches are bench.roofline's fc2 timing loop
+KMAP = {"gemm_bf16_b4_kernel<2": "gemm_qkv_temporal", "attn_temporal_bf16": "attn_temporal",
+        "gemm_rowln_kernel": "gemm_fc2_rowln"}
 res = collections.defaultdict(dict)
 for cname, scale in (("FETCH_SIZE", 2 * 1024), ("WRITE_SIZE", 1024)):
     p = os.path.join(REPO, "gpurun_out", "pmc_roof", f"{cname}_counter_collection.csv")

@@ -1,5 +1,5 @@
-"""Launch the two roofline kernels of bench.py (temporal q|k|v GEMM, temporal attention) at
-the bench shape after one eager sampling window, for rocprofv3 counter passes
+"""Launch the roofline kernels of bench.py (fc2 row-LN GEMM, temporal q|k|v GEMM, temporal
+attention) at the bench's per-lane shape after one eager sampling window, for rocprofv3 counter passes
 (tools/roof_pmc.sh).  Usage: python tools/roof_kernels.py [B T L]"""
 import os
 import sys
@@ -21,7 +21,7 @@ zs, kw, _ = bench.inputs(B, T, L, seed=100, device=dev)
 with torch.no_grad():
     eng.sample_euler(zs, num_steps=3, use_graph=False, **kw)
     torch.cuda.synchronize()
-    r1, r2 = bench.roofline(eng, eng._state(B, T, L), "bf16", B, T, L)
+    roofs = bench.roofline(eng, eng._state(B, T, L), "bf16", B, T, L)
 torch.cuda.synchronize()
-print(r1)
-print(r2)
+for r in roofs.values():
+    print(r)

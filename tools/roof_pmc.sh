@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 mkdir -p gpurun_out/pmc_roof
 for C in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 400 rocprofv3 --pmc $C --kernel-include-regex "gemm_bf16_b4|attn_temporal_bf16" \
+  timeout -k 10 400 rocprofv3 --pmc $C --kernel-include-regex "gemm_bf16_b4|attn_temporal_bf16|gemm_rowln" \
     --output-format csv -d gpurun_out/pmc_roof -o $C -- python tools/roof_kernels.py \
     > gpurun_out/pmc_roof/log_$C.txt 2>&1 || exit $?
 done
