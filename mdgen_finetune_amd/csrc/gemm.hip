@@ -845,6 +845,29 @@ __global__ __launch_bounds__(kRowThreads, BM == 64 ? 4 : 1) void gemm_rowln_kern
                                        (lds_ptr_t)(sa + ATILE + 16 * (wave * WLD + i) * BK), 16, 0, 0); \
   }
 
+  // Epilogue work unit u = (band u / UPB, row group u % UPB): RG rows of this wave.  Their h and
+  // gate rows are loaded one unit AHEAD of use (unit 0 before the main loop, so its HBM
+  // latency hides under the K loop; unit u+1 while unit u computes), so the epilogue pays the
+  // residual-read latency once instead of once per band.
+  constexpr int UPB = 4 / RG, NU = (BM / 32) * UPB;
+  const float inv_rpm = 1.0f / (float)p.rows_per_mod;
+  auto load_unit = [&](int u, float2 (&hv)[RG][NE], float2 (&gv)[RG][NE]) {
+#pragma unroll
+    for (int rr = 0; rr < RG; ++rr) {
+      const int m = min(m0 + (u / UPB) * 32 + wave * 4 + (u % UPB) * RG + rr, M - 1);
+      const float* hr = p.resid + (size_t)m * p.ldr;
+      const float* gr = p.gate ? p.gate + (size_t)fdiv(m, p.rows_per_mod, inv_rpm) * p.mod_stride + p.gate_off : nullptr;
+#pragma unroll
+      for (int e = 0; e < NE; ++e) {
+        const int k = 2 * lane + 128 * e;
+        hv[rr][e] = *reinterpret_cast<const float2*>(hr + k);
+        gv[rr][e] = gr ? *reinterpret_cast<const float2*>(gr + k) : make_float2(1.f, 1.f);
+      }
+    }
+  };
+  float2 hv[RG][NE], gv[RG][NE];
+  load_unit(0, hv, gv);
+
   f32x4 acc[4][NT];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -888,7 +911,7 @@ __global__ __launch_bounds__(kRowThreads, BM == 64 ? 4 : 1) void gemm_rowln_kern
 
   // ------------------------------------------------------------------ epilogue
   float* stage = reinterpret_cast<float*>(smem);
-  const float inv_rpm = 1.0f / (float)p.rows_per_mod, invN = 1.0f / (float)NCOL;
+  const float invN = 1.0f / (float)NCOL;
   float2 bb[NE];
 #pragma unroll
   for (int e = 0; e < NE; ++e)
@@ -913,19 +936,9 @@ __global__ __launch_bounds__(kRowThreads, BM == 64 ? 4 : 1) void gemm_rowln_kern
     // rows of this wave in groups of RG (fewer live registers at BM 64, two blocks per CU)
 #pragma unroll 1
     for (int g0 = 0; g0 < 4; g0 += RG) {
-      float2 hv[RG][NE], gv[RG][NE];
-  #pragma unroll
-      for (int rr = 0; rr < RG; ++rr) {
-        const int m = min(m0 + band * 32 + wave * 4 + g0 + rr, M - 1);
-        const float* hr = p.resid + (size_t)m * p.ldr;
-        const float* gr = p.gate ? p.gate + (size_t)fdiv(m, p.rows_per_mod, inv_rpm) * p.mod_stride + p.gate_off : nullptr;
-  #pragma unroll
-        for (int e = 0; e < NE; ++e) {
-          const int k = 2 * lane + 128 * e;
-          hv[rr][e] = *reinterpret_cast<const float2*>(hr + k);
-          gv[rr][e] = gr ? *reinterpret_cast<const float2*>(gr + k) : make_float2(1.f, 1.f);
-        }
-      }
+      const int u = band * UPB + g0 / RG;
+      float2 hn[RG][NE], gn[RG][NE];
+      if (u + 1 < NU) load_unit(u + 1, hn, gn);
       const int mb0 = min(m0 + band * 32 + wave * 4 + g0, M - 1), mb3 = min(mb0 + RG - 1, M - 1);
       const int b0 = fdiv(mb0, p.rows_per_mod, inv_rpm);
       const bool one_b = fdiv(mb3, p.rows_per_mod, inv_rpm) == b0;  // the 4 rows share a batch entry
@@ -1004,6 +1017,13 @@ __global__ __launch_bounds__(kRowThreads, BM == 64 ? 4 : 1) void gemm_rowln_kern
           }
         }
       }
+#pragma unroll
+      for (int rr = 0; rr < RG; ++rr)
+#pragma unroll
+        for (int e = 0; e < NE; ++e) {
+          hv[rr][e] = hn[rr][e];
+          gv[rr][e] = gn[rr][e];
+        }
     }
     __syncthreads();
   }

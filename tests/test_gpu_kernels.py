@@ -191,7 +191,7 @@ def _attn_ref(q, k, v, kb, vb, keyvalid, base2):
 
 
 @pytest.mark.parametrize("dt", ["f32", "bf16"])
-@pytest.mark.parametrize("T", [1, 63, 64, 129, 1000, 1300])
+@pytest.mark.parametrize("T", [1, 63, 64, 129, 600, 1000, 1024, 1300])
 def test_attn_temporal(lib, dt, T):
     from mdgen_finetune_amd import _lib
 
