@@ -30,6 +30,9 @@ hipError_t ln_mod_launch(int dtype, int M, int C, const float* h, const float* m
                          int rows_per_mod, int shift_off, int scale_off, float eps, void* xn,
                          hipStream_t s);
 hipError_t set_vpad_launch(int dtype, void* v, size_t rows, int D, hipStream_t s);
+hipError_t embed_ln_launch(int N, int TL, int L, int C, int K, const float* x, const float* Wt, const float* base,
+                           const float* ipa, const float* mods, int mod_stride, int shift_off, int scale_off,
+                           float eps, float* h, void* xn, hipStream_t s);
 hipError_t prep_latents_launch(int B, int T, int L, int lat, int tps, int no_offsets, int cond_mode,
                                int cond_interval, const float* rots, const float* trans, const float* torsions,
                                float* latents, float* x_cond, int64_t* cond_mask, hipStream_t s);
@@ -411,18 +414,21 @@ int mdg_denoise_step(const mdg_model* m, const mdg_step_io* io, const float* mas
   if (!io->x_in || !io->base || !io->mods || !io->mods_final || !io->h)
     return fail(MDG_E_ARG, "denoise_step: null io pointer");
   const int N = d->B * d->T * d->L;
-  if (int e = mdg_embed(N, d->T, d->L, d->C, d->latent, io->x_in, m->w_l2e_t, nullptr, io->base,
-                        nullptr, nullptr, nullptr, io->ipa, io->h, stream))
-    return e;
   const size_t mstride = (size_t)d->B * 9 * d->C;
   const WsLayout lay = ws_layout(*d);
   void* xn = (char*)ws + lay.xn;
   const int C = d->C;
   const bool fuse = d->dtype == MDG_BF16 && (C == 128 || C == 256 || C == 384 || C == 512);
-  if (fuse)  // layer 0's spatial LN input; later ones come out of the fused fc2 epilogues
-    if (int e = hip_check(mdg::ln_mod_launch(d->dtype, N, C, io->h, io->mods, 9 * C, d->T * d->L, 0, C, 1e-6f, xn,
-                                             (hipStream_t)stream), "ln_mod(layer 0)"))
+  if (fuse) {  // embedding + layer 0's spatial LN input in one pass; later LN inputs come out
+               // of the fused fc2 epilogues
+    if (int e = hip_check(mdg::embed_ln_launch(N, d->T * d->L, d->L, C, d->latent, io->x_in, m->w_l2e_t, io->base,
+                                               io->ipa, io->mods, 9 * C, 0, C, 1e-6f, io->h, xn,
+                                               (hipStream_t)stream), "embed_ln"))
       return e;
+  } else if (int e = mdg_embed(N, d->T, d->L, d->C, d->latent, io->x_in, m->w_l2e_t, nullptr, io->base,
+                               nullptr, nullptr, nullptr, io->ipa, io->h, stream)) {
+    return e;
+  }
   for (int i = 0; i < d->num_layers; ++i) {
     const bool last = i + 1 == d->num_layers;
     const LnHandoff ho{fuse, last ? io->mods_final : io->mods + (i + 1) * mstride, last ? 2 * C : 9 * C, 0, C};

@@ -214,6 +214,140 @@ hipError_t embed_launch(int N, int T, int L, int C, int K, const float* x, const
   return hipGetLastError();
 }
 
+// Token embedding fused with layer 0's spatial LayerNorm (bf16 path, C = 128 * NE):
+//   h  = x . W_l2e^T + (base + ipa[b, l])          (fp32, latent_model.py:242-255; same FMA
+//        order as embed_kernel: the K products from 0, then the x-independent terms)
+//   xn = LN(h) * (1 + scale[b]) + shift[b]         (bf16, eps 1e-6, latent_model.py:467)
+// One wave owns 4 rows; lane holds columns 2*lane + 128e (float2, e < NE), so every row is
+// read and written with full 512-B wave accesses and the row statistics are two wave
+// reductions.  W_l2e^T [K][C] is staged once per block in LDS; x[n][0..K) is one dword per lane
+// broadcast by v_readlane.  Every global operand of the 4 rows is issued before any is used.
+// Replaces embed_kernel + ln_mod_kernel (49 MB re-read of h gone).
+template <int NE>
+__global__ __launch_bounds__(256) void embed_ln_kernel(int N, int TL, int L, int K, const float* __restrict__ x,
+                                                       const float* __restrict__ Wt, const float* __restrict__ base,
+                                                       const float* __restrict__ ipa, const float* __restrict__ mods,
+                                                       int mod_stride, int shift_off, int scale_off, float eps,
+                                                       float* __restrict__ h, bf16_t* __restrict__ xn) {
+  constexpr int C = 128 * NE, R = 4;
+  extern __shared__ __attribute__((aligned(16))) float wl[];  // [K][C]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int i = tid; i < K * C / 4; i += 256) reinterpret_cast<float4*>(wl)[i] = reinterpret_cast<const float4*>(Wt)[i];
+  __syncthreads();
+  const float invC = 1.0f / (float)C;
+  const int groups = (N + 16 - 1) / 16;
+  for (int gi = blockIdx.x; gi < groups; gi += gridDim.x) {
+    const int r0 = gi * 16 + wave * R;
+    float2 hv[R][NE], sv[R][NE], cv[R][NE];
+    float xv[R];
+#pragma unroll
+    for (int rr = 0; rr < R; ++rr) {
+      const int n = min(r0 + rr, N - 1), b = n / TL, l = n % L;
+      xv[rr] = lane < K ? x[(size_t)n * K + lane] : 0.f;
+      const float* mr = mods + (size_t)b * mod_stride;
+#pragma unroll
+      for (int e = 0; e < NE; ++e) {
+        const int k = 2 * lane + 128 * e;
+        float2 t = *reinterpret_cast<const float2*>(base + (size_t)n * C + k);
+        if (ipa) {
+          const float2 u = *reinterpret_cast<const float2*>(ipa + ((size_t)b * L + l) * C + k);
+          t.x += u.x; t.y += u.y;
+        }
+        hv[rr][e] = t;
+        sv[rr][e] = *reinterpret_cast<const float2*>(mr + scale_off + k);
+        cv[rr][e] = *reinterpret_cast<const float2*>(mr + shift_off + k);
+      }
+    }
+    float2 a[R][NE];
+#pragma unroll
+    for (int rr = 0; rr < R; ++rr)
+#pragma unroll
+      for (int e = 0; e < NE; ++e) a[rr][e] = make_float2(0.f, 0.f);
+    for (int j = 0; j < K; ++j) {
+      float2 wv[NE];
+#pragma unroll
+      for (int e = 0; e < NE; ++e) wv[e] = *reinterpret_cast<const float2*>(wl + j * C + 2 * lane + 128 * e);
+#pragma unroll
+      for (int rr = 0; rr < R; ++rr) {
+        const float xs = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xv[rr]), j));
+#pragma unroll
+        for (int e = 0; e < NE; ++e) {
+          a[rr][e].x += xs * wv[e].x;
+          a[rr][e].y += xs * wv[e].y;
+        }
+      }
+    }
+    float sum[R], ss[R];
+#pragma unroll
+    for (int rr = 0; rr < R; ++rr) {
+      float t = 0.f;
+#pragma unroll
+      for (int e = 0; e < NE; ++e) {
+        hv[rr][e].x = a[rr][e].x + hv[rr][e].x;
+        hv[rr][e].y = a[rr][e].y + hv[rr][e].y;
+        t += hv[rr][e].x + hv[rr][e].y;
+      }
+      sum[rr] = t;
+      if (r0 + rr < N) {
+#pragma unroll
+        for (int e = 0; e < NE; ++e)
+          *reinterpret_cast<float2*>(h + (size_t)(r0 + rr) * C + 2 * lane + 128 * e) = hv[rr][e];
+      }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1)
+#pragma unroll
+      for (int rr = 0; rr < R; ++rr) sum[rr] += __shfl_xor(sum[rr], o, 64);
+#pragma unroll
+    for (int rr = 0; rr < R; ++rr) {
+      sum[rr] *= invC;
+      float t = 0.f;
+#pragma unroll
+      for (int e = 0; e < NE; ++e) {
+        const float d0 = hv[rr][e].x - sum[rr], d1 = hv[rr][e].y - sum[rr];
+        t += d0 * d0 + d1 * d1;
+      }
+      ss[rr] = t;
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1)
+#pragma unroll
+      for (int rr = 0; rr < R; ++rr) ss[rr] += __shfl_xor(ss[rr], o, 64);
+#pragma unroll
+    for (int rr = 0; rr < R; ++rr) {
+      if (r0 + rr >= N) continue;
+      const float rs = 1.0f / sqrtf(ss[rr] * invC + eps);
+#pragma unroll
+      for (int e = 0; e < NE; ++e) {
+        typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+        bf16x2 pr;
+        pr[0] = (bf16_t)((hv[rr][e].x - sum[rr]) * rs * (1.0f + sv[rr][e].x) + cv[rr][e].x);
+        pr[1] = (bf16_t)((hv[rr][e].y - sum[rr]) * rs * (1.0f + sv[rr][e].y) + cv[rr][e].y);
+        *reinterpret_cast<bf16x2*>(xn + (size_t)(r0 + rr) * C + 2 * lane + 128 * e) = pr;
+      }
+    }
+  }
+}
+
+hipError_t embed_ln_launch(int N, int TL, int L, int C, int K, const float* x, const float* Wt, const float* base,
+                           const float* ipa, const float* mods, int mod_stride, int shift_off, int scale_off,
+                           float eps, float* h, void* xn, hipStream_t s) {
+  if (K > 64 || (C != 128 && C != 256 && C != 384 && C != 512)) return hipErrorInvalidValue;
+  const int groups = (N + 15) / 16, grid = groups < 1024 ? groups : 1024;
+  const size_t smem = (size_t)K * C * 4;
+#define MDG_ELN(NE)                                                                                              \
+  hipLaunchKernelGGL((embed_ln_kernel<NE>), dim3(grid), dim3(256), smem, s, N, TL, L, K, x, Wt, base, ipa, mods, \
+                     mod_stride, shift_off, scale_off, eps, h, (bf16_t*)xn)
+  switch (C) {
+    case 128: MDG_ELN(1); break;
+    case 256: MDG_ELN(2); break;
+    case 384: MDG_ELN(3); break;
+    default: MDG_ELN(4); break;
+  }
+#undef MDG_ELN
+  return hipGetLastError();
+}
+
 hipError_t ln_mod_launch(int dtype, int M, int C, const float* h, const float* mods, int mod_stride,
                          int rows_per_mod, int shift_off, int scale_off, float eps, void* xn,
                          hipStream_t s) {
