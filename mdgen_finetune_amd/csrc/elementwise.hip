@@ -223,13 +223,14 @@ hipError_t embed_launch(int N, int T, int L, int C, int K, const float* x, const
 // reductions.  W_l2e^T [K][C] is staged once per block in LDS; x[n][0..K) is one dword per lane
 // broadcast by v_readlane.  Every global operand of the 4 rows is issued before any is used.
 // Replaces embed_kernel + ln_mod_kernel (49 MB re-read of h gone).
-template <int NE>
-__global__ __launch_bounds__(256) void embed_ln_kernel(int N, int TL, int L, int K, const float* __restrict__ x,
+template <int NE, int KC>  // KC: compile-time latent width (0 = runtime K)
+__global__ __launch_bounds__(256, 4) void embed_ln_kernel(int N, int TL, int L, int Kr, const float* __restrict__ x,
                                                        const float* __restrict__ Wt, const float* __restrict__ base,
                                                        const float* __restrict__ ipa, const float* __restrict__ mods,
                                                        int mod_stride, int shift_off, int scale_off, float eps,
                                                        float* __restrict__ h, bf16_t* __restrict__ xn) {
   constexpr int C = 128 * NE, R = 4;
+  const int K = KC ? KC : Kr;
   extern __shared__ __attribute__((aligned(16))) float wl[];  // [K][C]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   for (int i = tid; i < K * C / 4; i += 256) reinterpret_cast<float4*>(wl)[i] = reinterpret_cast<const float4*>(Wt)[i];
@@ -238,13 +239,23 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(int N, int TL, int L, int
   const int groups = (N + 16 - 1) / 16;
   for (int gi = blockIdx.x; gi < groups; gi += gridDim.x) {
     const int r0 = gi * 16 + wave * R;
-    float2 hv[R][NE], sv[R][NE], cv[R][NE];
+    float2 hv[R][NE], sv[NE], cv[NE];
     float xv[R];
+    // shift / scale of the first row's batch entry; a row of another entry (a group that
+    // straddles a trajectory boundary) reloads its own below
+    const int b0 = min(r0, N - 1) / TL;
+    {
+      const float* mr = mods + (size_t)b0 * mod_stride;
+#pragma unroll
+      for (int e = 0; e < NE; ++e) {
+        sv[e] = *reinterpret_cast<const float2*>(mr + scale_off + 2 * lane + 128 * e);
+        cv[e] = *reinterpret_cast<const float2*>(mr + shift_off + 2 * lane + 128 * e);
+      }
+    }
 #pragma unroll
     for (int rr = 0; rr < R; ++rr) {
       const int n = min(r0 + rr, N - 1), b = n / TL, l = n % L;
       xv[rr] = lane < K ? x[(size_t)n * K + lane] : 0.f;
-      const float* mr = mods + (size_t)b * mod_stride;
 #pragma unroll
       for (int e = 0; e < NE; ++e) {
         const int k = 2 * lane + 128 * e;
@@ -254,8 +265,6 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(int N, int TL, int L, int
           t.x += u.x; t.y += u.y;
         }
         hv[rr][e] = t;
-        sv[rr][e] = *reinterpret_cast<const float2*>(mr + scale_off + k);
-        cv[rr][e] = *reinterpret_cast<const float2*>(mr + shift_off + k);
       }
     }
     float2 a[R][NE];
@@ -263,7 +272,9 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(int N, int TL, int L, int
     for (int rr = 0; rr < R; ++rr)
 #pragma unroll
       for (int e = 0; e < NE; ++e) a[rr][e] = make_float2(0.f, 0.f);
-    for (int j = 0; j < K; ++j) {
+#pragma unroll 7
+    for (int j = 0; j < (KC ? KC : 64); ++j) {
+      if (!KC && j >= K) break;
       float2 wv[NE];
 #pragma unroll
       for (int e = 0; e < NE; ++e) wv[e] = *reinterpret_cast<const float2*>(wl + j * C + 2 * lane + 128 * e);
@@ -317,12 +328,21 @@ __global__ __launch_bounds__(256) void embed_ln_kernel(int N, int TL, int L, int
     for (int rr = 0; rr < R; ++rr) {
       if (r0 + rr >= N) continue;
       const float rs = 1.0f / sqrtf(ss[rr] * invC + eps);
+      const int b = (r0 + rr) / TL;
+      if (b != b0) {
+        const float* mr = mods + (size_t)b * mod_stride;
+#pragma unroll
+        for (int e = 0; e < NE; ++e) {
+          sv[e] = *reinterpret_cast<const float2*>(mr + scale_off + 2 * lane + 128 * e);
+          cv[e] = *reinterpret_cast<const float2*>(mr + shift_off + 2 * lane + 128 * e);
+        }
+      }
 #pragma unroll
       for (int e = 0; e < NE; ++e) {
         typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
         bf16x2 pr;
-        pr[0] = (bf16_t)((hv[rr][e].x - sum[rr]) * rs * (1.0f + sv[rr][e].x) + cv[rr][e].x);
-        pr[1] = (bf16_t)((hv[rr][e].y - sum[rr]) * rs * (1.0f + sv[rr][e].y) + cv[rr][e].y);
+        pr[0] = (bf16_t)((hv[rr][e].x - sum[rr]) * rs * (1.0f + sv[e].x) + cv[e].x);
+        pr[1] = (bf16_t)((hv[rr][e].y - sum[rr]) * rs * (1.0f + sv[e].y) + cv[e].y);
         *reinterpret_cast<bf16x2*>(xn + (size_t)(r0 + rr) * C + 2 * lane + 128 * e) = pr;
       }
     }
@@ -333,17 +353,17 @@ hipError_t embed_ln_launch(int N, int TL, int L, int C, int K, const float* x, c
                            const float* ipa, const float* mods, int mod_stride, int shift_off, int scale_off,
                            float eps, float* h, void* xn, hipStream_t s) {
   if (K > 64 || (C != 128 && C != 256 && C != 384 && C != 512)) return hipErrorInvalidValue;
-  const int groups = (N + 15) / 16, grid = groups < 1024 ? groups : 1024;
+  const int groups = (N + 15) / 16, grid = groups < 65535 ? groups : 65535;
   const size_t smem = (size_t)K * C * 4;
-#define MDG_ELN(NE)                                                                                              \
-  hipLaunchKernelGGL((embed_ln_kernel<NE>), dim3(grid), dim3(256), smem, s, N, TL, L, K, x, Wt, base, ipa, mods, \
-                     mod_stride, shift_off, scale_off, eps, h, (bf16_t*)xn)
-  switch (C) {
-    case 128: MDG_ELN(1); break;
-    case 256: MDG_ELN(2); break;
-    case 384: MDG_ELN(3); break;
-    default: MDG_ELN(4); break;
-  }
+#define MDG_ELN(NE, KC)                                                                                        \
+  hipLaunchKernelGGL((embed_ln_kernel<NE, KC>), dim3(grid), dim3(256), smem, s, N, TL, L, K, x, Wt, base, ipa, \
+                     mods, mod_stride, shift_off, scale_off, eps, h, (bf16_t*)xn)
+  if (C == 384 && K == 21) MDG_ELN(3, 21);        // the tetrapeptide / ATLAS latent
+  else if (C == 384 && K == 28) MDG_ELN(3, 28);   // TPS latent
+  else if (C == 128) MDG_ELN(1, 0);
+  else if (C == 256) MDG_ELN(2, 0);
+  else if (C == 384) MDG_ELN(3, 0);
+  else MDG_ELN(4, 0);
 #undef MDG_ELN
   return hipGetLastError();
 }
