@@ -30,6 +30,38 @@ if os.path.exists(stats):
     for r in rows[:20]:
         lines.append(f"| `{r['Name'][:90]}` | {r['Calls']} | {float(r['AverageNs']) / 1e3:.1f} | "
                      f"{float(r['Percentage']):.2f} |")
+    trace = os.path.join(REPO, "gpurun_out", "prof", "run_kernel_trace.csv")
+    if os.path.exists(trace):
+        # bench.roofline times each roofline kernel in a loop of 50 launches after the timed
+        # windows (plus one warm-up launch): those are the last 50 dispatches of its name; the
+        # rest ran inside the hipGraph windows.
+        pats = (("gemm_rowln_kernel", "gemm_fc2_rowln"), ("gemm_bf16_b4_kernel<2", "gemm_qkv_temporal"),
+                ("attn_temporal_bf16", "attn_temporal"))
+        per = collections.defaultdict(list)
+        for r in csv.DictReader(open(trace)):
+            for pat, name in pats:
+                if pat in r["Kernel_Name"]:
+                    per[name].append((int(r["Dispatch_Id"]), (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3))
+        bench_live = {}
+        bl = os.path.join(REPO, "gpurun_out", "prof", "bench_prof.log")
+        if os.path.exists(bl):
+            try:
+                d = json.loads([x for x in open(bl).read().splitlines() if x.startswith("{")][-1])
+                for rf in [d["roofline"]] + d.get("roofline_more", []):
+                    bench_live[rf["kernel"]] = rf["avg_launch_us"]
+            except Exception:
+                pass
+        lines += ["", "## Bench roofline kernels: rocprof vs the bench's live HIP-event timing",
+                  "", "| roofline kernel | rocprof avg of the 50 timed dispatches (us) | bench live avg (us) | in-graph avg (us) |",
+                  "|---|---|---|---|"]
+        for pat, name in pats:
+            v = sorted(per.get(name, []))
+            if len(v) < 60:
+                continue
+            loop = [x[1] for x in v[-50:]]
+            graph = [x[1] for x in v[:-51]]
+            lines.append(f"| {name} | {sum(loop) / len(loop):.1f} | {bench_live.get(name, 'n/a')} | "
+                         f"{sum(graph) / len(graph):.1f} |")
     open(os.path.join(out, f"r{rr}_summary.md"), "w").write("\n".join(lines) + "\n")
 
 # the rowln family's last 50 dispatches are bench.roofline's fc2 timing loop
