@@ -63,6 +63,10 @@ if __name__ == "__main__":
             for K in (384, 1536):
                 run(M, 384, K, 0, 1, rowln=True)
         _s.exit(0)
+    if len(_s.argv) > 1 and _s.argv[1] == "rowlnk":  # row-LN GEMM K sweep: epilogue vs main loop
+        for K in (64, 128, 384, 768, 1536):
+            run(32000, 384, K, 0, 1, rowln=True)
+        _s.exit(0)
     if len(_s.argv) > 1 and _s.argv[1] == "b4":  # the 128x128 streamed-A shapes (fc1, qkv)
         for M in (32000, 64000):
             run(M, 1536, 384, 0, 0, act=1)
