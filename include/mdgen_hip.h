@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define MDG_ABI_VERSION 7
+#define MDG_ABI_VERSION 8
 #define MDG_MAX_LAYERS 16
 #define MDG_DP 32 /* padded head dim of every attention operand buffer (head_dim <= 31) */
 
@@ -173,6 +173,12 @@ int mdg_final_euler(int32_t dtype, int32_t N, int32_t rows_per_b, int32_t C, int
 /* Whole denoising step: embed -> num_layers x layer -> FinalLayer -> Euler. */
 int mdg_denoise_step(const mdg_model* m, const mdg_step_io* io, const float* mask, void* ws,
                      void* stream);
+/* The same step in pieces: layers [first_layer, last_layer); first_layer == 0 includes the
+   embedding, last_layer == num_layers the FinalLayer + Euler update.  Calls covering
+   [0, k) then [k, num_layers) on one stream equal mdg_denoise_step bit for bit; the split
+   lets a caller record an event mid-step (the engine offsets concurrent lanes by it). */
+int mdg_denoise_step_layers(const mdg_model* m, const mdg_step_io* io, const float* mask, void* ws,
+                            int32_t first_layer, int32_t last_layer, void* stream);
 
 /* Building blocks (exposed for unit tests and for the conditioning precompute). */
 int mdg_gemm(const mdg_gemm_desc* g, void* stream);

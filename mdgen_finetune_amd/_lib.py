@@ -79,6 +79,8 @@ SIGNATURES = [
                              _vp, _vp, _vp, _vp]),
     ("mdg_final_euler", _i32, [_i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _vp]),
     ("mdg_denoise_step", _i32, [ctypes.POINTER(MdgModel), ctypes.POINTER(MdgStepIO), _vp, _vp, _vp]),
+    ("mdg_denoise_step_layers", _i32, [ctypes.POINTER(MdgModel), ctypes.POINTER(MdgStepIO), _vp, _vp, _i32, _i32,
+                                       _vp]),
     ("mdg_gemm", _i32, [ctypes.POINTER(MdgGemmDesc), _vp]),
     ("mdg_attn_spatial", _i32, [_i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
     ("mdg_attn_temporal", _i32, [_i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
@@ -86,7 +88,7 @@ SIGNATURES = [
     ("mdg_latents_to_atom14", _i32, [_i32, _i32, _i32, _i32, _i32, _i32] + [_vp] * 12),
 ]
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 _LIB = None
 
 

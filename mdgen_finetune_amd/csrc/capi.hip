@@ -406,8 +406,10 @@ int mdg_layer_fwd(const mdg_dims* d, const mdg_layer_weights* w, const float* ro
   return layer_fwd_impl(d, w, rope_l, rope_t, mods, mask, h, ws, stream, LnHandoff{false, nullptr, 0, 0, 0});
 }
 
-int mdg_denoise_step(const mdg_model* m, const mdg_step_io* io, const float* mask, void* ws,
-                     void* stream) {
+// Layers [first, last) of one denoising step; `first == 0` also runs the embedding (+ layer
+// 0's LN input), `last == num_layers` also the FinalLayer + Euler update.
+static int denoise_range(const mdg_model* m, const mdg_step_io* io, const float* mask, void* ws, int first, int last,
+                         void* stream) {
   if (!m || !io) return fail(MDG_E_ARG, "denoise_step: null model/io");
   const mdg_dims* d = &m->dims;
   if (int e = check_dims(d)) return e;
@@ -419,8 +421,11 @@ int mdg_denoise_step(const mdg_model* m, const mdg_step_io* io, const float* mas
   void* xn = (char*)ws + lay.xn;
   const int C = d->C;
   const bool fuse = d->dtype == MDG_BF16 && (C == 128 || C == 256 || C == 384 || C == 512);
-  if (fuse) {  // embedding + layer 0's spatial LN input in one pass; later LN inputs come out
-               // of the fused fc2 epilogues
+  if (first < 0 || last > d->num_layers || first > last) return fail(MDG_E_ARG, "denoise_step: layer range");
+  if (first > 0) {
+    // resumes a step whose layers [0, first) already ran: h and (fused path) xn are in place
+  } else if (fuse) {  // embedding + layer 0's spatial LN input in one pass; later LN inputs
+                      // come out of the fused fc2 epilogues
     if (int e = hip_check(mdg::embed_ln_launch(N, d->T * d->L, d->L, C, d->latent, io->x_in, m->w_l2e_t, io->base,
                                                io->ipa, io->mods, 9 * C, 0, C, 1e-6f, io->h, xn,
                                                (hipStream_t)stream), "embed_ln"))
@@ -429,14 +434,16 @@ int mdg_denoise_step(const mdg_model* m, const mdg_step_io* io, const float* mas
                                nullptr, nullptr, nullptr, io->ipa, io->h, stream)) {
     return e;
   }
-  for (int i = 0; i < d->num_layers; ++i) {
-    const bool last = i + 1 == d->num_layers;
-    const LnHandoff ho{fuse, last ? io->mods_final : io->mods + (i + 1) * mstride, last ? 2 * C : 9 * C, 0, C};
+  for (int i = first; i < last; ++i) {
+    const bool final_next = i + 1 == d->num_layers;  // the next LN input is the FinalLayer's
+    const LnHandoff ho{fuse, final_next ? io->mods_final : io->mods + (i + 1) * mstride, final_next ? 2 * C : 9 * C,
+                       0, C};
     if (!m->layers[i].wqkv[0]) return fail(MDG_E_ARG, "denoise_step: layer %d weights missing", i);
     if (int e = layer_fwd_impl(d, &m->layers[i], m->rope_l, m->rope_t, io->mods + i * mstride, mask, io->h, ws,
                                stream, ho))
       return e;
   }
+  if (last < d->num_layers) return 0;
   // FinalLayer: LN + modulate (layers.py:73) into xn (already there on the fused path), then
   // the EULER-epilogue GEMM
   if (!fuse)
@@ -453,6 +460,16 @@ int mdg_denoise_step(const mdg_model* m, const mdg_step_io* io, const float* mas
   g.out = io->x_out; g.ldo = d->latent; g.x_in = io->x_in; g.v_out = io->v_out; g.dt = io->dt;
   g.n_valid = d->latent;
   return mdg_gemm(&g, stream);
+}
+
+int mdg_denoise_step(const mdg_model* m, const mdg_step_io* io, const float* mask, void* ws, void* stream) {
+  if (!m) return fail(MDG_E_ARG, "denoise_step: null model/io");
+  return denoise_range(m, io, mask, ws, 0, m->dims.num_layers, stream);
+}
+
+int mdg_denoise_step_layers(const mdg_model* m, const mdg_step_io* io, const float* mask, void* ws,
+                            int32_t first_layer, int32_t last_layer, void* stream) {
+  return denoise_range(m, io, mask, ws, first_layer, last_layer, stream);
 }
 
 int mdg_prep_latents(int32_t B, int32_t T, int32_t L, int32_t latent, int32_t flags, int32_t cond_interval,

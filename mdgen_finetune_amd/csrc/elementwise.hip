@@ -272,9 +272,7 @@ __global__ __launch_bounds__(256, 4) void embed_ln_kernel(int N, int TL, int L, 
     for (int rr = 0; rr < R; ++rr)
 #pragma unroll
       for (int e = 0; e < NE; ++e) a[rr][e] = make_float2(0.f, 0.f);
-#pragma unroll 7
-    for (int j = 0; j < (KC ? KC : 64); ++j) {
-      if (!KC && j >= K) break;
+    auto kstep = [&](int j) {
       float2 wv[NE];
 #pragma unroll
       for (int e = 0; e < NE; ++e) wv[e] = *reinterpret_cast<const float2*>(wl + j * C + 2 * lane + 128 * e);
@@ -287,6 +285,12 @@ __global__ __launch_bounds__(256, 4) void embed_ln_kernel(int N, int TL, int L, 
           a[rr][e].y += xs * wv[e].y;
         }
       }
+    };
+    if constexpr (KC > 0) {
+#pragma unroll 7
+      for (int j = 0; j < KC; ++j) kstep(j);
+    } else {
+      for (int j = 0; j < K; ++j) kstep(j);
     }
     float sum[R], ss[R];
 #pragma unroll

@@ -67,6 +67,8 @@ class HipEngine:
         self._lane_streams = []
         # concurrent sub-batch chains per Euler window (MDG_LANES, default 1 = one chain)
         self.lanes = int(os.environ.get("MDG_LANES", "1"))
+        # layers of lane k-1's first step that run before lane k starts (0 = lanes in lock-step)
+        self.lane_offset = int(os.environ.get("MDG_LANE_OFFSET", "0"))
 
     # ------------------------------------------------------------------ packing
     def _param_key(self):
@@ -492,6 +494,12 @@ class HipEngine:
         lane_mods = [mods[:, :, k * Bl:(k + 1) * Bl].contiguous() for k in range(nlanes)]  # [S][nl][Bl][9C]
         gs.lane_keep = lane_mods
         gs.ios = []
+        # phase offset: lane k starts once lane k-1 is `lane_offset` layers into its first step,
+        # so the lanes' identical kernel sequences run out of step (one lane's HBM-bound row-LN
+        # GEMM beside the other's attention instead of two row-LN GEMMs splitting the CUs)
+        nlay = st.dims.num_layers
+        off = self.lane_offset if 0 < self.lane_offset < nlay else 0
+        gs.lane_events = []
         for k in range(nlanes):
             ls = self._state(Bl, st.T, st.L, lane=1 + k)
             strm = self._lane_streams[k]
@@ -501,14 +509,23 @@ class HipEngine:
                 mask_k = gs.mask[k * Bl:(k + 1) * Bl]
                 _lib.check(self.lib.mdg_prepare_mask(ctypes.byref(ls.dims), mask_k.data_ptr(), ls.ws.data_ptr(), sk),
                            "mdg_prepare_mask(lane)")
+                if off and k > 0:
+                    strm.wait_event(gs.lane_events[k - 1])
                 base_k = st.base.data_ptr() + k * rows * self.C * 4
                 for i in range(gs.S):
                     io = self._step_io(ls, gs.states[i, k * Bl].data_ptr(), gs.states[i + 1, k * Bl].data_ptr(), None,
                                        None if ipa is None else ipa[i, k * Bl].data_ptr(), lane_mods[k][i].data_ptr(),
                                        mods_f[i, k * Bl].data_ptr(), gs.dts[i], base=base_k)
                     gs.ios.append(io)
-                    _lib.check(self.lib.mdg_denoise_step(ctypes.byref(ls.model_struct), ctypes.byref(io),
-                                                         mask_k.data_ptr(), ls.ws.data_ptr(), sk), "mdg_denoise_step")
+                    args = (ctypes.byref(ls.model_struct), ctypes.byref(io), mask_k.data_ptr(), ls.ws.data_ptr())
+                    if off and i == 0 and k + 1 < nlanes:
+                        _lib.check(self.lib.mdg_denoise_step_layers(*args, 0, off, sk), "mdg_denoise_step_layers")
+                        ev = torch.cuda.Event()
+                        ev.record(strm)
+                        gs.lane_events.append(ev)
+                        _lib.check(self.lib.mdg_denoise_step_layers(*args, off, nlay, sk), "mdg_denoise_step_layers")
+                    else:
+                        _lib.check(self.lib.mdg_denoise_step(*args, sk), "mdg_denoise_step")
         for k in range(nlanes):
             main.wait_stream(self._lane_streams[k])
 

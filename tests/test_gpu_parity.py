@@ -231,13 +231,16 @@ def test_long_residue_axis_atlas_matches_oracle(T, L, n_pad, dtype):
     _check(v, ref, dtype)
 
 
-def test_concurrent_lanes_equal_single_chain():
-    """engine.lanes = 2: the window's steps as two concurrent sub-batch chains on two streams
-    (parallel graph branches) give exactly the single-chain result, eager and captured."""
+@pytest.mark.parametrize("lanes,offset", [(2, 0), (2, 2), (3, 1)])
+def test_concurrent_lanes_equal_single_chain(lanes, offset):
+    """engine.lanes > 1: the window's steps as concurrent sub-batch chains on their own streams
+    (parallel graph branches), optionally phase-offset by `offset` layers of the first step
+    (mdg_denoise_step_layers split + event), give exactly the single-chain result, eager and
+    captured."""
     from mdgen_finetune_amd.engine import get_engine
     from mdgen_finetune_amd.rigid_utils import Rigid, Rotation
 
-    inp, _, cfg = _oracle_full(64, seed=3, B=4)
+    inp, _, cfg = _oracle_full(64, seed=3, B=6 if lanes == 3 else 4)
     m, _ = build_model(cfg, "cuda", T=64)
     m.hip_dtype = "bf16"
     eng = get_engine(m)
@@ -246,11 +249,12 @@ def test_concurrent_lanes_equal_single_chain():
               x_cond_mask=g("x_cond_mask"), aatype=g("aatype"))
     eng.lanes = 1
     ref = eng.sample_euler(g("x"), num_steps=6, use_graph=False, **kw)
-    eng.lanes = 2
+    eng.lanes, eng.lane_offset = lanes, offset
     eng._graphs.clear()
     got_eager = eng.sample_euler(g("x"), num_steps=6, use_graph=False, **kw)
     got_graph = eng.sample_euler(g("x"), num_steps=6, use_graph=True, **kw)
     got_replay = eng.sample_euler(g("x"), num_steps=6, use_graph=True, **kw)
-    eng.lanes = 1
+    eng.lanes, eng.lane_offset = 1, 0
+    eng._graphs.clear()
     assert torch.equal(got_eager, ref)
     assert torch.equal(got_graph, ref) and torch.equal(got_replay, ref)
