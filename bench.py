@@ -18,10 +18,12 @@ trajectory), so N ranks run N independent replicas of the window ("replicas only
 scaling "weak"); no collective on the data path.
 
 Extra fields: "roofline" for the dominant kernel (gemm_rowln_kernel, the gated-residual +
-LayerNorm-epilogue GEMM, 30 % of the step per profiles/; quoted on its largest launch, fc2;
+LayerNorm-epilogue GEMM, 34 % of the step per profiles/; quoted on its largest launch, fc2;
 live HIP-event timing on the stream the kernel runs on), "roofline_more" for the next two
 (temporal q|k|v GEMM, temporal attention), "cpu_baseline" (the oracle restatement timed on
-this host's cores).
+this host's cores).  Each roofline entry is priced against its BINDING roof: algorithmic
+FLOPs / 2.5 PF vs algorithmic bytes / 8 TB/s, whichever is longer ("bound"); both fractions
+are reported ("mfma_frac", "hbm_frac") with the kernel's arithmetic intensity.
 """
 import argparse
 import ctypes
@@ -154,16 +156,34 @@ def roofline(eng, st, dtype, B, T, L):
     def fc2():
         _lib.check(lib.mdg_gemm(ctypes.byref(f), s), "fc2 rowln gemm")
 
+    # algorithmic bytes per launch: every operand read once + every output written once, in the
+    # path's storage types (bf16 activations / weights, fp32 residual stream), head dim UNPADDED
+    # (D = 24; the kernels' 32-wide pad is not counted), adaLN rows / biases / RoPE tables omitted
+    cb = 2 if dtype == "bf16" else 4
+    HD = H * D
+    bytes_fc2 = N * 4 * C * cb + 2 * N * C * 4 + N * C * cb + 4 * C * C * cb   # hid, h r+w, xn, W2
+    bytes_qkv = N * C * cb + 3 * N * HD * cb + 3 * C * C * cb                     # xn, q|k|v, Wqkv
+    bytes_attn = 3 * N * HD * cb + N * HD * cb                                    # q|k|v, o
     out = {}
-    for name, fn, flops in (("gemm_fc2_rowln", fc2, 2.0 * N * C * 4 * C),
-                            ("gemm_qkv_temporal", gemm, 2.0 * N * 3 * C * C),
-                            ("attn_temporal", attn, 4.0 * B * L * H * T * (T + 1) * D)):
+    for name, fn, flops, nbytes in (("gemm_fc2_rowln", fc2, 2.0 * N * C * 4 * C, bytes_fc2),
+                                    ("gemm_qkv_temporal", gemm, 2.0 * N * 3 * C * C, bytes_qkv),
+                                    ("attn_temporal", attn, 4.0 * B * L * H * T * (T + 1) * D, bytes_attn)):
         sec = time_kernel(fn, 50)
-        ach = flops / sec / 1e12
-        out[name] = {"kernel": name, "bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_TFLOPS[dtype],
-                     "unit": "TFLOP/s", "frac": round(ach / PEAK_TFLOPS[dtype], 4),
-                     "traffic": _traffic(name, B, T, L, dtype), "avg_launch_us": round(sec * 1e6, 2),
-                     "flops_per_launch": flops, "shape": f"B={B} T={T} L={L}"}
+        # the binding roof: whichever of the MFMA time and the HBM time of the algorithmic work
+        # is longer (arithmetic intensity below / above the ridge 2.5 PF / 8 TB/s = 312 FLOP/B)
+        t_mfma, t_hbm = flops / (PEAK_TFLOPS[dtype] * 1e12), nbytes / (PEAK_HBM_GBS * 1e9)
+        mfma_ach, hbm_ach = flops / sec / 1e12, nbytes / sec / 1e9
+        if t_hbm > t_mfma:
+            roof = {"bound": "hbm", "achieved": round(hbm_ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                    "frac": round(hbm_ach / PEAK_HBM_GBS, 4)}
+        else:
+            roof = {"bound": "mfma", "achieved": round(mfma_ach, 2), "peak": PEAK_TFLOPS[dtype], "unit": "TFLOP/s",
+                    "frac": round(mfma_ach / PEAK_TFLOPS[dtype], 4)}
+        out[name] = {"kernel": name, **roof, "traffic": _traffic(name, B, T, L, dtype),
+                     "avg_launch_us": round(sec * 1e6, 2), "flops_per_launch": flops, "bytes_per_launch": nbytes,
+                     "intensity_flop_per_byte": round(flops / nbytes, 1),
+                     "mfma_frac": round(mfma_ach / PEAK_TFLOPS[dtype], 4),
+                     "hbm_frac": round(hbm_ach / PEAK_HBM_GBS, 4), "shape": f"B={B} T={T} L={L}"}
     return out
 
 
