@@ -26,6 +26,13 @@ def test_library_loads_and_exports_every_declared_symbol():
     from mdgen_finetune_amd import _lib
 
     if not os.path.exists(_lib.LIB_PATH):
+        # a fresh checkout: build it the way __graft_entry__.build() does (hipcc cross-compiles
+        # gfx950 without a GPU)
+        import subprocess
+
+        subprocess.run(["make", "-C", os.path.join(REPO, "mdgen_finetune_amd", "csrc"), "-j8"], check=False,
+                       stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, timeout=600)
+    if not os.path.exists(_lib.LIB_PATH):
         pytest.fail(f"{_lib.LIB_PATH} is not built (run __graft_entry__.build())")
     lib = _lib.load()
     for name in _declared():
