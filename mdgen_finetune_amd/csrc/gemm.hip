@@ -415,7 +415,7 @@ __device__ __forceinline__ void epi_tile(const mdg_gemm_desc& p, const float* __
   // per-column operand (bias, head/which/pair of the QKV scatter) is loaded once, and the
   // per-row global operands (residual, gate, RoPE table) of 8 rows are gathered before any
   // of them is consumed — no load -> store -> load latency chain.
-  constexpr int U = 8;
+  constexpr int U = (EPI == MDG_EPI_QKV) ? 4 : 8;
   const int c = (tid & 31) * 4, n = n0 + c, r0 = tid >> 5;
   constexpr int RS = NT / 32, RPT = BM / RS;  // row stride, rows per thread
   float4 bb = make_float4(0.f, 0.f, 0.f, 0.f);
