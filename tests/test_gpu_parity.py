@@ -258,3 +258,38 @@ def test_concurrent_lanes_equal_single_chain(lanes, offset):
     eng._graphs.clear()
     assert torch.equal(got_eager, ref)
     assert torch.equal(got_graph, ref) and torch.equal(got_replay, ref)
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_tps_euler_solve_T100_matches_oracle(dtype):
+    """BASELINE config 4 (TPS / interpolation, T=100, crop 4, latent 28, frames 0 and T-1
+    conditioned): the 49-step Euler solve through Sampler.sample_ode against the oracle's solve.
+    Both sides use the oracle's relative 7-vectors (computed here on the CPU; the eigh sign is
+    LAPACK-build sensitive, rigid_utils.py:191-210)."""
+    from mdgen_finetune_amd.engine import get_engine
+    from mdgen_finetune_amd.transport import Sampler, create_transport
+    from oracle import mdgen_oracle as O
+
+    d, cfg = load_golden("full_tps_T100")
+    m, c = build_model(cfg, "cuda")
+    m.hip_dtype = dtype
+    f = lambda k: torch.from_numpy(d["in_" + k])  # noqa: E731
+    rel7 = (O.relative_tensor7(f("rots"), f("trans"), f("end_rots"), f("end_trans")),
+            O.relative_tensor7(f("end_rots"), f("end_trans"), f("rots"), f("trans")))
+    get_engine(m).rel7_override = rel7
+    fn = Sampler(create_transport(m.args, "GVP", "velocity")).sample_ode(sampling_method="euler")
+    with torch.no_grad():
+        ys = fn(f("x").cuda(), functools.partial(m.forward_inference, **_kw(d)))
+    torch.set_num_threads(16)
+    P = O.seeded_params(c, cfg["weights_seed"])
+    kw = O.kwargs_from_npz(d)
+    orig = O.relative_tensor7
+    try:  # the oracle's own TPS branch, fed the same 7-vectors
+        O.relative_tensor7 = lambda ra, ta, rb, tb: rel7[0] if ra is kw["rots"] else rel7[1]
+        with torch.no_grad():
+            ref = O.euler_sample(P, c, f("x"), num_steps=50, **kw)
+    finally:
+        O.relative_tensor7 = orig
+    assert ys.shape == ref.shape
+    _check(ys[1], ref[1].numpy(), dtype)
+    _check(ys[-1], ref[-1].numpy(), dtype, solve=True)
