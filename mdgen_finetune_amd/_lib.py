@@ -12,7 +12,8 @@ import os
 
 import torch  # noqa: F401  (must be imported before the HIP library is loaded)
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libmdgen_hip.so")
+# MDG_LIB_PATH: an alternative build of the same ABI (A/B timing of two kernel versions)
+LIB_PATH = os.environ.get("MDG_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libmdgen_hip.so")
 
 MDG_F32, MDG_BF16 = 0, 1
 MDG_A_PLAIN, MDG_A_LNMOD = 0, 1

@@ -851,21 +851,23 @@ __global__ __launch_bounds__(kRowThreads, BM == 64 ? 4 : 1) void gemm_rowln_kern
   // residual-read latency once instead of once per band.
   constexpr int UPB = 4 / RG, NU = (BM / 32) * UPB;
   const float inv_rpm = 1.0f / (float)p.rows_per_mod;
-  auto load_unit = [&](int u, float2 (&hv)[RG][NE], float2 (&gv)[RG][NE]) {
+  // the gate row is per trajectory: one row of it per unit (the unit's first row's entry; a
+  // row of another entry, in a unit straddling a trajectory boundary, reloads its own)
+  auto load_unit = [&](int u, float2 (&hv)[RG][NE], float2 (&gv)[NE]) {
+    const int mu = min(m0 + (u / UPB) * 32 + wave * 4 + (u % UPB) * RG, M - 1);
+    const float* gr = p.gate ? p.gate + (size_t)fdiv(mu, p.rows_per_mod, inv_rpm) * p.mod_stride + p.gate_off : nullptr;
+#pragma unroll
+    for (int e = 0; e < NE; ++e)
+      gv[e] = gr ? *reinterpret_cast<const float2*>(gr + 2 * lane + 128 * e) : make_float2(1.f, 1.f);
 #pragma unroll
     for (int rr = 0; rr < RG; ++rr) {
-      const int m = min(m0 + (u / UPB) * 32 + wave * 4 + (u % UPB) * RG + rr, M - 1);
+      const int m = min(mu + rr, M - 1);
       const float* hr = p.resid + (size_t)m * p.ldr;
-      const float* gr = p.gate ? p.gate + (size_t)fdiv(m, p.rows_per_mod, inv_rpm) * p.mod_stride + p.gate_off : nullptr;
 #pragma unroll
-      for (int e = 0; e < NE; ++e) {
-        const int k = 2 * lane + 128 * e;
-        hv[rr][e] = *reinterpret_cast<const float2*>(hr + k);
-        gv[rr][e] = gr ? *reinterpret_cast<const float2*>(gr + k) : make_float2(1.f, 1.f);
-      }
+      for (int e = 0; e < NE; ++e) hv[rr][e] = *reinterpret_cast<const float2*>(hr + 2 * lane + 128 * e);
     }
   };
-  float2 hv[RG][NE], gv[RG][NE];
+  float2 hv[RG][NE], gv[NE];
   load_unit(0, hv, gv);
 
   f32x4 acc[4][NT];
@@ -937,7 +939,7 @@ __global__ __launch_bounds__(kRowThreads, BM == 64 ? 4 : 1) void gemm_rowln_kern
 #pragma unroll 1
     for (int g0 = 0; g0 < 4; g0 += RG) {
       const int u = band * UPB + g0 / RG;
-      float2 hn[RG][NE], gn[RG][NE];
+      float2 hn[RG][NE], gn[NE];
       if (u + 1 < NU) load_unit(u + 1, hn, gn);
       const int mb0 = min(m0 + band * 32 + wave * 4 + g0, M - 1), mb3 = min(mb0 + RG - 1, M - 1);
       const int b0 = fdiv(mb0, p.rows_per_mod, inv_rpm);
@@ -956,12 +958,23 @@ __global__ __launch_bounds__(kRowThreads, BM == 64 ? 4 : 1) void gemm_rowln_kern
   #pragma unroll
       for (int rr = 0; rr < RG; ++rr) {
         const float* srow = stage + (wave * 4 + g0 + rr) * LDS_ST;
+        float2 g2[NE];
+  #pragma unroll
+        for (int e = 0; e < NE; ++e) g2[e] = gv[e];
+        if (!one_b && p.gate) {  // rare: this row belongs to the next trajectory
+          const int br = fdiv(min(m0 + band * 32 + wave * 4 + g0 + rr, M - 1), p.rows_per_mod, inv_rpm);
+          if (br != b0) {
+            const float* gr = p.gate + (size_t)br * p.mod_stride + p.gate_off;
+  #pragma unroll
+            for (int e = 0; e < NE; ++e) g2[e] = *reinterpret_cast<const float2*>(gr + 2 * lane + 128 * e);
+          }
+        }
         float s = 0.f;
   #pragma unroll
         for (int e = 0; e < NE; ++e) {
           const float2 v = *reinterpret_cast<const float2*>(srow + 2 * lane + 128 * e);
-          hv[rr][e].x += gv[rr][e].x * (v.x + bb[e].x);
-          hv[rr][e].y += gv[rr][e].y * (v.y + bb[e].y);
+          hv[rr][e].x += g2[e].x * (v.x + bb[e].x);
+          hv[rr][e].y += g2[e].y * (v.y + bb[e].y);
           s += hv[rr][e].x + hv[rr][e].y;
         }
         sum[rr] = s;
@@ -1018,12 +1031,11 @@ __global__ __launch_bounds__(kRowThreads, BM == 64 ? 4 : 1) void gemm_rowln_kern
         }
       }
 #pragma unroll
-      for (int rr = 0; rr < RG; ++rr)
+      for (int e = 0; e < NE; ++e) {
+        gv[e] = gn[e];
 #pragma unroll
-        for (int e = 0; e < NE; ++e) {
-          hv[rr][e] = hn[rr][e];
-          gv[rr][e] = gn[rr][e];
-        }
+        for (int rr = 0; rr < RG; ++rr) hv[rr][e] = hn[rr][e];
+      }
     }
     __syncthreads();
   }
