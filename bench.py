@@ -233,12 +233,20 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal of the N-rank path on a one-GPU box: MDG_BENCH_SHARE_GPU=1 puts every rank on
+    # cuda:0 and uses gloo for the barrier / max-over-ranks (RCCL refuses two ranks per GPU)
+    share = os.environ.get("MDG_BENCH_SHARE_GPU") == "1"
+    if share:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=dev)
+        if share:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
     from mdgen_finetune_amd.engine import get_engine
 
     B, T, L = a.batch, a.frames, a.crop
@@ -270,7 +278,7 @@ def main():
         barrier()
         el = time.perf_counter() - t0
         if world > 1:
-            tt = torch.tensor([el], device=dev, dtype=torch.float64)
+            tt = torch.tensor([el], device="cpu" if share else dev, dtype=torch.float64)
             torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
             el = tt.item()
         n_euler = a.num_steps - 1
