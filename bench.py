@@ -56,6 +56,10 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--lanes", type=int, default=2, help="concurrent sub-batch chains per window (streams)")
+    ap.add_argument("--sweep-batches", default="1,8,32",
+                    help="extra per-GPU batch sizes timed beside the headline (comma list, '' = none)")
+    ap.add_argument("--no-f32-line", action="store_true", help="skip the fp32-operand (parity path) line")
+    ap.add_argument("--sweep-steps", type=int, default=2, help="timed windows per sweep / f32 line")
     return ap.parse_args()
 
 
@@ -187,6 +191,105 @@ def roofline(eng, st, dtype, B, T, L):
     return out
 
 
+def max_over_ranks(el, world, device):
+    """The job's time: the slowest rank's timed region (all_reduce MAX; identity at world 1)."""
+    if world > 1:
+        tt = torch.tensor([el], device=device, dtype=torch.float64)
+        torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
+        el = tt.item()
+    return el
+
+
+def job_value(world, B, T, n_euler, steps, el):
+    """Whole-job frames/s: every rank denoises B*T frames per Euler step (replicas, weak
+    scaling), over the max-over-ranks time."""
+    return world * B * T * n_euler * steps / el
+
+
+def step_model(B, T, L, C=384, H=16, nl=5, lat=21, dtype="bf16"):
+    """Algorithmic work of ONE denoise step (forward + Euler update) of B trajectories, from the
+    model dims (counted 2*M*N*K per GEMM, 4*S*(S+1)*D per attention head-sequence):
+      flops        — GEMMs 32*C^2 per token per layer + temporal attention 4*(T+1)*C per token
+                     per layer + spatial 4*(L+1)*C + embedding / FinalLayer 4*lat*C per token
+                     (the per-window IPA / adaLN precompute is excluded: x-independent, amortised
+                     over 49 steps);
+      design_bytes — the HBM bytes the kernel sequence of this build moves per step when every
+                     kernel reads its operands once and writes its outputs once (DESIGN.md §3
+                     per-kernel min bytes x launches): the data-flow floor of the unfused-layer
+                     design, not of the model;
+      floor_bytes  — model floor: bf16/f32 weights once + x in, x out (fp32)."""
+    N = B * T * L
+    D = C // H
+    cb = 2 if dtype == "bf16" else 4
+    flops = N * nl * (32.0 * C * C + 4.0 * (T + 1) * C + 4.0 * (L + 1) * C) + N * 4.0 * lat * C
+    emb = N * (lat * 4 + C * 4 + C * 4 + C * cb)
+    spatial = N * C * cb * 2
+    rowln = N * (C * cb + 8 * C + C * cb)
+    qkv = N * (C * cb + 3 * C * cb)
+    attn = N * 4 * C * cb
+    fc1 = N * (C * cb + 4 * C * cb)
+    fc2 = N * (4 * C * cb + 8 * C + C * cb)
+    final = N * (C * cb + 3 * lat * 4)
+    design = emb + nl * (spatial + 2 * rowln + qkv + attn + fc1 + fc2) + final
+    params = nl * 16 * C * C + 2 * lat * C
+    floor = params * cb + N * lat * 4 * 2
+    return {"flops": flops, "design_bytes": design, "floor_bytes": floor, "D": D}
+
+
+def step_roofline(B, T, L, dtype, sec_per_denoise):
+    """Whole-step position against both roofs (not one kernel): achieved TFLOP/s of the step's
+    algorithmic FLOPs vs the dense MFMA peak, and achieved GB/s of the design's data flow vs HBM."""
+    sm = step_model(B, T, L, dtype=dtype)
+    tf = sm["flops"] / sec_per_denoise / 1e12
+    gbs = sm["design_bytes"] / sec_per_denoise / 1e9
+    t_mfma = sm["flops"] / (PEAK_TFLOPS[dtype] * 1e12)
+    t_hbm = sm["design_bytes"] / (PEAK_HBM_GBS * 1e9)
+    return {"flops_per_frame": round(sm["flops"] / (B * T), 1), "flops_per_denoise_step": sm["flops"],
+            "achieved_tflops": round(tf, 1), "peak_tflops": PEAK_TFLOPS[dtype],
+            "mfma_frac": round(tf / PEAK_TFLOPS[dtype], 4),
+            "design_bytes_per_denoise_step": sm["design_bytes"], "achieved_gbs": round(gbs, 1),
+            "hbm_frac": round(gbs / PEAK_HBM_GBS, 4),
+            "design_floor_frac": round(max(t_mfma, t_hbm) / sec_per_denoise, 4),
+            "binding": "hbm (design data flow)" if t_hbm > t_mfma else "mfma",
+            "roof_frames_per_s_mfma": round(B * T / t_mfma, 1),
+            "roof_frames_per_s_design_hbm": round(B * T / t_hbm, 1),
+            "model_floor_bytes": sm["floor_bytes"]}
+
+
+def time_windows(eng, zs, kw, num_steps, steps, warmup, use_graph=True):
+    """Wall time of `steps` rollout windows (after `warmup`), inputs resident on the device."""
+    for _ in range(max(1, warmup)):
+        ys = eng.sample_euler(zs, num_steps=num_steps, use_graph=use_graph, **kw)
+    torch.cuda.synchronize()
+    assert torch.isfinite(ys[-1]).all(), "non-finite samples"
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        eng.sample_euler(zs, num_steps=num_steps, use_graph=use_graph, **kw)
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps
+
+
+def sweep_line(dev, T, L, B, dtype, lanes, num_steps, steps, seed):
+    """One extra (batch, dtype) point: frames/s and the step-level roofline."""
+    from mdgen_finetune_amd.engine import get_engine
+
+    m = make_model(T, L).to(dev)
+    m.hip_dtype = dtype
+    eng = get_engine(m)
+    eng.lanes = lanes if (lanes > 1 and B % lanes == 0 and B >= 8) else 1
+    zs, kw, _ = inputs(B, T, L, seed=seed, device=dev)
+    with torch.no_grad():
+        sec = time_windows(eng, zs, kw, num_steps, steps, 1)
+    n_euler = num_steps - 1
+    out = {"batch": B, "dtype": dtype, "lanes": eng.lanes, "value": round(B * T * n_euler / sec, 1),
+           "unit": "frames/s", "ms_per_window": round(sec * 1e3, 3),
+           "us_per_denoise_step": round(sec / n_euler * 1e6, 2),
+           "step_roofline": step_roofline(B, T, L, dtype, sec / n_euler)}
+    del eng, m
+    torch.cuda.empty_cache()
+    return out
+
+
 def cpu_baseline(T, L, seconds):
     """The oracle (oracle/mdgen_oracle.py, fp32 PyTorch-CPU restatement pinned to the
     reference) timed on this host: forward + Euler update at B=1 T=1000 L=4, repeated until
@@ -277,18 +380,25 @@ def main():
         torch.cuda.synchronize()
         barrier()
         el = time.perf_counter() - t0
-        if world > 1:
-            tt = torch.tensor([el], device="cpu" if share else dev, dtype=torch.float64)
-            torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
-            el = tt.item()
+        el = max_over_ranks(el, world, torch.device("cpu") if share else dev)
         n_euler = a.num_steps - 1
-        frames = world * B * T * n_euler * a.steps
-        value = frames / el
+        value = job_value(world, B, T, n_euler, a.steps, el)
         # roofline launches at the shape the timed region runs them with (one lane's batch)
         nl = a.lanes if (a.lanes > 1 and B % a.lanes == 0) else 1
         Bl = B // nl
         st = eng._state(Bl, T, L, lane=1 if nl > 1 else 0)
         roofs = roofline(eng, st, a.dtype, Bl, T, L) if rank == 0 else None
+        plan = eng.describe_plan(Bl, T, L)
+
+    # extra lines (rank 0, single process): the B sweep SURVEY §8(d) asks for and the fp32
+    # parity-path throughput, each with its own step-level roofline
+    sweep = []
+    if rank == 0 and world == 1:
+        for Bs in [int(b) for b in a.sweep_batches.split(",") if b.strip()]:
+            if Bs != B:
+                sweep.append(sweep_line(dev, T, L, Bs, a.dtype, a.lanes, a.num_steps, a.sweep_steps, 300 + Bs))
+        if not a.no_f32_line and a.dtype != "f32":
+            sweep.append(sweep_line(dev, T, L, B, "f32", a.lanes, a.num_steps, a.sweep_steps, 100))
 
     out = None
     if rank == 0:
@@ -297,7 +407,7 @@ def main():
             "metric": "denoised frames/sec, 1000-frame x crop4 forward-sim step, 1/2/4/8 MI355X",
             "value": round(value, 1),
             "unit": "frames/s",
-            "n_gpus": world,
+            "n_gpus": 1 if share else world,
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": round(el / a.steps * 1e3, 3),
@@ -314,10 +424,16 @@ def main():
                        "parallelism": f"replicas{world}", "hipgraph": not a.no_graph,
                        "lanes": a.lanes},
             "us_per_denoise_step": round(el / a.steps / n_euler * 1e6, 2),
+            "step_roofline": step_roofline(B, T, L, a.dtype, el / a.steps / n_euler / world),
+            "kernel_plan": plan,
+            "batch_sweep": sweep,
             "roofline": roofs["gemm_fc2_rowln"] if roofs else None,
             "roofline_more": [roofs["gemm_qkv_temporal"], roofs["attn_temporal"]] if roofs else None,
             "cpu_baseline": cpu,
         }
+        if share:  # rehearsal: every rank on cuda:0 — not a multi-GPU measurement
+            out["shared_gpu"] = True
+            out["ranks_sharing_gpu"] = world
         print(json.dumps(out), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define MDG_ABI_VERSION 8
+#define MDG_ABI_VERSION 9
 #define MDG_MAX_LAYERS 16
 #define MDG_DP 32 /* padded head dim of every attention operand buffer (head_dim <= 31) */
 
@@ -179,6 +179,10 @@ int mdg_denoise_step(const mdg_model* m, const mdg_step_io* io, const float* mas
    lets a caller record an event mid-step (the engine offsets concurrent lanes by it). */
 int mdg_denoise_step_layers(const mdg_model* m, const mdg_step_io* io, const float* mask, void* ws,
                             int32_t first_layer, int32_t last_layer, void* stream);
+
+/* JSON text naming the kernel path each part of a denoising step takes for these dims (the
+   fused / fallback routes chosen in mdg_denoise_step), for benchmark records.  0 on success. */
+int mdg_describe_plan(const mdg_dims* d, char* buf, size_t n);
 
 /* Building blocks (exposed for unit tests and for the conditioning precompute). */
 int mdg_gemm(const mdg_gemm_desc* g, void* stream);

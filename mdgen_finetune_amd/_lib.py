@@ -82,6 +82,7 @@ SIGNATURES = [
     ("mdg_denoise_step", _i32, [ctypes.POINTER(MdgModel), ctypes.POINTER(MdgStepIO), _vp, _vp, _vp]),
     ("mdg_denoise_step_layers", _i32, [ctypes.POINTER(MdgModel), ctypes.POINTER(MdgStepIO), _vp, _vp, _i32, _i32,
                                        _vp]),
+    ("mdg_describe_plan", _i32, [ctypes.POINTER(MdgDims), ctypes.c_char_p, ctypes.c_size_t]),
     ("mdg_gemm", _i32, [ctypes.POINTER(MdgGemmDesc), _vp]),
     ("mdg_attn_spatial", _i32, [_i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
     ("mdg_attn_temporal", _i32, [_i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
@@ -89,7 +90,7 @@ SIGNATURES = [
     ("mdg_latents_to_atom14", _i32, [_i32, _i32, _i32, _i32, _i32, _i32] + [_vp] * 12),
 ]
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 _LIB = None
 
 

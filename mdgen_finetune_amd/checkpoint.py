@@ -23,8 +23,10 @@ def _safe_load(path, map_location="cpu"):
         return torch.load(path, map_location=map_location, weights_only=True)
 
 
-def save_checkpoint(path, wrapper, optimizer=None, epoch=0, global_step=0):
-    """Lightning layout; ``args`` is stored as a Namespace of plain values."""
+def save_checkpoint(path, wrapper, optimizer=None, epoch=0, global_step=0, epoch_complete=True, batches_done=0):
+    """Lightning layout; ``args`` is stored as a Namespace of plain values.  ``loops`` records
+    where in the epoch the save happened (a mid-epoch save, e.g. at --max_steps, resumes the
+    same epoch after its ``batches_done`` consumed batches, as Lightning's fit loop does)."""
     if wrapper.cached_weights is not None:  # wrapper.py:126-129
         wrapper.restore_cached_weights()
     args = argparse.Namespace(**{k: v for k, v in vars(wrapper.args).items()
@@ -37,6 +39,7 @@ def save_checkpoint(path, wrapper, optimizer=None, epoch=0, global_step=0):
         "hyper_parameters": {"args": args},
         "optimizer_states": [optimizer.state_dict()] if optimizer is not None else [],
         "lr_schedulers": [],
+        "loops": {"fit_loop": {"epoch_complete": bool(epoch_complete), "batches_done": int(batches_done)}},
     }
     if wrapper.ema is not None:
         ema = wrapper.ema.state_dict()

@@ -472,6 +472,28 @@ int mdg_denoise_step_layers(const mdg_model* m, const mdg_step_io* io, const flo
   return denoise_range(m, io, mask, ws, first_layer, last_layer, stream);
 }
 
+int mdg_describe_plan(const mdg_dims* d, char* buf, size_t n) {
+  if (int e = check_dims(d)) return e;
+  if (!buf || n == 0) return fail(MDG_E_ARG, "describe_plan: null buffer");
+  const int C = d->C;
+  const bool fuse = d->dtype == MDG_BF16 && (C == 128 || C == 256 || C == 384 || C == 512);
+  const char* spatial;
+  if (d->L >= kSpatialMfmaMinL && (size_t)d->B * d->T <= 65535)
+    spatial = "qkv_gemm(temporal layout)+attn_temporal_mfma(one sequence per frame)";
+  else if (fuse_spatial_attn(*d))
+    spatial = "gemm_qkv_attn_spatial(fused projection+attention)";
+  else
+    spatial = "qkv_gemm(spatial layout)+attn_spatial(valu)";
+  snprintf(buf, n,
+           "{\"dtype\": \"%s\", \"spatial\": \"%s\", \"ln_handoff\": \"%s\", "
+           "\"temporal\": \"qkv_gemm+%s\", \"mlp\": \"fc1_gemm(gelu)+%s\", \"final\": \"euler_epilogue_gemm\"}",
+           d->dtype == MDG_BF16 ? "bf16" : "f32", spatial,
+           fuse ? "fused into gated-residual row-LN GEMM epilogues" : "stand-alone ln_mod pass",
+           d->dtype == MDG_BF16 ? "attn_temporal_bf16(32x32x16 mfma)" : "attn_temporal(f32 16x16x4 mfma)",
+           fuse ? "fc2_rowln_gemm" : "fc2_gate_res_gemm");
+  return MDG_OK;
+}
+
 int mdg_prep_latents(int32_t B, int32_t T, int32_t L, int32_t latent, int32_t flags, int32_t cond_interval,
                      const float* rots, const float* trans, const float* torsions, float* latents,
                      float* x_cond, int64_t* cond_mask, void* stream) {

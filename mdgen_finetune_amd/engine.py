@@ -203,6 +203,15 @@ class HipEngine:
         self._states[key] = st
         return st
 
+    def describe_plan(self, B, T, L):
+        """The kernel route mdg_denoise_step takes for (B, T, L) at this dtype (mdg_describe_plan)."""
+        import json
+
+        st = self._state(B, T, L)
+        buf = ctypes.create_string_buffer(1024)
+        _lib.check(self.lib.mdg_describe_plan(ctypes.byref(st.dims), buf, 1024), "mdg_describe_plan")
+        return json.loads(buf.value.decode())
+
     # ------------------------------------------------------------------ conditioning
     def conditioning(self, t_sb, mask, rots, trans, erots, etrans, aatype):
         """x-independent conditioning for S time points at once.
@@ -339,7 +348,7 @@ class HipEngine:
         B, T, L, mask, rots, trans, erots, etrans, aa = self._inputs(zs, mask, start_frames, end_frames, aatype)
         st = self._state(B, T, L)
         self._prepare_tps(rots, trans, erots, etrans)
-        key = (B, T, L, num_steps)
+        key = (B, T, L, num_steps, self._nlanes(B))
         gs = self._graphs.get(key) if use_graph else None
         if gs is None:
             gs = self._build_sampler(st, num_steps, key if use_graph else None)
@@ -435,6 +444,8 @@ class HipEngine:
 
     def _copy_opt(self, gs, name, val):
         if val is None:
+            if getattr(gs, name, None) is not None:
+                gs.graph = None  # an input went from present to absent: the captured program read it
             setattr(gs, name, None)
             return
         buf = getattr(gs, name, None)
@@ -443,6 +454,11 @@ class HipEngine:
             setattr(gs, name, buf)
             gs.graph = None  # static buffers changed: recapture
         buf.copy_(val)
+
+    def _nlanes(self, B):
+        """Concurrent sub-batch chains for a window of B trajectories (part of the graph key)."""
+        want = self.lanes if self.lanes > 0 else (2 if B >= 8 else 1)
+        return want if (want > 1 and B % want == 0) else 1
 
     def _build_sampler(self, st, num_steps, key):
         gs = _ShapeState()
@@ -468,8 +484,7 @@ class HipEngine:
         self._base(st, gs.x_cond if gs.has_cond else None, gs.x_cond_mask if gs.has_cond else None)
         _lib.check(self.lib.mdg_prepare_mask(ctypes.byref(st.dims), gs.mask.data_ptr(), st.ws.data_ptr(), s),
                    "mdg_prepare_mask")
-        want = self.lanes if self.lanes > 0 else (2 if st.B >= 8 else 1)
-        nlanes = want if (want > 1 and st.B % want == 0) else 1
+        nlanes = self._nlanes(st.B)
         if nlanes > 1:
             self._run_lanes(gs, st, mods, mods_f, ipa, nlanes)
             return

@@ -205,7 +205,7 @@ class LatentMDGenModel(nn.Module):
                 aatype=None, *args, **kwargs):
         if mask.dim() == 2:  # latent_model.py:233-234
             mask = mask.repeat(x.shape[0], 1, 1)
-        if self._use_hip():
+        if self._use_hip(x):
             from ..engine import get_engine
 
             return get_engine(self).forward(x, t, mask, start_frames, end_frames, x_cond, x_cond_mask, aatype)
@@ -215,13 +215,23 @@ class LatentMDGenModel(nn.Module):
                           x_cond_mask=None, aatype=None):
         return self.forward(x, t, mask, start_frames, end_frames, x_cond, x_cond_mask, aatype)
 
-    def _use_hip(self):
+    def _needs_grad(self, x):
+        """True when autograd records this call: grad mode on and x or any parameter requires
+        grad — whatever the module's train/eval mode (an eval()-mode prior used for guidance
+        still has to return a differentiable output)."""
+        if not torch.is_grad_enabled():
+            return False
+        return bool(x.requires_grad) or any(p.requires_grad for p in self.parameters())
+
+    def _use_hip(self, x):
+        """The graph-captured HIP inference engine (no autograd) serves a call only when nothing
+        needs a gradient; differentiable calls go through forward_torch (whose block stack runs
+        the HIP autograd kernels on a ROCm device, see _hip_blocks)."""
         if self.backend == "torch":
             return False
         if self.backend != "hip":
             raise ValueError(f"unknown backend {self.backend!r}")
-        # autograd through the block stack needs the eager path (HIP backward: DESIGN.md §Scope)
-        return not (torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()) and self.training)
+        return not self._needs_grad(x)
 
     def forward_torch(self, x, t, mask, start_frames=None, end_frames=None, x_cond=None, x_cond_mask=None,
                       aatype=None):

@@ -55,7 +55,7 @@ _EXTRA = [
     ("synthetic_size", _I, 64, "number of synthetic trajectories"),
     ("max_steps", _I, None, "stop after this many optimizer steps"),
     ("seed", _I, 137, "base RNG seed (rank r uses seed + r for its noise draws)"),
-    ("bucket_cap_mb", _I, 32, "DDP gradient bucket size (all-reduce overlaps backward per bucket)"),
+    ("bucket_cap_mb", _F, 32.0, "DDP gradient bucket size (all-reduce overlaps backward per bucket)"),
     ("model_dir", _S, None, "checkpoint directory (default workdir/<run_name>, the reference's MODEL_DIR)"),
 ]
 

@@ -63,9 +63,10 @@ def batch_from_atom14(atom14, aatype, device):
             "rots": fr.get_rots().get_rot_mats()[None], "seqres": aatype[None], "mask": torch.ones(1, L, device=device)}
 
 
-def rollout(model, batch, num_frames, n_traj=1):
+def rollout(model, batch, num_frames, n_traj=1, zs0=None):
     """sim_inference.py:65-93: one window from the batch's start frame; returns the window's
-    atom14 [n_traj, T, L, 14, 3] and the batch restarted from each trajectory's last frame."""
+    atom14 [n_traj, T, L, 14, 3] and the batch restarted from each trajectory's last frame
+    (``zs0``: the window's prior noise, drawn by the wrapper when None)."""
     B = batch["trans"].shape[0]
     if B != n_traj:
         batch = {k: v.expand(n_traj, *v.shape[1:]) for k, v in batch.items()}
@@ -77,7 +78,7 @@ def rollout(model, batch, num_frames, n_traj=1):
         "seqres": batch["seqres"],
         "mask": batch["mask"],
     }
-    atom14, _ = model.inference(ex)
+    atom14, _ = model.inference(ex, zs0=zs0)
     last = atom14[:, -1]                                                # [n,L,14,3]
     fr = G.atom14_to_frames(last)
     a37 = G.atom14_to_atom37(last, batch["seqres"])

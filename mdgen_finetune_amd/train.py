@@ -91,7 +91,9 @@ class Trainer:
             self.model = DDP(self.wrapper.model, device_ids=[self.device.index] if self.device.type == "cuda" else None,
                              bucket_cap_mb=args.bucket_cap_mb, gradient_as_bucket_view=True, static_graph=True)
         self.optimizer = self.wrapper.configure_optimizers()
-        self.epoch, self.global_step = 0, 0
+        self.epoch, self.global_step, self.skip_batches = 0, 0, 0
+        self.precision = resolve_precision(args.precision, self.device)
+        self.scaler = torch.amp.GradScaler(self.device.type) if self.precision == torch.float16 else None
         if dataset is None:
             if not args.synthetic:
                 raise NotImplementedError("only --synthetic data is available offline (the reference's "
@@ -114,13 +116,19 @@ class Trainer:
         if self.wrapper.ema is not None and "ema" in ck:
             self.wrapper.ema.load_state_dict(ck["ema"])
             self.wrapper.ema.to(self.device)
-        self.epoch, self.global_step = int(ck["epoch"]) + 1, int(ck["global_step"])
+        loop = ck.get("loops", {}).get("fit_loop", {"epoch_complete": True, "batches_done": 0})
+        self.global_step = int(ck["global_step"])
+        if loop.get("epoch_complete", True):
+            self.epoch, self.skip_batches = int(ck["epoch"]) + 1, 0
+        else:  # saved mid-epoch (--max_steps): finish that epoch's remaining batches first
+            self.epoch, self.skip_batches = int(ck["epoch"]), int(loop.get("batches_done", 0))
 
-    def save(self):
+    def save(self, epoch_complete=True, batches_done=0):
         if self.rank != 0:
             return None
         path = os.path.join(self.args.model_dir, f"epoch={self.epoch}-step={self.global_step}.ckpt")
-        save_checkpoint(path, self.wrapper, self.optimizer, self.epoch, self.global_step)
+        save_checkpoint(path, self.wrapper, self.optimizer, self.epoch, self.global_step,
+                        epoch_complete=epoch_complete, batches_done=batches_done)
         return path
 
     # ------------------------------------------------------------------ one optimizer step
@@ -135,7 +143,7 @@ class Trainer:
         n = len(micro_batches)
         self.wrapper.train()
         losses = []
-        autocast = (torch.autocast(self.device.type, dtype=torch.bfloat16) if a.precision.startswith("bf16")
+        autocast = (torch.autocast(self.device.type, dtype=self.precision) if self.precision is not None
                     else torch.autocast(self.device.type, enabled=False))
         for i, batch in enumerate(micro_batches):
             batch = self._to_device(batch)
@@ -144,10 +152,17 @@ class Trainer:
             with ctx:
                 with autocast:
                     loss = self.wrapper.general_step(batch, "train", model=self.model)
-                (loss / n).backward()
+                scaled = loss / n
+                (self.scaler.scale(scaled) if self.scaler is not None else scaled).backward()
             losses.append(loss.detach())
+        if self.scaler is not None:
+            self.scaler.unscale_(self.optimizer)
         gnorm = torch.nn.utils.clip_grad_norm_(self.wrapper.model.parameters(), a.grad_clip) if a.grad_clip else None
-        self.optimizer.step()
+        if self.scaler is not None:
+            self.scaler.step(self.optimizer)
+            self.scaler.update()
+        else:
+            self.optimizer.step()
         self.wrapper.on_before_zero_grad()
         self.optimizer.zero_grad(set_to_none=True)
         self.global_step += 1
@@ -174,9 +189,12 @@ class Trainer:
         while self.epoch < a.epochs:
             self.sampler.set_epoch(self.epoch)
             pending = []
+            skip, self.skip_batches = self.skip_batches, 0
             for bi, batch in enumerate(self.loader):
                 if a.train_batches is not None and bi >= a.train_batches:
                     break
+                if bi < skip:  # resumed mid-epoch: these batches were consumed before the save
+                    continue
                 pending.append(batch)
                 if len(pending) < acc:
                     continue
@@ -185,12 +203,28 @@ class Trainer:
                 if self.global_step % a.print_freq == 0:
                     self.print_log("iter")
                 if a.max_steps is not None and self.global_step >= a.max_steps:
-                    self.save()
+                    self.save(epoch_complete=False, batches_done=bi + 1)
                     return
             self.print_log("train")
             if (self.epoch + 1) % a.ckpt_freq == 0:
                 self.save()
             self.epoch += 1
+
+
+# Lightning precision strings the reference passes to pl.Trainer(precision=...) (train.py:52)
+_PRECISIONS = {"32-true": None, "32": None, "bf16-mixed": torch.bfloat16, "16-mixed": torch.float16}
+
+
+def resolve_precision(precision, device):
+    """autocast dtype for --precision (None = full fp32).  'bf16-true' / '16-true' (weights
+    held in half precision) and unknown strings are refused instead of silently training fp32."""
+    key = str(precision)
+    if key not in _PRECISIONS:
+        raise NotImplementedError(f"--precision {precision!r}: supported are {sorted(_PRECISIONS)}")
+    dt = _PRECISIONS[key]
+    if dt == torch.float16 and device.type != "cuda":
+        raise NotImplementedError("--precision 16-mixed needs a GPU (fp16 autocast + GradScaler)")
+    return dt
 
 
 class _null:

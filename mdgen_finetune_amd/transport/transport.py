@@ -120,7 +120,7 @@ class Transport:
         return body_fn
 
 
-def _hip_model_of(model):
+def _hip_model_of(model, x):
     """(LatentMDGenModel, kwargs) if `model` is partial(m.forward_inference|m.forward, **kw) of
     our module on the HIP backend, else None."""
     if not isinstance(model, functools.partial) or model.args:
@@ -131,7 +131,7 @@ def _hip_model_of(model):
 
     if not isinstance(owner, LatentMDGenModel) or fn.__name__ not in ("forward_inference", "forward"):
         return None
-    if not owner._use_hip():
+    if not owner._use_hip(x):
         return None
     return owner, dict(model.keywords)
 
@@ -155,7 +155,7 @@ class Sampler:
 
         if sampling_method == "dopri5":
             def _sample_dopri5(x, model, **model_kwargs):
-                hip = None if (reverse or model_kwargs) else _hip_model_of(model)
+                hip = None if (reverse or model_kwargs) else _hip_model_of(model, x)
                 if hip is not None:  # each evaluation = one hipGraph replay (HipEngine.velocity_field)
                     m, kw = hip
                     from ..engine import get_engine
@@ -177,7 +177,7 @@ class Sampler:
             return _sample_dopri5
 
         def _sample(x, model, **model_kwargs):
-            hip = None if (reverse or model_kwargs or (t0, t1) != (0, 1)) else _hip_model_of(model)
+            hip = None if (reverse or model_kwargs or (t0, t1) != (0, 1)) else _hip_model_of(model, x)
             if hip is not None:
                 m, kw = hip
                 from ..engine import get_engine

@@ -48,19 +48,20 @@ def test_pdb_text_matches_reference_byte_for_byte(golden):
     assert txt == str(d["out_pdb"])
 
 
-def _small_ckpt(tmp_path, T=4):
+def _small_ckpt(tmp_path, T=4, tps=False):
     from mdgen_finetune_amd import synthetic
     from mdgen_finetune_amd.checkpoint import save_checkpoint
     from mdgen_finetune_amd.parsing import parse_train_args
     from mdgen_finetune_amd.wrapper import NewMDGenWrapper
 
-    a = parse_train_args(["--synthetic", "--sim_condition", "--prepend_ipa", "--abs_pos_emb", "--num_frames", str(T),
+    a = parse_train_args(["--synthetic", "--tps_condition" if tps else "--sim_condition", "--prepend_ipa",
+                          "--abs_pos_emb", "--num_frames", str(T),
                           "--crop", "4", "--embed_dim", "64", "--mha_heads", "4", "--num_layers", "2",
                           "--ipa_heads", "2", "--ipa_head_dim", "8", "--ipa_qk", "4", "--ipa_v", "4",
                           "--sampling_method", "euler", "--model_dir", str(tmp_path)])
     w = NewMDGenWrapper(a)
     synthetic.fill_module_(w.model, 5)
-    path = str(tmp_path / "sim.ckpt")
+    path = str(tmp_path / ("tps.ckpt" if tps else "sim.ckpt"))
     save_checkpoint(path, w)
     return path
 
@@ -75,3 +76,38 @@ def test_sim_inference_rollout_cpu_writes_multimodel_pdb(tmp_path):
         txt = (tmp_path / "out" / f"AKDW_{j}.pdb").read_text()
         assert txt.count("MODEL ") == 8 and txt.count("ENDMDL") == 8
         assert "nan" not in txt.lower()
+
+
+def test_tps_inference_cpu_writes_paths_and_metadata(tmp_path):
+    """tps_inference drop-in (tps_inference.py:43-149) on the eager CPU backend: windows whose
+    first / last frames are the chosen start / end frames, one PDB + metadata record each."""
+    import json
+
+    from mdgen_finetune_amd.tps_inference import main
+
+    ck = _small_ckpt(tmp_path, T=6, tps=True)
+    out = tmp_path / "tps"
+    main(["--sim_ckpt", ck, "--synthetic", "AKDW", "--num_frames", "6", "--num_batches", "2", "--batch_size", "2",
+          "--start_idxs", "0", "1", "--end_idxs", "40", "50", "--out_dir", str(out)])
+    meta = json.loads((out / "AKDW_metadata.json").read_text())
+    assert len(meta) == 4 and all(m["start_idx"] in (0, 1) and m["end_idx"] in (40, 50) for m in meta)
+    for m in meta:
+        txt = open(m["path"]).read()
+        assert txt.count("ENDMDL") == 6 and "nan" not in txt.lower()
+
+
+def test_tps_get_sample_window_layout():
+    """get_sample: frame 0 = start frame, frame T-1 = end frame, frames between = start frame."""
+    import numpy as np
+
+    from mdgen_finetune_amd import geometry as G
+    from mdgen_finetune_amd.tps_inference import _synthetic_traj, get_sample
+
+    arr, aat = _synthetic_traj("AKDW", 16, 3)
+    s = get_sample(arr, aat, [2], [11], num_frames=5, rng=np.random.RandomState(0))
+    fr2 = G.atom14_to_frames(torch.from_numpy(arr[2:3]))
+    fr11 = G.atom14_to_frames(torch.from_numpy(arr[11:12]))
+    for t in range(4):
+        assert torch.allclose(s["trans"][t], fr2.get_trans()[0])
+    assert torch.allclose(s["trans"][4], fr11.get_trans()[0])
+    assert s["start_idx"] == 2 and s["end_idx"] == 11

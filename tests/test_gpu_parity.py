@@ -4,9 +4,15 @@ from the reference itself and, at full size, the pinned CPU oracle.
 Tolerances (stated, per the north star's "fp32 tolerance"):
   * f32 path (hip_dtype='f32', exact-f32 MFMA):  max|d| <= 1e-3 and ||d||/||ref|| <= 1e-4
   * bf16 path (perf path, bf16 GEMM/attention operands, fp32 accumulate/softmax/residual):
-    ||d||/||ref|| <= 2.5e-2 per forward, 5e-2 after a 49-step Euler solve
+    a norm bound  ||d||/||ref|| <= BF16_REL per forward (BF16_REL_SOLVE after a 49-step Euler
+    solve) AND a per-element bound  max|d| <= BF16_ELEM * max|ref|, so a localised error (one
+    head, one padded row) cannot hide inside the norm budget.  The bounds are ~2x the largest
+    error observed over this file's cases on MI355X (profiles/r02_parity_errors.jsonl, written
+    when MDG_PARITY_LOG is set).
 """
 import functools
+import json
+import os
 
 import numpy as np
 import pytest
@@ -18,6 +24,7 @@ pytestmark = pytest.mark.gpu
 
 F32_MAX, F32_REL = 1e-3, 1e-4
 BF16_REL, BF16_REL_SOLVE = 2.5e-2, 5e-2
+BF16_ELEM, BF16_ELEM_SOLVE = 5e-2, 1e-1
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -43,14 +50,30 @@ def _rel(a, b):
     return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30)
 
 
+def _log_err(dtype, solve, out, ref):
+    """Observed errors of every comparison (MDG_PARITY_LOG=path appends one JSON line each)."""
+    path = os.environ.get("MDG_PARITY_LOG")
+    if not path:
+        return
+    err = np.abs(np.asarray(out, np.float64) - np.asarray(ref, np.float64))
+    rec = {"test": os.environ.get("PYTEST_CURRENT_TEST", "?").split(" ")[0], "dtype": dtype, "solve": solve,
+           "max_abs": float(err.max()), "max_ref": float(np.abs(ref).max()), "rel_fro": float(_rel(out, ref)),
+           "elem_frac": float(err.max() / max(np.abs(ref).max(), 1e-30))}
+    with open(path, "a") as f:
+        f.write(json.dumps(rec) + "\n")
+
+
 def _check(out, ref, dtype, solve=False):
     out = out.detach().float().cpu().numpy() if torch.is_tensor(out) else out
     assert np.isfinite(out).all()
+    _log_err(dtype, solve, out, ref)
     if dtype == "f32":
         assert np.abs(out - ref).max() <= F32_MAX, np.abs(out - ref).max()
         assert _rel(out, ref) <= F32_REL, _rel(out, ref)
     else:
         assert _rel(out, ref) <= (BF16_REL_SOLVE if solve else BF16_REL), _rel(out, ref)
+        elem = np.abs(out - ref).max() / max(np.abs(ref).max(), 1e-30)
+        assert elem <= (BF16_ELEM_SOLVE if solve else BF16_ELEM), elem
 
 
 FWD = ["small_sim_T1", "small_sim_T8", "small_sim_pad", "small_tps_T8", "full_sim_T1", "full_sim_T64",
@@ -93,6 +116,7 @@ def test_euler_solve_matches_reference_golden(name, dtype):
             _check(ys[-1], d["out_euler_final"], dtype, solve=True)
 
 
+@functools.lru_cache(maxsize=4)
 def _oracle_full(T, seed=7, B=1, n_pad=0, L=4):
     from mdgen_finetune_amd import synthetic
     from oracle import mdgen_oracle as O
@@ -293,3 +317,22 @@ def test_tps_euler_solve_T100_matches_oracle(dtype):
     assert ys.shape == ref.shape
     _check(ys[1], ref[1].numpy(), dtype)
     _check(ys[-1], ref[-1].numpy(), dtype, solve=True)
+
+
+def test_atlas_full_size_T250_crop256_matches_oracle_both_dtypes():
+    """BASELINE config 5 at its stated size: ATLAS forward-sim, T=250 frames x crop 256, B=1,
+    20 % padded residues (51 of 256), default model dims; f32 and bf16 HIP paths against the
+    oracle's T=250 / L=256 forward (one CPU forward, ~10 s on the box's host threads)."""
+    from mdgen_finetune_amd.rigid_utils import Rigid, Rotation
+
+    inp, ref, cfg = _oracle_full(250, seed=23, B=1, n_pad=51, L=256)
+    g = lambda k: torch.from_numpy(inp[k]).cuda()  # noqa: E731
+    for dtype in ("f32", "bf16"):
+        m, _ = build_model(cfg, "cuda", T=250)
+        m.hip_dtype = dtype
+        with torch.no_grad():
+            v = m(g("x"), g("t"), g("mask"), start_frames=Rigid(Rotation(rot_mats=g("rots")), g("trans")),
+                  x_cond=g("x_cond"), x_cond_mask=g("x_cond_mask"), aatype=g("aatype"))
+        _check(v, ref, dtype)
+        del m
+        torch.cuda.empty_cache()

@@ -138,13 +138,26 @@ def _ddp_worker(rank, world, port, out):
     from mdgen_finetune_amd.train import Trainer, setup_distributed
 
     r, w, dev = setup_distributed()
-    a = _args(["--grad_clip", "0", "--bucket_cap_mb", "1"])
+    dist._DEFAULT_FIRST_BUCKET_BYTES = 50 * 1024  # DDP's first bucket would hold this whole small model
+    a = _args(["--grad_clip", "0", "--bucket_cap_mb", "0.05"])
     tr = Trainer(a, r, w, dev)
     b = _batch(a, B=2, seed=100 + rank)
     # local gradient without communication, from the same (t, x0) draw
     g = torch.Generator().manual_seed(7 + rank)
     x0, t = torch.randn(2, 8, 4, 21, generator=g), torch.rand(2, generator=g)
     tr.wrapper.transport.sample = lambda x1: (t, x0, x1)
+    # record the order in which DDP launches bucket all-reduces and autograd finishes gradients
+    from torch.distributed.algorithms.ddp_comm_hooks.default_hooks import allreduce_hook
+
+    events = []
+
+    def hook(state, bucket):
+        events.append(("bucket", bucket.index()))
+        return allreduce_hook(None, bucket)
+
+    tr.model.register_comm_hook(None, hook)
+    for n, p in tr.wrapper.model.named_parameters():
+        p.register_post_accumulate_grad_hook(lambda p, n=n: events.append(("grad", n)))
     prep = tr.wrapper.prep_batch(b)
     loss = tr.wrapper.transport.training_losses(tr.wrapper.model, prep["latents"], mask=prep["loss_mask"],
                                                 model_kwargs=prep["model_kwargs"])["loss"].mean()
@@ -155,8 +168,18 @@ def _ddp_worker(rank, world, port, out):
     dist.all_reduce(ref)
     ref /= w
     # the DDP path (bucketed all-reduce during backward)
+    # DDP does not bucket its first iterations (one all-reduce after backward; with static_graph
+    # the buckets are rebuilt in backward order after iteration 2), so measure on the third
+    for _ in range(2):
+        tr.wrapper.general_step(b, model=tr.model).backward()
+        tr.optimizer.zero_grad(set_to_none=True)
+    events.clear()
     loss = tr.wrapper.general_step(b, model=tr.model)
     loss.backward()
+    kinds = [k for k, _ in events]
+    n_buckets = len({i for k, i in events if k == "bucket"})
+    first_bucket = kinds.index("bucket") if "bucket" in kinds else len(kinds)
+    last_grad = len(kinds) - 1 - kinds[::-1].index("grad") if "grad" in kinds else -1
     ddp = torch.cat([(p.grad if p.grad is not None else torch.zeros_like(p)).flatten()
                      for p in tr.wrapper.model.parameters()])
     tr.optimizer.step()
@@ -164,7 +187,8 @@ def _ddp_worker(rank, world, port, out):
     gathered = [torch.zeros_like(params) for _ in range(w)]
     dist.all_gather(gathered, params)
     out[rank] = (float((ddp - ref).abs().max()), float(ref.abs().max()),
-                 float((gathered[0] - gathered[1]).abs().max()), float((local - ref).abs().max()))
+                 float((gathered[0] - gathered[1]).abs().max()), float((local - ref).abs().max()),
+                 n_buckets, first_bucket, last_grad)
     dist.destroy_process_group()
 
 
@@ -173,7 +197,65 @@ def test_ddp_world2_gloo_allreduce_matches_local_mean():
     out = mgr.dict()
     mp.spawn(_ddp_worker, args=(2, _free_port(), out), nprocs=2, join=True)
     for r in range(2):
-        err, scale, drift, spread = out[r]
+        err, scale, drift, spread, n_buckets, first_bucket, last_grad = out[r]
         assert err <= 1e-6 * max(1.0, scale), (r, err, scale)
         assert drift == 0.0
         assert spread > 0.0  # the ranks really had different data
+        # overlap: several buckets, and the first bucket's all-reduce was launched while
+        # backward was still producing gradients (before the last parameter's grad landed)
+        assert n_buckets >= 2, n_buckets
+        assert first_bucket < last_grad, (first_bucket, last_grad)
+
+
+def _bench_worker(rank, world, port, out):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+
+    el = bench.max_over_ranks(1.0 + 0.5 * rank, world, torch.device("cpu"))  # rank r timed 1 + r/2 s
+    out[rank] = (el, bench.job_value(world, 16, 1000, 49, 10, el))
+    dist.destroy_process_group()
+
+
+def test_bench_n_rank_reporting_world2_gloo():
+    """bench.py's N-rank reduction: every rank sees the max-over-ranks time, and the reported
+    value is the WHOLE-job frames (world x B x T x 49 x steps) over that time."""
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_bench_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    for r in range(2):
+        el, value = out[r]
+        assert el == 1.5
+        assert value == 2 * 16 * 1000 * 49 * 10 / 1.5
+
+
+def test_precision_strings_mapped_or_refused():
+    from mdgen_finetune_amd.train import resolve_precision
+
+    cpu = torch.device("cpu")
+    assert resolve_precision("32-true", cpu) is None
+    assert resolve_precision("bf16-mixed", cpu) == torch.bfloat16
+    for bad in ("bf16-true", "16-true", "64", "mixed"):
+        with pytest.raises(NotImplementedError):
+            resolve_precision(bad, cpu)
+
+
+def test_resume_mid_epoch_continues_same_epoch(tmp_path):
+    """A --max_steps save lands mid-epoch: resuming finishes that epoch's remaining batches
+    (Lightning's fit-loop semantics) instead of skipping to the next epoch."""
+    from mdgen_finetune_amd.checkpoint import load_checkpoint
+    from mdgen_finetune_amd.train import Trainer
+
+    a = _args(["--max_steps", "1", "--epochs", "1", "--synthetic_size", "8"], tmp_path)  # 4 batches / epoch
+    tr = Trainer(a)
+    tr.fit()
+    path = os.path.join(tmp_path, sorted(os.listdir(tmp_path))[-1])
+    ck = load_checkpoint(path)
+    assert ck["loops"]["fit_loop"] == {"epoch_complete": False, "batches_done": 1}
+    a2 = _args(["--epochs", "1", "--synthetic_size", "8", "--ckpt", path], tmp_path)
+    tr2 = Trainer(a2)
+    assert tr2.epoch == 0 and tr2.skip_batches == 1
+    tr2.fit()
+    assert tr2.global_step == 4  # 1 before the save + the epoch's 3 remaining batches
