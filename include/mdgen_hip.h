@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define MDG_ABI_VERSION 9
+#define MDG_ABI_VERSION 10
 #define MDG_MAX_LAYERS 16
 #define MDG_DP 32 /* padded head dim of every attention operand buffer (head_dim <= 31) */
 
@@ -50,7 +50,7 @@ enum {
 /* GEMM building block: out = epilogue( prologue(A) . W^T + bias ) */
 enum { MDG_A_PLAIN = 0, MDG_A_LNMOD = 1 };
 enum { MDG_EPI_STORE = 0, MDG_EPI_GATE_RES = 1, MDG_EPI_QKV = 2, MDG_EPI_EULER = 3, MDG_EPI_ATTN_SPATIAL = 4 };
-enum { MDG_ACT_NONE = 0, MDG_ACT_GELU = 1, MDG_ACT_SILU = 2 };
+enum { MDG_ACT_NONE = 0, MDG_ACT_GELU = 1, MDG_ACT_SILU = 2, MDG_ACT_DGELU = 3 };
 enum { MDG_QKV_SPATIAL = 0, MDG_QKV_TEMPORAL = 1 };
 
 typedef struct {
@@ -132,6 +132,12 @@ typedef struct {
      mdg_layer_weights) and the frame's residues with key_mask != 0 (null = all) of q.k, times
      v.  q|k|v are never written. */
   const float* kvb; const float* key_mask;
+  /* Training extensions (null / 0 = off; any of them selects the non-fused tile kernels):
+     resid_in  GATE_RES reads the residual from resid_in [M][ldr] and writes resid (out of place);
+     aux       STORE with act GELU: also stores CT(pre-activation) to aux [M][ldaux] (saved for
+               the backward); STORE with act DGELU: out = acc * gelu'(aux) (aux = the forward's
+               pre-activation, read); GATE_RES: also stores CT(acc + bias), the pre-gate value. */
+  const float* resid_in; void* aux; int32_t ldaux;
 } mdg_gemm_desc;
 
 int mdg_abi_version(void);
@@ -195,6 +201,11 @@ int mdg_attn_spatial(int32_t dtype, int32_t n_frames, int32_t L, int32_t H, int3
 int mdg_attn_temporal(int32_t dtype, int32_t B, int32_t T, int32_t L, int32_t H, int32_t D,
                       const void* qkv_t, const float* kbias, const float* kvb, void* out,
                       void* stream);
+/* The same, also writing lse [B*L][H][T] = log2 of each query row's softmax normaliser in the
+   planes' score units (the training backward recomputes P from it). */
+int mdg_attn_temporal_lse(int32_t dtype, int32_t B, int32_t T, int32_t L, int32_t H, int32_t D,
+                          const void* qkv_t, const float* kbias, const float* kvb, void* out, float* lse,
+                          void* stream);
 
 /* Batch preparation (NewMDGenWrapper.prep_batch, wrapper.py:283-365 with get_offsets,
    utils.py:7-14, and rot_to_quat, rigid_utils.py:191-210), per token (b, t, l):
@@ -229,6 +240,83 @@ int mdg_latents_to_atom14(int32_t B, int32_t T, int32_t L, int32_t latent, int32
                           const int64_t* aatype, const float* default_frames, const int32_t* group_idx,
                           const float* atom_mask, const float* lit, float* atom14, float* out_rots,
                           float* out_trans, void* stream);
+
+
+/* ---------------------------------------------------------------------------------------
+   Training (Transport.training_losses -> model forward -> loss.backward(): transport.py:137-222,
+   wrapper.py:367-403; the block latent_model.py:456-493 under autograd).  The forward of one
+   LatentMDGenLayer runs here and keeps what its backward needs; the backward runs as the
+   kernels below plus the weight / input-gradient GEMMs (mdg_gemm with DGELU for fc1's input
+   gradient; the weight-gradient GEMMs dW = dY^T X are plain library GEMMs on the host side).
+   Every buffer is caller-owned. */
+typedef struct {
+  void* xn[3];       /* CT [N][C]: LN + modulate outputs feeding the spatial q|k|v, temporal
+                        q|k|v and fc1 GEMMs */
+  float* stats[3];   /* [N][2] (mean, rstd) of those three LayerNorms */
+  void* qkv_s;       /* L < 16: CT [N][3C] spatial q|k|v (q scaled, q / k RoPE-rotated, packed
+                        order); L >= 16: CT [3][B*T][H][L][32] planes (k, v pad column D = 1) */
+  float* lse_s;      /* L >= 16: [B*T][H][L] log2-sum-exp2 of the spatial softmax rows */
+  void* qkv_t;       /* CT [3][B*L][H][T][32] temporal q|k|v planes (k, v pad column D = 1) */
+  float* lse_t;      /* [B*L][H][T] */
+  void* o[2];        /* CT [N][C] attention outputs: spatial, temporal */
+  void* y[3];        /* CT [N][C] pre-gate projection outputs: spatial out_proj, temporal
+                        out_proj, fc2 */
+  float* h1;         /* fp32 [N][C] residual after the spatial sublayer */
+  float* h2;         /* fp32 [N][C] residual after the temporal sublayer */
+  void* u;           /* CT [N][F] fc1 pre-activation */
+  void* act;         /* CT [N][F] gelu(u), fc2's input */
+  int32_t init_planes; /* nonzero: zero the plane buffers and set their pad columns first
+                          (fresh allocations); 0: the pads are already in place */
+} mdg_layer_saved;
+
+/* Key-padding biases from mask [B,T,L] (0 -> -inf): temporal [B*L][T], spatial [B*T][L]. */
+int mdg_mask_bias(int32_t B, int32_t T, int32_t L, const float* mask, float* kbias_t, float* kbias_s,
+                  void* stream);
+
+/* One LatentMDGenLayer forward for training: h_out = layer(h_in) (both fp32 [N][C], distinct),
+   mods = this layer's adaLN rows [B][9C]; everything the backward needs is written to *sv.
+   mask [B,T,L] (spatial key validity for L < 16), kbias_t / kbias_s from mdg_mask_bias. */
+int mdg_layer_fwd_train(const mdg_dims* d, const mdg_layer_weights* w, const float* rope_l, const float* rope_t,
+                        const float* mods, const float* mask, const float* kbias_t, const float* kbias_s,
+                        const float* h_in, float* h_out, const mdg_layer_saved* sv, void* stream);
+
+/* Row blocks per trajectory of mdg_ln_gate_bwd's partial sums. */
+int32_t mdg_ln_gate_bwd_blocks(int32_t rows_per_b);
+/* Backward of  xn = LN(h_ln)*(1 + scale) + shift  (no-affine LN, stats from the forward) and of
+   the gated residual  h = h_prev + gate * y  of the sublayer below, per row m (b = m / rows_per_b):
+     dh_out = dh_res + LN_bwd(dxn)                      (dxn null: dh_out = dh_res)
+     dy     = CT(dh_out * gate[b])                      (y null: skipped)
+   part [B][blocks][4][C] (fp32): per row block the column sums of dxn (d shift), dxn * xhat
+   (d scale), dh_out * y (d gate) and dh_out * gate (the projection's bias gradient).
+   mods rows [B][mod_stride]: shift at shift_off, scale at scale_off, gate at gate_off.
+   dh_out may alias dh_res. */
+int mdg_ln_gate_bwd(int32_t dtype, int32_t M, int32_t C, int32_t rows_per_b, const void* dxn, const float* h_ln,
+                    const float* stats, const float* mods, int32_t mod_stride, int32_t shift_off, int32_t scale_off,
+                    const float* dh_res, float* dh_out, const void* y, int32_t gate_off, void* dy, float* part,
+                    void* stream);
+
+/* Bias-key gradient partial slots per head of the attention backward kernels below. */
+int32_t mdg_attn_temporal_bwd_parts(int32_t dtype, int32_t B, int32_t T, int32_t L);
+int32_t mdg_attn_spatial_bwd_parts(int32_t n_frames, int32_t L, int32_t D);
+/* Scratch of mdg_attn_temporal_bwd: dO planes CT [B*L][H][T][32] then delta fp32 [B*L][H][T]. */
+size_t mdg_attn_temporal_bwd_scratch(int32_t dtype, int32_t B, int32_t T, int32_t L, int32_t H);
+/* Temporal (and L >= 16 spatial) attention backward: from the forward's planes (qkv_t), lse,
+   output o (CT [N][C]) and its gradient dout (CT [N][C]), writes dq | dk | dv of the linear
+   projections (RoPE and the q scale undone: qscale = D^-1/2) into dqkv (CT, token-major rows of
+   ld_dqkv >= 3C, packed column order); kscale = ln 2 for planes in log2 units (the forward's
+   q carries log2 e).  bias_k / bias_v gradients (w.r.t. the rotated kvb rows) are written as
+   per-slot partials bpart [H][parts][2][32].  generic = 1 selects the scalar kernels (the
+   fp32 path always uses them). */
+int mdg_attn_temporal_bwd(int32_t dtype, int32_t B, int32_t T, int32_t L, int32_t H, int32_t D, const void* qkv_t,
+                          const float* kbias, const float* kvb, const void* o, const void* dout, const float* lse,
+                          const float* rope, int32_t rope_rows, void* scratch, void* dqkv, int32_t ld_dqkv,
+                          float* bpart, float qscale, float kscale, int32_t generic, void* stream);
+/* Spatial attention backward (L < 16): q|k|v [N][3C] as saved by the forward, dout CT [N][C];
+   dq | dk | dv into dqkv [N][3C]; bias partials bpart [H][parts][2][32] (zero the buffer:
+   columns >= D of a slot may be left unwritten). */
+int mdg_attn_spatial_bwd(int32_t dtype, int32_t n_frames, int32_t L, int32_t H, int32_t D, const void* qkv,
+                         const float* kvb, const float* mask, const void* dout, const float* rope, int32_t rope_rows,
+                         void* dqkv, float* bpart, float qscale, void* stream);
 
 #ifdef __cplusplus
 }

@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("MDG_LIB_PATH") or os.path.join(os.path.dirname(os.pat
 MDG_F32, MDG_BF16 = 0, 1
 MDG_A_PLAIN, MDG_A_LNMOD = 0, 1
 MDG_EPI_STORE, MDG_EPI_GATE_RES, MDG_EPI_QKV, MDG_EPI_EULER, MDG_EPI_ATTN_SPATIAL = 0, 1, 2, 3, 4
-MDG_ACT_NONE, MDG_ACT_GELU, MDG_ACT_SILU = 0, 1, 2
+MDG_ACT_NONE, MDG_ACT_GELU, MDG_ACT_SILU, MDG_ACT_DGELU = 0, 1, 2, 3
 MDG_QKV_SPATIAL, MDG_QKV_TEMPORAL = 0, 1
 MDG_PREP_TPS, MDG_PREP_NO_OFFSETS, MDG_PREP_COND_FIRST, MDG_PREP_COND_LAST = 1, 2, 4, 8
 MDG_MAX_LAYERS = 16
@@ -63,7 +63,14 @@ class MdgGemmDesc(ctypes.Structure):
         ("x_in", _vp), ("v_out", _vp), ("dt", _f32), ("n_valid", _i32),
         ("xn_out", _vp), ("xn_mods", _vp), ("xn_mod_stride", _i32), ("xn_shift_off", _i32), ("xn_scale_off", _i32),
         ("kvb", _vp), ("key_mask", _vp),
+        ("resid_in", _vp), ("aux", _vp), ("ldaux", _i32),
     ]
+
+
+class MdgLayerSaved(ctypes.Structure):
+    _fields_ = [("xn", _vp * 3), ("stats", _vp * 3), ("qkv_s", _vp), ("lse_s", _vp), ("qkv_t", _vp),
+                ("lse_t", _vp), ("o", _vp * 2), ("y", _vp * 3), ("h1", _vp), ("h2", _vp), ("u", _vp), ("act", _vp),
+                ("init_planes", _i32)]
 
 
 # (name, restype, argtypes) of every exported entry point — the test suite checks that the
@@ -86,11 +93,25 @@ SIGNATURES = [
     ("mdg_gemm", _i32, [ctypes.POINTER(MdgGemmDesc), _vp]),
     ("mdg_attn_spatial", _i32, [_i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
     ("mdg_attn_temporal", _i32, [_i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
+    ("mdg_attn_temporal_lse", _i32, [_i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
     ("mdg_prep_latents", _i32, [_i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     ("mdg_latents_to_atom14", _i32, [_i32, _i32, _i32, _i32, _i32, _i32] + [_vp] * 12),
+    ("mdg_mask_bias", _i32, [_i32, _i32, _i32, _vp, _vp, _vp, _vp]),
+    ("mdg_layer_fwd_train", _i32, [ctypes.POINTER(MdgDims), ctypes.POINTER(MdgLayerWeights), _vp, _vp, _vp, _vp, _vp,
+                                   _vp, _vp, _vp, ctypes.POINTER(MdgLayerSaved), _vp]),
+    ("mdg_ln_gate_bwd_blocks", _i32, [_i32]),
+    ("mdg_ln_gate_bwd", _i32, [_i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp, _i32,
+                               _vp, _vp, _vp]),
+    ("mdg_attn_temporal_bwd_parts", _i32, [_i32, _i32, _i32, _i32]),
+    ("mdg_attn_spatial_bwd_parts", _i32, [_i32, _i32, _i32]),
+    ("mdg_attn_temporal_bwd_scratch", ctypes.c_size_t, [_i32, _i32, _i32, _i32, _i32]),
+    ("mdg_attn_temporal_bwd", _i32, [_i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32,
+                                     _vp, _vp, _i32, _vp, _f32, _f32, _i32, _vp]),
+    ("mdg_attn_spatial_bwd", _i32, [_i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _f32,
+                                    _vp]),
 ]
 
-ABI_VERSION = 9
+ABI_VERSION = 10
 _LIB = None
 
 

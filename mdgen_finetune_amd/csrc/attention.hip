@@ -32,7 +32,7 @@ __global__ __launch_bounds__(256) void attn_temporal_kernel(const CT* __restrict
                                                             const float* __restrict__ kbias,
                                                             const float* __restrict__ kvb,
                                                             CT* __restrict__ out, int T, int L,
-                                                            int H, int D, int BL) {
+                                                            int H, int D, int BL, float* __restrict__ lse) {
   constexpr int DP = MDG_DP, KC = 64, LDK = 48;  // 96-B LDS rows (bf16): conflict-free b128 + tr reads
   constexpr int VEC = 16 / sizeof(CT);
   constexpr int PIECES = KC * DP / VEC / 256;
@@ -241,6 +241,7 @@ __global__ __launch_bounds__(256) void attn_temporal_kernel(const CT* __restrict
     const float lsum = __shfl(mine, lr + 16 * g_s, 64);
     const float inv = 1.0f / lsum;
     const int q = q0 + qg * 16 + lr;
+    if (lse && q < T && lg == 0) lse[((size_t)seq * H + head) * T + q] = mt[qg] + log2f(lsum);
     if (q < T) {
       CT* orow = out + ((size_t)(b * T + q) * L + l) * C + head * D;
 #pragma unroll
@@ -369,14 +370,18 @@ __device__ __forceinline__ void ta_setup(const bf16_t* Qg, const float* kvh, int
 
 // O = O^T / row sum (O^T row D), stored as O[token][head*D + d]
 __device__ __forceinline__ void ta_store(const f32x16& o, bf16_t* out, int q, int T, int L, int H, int D, int seq,
-                                         int head, int h) {
+                                         int head, int h, float mt, float* lse) {
   const int hD = (D >> 2) & 1, regD = (D & 3) + 4 * (D >> 3);
   float mine = 0.f;
 #pragma unroll
   for (int i = 0; i < 16; ++i)
     if (i == regD) mine = o[i];
   const float other = __shfl_xor(mine, 32, 64);
-  const float inv = 1.0f / ((h == hD) ? mine : other);
+  const float lsum = (h == hD) ? mine : other;
+  const float inv = 1.0f / lsum;
+  // log2 of the row's softmax normaliser in the score units of the kernel (q pre-scaled by
+  // log2 e): the training backward recomputes P = exp2(S - lse) from it
+  if (lse && q < T && h == 0) lse[((size_t)seq * H + head) * T + q] = mt + log2f(lsum);
   if (q < T) {
     const int C = H * D, b = seq / L, l = seq % L;
     bf16_t* orow = out + ((size_t)(b * T + q) * L + l) * C + head * D;
@@ -395,7 +400,7 @@ __global__ __launch_bounds__(kTW * 64) void attn_temporal_bf16_kernel(const bf16
                                                                     const float* __restrict__ kbias,
                                                                     const float* __restrict__ kvb,
                                                                     bf16_t* __restrict__ out, int T, int L,
-                                                                    int H, int D, int BL) {
+                                                                    int H, int D, int BL, float* __restrict__ lse) {
   constexpr int DP = MDG_DP, KC = kTKC, NTH = kTW * 64;
   static_assert(KC * DP / 8 == NTH, "one 16-B K piece and one V piece per thread per chunk");
   __shared__ __attribute__((aligned(16))) bf16_t Ks[2][KC * DP];
@@ -478,7 +483,7 @@ __global__ __launch_bounds__(kTW * 64) void attn_temporal_bf16_kernel(const bf16
 #undef MDG_TA_GLOAD
 #undef MDG_TA_LSTORE
 
-  ta_store(o, out, q, T, L, H, D, seq, head, h);
+  ta_store(o, out, q, T, L, H, D, seq, head, h, mt, lse);
 }
 
 
@@ -643,7 +648,7 @@ __global__ __launch_bounds__(256) void attn_spatial_quad_kernel(const CT* __rest
 }
 
 hipError_t attn_temporal_launch(int dtype, int B, int T, int L, int H, int D, const void* qkv_t,
-                                const float* kbias, const float* kvb, void* out, hipStream_t s) {
+                                const float* kbias, const float* kvb, void* out, hipStream_t s, float* lse) {
   if (dtype == MDG_BF16) {
     // MDG_ATTN_WAVES=4 selects 4-wave blocks with 64-key chunks (tuning knob; default 8 / 128)
     static const int waves = [] {
@@ -653,21 +658,21 @@ hipError_t attn_temporal_launch(int dtype, int B, int T, int L, int H, int D, co
     if (waves == 4) {
       dim3 grid((unsigned)((T + 127) / 128 * H * B * L));
       hipLaunchKernelGGL((attn_temporal_bf16_kernel<4, 64>), grid, dim3(256), 0, s, (const bf16_t*)qkv_t, kbias, kvb,
-                         (bf16_t*)out, T, L, H, D, B * L);
+                         (bf16_t*)out, T, L, H, D, B * L, lse);
     } else {
       dim3 grid((unsigned)((T + 255) / 256 * H * B * L));
       hipLaunchKernelGGL((attn_temporal_bf16_kernel<8, 128>), grid, dim3(512), 0, s, (const bf16_t*)qkv_t, kbias, kvb,
-                         (bf16_t*)out, T, L, H, D, B * L);
+                         (bf16_t*)out, T, L, H, D, B * L, lse);
     }
     return hipGetLastError();
   }
   dim3 grid((T + 127) / 128, H, B * L);
   if (dtype == MDG_BF16)
     hipLaunchKernelGGL(attn_temporal_kernel<bf16_t>, grid, dim3(256), 0, s,
-                       (const bf16_t*)qkv_t, kbias, kvb, (bf16_t*)out, T, L, H, D, B * L);
+                       (const bf16_t*)qkv_t, kbias, kvb, (bf16_t*)out, T, L, H, D, B * L, lse);
   else
     hipLaunchKernelGGL(attn_temporal_kernel<float>, grid, dim3(256), 0, s, (const float*)qkv_t,
-                       kbias, kvb, (float*)out, T, L, H, D, B * L);
+                       kbias, kvb, (float*)out, T, L, H, D, B * L, lse);
   return hipGetLastError();
 }
 

@@ -19,7 +19,8 @@ struct GemmPlan {
 GemmPlan gemm_plan(const mdg_gemm_desc& p);
 hipError_t gemm_launch(const mdg_gemm_desc& p, const GemmPlan& g, hipStream_t s);
 hipError_t attn_temporal_launch(int dtype, int B, int T, int L, int H, int D, const void* qkv_t,
-                                const float* kbias, const float* kvb, void* out, hipStream_t s);
+                                const float* kbias, const float* kvb, void* out, hipStream_t s,
+                                float* lse = nullptr);
 hipError_t attn_spatial_launch(int dtype, int nf, int L, int H, int D, const void* qkv,
                                const float* kvb, const float* mask, void* out, hipStream_t s);
 hipError_t embed_launch(int N, int T, int L, int C, int K, const float* x, const float* W,
@@ -28,7 +29,7 @@ hipError_t embed_launch(int N, int T, int L, int C, int K, const float* x, const
 hipError_t mask_bias_launch(int B, int T, int L, const float* mask, float* kbias, float* kbias_s, hipStream_t s);
 hipError_t ln_mod_launch(int dtype, int M, int C, const float* h, const float* mods, int mod_stride,
                          int rows_per_mod, int shift_off, int scale_off, float eps, void* xn,
-                         hipStream_t s);
+                         hipStream_t s, float* stats = nullptr);
 hipError_t set_vpad_launch(int dtype, void* v, size_t rows, int D, hipStream_t s);
 hipError_t embed_ln_launch(int N, int TL, int L, int C, int K, const float* x, const float* Wt, const float* base,
                            const float* ipa, const float* mods, int mod_stride, int shift_off, int scale_off,
@@ -41,6 +42,21 @@ hipError_t latents_to_atom14_launch(int B, int T, int L, int lat, int tors_off, 
                                     const float* default_frames, const int* group_idx, const float* atom_mask,
                                     const float* lit, float* atom14, float* out_rots, float* out_trans,
                                     hipStream_t s);
+// train.hip
+int ln_gate_bwd_blocks(int TL);
+hipError_t ln_gate_bwd_launch(int dtype, int M, int C, int TL, const void* dxn, const float* hln, const float* stats,
+                              const float* mods, int mod_stride, int shift_off, int scale_off, const float* dh_res,
+                              float* dh_out, const void* y, int gate_off, void* dy, float* part, hipStream_t s);
+int attn_bwd_parts(int dtype, int B, int T, int L);
+hipError_t attn_temporal_bwd_launch(int dtype, int B, int T, int L, int H, int D, const void* qkv_t,
+                                    const float* kbias, const float* kvb, const void* o, const void* dout,
+                                    const float* lse, const float* rope, int rope_rows, void* dop, float* delta,
+                                    void* dqkv, int ldq, float* bpart, float qscale, float kscale, int generic,
+                                    hipStream_t s);
+int attn_spatial_bwd_parts(int nf, int L, int D);
+hipError_t attn_spatial_bwd_launch(int dtype, int nf, int L, int H, int D, const void* qkv, const float* kvb,
+                                   const float* mask, const void* dout, const float* rope, int rope_rows, void* dqkv,
+                                   float* bpart, float qscale, hipStream_t s);
 }  // namespace mdg
 
 namespace {
@@ -248,6 +264,18 @@ int mdg_attn_temporal(int32_t dtype, int32_t B, int32_t T, int32_t L, int32_t H,
   return hip_check(mdg::attn_temporal_launch(dtype, B, T, L, H, D, qkv_t, kbias, kvb, out,
                                              (hipStream_t)stream),
                    "attn_temporal");
+}
+
+int mdg_attn_temporal_lse(int32_t dtype, int32_t B, int32_t T, int32_t L, int32_t H, int32_t D,
+                          const void* qkv_t, const float* kbias, const float* kvb, void* out, float* lse,
+                          void* stream) {
+  if (dtype != MDG_F32 && dtype != MDG_BF16) return fail(MDG_E_DTYPE, "dtype %d", dtype);
+  if (!qkv_t || !kbias || !kvb || !out || !lse) return fail(MDG_E_ARG, "attn_temporal_lse: null pointer");
+  if (B <= 0 || T <= 0 || L <= 0 || H <= 0 || D <= 0 || D % 4 || D >= MDG_DP)
+    return fail(MDG_E_SHAPE, "attn_temporal_lse: B=%d T=%d L=%d H=%d D=%d", B, T, L, H, D);
+  if (H > 65535 || B * L > 65535) return fail(MDG_E_SHAPE, "attn_temporal_lse: grid too large");
+  return hip_check(mdg::attn_temporal_launch(dtype, B, T, L, H, D, qkv_t, kbias, kvb, out, (hipStream_t)stream, lse),
+                   "attn_temporal_lse");
 }
 
 int mdg_embed(int32_t N, int32_t T, int32_t L, int32_t C, int32_t K, const float* x,
@@ -524,6 +552,165 @@ int mdg_latents_to_atom14(int32_t B, int32_t T, int32_t L, int32_t latent, int32
                                                  ref_trans, aatype, default_frames, group_idx, atom_mask, lit,
                                                  atom14, out_rots, out_trans, (hipStream_t)stream),
                    "latents_to_atom14");
+}
+
+// ------------------------------------------------------------------------------------------
+// Training entry points (train.hip kernels + the GEMM's training epilogues).
+int mdg_mask_bias(int32_t B, int32_t T, int32_t L, const float* mask, float* kbias_t, float* kbias_s, void* stream) {
+  if (!mask || !kbias_t || !kbias_s) return fail(MDG_E_ARG, "mask_bias: null pointer");
+  if (B <= 0 || T <= 0 || L <= 0) return fail(MDG_E_SHAPE, "mask_bias: B,T,L = %d,%d,%d", B, T, L);
+  return hip_check(mdg::mask_bias_launch(B, T, L, mask, kbias_t, kbias_s, (hipStream_t)stream), "mask_bias");
+}
+
+static int init_planes(const mdg_dims* d, void* planes, int B, int T, int L, hipStream_t s) {
+  const size_t cs = ct_size(d->dtype);
+  const size_t rows = (size_t)B * L * d->H * T;
+  if (int e = hip_check(hipMemsetAsync(planes, 0, 3 * rows * MDG_DP * cs, s), "planes memset")) return e;
+  return hip_check(mdg::set_vpad_launch(d->dtype, (char*)planes + rows * MDG_DP * cs, 2 * rows, d->D, s), "set_vpad");
+}
+
+int mdg_layer_fwd_train(const mdg_dims* d, const mdg_layer_weights* w, const float* rope_l, const float* rope_t,
+                        const float* mods, const float* mask, const float* kbias_t, const float* kbias_s,
+                        const float* h_in, float* h_out, const mdg_layer_saved* sv, void* stream) {
+  if (int e = check_dims(d)) return e;
+  if (!w || !mods || !kbias_t || !h_in || !h_out || !sv || h_in == h_out)
+    return fail(MDG_E_ARG, "layer_fwd_train: null pointer or h_in == h_out");
+  for (int i = 0; i < 3; ++i)
+    if (!sv->xn[i] || !sv->stats[i] || !sv->y[i]) return fail(MDG_E_ARG, "layer_fwd_train: saved xn/stats/y %d", i);
+  if (!sv->qkv_s || !sv->qkv_t || !sv->lse_t || !sv->o[0] || !sv->o[1] || !sv->h1 || !sv->h2 || !sv->u || !sv->act)
+    return fail(MDG_E_ARG, "layer_fwd_train: null saved buffer");
+  const int B = d->B, T = d->T, L = d->L, C = d->C, H = d->H, D = d->D, F = d->F;
+  const int N = B * T * L, TL = T * L, ms = 9 * C;
+  const bool long_l = L >= kSpatialMfmaMinL && (size_t)B * T <= 65535;
+  if (long_l && (!sv->lse_s || !kbias_s)) return fail(MDG_E_ARG, "layer_fwd_train: L >= 16 needs lse_s, kbias_s");
+  if (!long_l && L >= kSpatialMfmaMinL) return fail(MDG_E_SHAPE, "layer_fwd_train: B*T > 65535 at L >= 16");
+  const float qs = 1.0f / sqrtf((float)D), log2e = 1.4426950408889634f;
+  hipStream_t s = (hipStream_t)stream;
+  if (sv->init_planes) {
+    if (int e = init_planes(d, sv->qkv_t, B, T, L, s)) return e;
+    if (long_l)
+      if (int e = init_planes(d, sv->qkv_s, B * T, L, 1, s)) return e;
+  }
+  auto ln = [&](const float* h, int i, int shift_off, int scale_off) -> int {
+    return hip_check(mdg::ln_mod_launch(d->dtype, N, C, h, mods, ms, TL, shift_off, scale_off, 1e-6f, sv->xn[i], s,
+                                        sv->stats[i]), "ln_mod(train)");
+  };
+  mdg_gemm_desc g;
+  memset(&g, 0, sizeof(g));
+  g.dtype = d->dtype; g.M = N; g.a_mode = MDG_A_PLAIN;
+  g.mods = mods; g.mod_stride = ms; g.rows_per_mod = TL;
+  g.H = H; g.D = D; g.T = T; g.L = L;
+
+  // ---- spatial sublayer (latent_model.py:466-472)
+  if (int e = ln(h_in, 0, 0, C)) return e;
+  mdg_gemm_desc q = g;
+  q.epi = MDG_EPI_QKV; q.N = 3 * C; q.K = C; q.A = sv->xn[0]; q.lda = C; q.W = w->wqkv[0]; q.ldw = C;
+  q.bias = w->bqkv[0]; q.rope = rope_l; q.rope_rows = L + 1;
+  if (long_l) {
+    q.qkv_layout = MDG_QKV_TEMPORAL; q.qkv_out = sv->qkv_s; q.qscale = qs * log2e; q.T = L; q.L = 1;
+    if (int e = mdg_gemm(&q, stream)) return e;
+    if (int e = mdg_attn_temporal_lse(d->dtype, B * T, L, 1, H, D, sv->qkv_s, kbias_s, w->kvb[0], sv->o[0], sv->lse_s,
+                                      stream))
+      return e;
+    q.T = T; q.L = L;
+  } else {
+    q.qkv_layout = MDG_QKV_SPATIAL; q.qkv_out = sv->qkv_s; q.qscale = qs;
+    if (int e = mdg_gemm(&q, stream)) return e;
+    if (int e = mdg_attn_spatial(d->dtype, B * T, L, H, D, sv->qkv_s, w->kvb[0], mask, sv->o[0], stream)) return e;
+  }
+  mdg_gemm_desc r = g;
+  r.epi = MDG_EPI_GATE_RES; r.N = C; r.K = C; r.A = sv->o[0]; r.lda = C; r.W = w->wo[0]; r.ldw = C; r.bias = w->bo[0];
+  r.resid_in = h_in; r.resid = sv->h1; r.ldr = C; r.gate = mods; r.gate_off = 2 * C; r.aux = sv->y[0]; r.ldaux = C;
+  if (int e = mdg_gemm(&r, stream)) return e;
+
+  // ---- temporal sublayer (latent_model.py:474-486)
+  if (int e = ln(sv->h1, 1, 3 * C, 4 * C)) return e;
+  q.epi = MDG_EPI_QKV; q.A = sv->xn[1]; q.W = w->wqkv[1]; q.bias = w->bqkv[1];
+  q.qkv_layout = MDG_QKV_TEMPORAL; q.qkv_out = sv->qkv_t; q.qscale = qs * log2e; q.rope = rope_t; q.rope_rows = T + 1;
+  if (int e = mdg_gemm(&q, stream)) return e;
+  if (int e = mdg_attn_temporal_lse(d->dtype, B, T, L, H, D, sv->qkv_t, kbias_t, w->kvb[1], sv->o[1], sv->lse_t, stream))
+    return e;
+  r.A = sv->o[1]; r.W = w->wo[1]; r.bias = w->bo[1]; r.resid_in = sv->h1; r.resid = sv->h2; r.gate_off = 5 * C;
+  r.aux = sv->y[1];
+  if (int e = mdg_gemm(&r, stream)) return e;
+
+  // ---- MLP (latent_model.py:488-491)
+  if (int e = ln(sv->h2, 2, 6 * C, 7 * C)) return e;
+  mdg_gemm_desc f1 = g;
+  f1.epi = MDG_EPI_STORE; f1.act = MDG_ACT_GELU; f1.N = F; f1.K = C; f1.A = sv->xn[2]; f1.lda = C; f1.W = w->w1;
+  f1.ldw = C; f1.bias = w->b1; f1.out = sv->act; f1.ldo = F; f1.aux = sv->u; f1.ldaux = F;
+  if (int e = mdg_gemm(&f1, stream)) return e;
+  mdg_gemm_desc f2 = g;
+  f2.epi = MDG_EPI_GATE_RES; f2.N = C; f2.K = F; f2.A = sv->act; f2.lda = F; f2.W = w->w2; f2.ldw = F; f2.bias = w->b2;
+  f2.resid_in = sv->h2; f2.resid = h_out; f2.ldr = C; f2.gate = mods; f2.gate_off = 8 * C; f2.aux = sv->y[2];
+  f2.ldaux = C;
+  return mdg_gemm(&f2, stream);
+}
+
+int32_t mdg_ln_gate_bwd_blocks(int32_t rows_per_b) { return rows_per_b > 0 ? mdg::ln_gate_bwd_blocks(rows_per_b) : 0; }
+
+int mdg_ln_gate_bwd(int32_t dtype, int32_t M, int32_t C, int32_t rows_per_b, const void* dxn, const float* h_ln,
+                    const float* stats, const float* mods, int32_t mod_stride, int32_t shift_off, int32_t scale_off,
+                    const float* dh_res, float* dh_out, const void* y, int32_t gate_off, void* dy, float* part,
+                    void* stream) {
+  if (dtype != MDG_F32 && dtype != MDG_BF16) return fail(MDG_E_DTYPE, "dtype %d", dtype);
+  if (M <= 0 || C <= 0 || C > 512 || C % 64 || rows_per_b <= 0 || M % rows_per_b)
+    return fail(MDG_E_SHAPE, "ln_gate_bwd: M=%d C=%d rows_per_b=%d", M, C, rows_per_b);
+  if (!mods || !dh_res || !dh_out || !part) return fail(MDG_E_ARG, "ln_gate_bwd: null mods/dh/part");
+  if (dxn && (!h_ln || !stats)) return fail(MDG_E_ARG, "ln_gate_bwd: dxn without h_ln/stats");
+  if (y && !dy) return fail(MDG_E_ARG, "ln_gate_bwd: y without dy");
+  return hip_check(mdg::ln_gate_bwd_launch(dtype, M, C, rows_per_b, dxn, h_ln, stats, mods, mod_stride, shift_off,
+                                           scale_off, dh_res, dh_out, y, gate_off, dy, part, (hipStream_t)stream),
+                   "ln_gate_bwd");
+}
+
+int32_t mdg_attn_temporal_bwd_parts(int32_t dtype, int32_t B, int32_t T, int32_t L) {
+  if (B <= 0 || T <= 0 || L <= 0) return 0;
+  return mdg::attn_bwd_parts(dtype, B, T, L);
+}
+
+int32_t mdg_attn_spatial_bwd_parts(int32_t n_frames, int32_t L, int32_t D) {
+  if (n_frames <= 0 || L <= 0) return 0;
+  return mdg::attn_spatial_bwd_parts(n_frames, L, D);
+}
+
+size_t mdg_attn_temporal_bwd_scratch(int32_t dtype, int32_t B, int32_t T, int32_t L, int32_t H) {
+  const size_t rows = (size_t)B * L * H * T;
+  return align256(rows * MDG_DP * ct_size(dtype)) + align256(rows * sizeof(float));
+}
+
+int mdg_attn_temporal_bwd(int32_t dtype, int32_t B, int32_t T, int32_t L, int32_t H, int32_t D, const void* qkv_t,
+                          const float* kbias, const float* kvb, const void* o, const void* dout, const float* lse,
+                          const float* rope, int32_t rope_rows, void* scratch, void* dqkv, int32_t ld_dqkv,
+                          float* bpart, float qscale, float kscale, int32_t generic, void* stream) {
+  if (dtype != MDG_F32 && dtype != MDG_BF16) return fail(MDG_E_DTYPE, "dtype %d", dtype);
+  if (!qkv_t || !kbias || !kvb || !o || !dout || !lse || !scratch || !dqkv || !bpart)
+    return fail(MDG_E_ARG, "attn_temporal_bwd: null pointer");
+  if (B <= 0 || T <= 0 || L <= 0 || H <= 0 || D <= 0 || D % 4 || D >= MDG_DP || ld_dqkv < 3 * H * D ||
+      ld_dqkv % 4)
+    return fail(MDG_E_SHAPE, "attn_temporal_bwd: B=%d T=%d L=%d H=%d D=%d ld=%d", B, T, L, H, D, ld_dqkv);
+  if (rope && rope_rows < T) return fail(MDG_E_SHAPE, "attn_temporal_bwd: rope table too short");
+  if ((size_t)B * L * H > 65535u * 256u) return fail(MDG_E_SHAPE, "attn_temporal_bwd: grid too large");
+  const size_t rows = (size_t)B * L * H * T;
+  void* dop = scratch;
+  float* delta = (float*)((char*)scratch + align256(rows * MDG_DP * ct_size(dtype)));
+  return hip_check(mdg::attn_temporal_bwd_launch(dtype, B, T, L, H, D, qkv_t, kbias, kvb, o, dout, lse, rope,
+                                                 rope_rows, dop, delta, dqkv, ld_dqkv, bpart, qscale, kscale,
+                                                 generic || dtype == MDG_F32, (hipStream_t)stream),
+                   "attn_temporal_bwd");
+}
+
+int mdg_attn_spatial_bwd(int32_t dtype, int32_t n_frames, int32_t L, int32_t H, int32_t D, const void* qkv,
+                         const float* kvb, const float* mask, const void* dout, const float* rope, int32_t rope_rows,
+                         void* dqkv, float* bpart, float qscale, void* stream) {
+  if (dtype != MDG_F32 && dtype != MDG_BF16) return fail(MDG_E_DTYPE, "dtype %d", dtype);
+  if (!qkv || !kvb || !dout || !dqkv || !bpart) return fail(MDG_E_ARG, "attn_spatial_bwd: null pointer");
+  if (n_frames <= 0 || L <= 0 || L > 16 || H <= 0 || D <= 0 || D % 4 || D >= MDG_DP)
+    return fail(MDG_E_SHAPE, "attn_spatial_bwd: nf=%d L=%d H=%d D=%d (L <= 16)", n_frames, L, H, D);
+  if (rope && rope_rows < L) return fail(MDG_E_SHAPE, "attn_spatial_bwd: rope table too short");
+  return hip_check(mdg::attn_spatial_bwd_launch(dtype, n_frames, L, H, D, qkv, kvb, mask, dout, rope, rope_rows, dqkv,
+                                                bpart, qscale, (hipStream_t)stream),
+                   "attn_spatial_bwd");
 }
 
 }  // extern "C"

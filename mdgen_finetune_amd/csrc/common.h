@@ -120,6 +120,26 @@ __device__ __forceinline__ float gelu_fast(float x) {
   return x >= 0.f ? x * (1.0f - 0.5f * q) : x * (0.5f * q);
 }
 
+// d/dx of the exact-erf GELU: Phi(x) + x phi(x)  (the training backward of layers.py:78-85)
+__device__ __forceinline__ float gelu_grad(float x) {
+  return 0.5f * (1.0f + erff(x * 0.70710678118654752440f)) + x * 0.39894228040143267794f * expf(-0.5f * x * x);
+}
+
+// the same with Phi from the A&S erfc of gelu_fast (bf16 path: the derivative of what the
+// forward computed)
+__device__ __forceinline__ float gelu_grad_fast(float x) {
+  const float a = fabsf(x) * 0.70710678118654752440f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, a, 1.0f));
+  float q = fmaf(1.061405429f, t, -1.453152027f);
+  q = fmaf(q, t, 1.421413741f);
+  q = fmaf(q, t, -0.284496736f);
+  q = fmaf(q, t, 0.254829592f);
+  const float e = __builtin_amdgcn_exp2f(-a * a * 1.4426950408889634f);  // exp(-x^2/2)
+  q *= t * e;                                                             // erfc(|x|/sqrt2)
+  const float phi_cdf = x >= 0.f ? 1.0f - 0.5f * q : 0.5f * q;
+  return phi_cdf + x * 0.39894228040143267794f * e;
+}
+
 __device__ __forceinline__ float silu(float x) { return x / (1.0f + expf(-x)); }
 
 static inline int cdiv(int a, int b) { return (a + b - 1) / b; }

@@ -94,7 +94,7 @@ template <typename CT, int W>
 __global__ __launch_bounds__(256) void ln_mod_kernel(int M, int C, const float* __restrict__ h,
                                                      const float* __restrict__ mods, int mod_stride,
                                                      int rows_per_mod, int shift_off, int scale_off,
-                                                     float eps, CT* __restrict__ xn) {
+                                                     float eps, CT* __restrict__ xn, float* __restrict__ stats) {
   constexpr int E = 8 / W, R = 4;  // C <= 512
   const int lane = threadIdx.x & 63;
   const int m0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * R;
@@ -160,6 +160,7 @@ __global__ __launch_bounds__(256) void ln_mod_kernel(int M, int C, const float* 
           ss += a * a;
         }
     const float rs = 1.0f / sqrtf(wave_sum(ss) / (float)C + eps);
+    if (stats && lane == 0) *reinterpret_cast<float2*>(stats + 2 * (size_t)m) = make_float2(mean, rs);
 #pragma unroll
     for (int e = 0; e < E; ++e) {
       if (e < nE) {
@@ -374,11 +375,11 @@ hipError_t embed_ln_launch(int N, int TL, int L, int C, int K, const float* x, c
 
 hipError_t ln_mod_launch(int dtype, int M, int C, const float* h, const float* mods, int mod_stride,
                          int rows_per_mod, int shift_off, int scale_off, float eps, void* xn,
-                         hipStream_t s) {
+                         hipStream_t s, float* stats) {
   dim3 grid((M + 15) / 16);
 #define MDG_LN(CTT, W)                                                                        \
   hipLaunchKernelGGL((ln_mod_kernel<CTT, W>), grid, dim3(256), 0, s, M, C, h, mods, mod_stride, \
-                     rows_per_mod, shift_off, scale_off, eps, (CTT*)xn)
+                     rows_per_mod, shift_off, scale_off, eps, (CTT*)xn, stats)
   const bool w2 = (C % 128) == 0;
   if (dtype == MDG_BF16) {
     if (w2) MDG_LN(bf16_t, 2); else MDG_LN(bf16_t, 1);

@@ -60,7 +60,11 @@ __device__ __forceinline__ void epi4(const mdg_gemm_desc& p, int m, int n, float
   }
   if constexpr (EPI == MDG_EPI_STORE) {
     if (p.act == MDG_ACT_GELU) {
+      if (p.aux) st4<CT>(reinterpret_cast<CT*>(p.aux) + (size_t)m * p.ldaux + n, v.x, v.y, v.z, v.w);
       v.x = gelu_erf(v.x); v.y = gelu_erf(v.y); v.z = gelu_erf(v.z); v.w = gelu_erf(v.w);
+    } else if (p.act == MDG_ACT_DGELU) {
+      const float4 u = ld4f<CT>(reinterpret_cast<const CT*>(p.aux) + (size_t)m * p.ldaux + n);
+      v.x *= gelu_grad(u.x); v.y *= gelu_grad(u.y); v.z *= gelu_grad(u.z); v.w *= gelu_grad(u.w);
     } else if (p.act == MDG_ACT_SILU) {
       v.x = silu(v.x); v.y = silu(v.y); v.z = silu(v.z); v.w = silu(v.w);
     }
@@ -68,7 +72,8 @@ __device__ __forceinline__ void epi4(const mdg_gemm_desc& p, int m, int n, float
     else st4<CT>(reinterpret_cast<CT*>(p.out) + (size_t)m * p.ldo + n, v.x, v.y, v.z, v.w);
   } else if constexpr (EPI == MDG_EPI_GATE_RES) {
     float4* R = reinterpret_cast<float4*>(p.resid + (size_t)m * p.ldr + n);
-    float4 hv = *R;
+    float4 hv = p.resid_in ? *reinterpret_cast<const float4*>(p.resid_in + (size_t)m * p.ldr + n) : *R;
+    if (p.aux) st4<CT>(reinterpret_cast<CT*>(p.aux) + (size_t)m * p.ldaux + n, v.x, v.y, v.z, v.w);
     if (p.gate) {
       const float4 g = *reinterpret_cast<const float4*>(
           p.gate + (size_t)(m / p.rows_per_mod) * p.mod_stride + p.gate_off + n);
@@ -429,7 +434,15 @@ __device__ __forceinline__ void epi_tile(const mdg_gemm_desc& p, const float* __
         v[u] = *reinterpret_cast<const float4*>(stage + (r0 + RS * (u0 + u)) * LDS_ST + c);
         v[u].x += bb.x; v[u].y += bb.y; v[u].z += bb.z; v[u].w += bb.w;
         if (p.act == MDG_ACT_GELU) {
+          if (p.aux && m0 + r0 + RS * (u0 + u) < M)
+            st4<bf16_t>(reinterpret_cast<bf16_t*>(p.aux) + (size_t)(m0 + r0 + RS * (u0 + u)) * p.ldaux + n, v[u].x,
+                        v[u].y, v[u].z, v[u].w);
           v[u].x = gelu_fast(v[u].x); v[u].y = gelu_fast(v[u].y); v[u].z = gelu_fast(v[u].z); v[u].w = gelu_fast(v[u].w);
+        } else if (p.act == MDG_ACT_DGELU) {
+          const int mm = min(m0 + r0 + RS * (u0 + u), M - 1);
+          const float4 a = ld4f<bf16_t>(reinterpret_cast<const bf16_t*>(p.aux) + (size_t)mm * p.ldaux + n);
+          v[u].x *= gelu_grad_fast(a.x); v[u].y *= gelu_grad_fast(a.y);
+          v[u].z *= gelu_grad_fast(a.z); v[u].w *= gelu_grad_fast(a.w);
         } else if (p.act == MDG_ACT_SILU) {
           v[u].x = silu(v[u].x); v[u].y = silu(v[u].y); v[u].z = silu(v[u].z); v[u].w = silu(v[u].w);
         }
@@ -450,7 +463,7 @@ __device__ __forceinline__ void epi_tile(const mdg_gemm_desc& p, const float* __
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int m = min(m0 + r0 + RS * (u0 + u), M - 1);
-        hv[u] = *reinterpret_cast<const float4*>(p.resid + (size_t)m * p.ldr + n);
+        hv[u] = *reinterpret_cast<const float4*>((p.resid_in ? p.resid_in : p.resid) + (size_t)m * p.ldr + n);
         g[u] = make_float4(1.f, 1.f, 1.f, 1.f);
         if (p.gate)
           g[u] = *reinterpret_cast<const float4*>(p.gate + (size_t)fdiv(m, p.rows_per_mod, inv_rpm) * p.mod_stride +
@@ -462,6 +475,7 @@ __device__ __forceinline__ void epi_tile(const mdg_gemm_desc& p, const float* __
         if (m >= M) break;
         float4 v = *reinterpret_cast<const float4*>(stage + (r0 + RS * (u0 + u)) * LDS_ST + c);
         v.x += bb.x; v.y += bb.y; v.z += bb.z; v.w += bb.w;
+        if (p.aux) st4<bf16_t>(reinterpret_cast<bf16_t*>(p.aux) + (size_t)m * p.ldaux + n, v.x, v.y, v.z, v.w);
         float4 h = hv[u];
         if (p.gate) {
           h.x += g[u].x * v.x; h.y += g[u].y * v.y; h.z += g[u].z * v.z; h.w += g[u].w * v.w;
@@ -1347,8 +1361,9 @@ GemmPlan gemm_plan(const mdg_gemm_desc& p) {
     g.bn = kSpaBN;
     return g;
   }
+  const bool ext = p.resid_in || p.aux;  // training extensions: epi4 / epi_tile kernels only
   if (bf && ln) cfg = (p.N % 128 == 0) ? (big ? 0 : 2) : (p.N % 32 == 0 ? (big ? 1 : 3) : -1);
-  else if (bf && p.epi == MDG_EPI_GATE_RES && p.xn_out && p.K % 64 == 0 && p.lda % 8 == 0 && p.ldw % 8 == 0 &&
+  else if (bf && !ext && p.epi == MDG_EPI_GATE_RES && p.xn_out && p.K % 64 == 0 && p.lda % 8 == 0 && p.ldw % 8 == 0 &&
            (p.N == 128 || p.N == 256 || p.N == 384 || p.N == 512)) {
     g.cfg = kCfgRow;  // full-row gated residual + LayerNorm
     const bool b64 = rowln_bm() == 64 && p.N <= 384;
@@ -1365,7 +1380,7 @@ GemmPlan gemm_plan(const mdg_gemm_desc& p) {
       const char* e = getenv("MDG_GEMM_TILE");
       return e ? atoi(e) : 0;
     }();
-    if (forced == 256) {
+    if (forced == 256 && !ext) {
       g.cfg = kCfgB8;  // 256x128, 3-stage glds ring
       g.smem = kB8Smem;
       g.bm = kB8M;

@@ -1,0 +1,1025 @@
+// Training backward of the MDGen block on gfx950: the kernels autograd needs around the
+// forward GEMMs, so that a LatentMDGenLayer's forward AND backward run in libmdgen_hip.so
+// (reference: Transport.training_losses -> model(xt, t, **kw) -> loss.backward(),
+// transport.py:137-222, wrapper.py:367-403, the block latent_model.py:456-493).
+//
+//  * ln_gate_bwd: one row pass fusing the backward of a no-affine LayerNorm + adaLN modulate
+//    (latent_model.py:467/475/489, layers.py:14-15) with the backward of the gated residual
+//    of the sublayer below it (x + gate * y, latent_model.py:472/486/491): the residual
+//    gradient dh is read once, the LN branch gradient added, dh written once, and the next
+//    projection's output gradient dy = dh * gate produced from the same registers.  The adaLN
+//    parameter gradients (d shift, d scale, d gate) and the projection's bias gradient are
+//    column sums per trajectory: per-block partials, summed deterministically by the caller.
+//  * attention backward (mha.py:255-397 under autograd), flash-style: P is recomputed from
+//    the forward's saved q|k|v planes and per-row log2-sum-exp2 (lse), never stored.
+//      attn_bwd_prep      delta = rowsum(dO * O) and dO scattered into the [seq][head][T][32]
+//                         plane layout the MFMA kernels stage;
+//      dq kernel          per wave 32 queries, keys streamed through LDS: S^T = K Q^T,
+//                         dP^T = V dO^T, dS = P (dP - delta), dQ^T += K^T dS^T  (K^T by the
+//                         ds_read_b64_tr_b16 transpose of the same swizzled K image);
+//      dk/dv kernel       per wave 32 keys, queries streamed: S = Q K^T, dP = dO V^T,
+//                         dV^T += dO^T P, dK^T += Q^T dS;
+//    both on v_mfma_f32_32x32x16_bf16 with the accumulator-as-operand map of the forward
+//    kernel (attention.hip), the bias_k / bias_v virtual key in the dq kernel's prologue, and
+//    the epilogues undoing RoPE (rotate by -theta, pair-interleaved columns) and the q scale,
+//    writing dq | dk | dv straight into the token-major [N][3C] gradient the weight GEMMs read.
+//    fp32 parity path: scalar kernels of the same algorithm (also the unit-test reference).
+//  * spatial attention backward over the L = 4 residues of a frame (+ bias key): one lane per
+//    (frame, head, residue), quad DPP broadcasts as in the forward; a scalar kernel for other L.
+// Bias-key gradients (per head) leave every kernel as per-block partials (no float atomics:
+// the sums are reproducible run to run).
+#include "../../include/mdgen_hip.h"
+#include "common.h"
+
+namespace mdg {
+
+// ------------------------------------------------------------------------------------------
+// LayerNorm + modulate backward fused with the gated-residual backward of the sublayer below.
+constexpr int kLnbRows = 64;  // rows per block (all of one trajectory)
+
+template <typename CT, int W>
+__global__ __launch_bounds__(256) void ln_gate_bwd_kernel(int M, int C, int TL, const CT* __restrict__ dxn,
+                                                          const float* __restrict__ hln,
+                                                          const float* __restrict__ stats,
+                                                          const float* __restrict__ mods, int mod_stride,
+                                                          int shift_off, int scale_off, const float* dh_res,
+                                                          float* dh_out, const CT* __restrict__ y, int gate_off,
+                                                          CT* __restrict__ dy, float* __restrict__ part) {
+  constexpr int E = 8 / W;
+  __shared__ float red[4][4][512];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int b = blockIdx.y, jb = blockIdx.x, nE = C / (64 * W);
+  const int r0 = b * TL + jb * kLnbRows;
+  const int r1 = min(b * TL + min((jb + 1) * kLnbRows, TL), M);
+  const float* mr = mods + (size_t)b * mod_stride;
+  float sc1[E][W], gt[E][W], acc[4][E][W];
+#pragma unroll
+  for (int e = 0; e < E; ++e)
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      const int k = W * lane + 64 * W * e + w;
+      const bool ok = e < nE;
+      sc1[e][w] = (ok && dxn) ? 1.0f + mr[scale_off + k] : 0.f;
+      gt[e][w] = (ok && y) ? mr[gate_off + k] : 0.f;
+#pragma unroll
+      for (int a = 0; a < 4; ++a) acc[a][e][w] = 0.f;
+    }
+  const float invC = 1.0f / (float)C;
+  for (int m = r0 + wave; m < r1; m += 4) {
+    float d[E][W];
+#pragma unroll
+    for (int e = 0; e < E; ++e)
+#pragma unroll
+      for (int w = 0; w < W; ++w) d[e][w] = (e < nE) ? dh_res[(size_t)m * C + W * lane + 64 * W * e + w] : 0.f;
+    if (dxn) {
+      const float2 st = *reinterpret_cast<const float2*>(stats + 2 * (size_t)m);
+      float g[E][W], xh[E][W], s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int e = 0; e < E; ++e)
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+          const int k = W * lane + 64 * W * e + w;
+          float dx = 0.f, hv = st.x;
+          if (e < nE) {
+            dx = (float)dxn[(size_t)m * C + k];
+            hv = hln[(size_t)m * C + k];
+          }
+          xh[e][w] = (hv - st.x) * st.y;
+          g[e][w] = dx * sc1[e][w];
+          acc[0][e][w] += dx;
+          acc[1][e][w] += dx * xh[e][w];
+          s1 += g[e][w];
+          s2 += g[e][w] * xh[e][w];
+        }
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) {
+        s1 += __shfl_xor(s1, o, 64);
+        s2 += __shfl_xor(s2, o, 64);
+      }
+      s1 *= invC;
+      s2 *= invC;
+#pragma unroll
+      for (int e = 0; e < E; ++e)
+#pragma unroll
+        for (int w = 0; w < W; ++w) d[e][w] += st.y * (g[e][w] - s1 - xh[e][w] * s2);
+    }
+    if (y) {
+#pragma unroll
+      for (int e = 0; e < E; ++e)
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+          if (e < nE) {
+            const size_t i = (size_t)m * C + W * lane + 64 * W * e + w;
+            const float yv = (float)y[i];
+            const float dyv = d[e][w] * gt[e][w];
+            dy[i] = (CT)dyv;
+            acc[2][e][w] += d[e][w] * yv;
+            acc[3][e][w] += dyv;
+          }
+        }
+    }
+    if (dxn || dh_out != dh_res) {
+#pragma unroll
+      for (int e = 0; e < E; ++e)
+#pragma unroll
+        for (int w = 0; w < W; ++w)
+          if (e < nE) dh_out[(size_t)m * C + W * lane + 64 * W * e + w] = d[e][w];
+    }
+  }
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int e = 0; e < E; ++e)
+#pragma unroll
+      for (int w = 0; w < W; ++w)
+        if (e < nE) red[wave][a][W * lane + 64 * W * e + w] = acc[a][e][w];
+  __syncthreads();
+  const int nb = gridDim.x;
+  for (int i = threadIdx.x; i < 4 * C; i += 256) {
+    const int a = i / C, c = i - a * C;
+    const float v = red[0][a][c] + red[1][a][c] + red[2][a][c] + red[3][a][c];
+    part[(((size_t)b * nb + jb) * 4 + a) * C + c] = v;
+  }
+}
+
+int ln_gate_bwd_blocks(int TL) { return (TL + kLnbRows - 1) / kLnbRows; }
+
+hipError_t ln_gate_bwd_launch(int dtype, int M, int C, int TL, const void* dxn, const float* hln, const float* stats,
+                              const float* mods, int mod_stride, int shift_off, int scale_off, const float* dh_res,
+                              float* dh_out, const void* y, int gate_off, void* dy, float* part, hipStream_t s) {
+  const int B = M / TL;
+  dim3 grid(ln_gate_bwd_blocks(TL), B);
+  const bool w2 = C % 128 == 0;
+#define MDG_LNB(CTT, W)                                                                                         \
+  hipLaunchKernelGGL((ln_gate_bwd_kernel<CTT, W>), grid, dim3(256), 0, s, M, C, TL, (const CTT*)dxn, hln, stats, \
+                     mods, mod_stride, shift_off, scale_off, dh_res, dh_out, (const CTT*)y, gate_off, (CTT*)dy, part)
+  if (dtype == MDG_BF16) {
+    if (w2) MDG_LNB(bf16_t, 2); else MDG_LNB(bf16_t, 1);
+  } else {
+    if (w2) MDG_LNB(float, 2); else MDG_LNB(float, 1);
+  }
+#undef MDG_LNB
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+// Attention backward: shared helpers.
+constexpr int kDP = MDG_DP;
+
+// RoPE inverse on a pair-interleaved column pair (2i, 2i+1) at position pos: the transpose of
+// the forward rotation x0' = x0 c - x1 s, x1' = x1 c + x0 s (gemm.hip QKV epilogue).
+__device__ __forceinline__ void rope_inv(float& a, float& b, const float* rope, int rope_rows, int half, int pos,
+                                         int pi) {
+  const float c = rope[(size_t)pos * half + pi], s = rope[(size_t)(rope_rows + pos) * half + pi];
+  const float x0 = a * c + b * s, x1 = b * c - a * s;
+  a = x0;
+  b = x1;
+}
+
+// delta[seq][head][t] = sum_d dO[n][head*D + d] * O[n][head*D + d];  dO scattered to planes
+// [seq][head][T][32] (pad columns 0).  n = (b*T + t)*L + l, seq = b*L + l.
+template <typename CT>
+__global__ __launch_bounds__(256) void attn_bwd_prep_kernel(int B, int T, int L, int H, int D, const CT* __restrict__ o,
+                                                            const CT* __restrict__ dout, CT* __restrict__ dop,
+                                                            float* __restrict__ delta) {
+  const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;
+  const size_t total = (size_t)B * T * L * H;
+  if (idx >= total) return;
+  const int head = (int)(idx % H);
+  const size_t n = idx / H;
+  const int l = (int)(n % L), t = (int)((n / L) % T), b = (int)(n / ((size_t)L * T));
+  const int seq = b * L + l, C = H * D;
+  const CT* orow = o + n * C + head * D;
+  const CT* drow = dout + n * C + head * D;
+  CT* prow = dop + (((size_t)seq * H + head) * T + t) * kDP;
+  float dl = 0.f;
+  for (int d0 = 0; d0 < kDP; d0 += 4) {
+    float4 dv = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (d0 < D) {
+      const float4 ov = ld4f<CT>(orow + d0);
+      dv = ld4f<CT>(drow + d0);
+      dl += dv.x * ov.x + dv.y * ov.y + dv.z * ov.z + dv.w * ov.w;
+    }
+    st4<CT>(prow + d0, dv.x, dv.y, dv.z, dv.w);
+  }
+  delta[((size_t)seq * H + head) * T + t] = dl;
+}
+
+// Scalar reference / fp32 path: dq pass (one thread per (seq, head, query)) including the bias
+// key and its parameter gradients (block partials over the block's 256 queries).
+template <typename CT>
+__global__ __launch_bounds__(256) void attn_bwd_dq_generic_kernel(
+    const CT* __restrict__ qkv, const CT* __restrict__ dop, const float* __restrict__ lse,
+    const float* __restrict__ delta, const float* __restrict__ kbias, const float* __restrict__ kvb,
+    const float* __restrict__ rope, int rope_rows, CT* __restrict__ dqkv, int ldq, float* __restrict__ bpart, int T,
+    int L, int H, int D, int BL, float qscale, float kscale) {
+  __shared__ float red[256][2 * kDP + 1];
+  const int sh = blockIdx.y, seq = sh / H, head = sh % H;
+  const int q = blockIdx.x * 256 + threadIdx.x;
+  const bool live = q < T;
+  const size_t plane = (size_t)BL * H * T * kDP;
+  const CT* Qg = qkv + (size_t)sh * T * kDP;
+  const CT* Kg = Qg + plane;
+  const CT* Vg = Qg + 2 * plane;
+  const CT* dOg = dop + (size_t)sh * T * kDP;
+  float qv[kDP], dov[kDP], dq[kDP];
+  const int qq = live ? q : 0;
+#pragma unroll
+  for (int d = 0; d < kDP; ++d) {
+    qv[d] = live && d < D ? (float)Qg[(size_t)qq * kDP + d] : 0.f;
+    dov[d] = live && d < D ? (float)dOg[(size_t)qq * kDP + d] : 0.f;
+  }
+  const float l2 = live ? lse[(size_t)sh * T + q] : INFINITY;
+  const float dl = live ? delta[(size_t)sh * T + q] : 0.f;
+  const float* bk = kvb + head * 2 * kDP;
+  const float* bv = bk + kDP;
+  float sb = 0.f, dpb = 0.f;
+#pragma unroll
+  for (int d = 0; d < kDP; ++d) {
+    if (d < D) {
+      sb += qv[d] * bk[d];
+      dpb += dov[d] * bv[d];
+    }
+  }
+  const float pb = live ? exp2f(sb - l2) : 0.f;
+  const float dsb = pb * (dpb - dl);
+#pragma unroll
+  for (int d = 0; d < kDP; ++d) {
+    dq[d] = dsb * bk[d];
+    red[threadIdx.x][d] = (d < D) ? dsb * qv[d] * kscale : 0.f;
+    red[threadIdx.x][kDP + d] = (d < D) ? pb * dov[d] : 0.f;
+  }
+  if (live) {
+    for (int k = 0; k < T; ++k) {
+      const float kb = kbias[(size_t)seq * T + k];
+      if (kb == -INFINITY) continue;
+      float s = kb, dp = 0.f;
+#pragma unroll
+      for (int d = 0; d < kDP; ++d) {
+        if (d < D) {
+          s += qv[d] * (float)Kg[(size_t)k * kDP + d];
+          dp += dov[d] * (float)Vg[(size_t)k * kDP + d];
+        }
+      }
+      const float ds = exp2f(s - l2) * (dp - dl);
+#pragma unroll
+      for (int d = 0; d < kDP; ++d)
+        if (d < D) dq[d] += ds * (float)Kg[(size_t)k * kDP + d];
+    }
+    const int b = seq / L, l = seq % L, half = D >> 1;
+    const size_t tok = ((size_t)b * T + q) * L + l;
+    CT* out = dqkv + tok * ldq + head * D;
+    for (int d = 0; d < D; d += 2) {
+      float a = dq[d] * qscale, c = dq[d + 1] * qscale;
+      if (rope) rope_inv(a, c, rope, rope_rows, half, q, d >> 1);
+      out[d] = (CT)a;
+      out[d + 1] = (CT)c;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 2 * kDP) {
+    float s = 0.f;
+    for (int i = 0; i < 256; ++i) s += red[i][threadIdx.x];
+    const size_t slot = (size_t)seq * gridDim.x + blockIdx.x;
+    bpart[((size_t)head * BL * gridDim.x + slot) * 2 * kDP + threadIdx.x] = s;
+  }
+}
+
+// Scalar reference / fp32 path: dk / dv pass (one thread per (seq, head, key)).
+template <typename CT>
+__global__ __launch_bounds__(256) void attn_bwd_dkdv_generic_kernel(
+    const CT* __restrict__ qkv, const CT* __restrict__ dop, const float* __restrict__ lse,
+    const float* __restrict__ delta, const float* __restrict__ kbias, const float* __restrict__ rope, int rope_rows,
+    CT* __restrict__ dqkv, int ldq, int T, int L, int H, int D, int BL, float kscale) {
+  const int sh = blockIdx.y, seq = sh / H, head = sh % H;
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= T) return;
+  const size_t plane = (size_t)BL * H * T * kDP;
+  const CT* Qg = qkv + (size_t)sh * T * kDP;
+  const CT* Kg = Qg + plane;
+  const CT* Vg = Qg + 2 * plane;
+  const CT* dOg = dop + (size_t)sh * T * kDP;
+  const float kb = kbias[(size_t)seq * T + k];
+  float kv[kDP], vv[kDP], dk[kDP], dv[kDP];
+#pragma unroll
+  for (int d = 0; d < kDP; ++d) {
+    kv[d] = d < D ? (float)Kg[(size_t)k * kDP + d] : 0.f;
+    vv[d] = d < D ? (float)Vg[(size_t)k * kDP + d] : 0.f;
+    dk[d] = dv[d] = 0.f;
+  }
+  if (kb != -INFINITY) {
+    for (int q = 0; q < T; ++q) {
+      float s = kb, dp = 0.f;
+#pragma unroll
+      for (int d = 0; d < kDP; ++d) {
+        if (d < D) {
+          s += (float)Qg[(size_t)q * kDP + d] * kv[d];
+          dp += (float)dOg[(size_t)q * kDP + d] * vv[d];
+        }
+      }
+      const float p = exp2f(s - lse[(size_t)sh * T + q]);
+      const float ds = p * (dp - delta[(size_t)sh * T + q]);
+#pragma unroll
+      for (int d = 0; d < kDP; ++d) {
+        if (d < D) {
+          dk[d] += ds * (float)Qg[(size_t)q * kDP + d];
+          dv[d] += p * (float)dOg[(size_t)q * kDP + d];
+        }
+      }
+    }
+  }
+  const int b = seq / L, l = seq % L, half = D >> 1, C = H * D;
+  const size_t tok = ((size_t)b * T + k) * L + l;
+  CT* ok = dqkv + tok * ldq + C + head * D;
+  CT* ov = dqkv + tok * ldq + 2 * C + head * D;
+  for (int d = 0; d < D; d += 2) {
+    float a = dk[d] * kscale, c = dk[d + 1] * kscale;
+    if (rope) rope_inv(a, c, rope, rope_rows, half, k, d >> 1);
+    ok[d] = (CT)a;
+    ok[d + 1] = (CT)c;
+    ov[d] = (CT)dv[d];
+    ov[d + 1] = (CT)dv[d + 1];
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// bf16 MFMA kernels.  LDS images are [row][32] bf16 (64-B rows) with 16-B chunk c of row r at
+// chunk c ^ ((r >> 3) & 3) (the forward's K image): row reads (ds_read_b128, MFMA A operand
+// rows) and transposed reads (ds_read_b64_tr_b16: lane 4q+p of each 16-lane group supplies
+// row q, columns 4p..4p+3 of its block) address the same image.
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+
+__device__ __forceinline__ int img_off(int row, int col) {  // element offset of (row, col)
+  return row * kDP + ((((col >> 3) ^ (row >> 3)) & 3) << 3) + (col & 7);
+}
+
+// A operand rows of a 32-row MFMA tile: lane holds row `row`, d = 16*s2 + 8*h + j
+__device__ __forceinline__ bf16x8 img_row(const bf16_t* img, int row, int s2, int h) {
+  return *reinterpret_cast<const bf16x8*>(img + img_off(row, 16 * s2 + 8 * h));
+}
+
+// A operand X^T of a 32 x 32 tile whose reduction runs over image rows base..base+31 in the
+// accumulator-as-operand order of k-step s2: lane (h, i = lane & 31) receives X[row(j)][i] with
+// row(j) = base + 16 s2 + 8 (j >> 2) + 4 h + (j & 3)  (attention.hip ta_subchunk's V^T read).
+__device__ __forceinline__ bf16x8 img_tr(const bf16_t* img, int base, int s2, int lane) {
+  const int h = lane >> 5, gi = lane & 15;
+  const int col = 16 * ((lane >> 4) & 1) + 4 * (gi & 3), row = base + 16 * s2 + 4 * h + (gi >> 2);
+  const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(img + img_off(row, col)));
+  const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(img + img_off(row + 8, col)));
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    r[j] = lo[j];
+    r[4 + j] = hi[j];
+  }
+  return r;
+}
+
+// B operand of one 32-row tile in registers: lane holds X[row r][16 s2 + 8 h + j] of a plane
+__device__ __forceinline__ void plane_frag(const bf16_t* g, int row, bool ok, int h, bf16x8 (&f)[2]) {
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2)
+    f[s2] = ok ? *reinterpret_cast<const bf16x8*>(g + (size_t)row * kDP + 16 * s2 + 8 * h) : zero8<bf16_t>();
+}
+
+// XCD-aware bijective remap of a 1-D grid of nwg blocks (attention.hip)
+__device__ __forceinline__ int xcd_remap(int nwg) {
+  const int xcd = blockIdx.x & 7, loc = blockIdx.x >> 3, qq = nwg >> 3, r8 = nwg & 7;
+  return (xcd < r8 ? xcd * (qq + 1) : r8 * (qq + 1) + (xcd - r8) * qq) + loc;
+}
+
+// dQ: 8 waves x 32 queries per block, keys through LDS in 128-key chunks (register-staged
+// double buffer, one barrier per chunk).
+constexpr int kBW = 8, kBKC = 128;
+
+__global__ __launch_bounds__(kBW * 64) void attn_bwd_dq_bf16_kernel(
+    const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dop, const float* __restrict__ lse,
+    const float* __restrict__ delta, const float* __restrict__ kbias, const float* __restrict__ kvb,
+    const float* __restrict__ rope, int rope_rows, bf16_t* __restrict__ dqkv, int ldq, float* __restrict__ bpart,
+    int T, int L, int H, int D, int BL, float qscale, float kscale) {
+  constexpr int KC = kBKC, NTH = kBW * 64;
+  static_assert(KC * kDP / 8 == NTH, "one 16-B piece of K and of V per thread per chunk");
+  __shared__ __attribute__((aligned(16))) bf16_t Ks[2][KC * kDP];
+  __shared__ __attribute__((aligned(16))) bf16_t Vs[2][KC * kDP];
+  __shared__ float kbs[2][KC];
+  __shared__ int kflag[2][KC / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
+  const int nqb = (T + kBW * 32 - 1) / (kBW * 32), nwg = nqb * H * BL;
+  const int wg = xcd_remap(nwg);
+  const int qb = wg % nqb, head = (wg / nqb) % H, seq = wg / (nqb * H);
+  const int sh = seq * H + head;
+  const int q = qb * (kBW * 32) + wave * 32 + r;
+  const bool live = q < T;
+  const size_t plane = (size_t)BL * H * T * kDP;
+  const bf16_t* Qg = qkv + (size_t)sh * T * kDP;
+  const bf16_t* Kg = Qg + plane;
+  const bf16_t* Vg = Qg + 2 * plane;
+  const float* kb = kbias + (size_t)seq * T;
+  bf16x8 qf[2], df[2];
+  plane_frag(Qg, q, live, h, qf);
+  plane_frag(dop + (size_t)sh * T * kDP, q, live, h, df);
+  const float l2 = live ? lse[(size_t)sh * T + q] : INFINITY;
+  const float dl = live ? delta[(size_t)sh * T + q] : 0.f;
+
+  // bias key (never masked): s_b = q.bk, dp_b = dO.bv
+  const float* bk = kvb + head * 2 * kDP;
+  const float* bv = bk + kDP;
+  float sb = 0.f, dpb = 0.f;
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int d = 16 * s2 + 8 * h + j;
+      sb += (float)qf[s2][j] * bk[d];
+      dpb += (float)df[s2][j] * (d < D ? bv[d] : 0.f);
+    }
+  sb += __shfl_xor(sb, 32, 64);
+  dpb += __shfl_xor(dpb, 32, 64);
+  const float pb = live ? __builtin_amdgcn_exp2f(sb - l2) : 0.f;
+  const float dsb = pb * (dpb - dl);
+  f32x16 o;  // dQ^T: row d = (i&3) + 8(i>>2) + 4h, column = query r
+#pragma unroll
+  for (int i = 0; i < 16; ++i) o[i] = dsb * bk[(i & 3) + 8 * (i >> 2) + 4 * h];
+  {  // bias_k / bias_v gradient partials of this wave's 32 queries
+    float gk[16], gv[16];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        gk[8 * s2 + j] = dsb * (float)qf[s2][j] * kscale;
+        gv[8 * s2 + j] = pb * (float)df[s2][j];
+      }
+#pragma unroll
+    for (int off = 1; off < 32; off <<= 1)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        gk[i] += __shfl_xor(gk[i], off, 64);
+        gv[i] += __shfl_xor(gv[i], off, 64);
+      }
+    if (r == 0) {
+      const size_t slot = ((size_t)seq * nqb + qb) * kBW + wave;
+      float* dst = bpart + ((size_t)head * BL * nqb * kBW + slot) * 2 * kDP;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          dst[16 * s2 + 8 * h + j] = gk[8 * s2 + j];
+          dst[kDP + 16 * s2 + 8 * h + j] = gv[8 * s2 + j];
+        }
+    }
+  }
+
+  const int srow = tid >> 2, spc = tid & 3;
+  u32x4 kreg, vreg;
+  float kbreg = 0.f;
+  auto gload = [&](int c) {
+    const int key = c * KC + srow;
+    kreg = vreg = u32x4{0u, 0u, 0u, 0u};
+    if (key < T) {
+      kreg = *reinterpret_cast<const u32x4*>(Kg + (size_t)key * kDP + spc * 8);
+      vreg = *reinterpret_cast<const u32x4*>(Vg + (size_t)key * kDP + spc * 8);
+    }
+    if (tid < KC) {
+      const int kk = c * KC + tid;
+      kbreg = (kk < T) ? kb[kk] : -INFINITY;
+    }
+  };
+  auto lstore = [&](int buf) {
+    *reinterpret_cast<u32x4*>(&Ks[buf][img_off(srow, spc * 8)]) = kreg;
+    *reinterpret_cast<u32x4*>(&Vs[buf][img_off(srow, spc * 8)]) = vreg;
+    if (tid < KC) {
+      kbs[buf][tid] = kbreg;
+      const bool any = __any(kbreg != 0.f);
+      if (lane == 0) kflag[buf][wave] = any ? 1 : 0;
+    }
+  };
+  const int nchunks = (T + KC - 1) / KC;
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  for (int c = 0; c < nchunks; ++c) {
+    const int cur = c & 1;
+    if (c + 1 < nchunks) gload(c + 1);
+    int mflag = 0;
+#pragma unroll
+    for (int f = 0; f < KC / 64; ++f) mflag |= kflag[cur][f];
+#pragma unroll
+    for (int sub = 0; sub < KC / 64; ++sub) {
+      const bf16_t* Kc = Ks[cur] + sub * 64 * kDP;
+      const bf16_t* Vc = Vs[cur] + sub * 64 * kDP;
+      const float* kbsub = kbs[cur] + sub * 64;
+      f32x16 sacc[2], pacc[2];
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sacc[kt][i] = pacc[kt][i] = 0.f;
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          sacc[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(img_row(Kc, kt * 32 + r, s2, h), qf[s2], sacc[kt], 0, 0, 0);
+          pacc[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(img_row(Vc, kt * 32 + r, s2, h), df[s2], pacc[kt], 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          float s = sacc[kt][i] - l2;
+          if (mflag) s += kbsub[kt * 32 + (i & 3) + 8 * (i >> 2) + 4 * h];
+          sacc[kt][i] = __builtin_amdgcn_exp2f(s) * (pacc[kt][i] - dl);  // dS^T
+        }
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          bf16x8 dsf;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) dsf[j] = (bf16_t)sacc[kt][8 * s2 + j];
+          o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(img_tr(Kc, kt * 32, s2, lane), dsf, o, 0, 0, 0);
+        }
+    }
+    if (c + 1 < nchunks) lstore(cur ^ 1);
+    __syncthreads();
+  }
+  if (live) {
+    const int b = seq / L, l = seq % L, half = D >> 1;
+    const size_t tok = ((size_t)b * T + q) * L + l;
+    bf16_t* out = dqkv + tok * ldq + head * D;
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const int d0 = 8 * g4 + 4 * h;
+      if (d0 < D) {
+        float a0 = o[4 * g4] * qscale, a1 = o[4 * g4 + 1] * qscale;
+        float a2 = o[4 * g4 + 2] * qscale, a3 = o[4 * g4 + 3] * qscale;
+        if (rope) {
+          rope_inv(a0, a1, rope, rope_rows, half, q, d0 >> 1);
+          rope_inv(a2, a3, rope, rope_rows, half, q, (d0 >> 1) + 1);
+        }
+        st4<bf16_t>(out + d0, a0, a1, a2, a3);
+      }
+    }
+  }
+}
+
+// dK / dV: 8 waves x 32 keys per block, queries (Q, dO images + lse, delta) through LDS in
+// 128-query chunks.
+__global__ __launch_bounds__(kBW * 64) void attn_bwd_dkdv_bf16_kernel(
+    const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dop, const float* __restrict__ lse,
+    const float* __restrict__ delta, const float* __restrict__ kbias, const float* __restrict__ rope, int rope_rows,
+    bf16_t* __restrict__ dqkv, int ldq, int T, int L, int H, int D, int BL, float kscale) {
+  constexpr int QC = kBKC, NTH = kBW * 64;
+  static_assert(QC * kDP / 8 == NTH, "one 16-B piece of Q and of dO per thread per chunk");
+  __shared__ __attribute__((aligned(16))) bf16_t Qs[2][QC * kDP];
+  __shared__ __attribute__((aligned(16))) bf16_t Ds[2][QC * kDP];
+  __shared__ __attribute__((aligned(16))) float ls[2][QC];
+  __shared__ __attribute__((aligned(16))) float dls[2][QC];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
+  const int nkb = (T + kBW * 32 - 1) / (kBW * 32), nwg = nkb * H * BL;
+  const int wg = xcd_remap(nwg);
+  const int kbk = wg % nkb, head = (wg / nkb) % H, seq = wg / (nkb * H);
+  const int sh = seq * H + head;
+  const int key = kbk * (kBW * 32) + wave * 32 + r;
+  const bool live = key < T;
+  const size_t plane = (size_t)BL * H * T * kDP;
+  const bf16_t* Qg = qkv + (size_t)sh * T * kDP;
+  const bf16_t* dOg = dop + (size_t)sh * T * kDP;
+  bf16x8 kf[2], vf[2];
+  plane_frag(Qg + plane, key, live, h, kf);
+  plane_frag(Qg + 2 * plane, key, live, h, vf);
+  const float kbl = live ? kbias[(size_t)seq * T + key] : -INFINITY;
+  f32x16 dk, dv;  // dK^T / dV^T: row d = (i&3) + 8(i>>2) + 4h, column = key r
+#pragma unroll
+  for (int i = 0; i < 16; ++i) dk[i] = dv[i] = 0.f;
+
+  const int srow = tid >> 2, spc = tid & 3;
+  u32x4 qreg, dreg;
+  float lreg = 0.f, dlreg = 0.f;
+  auto gload = [&](int c) {
+    const int qq = c * QC + srow;
+    qreg = dreg = u32x4{0u, 0u, 0u, 0u};
+    if (qq < T) {
+      qreg = *reinterpret_cast<const u32x4*>(Qg + (size_t)qq * kDP + spc * 8);
+      dreg = *reinterpret_cast<const u32x4*>(dOg + (size_t)qq * kDP + spc * 8);
+    }
+    if (tid < QC) {
+      const int q2 = c * QC + tid;
+      lreg = (q2 < T) ? lse[(size_t)sh * T + q2] : INFINITY;
+      dlreg = (q2 < T) ? delta[(size_t)sh * T + q2] : 0.f;
+    }
+  };
+  auto lstore = [&](int buf) {
+    *reinterpret_cast<u32x4*>(&Qs[buf][img_off(srow, spc * 8)]) = qreg;
+    *reinterpret_cast<u32x4*>(&Ds[buf][img_off(srow, spc * 8)]) = dreg;
+    if (tid < QC) {
+      ls[buf][tid] = lreg;
+      dls[buf][tid] = dlreg;
+    }
+  };
+  const int nchunks = (T + QC - 1) / QC;
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  for (int c = 0; c < nchunks; ++c) {
+    const int cur = c & 1;
+    if (c + 1 < nchunks) gload(c + 1);
+#pragma unroll
+    for (int sub = 0; sub < QC / 64; ++sub) {
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) {
+        const int base = sub * 64 + qt * 32;
+        f32x16 sacc, pacc;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sacc[i] = pacc[i] = 0.f;
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(img_row(Qs[cur], base + r, s2, h), kf[s2], sacc, 0, 0, 0);
+          pacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(img_row(Ds[cur], base + r, s2, h), vf[s2], pacc, 0, 0, 0);
+        }
+        // S[q][key] with q = base + (i&3) + 8(i>>2) + 4h: its lse / delta, 4 at a time
+        float pr[16], dsr[16];
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const float4 l4 = *reinterpret_cast<const float4*>(&ls[cur][base + 8 * g4 + 4 * h]);
+          const float4 d4 = *reinterpret_cast<const float4*>(&dls[cur][base + 8 * g4 + 4 * h]);
+          const float lv[4] = {l4.x, l4.y, l4.z, l4.w}, dv4[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int i = 4 * g4 + e;
+            const float p = __builtin_amdgcn_exp2f(sacc[i] + kbl - lv[e]);
+            pr[i] = p;
+            dsr[i] = p * (pacc[i] - dv4[e]);
+          }
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          bf16x8 pf, dsf;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            pf[j] = (bf16_t)pr[8 * s2 + j];
+            dsf[j] = (bf16_t)dsr[8 * s2 + j];
+          }
+          dv = __builtin_amdgcn_mfma_f32_32x32x16_bf16(img_tr(Ds[cur], base, s2, lane), pf, dv, 0, 0, 0);
+          dk = __builtin_amdgcn_mfma_f32_32x32x16_bf16(img_tr(Qs[cur], base, s2, lane), dsf, dk, 0, 0, 0);
+        }
+      }
+    }
+    if (c + 1 < nchunks) lstore(cur ^ 1);
+    __syncthreads();
+  }
+  if (live) {
+    const int b = seq / L, l = seq % L, half = D >> 1, C = H * D;
+    const size_t tok = ((size_t)b * T + key) * L + l;
+    bf16_t* ok = dqkv + tok * ldq + C + head * D;
+    bf16_t* ov = dqkv + tok * ldq + 2 * C + head * D;
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const int d0 = 8 * g4 + 4 * h;
+      if (d0 < D) {
+        float a0 = dk[4 * g4] * kscale, a1 = dk[4 * g4 + 1] * kscale;
+        float a2 = dk[4 * g4 + 2] * kscale, a3 = dk[4 * g4 + 3] * kscale;
+        if (rope) {
+          rope_inv(a0, a1, rope, rope_rows, half, key, d0 >> 1);
+          rope_inv(a2, a3, rope, rope_rows, half, key, (d0 >> 1) + 1);
+        }
+        st4<bf16_t>(ok + d0, a0, a1, a2, a3);
+        st4<bf16_t>(ov + d0, dv[4 * g4], dv[4 * g4 + 1], dv[4 * g4 + 2], dv[4 * g4 + 3]);
+      }
+    }
+  }
+}
+
+int attn_bwd_parts(int dtype, int B, int T, int L) {  // bias-gradient partial slots per head
+  if (dtype == MDG_BF16) return B * L * ((T + kBW * 32 - 1) / (kBW * 32)) * kBW;
+  return B * L * ((T + 255) / 256);
+}
+
+hipError_t attn_temporal_bwd_launch(int dtype, int B, int T, int L, int H, int D, const void* qkv_t,
+                                    const float* kbias, const float* kvb, const void* o, const void* dout,
+                                    const float* lse, const float* rope, int rope_rows, void* dop, float* delta,
+                                    void* dqkv, int ldq, float* bpart, float qscale, float kscale, int generic,
+                                    hipStream_t s) {
+  const int BL = B * L;
+  const size_t nth = (size_t)B * T * L * H;
+  dim3 pgrid((unsigned)((nth + 255) / 256));
+  if (dtype == MDG_BF16) {
+    hipLaunchKernelGGL(attn_bwd_prep_kernel<bf16_t>, pgrid, dim3(256), 0, s, B, T, L, H, D, (const bf16_t*)o,
+                       (const bf16_t*)dout, (bf16_t*)dop, delta);
+  } else {
+    hipLaunchKernelGGL(attn_bwd_prep_kernel<float>, pgrid, dim3(256), 0, s, B, T, L, H, D, (const float*)o,
+                       (const float*)dout, (float*)dop, delta);
+  }
+  if (hipError_t e = hipGetLastError()) return e;
+  if (dtype == MDG_BF16 && !generic) {
+    const int nblk = (T + kBW * 32 - 1) / (kBW * 32) * H * BL;
+    hipLaunchKernelGGL(attn_bwd_dq_bf16_kernel, dim3(nblk), dim3(kBW * 64), 0, s, (const bf16_t*)qkv_t,
+                       (const bf16_t*)dop, lse, delta, kbias, kvb, rope, rope_rows, (bf16_t*)dqkv, ldq, bpart, T, L,
+                       H, D, BL, qscale, kscale);
+    if (hipError_t e = hipGetLastError()) return e;
+    hipLaunchKernelGGL(attn_bwd_dkdv_bf16_kernel, dim3(nblk), dim3(kBW * 64), 0, s, (const bf16_t*)qkv_t,
+                       (const bf16_t*)dop, lse, delta, kbias, rope, rope_rows, (bf16_t*)dqkv, ldq, T, L, H, D, BL,
+                       kscale);
+    return hipGetLastError();
+  }
+  dim3 grid((T + 255) / 256, BL * H);
+#define MDG_GEN(CTT)                                                                                               \
+  hipLaunchKernelGGL(attn_bwd_dq_generic_kernel<CTT>, grid, dim3(256), 0, s, (const CTT*)qkv_t, (const CTT*)dop,    \
+                     lse, delta, kbias, kvb, rope, rope_rows, (CTT*)dqkv, ldq, bpart, T, L, H, D, BL, qscale, kscale); \
+  hipLaunchKernelGGL(attn_bwd_dkdv_generic_kernel<CTT>, grid, dim3(256), 0, s, (const CTT*)qkv_t, (const CTT*)dop,  \
+                     lse, delta, kbias, rope, rope_rows, (CTT*)dqkv, ldq, T, L, H, D, BL, kscale)
+  if (dtype == MDG_BF16) {
+    MDG_GEN(bf16_t);
+  } else {
+    MDG_GEN(float);
+  }
+#undef MDG_GEN
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+// Spatial attention backward.  q|k|v [token][3][H][D] as the forward's QKV (spatial layout)
+// GEMM wrote them (q scaled by D^-1/2, q and k RoPE-rotated at position l, natural units).
+template <int I>
+__device__ __forceinline__ float qb(float x) {  // broadcast lane I of every quad
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), I | (I << 2) | (I << 4) | (I << 6), 0xF, 0xF, true));
+}
+__device__ __forceinline__ float qbi(float x, int i) {
+  switch (i) {
+    case 0: return qb<0>(x);
+    case 1: return qb<1>(x);
+    case 2: return qb<2>(x);
+    default: return qb<3>(x);
+  }
+}
+
+
+template <typename CT, int DM>
+__global__ __launch_bounds__(256) void attn_spatial_bwd_quad_kernel(const CT* __restrict__ qkv,
+                                                                    const float* __restrict__ kvb,
+                                                                    const float* __restrict__ mask,
+                                                                    const CT* __restrict__ dout,
+                                                                    const float* __restrict__ rope, int rope_rows,
+                                                                    CT* __restrict__ dqkv, float* __restrict__ bpart,
+                                                                    int nf, int H, int D, float qscale) {
+  __shared__ float red[256][2 * DM + 1];
+  const int head = blockIdx.y;
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  const bool live = idx < nf * 4;
+  const int j = idx & 3, f = (live ? idx : nf * 4 - 1) >> 2, tok = f * 4 + j;
+  const int C = H * D;
+  const CT* base = qkv + (size_t)tok * 3 * C + head * D;
+  float q[DM], k[DM], v[DM], g[DM];
+#pragma unroll
+  for (int d = 0; d < DM; d += 4) {
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a, c = a, e = a;
+    if (d < D) {
+      a = ld4f<CT>(base + d);
+      b = ld4f<CT>(base + C + d);
+      c = ld4f<CT>(base + 2 * C + d);
+      e = ld4f<CT>(dout + (size_t)tok * C + head * D + d);
+    }
+    q[d] = a.x; q[d + 1] = a.y; q[d + 2] = a.z; q[d + 3] = a.w;
+    k[d] = b.x; k[d + 1] = b.y; k[d + 2] = b.z; k[d + 3] = b.w;
+    v[d] = c.x; v[d + 1] = c.y; v[d + 2] = c.z; v[d + 3] = c.w;
+    g[d] = e.x; g[d + 1] = e.y; g[d + 2] = e.z; g[d + 3] = e.w;
+  }
+  const float kvalid = (!mask || mask[tok] != 0.f) ? 1.f : 0.f;
+  const float* bk = kvb + head * 2 * kDP;
+  const float* bv = bk + kDP;
+  float sb = 0.f, dpb = 0.f;
+#pragma unroll
+  for (int d = 0; d < DM; ++d) {
+    sb += q[d] * bk[d];
+    dpb += g[d] * (d < D ? bv[d] : 0.f);
+  }
+  float sc[4], dp[4], valid[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    float s = 0.f, t = 0.f;
+#pragma unroll
+    for (int d = 0; d < DM; ++d) {
+      s += q[d] * qbi(k[d], i);
+      t += g[d] * qbi(v[d], i);
+    }
+    sc[i] = s;
+    dp[i] = t;
+    valid[i] = qbi(kvalid, i);
+  }
+  float m = sb;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if (valid[i] != 0.f) m = fmaxf(m, sc[i]);
+  float pb = expf(sb - m), lsum = pb, p[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    p[i] = (valid[i] != 0.f) ? expf(sc[i] - m) : 0.f;
+    lsum += p[i];
+  }
+  const float inv = 1.0f / lsum;
+  pb *= inv;
+  float dl = pb * dpb;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    p[i] *= inv;
+    dl += p[i] * dp[i];
+  }
+  const float dsb = pb * (dpb - dl);
+  float ds[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) ds[i] = p[i] * (dp[i] - dl);
+  // dq = ds_b bk + sum_i ds_i k_i;  as key j: dk = sum_J ds_J[j] q_J, dv = sum_J p_J[j] dO_J
+  float dq[DM], dk[DM], dv[DM];
+#pragma unroll
+  for (int d = 0; d < DM; ++d) {
+    dq[d] = dsb * bk[d];
+    dk[d] = 0.f;
+    dv[d] = 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int d = 0; d < DM; ++d) dq[d] += ds[i] * qbi(k[d], i);
+    // lane J = i's ds / p for key j (this lane's residue)
+    float dsJ = 0.f, pJ = 0.f;
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const float a = qbi(ds[jj], i), b = qbi(p[jj], i);
+      if (jj == j) {
+        dsJ = a;
+        pJ = b;
+      }
+    }
+#pragma unroll
+    for (int d = 0; d < DM; ++d) {
+      dk[d] += dsJ * qbi(q[d], i);
+      dv[d] += pJ * qbi(g[d], i);
+    }
+  }
+#pragma unroll
+  for (int d = 0; d < DM; ++d) {
+    red[threadIdx.x][d] = live ? dsb * q[d] : 0.f;
+    red[threadIdx.x][DM + d] = live ? pb * g[d] : 0.f;
+  }
+  if (live) {
+    CT* oq = dqkv + (size_t)tok * 3 * C + head * D;
+    const int half = D >> 1;
+#pragma unroll
+    for (int d = 0; d < DM; d += 2) {
+      if (d < D) {
+        float a = dq[d] * qscale, b = dq[d + 1] * qscale, c = dk[d], e = dk[d + 1];
+        if (rope) {
+          rope_inv(a, b, rope, rope_rows, half, j, d >> 1);
+          rope_inv(c, e, rope, rope_rows, half, j, d >> 1);
+        }
+        oq[d] = (CT)a;
+        oq[d + 1] = (CT)b;
+        oq[C + d] = (CT)c;
+        oq[C + d + 1] = (CT)e;
+        oq[2 * C + d] = (CT)dv[d];
+        oq[2 * C + d + 1] = (CT)dv[d + 1];
+      }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 2 * DM) {
+    float s = 0.f;
+    for (int i = 0; i < 256; ++i) s += red[i][threadIdx.x];
+    const int which = threadIdx.x / DM, d = threadIdx.x % DM;
+    if (d < kDP) bpart[((size_t)head * gridDim.x + blockIdx.x) * 2 * kDP + which * kDP + d] = s;
+  }
+}
+
+// Any L (< the MFMA route's 16), any D <= 31: one thread per (frame, head).
+template <typename CT>
+__global__ __launch_bounds__(128) void attn_spatial_bwd_generic_kernel(
+    const CT* __restrict__ qkv, const float* __restrict__ kvb, const float* __restrict__ mask,
+    const CT* __restrict__ dout, const float* __restrict__ rope, int rope_rows, CT* __restrict__ dqkv,
+    float* __restrict__ bpart, int nf, int L, int H, int D, float qscale) {
+  constexpr int LM = 16;
+  __shared__ float red[128][2 * kDP + 1];
+  const int head = blockIdx.y;
+  const int f = blockIdx.x * 128 + threadIdx.x;
+  const bool live = f < nf;
+  const int C = H * D;
+  const float* bk = kvb + head * 2 * kDP;
+  const float* bv = bk + kDP;
+  float P[LM][LM + 1], DS[LM][LM + 1];
+  float gbk[kDP], gbv[kDP];
+#pragma unroll
+  for (int d = 0; d < kDP; ++d) gbk[d] = gbv[d] = 0.f;
+  if (live) {
+    auto at = [&](int tk, int which, int d) -> float {
+      return (float)qkv[((size_t)(f * L + tk) * 3 + which) * C + head * D + d];
+    };
+    for (int jq = 0; jq < L; ++jq) {
+      const CT* gq = dout + (size_t)(f * L + jq) * C + head * D;
+      float sb = 0.f, dpb = 0.f;
+      for (int d = 0; d < D; ++d) {
+        sb += at(jq, 0, d) * bk[d];
+        dpb += (float)gq[d] * bv[d];
+      }
+      float s[LM], dp[LM], m = sb;
+      for (int i = 0; i < L; ++i) {
+        float a = 0.f, b = 0.f;
+        for (int d = 0; d < D; ++d) {
+          a += at(jq, 0, d) * at(i, 1, d);
+          b += (float)gq[d] * at(i, 2, d);
+        }
+        s[i] = a;
+        dp[i] = b;
+        if (!mask || mask[f * L + i] != 0.f) m = fmaxf(m, a);
+      }
+      float pb = expf(sb - m), lsum = pb;
+      for (int i = 0; i < L; ++i) {
+        P[jq][i] = (!mask || mask[f * L + i] != 0.f) ? expf(s[i] - m) : 0.f;
+        lsum += P[jq][i];
+      }
+      pb /= lsum;
+      float dl = pb * dpb;
+      for (int i = 0; i < L; ++i) {
+        P[jq][i] /= lsum;
+        dl += P[jq][i] * dp[i];
+      }
+      const float dsb = pb * (dpb - dl);
+      for (int i = 0; i < L; ++i) DS[jq][i] = P[jq][i] * (dp[i] - dl);
+      for (int d = 0; d < D; ++d) {
+        gbk[d] += dsb * at(jq, 0, d);
+        gbv[d] += pb * (float)gq[d];
+      }
+      CT* oq = dqkv + (size_t)(f * L + jq) * 3 * C + head * D;
+      for (int d = 0; d < D; d += 2) {
+        float a = dsb * bk[d], b = dsb * bk[d + 1];
+        for (int i = 0; i < L; ++i) {
+          a += DS[jq][i] * at(i, 1, d);
+          b += DS[jq][i] * at(i, 1, d + 1);
+        }
+        a *= qscale;
+        b *= qscale;
+        if (rope) rope_inv(a, b, rope, rope_rows, D >> 1, jq, d >> 1);
+        oq[d] = (CT)a;
+        oq[d + 1] = (CT)b;
+      }
+    }
+    for (int i = 0; i < L; ++i) {
+      CT* ok = dqkv + (size_t)(f * L + i) * 3 * C + C + head * D;
+      for (int d = 0; d < D; d += 2) {
+        float a = 0.f, b = 0.f, c = 0.f, e = 0.f;
+        for (int jq = 0; jq < L; ++jq) {
+          const CT* gq = dout + (size_t)(f * L + jq) * C + head * D;
+          a += DS[jq][i] * at(jq, 0, d);
+          b += DS[jq][i] * at(jq, 0, d + 1);
+          c += P[jq][i] * (float)gq[d];
+          e += P[jq][i] * (float)gq[d + 1];
+        }
+        if (rope) rope_inv(a, b, rope, rope_rows, D >> 1, i, d >> 1);
+        ok[d] = (CT)a;
+        ok[d + 1] = (CT)b;
+        ok[C + d] = (CT)c;
+        ok[C + d + 1] = (CT)e;
+      }
+    }
+  }
+#pragma unroll
+  for (int d = 0; d < kDP; ++d) {
+    red[threadIdx.x][d] = gbk[d];
+    red[threadIdx.x][kDP + d] = gbv[d];
+  }
+  __syncthreads();
+  if (threadIdx.x < 2 * kDP) {
+    float s = 0.f;
+    for (int i = 0; i < 128; ++i) s += red[i][threadIdx.x];
+    bpart[((size_t)head * gridDim.x + blockIdx.x) * 2 * kDP + threadIdx.x] = s;
+  }
+}
+
+int attn_spatial_bwd_parts(int nf, int L, int D) {
+  if (L == 4 && D % 8 == 0) return (nf * 4 + 255) / 256;
+  return (nf + 127) / 128;
+}
+
+hipError_t attn_spatial_bwd_launch(int dtype, int nf, int L, int H, int D, const void* qkv, const float* kvb,
+                                   const float* mask, const void* dout, const float* rope, int rope_rows, void* dqkv,
+                                   float* bpart, float qscale, hipStream_t s) {
+  if (L == 4 && D % 8 == 0) {
+    dim3 grid((unsigned)((nf * 4 + 255) / 256), H);
+#define MDG_SQ(CTT, DM)                                                                                           \
+  hipLaunchKernelGGL((attn_spatial_bwd_quad_kernel<CTT, DM>), grid, dim3(256), 0, s, (const CTT*)qkv, kvb, mask, \
+                     (const CTT*)dout, rope, rope_rows, (CTT*)dqkv, bpart, nf, H, D, qscale)
+    if (dtype == MDG_BF16) {
+      if (D <= 16) MDG_SQ(bf16_t, 16); else if (D <= 24) MDG_SQ(bf16_t, 24); else MDG_SQ(bf16_t, 32);
+    } else {
+      if (D <= 16) MDG_SQ(float, 16); else if (D <= 24) MDG_SQ(float, 24); else MDG_SQ(float, 32);
+    }
+#undef MDG_SQ
+    return hipGetLastError();
+  }
+  dim3 grid((unsigned)((nf + 127) / 128), H);
+  if (dtype == MDG_BF16)
+    hipLaunchKernelGGL(attn_spatial_bwd_generic_kernel<bf16_t>, grid, dim3(128), 0, s, (const bf16_t*)qkv, kvb, mask,
+                       (const bf16_t*)dout, rope, rope_rows, (bf16_t*)dqkv, bpart, nf, L, H, D, qscale);
+  else
+    hipLaunchKernelGGL(attn_spatial_bwd_generic_kernel<float>, grid, dim3(128), 0, s, (const float*)qkv, kvb, mask,
+                       (const float*)dout, rope, rope_rows, (float*)dqkv, bpart, nf, L, H, D, qscale);
+  return hipGetLastError();
+}
+
+}  // namespace mdg

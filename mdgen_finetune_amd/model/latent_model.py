@@ -136,6 +136,7 @@ class LatentMDGenModel(nn.Module):
             self.register_buffer("time_embed", torch.zeros(1, args.num_frames, C))
         self.initialize_weights()
         self.backend = "hip"
+        self.train_backend = "hip"
         self._engine = None
 
     # ------------------------------------------------------------------ init (latent_model.py:134-177)
@@ -248,12 +249,40 @@ class LatentMDGenModel(nn.Module):
         c = self.embed_time(t)[:, None]
         if self.args.prepend_ipa:
             h = h + self.run_ipa(c[:, 0], mask[:, 0], start_frames, end_frames, aatype)[:, None]
+        hip_layers = self._use_hip_layers(h)
+        if hip_layers:
+            from ..train_hip import hip_layer_forward
+            hl = self._train_helper()
         for layer in self.layers:
-            if getattr(self.args, "grad_checkpointing", False) and self.training:
+            if hip_layers:  # block forward + backward in libmdgen_hip.so (train_hip.py)
+                h = hip_layer_forward(hl, layer, h, layer.adaLN_modulation(c[:, 0]), mask)
+            elif getattr(self.args, "grad_checkpointing", False) and self.training:
                 h = torch.utils.checkpoint.checkpoint(layer, h, c, mask, use_reentrant=False)
             else:
                 h = layer(h, c, mask)
         return self.emb_to_latent(h, c)
+
+    def _use_hip_layers(self, h):
+        """Differentiable calls on a ROCm device run the block stack through the HIP training
+        Function (train_backend 'hip', the default); dropout > 0 while training is not built
+        there and takes eager autograd."""
+        if self.backend != "hip" or getattr(self, "train_backend", "hip") != "hip" or not h.is_cuda:
+            return False
+        if not torch.is_grad_enabled():
+            return False
+        return not (self.training and float(getattr(self.args, "dropout", 0.0) or 0.0) > 0.0)
+
+    def _train_helper(self):
+        from ..train_hip import LayerHelper
+
+        dt = getattr(self, "hip_dtype", "bf16")
+        hl = getattr(self, "_hip_train", None)
+        if hl is None:
+            hl = LayerHelper(self, dt)
+            self._hip_train = hl
+        elif hl.dtype_name != dt:
+            hl.set_dtype(dt)
+        return hl
 
 
 def relative_tensor7(rots_a, trans_a, rots_b, trans_b):

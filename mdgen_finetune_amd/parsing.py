@@ -57,6 +57,10 @@ _EXTRA = [
     ("seed", _I, 137, "base RNG seed (rank r uses seed + r for its noise draws)"),
     ("bucket_cap_mb", _F, 32.0, "DDP gradient bucket size (all-reduce overlaps backward per bucket)"),
     ("model_dir", _S, None, "checkpoint directory (default workdir/<run_name>, the reference's MODEL_DIR)"),
+    ("train_backend", _S, "hip", "'hip': on a ROCm device every block's forward + backward runs in "
+                                 "libmdgen_hip.so (train_hip.py); 'torch': eager autograd"),
+    ("hip_dtype", _S, "bf16", "operand type of the HIP GEMM / attention kernels: 'bf16' (fp32 accumulate, "
+                              "the reference's matmul precision 'medium') or 'f32' (exact fp32)"),
 ]
 
 _REQUIRED = ("train_split", "val_split", "data_dir")

@@ -84,7 +84,12 @@ class Trainer:
         self.device = device or torch.device("cpu")
         torch.manual_seed(args.seed)  # identical initial weights on every rank
         self.wrapper = NewMDGenWrapper(args).to(self.device)
-        self.wrapper.model.backend = "torch"  # autograd path (HIP backward: DESIGN.md §7)
+        m = self.wrapper.model
+        if self.device.type == "cuda":  # block forward + backward on the HIP kernels (train_hip.py)
+            m.backend, m.train_backend = "hip", getattr(args, "train_backend", "hip")
+            m.hip_dtype = getattr(args, "hip_dtype", "bf16")
+        else:
+            m.backend = "torch"
         torch.manual_seed(args.seed + 1 + 1000 * rank)  # independent (t, x0) draws per rank
         self.model = self.wrapper.model
         if world > 1:

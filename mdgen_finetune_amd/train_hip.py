@@ -1,0 +1,337 @@
+"""HIP training path: a LatentMDGenLayer's forward AND backward on libmdgen_hip.so.
+
+The reference trains the block with eager PyTorch autograd (Transport.training_losses ->
+model(xt, t, **kw) -> loss.backward(): transport.py:137-222, wrapper.py:367-403; the block
+latent_model.py:456-493).  Here each block is one ``torch.autograd.Function``:
+
+forward   ``mdg_layer_fwd_train``: LN + adaLN modulate (with row statistics) -> q|k|v GEMM +
+          RoPE -> spatial / temporal attention (temporal with per-row log2-sum-exp2) -> out_proj
+          GEMM with the gated residual out of place (pre-gate output kept) -> ... -> fc1 GEMM
+          (pre-activation kept) -> fc2 gated residual.  Everything is saved on device for the
+          backward; nothing is recomputed by torch.
+backward  per sublayer, top down:
+            mdg_ln_gate_bwd     LN/modulate backward of sublayer k fused with the gated-residual
+                                backward of sublayer k-1 (dh, dy = dh * gate, adaLN and bias
+                                gradient partials);
+            mdg_gemm            input gradients dX = dY W through the HIP GEMM (Wt packed once per
+                                step); fc1's with the GELU-derivative epilogue (MDG_ACT_DGELU);
+            mdg_attn_*_bwd      flash-style attention backward (P recomputed from the saved lse),
+                                RoPE / q-scale undone in the epilogue, bias_k / bias_v partials;
+            torch.mm            the weight gradients dW = dY^T X (plain GEMMs, hipBLASLt) —
+                                the only library calls on the path.
+The adaLN modulation vectors enter as a [B, 9C] input of the Function, so the t-embedding /
+adaLN linears upstream stay ordinary autograd modules (x-independent, tiny).
+
+Parity: the f32 dtype (``model.hip_dtype = 'f32'``) runs exact-f32 MFMA / scalar kernels and
+matches eager autograd to ~1e-5 relative; bf16 (the default) rounds GEMM / attention operands
+to bf16 with fp32 accumulation — ``torch.set_float32_matmul_precision('medium')`` semantics, as
+the reference's train.py:13 requests.  tests/test_gpu_train.py states the tolerances.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+
+import torch
+
+from . import _lib
+
+_LN2 = math.log(2.0)
+
+
+def _mm_f32(a, b):
+    """a @ b with fp32 output (fp32 accumulate) for bf16 operands."""
+    if a.dtype == torch.float32:
+        return a @ b
+    try:
+        return torch.mm(a, b, out_dtype=torch.float32)
+    except (RuntimeError, TypeError):
+        return (a @ b).float()
+
+
+class LayerHelper:
+    """Per-model state of the HIP training path: ctypes library, RoPE tables per length, the
+    pair-interleave permutation, dtype."""
+
+    def __init__(self, model, dtype="bf16"):
+        self.model = model
+        self.lib = _lib.load()
+        a = model.args
+        self.C, self.H = a.embed_dim, a.mha_heads
+        self.D = self.C // self.H
+        self.F = 4 * self.C
+        self.rope = not a.no_rope
+        self.set_dtype(dtype)
+        self._tables = {}
+        self._perm = None
+
+    def set_dtype(self, dtype):
+        if dtype not in ("bf16", "f32"):
+            raise ValueError(f"hip_dtype must be 'bf16' or 'f32', got {dtype!r}")
+        self.dtype_name = dtype
+        self.mdg_dtype = _lib.MDG_BF16 if dtype == "bf16" else _lib.MDG_F32
+        self.ct = torch.bfloat16 if dtype == "bf16" else torch.float32
+
+    def perm(self, device):
+        if self._perm is None or self._perm.device != device:
+            D, half = self.D, self.D // 2
+            idx = torch.arange(D)
+            within = torch.where(idx % 2 == 0, idx // 2, idx // 2 + half)
+            self._perm = (torch.arange(self.H)[:, None] * D + within[None]).reshape(-1).to(device)
+        return self._perm
+
+    def table(self, n_rows, inv_freq):
+        """cos | sin [n_rows][D/2] (fair-esm: fp32 outer product on the CPU, then cos / sin)."""
+        key = (n_rows, inv_freq.device)
+        t = self._tables.get(key)
+        if t is None:
+            inv = inv_freq.detach().float().cpu()
+            freqs = torch.einsum("i,j->ij", torch.arange(n_rows).type_as(inv), inv)
+            t = torch.cat([freqs.cos().reshape(-1), freqs.sin().reshape(-1)]).to(inv_freq.device)
+            self._tables[key] = t
+        return t
+
+    def dims(self, B, T, L):
+        return _lib.MdgDims(B=B, T=T, L=L, C=self.C, H=self.H, D=self.D, F=self.F, latent=self.model.latent_dim,
+                            num_layers=self.model.args.num_layers, dtype=self.mdg_dtype)
+
+    # -------------------------------------------------------------- bias-key rotation
+    def _rot(self, S, n_rows, inv_freq, dev):
+        half = self.D // 2
+        tab = self.table(n_rows, inv_freq)
+        cos = tab[: n_rows * half].reshape(n_rows, half)[S]
+        sin = tab[n_rows * half:].reshape(n_rows, half)[S]
+        return torch.cat([cos, cos]), torch.cat([sin, sin])
+
+    def kvb(self, bias_k, bias_v, S, n_rows, inv_freq):
+        """[H][2][32] as the kernels read it (engine._kvb): bias_k RoPE-rotated at position S in
+        the pair-interleaved order, bias_v natural with 1.0 in pad column D."""
+        H, D, half = self.H, self.D, self.D // 2
+        kb = bias_k.detach().float().reshape(H, D)
+        if self.rope:
+            c2, s2 = self._rot(S, n_rows, inv_freq, kb.device)
+            kb = kb * c2 + torch.cat([-kb[:, half:], kb[:, :half]], -1) * s2
+            kb = kb.reshape(-1)[self.perm(kb.device)].reshape(H, D)
+        out = torch.zeros(H, 2, _lib.MDG_DP, device=kb.device)
+        out[:, 0, :D] = kb
+        out[:, 1, :D] = bias_v.detach().float().reshape(H, D)
+        out[:, 1, D] = 1.0
+        return out
+
+    def kvb_grad(self, g, S, n_rows, inv_freq):
+        """Map the kernels' [H][2][32] bias-key gradient (w.r.t. the rotated, interleaved rows)
+        back to d bias_k, d bias_v [1, 1, C] of the parameters."""
+        H, D, half = self.H, self.D, self.D // 2
+        gk = g[:, 0, :D].reshape(-1)
+        if self.rope:
+            nat = torch.empty_like(gk)
+            nat[self.perm(gk.device)] = gk
+            gk = nat.reshape(H, D)
+            c2, s2 = self._rot(S, n_rows, inv_freq, gk.device)
+            z = gk * s2
+            gk = gk * c2 + torch.cat([z[:, half:], -z[:, :half]], -1)  # transpose of rotate_half
+        gv = g[:, 1, :D]
+        return gk.reshape(1, 1, -1), gv.reshape(1, 1, -1)
+
+
+def _layer_params(layer):
+    out = []
+    for mha in (layer.mha_l.attn, layer.mha_t.attn):
+        out += [mha.q_proj.weight, mha.q_proj.bias, mha.k_proj.weight, mha.k_proj.bias, mha.v_proj.weight,
+                mha.v_proj.bias, mha.out_proj.weight, mha.out_proj.bias, mha.bias_k, mha.bias_v]
+    out += [layer.fc1.weight, layer.fc1.bias, layer.fc2.weight, layer.fc2.bias]
+    return out
+
+
+def hip_layer_forward(hl, layer, h, mods, mask):
+    """h [B,T,L,C] fp32, mods [B, 9C] (adaLN output), mask [B,T,L] -> layer(h) through the
+    HIP training Function."""
+    inv_freq = layer.mha_l.attn.rot_emb.inv_freq if hl.rope else None
+    return _HipLayerFn.apply(h, mods, mask, hl, inv_freq, *_layer_params(layer))
+
+
+class _HipLayerFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, h, mods, mask, hl, inv_freq, *params):
+        lib = hl.lib
+        B, T, L, C = h.shape
+        H, D, F, ct = hl.H, hl.D, hl.F, hl.ct
+        N, dev = B * T * L, h.device
+        s = _lib.stream_handle()
+        h = h.contiguous().float()
+        mods = mods.contiguous().float()
+        mask = mask.contiguous().float()
+        perm = hl.perm(dev) if hl.rope else None
+        P = {}
+        with torch.no_grad():
+            for i in range(2):
+                wq, bq, wk, bk, wv, bv, wo, bo, bias_k, bias_v = params[10 * i:10 * i + 10]
+                if perm is not None:
+                    wq, wk, bq, bk = wq[perm], wk[perm], bq[perm], bk[perm]
+                P[f"wqkv{i}"] = torch.cat([wq, wk, wv]).to(ct).contiguous()
+                P[f"bqkv{i}"] = torch.cat([bq, bk, bv]).float().contiguous()
+                P[f"wo{i}"] = wo.to(ct).contiguous()
+                P[f"bo{i}"] = bo.float().contiguous()
+                S, rows = (L, L + 1) if i == 0 else (T, T + 1)
+                P[f"kvb{i}"] = hl.kvb(bias_k, bias_v, S, rows, inv_freq)
+            w1, b1, w2, b2 = params[20:24]
+            P["w1"], P["b1"] = w1.to(ct).contiguous(), b1.float().contiguous()
+            P["w2"], P["b2"] = w2.to(ct).contiguous(), b2.float().contiguous()
+            rope_l = hl.table(L + 1, inv_freq) if hl.rope else None
+            rope_t = hl.table(T + 1, inv_freq) if hl.rope else None
+        lw = _lib.MdgLayerWeights()
+        for i in range(2):
+            lw.wqkv[i], lw.bqkv[i] = P[f"wqkv{i}"].data_ptr(), P[f"bqkv{i}"].data_ptr()
+            lw.wo[i], lw.bo[i], lw.kvb[i] = P[f"wo{i}"].data_ptr(), P[f"bo{i}"].data_ptr(), P[f"kvb{i}"].data_ptr()
+        lw.w1, lw.b1, lw.w2, lw.b2 = P["w1"].data_ptr(), P["b1"].data_ptr(), P["w2"].data_ptr(), P["b2"].data_ptr()
+        dims = hl.dims(B, T, L)
+        long_l = L >= 16
+        kb_t = torch.empty(B * L, T, device=dev)
+        kb_s = torch.empty(B * T, L, device=dev)
+        _lib.check(lib.mdg_mask_bias(B, T, L, mask.data_ptr(), kb_t.data_ptr(), kb_s.data_ptr(), s), "mdg_mask_bias")
+        e = lambda *shape, dt=ct: torch.empty(*shape, device=dev, dtype=dt)  # noqa: E731
+        sv = {"xn": [e(N, C) for _ in range(3)], "stats": [e(N, 2, dt=torch.float32) for _ in range(3)],
+              "qkv_s": e(3, B * T, H, L, _lib.MDG_DP) if long_l else e(N, 3 * C),
+              "lse_s": e(B * T, H, L, dt=torch.float32) if long_l else None,
+              "qkv_t": e(3, B * L, H, T, _lib.MDG_DP), "lse_t": e(B * L, H, T, dt=torch.float32),
+              "o": [e(N, C), e(N, C)], "y": [e(N, C) for _ in range(3)],
+              "h1": e(N, C, dt=torch.float32), "h2": e(N, C, dt=torch.float32), "u": e(N, F), "act": e(N, F)}
+        cs = _lib.MdgLayerSaved()
+        for i in range(3):
+            cs.xn[i], cs.stats[i], cs.y[i] = sv["xn"][i].data_ptr(), sv["stats"][i].data_ptr(), sv["y"][i].data_ptr()
+        cs.qkv_s, cs.lse_s = sv["qkv_s"].data_ptr(), _lib.ptr(sv["lse_s"])
+        cs.qkv_t, cs.lse_t = sv["qkv_t"].data_ptr(), sv["lse_t"].data_ptr()
+        cs.o[0], cs.o[1] = sv["o"][0].data_ptr(), sv["o"][1].data_ptr()
+        cs.h1, cs.h2, cs.u, cs.act = sv["h1"].data_ptr(), sv["h2"].data_ptr(), sv["u"].data_ptr(), sv["act"].data_ptr()
+        cs.init_planes = 1
+        h_out = torch.empty_like(h)
+        _lib.check(lib.mdg_layer_fwd_train(ctypes.byref(dims), ctypes.byref(lw), _lib.ptr(rope_l), _lib.ptr(rope_t),
+                                           mods.data_ptr(), mask.data_ptr(), kb_t.data_ptr(), kb_s.data_ptr(),
+                                           h.data_ptr(), h_out.data_ptr(), ctypes.byref(cs), s),
+                   "mdg_layer_fwd_train")
+        ctx.hl, ctx.sv, ctx.P = hl, sv, P
+        ctx.shape = (B, T, L)
+        ctx.kb = (kb_t, kb_s)
+        ctx.mask = mask
+        ctx.rope = (rope_l, rope_t)
+        ctx.inv_freq = inv_freq
+        ctx.save_for_backward(h, mods)
+        return h_out
+
+    @staticmethod
+    def backward(ctx, dh3):
+        hl, sv, P = ctx.hl, ctx.sv, ctx.P
+        lib = hl.lib
+        h, mods = ctx.saved_tensors
+        B, T, L = ctx.shape
+        C, H, D, F, ct, dt = hl.C, hl.H, hl.D, hl.F, hl.ct, hl.mdg_dtype
+        N, TL, dev = B * T * L, T * L, h.device
+        s = _lib.stream_handle()
+        rope_l, rope_t = ctx.rope
+        kb_t, kb_s = ctx.kb
+        dh3 = dh3.contiguous().float().reshape(N, C)
+        mods = mods.contiguous()
+        nblk = lib.mdg_ln_gate_bwd_blocks(TL)
+        qscale = D ** -0.5
+        e = lambda *shape, dtp=ct: torch.empty(*shape, device=dev, dtype=dtp)  # noqa: E731
+
+        def lngate(dxn, h_ln, stats, shift_off, scale_off, dh_res, dh_out, y, gate_off, dy):
+            part = torch.empty(B, nblk, 4, C, device=dev)
+            _lib.check(lib.mdg_ln_gate_bwd(dt, N, C, TL, _lib.ptr(dxn), _lib.ptr(h_ln), _lib.ptr(stats),
+                                           mods.data_ptr(), 9 * C, shift_off, scale_off, dh_res.data_ptr(),
+                                           dh_out.data_ptr(), _lib.ptr(y), gate_off, _lib.ptr(dy), part.data_ptr(), s),
+                       "mdg_ln_gate_bwd")
+            return part
+
+        def dx_gemm(dy, w_t, K, Nout, act=_lib.MDG_ACT_NONE, aux=None):
+            """out [N][Nout] (CT) = dy [N][K] . w_t^T with w_t = W^T [Nout][K]."""
+            out = e(N, Nout)
+            g = _lib.MdgGemmDesc()
+            g.dtype, g.a_mode, g.epi, g.act = dt, _lib.MDG_A_PLAIN, _lib.MDG_EPI_STORE, act
+            g.M, g.N, g.K = N, Nout, K
+            g.A, g.lda, g.W, g.ldw = dy.data_ptr(), K, w_t.data_ptr(), K
+            g.out, g.ldo = out.data_ptr(), Nout
+            if aux is not None:
+                g.aux, g.ldaux = aux.data_ptr(), Nout
+            _lib.check(lib.mdg_gemm(ctypes.byref(g), s), "mdg_gemm(dX)")
+            return out
+
+        grads = {}
+        # ---- MLP: h3 = h2 + g_m * (fc2(gelu(fc1(xn3))))
+        dy_m = e(N, C)
+        part_m = lngate(None, None, None, 0, 0, dh3, dh3, sv["y"][2], 8 * C, dy_m)
+        grads["w2"] = _mm_f32(dy_m.t(), sv["act"])
+        grads["b2"] = part_m[:, :, 3].sum((0, 1))
+        du = dx_gemm(dy_m, P["w2"].t().contiguous(), C, F, _lib.MDG_ACT_DGELU, sv["u"])
+        grads["w1"] = _mm_f32(du.t(), sv["xn"][2])
+        grads["b1"] = du.float().sum(0)
+        dxn3 = dx_gemm(du, P["w1"].t().contiguous(), F, C)
+        dh2 = e(N, C, dtp=torch.float32)
+        dy_t = e(N, C)
+        part_t = lngate(dxn3, sv["h2"], sv["stats"][2], 6 * C, 7 * C, dh3, dh2, sv["y"][1], 5 * C, dy_t)
+
+        def attention(i, dy, o, xn, qkv, lse):
+            """out_proj + attention backward of attention i (0 spatial, 1 temporal); returns dxn."""
+            grads[f"wo{i}"] = _mm_f32(dy.t(), o)
+            do = dx_gemm(dy, P[f"wo{i}"].t().contiguous(), C, C)
+            dqkv = e(N, 3 * C)
+            if i == 1 or L >= 16:
+                Bq, Tq, Lq = (B, T, L) if i == 1 else (B * T, L, 1)
+                rope, rows = (rope_t, T + 1) if i == 1 else (rope_l, L + 1)
+                kb = kb_t if i == 1 else kb_s
+                parts = lib.mdg_attn_temporal_bwd_parts(dt, Bq, Tq, Lq)
+                bpart = torch.zeros(H, parts, 2, _lib.MDG_DP, device=dev)
+                scratch = torch.empty(lib.mdg_attn_temporal_bwd_scratch(dt, Bq, Tq, Lq, H), device=dev,
+                                      dtype=torch.uint8)
+                _lib.check(lib.mdg_attn_temporal_bwd(dt, Bq, Tq, Lq, H, D, qkv.data_ptr(), kb.data_ptr(),
+                                                     P[f"kvb{i}"].data_ptr(), o.data_ptr(), do.data_ptr(),
+                                                     lse.data_ptr(), _lib.ptr(rope), rows, scratch.data_ptr(),
+                                                     dqkv.data_ptr(), 3 * C, bpart.data_ptr(), qscale, _LN2, 0, s),
+                           "mdg_attn_temporal_bwd")
+            else:
+                parts = lib.mdg_attn_spatial_bwd_parts(B * T, L, D)
+                bpart = torch.zeros(H, parts, 2, _lib.MDG_DP, device=dev)
+                _lib.check(lib.mdg_attn_spatial_bwd(dt, B * T, L, H, D, qkv.data_ptr(), P["kvb0"].data_ptr(),
+                                                    ctx.mask.data_ptr(), do.data_ptr(), _lib.ptr(rope_l), L + 1,
+                                                    dqkv.data_ptr(), bpart.data_ptr(), qscale, s),
+                           "mdg_attn_spatial_bwd")
+            grads[f"kvb{i}"] = bpart.sum(1)
+            grads[f"wqkv{i}"] = _mm_f32(dqkv.t(), xn)
+            grads[f"bqkv{i}"] = dqkv.float().sum(0)
+            return dx_gemm(dqkv, P[f"wqkv{i}"].t().contiguous(), 3 * C, C)
+
+        dxn2 = attention(1, dy_t, sv["o"][1], sv["xn"][1], sv["qkv_t"], sv["lse_t"])
+        dh1 = e(N, C, dtp=torch.float32)
+        dy_s = e(N, C)
+        part_s = lngate(dxn2, sv["h1"], sv["stats"][1], 3 * C, 4 * C, dh2, dh1, sv["y"][0], 2 * C, dy_s)
+        dxn1 = attention(0, dy_s, sv["o"][0], sv["xn"][0], sv["qkv_s"], sv["lse_s"])
+        dh0 = e(N, C, dtp=torch.float32)
+        part_0 = lngate(dxn1, h.reshape(N, C), sv["stats"][0], 0, C, dh1, dh0, None, 0, None)
+
+        # adaLN chunks, latent_model.py:459-461 order
+        red = lambda part, k: part[:, :, k].sum(1)  # noqa: E731
+        dmods = torch.cat([red(part_0, 0), red(part_0, 1), red(part_s, 2), red(part_s, 0), red(part_s, 1),
+                           red(part_t, 2), red(part_t, 0), red(part_t, 1), red(part_m, 2)], -1)
+        grads["bo0"] = part_s[:, :, 3].sum((0, 1))
+        grads["bo1"] = part_t[:, :, 3].sum((0, 1))
+
+        # packed -> parameter layout
+        perm = hl.perm(dev) if hl.rope else None
+        out = []
+        for i in range(2):
+            gw, gb = grads[f"wqkv{i}"], grads[f"bqkv{i}"]
+            gq, gk, gv = gw[:C], gw[C:2 * C], gw[2 * C:]
+            bq, bk, bv = gb[:C], gb[C:2 * C], gb[2 * C:]
+            if perm is not None:
+                def unperm(x):
+                    y = torch.empty_like(x)
+                    y[perm] = x
+                    return y
+
+                gq, gk, bq, bk = unperm(gq), unperm(gk), unperm(bq), unperm(bk)
+            S, rows = (L, L + 1) if i == 0 else (T, T + 1)
+            gbk, gbv = hl.kvb_grad(grads[f"kvb{i}"], S, rows, ctx.inv_freq)
+            out += [gq, bq, gk, bk, gv, bv, grads[f"wo{i}"], grads[f"bo{i}"], gbk, gbv]
+        out += [grads["w1"], grads["b1"], grads["w2"], grads["b2"]]
+        del ctx.sv, ctx.P
+        return (dh0.reshape(B, T, L, C), dmods, None, None, None, *out)

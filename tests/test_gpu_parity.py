@@ -23,8 +23,8 @@ from tests.conftest import build_model, load_golden
 pytestmark = pytest.mark.gpu
 
 F32_MAX, F32_REL = 1e-3, 1e-4
-BF16_REL, BF16_REL_SOLVE = 2.5e-2, 5e-2
-BF16_ELEM, BF16_ELEM_SOLVE = 5e-2, 1e-1
+BF16_REL, BF16_REL_SOLVE = 6e-3, 8e-3
+BF16_ELEM, BF16_ELEM_SOLVE = 7e-3, 6e-3
 
 
 @pytest.fixture(scope="module", autouse=True)

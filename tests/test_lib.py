@@ -13,7 +13,7 @@ HEADER = os.path.join(REPO, "include", "mdgen_hip.h")
 
 def _declared():
     src = open(HEADER).read()
-    return set(re.findall(r"^\s*(?:int|size_t|const char\*)\s+(mdg_\w+)\s*\(", src, re.M))
+    return set(re.findall(r"^\s*(?:int|int32_t|size_t|const char\*)\s+(mdg_\w+)\s*\(", src, re.M))
 
 
 def test_header_declares_binding_signatures():
@@ -52,10 +52,11 @@ def test_struct_layouts_match_header():
 #include <stddef.h>
 #include "mdgen_hip.h"
 int main(void){
- printf("%zu %zu %zu %zu %zu\n", sizeof(mdg_dims), sizeof(mdg_layer_weights), sizeof(mdg_model),
-        sizeof(mdg_step_io), sizeof(mdg_gemm_desc));
- printf("%zu %zu %zu %zu\n", offsetof(mdg_step_io, dt), offsetof(mdg_step_io, h),
-        offsetof(mdg_gemm_desc, qscale), offsetof(mdg_gemm_desc, rope_rows));
+ printf("%zu %zu %zu %zu %zu %zu\n", sizeof(mdg_dims), sizeof(mdg_layer_weights), sizeof(mdg_model),
+        sizeof(mdg_step_io), sizeof(mdg_gemm_desc), sizeof(mdg_layer_saved));
+ printf("%zu %zu %zu %zu %zu %zu %zu\n", offsetof(mdg_step_io, dt), offsetof(mdg_step_io, h),
+        offsetof(mdg_gemm_desc, qscale), offsetof(mdg_gemm_desc, rope_rows), offsetof(mdg_gemm_desc, aux),
+        offsetof(mdg_gemm_desc, ldaux), offsetof(mdg_layer_saved, init_planes));
  return 0; }
 """
     with tempfile.TemporaryDirectory() as td:
@@ -64,12 +65,13 @@ int main(void){
         exe = os.path.join(td, "t")
         subprocess.check_call(["gcc", "-I", os.path.dirname(HEADER), c, "-o", exe])
         out = subprocess.check_output([exe]).decode().split()
-    sizes = [int(v) for v in out[:5]]
-    offs = [int(v) for v in out[5:]]
+    sizes = [int(v) for v in out[:6]]
+    offs = [int(v) for v in out[6:]]
     assert sizes == [ctypes.sizeof(s) for s in (_lib.MdgDims, _lib.MdgLayerWeights, _lib.MdgModel,
-                                                 _lib.MdgStepIO, _lib.MdgGemmDesc)]
+                                                 _lib.MdgStepIO, _lib.MdgGemmDesc, _lib.MdgLayerSaved)]
     assert offs == [_lib.MdgStepIO.dt.offset, _lib.MdgStepIO.h.offset, _lib.MdgGemmDesc.qscale.offset,
-                    _lib.MdgGemmDesc.rope_rows.offset]
+                    _lib.MdgGemmDesc.rope_rows.offset, _lib.MdgGemmDesc.aux.offset, _lib.MdgGemmDesc.ldaux.offset,
+                    _lib.MdgLayerSaved.init_planes.offset]
 
 
 def test_shape_validation_without_gpu():
