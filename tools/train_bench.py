@@ -27,12 +27,15 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--precision", default="32-true")
     ap.add_argument("--bucket_cap_mb", type=int, default=32)
+    ap.add_argument("--train_backend", default="hip", choices=["hip", "torch"])
+    ap.add_argument("--hip_dtype", default="bf16", choices=["bf16", "f32"])
     a = ap.parse_args()
     rank, world, dev = setup_distributed()
     args = parse_train_args(["--synthetic", "--sim_condition", "--prepend_ipa", "--abs_pos_emb",
                              "--num_frames", str(a.frames), "--crop", str(a.crop), "--batch_size", str(a.batch),
                              "--synthetic_size", str(a.batch * world), "--precision", a.precision,
-                             "--bucket_cap_mb", str(a.bucket_cap_mb)])
+                             "--bucket_cap_mb", str(a.bucket_cap_mb),
+                             "--train_backend", a.train_backend, "--hip_dtype", a.hip_dtype])
     torch.set_float32_matmul_precision("medium")
     tr = Trainer(args, rank, world, dev)
     batch = next(iter(tr.loader))
@@ -57,7 +60,8 @@ def main():
             "metric": "training frames/sec (GVP flow-matching step, forward+backward+Adam)",
             "value": round(world * a.batch * a.frames * a.steps / el, 1), "unit": "frames/s",
             "n_gpus": world, "ms_per_step": round(el / a.steps * 1e3, 2), "batch_per_gpu": a.batch,
-            "frames": a.frames, "crop": a.crop, "precision": a.precision, "loss": float(loss),
+            "frames": a.frames, "crop": a.crop, "precision": a.precision,
+            "train_backend": a.train_backend, "hip_dtype": a.hip_dtype if a.train_backend == "hip" else None, "loss": float(loss),
             "max_mem_gb": round(torch.cuda.max_memory_allocated() / 2 ** 30, 2)}), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
