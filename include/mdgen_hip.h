@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define MDG_ABI_VERSION 10
+#define MDG_ABI_VERSION 11
 #define MDG_MAX_LAYERS 16
 #define MDG_DP 32 /* padded head dim of every attention operand buffer (head_dim <= 31) */
 
@@ -241,6 +241,82 @@ int mdg_latents_to_atom14(int32_t B, int32_t T, int32_t L, int32_t latent, int32
                           const float* atom_mask, const float* lit, float* atom14, float* out_rots,
                           float* out_trans, void* stream);
 
+
+/* ---------------------------------------------------------------------------------------
+   Conditioning precompute (x-independent, once per rollout window for all S time points):
+     c        = TimestepEmbedder(t * time_multiplier)            layers.py:17-55, latent_model.py:252
+     mods     = adaLN_modulation(c) of every LatentMDGenLayer     latent_model.py:459-461
+     mods_fin = FinalLayer.adaLN_modulation(c)                    layers.py:72
+     ipa      = run_ipa(c, mask[:, 0], start/end frames, aatype)  latent_model.py:179-214, 341-394
+                (IPALayer: affine LN -> InvariantPointAttention ipa.py:92-255 -> gated MHA over the
+                 L residues with RoPE + bias_kv -> gated MLP); TPS: two IPA stacks on the relative
+                 frames start^-1 o end / end^-1 o start (rigid_utils.py Rigid.invert/compose/
+                 to_tensor_7), summed.
+   Everything runs in fp32 (exact-f32 MFMA / VALU), whatever the denoiser's operand type.
+   Rows r = s*B + b.  Weights are fp32 (nn.Linear layout unless stated). */
+typedef struct {
+  int32_t S, B, L;          /* time points, trajectories, residues */
+  int32_t C, H, D;          /* embed_dim, mha_heads, head_dim (the IPA layers' MHA) */
+  int32_t num_layers;       /* LatentMDGenLayers (adaLN 9C rows each) */
+  int32_t ipa_layers;       /* IPALayers (0 = no IPA prepend) */
+  int32_t ipa_heads, ipa_c, ipa_qk, ipa_v; /* InvariantPointAttention no_heads, c_hidden, P_q, P_v */
+  int32_t tps;              /* 1: TPS branch (two IPA stacks on relative frames) */
+  int32_t freq_dim;         /* TimestepEmbedder frequency_embedding_size (256) */
+} mdg_cond_dims;
+
+typedef struct {
+  const float* ln_w; const float* ln_b; /* ipa_norm (affine LayerNorm, eps 1e-5) [C] */
+  const float* w_proj; const float* b_proj; /* [P_pad][C], [P_pad]: rows linear_q (H*c) | linear_kv
+                                               (H*2c) | linear_q_points (3*H*P_q) | linear_kv_points
+                                               (3*H*(P_q+P_v)), zero rows up to P_pad = round_up(P, 32) */
+  const float* head_weights; /* raw ipa.head_weights [H] (softplus applied on the device) */
+  const float* w_out; const float* b_out; /* linear_out [C][K_pad], K = H*(c + 4*P_v) zero-padded to 64k */
+  const float* wqkv; const float* bqkv;   /* mha_l q|k|v [3C][C] / [3C] packed as mdg_layer_weights */
+  const float* kvb;                        /* [H][2][32] as mdg_layer_weights (position L) */
+  const float* wo; const float* bo;        /* out_proj */
+  const float* w1; const float* b1; const float* w2; const float* b2; /* fc1 [4C][C], fc2 [C][4C] */
+} mdg_ipa_layer_weights;
+
+typedef struct {
+  mdg_cond_dims dims;
+  float time_multiplier;
+  const float* t_freqs;                   /* [freq_dim/2] exp(-ln(1e4) i / half) */
+  const float* t_w0; const float* t_b0;   /* t_embedder.mlp.0 [C][freq_dim] */
+  const float* t_w2; const float* t_b2;   /* t_embedder.mlp.2 [C][C] */
+  const float* ada_w; const float* ada_b; /* every adaLN Linear stacked: rows num_layers*9C (layers) |
+                                             2C (FinalLayer) | ipa_layers*6C (IPA layers), [.][C] */
+  const float* aa_emb;                    /* aatype_to_emb [21][C] (null = no aa embedding) */
+  const float* l2e_f_w; const float* l2e_f_b; /* TPS latent_to_emb_f [C][7], [C] */
+  const float* l2e_r_w; const float* l2e_r_b; /* TPS latent_to_emb_r */
+  const float* rope_l;                    /* [L+1][D/2] cos | sin (null = no RoPE) */
+  mdg_ipa_layer_weights ipa[MDG_MAX_LAYERS];
+} mdg_cond_model;
+
+typedef struct {
+  const float* t;          /* [S*B] raw t (time_multiplier applied here) */
+  const float* mask;       /* frame mask (the reference's mask[:, 0]): mask[b*mask_stride + l] */
+  int32_t mask_stride;     /* elements between trajectories' mask rows (0 = L; T*L for a [B,T,L]
+                              mask, whose frame-0 rows are then read in place) */
+  const float* rots; const float* trans;         /* start frames [B][L][3][3], [B][L][3] */
+  const float* end_rots; const float* end_trans; /* TPS end frames */
+  const float* rel7;       /* TPS: [2][B][L][7] (start^-1 o end | end^-1 o start) 7-vectors; null =
+                              computed on the device (mdg_tps_rel7) */
+  const int64_t* aatype;   /* [B][L] in [0, 21) or null */
+  float* mods;             /* out [S][num_layers][B][9C] */
+  float* mods_final;       /* out [S][B][2C] */
+  float* ipa;              /* out [S][B][L][C] (ignored when ipa_layers == 0) */
+} mdg_cond_io;
+
+size_t mdg_cond_workspace_bytes(const mdg_cond_dims* d);
+int mdg_precompute_cond(const mdg_cond_model* m, const mdg_cond_io* io, void* ws, void* stream);
+
+/* TPS relative 7-vectors on the device, per residue (b, l): out[0] = start^-1 o end, out[1] =
+   end^-1 o start, each [quaternion (w,x,y,z) | translation] (Rigid.invert().compose().
+   to_tensor_7(), latent_model.py:197-199).  The quaternion is the dominant eigenvector of
+   rot_to_quat's K matrix (rigid_utils.py:191-210); LAPACK leaves its sign arbitrary, here it is
+   fixed to w >= 0.  out [2][B][L][7]. */
+int mdg_tps_rel7(int32_t B, int32_t L, const float* rots, const float* trans, const float* end_rots,
+                 const float* end_trans, float* out, void* stream);
 
 /* ---------------------------------------------------------------------------------------
    Training (Transport.training_losses -> model forward -> loss.backward(): transport.py:137-222,

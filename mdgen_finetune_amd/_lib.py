@@ -73,6 +73,27 @@ class MdgLayerSaved(ctypes.Structure):
                 ("init_planes", _i32)]
 
 
+class MdgCondDims(ctypes.Structure):
+    _fields_ = [(n, _i32) for n in ("S", "B", "L", "C", "H", "D", "num_layers", "ipa_layers", "ipa_heads", "ipa_c",
+                                    "ipa_qk", "ipa_v", "tps", "freq_dim")]
+
+
+class MdgIpaLayerWeights(ctypes.Structure):
+    _fields_ = [(n, _vp) for n in ("ln_w", "ln_b", "w_proj", "b_proj", "head_weights", "w_out", "b_out", "wqkv",
+                                   "bqkv", "kvb", "wo", "bo", "w1", "b1", "w2", "b2")]
+
+
+class MdgCondModel(ctypes.Structure):
+    _fields_ = [("dims", MdgCondDims), ("time_multiplier", _f32)] + [
+        (n, _vp) for n in ("t_freqs", "t_w0", "t_b0", "t_w2", "t_b2", "ada_w", "ada_b", "aa_emb", "l2e_f_w", "l2e_f_b",
+                           "l2e_r_w", "l2e_r_b", "rope_l")] + [("ipa", MdgIpaLayerWeights * MDG_MAX_LAYERS)]
+
+
+class MdgCondIO(ctypes.Structure):
+    _fields_ = [("t", _vp), ("mask", _vp), ("mask_stride", _i32)] + [
+        (n, _vp) for n in ("rots", "trans", "end_rots", "end_trans", "rel7", "aatype", "mods", "mods_final", "ipa")]
+
+
 # (name, restype, argtypes) of every exported entry point — the test suite checks that the
 # built library exports exactly these and that include/mdgen_hip.h declares them.
 SIGNATURES = [
@@ -96,6 +117,9 @@ SIGNATURES = [
     ("mdg_attn_temporal_lse", _i32, [_i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
     ("mdg_prep_latents", _i32, [_i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     ("mdg_latents_to_atom14", _i32, [_i32, _i32, _i32, _i32, _i32, _i32] + [_vp] * 12),
+    ("mdg_cond_workspace_bytes", ctypes.c_size_t, [ctypes.POINTER(MdgCondDims)]),
+    ("mdg_precompute_cond", _i32, [ctypes.POINTER(MdgCondModel), ctypes.POINTER(MdgCondIO), _vp, _vp]),
+    ("mdg_tps_rel7", _i32, [_i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
     ("mdg_mask_bias", _i32, [_i32, _i32, _i32, _vp, _vp, _vp, _vp]),
     ("mdg_layer_fwd_train", _i32, [ctypes.POINTER(MdgDims), ctypes.POINTER(MdgLayerWeights), _vp, _vp, _vp, _vp, _vp,
                                    _vp, _vp, _vp, ctypes.POINTER(MdgLayerSaved), _vp]),
@@ -111,7 +135,7 @@ SIGNATURES = [
                                     _vp]),
 ]
 
-ABI_VERSION = 10
+ABI_VERSION = 11
 _LIB = None
 
 

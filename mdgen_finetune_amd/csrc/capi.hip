@@ -57,6 +57,21 @@ int attn_spatial_bwd_parts(int nf, int L, int D);
 hipError_t attn_spatial_bwd_launch(int dtype, int nf, int L, int H, int D, const void* qkv, const float* kvb,
                                    const float* mask, const void* dout, const float* rope, int rope_rows, void* dqkv,
                                    float* bpart, float qscale, hipStream_t s);
+// cond.hip
+hipError_t temb_freq_launch(int R, int half, float mult, const float* t, const float* freqs, float* out,
+                            hipStream_t s);
+hipError_t cond_scatter_launch(int S, int B, int nl, int C, int W, const float* all, float* mods, float* mods_final,
+                               hipStream_t s);
+hipError_t ipa_init_launch(int R, int B, int L, int C, int mstride, const int64_t* aatype, const float* aa_emb, const float* rel7,
+                           const float* w, const float* bias, const float* mask, float* x, float* mask_rep,
+                           hipStream_t s);
+hipError_t add_inplace_launch(size_t n, float* y, const float* x, hipStream_t s);
+bool ipa_attn_supported(int c, int pq, int pv);
+hipError_t ipa_attn_launch(int R, int B, int L, int H, int c, int pq, int pv, const float* proj, int ldp,
+                           const float* rots, const float* trans, const float* mask, const float* head_weights,
+                           float* out, int ldc, hipStream_t s);
+hipError_t tps_rel7_launch(int B, int L, const float* rots, const float* trans, const float* erots,
+                           const float* etrans, float* out, hipStream_t s);
 }  // namespace mdg
 
 namespace {
@@ -711,6 +726,230 @@ int mdg_attn_spatial_bwd(int32_t dtype, int32_t n_frames, int32_t L, int32_t H, 
   return hip_check(mdg::attn_spatial_bwd_launch(dtype, n_frames, L, H, D, qkv, kvb, mask, dout, rope, rope_rows, dqkv,
                                                 bpart, qscale, (hipStream_t)stream),
                    "attn_spatial_bwd");
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------------------------------
+// Conditioning precompute (mdg_precompute_cond): t-embedding, every adaLN modulation and the
+// IPA prepend for all S time points of a window, fp32 throughout.
+namespace {
+
+struct CondLayout {
+  int R, M, W, P, Ppad, Kout, Kpad;
+  size_t emb, hmid, sc, all, x2, xn, proj, cat, qkv, o, hid, mrep, kb_t, kb_s, rel7, total;
+};
+
+CondLayout cond_layout(const mdg_cond_dims& d) {
+  CondLayout c;
+  c.R = d.S * d.B;
+  c.M = c.R * d.L;
+  c.W = d.num_layers * 9 * d.C + 2 * d.C + d.ipa_layers * 6 * d.C;
+  const int H = d.ipa_heads;
+  c.P = H * d.ipa_c * 3 + 3 * H * d.ipa_qk + 3 * H * (d.ipa_qk + d.ipa_v);
+  c.Ppad = (c.P + 31) / 32 * 32;
+  c.Kout = H * (d.ipa_c + 4 * d.ipa_v);
+  c.Kpad = (c.Kout + 63) / 64 * 64;
+  const size_t f = sizeof(float), M = (size_t)c.M, C = d.C;
+  const bool ipa = d.ipa_layers > 0;
+  size_t off = 0;
+  auto take = [&](size_t bytes) { const size_t o = off; off += align256(bytes); return o; };
+  c.emb = take((size_t)c.R * d.freq_dim * f);
+  c.hmid = take((size_t)c.R * C * f);
+  c.sc = take((size_t)c.R * C * f);
+  c.all = take((size_t)c.R * c.W * f);
+  const size_t qkv_spatial = M * 3 * C * f;
+  const size_t qkv_planes = 3ull * c.R * d.H * d.L * MDG_DP * f;
+  c.x2 = take(ipa && d.tps ? M * C * f : 0);
+  c.xn = take(ipa ? M * C * f : 0);
+  c.proj = take(ipa ? M * c.Ppad * f : 0);
+  c.cat = take(ipa ? M * c.Kpad * f : 0);
+  c.qkv = take(ipa ? (qkv_spatial > qkv_planes ? qkv_spatial : qkv_planes) : 0);
+  c.o = take(ipa ? M * C * f : 0);
+  c.hid = take(ipa ? M * 4 * C * f : 0);
+  c.mrep = take(ipa ? M * f : 0);
+  c.kb_t = take(ipa ? M * f : 0);
+  c.kb_s = take(ipa ? M * f : 0);
+  c.rel7 = take(ipa && d.tps ? 2ull * d.B * d.L * 7 * f : 0);
+  c.total = off;
+  return c;
+}
+
+int check_cond_dims(const mdg_cond_dims* d) {
+  if (!d) return fail(MDG_E_ARG, "null cond dims");
+  if (d->S <= 0 || d->B <= 0 || d->L <= 0 || d->C <= 0 || d->num_layers < 0 || d->num_layers > MDG_MAX_LAYERS ||
+      d->ipa_layers < 0 || d->ipa_layers > MDG_MAX_LAYERS)
+    return fail(MDG_E_SHAPE, "cond: S,B,L,C,layers = %d,%d,%d,%d,%d/%d", d->S, d->B, d->L, d->C, d->num_layers,
+                d->ipa_layers);
+  if (d->C % 64 || d->C > 384) return fail(MDG_E_SHAPE, "cond: embed_dim %d (64k, <= 384 on the fp32 path)", d->C);
+  if (d->freq_dim <= 0 || d->freq_dim % 64) return fail(MDG_E_SHAPE, "cond: freq_dim %d (64k)", d->freq_dim);
+  if ((long long)d->S * d->B * d->L * 4 * d->C >= (1ll << 31)) return fail(MDG_E_SHAPE, "cond: problem too large");
+  if (d->ipa_layers > 0) {
+    if (d->H <= 0 || d->C != d->H * d->D || d->D % 4 || d->D >= MDG_DP)
+      return fail(MDG_E_SHAPE, "cond: IPA-layer MHA C=%d H=%d D=%d", d->C, d->H, d->D);
+    if (d->ipa_heads <= 0 || !mdg::ipa_attn_supported(d->ipa_c, d->ipa_qk, d->ipa_v))
+      return fail(MDG_E_SHAPE, "cond: IPA heads=%d c=%d P_q=%d P_v=%d has no kernel instance", d->ipa_heads, d->ipa_c,
+                  d->ipa_qk, d->ipa_v);
+  }
+  return MDG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t mdg_cond_workspace_bytes(const mdg_cond_dims* d) {
+  if (check_cond_dims(d)) return 0;
+  return cond_layout(*d).total;
+}
+
+int mdg_tps_rel7(int32_t B, int32_t L, const float* rots, const float* trans, const float* end_rots,
+                 const float* end_trans, float* out, void* stream) {
+  if (!rots || !trans || !end_rots || !end_trans || !out) return fail(MDG_E_ARG, "tps_rel7: null pointer");
+  if (B <= 0 || L <= 0) return fail(MDG_E_SHAPE, "tps_rel7: B=%d L=%d", B, L);
+  return hip_check(mdg::tps_rel7_launch(B, L, rots, trans, end_rots, end_trans, out, (hipStream_t)stream), "tps_rel7");
+}
+
+int mdg_precompute_cond(const mdg_cond_model* m, const mdg_cond_io* io, void* ws, void* stream) {
+  if (!m || !io || !ws) return fail(MDG_E_ARG, "precompute_cond: null model/io/workspace");
+  const mdg_cond_dims& d = m->dims;
+  if (int e = check_cond_dims(&d)) return e;
+  if (!io->t || !io->mods || !io->mods_final || !m->t_freqs || !m->t_w0 || !m->t_w2 || !m->ada_w)
+    return fail(MDG_E_ARG, "precompute_cond: null t / outputs / t-embedder / adaLN weights");
+  const CondLayout c = cond_layout(d);
+  char* wb = (char*)ws;
+  auto F = [&](size_t off) { return (float*)(wb + off); };
+  hipStream_t s = (hipStream_t)stream;
+  const int C = d.C;
+
+  mdg_gemm_desc g;
+  memset(&g, 0, sizeof(g));
+  g.dtype = MDG_F32;
+  g.a_mode = MDG_A_PLAIN;
+  g.out_f32 = 1;
+
+  // ---- c = TimestepEmbedder(t * mult); only SiLU(c) is consumed (every adaLN Linear, and the
+  //      IPA layers', is nn.Sequential(SiLU, Linear)), so mlp.2's epilogue applies the SiLU
+  if (int e = hip_check(mdg::temb_freq_launch(c.R, d.freq_dim / 2, m->time_multiplier, io->t, m->t_freqs,
+                                              F(c.emb), s), "temb_freq"))
+    return e;
+  mdg_gemm_desc t0 = g;
+  t0.epi = MDG_EPI_STORE; t0.act = MDG_ACT_SILU;
+  t0.M = c.R; t0.N = C; t0.K = d.freq_dim; t0.A = F(c.emb); t0.lda = d.freq_dim;
+  t0.W = m->t_w0; t0.ldw = d.freq_dim; t0.bias = m->t_b0; t0.out = F(c.hmid); t0.ldo = C;
+  if (int e = mdg_gemm(&t0, stream)) return e;
+  mdg_gemm_desc t2 = t0;
+  t2.K = C; t2.A = F(c.hmid); t2.lda = C; t2.W = m->t_w2; t2.ldw = C; t2.bias = m->t_b2; t2.out = F(c.sc);
+  if (int e = mdg_gemm(&t2, stream)) return e;
+  // ---- every adaLN modulation in one GEMM, rows scattered to the denoiser's layouts
+  mdg_gemm_desc ad = g;
+  ad.epi = MDG_EPI_STORE;
+  ad.M = c.R; ad.N = c.W; ad.K = C; ad.A = F(c.sc); ad.lda = C; ad.W = m->ada_w; ad.ldw = C; ad.bias = m->ada_b;
+  ad.out = F(c.all); ad.ldo = c.W;
+  if (int e = mdg_gemm(&ad, stream)) return e;
+  if (int e = hip_check(mdg::cond_scatter_launch(d.S, d.B, d.num_layers, C, c.W, F(c.all), io->mods, io->mods_final,
+                                                 s), "cond_scatter"))
+    return e;
+  if (d.ipa_layers == 0) return MDG_OK;
+
+  // ---- IPA prepend (run_ipa, latent_model.py:179-214) on M = S*B*L residue tokens
+  if (!io->ipa || !io->mask || !io->rots || !io->trans) return fail(MDG_E_ARG, "precompute_cond: IPA inputs");
+  if (io->aatype && !m->aa_emb) return fail(MDG_E_ARG, "precompute_cond: aatype without aa_emb");
+  if (d.tps && (!io->end_rots || !io->end_trans || !m->l2e_f_w || !m->l2e_r_w))
+    return fail(MDG_E_ARG, "precompute_cond: TPS end frames / latent_to_emb_f/_r");
+  const int L = d.L, M = c.M, H = d.H, D = d.D;
+  const float* rel7 = io->rel7;
+  if (d.tps && !rel7) {
+    if (int e = hip_check(mdg::tps_rel7_launch(d.B, L, io->rots, io->trans, io->end_rots, io->end_trans, F(c.rel7), s),
+                          "tps_rel7"))
+      return e;
+    rel7 = F(c.rel7);
+  }
+  const bool long_l = L >= kSpatialMfmaMinL && c.R <= 65535;
+  if (int e = hip_check(hipMemsetAsync(wb + c.cat, 0, (size_t)M * c.Kpad * sizeof(float), s), "cond memset"))
+    return e;
+  if (long_l) {  // the q|k|v planes of the MFMA route: zero pads, 1.0 in k / v pad column D
+    const size_t rows = (size_t)c.R * H * L;
+    if (int e = hip_check(hipMemsetAsync(wb + c.qkv, 0, 3 * rows * MDG_DP * sizeof(float), s), "cond memset"))
+      return e;
+    if (int e = hip_check(mdg::set_vpad_launch(MDG_F32, F(c.qkv) + rows * MDG_DP, 2 * rows, D, s), "set_vpad"))
+      return e;
+  }
+  const int ipa_mod0 = d.num_layers * 9 * C + 2 * C;
+  const float qs = 1.0f / sqrtf((float)D);
+  for (int stack = 0; stack < (d.tps ? 2 : 1); ++stack) {
+    // stack 0: x (sim) or x_r (TPS, start frames) -> io->ipa; stack 1: x_f (end frames) -> x2
+    float* x = stack == 0 ? io->ipa : F(c.x2);
+    const float* rots = stack == 0 ? io->rots : io->end_rots;
+    const float* trans = stack == 0 ? io->trans : io->end_trans;
+    const float* r7 = d.tps ? rel7 + (size_t)(stack == 0 ? 1 : 0) * d.B * L * 7 : nullptr;
+    const float* lw = d.tps ? (stack == 0 ? m->l2e_r_w : m->l2e_f_w) : nullptr;
+    const float* lb = d.tps ? (stack == 0 ? m->l2e_r_b : m->l2e_f_b) : nullptr;
+    if (int e = hip_check(mdg::ipa_init_launch(c.R, d.B, L, C, io->mask_stride > 0 ? io->mask_stride : L, io->aatype, io->aatype ? m->aa_emb : nullptr, r7, lw, lb,
+                                               io->mask, x, F(c.mrep), s), "ipa_init"))
+      return e;
+    if (long_l && stack == 0)
+      if (int e = hip_check(mdg::mask_bias_launch(c.R, 1, L, F(c.mrep), F(c.kb_t), F(c.kb_s), s), "mask_bias"))
+        return e;
+    for (int li = 0; li < d.ipa_layers; ++li) {
+      const mdg_ipa_layer_weights& w = m->ipa[li];
+      if (!w.w_proj || !w.w_out || !w.wqkv || !w.wo || !w.w1 || !w.w2 || !w.kvb || !w.head_weights)
+        return fail(MDG_E_ARG, "precompute_cond: IPA layer %d weights missing", li);
+      const float* mods = F(c.all) + ipa_mod0 + li * 6 * C;  // shift_l scale_l gate_l shift_m scale_m gate_m
+      // x += linear_out(IPA(ipa_norm(x)))
+      mdg_gemm_desc pj = g;
+      pj.a_mode = MDG_A_LNMOD; pj.epi = MDG_EPI_STORE;
+      pj.M = M; pj.N = c.Ppad; pj.K = C; pj.A = x; pj.lda = C; pj.W = w.w_proj; pj.ldw = C; pj.bias = w.b_proj;
+      pj.ln_w = w.ln_w; pj.ln_b = w.ln_b; pj.ln_eps = 1e-5f; pj.out = F(c.proj); pj.ldo = c.Ppad;
+      if (int e = mdg_gemm(&pj, stream)) return e;
+      if (int e = hip_check(mdg::ipa_attn_launch(c.R, d.B, L, d.ipa_heads, d.ipa_c, d.ipa_qk, d.ipa_v, F(c.proj), c.Ppad,
+                                                 rots, trans, F(c.mrep), w.head_weights, F(c.cat), c.Kpad, s),
+                            "ipa_attn"))
+        return e;
+      mdg_gemm_desc po = g;
+      po.epi = MDG_EPI_GATE_RES;
+      po.M = M; po.N = C; po.K = c.Kpad; po.A = F(c.cat); po.lda = c.Kpad; po.W = w.w_out; po.ldw = c.Kpad;
+      po.bias = w.b_out; po.resid = x; po.ldr = C;
+      if (int e = mdg_gemm(&po, stream)) return e;
+      // x += gate_l * mha_l(modulate(LN x, shift_l, scale_l), mask)
+      if (int e = hip_check(mdg::ln_mod_launch(MDG_F32, M, C, x, mods, c.W, L, 0, C, 1e-6f, F(c.xn), s), "ln_mod"))
+        return e;
+      mdg_gemm_desc q = g;
+      q.epi = MDG_EPI_QKV;
+      q.M = M; q.N = 3 * C; q.K = C; q.A = F(c.xn); q.lda = C; q.W = w.wqkv; q.ldw = C; q.bias = w.bqkv;
+      q.H = H; q.D = D; q.T = 1; q.L = L; q.rope = m->rope_l; q.rope_rows = L + 1;
+      if (long_l) {
+        q.qkv_layout = MDG_QKV_TEMPORAL; q.qkv_out = F(c.qkv); q.qscale = qs * 1.4426950408889634f;
+        q.T = L; q.L = 1;
+        if (int e = mdg_gemm(&q, stream)) return e;
+        if (int e = mdg_attn_temporal(MDG_F32, c.R, L, 1, H, D, F(c.qkv), F(c.kb_s), w.kvb, F(c.o), stream)) return e;
+      } else {
+        q.qkv_layout = MDG_QKV_SPATIAL; q.qkv_out = F(c.qkv); q.qscale = qs;
+        if (int e = mdg_gemm(&q, stream)) return e;
+        if (int e = mdg_attn_spatial(MDG_F32, c.R, L, H, D, F(c.qkv), w.kvb, F(c.mrep), F(c.o), stream)) return e;
+      }
+      mdg_gemm_desc r = g;
+      r.epi = MDG_EPI_GATE_RES;
+      r.M = M; r.N = C; r.K = C; r.A = F(c.o); r.lda = C; r.W = w.wo; r.ldw = C; r.bias = w.bo;
+      r.resid = x; r.ldr = C; r.gate = mods; r.gate_off = 2 * C; r.mod_stride = c.W; r.rows_per_mod = L;
+      if (int e = mdg_gemm(&r, stream)) return e;
+      // x += gate_m * fc2(gelu(fc1(modulate(LN x, shift_m, scale_m))))
+      if (int e = hip_check(mdg::ln_mod_launch(MDG_F32, M, C, x, mods, c.W, L, 3 * C, 4 * C, 1e-6f, F(c.xn), s),
+                            "ln_mod"))
+        return e;
+      mdg_gemm_desc f1 = g;
+      f1.epi = MDG_EPI_STORE; f1.act = MDG_ACT_GELU;
+      f1.M = M; f1.N = 4 * C; f1.K = C; f1.A = F(c.xn); f1.lda = C; f1.W = w.w1; f1.ldw = C; f1.bias = w.b1;
+      f1.out = F(c.hid); f1.ldo = 4 * C;
+      if (int e = mdg_gemm(&f1, stream)) return e;
+      mdg_gemm_desc f2 = r;
+      f2.K = 4 * C; f2.A = F(c.hid); f2.lda = 4 * C; f2.W = w.w2; f2.ldw = 4 * C; f2.bias = w.b2; f2.gate_off = 5 * C;
+      if (int e = mdg_gemm(&f2, stream)) return e;
+    }
+  }
+  if (d.tps)  // x_r + x_f (latent_model.py:211)
+    if (int e = hip_check(mdg::add_inplace_launch((size_t)M * C, io->ipa, F(c.x2), s), "ipa add")) return e;
+  return MDG_OK;
 }
 
 }  // extern "C"

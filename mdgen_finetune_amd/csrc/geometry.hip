@@ -278,4 +278,36 @@ hipError_t latents_to_atom14_launch(int B, int T, int L, int lat, int tors_off, 
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------------------
+// TPS relative frames (latent_model.py:197-199): per residue (b, l) the 7-vectors of
+// start^-1 o end and end^-1 o start (Rigid.invert / compose / to_tensor_7), quaternion by the
+// same dominant-eigenvector construction as prep_latents, sign fixed to w >= 0 (LAPACK's
+// eigh leaves it arbitrary; the reference passes it on unfixed).
+__global__ void tps_rel7_kernel(int BL, const float* __restrict__ rots, const float* __restrict__ trans,
+                                const float* __restrict__ erots, const float* __restrict__ etrans,
+                                float* __restrict__ out) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= BL) return;
+  const Rig a = load_rig(rots, trans, n), e = load_rig(erots, etrans, n);
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const Rig o = k == 0 ? rel(a, e) : rel(e, a);
+    float q[4];
+    rot_to_quat_dev(o.r, q);
+    const float sg = q[0] < 0.f ? -1.f : 1.f;
+    float* row = out + ((size_t)k * BL + n) * 7;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) row[i] = q[i] * sg;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) row[4 + i] = o.t[i];
+  }
+}
+
+hipError_t tps_rel7_launch(int B, int L, const float* rots, const float* trans, const float* erots,
+                           const float* etrans, float* out, hipStream_t s) {
+  const int BL = B * L;
+  hipLaunchKernelGGL(tps_rel7_kernel, dim3((BL + 127) / 128), dim3(128), 0, s, BL, rots, trans, erots, etrans, out);
+  return hipGetLastError();
+}
+
 }  // namespace mdg

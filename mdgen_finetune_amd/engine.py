@@ -13,9 +13,10 @@ Responsibilities
     (Sampler.sample_ode('euler'), transport.py:407-450 + integrators.py:95-114), optionally
     captured with the conditioning precompute into ONE hipGraph and replayed.
 
-The conditioning precompute currently uses eager PyTorch ops on the GPU (t-embedding MLP,
-the adaLN GEMVs, the 5 IPA layers on B*L tokens: < 0.5% of a window's FLOPs); every
-token-wise op of the 49 denoising steps runs in libmdgen_hip.so.
+The conditioning precompute runs in libmdgen_hip.so too (mdg_precompute_cond: t-embedding
+MLP, one stacked adaLN GEMM, the IPA layers on S*B*L residue tokens with the TPS relative
+frames computed on the device; fp32 throughout, < 1 % of a window's time), so a window's
+hipGraph holds no PyTorch kernels besides input staging.
 """
 from __future__ import annotations
 
@@ -65,6 +66,7 @@ class HipEngine:
         self._states = {}
         self._graphs = {}
         self._lane_streams = []
+        self._rel7 = None  # TPS relative 7-vectors staged by _prepare_tps (None: computed on the device)
         # concurrent sub-batch chains per Euler window (MDG_LANES, default 1 = one chain)
         # concurrent sub-batch chains per window; 0 = auto: 2 lanes once a window has >= 8
         # trajectories (even count) — measured best at B = 16, bit-identical to 1
@@ -117,10 +119,99 @@ class HipEngine:
             P["w_final"] = wf.to(ct).contiguous()
             P["b_final"] = bf
             P["inv_freq"] = m.layers[0].mha_l.attn.rot_emb.inv_freq if self.rope else None
+            P["cond"] = self._pack_cond(perm)
         self._packed, self._pack_key = P, key
         self._states.clear()
         self._graphs.clear()
         return P
+
+    def _pack_cond(self, perm):
+        """fp32 operands of mdg_precompute_cond (mdg_cond_model): the t-embedder MLP, every
+        adaLN Linear stacked [layers 9C | final 2C | IPA layers 6C][C], and per IPA layer the
+        fused q | kv | q_points | kv_points projection (rows padded to 32), linear_out (columns
+        padded to 64), the mha_l q|k|v in the pair-interleaved RoPE order, out_proj, fc1, fc2."""
+        m = self.model
+        f = lambda t: t.detach().float().contiguous()  # noqa: E731
+        te = m.t_embedder
+        cp = {"t_freqs": f(te.freqs), "t_w0": f(te.mlp[0].weight), "t_b0": f(te.mlp[0].bias),
+              "t_w2": f(te.mlp[2].weight), "t_b2": f(te.mlp[2].bias)}
+        ada = [l.adaLN_modulation[1] for l in m.layers] + [m.emb_to_latent.adaLN_modulation[1]]
+        ipa_layers = list(m.ipa_layers) if m.args.prepend_ipa else []
+        ada += [l.adaLN_modulation[1] for l in ipa_layers]
+        cp["ada_w"] = f(torch.cat([a.weight for a in ada]))
+        cp["ada_b"] = f(torch.cat([a.bias for a in ada]))
+        cp["aa_emb"] = f(m.aatype_to_emb.weight) if hasattr(m, "aatype_to_emb") else None
+        if m.tps:
+            cp["l2e_f_w"], cp["l2e_f_b"] = f(m.latent_to_emb_f.weight), f(m.latent_to_emb_f.bias)
+            cp["l2e_r_w"], cp["l2e_r_b"] = f(m.latent_to_emb_r.weight), f(m.latent_to_emb_r.bias)
+        cp["ipa"] = []
+        for layer in ipa_layers:
+            ipa = layer.ipa
+            w = torch.cat([ipa.linear_q.weight, ipa.linear_kv.weight, ipa.linear_q_points.weight,
+                           ipa.linear_kv_points.weight])
+            b = torch.cat([ipa.linear_q.bias, ipa.linear_kv.bias, ipa.linear_q_points.bias, ipa.linear_kv_points.bias])
+            pp = (w.shape[0] + 31) // 32 * 32
+            wp = torch.zeros(pp, self.C, device=w.device)
+            wp[: w.shape[0]] = w
+            bp = torch.zeros(pp, device=w.device)
+            bp[: b.shape[0]] = b
+            ko = ipa.linear_out.weight.shape[1]
+            wo = torch.zeros(self.C, (ko + 63) // 64 * 64, device=w.device)
+            wo[:, :ko] = ipa.linear_out.weight
+            mha = layer.mha_l.attn
+            wq, wk, bq, bk = mha.q_proj.weight, mha.k_proj.weight, mha.q_proj.bias, mha.k_proj.bias
+            if perm is not None:
+                wq, wk, bq, bk = wq[perm], wk[perm], bq[perm], bk[perm]
+            cp["ipa"].append({
+                "ln_w": f(layer.ipa_norm.weight), "ln_b": f(layer.ipa_norm.bias), "w_proj": f(wp), "b_proj": f(bp),
+                "head_weights": f(ipa.head_weights), "w_out": f(wo), "b_out": f(ipa.linear_out.bias),
+                "wqkv": f(torch.cat([wq, wk, mha.v_proj.weight])), "bqkv": f(torch.cat([bq, bk, mha.v_proj.bias])),
+                "bias_k": f(mha.bias_k.reshape(-1)), "bias_v": f(mha.bias_v.reshape(-1)),
+                "wo": f(mha.out_proj.weight), "bo": f(mha.out_proj.bias), "w1": f(layer.fc1.weight),
+                "b1": f(layer.fc1.bias), "w2": f(layer.fc2.weight), "b2": f(layer.fc2.bias)})
+        return cp
+
+    def _cond_state(self, S, B, L):
+        """Workspace, rope / bias-kv rows and the mdg_cond_model struct for (S, B, L)."""
+        P = self._pack()
+        key = ("cond", S, B, L)
+        cs = self._states.get(key)
+        if cs is not None:
+            return cs
+        m, dev, cp = self.model, self.model.device, P["cond"]
+        a = m.args
+        cs = _ShapeState()
+        has_ipa = bool(a.prepend_ipa)
+        dims = _lib.MdgCondDims(S=S, B=B, L=L, C=self.C, H=self.H, D=self.D, num_layers=self.nl,
+                                ipa_layers=len(cp["ipa"]), ipa_heads=a.ipa_heads if has_ipa else 0,
+                                ipa_c=a.ipa_head_dim if has_ipa else 0, ipa_qk=a.ipa_qk if has_ipa else 0,
+                                ipa_v=a.ipa_v if has_ipa else 0, tps=1 if m.tps else 0,
+                                freq_dim=m.t_embedder.frequency_embedding_size)
+        nbytes = self.lib.mdg_cond_workspace_bytes(ctypes.byref(dims))
+        if nbytes == 0:
+            _lib.check(1001, f"conditioning workspace for S={S} B={B} L={L}")
+        cs.ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        cs.rope_l = self._rope_table(L + 1) if self.rope else None
+        cm = _lib.MdgCondModel()
+        cm.dims = dims
+        cm.time_multiplier = float(a.time_multiplier)
+        for k in ("t_freqs", "t_w0", "t_b0", "t_w2", "t_b2", "ada_w", "ada_b", "aa_emb", "l2e_f_w", "l2e_f_b",
+                  "l2e_r_w", "l2e_r_b"):
+            setattr(cm, k, _lib.ptr(cp.get(k)))
+        cm.rope_l = _lib.ptr(cs.rope_l)
+        cs.kvb = []
+        for i, d in enumerate(cp["ipa"]):
+            kvb = self._kvb(d["bias_k"], d["bias_v"], L, cs.rope_l, L + 1)
+            cs.kvb.append(kvb)
+            lw = cm.ipa[i]
+            for k in ("ln_w", "ln_b", "w_proj", "b_proj", "head_weights", "w_out", "b_out", "wqkv", "bqkv", "wo", "bo",
+                      "w1", "b1", "w2", "b2"):
+                setattr(lw, k, d[k].data_ptr())
+            lw.kvb = kvb.data_ptr()
+        cs.model_struct = cm
+        cs.S, cs.B, cs.L = S, B, L
+        self._states[key] = cs
+        return cs
 
     def _pair_perm(self):
         """Row permutation of a [C] q/k projection: within each head, new row 2i = dim i and
@@ -214,63 +305,46 @@ class HipEngine:
 
     # ------------------------------------------------------------------ conditioning
     def conditioning(self, t_sb, mask, rots, trans, erots, etrans, aatype):
-        """x-independent conditioning for S time points at once.
-        t_sb [S, B] -> mods [S][nl][B][9C], mods_final [S][B][2C], ipa [S][B][L][C] (or None)."""
+        """x-independent conditioning for S time points at once (mdg_precompute_cond).
+        t_sb [S, B] -> mods [S][nl][B][9C], mods_final [S][B][2C], ipa [S][B][L][C] (or None).
+        mask is the [B, T, L] token mask: its frame-0 rows are the IPA frame mask, read in place."""
         m = self.model
         S, B = t_sb.shape
-        C = self.C
-        c = m.embed_time(t_sb.reshape(-1))                                    # [S*B, C]
-        sc = F.silu(c)
-        mods = torch.stack([F.linear(sc, l.adaLN_modulation[1].weight, l.adaLN_modulation[1].bias)
-                            for l in m.layers], 1)                             # [S*B, nl, 9C]
-        mods = mods.reshape(S, B, self.nl, 9 * C).permute(0, 2, 1, 3).contiguous()
-        fl = m.emb_to_latent.adaLN_modulation[1]
-        mods_f = F.linear(sc, fl.weight, fl.bias).reshape(S, B, 2 * C).contiguous()
-        ipa = None
-        if m.args.prepend_ipa:
-            L = mask.shape[-1]
-            mask_b = mask[:, 0].repeat(S, 1)                                  # [S*B, L]
-            rep = lambda z: None if z is None else z.repeat(S, *([1] * (z.dim() - 1)))  # noqa: E731
-            aa = rep(aatype)
-            ipa = self._run_ipa(c, mask_b, rep(rots), rep(trans), rep(erots), rep(etrans), aa)
-            ipa = ipa.reshape(S, B, L, C).contiguous()
+        C, L, T = self.C, mask.shape[-1], mask.shape[-2]
+        cs = self._cond_state(S, B, L)
+        dev = t_sb.device
+        mods = torch.empty(S, self.nl, B, 9 * C, device=dev)
+        mods_f = torch.empty(S, B, 2 * C, device=dev)
+        ipa = torch.empty(S, B, L, C, device=dev) if m.args.prepend_ipa else None
+        io = _lib.MdgCondIO()
+        tt = t_sb if (t_sb.dtype == torch.float32 and t_sb.is_contiguous()) else t_sb.float().contiguous()
+        io.t, io.mask, io.mask_stride = tt.data_ptr(), mask.data_ptr(), T * L
+        io.rots, io.trans = _lib.ptr(rots), _lib.ptr(trans)
+        io.end_rots, io.end_trans = _lib.ptr(erots), _lib.ptr(etrans)
+        io.rel7 = _lib.ptr(self._rel7)
+        io.aatype = _lib.ptr(aatype) if hasattr(m, "aatype_to_emb") else None
+        io.mods, io.mods_final, io.ipa = mods.data_ptr(), mods_f.data_ptr(), _lib.ptr(ipa)
+        cs.keep = (tt, mask, rots, trans, erots, etrans, aatype, self._rel7)
+        _lib.check(self.lib.mdg_precompute_cond(ctypes.byref(cs.model_struct), ctypes.byref(io), cs.ws.data_ptr(),
+                                                _lib.stream_handle()), "mdg_precompute_cond")
         return mods, mods_f, ipa
 
-    def _run_ipa(self, c, mask_b, rots, trans, erots, etrans, aatype):
-        m = self.model
-        B, L = mask_b.shape
-        use_aa = aatype is not None and hasattr(m, "aatype_to_emb")
-        if not m.tps:
-            x = torch.zeros(B, L, self.C, device=mask_b.device)
-            if use_aa:
-                x = x + m.aatype_to_emb(aatype)
-            for layer in m.ipa_layers:
-                x = layer(x, c, mask_b, rots, trans)
-            return x
-        x_f = m.latent_to_emb_f(self._rel7[0].repeat(B // self._rel7[0].shape[0], 1, 1))
-        x_r = m.latent_to_emb_r(self._rel7[1].repeat(B // self._rel7[1].shape[0], 1, 1))
-        if use_aa:
-            x_f = x_f + m.aatype_to_emb(aatype)
-            x_r = x_r + m.aatype_to_emb(aatype)
-        for layer in m.ipa_layers:
-            x_r = layer(x_r, c, mask_b, rots, trans)
-            x_f = layer(x_f, c, mask_b, erots, etrans)
-        return x_r + x_f
-
     def _prepare_tps(self, rots, trans, erots, etrans):
-        # relative frames use an eigen-solve on the host (rot_to_quat); done once per window,
-        # outside any captured graph.
+        """TPS relative 7-vectors: None = computed on the device inside mdg_precompute_cond
+        (quaternion sign w >= 0).  ``rel7_override`` (tests: the reference's own vectors, whose
+        eigenvector sign LAPACK chose) or MDG_TPS_REL7=host (the reference's host arithmetic,
+        rot_to_quat by CPU eigh) instead stage a [2][B][L][7] tensor outside any graph."""
         from .model.latent_model import relative_tensor7
 
-        if self.model.tps:
-            ov = getattr(self, "rel7_override", None)
-            if ov is not None:  # test hook: inject the reference's own 7-vectors (eigh sign)
-                self._rel7 = tuple(t.to(rots.device, torch.float32) for t in ov)
-            else:
-                self._rel7 = (relative_tensor7(rots, trans, erots, etrans),
-                              relative_tensor7(erots, etrans, rots, trans))
-        else:
-            self._rel7 = None
+        self._rel7 = None
+        if not self.model.tps:
+            return
+        ov = getattr(self, "rel7_override", None)
+        if ov is not None:
+            self._rel7 = torch.stack([t.to(rots.device, torch.float32) for t in ov]).contiguous()
+        elif os.environ.get("MDG_TPS_REL7") == "host":
+            self._rel7 = torch.stack([relative_tensor7(rots, trans, erots, etrans),
+                                      relative_tensor7(erots, etrans, rots, trans)]).contiguous()
 
     def _base(self, st, x_cond, x_cond_mask):
         """Step-invariant embedding: cond_to_emb(x_cond) + mask_to_emb + pos_embed + both biases
@@ -303,11 +377,12 @@ class HipEngine:
         if self.model.args.abs_pos_emb and L != self.model.args.crop:
             raise ValueError(f"abs_pos_emb needs L == crop ({L} vs {self.model.args.crop})")
         mask = mask.to(x.device, torch.float32).contiguous()
-        rots, trans = frames_to_tensors(start_frames, x.device)
-        erots, etrans = frames_to_tensors(end_frames, x.device) if self.model.tps else (None, None)
+        cont = lambda z: None if z is None else z.contiguous()  # noqa: E731  (the C ABI reads [B][L][...] rows)
+        rots, trans = map(cont, frames_to_tensors(start_frames, x.device))
+        erots, etrans = map(cont, frames_to_tensors(end_frames, x.device)) if self.model.tps else (None, None)
         if self.model.args.prepend_ipa and rots is None:
             raise ValueError("prepend_ipa needs start_frames")
-        aa = None if aatype is None else aatype.to(x.device)
+        aa = None if aatype is None else aatype.to(x.device, torch.int64).contiguous()
         return B, T, L, mask, rots, trans, erots, etrans, aa
 
     def _step_io(self, st, x_in, x_out, v_out, ipa, mods, mods_f, dt, base=None):
@@ -360,10 +435,8 @@ class HipEngine:
         self._copy_opt(gs, "erots", erots)
         self._copy_opt(gs, "etrans", etrans)
         self._copy_opt(gs, "aatype", aa)
-        if self._rel7 is not None:  # TPS relative frames: static copies the graph reads
-            self._copy_opt(gs, "rel7f", self._rel7[0])
-            self._copy_opt(gs, "rel7r", self._rel7[1])
-            self._rel7 = (gs.rel7f, gs.rel7r)
+        self._copy_opt(gs, "rel7", self._rel7)  # TPS relative frames staged on the host path only
+        self._rel7 = gs.rel7
         gs.has_cond = x_cond is not None
         if gs.has_cond:
             self._copy_opt(gs, "x_cond", x_cond.float())
@@ -397,12 +470,7 @@ class HipEngine:
         vs.graph = None
         for name, val in (("rots", rots), ("trans", trans), ("erots", erots), ("etrans", etrans), ("aatype", aa)):
             self._copy_opt(vs, name, val)
-        if self._rel7 is not None:
-            self._copy_opt(vs, "rel7f", self._rel7[0])
-            self._copy_opt(vs, "rel7r", self._rel7[1])
-            vs.rel7 = (vs.rel7f, vs.rel7r)
-        else:
-            vs.rel7 = None
+        self._copy_opt(vs, "rel7", self._rel7)
         vs.has_cond = x_cond is not None
         if vs.has_cond:
             self._copy_opt(vs, "x_cond", x_cond.float())

@@ -134,10 +134,13 @@ def test_sim_rollout_three_windows_hip_matches_cpu_eager(tmp_path):
         assert et <= 1e-4 and er <= 1e-4 and etor <= 1e-4, (k, et, er, etor)
 
 
-def test_tps_inference_batch_hip_matches_cpu_eager(tmp_path):
+def test_tps_inference_batch_hip_matches_cpu_eager(tmp_path, monkeypatch):
     """tps_inference.py:119-131: a batch of transition-path windows (frames 0 and T-1
     conditioned, latent 28) on HIP (f32) vs eager CPU with identical noise and start / end
-    frames built once on the CPU."""
+    frames built once on the CPU.  The HIP engine takes the relative frames' quaternion sign
+    from the host eigen-solve here (MDG_TPS_REL7=host), as the eager CPU path does; its default
+    device frames fix the sign to w >= 0 (tests/test_gpu_cond.py)."""
+    monkeypatch.setenv("MDG_TPS_REL7", "host")
     outs = _rollout_both(tmp_path, tps=True, n_windows=1)
     err = (outs["cuda"][0] - outs["cpu"][0]).abs().max().item()
     assert err <= 2e-3, err

@@ -63,9 +63,23 @@ def _log_err(dtype, solve, out, ref):
         f.write(json.dumps(rec) + "\n")
 
 
-def _check(out, ref, dtype, solve=False):
+# Padded residues (frame mask 0) are ill-conditioned in the reference itself: their IPA logits
+# are (a + pt) - 1e5 for EVERY key (ipa.py:192-205), rounded to ulp(1e5) = 7.8e-3 in fp32, so
+# any implementation whose a + pt differs by one ulp lands on a neighbouring multiple and moves
+# those rows' softmax weights by up to ~1 %.  Their outputs are masked everywhere downstream
+# (loss, geometry); they are compared at PAD_MAX, the valid residues at the f32 bounds.
+PAD_MAX = 1e-2
+
+
+def _check(out, ref, dtype, solve=False, valid=None):
+    """valid: [L] residue mask (1 = real residue) of [B,T,L,...] outputs; padded residues are
+    checked against PAD_MAX (f32) and the valid ones against the normal bounds."""
     out = out.detach().float().cpu().numpy() if torch.is_tensor(out) else out
     assert np.isfinite(out).all()
+    if valid is not None and not valid.all() and dtype == "f32":
+        pad_err = np.abs(out[:, :, ~valid] - ref[:, :, ~valid]).max()
+        assert pad_err <= PAD_MAX, ("padded residues", pad_err)
+        out, ref = out[:, :, valid], ref[:, :, valid]
     _log_err(dtype, solve, out, ref)
     if dtype == "f32":
         assert np.abs(out - ref).max() <= F32_MAX, np.abs(out - ref).max()
@@ -252,7 +266,7 @@ def test_long_residue_axis_atlas_matches_oracle(T, L, n_pad, dtype):
     with torch.no_grad():
         v = m(g("x"), g("t"), g("mask"), start_frames=Rigid(Rotation(rot_mats=g("rots")), g("trans")),
               x_cond=g("x_cond"), x_cond_mask=g("x_cond_mask"), aatype=g("aatype"))
-    _check(v, ref, dtype)
+    _check(v, ref, dtype, valid=inp["mask"][0, 0] > 0)
 
 
 @pytest.mark.parametrize("lanes,offset", [(2, 0), (2, 2), (3, 1)])
@@ -333,6 +347,6 @@ def test_atlas_full_size_T250_crop256_matches_oracle_both_dtypes():
         with torch.no_grad():
             v = m(g("x"), g("t"), g("mask"), start_frames=Rigid(Rotation(rot_mats=g("rots")), g("trans")),
                   x_cond=g("x_cond"), x_cond_mask=g("x_cond_mask"), aatype=g("aatype"))
-        _check(v, ref, dtype)
+        _check(v, ref, dtype, valid=inp["mask"][0, 0] > 0)
         del m
         torch.cuda.empty_cache()

@@ -54,6 +54,9 @@ def test_struct_layouts_match_header():
 int main(void){
  printf("%zu %zu %zu %zu %zu %zu\n", sizeof(mdg_dims), sizeof(mdg_layer_weights), sizeof(mdg_model),
         sizeof(mdg_step_io), sizeof(mdg_gemm_desc), sizeof(mdg_layer_saved));
+ printf("%zu %zu %zu %zu %zu %zu %zu\n", sizeof(mdg_cond_dims), sizeof(mdg_ipa_layer_weights),
+        sizeof(mdg_cond_model), sizeof(mdg_cond_io), offsetof(mdg_cond_model, time_multiplier),
+        offsetof(mdg_cond_model, t_freqs), offsetof(mdg_cond_model, ipa));
  printf("%zu %zu %zu %zu %zu %zu %zu\n", offsetof(mdg_step_io, dt), offsetof(mdg_step_io, h),
         offsetof(mdg_gemm_desc, qscale), offsetof(mdg_gemm_desc, rope_rows), offsetof(mdg_gemm_desc, aux),
         offsetof(mdg_gemm_desc, ldaux), offsetof(mdg_layer_saved, init_planes));
@@ -66,7 +69,12 @@ int main(void){
         subprocess.check_call(["gcc", "-I", os.path.dirname(HEADER), c, "-o", exe])
         out = subprocess.check_output([exe]).decode().split()
     sizes = [int(v) for v in out[:6]]
-    offs = [int(v) for v in out[6:]]
+    cond = [int(v) for v in out[6:13]]
+    offs = [int(v) for v in out[13:]]
+    assert cond == [ctypes.sizeof(_lib.MdgCondDims), ctypes.sizeof(_lib.MdgIpaLayerWeights),
+                    ctypes.sizeof(_lib.MdgCondModel), ctypes.sizeof(_lib.MdgCondIO),
+                    _lib.MdgCondModel.time_multiplier.offset, _lib.MdgCondModel.t_freqs.offset,
+                    _lib.MdgCondModel.ipa.offset]
     assert sizes == [ctypes.sizeof(s) for s in (_lib.MdgDims, _lib.MdgLayerWeights, _lib.MdgModel,
                                                  _lib.MdgStepIO, _lib.MdgGemmDesc, _lib.MdgLayerSaved)]
     assert offs == [_lib.MdgStepIO.dt.offset, _lib.MdgStepIO.h.offset, _lib.MdgGemmDesc.qscale.offset,
