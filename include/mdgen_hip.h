@@ -302,7 +302,10 @@ typedef struct {
   const float* rel7;       /* TPS: [2][B][L][7] (start^-1 o end | end^-1 o start) 7-vectors; null =
                               computed on the device (mdg_tps_rel7) */
   const int64_t* aatype;   /* [B][L] in [0, 21) or null */
-  float* mods;             /* out [S][num_layers][B][9C] */
+  int32_t lanes;           /* 0 / 1: mods [S][num_layers][B][9C]; n > 1 (B % n == 0): lane-major
+                              [n][S][num_layers][B/n][9C], each lane's step rows contiguous (the
+                              engine's concurrent sub-batch chains) */
+  float* mods;             /* out, layout above */
   float* mods_final;       /* out [S][B][2C] */
   float* ipa;              /* out [S][B][L][C] (ignored when ipa_layers == 0) */
 } mdg_cond_io;

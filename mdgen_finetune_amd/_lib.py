@@ -91,7 +91,8 @@ class MdgCondModel(ctypes.Structure):
 
 class MdgCondIO(ctypes.Structure):
     _fields_ = [("t", _vp), ("mask", _vp), ("mask_stride", _i32)] + [
-        (n, _vp) for n in ("rots", "trans", "end_rots", "end_trans", "rel7", "aatype", "mods", "mods_final", "ipa")]
+        (n, _vp) for n in ("rots", "trans", "end_rots", "end_trans", "rel7", "aatype")] + [
+        ("lanes", _i32), ("mods", _vp), ("mods_final", _vp), ("ipa", _vp)]
 
 
 # (name, restype, argtypes) of every exported entry point — the test suite checks that the

@@ -60,8 +60,8 @@ hipError_t attn_spatial_bwd_launch(int dtype, int nf, int L, int H, int D, const
 // cond.hip
 hipError_t temb_freq_launch(int R, int half, float mult, const float* t, const float* freqs, float* out,
                             hipStream_t s);
-hipError_t cond_scatter_launch(int S, int B, int nl, int C, int W, const float* all, float* mods, float* mods_final,
-                               hipStream_t s);
+hipError_t cond_scatter_launch(int S, int B, int nl, int C, int W, int lanes, const float* all, float* mods,
+                               float* mods_final, hipStream_t s);
 hipError_t ipa_init_launch(int R, int B, int L, int C, int mstride, const int64_t* aatype, const float* aa_emb, const float* rel7,
                            const float* w, const float* bias, const float* mask, float* x, float* mask_rep,
                            hipStream_t s);
@@ -847,8 +847,10 @@ int mdg_precompute_cond(const mdg_cond_model* m, const mdg_cond_io* io, void* ws
   ad.M = c.R; ad.N = c.W; ad.K = C; ad.A = F(c.sc); ad.lda = C; ad.W = m->ada_w; ad.ldw = C; ad.bias = m->ada_b;
   ad.out = F(c.all); ad.ldo = c.W;
   if (int e = mdg_gemm(&ad, stream)) return e;
-  if (int e = hip_check(mdg::cond_scatter_launch(d.S, d.B, d.num_layers, C, c.W, F(c.all), io->mods, io->mods_final,
-                                                 s), "cond_scatter"))
+  const int lanes = io->lanes > 1 ? io->lanes : 1;
+  if (d.B % lanes) return fail(MDG_E_SHAPE, "precompute_cond: B=%d not a multiple of lanes=%d", d.B, lanes);
+  if (int e = hip_check(mdg::cond_scatter_launch(d.S, d.B, d.num_layers, C, c.W, lanes, F(c.all), io->mods,
+                                                 io->mods_final, s), "cond_scatter"))
     return e;
   if (d.ipa_layers == 0) return MDG_OK;
 

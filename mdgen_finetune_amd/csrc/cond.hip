@@ -28,8 +28,8 @@ __global__ void temb_freq_kernel(int R, int half, float mult, const float* __res
   out[(size_t)r * 2 * half + half + k] = sinf(arg);
 }
 
-// cond_all [S*B][W] (W = nl*9C + 2C + ...) -> mods [S][nl][B][9C], mods_final [S][B][2C]
-__global__ void cond_scatter_kernel(int S, int B, int nl, int C, int W, const float* __restrict__ all,
+// cond_all [S*B][W] (W = nl*9C + 2C + ...) -> mods [lanes][S][nl][B/lanes][9C], mods_final [S][B][2C]
+__global__ void cond_scatter_kernel(int S, int B, int nl, int C, int W, int lanes, const float* __restrict__ all,
                                     float* __restrict__ mods, float* __restrict__ mods_final) {
   const int per = nl * 9 * C + 2 * C;  // floats copied per row r
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -39,7 +39,8 @@ __global__ void cond_scatter_kernel(int S, int B, int nl, int C, int W, const fl
   const float v = all[(size_t)r * W + k];
   if (k < nl * 9 * C) {
     const int layer = k / (9 * C), j = k - layer * 9 * C;
-    mods[(((size_t)s * nl + layer) * B + b) * 9 * C + j] = v;
+    const int Bl = B / lanes, lane = b / Bl, bl = b - lane * Bl;
+    mods[((((size_t)lane * S + s) * nl + layer) * Bl + bl) * 9 * C + j] = v;
   } else {
     mods_final[(size_t)r * 2 * C + (k - nl * 9 * C)] = v;
   }
@@ -210,11 +211,11 @@ hipError_t temb_freq_launch(int R, int half, float mult, const float* t, const f
   return hipGetLastError();
 }
 
-hipError_t cond_scatter_launch(int S, int B, int nl, int C, int W, const float* all, float* mods, float* mods_final,
-                               hipStream_t s) {
+hipError_t cond_scatter_launch(int S, int B, int nl, int C, int W, int lanes, const float* all, float* mods,
+                               float* mods_final, hipStream_t s) {
   const size_t n = (size_t)S * B * (nl * 9 * C + 2 * C);
-  hipLaunchKernelGGL(cond_scatter_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, S, B, nl, C, W, all,
-                     mods, mods_final);
+  hipLaunchKernelGGL(cond_scatter_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, S, B, nl, C, W, lanes,
+                     all, mods, mods_final);
   return hipGetLastError();
 }
 

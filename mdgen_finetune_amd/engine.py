@@ -304,16 +304,18 @@ class HipEngine:
         return json.loads(buf.value.decode())
 
     # ------------------------------------------------------------------ conditioning
-    def conditioning(self, t_sb, mask, rots, trans, erots, etrans, aatype):
+    def conditioning(self, t_sb, mask, rots, trans, erots, etrans, aatype, lanes=1):
         """x-independent conditioning for S time points at once (mdg_precompute_cond).
-        t_sb [S, B] -> mods [S][nl][B][9C], mods_final [S][B][2C], ipa [S][B][L][C] (or None).
-        mask is the [B, T, L] token mask: its frame-0 rows are the IPA frame mask, read in place."""
+        t_sb [S, B] -> mods [S][nl][B][9C] (lanes > 1: [lanes][S][nl][B/lanes][9C]), mods_final
+        [S][B][2C], ipa [S][B][L][C] (or None).  mask is the [B, T, L] token mask: its frame-0
+        rows are the IPA frame mask, read in place."""
         m = self.model
         S, B = t_sb.shape
         C, L, T = self.C, mask.shape[-1], mask.shape[-2]
         cs = self._cond_state(S, B, L)
         dev = t_sb.device
-        mods = torch.empty(S, self.nl, B, 9 * C, device=dev)
+        mods = (torch.empty(S, self.nl, B, 9 * C, device=dev) if lanes <= 1 else
+                torch.empty(lanes, S, self.nl, B // lanes, 9 * C, device=dev))
         mods_f = torch.empty(S, B, 2 * C, device=dev)
         ipa = torch.empty(S, B, L, C, device=dev) if m.args.prepend_ipa else None
         io = _lib.MdgCondIO()
@@ -323,6 +325,7 @@ class HipEngine:
         io.end_rots, io.end_trans = _lib.ptr(erots), _lib.ptr(etrans)
         io.rel7 = _lib.ptr(self._rel7)
         io.aatype = _lib.ptr(aatype) if hasattr(m, "aatype_to_emb") else None
+        io.lanes = lanes
         io.mods, io.mods_final, io.ipa = mods.data_ptr(), mods_f.data_ptr(), _lib.ptr(ipa)
         cs.keep = (tt, mask, rots, trans, erots, etrans, aatype, self._rel7)
         _lib.check(self.lib.mdg_precompute_cond(ctypes.byref(cs.model_struct), ctypes.byref(io), cs.ws.data_ptr(),
@@ -546,13 +549,13 @@ class HipEngine:
     def _run_sampler(self, gs, st):
         """The whole window: conditioning for all steps, base embedding, mask bias, S steps."""
         s = _lib.stream_handle()
+        nlanes = self._nlanes(st.B)
         mods, mods_f, ipa = self.conditioning(gs.t_sb, gs.mask, gs.rots, gs.trans, getattr(gs, "erots", None),
-                                              getattr(gs, "etrans", None), getattr(gs, "aatype", None))
+                                              getattr(gs, "etrans", None), getattr(gs, "aatype", None), nlanes)
         gs.cond = (mods, mods_f, ipa)  # keep alive (graph-pool memory during capture)
         self._base(st, gs.x_cond if gs.has_cond else None, gs.x_cond_mask if gs.has_cond else None)
         _lib.check(self.lib.mdg_prepare_mask(ctypes.byref(st.dims), gs.mask.data_ptr(), st.ws.data_ptr(), s),
                    "mdg_prepare_mask")
-        nlanes = self._nlanes(st.B)
         if nlanes > 1:
             self._run_lanes(gs, st, mods, mods_f, ipa, nlanes)
             return
@@ -577,8 +580,7 @@ class HipEngine:
         rows = Bl * st.T * st.L
         if len(self._lane_streams) < nlanes:
             self._lane_streams += [torch.cuda.Stream() for _ in range(nlanes - len(self._lane_streams))]
-        lane_mods = [mods[:, :, k * Bl:(k + 1) * Bl].contiguous() for k in range(nlanes)]  # [S][nl][Bl][9C]
-        gs.lane_keep = lane_mods
+        lane_mods = mods  # lane-major [nlanes][S][nl][Bl][9C] straight from mdg_precompute_cond
         gs.ios = []
         # phase offset: lane k starts once lane k-1 is `lane_offset` layers into its first step,
         # so the lanes' identical kernel sequences run out of step (one lane's HBM-bound row-LN
