@@ -932,6 +932,125 @@ __global__ __launch_bounds__(kRowThreads, BM == 64 ? 4 : 1) void gemm_rowln_kern
 #pragma unroll
   for (int e = 0; e < NE; ++e)
     bb[e] = p.bias ? *reinterpret_cast<const float2*>(p.bias + 2 * lane + 128 * e) : make_float2(0.f, 0.f);
+  // The adaLN rows the epilogue needs (gate; the next LayerNorm's scale and shift) of the <= 2
+  // trajectory entries a 128-row tile spans go to LDS once, and the per-row loop reads them
+  // with ds_read.  (Per-row global loads in exec-masked branches -- the rare row of the next
+  // trajectory -- made the compiler drain every outstanding store and prefetch with
+  // s_waitcnt vmcnt(0) on every row.)  The band barriers are raw s_barrier after an LDS wait:
+  // they order the stage buffer only, so the h / xn stores stay in flight across them.
+  int b_lo = 0, b_hi = 0;
+  if (BM == 128) {
+    b_lo = fdiv(m0, p.rows_per_mod, inv_rpm);
+    b_hi = fdiv(min(m0 + BM - 1, M - 1), p.rows_per_mod, inv_rpm);
+  }
+  if (BM == 128 && b_hi - b_lo < 2) {
+    float* emods = stage + 32 * LDS_ST;  // [2][3][NCOL]: gate | xn scale | xn shift
+    static_assert(BM != 128 || (32 * LDS_ST + 6 * NCOL) * 4 <= kRowStages * STAGE * 2, "adaLN rows fit the ring");
+    __builtin_amdgcn_s_barrier();  // every wave is done reading the ring (its loads were all waited)
+    for (int i = tid; i < 6 * NCOL; i += kRowThreads) {
+      const int eb = i / (3 * NCOL), w = (i / NCOL) % 3, k = i % NCOL;
+      const size_t b = (size_t)min(b_lo + eb, b_hi);
+      float v;
+      if (w == 0) v = p.gate ? p.gate[b * p.mod_stride + p.gate_off + k] : 1.0f;
+      else if (w == 1) v = p.xn_out ? p.xn_mods[b * p.xn_mod_stride + p.xn_scale_off + k] : 0.0f;
+      else v = p.xn_out ? p.xn_mods[b * p.xn_mod_stride + p.xn_shift_off + k] : 0.0f;
+      emods[i] = v;
+    }
+    // h rows of unit 0 were loaded before the K loop (with its gate row, unused here)
+#pragma unroll 1
+    for (int band = 0; band < BM / 32; ++band) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // previous band's stage reads (and the adaLN rows) are done
+      if (wm == (band >> 1)) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          if ((i >> 1) != (band & 1)) continue;
+#pragma unroll
+          for (int j = 0; j < NT; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              stage[((i & 1) * 16 + lg * 4 + r) * LDS_ST + wn * WTN + j * 16 + lr] = acc[i][j][r];
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+#pragma unroll 1
+      for (int g0 = 0; g0 < 4; g0 += RG) {
+        const int u = band * UPB + g0 / RG;
+        float2 hn[RG][NE], gn[NE];
+        if (u + 1 < NU) load_unit(u + 1, hn, gn);
+        float sum[RG];
+        int eb[RG];
+#pragma unroll
+        for (int rr = 0; rr < RG; ++rr) {
+          const int m = m0 + band * 32 + wave * 4 + g0 + rr;
+          eb[rr] = fdiv(min(m, M - 1), p.rows_per_mod, inv_rpm) - b_lo;
+          const float* srow = stage + (wave * 4 + g0 + rr) * LDS_ST;
+          const float* gr = emods + eb[rr] * 3 * NCOL;
+          float s = 0.f;
+#pragma unroll
+          for (int e = 0; e < NE; ++e) {
+            const int k = 2 * lane + 128 * e;
+            const float2 v = *reinterpret_cast<const float2*>(srow + k);
+            const float2 g2 = *reinterpret_cast<const float2*>(gr + k);
+            hv[rr][e].x += g2.x * (v.x + bb[e].x);
+            hv[rr][e].y += g2.y * (v.y + bb[e].y);
+            s += hv[rr][e].x + hv[rr][e].y;
+          }
+          sum[rr] = s;
+          if (m < M) {
+#pragma unroll
+            for (int e = 0; e < NE; ++e)
+              *reinterpret_cast<float2*>(p.resid + (size_t)m * p.ldr + 2 * lane + 128 * e) = hv[rr][e];
+          }
+        }
+        if (p.xn_out) {
+#pragma unroll
+          for (int o = 32; o >= 1; o >>= 1)
+#pragma unroll
+            for (int rr = 0; rr < RG; ++rr) sum[rr] += __shfl_xor(sum[rr], o, 64);
+          float ss[RG];
+#pragma unroll
+          for (int rr = 0; rr < RG; ++rr) {
+            sum[rr] *= invN;  // mean
+            float t = 0.f;
+#pragma unroll
+            for (int e = 0; e < NE; ++e) {
+              const float a0 = hv[rr][e].x - sum[rr], a1 = hv[rr][e].y - sum[rr];
+              t += a0 * a0 + a1 * a1;
+            }
+            ss[rr] = t;
+          }
+#pragma unroll
+          for (int o = 32; o >= 1; o >>= 1)
+#pragma unroll
+            for (int rr = 0; rr < RG; ++rr) ss[rr] += __shfl_xor(ss[rr], o, 64);
+#pragma unroll
+          for (int rr = 0; rr < RG; ++rr) {
+            const int m = m0 + band * 32 + wave * 4 + g0 + rr;
+            const float rs = 1.0f / sqrtf(ss[rr] * invN + p.ln_eps);
+            const float* mr = emods + eb[rr] * 3 * NCOL;
+#pragma unroll
+            for (int e = 0; e < NE; ++e) {
+              const int k = 2 * lane + 128 * e;
+              const float2 xs = *reinterpret_cast<const float2*>(mr + NCOL + k);
+              const float2 xh = *reinterpret_cast<const float2*>(mr + 2 * NCOL + k);
+              typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+              bf16x2 pr;
+              pr[0] = (bf16_t)((hv[rr][e].x - sum[rr]) * rs * (1.0f + xs.x) + xh.x);
+              pr[1] = (bf16_t)((hv[rr][e].y - sum[rr]) * rs * (1.0f + xs.y) + xh.y);
+              if (m < M) *reinterpret_cast<bf16x2*>(reinterpret_cast<bf16_t*>(p.xn_out) + (size_t)m * NCOL + k) = pr;
+            }
+          }
+        }
+#pragma unroll
+        for (int e = 0; e < NE; ++e)
+#pragma unroll
+          for (int rr = 0; rr < RG; ++rr) hv[rr][e] = hn[rr][e];
+      }
+    }
+    return;
+  }
   __syncthreads();  // all waves are done with the ring
 #pragma unroll 1
   for (int band = 0; band < BM / 32; ++band) {

@@ -89,7 +89,8 @@ def test_gemm_lnmod_gate_res(lib, dt):
     torch.testing.assert_close(resid, ref, rtol=rtol, atol=atol * 10)
 
 
-@pytest.mark.parametrize("N,K,M", [(384, 384, 300), (384, 1536, 4000), (128, 256, 257), (512, 512, 130)])
+@pytest.mark.parametrize("N,K,M", [(384, 384, 300), (384, 1536, 4000), (128, 256, 257), (512, 512, 130),
+                                   (384, 64, 200), (256, 128, 129), (384, 192, 1000)])
 def test_gemm_gate_res_fused_layernorm(lib, N, K, M):
     """bf16 full-row gated residual + next-LN epilogue (gemm_rowln_kernel): h and xn vs torch."""
     from mdgen_finetune_amd import _lib

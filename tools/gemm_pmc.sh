@@ -1,13 +1,18 @@
 #!/bin/bash
-# SQ counter pass over one GEMM shape for both tile variants (counters only, no tracing).
+# SQ / TA counter passes over the GEMM microbench (tools/gemm_bench.py MODE): where the main
+# loop's cycles go (MFMA busy, waits, issue stalls, VMEM / LDS instruction counts).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-mkdir -p gpurun_out/pmc
-SHAPE="${SHAPE:-32000 1536 384 0 0}"
-for T in 128 256; do
-  MDG_GEMM_TILE=$T timeout -k 10 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
-    SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES \
-    --output-format csv -d gpurun_out/pmc -o sq_$T -- python tools/gemm_one.py $SHAPE > gpurun_out/pmc/log_$T.txt 2>&1 || exit $?
+mkdir -p gpurun_out/pmc_gemm
+MODE=${1:-b4}
+timeout -k 10 60 rocprofv3 -L > gpurun_out/pmc_gemm/counters.txt 2>&1 || true
+i=0
+for C in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VMEM SQ_INSTS_LDS" \
+         "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_MFMA SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE GRBM_COUNT" \
+         "TA_TA_BUSY_sum TA_BUFFER_WAVEFRONTS_sum TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum"; do
+  i=$((i+1))
+  timeout -s KILL 90 rocprofv3 --pmc $C --kernel-include-regex "gemm_" --output-format csv \
+    -d gpurun_out/pmc_gemm -o p$i -- python tools/gemm_bench.py $MODE > gpurun_out/pmc_gemm/log_$i.txt 2>&1 || echo "pass $i rc=$?"
 done
 echo done
