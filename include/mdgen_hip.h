@@ -36,7 +36,10 @@ extern "C" {
 
 #define MDG_ABI_VERSION 11
 #define MDG_MAX_LAYERS 16
-#define MDG_DP 32 /* padded head dim of every attention operand buffer (head_dim <= 31) */
+#define MDG_DP 32      /* padded head dim of the attention operand buffers for head_dim <= 31 */
+#define MDG_DP_WIDE 64 /* ... and for 32 <= head_dim <= 63 (column head_dim of the padded k / v rows
+                          carries the softmax offset / row sum, so it must exist) */
+#define MDG_HEAD_STRIDE(D) ((D) < MDG_DP ? MDG_DP : MDG_DP_WIDE)
 
 typedef enum { MDG_F32 = 0, MDG_BF16 = 1 } mdg_dtype;
 
@@ -68,7 +71,7 @@ typedef struct {
   const float* bqkv[2]; /* [3C], same row order */
   const void* wo[2];    /* CT [C][C] out_proj */
   const float* bo[2];   /* [C] */
-  const float* kvb[2];  /* [H][2][32]: bias_k RoPE-rotated at position S (=L or T) in the
+  const float* kvb[2];  /* [H][2][MDG_HEAD_STRIDE(D)]: bias_k RoPE-rotated at position S (=L or T) in the
                            interleaved order, bias_v natural order with bias_v[D] = 1 (the
                            softmax row sum rides in the pad column) */
   const void* w1;       /* CT [F][C] fc1 */
@@ -196,8 +199,9 @@ int mdg_gemm(const mdg_gemm_desc* g, void* stream);
 int mdg_attn_spatial(int32_t dtype, int32_t n_frames, int32_t L, int32_t H, int32_t D,
                      const void* qkv, const float* kvb, const float* mask, void* out,
                      void* stream);
-/* qkv_t: CT [3][B*L][H][T][32] (q | k | v planes), head dim in columns < D, k and v rows
-   with 1.0 in pad column D (mdg_workspace_init sets it), other pad columns 0. */
+/* qkv_t: CT [3][B*L][H][T][MDG_HEAD_STRIDE(D)] (q | k | v planes), head dim in columns < D,
+   k and v rows with 1.0 in pad column D (mdg_workspace_init sets it), other pad columns 0.
+   head_dim <= 31 runs the 32x32x16 bf16 kernel; 32..63 the generic 16x16 MFMA kernel. */
 int mdg_attn_temporal(int32_t dtype, int32_t B, int32_t T, int32_t L, int32_t H, int32_t D,
                       const void* qkv_t, const float* kbias, const float* kvb, void* out,
                       void* stream);

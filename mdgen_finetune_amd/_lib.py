@@ -23,6 +23,12 @@ MDG_QKV_SPATIAL, MDG_QKV_TEMPORAL = 0, 1
 MDG_PREP_TPS, MDG_PREP_NO_OFFSETS, MDG_PREP_COND_FIRST, MDG_PREP_COND_LAST = 1, 2, 4, 8
 MDG_MAX_LAYERS = 16
 MDG_DP = 32
+MDG_DP_WIDE = 64
+
+
+def head_stride(D: int) -> int:
+    """Row stride of the padded attention operands for head dim D (MDG_HEAD_STRIDE)."""
+    return MDG_DP if D < MDG_DP else MDG_DP_WIDE
 
 _vp = ctypes.c_void_p
 _i32 = ctypes.c_int32

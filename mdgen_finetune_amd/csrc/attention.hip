@@ -27,13 +27,16 @@
 namespace mdg {
 
 
-template <typename CT>
+// DP = padded head dim (MDG_DP for head_dim <= 31, MDG_DP_WIDE up to 63): the QK product runs
+// DP / 32 K-steps and O^T has DP / 16 row tiles.
+template <typename CT, int DP>
 __global__ __launch_bounds__(256) void attn_temporal_kernel(const CT* __restrict__ qkv,
                                                             const float* __restrict__ kbias,
                                                             const float* __restrict__ kvb,
                                                             CT* __restrict__ out, int T, int L,
                                                             int H, int D, int BL, float* __restrict__ lse) {
-  constexpr int DP = MDG_DP, KC = 64, LDK = 48;  // 96-B LDS rows (bf16): conflict-free b128 + tr reads
+  constexpr int KC = 64, LDK = DP + 16;  // DP 32: 96-B LDS rows (bf16), conflict-free b128 + tr reads
+  constexpr int KS = DP / 32, DT = DP / 16;
   constexpr int VEC = 16 / sizeof(CT);
   constexpr int PIECES = KC * DP / VEC / 256;
   __shared__ __attribute__((aligned(16))) CT Ks[2][KC * LDK];
@@ -51,11 +54,12 @@ __global__ __launch_bounds__(256) void attn_temporal_kernel(const CT* __restrict
   const CT* Vg = Qg + 2 * plane;
   const float* kb = kbias + (size_t)seq * T;
 
-  typename V8<CT>::T qf[2];
+  typename V8<CT>::T qf[2][KS];
 #pragma unroll
   for (int qg = 0; qg < 2; ++qg) {
     const int q = q0 + qg * 16 + lr;
-    qf[qg] = (q < T) ? ld8<CT>(Qg + (size_t)q * DP + 8 * lg) : zero8<CT>();
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) qf[qg][ks] = (q < T) ? ld8<CT>(Qg + (size_t)q * DP + 32 * ks + 8 * lg) : zero8<CT>();
   }
 
   // virtual bias key first.  The running softmax offset mt (per query, exactly representable
@@ -64,26 +68,30 @@ __global__ __launch_bounds__(256) void attn_temporal_kernel(const CT* __restrict
   // needs one v_exp_f32 per score and nothing else.  mt is only raised (rare path below)
   // when a score exceeds it by more than kGrow (log2 units), so p <= 2^kGrow.
   constexpr float kGrow = 8.0f;
-  const int padg = D >> 3, pade = D & 7;  // lane group / element of the pad column
+  const int pads = D >> 5, padg = (D & 31) >> 3, pade = D & 7;  // K-step / lane group / element of pad column
   const float* kvh = kvb + head * 2 * DP;
   float mt[2];
-  f32x4 o[2][2];  // [d-tile][q-group]: O^T[d = 16dt + 4lg + i][q = lr]
+  f32x4 o[DT][2];  // [d-tile][q-group]: O^T[d = 16dt + 4lg + i][q = lr]
 #pragma unroll
   for (int qg = 0; qg < 2; ++qg) {
     float sb = 0.f;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) sb += (float)qf[qg][j] * kvh[8 * lg + j];
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sb += (float)qf[qg][ks][j] * kvh[32 * ks + 8 * lg + j];
     sb += __shfl_xor(sb, 16, 64);
     sb += __shfl_xor(sb, 32, 64);
     mt[qg] = (float)(CT)sb;
     const float pb = __builtin_amdgcn_exp2f(sb - mt[qg]);
 #pragma unroll
-    for (int dt = 0; dt < 2; ++dt)
+    for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
       for (int i = 0; i < 4; ++i) o[dt][qg][i] = pb * kvh[DP + dt * 16 + lg * 4 + i];
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
-      if (lg == padg && j == pade) qf[qg][j] = (CT)(-mt[qg]);
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (ks == pads && lg == padg && j == pade) qf[qg][ks][j] = (CT)(-mt[qg]);
   }
 
   uint4 kreg[PIECES], vreg[PIECES];
@@ -133,11 +141,13 @@ __global__ __launch_bounds__(256) void attn_temporal_kernel(const CT* __restrict
     f32x4 s[4][2];
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt) {
-      const typename V8<CT>::T kf = ld8<CT>(Kc + (kt * 16 + lr) * LDK + 8 * lg);
 #pragma unroll
-      for (int qg = 0; qg < 2; ++qg) {
-        s[kt][qg] = f32x4{0.f, 0.f, 0.f, 0.f};
-        mma_k32<CT>(s[kt][qg], kf, qf[qg]);
+      for (int qg = 0; qg < 2; ++qg) s[kt][qg] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const typename V8<CT>::T kf = ld8<CT>(Kc + (kt * 16 + lr) * LDK + 32 * ks + 8 * lg);
+#pragma unroll
+        for (int qg = 0; qg < 2; ++qg) mma_k32<CT>(s[kt][qg], kf, qf[qg][ks]);
       }
     }
     if (kflag[cur]) {
@@ -170,7 +180,7 @@ __global__ __launch_bounds__(256) void attn_temporal_kernel(const CT* __restrict
         const float alpha = __builtin_amdgcn_exp2f(-delta);
         mt[qg] = nm;
 #pragma unroll
-        for (int dt = 0; dt < 2; ++dt)
+        for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
           for (int i = 0; i < 4; ++i) o[dt][qg][i] *= alpha;
 #pragma unroll
@@ -178,8 +188,10 @@ __global__ __launch_bounds__(256) void attn_temporal_kernel(const CT* __restrict
 #pragma unroll
           for (int i = 0; i < 4; ++i) s[kt][qg][i] -= delta;
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if (lg == padg && j == pade) qf[qg][j] = (CT)(-nm);
+        for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (ks == pads && lg == padg && j == pade) qf[qg][ks][j] = (CT)(-nm);
       }
     }
 #pragma unroll
@@ -199,7 +211,7 @@ __global__ __launch_bounds__(256) void attn_temporal_kernel(const CT* __restrict
           pf[qg][4 + j] = (CT)s[2 * kh + 1][qg][j];
         }
 #pragma unroll
-      for (int dt = 0; dt < 2; ++dt) {
+      for (int dt = 0; dt < DT; ++dt) {
         typename V8<CT>::T vf;
         if constexpr (is_bf16<CT>()) {
           typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
@@ -234,7 +246,7 @@ __global__ __launch_bounds__(256) void attn_temporal_kernel(const CT* __restrict
   for (int qg = 0; qg < 2; ++qg) {
     float mine = 0.f;
 #pragma unroll
-    for (int dt = 0; dt < 2; ++dt)
+    for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
         if (dt == dt_s && i == i_s) mine = o[dt][qg][i];
@@ -245,7 +257,7 @@ __global__ __launch_bounds__(256) void attn_temporal_kernel(const CT* __restrict
     if (q < T) {
       CT* orow = out + ((size_t)(b * T + q) * L + l) * C + head * D;
 #pragma unroll
-      for (int dt = 0; dt < 2; ++dt) {
+      for (int dt = 0; dt < DT; ++dt) {
         const int d0 = dt * 16 + lg * 4;
         if (d0 < D)
           st4<CT>(orow + d0, o[dt][qg][0] * inv, o[dt][qg][1] * inv, o[dt][qg][2] * inv,
@@ -489,13 +501,12 @@ __global__ __launch_bounds__(kTW * 64) void attn_temporal_bf16_kernel(const bf16
 
 // Spatial attention over the L residues of one frame (+ the bias key): q|k|v come unpadded,
 // [token][3][H][D] (no MFMA reads them), so each (token, head) thread reads D-element rows.
-template <typename CT>
+template <typename CT, int DP>
 __global__ __launch_bounds__(256) void attn_spatial_kernel(const CT* __restrict__ qkv,
                                                            const float* __restrict__ kvb,
                                                            const float* __restrict__ mask,
                                                            CT* __restrict__ out, int nf, int L,
                                                            int H, int D) {
-  constexpr int DP = MDG_DP;
   const int idx = blockIdx.x * 256 + threadIdx.x;
   if (idx >= nf * L * H) return;
   const int h = idx % H, tok = idx / H, f = tok / L;
@@ -579,7 +590,7 @@ __global__ __launch_bounds__(256) void attn_spatial_quad_kernel(const CT* __rest
                                                                 const float* __restrict__ kvb,
                                                                 const float* __restrict__ mask,
                                                                 CT* __restrict__ out, int nf, int H, int D) {
-  constexpr int DP = MDG_DP;  // kvb row stride
+  const int DP = dp_of(D);  // kvb row stride
   const int idx = blockIdx.x * 256 + threadIdx.x;   // ((f * H + h) * 4 + j); nf*H*4 % 64 == 0 not assumed
   const int total = nf * H * 4;
   const bool live = idx < total;
@@ -649,6 +660,16 @@ __global__ __launch_bounds__(256) void attn_spatial_quad_kernel(const CT* __rest
 
 hipError_t attn_temporal_launch(int dtype, int B, int T, int L, int H, int D, const void* qkv_t,
                                 const float* kbias, const float* kvb, void* out, hipStream_t s, float* lse) {
+  if (D >= MDG_DP) {  // wide heads (32..63): the generic 16x16 MFMA kernel on 64-column rows
+    dim3 grid((T + 127) / 128, H, B * L);
+    if (dtype == MDG_BF16)
+      hipLaunchKernelGGL((attn_temporal_kernel<bf16_t, MDG_DP_WIDE>), grid, dim3(256), 0, s, (const bf16_t*)qkv_t,
+                         kbias, kvb, (bf16_t*)out, T, L, H, D, B * L, lse);
+    else
+      hipLaunchKernelGGL((attn_temporal_kernel<float, MDG_DP_WIDE>), grid, dim3(256), 0, s, (const float*)qkv_t,
+                         kbias, kvb, (float*)out, T, L, H, D, B * L, lse);
+    return hipGetLastError();
+  }
   if (dtype == MDG_BF16) {
     // MDG_ATTN_WAVES=4 selects 4-wave blocks with 64-key chunks (tuning knob; default 8 / 128)
     static const int waves = [] {
@@ -667,18 +688,14 @@ hipError_t attn_temporal_launch(int dtype, int B, int T, int L, int H, int D, co
     return hipGetLastError();
   }
   dim3 grid((T + 127) / 128, H, B * L);
-  if (dtype == MDG_BF16)
-    hipLaunchKernelGGL(attn_temporal_kernel<bf16_t>, grid, dim3(256), 0, s,
-                       (const bf16_t*)qkv_t, kbias, kvb, (bf16_t*)out, T, L, H, D, B * L, lse);
-  else
-    hipLaunchKernelGGL(attn_temporal_kernel<float>, grid, dim3(256), 0, s, (const float*)qkv_t,
-                       kbias, kvb, (float*)out, T, L, H, D, B * L, lse);
+  hipLaunchKernelGGL((attn_temporal_kernel<float, MDG_DP>), grid, dim3(256), 0, s, (const float*)qkv_t, kbias, kvb,
+                     (float*)out, T, L, H, D, B * L, lse);
   return hipGetLastError();
 }
 
 hipError_t attn_spatial_launch(int dtype, int nf, int L, int H, int D, const void* qkv,
                                const float* kvb, const float* mask, void* out, hipStream_t s) {
-  if (L == 4 && D % 8 == 0) {
+  if (L == 4 && D % 8 == 0 && D <= 32) {
     dim3 grid((unsigned)(((size_t)nf * H * 4 + 255) / 256));
 #define MDG_QUAD(CTT, DM)                                                                                  \
   hipLaunchKernelGGL((attn_spatial_quad_kernel<CTT, DM>), grid, dim3(256), 0, s, (const CTT*)qkv, kvb, mask, \
@@ -693,12 +710,15 @@ hipError_t attn_spatial_launch(int dtype, int nf, int L, int H, int D, const voi
   }
   const int total = nf * L * H;
   dim3 grid((total + 255) / 256);
-  if (dtype == MDG_BF16)
-    hipLaunchKernelGGL(attn_spatial_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)qkv,
-                       kvb, mask, (bf16_t*)out, nf, L, H, D);
-  else
-    hipLaunchKernelGGL(attn_spatial_kernel<float>, grid, dim3(256), 0, s, (const float*)qkv, kvb,
-                       mask, (float*)out, nf, L, H, D);
+#define MDG_SPA(CTT, DPP)                                                                            \
+  hipLaunchKernelGGL((attn_spatial_kernel<CTT, DPP>), grid, dim3(256), 0, s, (const CTT*)qkv, kvb, mask, \
+                     (CTT*)out, nf, L, H, D)
+  if (dtype == MDG_BF16) {
+    if (D < MDG_DP) MDG_SPA(bf16_t, MDG_DP); else MDG_SPA(bf16_t, MDG_DP_WIDE);
+  } else {
+    if (D < MDG_DP) MDG_SPA(float, MDG_DP); else MDG_SPA(float, MDG_DP_WIDE);
+  }
+#undef MDG_SPA
   return hipGetLastError();
 }
 

@@ -120,7 +120,7 @@ WsLayout ws_layout(const mdg_dims& d) {
   WsLayout w;
   size_t off = 0;
   w.qkv_s = off; off += align256(N * 3 * d.H * d.D * cs);
-  w.qkv_t = off; off += align256(3ull * d.B * d.L * d.H * d.T * MDG_DP * cs);
+  w.qkv_t = off; off += align256(3ull * d.B * d.L * d.H * d.T * dp_of(d.D) * cs);
   w.o = off;     off += align256(N * d.C * cs);
   w.hid = off;   off += align256(N * d.F * cs);
   w.xn = off;    off += align256(N * d.C * cs);
@@ -136,8 +136,8 @@ int check_dims(const mdg_dims* d) {
   if (d->B <= 0 || d->T <= 0 || d->L <= 0 || d->H <= 0)
     return fail(MDG_E_SHAPE, "B,T,L,H must be positive (%d,%d,%d,%d)", d->B, d->T, d->L, d->H);
   if (d->C != d->H * d->D) return fail(MDG_E_SHAPE, "C (%d) != H*D (%d*%d)", d->C, d->H, d->D);
-  if (d->D % 4 || d->D >= MDG_DP)
-    return fail(MDG_E_SHAPE, "head_dim %d unsupported (multiple of 4, < %d)", d->D, MDG_DP);
+  if (d->D % 4 || d->D >= MDG_DP_WIDE)
+    return fail(MDG_E_SHAPE, "head_dim %d unsupported (multiple of 4, < %d)", d->D, MDG_DP_WIDE);
   if (d->C % 64 || d->C > 512) return fail(MDG_E_SHAPE, "embed_dim %d unsupported (64k, <= 512)", d->C);
   if (d->F % 64) return fail(MDG_E_SHAPE, "ffn dim %d not a multiple of 64", d->F);
   if (d->latent <= 0 || d->latent > 64) return fail(MDG_E_SHAPE, "latent %d unsupported", d->latent);
@@ -180,7 +180,7 @@ int mdg_workspace_init(const mdg_dims* d, void* ws, void* stream) {
   if (int e = hip_check(hipMemsetAsync(ws, 0, w.total, s), "workspace memset")) return e;
   // 1.0 in pad column D of every temporal K row (softmax offset) and V row (row sum)
   const size_t vrows = (size_t)d->B * d->L * d->H * d->T;
-  char* k = (char*)ws + w.qkv_t + vrows * MDG_DP * ct_size(d->dtype);
+  char* k = (char*)ws + w.qkv_t + vrows * dp_of(d->D) * ct_size(d->dtype);
   return hip_check(mdg::set_vpad_launch(d->dtype, k, 2 * vrows, d->D, s), "set_vpad");
 }
 
@@ -226,7 +226,7 @@ int mdg_gemm(const mdg_gemm_desc* g, void* stream) {
       }
       break;
     case MDG_EPI_QKV:
-      if (!g->qkv_out || g->D <= 0 || g->D % 4 || g->D >= MDG_DP || g->N != 3 * g->H * g->D)
+      if (!g->qkv_out || g->D <= 0 || g->D % 4 || g->D >= MDG_DP_WIDE || g->N != 3 * g->H * g->D)
         return fail(MDG_E_SHAPE, "gemm QKV: N=%d H=%d D=%d", g->N, g->H, g->D);
       if (g->T <= 0 || g->L <= 0 || g->M % (g->T * g->L))
         return fail(MDG_E_SHAPE, "gemm QKV: M=%d not a multiple of T*L", g->M);
@@ -261,7 +261,7 @@ int mdg_attn_spatial(int32_t dtype, int32_t n_frames, int32_t L, int32_t H, int3
                      void* stream) {
   if (dtype != MDG_F32 && dtype != MDG_BF16) return fail(MDG_E_DTYPE, "dtype %d", dtype);
   if (!qkv || !kvb || !out) return fail(MDG_E_ARG, "attn_spatial: null pointer");
-  if (n_frames <= 0 || L <= 0 || H <= 0 || D <= 0 || D % 4 || D >= MDG_DP)
+  if (n_frames <= 0 || L <= 0 || H <= 0 || D <= 0 || D % 4 || D >= MDG_DP_WIDE)
     return fail(MDG_E_SHAPE, "attn_spatial: nf=%d L=%d H=%d D=%d", n_frames, L, H, D);
   return hip_check(mdg::attn_spatial_launch(dtype, n_frames, L, H, D, qkv, kvb, mask, out,
                                             (hipStream_t)stream),
@@ -273,7 +273,7 @@ int mdg_attn_temporal(int32_t dtype, int32_t B, int32_t T, int32_t L, int32_t H,
                       void* stream) {
   if (dtype != MDG_F32 && dtype != MDG_BF16) return fail(MDG_E_DTYPE, "dtype %d", dtype);
   if (!qkv_t || !kbias || !kvb || !out) return fail(MDG_E_ARG, "attn_temporal: null pointer");
-  if (B <= 0 || T <= 0 || L <= 0 || H <= 0 || D <= 0 || D % 4 || D >= MDG_DP)
+  if (B <= 0 || T <= 0 || L <= 0 || H <= 0 || D <= 0 || D % 4 || D >= MDG_DP_WIDE)
     return fail(MDG_E_SHAPE, "attn_temporal: B=%d T=%d L=%d H=%d D=%d", B, T, L, H, D);
   if (H > 65535 || B * L > 65535) return fail(MDG_E_SHAPE, "attn_temporal: grid too large");
   return hip_check(mdg::attn_temporal_launch(dtype, B, T, L, H, D, qkv_t, kbias, kvb, out,
@@ -287,7 +287,8 @@ int mdg_attn_temporal_lse(int32_t dtype, int32_t B, int32_t T, int32_t L, int32_
   if (dtype != MDG_F32 && dtype != MDG_BF16) return fail(MDG_E_DTYPE, "dtype %d", dtype);
   if (!qkv_t || !kbias || !kvb || !out || !lse) return fail(MDG_E_ARG, "attn_temporal_lse: null pointer");
   if (B <= 0 || T <= 0 || L <= 0 || H <= 0 || D <= 0 || D % 4 || D >= MDG_DP)
-    return fail(MDG_E_SHAPE, "attn_temporal_lse: B=%d T=%d L=%d H=%d D=%d", B, T, L, H, D);
+    return fail(MDG_E_SHAPE, "attn_temporal_lse: B=%d T=%d L=%d H=%d D=%d (training kernels: head_dim < %d)", B, T,
+                L, H, D, MDG_DP);
   if (H > 65535 || B * L > 65535) return fail(MDG_E_SHAPE, "attn_temporal_lse: grid too large");
   return hip_check(mdg::attn_temporal_launch(dtype, B, T, L, H, D, qkv_t, kbias, kvb, out, (hipStream_t)stream, lse),
                    "attn_temporal_lse");
@@ -532,7 +533,9 @@ int mdg_describe_plan(const mdg_dims* d, char* buf, size_t n) {
            "\"temporal\": \"qkv_gemm+%s\", \"mlp\": \"fc1_gemm(gelu)+%s\", \"final\": \"euler_epilogue_gemm\"}",
            d->dtype == MDG_BF16 ? "bf16" : "f32", spatial,
            fuse ? "fused into gated-residual row-LN GEMM epilogues" : "stand-alone ln_mod pass",
-           d->dtype == MDG_BF16 ? "attn_temporal_bf16(32x32x16 mfma)" : "attn_temporal(f32 16x16x4 mfma)",
+           d->D >= MDG_DP ? (d->dtype == MDG_BF16 ? "attn_temporal(wide heads: bf16 16x16x32 mfma, 64-col rows)"
+                                                  : "attn_temporal(wide heads: f32 16x16x4 mfma, 64-col rows)")
+           : d->dtype == MDG_BF16 ? "attn_temporal_bf16(32x32x16 mfma)" : "attn_temporal(f32 16x16x4 mfma)",
            fuse ? "fc2_rowln_gemm" : "fc2_gate_res_gemm");
   return MDG_OK;
 }
@@ -588,6 +591,8 @@ int mdg_layer_fwd_train(const mdg_dims* d, const mdg_layer_weights* w, const flo
                         const float* mods, const float* mask, const float* kbias_t, const float* kbias_s,
                         const float* h_in, float* h_out, const mdg_layer_saved* sv, void* stream) {
   if (int e = check_dims(d)) return e;
+  if (d->D >= MDG_DP)
+    return fail(MDG_E_SHAPE, "layer_fwd_train: head_dim %d (the training kernels take head_dim < %d)", d->D, MDG_DP);
   if (!w || !mods || !kbias_t || !h_in || !h_out || !sv || h_in == h_out)
     return fail(MDG_E_ARG, "layer_fwd_train: null pointer or h_in == h_out");
   for (int i = 0; i < 3; ++i)
@@ -759,7 +764,7 @@ CondLayout cond_layout(const mdg_cond_dims& d) {
   c.sc = take((size_t)c.R * C * f);
   c.all = take((size_t)c.R * c.W * f);
   const size_t qkv_spatial = M * 3 * C * f;
-  const size_t qkv_planes = 3ull * c.R * d.H * d.L * MDG_DP * f;
+  const size_t qkv_planes = 3ull * c.R * d.H * d.L * dp_of(d.D) * f;
   c.x2 = take(ipa && d.tps ? M * C * f : 0);
   c.xn = take(ipa ? M * C * f : 0);
   c.proj = take(ipa ? M * c.Ppad * f : 0);
@@ -785,7 +790,7 @@ int check_cond_dims(const mdg_cond_dims* d) {
   if (d->freq_dim <= 0 || d->freq_dim % 64) return fail(MDG_E_SHAPE, "cond: freq_dim %d (64k)", d->freq_dim);
   if ((long long)d->S * d->B * d->L * 4 * d->C >= (1ll << 31)) return fail(MDG_E_SHAPE, "cond: problem too large");
   if (d->ipa_layers > 0) {
-    if (d->H <= 0 || d->C != d->H * d->D || d->D % 4 || d->D >= MDG_DP)
+    if (d->H <= 0 || d->C != d->H * d->D || d->D % 4 || d->D >= MDG_DP_WIDE)
       return fail(MDG_E_SHAPE, "cond: IPA-layer MHA C=%d H=%d D=%d", d->C, d->H, d->D);
     if (d->ipa_heads <= 0 || !mdg::ipa_attn_supported(d->ipa_c, d->ipa_qk, d->ipa_v))
       return fail(MDG_E_SHAPE, "cond: IPA heads=%d c=%d P_q=%d P_v=%d has no kernel instance", d->ipa_heads, d->ipa_c,
@@ -872,9 +877,9 @@ int mdg_precompute_cond(const mdg_cond_model* m, const mdg_cond_io* io, void* ws
     return e;
   if (long_l) {  // the q|k|v planes of the MFMA route: zero pads, 1.0 in k / v pad column D
     const size_t rows = (size_t)c.R * H * L;
-    if (int e = hip_check(hipMemsetAsync(wb + c.qkv, 0, 3 * rows * MDG_DP * sizeof(float), s), "cond memset"))
+    if (int e = hip_check(hipMemsetAsync(wb + c.qkv, 0, 3 * rows * dp_of(D) * sizeof(float), s), "cond memset"))
       return e;
-    if (int e = hip_check(mdg::set_vpad_launch(MDG_F32, F(c.qkv) + rows * MDG_DP, 2 * rows, D, s), "set_vpad"))
+    if (int e = hip_check(mdg::set_vpad_launch(MDG_F32, F(c.qkv) + rows * dp_of(D), 2 * rows, D, s), "set_vpad"))
       return e;
   }
   const int ipa_mod0 = d.num_layers * 9 * C + 2 * C;

@@ -17,6 +17,8 @@
 
 #include <type_traits>
 
+#include "../../include/mdgen_hip.h"
+
 typedef __bf16 bf16_t;
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
@@ -143,3 +145,6 @@ __device__ __forceinline__ float gelu_grad_fast(float x) {
 __device__ __forceinline__ float silu(float x) { return x / (1.0f + expf(-x)); }
 
 static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+
+// row stride of the padded attention operands (planes, bias_kv rows) for head dim D
+__host__ __device__ constexpr int dp_of(int D) { return MDG_HEAD_STRIDE(D); }

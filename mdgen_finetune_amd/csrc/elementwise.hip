@@ -201,7 +201,7 @@ __global__ void mask_bias_kernel(int B, int T, int L, const float* __restrict__ 
 template <typename CT>
 __global__ void set_vpad_kernel(CT* v, size_t rows, int D) {
   const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
-  if (i < rows) v[i * MDG_DP + D] = (CT)1.0f;
+  if (i < rows) v[i * dp_of(D) + D] = (CT)1.0f;
 }
 
 hipError_t embed_launch(int N, int T, int L, int C, int K, const float* x, const float* Wt,

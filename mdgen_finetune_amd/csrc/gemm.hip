@@ -107,8 +107,9 @@ __device__ __forceinline__ void epi4(const mdg_gemm_desc& p, int m, int n, float
       dst = reinterpret_cast<CT*>(p.qkv_out) + ((size_t)(m * 3 + which) * p.H + head) * D + cp;
     } else {
       const int BL = (M / (p.T * p.L)) * p.L, seq = mt * p.L + l;
-      dst = reinterpret_cast<CT*>(p.qkv_out) + (size_t)which * BL * p.H * p.T * MDG_DP +
-            ((size_t)(seq * p.H + head) * p.T + t) * MDG_DP + cp;
+      const int dp = dp_of(p.D);
+      dst = reinterpret_cast<CT*>(p.qkv_out) + (size_t)which * BL * p.H * p.T * dp +
+            ((size_t)(seq * p.H + head) * p.T + t) * dp + cp;
     }
     st4<CT>(dst, v.x, v.y, v.z, v.w);
   } else {  // EULER
@@ -495,7 +496,8 @@ __device__ __forceinline__ void epi_tile(const mdg_gemm_desc& p, const float* __
     const int BL = (M / (p.T * p.L)) * p.L;
     bf16_t* qo = reinterpret_cast<bf16_t*>(p.qkv_out);
     const size_t colS = (size_t)(which * p.H + head) * D + cp;               // spatial: + m*3*H*D
-    const size_t colT = (size_t)which * BL * p.H * p.T * MDG_DP + (size_t)head * p.T * MDG_DP + cp;
+    const int dp = dp_of(D);
+    const size_t colT = (size_t)which * BL * p.H * p.T * dp + (size_t)head * p.T * dp + cp;
 #pragma unroll
     for (int u0 = 0; u0 < RPT; u0 += U) {
       float2 cs[U], sn[U];
@@ -529,7 +531,7 @@ __device__ __forceinline__ void epi_tile(const mdg_gemm_desc& p, const float* __
         } else {
           const int ml = fdiv(m, p.L, invL), l = m - ml * p.L;
           const int b = fdiv(ml, p.T, invT), t = ml - b * p.T;
-          off = colT + ((size_t)(b * p.L + l) * p.H * p.T + t) * MDG_DP;
+          off = colT + ((size_t)(b * p.L + l) * p.H * p.T + t) * dp;
         }
         st4<bf16_t>(qo + off, v.x, v.y, v.z, v.w);
       }

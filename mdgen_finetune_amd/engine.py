@@ -230,8 +230,8 @@ class HipEngine:
         return torch.cat([freqs.cos().reshape(-1), freqs.sin().reshape(-1)]).to(self.model.device)
 
     def _kvb(self, bias_k, bias_v, S, table, n_rows):
-        """[H][2][32]: bias_k rotated at position S (the appended row's index), bias_v with 1.0
-        in pad column D (the temporal kernel's softmax row sum)."""
+        """[H][2][dp]: bias_k rotated at position S (the appended row's index), bias_v with 1.0
+        in pad column D (the temporal kernel's softmax row sum); dp = 32 (D <= 31) or 64."""
         H, D, half = self.H, self.D, self.D // 2
         kb = bias_k.reshape(H, D)
         if table is not None:
@@ -242,7 +242,7 @@ class HipEngine:
             kb = kb * c2 + rot * s2
         if table is not None:  # same pair-interleaved order as the packed k rows
             kb = kb.reshape(-1)[self._pair_perm()].reshape(H, D)
-        out = torch.zeros(H, 2, _lib.MDG_DP, device=bias_k.device, dtype=torch.float32)
+        out = torch.zeros(H, 2, _lib.head_stride(D), device=bias_k.device, dtype=torch.float32)
         out[:, 0, :D] = kb
         out[:, 1, :D] = bias_v.reshape(H, D)
         out[:, 1, D] = 1.0

@@ -264,11 +264,13 @@ class LatentMDGenModel(nn.Module):
 
     def _use_hip_layers(self, h):
         """Differentiable calls on a ROCm device run the block stack through the HIP training
-        Function (train_backend 'hip', the default); dropout > 0 while training is not built
-        there and takes eager autograd."""
+        Function (train_backend 'hip', the default); dropout > 0 while training and head_dim >= 32
+        are not built there and take eager autograd."""
         if self.backend != "hip" or getattr(self, "train_backend", "hip") != "hip" or not h.is_cuda:
             return False
         if not torch.is_grad_enabled():
+            return False
+        if self.args.embed_dim // self.args.mha_heads >= 32:  # the training kernels take head_dim < 32
             return False
         return not (self.training and float(getattr(self.args, "dropout", 0.0) or 0.0) > 0.0)
 

@@ -89,7 +89,9 @@ def test_shape_validation_without_gpu():
     lib = _lib.load()
     d = _lib.MdgDims(B=1, T=1000, L=4, C=384, H=16, D=24, F=1536, latent=21, num_layers=5, dtype=1)
     assert lib.mdg_workspace_bytes(ctypes.byref(d)) > 0
-    bad = _lib.MdgDims(B=1, T=10, L=4, C=384, H=12, D=32, F=1536, latent=21, num_layers=5, dtype=1)
+    wide = _lib.MdgDims(B=1, T=10, L=4, C=384, H=12, D=32, F=1536, latent=21, num_layers=5, dtype=1)
+    assert lib.mdg_workspace_bytes(ctypes.byref(wide)) > 0  # head_dim 32: 64-column operand rows
+    bad = _lib.MdgDims(B=1, T=10, L=4, C=512, H=8, D=64, F=2048, latent=21, num_layers=5, dtype=1)
     assert lib.mdg_workspace_bytes(ctypes.byref(bad)) == 0
     assert b"head_dim" in lib.mdg_last_error_string()
     offs = _lib.workspace_offsets(d)
