@@ -130,15 +130,20 @@ def roofline(eng, st, dtype, B, T, L):
     s = _lib.stream_handle()
     kvb = st.kvb[0][1]
 
+    # the planes as the step stores them (packed: row stride D, bf16 with D % 8 == 0)
+    packed = eng.describe_plan(B, T, L).get("planes", "").startswith("packed")
+    attn_fn = lib.mdg_attn_temporal_packed if packed else lib.mdg_attn_temporal
+
     def attn():
-        _lib.check(lib.mdg_attn_temporal(eng.mdg_dtype, B, T, L, H, D, ws + off["qkv_t"], ws + off["kbias"],
-                                         kvb.data_ptr(), ws + off["o"], s), "attn_temporal")
+        _lib.check(attn_fn(eng.mdg_dtype, B, T, L, H, D, ws + off["qkv_t"], ws + off["kbias"], kvb.data_ptr(),
+                           ws + off["o"], s), "attn_temporal")
 
     g = _lib.MdgGemmDesc()
     g.dtype, g.a_mode, g.epi, g.M, g.N, g.K = eng.mdg_dtype, _lib.MDG_A_PLAIN, _lib.MDG_EPI_QKV, N, 3 * C, C
     g.A, g.lda = ws + off["xn"], C
     g.W, g.ldw, g.bias = P["layers"][0]["wqkv1"].data_ptr(), C, P["layers"][0]["bqkv1"].data_ptr()
-    g.qkv_layout, g.qkv_out, g.H, g.D, g.T, g.L = _lib.MDG_QKV_TEMPORAL, ws + off["qkv_t"], H, D, T, L
+    g.qkv_layout = _lib.MDG_QKV_TEMPORAL_PACKED if packed else _lib.MDG_QKV_TEMPORAL
+    g.qkv_out, g.H, g.D, g.T, g.L = ws + off["qkv_t"], H, D, T, L
     g.qscale = D ** -0.5 * math.log2(math.e)
     g.rope, g.rope_rows = _lib.ptr(st.rope_t), T + 1
 
@@ -168,6 +173,8 @@ def roofline(eng, st, dtype, B, T, L):
     bytes_fc2 = N * 4 * C * cb + 2 * N * C * 4 + N * C * cb + 4 * C * C * cb   # hid, h r+w, xn, W2
     bytes_qkv = N * C * cb + 3 * N * HD * cb + 3 * C * C * cb                     # xn, q|k|v, Wqkv
     bytes_attn = 3 * N * HD * cb + N * HD * cb                                    # q|k|v, o
+    # (the bf16 step stores the planes packed: these are also the bytes it moves; the f32 path
+    # pads D to 32 columns)
     out = {}
     for name, fn, flops, nbytes in (("gemm_fc2_rowln", fc2, 2.0 * N * C * 4 * C, bytes_fc2),
                                     ("gemm_qkv_temporal", gemm, 2.0 * N * 3 * C * C, bytes_qkv),

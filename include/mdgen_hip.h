@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define MDG_ABI_VERSION 11
+#define MDG_ABI_VERSION 12
 #define MDG_MAX_LAYERS 16
 #define MDG_DP 32      /* padded head dim of the attention operand buffers for head_dim <= 31 */
 #define MDG_DP_WIDE 64 /* ... and for 32 <= head_dim <= 63 (column head_dim of the padded k / v rows
@@ -54,7 +54,7 @@ enum {
 enum { MDG_A_PLAIN = 0, MDG_A_LNMOD = 1 };
 enum { MDG_EPI_STORE = 0, MDG_EPI_GATE_RES = 1, MDG_EPI_QKV = 2, MDG_EPI_EULER = 3, MDG_EPI_ATTN_SPATIAL = 4 };
 enum { MDG_ACT_NONE = 0, MDG_ACT_GELU = 1, MDG_ACT_SILU = 2, MDG_ACT_DGELU = 3 };
-enum { MDG_QKV_SPATIAL = 0, MDG_QKV_TEMPORAL = 1 };
+enum { MDG_QKV_SPATIAL = 0, MDG_QKV_TEMPORAL = 1, MDG_QKV_TEMPORAL_PACKED = 2 };
 
 typedef struct {
   int32_t B, T, L;    /* batch, frames (num_frames), residues (crop) */
@@ -118,7 +118,10 @@ typedef struct {
   /* GATE_RES: resid[m][n] += gate[(m/rows_per_mod)*mod_stride + gate_off + n] * v
      (gate null: += v) */
   float* resid; int32_t ldr; const float* gate; int32_t gate_off;
-  /* QKV: N == 3*H*D; q scaled by qscale; RoPE on q,k at pos l (spatial) or t (temporal) */
+  /* QKV: N == 3*H*D; q scaled by qscale; RoPE on q,k at pos l (spatial) or t (temporal).
+     TEMPORAL: [3][B*L][H][T][MDG_HEAD_STRIDE(D)] planes (pad columns left as they are);
+     TEMPORAL_PACKED (D % 8 == 0, D < 32): the same planes with row stride D (no pad columns in
+     memory: the attention synthesises them), read by mdg_attn_temporal_packed. */
   int32_t qkv_layout; void* qkv_out; int32_t H, D, T, L; float qscale;
   const float* rope; int32_t rope_rows; /* cos [rope_rows][D/2] then sin; null = no RoPE */
   /* EULER: x_out (= out, row stride ldo) = x_in + dt * v, v_out = v, for columns < n_valid */
@@ -205,6 +208,12 @@ int mdg_attn_spatial(int32_t dtype, int32_t n_frames, int32_t L, int32_t H, int3
 int mdg_attn_temporal(int32_t dtype, int32_t B, int32_t T, int32_t L, int32_t H, int32_t D,
                       const void* qkv_t, const float* kbias, const float* kvb, void* out,
                       void* stream);
+/* The same attention on PACKED planes (CT [3][B*L][H][T][D], row stride D; bf16, D % 8 == 0,
+   D < 32): the k / v pad column D (softmax offset, row sum) is synthesised while staging, so
+   the planes carry only the head dim (24 of 32 columns for the default model). */
+int mdg_attn_temporal_packed(int32_t dtype, int32_t B, int32_t T, int32_t L, int32_t H, int32_t D,
+                             const void* qkv_t, const float* kbias, const float* kvb, void* out,
+                             void* stream);
 /* The same, also writing lse [B*L][H][T] = log2 of each query row's softmax normaliser in the
    planes' score units (the training backward recomputes P from it). */
 int mdg_attn_temporal_lse(int32_t dtype, int32_t B, int32_t T, int32_t L, int32_t H, int32_t D,

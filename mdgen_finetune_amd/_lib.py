@@ -19,7 +19,7 @@ MDG_F32, MDG_BF16 = 0, 1
 MDG_A_PLAIN, MDG_A_LNMOD = 0, 1
 MDG_EPI_STORE, MDG_EPI_GATE_RES, MDG_EPI_QKV, MDG_EPI_EULER, MDG_EPI_ATTN_SPATIAL = 0, 1, 2, 3, 4
 MDG_ACT_NONE, MDG_ACT_GELU, MDG_ACT_SILU, MDG_ACT_DGELU = 0, 1, 2, 3
-MDG_QKV_SPATIAL, MDG_QKV_TEMPORAL = 0, 1
+MDG_QKV_SPATIAL, MDG_QKV_TEMPORAL, MDG_QKV_TEMPORAL_PACKED = 0, 1, 2
 MDG_PREP_TPS, MDG_PREP_NO_OFFSETS, MDG_PREP_COND_FIRST, MDG_PREP_COND_LAST = 1, 2, 4, 8
 MDG_MAX_LAYERS = 16
 MDG_DP = 32
@@ -121,6 +121,7 @@ SIGNATURES = [
     ("mdg_gemm", _i32, [ctypes.POINTER(MdgGemmDesc), _vp]),
     ("mdg_attn_spatial", _i32, [_i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
     ("mdg_attn_temporal", _i32, [_i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
+    ("mdg_attn_temporal_packed", _i32, [_i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
     ("mdg_attn_temporal_lse", _i32, [_i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
     ("mdg_prep_latents", _i32, [_i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     ("mdg_latents_to_atom14", _i32, [_i32, _i32, _i32, _i32, _i32, _i32] + [_vp] * 12),
@@ -142,7 +143,7 @@ SIGNATURES = [
                                     _vp]),
 ]
 
-ABI_VERSION = 11
+ABI_VERSION = 12
 _LIB = None
 
 

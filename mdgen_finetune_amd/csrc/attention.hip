@@ -356,12 +356,17 @@ __device__ __forceinline__ void ta_subchunk(const bf16_t* Kc, const bf16_t* Vc, 
 // Bias key + offset setup shared by both bf16 temporal kernels: Q fragments (B operand,
 // d = 16s + 8h + j), mt = bf16(score of the bias key), O^T = exp2(score_b - mt) * bias_v,
 // Q pad element = -mt.
-__device__ __forceinline__ void ta_setup(const bf16_t* Qg, const float* kvh, int q, int T, int D, int r, int h,
-                                         bf16x8 (&qf)[2], float& mt, f32x16& o) {
+// rs = the planes' row stride: MDG_DP (padded) or D (packed: the 8-column pieces at and after
+// column D are not in memory and read as zeros)
+__device__ __forceinline__ void ta_setup(const bf16_t* Qg, const float* kvh, int q, int T, int D, int rs, int r,
+                                         int h, bf16x8 (&qf)[2], float& mt, f32x16& o) {
   constexpr int DP = MDG_DP;
 #pragma unroll
-  for (int s2 = 0; s2 < 2; ++s2)
-    qf[s2] = (q < T) ? *reinterpret_cast<const bf16x8*>(Qg + (size_t)q * DP + 16 * s2 + 8 * h) : zero8<bf16_t>();
+  for (int s2 = 0; s2 < 2; ++s2) {
+    const int pc = 16 * s2 + 8 * h;  // first column of this lane's 8-column piece
+    qf[s2] = (q < T && pc < (rs == DP ? DP : D)) ? *reinterpret_cast<const bf16x8*>(Qg + (size_t)q * rs + pc)
+                                                 : zero8<bf16_t>();
+  }
   float sb = 0.f;
 #pragma unroll
   for (int s2 = 0; s2 < 2; ++s2)
@@ -407,13 +412,16 @@ __device__ __forceinline__ void ta_store(const f32x16& o, bf16_t* out, int q, in
 }
 
 
-template <int kTW, int kTKC>  // waves per block, keys per LDS chunk
-__global__ __launch_bounds__(kTW * 64) void attn_temporal_bf16_kernel(const bf16_t* __restrict__ qkv,
+template <int kTW, int kTKC, int PD>  // waves per block, keys per LDS chunk, packed head dim (0: padded)
+__global__ __launch_bounds__(kTW * 64, 4) void attn_temporal_bf16_kernel(const bf16_t* __restrict__ qkv,
                                                                     const float* __restrict__ kbias,
                                                                     const float* __restrict__ kvb,
                                                                     bf16_t* __restrict__ out, int T, int L,
                                                                     int H, int D, int BL, float* __restrict__ lse) {
   constexpr int DP = MDG_DP, KC = kTKC, NTH = kTW * 64;
+  constexpr bool PACKED = PD > 0;
+  constexpr int RS = PACKED ? PD : DP;  // plane row stride (a compile-time constant either way)
+  if constexpr (PACKED) D = PD;
   static_assert(KC * DP / 8 == NTH, "one 16-B K piece and one V piece per thread per chunk");
   __shared__ __attribute__((aligned(16))) bf16_t Ks[2][KC * DP];
   __shared__ __attribute__((aligned(16))) bf16_t Vs[2][KC * DP];
@@ -429,8 +437,8 @@ __global__ __launch_bounds__(kTW * 64) void attn_temporal_bf16_kernel(const bf16
   const int wg = (xcd < r8 ? xcd * (qq + 1) : r8 * (qq + 1) + (xcd - r8) * qq) + loc;
   const int qb = wg % nqb, head = (wg / nqb) % H, seq = wg / (nqb * H);
   const int q0 = qb * (kTW * 32) + wave * 32;
-  const size_t plane = (size_t)BL * H * T * DP;
-  const bf16_t* Qg = qkv + ((size_t)seq * H + head) * T * DP;
+  const size_t plane = (size_t)BL * H * T * RS;
+  const bf16_t* Qg = qkv + ((size_t)seq * H + head) * T * RS;
   const bf16_t* Kg = Qg + plane;
   const bf16_t* Vg = Qg + 2 * plane;
   const float* kb = kbias + (size_t)seq * T;
@@ -439,20 +447,38 @@ __global__ __launch_bounds__(kTW * 64) void attn_temporal_bf16_kernel(const bf16
   bf16x8 qf[2];
   float mt;
   f32x16 o;
-  ta_setup(Qg, kvb + head * 2 * DP, q, T, D, r, h, qf, mt, o);
+  ta_setup(Qg, kvb + head * 2 * DP, q, T, D, RS, r, h, qf, mt, o);
   const int padS = D >> 4, padH = (D >> 3) & 1, padJ = D & 7;  // Q element holding -mt
 
   // chunk staging: thread -> key row tid/4, 16-B piece tid%4 of K and of V
   const int srow = tid >> 2, spc = tid & 3;
   u32x4 kreg, vreg;
   float kbreg = 0.f;
+  // packed planes: the pieces at and after column D are not in memory.  Their LDS slots (fixed
+  // per thread) are written once here -- 1.0 at column D for k (softmax offset) and v (row sum),
+  // zeros elsewhere, exactly the padded rows' content -- and never restaged (rows past T are
+  // masked by the -inf key bias, so their constant pad is harmless).
+  const bool real = !PACKED || spc * 8 < D;
+  if (PACKED && !real) {
+    u32x4 synth = u32x4{0u, 0u, 0u, 0u};
+    if (spc == (D >> 3)) {
+      const int e = D & 7;  // bf16 1.0 = 0x3F80 in half e & 1 of dword e >> 1
+#pragma unroll
+      for (int w = 0; w < 4; ++w) synth[w] = (w == (e >> 1)) ? (0x3F80u << (16 * (e & 1))) : 0u;
+    }
+#pragma unroll
+    for (int bf = 0; bf < 2; ++bf) {
+      *reinterpret_cast<u32x4*>(&Ks[bf][srow * DP + ((spc ^ ((srow >> 3) & 3)) * 8)]) = synth;
+      *reinterpret_cast<u32x4*>(&Vs[bf][srow * DP + spc * 8]) = synth;
+    }
+  }
 #define MDG_TA_GLOAD(c_)                                                                      \
   {                                                                                           \
     const int key = (c_) * KC + srow;                                                         \
     kreg = vreg = u32x4{0u, 0u, 0u, 0u};                                                      \
-    if (key < T) {                                                                            \
-      kreg = *reinterpret_cast<const u32x4*>(Kg + (size_t)key * DP + spc * 8);                \
-      vreg = *reinterpret_cast<const u32x4*>(Vg + (size_t)key * DP + spc * 8);                \
+    if (key < T && real) {                                                                    \
+      kreg = *reinterpret_cast<const u32x4*>(Kg + (size_t)key * RS + spc * 8);                \
+      vreg = *reinterpret_cast<const u32x4*>(Vg + (size_t)key * RS + spc * 8);                \
     }                                                                                         \
     if (tid < KC) {                                                                           \
       const int kk = (c_) * KC + tid;                                                         \
@@ -461,8 +487,10 @@ __global__ __launch_bounds__(kTW * 64) void attn_temporal_bf16_kernel(const bf16
   }
 #define MDG_TA_LSTORE(buf)                                                                    \
   {                                                                                           \
-    *reinterpret_cast<u32x4*>(&Ks[buf][srow * DP + ((spc ^ ((srow >> 3) & 3)) * 8)]) = kreg;  \
-    *reinterpret_cast<u32x4*>(&Vs[buf][srow * DP + spc * 8]) = vreg;                          \
+    if (real) {                                                                               \
+      *reinterpret_cast<u32x4*>(&Ks[buf][srow * DP + ((spc ^ ((srow >> 3) & 3)) * 8)]) = kreg; \
+      *reinterpret_cast<u32x4*>(&Vs[buf][srow * DP + spc * 8]) = vreg;                        \
+    }                                                                                         \
     if (tid < KC) {                                                                           \
       kbs[buf][tid] = kbreg;                                                                  \
       const bool any = __any(kbreg != 0.f);                                                   \
@@ -659,7 +687,9 @@ __global__ __launch_bounds__(256) void attn_spatial_quad_kernel(const CT* __rest
 }
 
 hipError_t attn_temporal_launch(int dtype, int B, int T, int L, int H, int D, const void* qkv_t,
-                                const float* kbias, const float* kvb, void* out, hipStream_t s, float* lse) {
+                                const float* kbias, const float* kvb, void* out, hipStream_t s, float* lse,
+                                bool packed) {
+  if (packed && (dtype != MDG_BF16 || D % 8 || D >= MDG_DP)) return hipErrorInvalidValue;
   if (D >= MDG_DP) {  // wide heads (32..63): the generic 16x16 MFMA kernel on 64-column rows
     dim3 grid((T + 127) / 128, H, B * L);
     if (dtype == MDG_BF16)
@@ -678,12 +708,18 @@ hipError_t attn_temporal_launch(int dtype, int B, int T, int L, int H, int D, co
     }();
     if (waves == 4) {
       dim3 grid((unsigned)((T + 127) / 128 * H * B * L));
-      hipLaunchKernelGGL((attn_temporal_bf16_kernel<4, 64>), grid, dim3(256), 0, s, (const bf16_t*)qkv_t, kbias, kvb,
-                         (bf16_t*)out, T, L, H, D, B * L, lse);
+#define MDG_TA4(PD_)                                                                                     \
+  hipLaunchKernelGGL((attn_temporal_bf16_kernel<4, 64, PD_>), grid, dim3(256), 0, s, (const bf16_t*)qkv_t, kbias, \
+                     kvb, (bf16_t*)out, T, L, H, D, B * L, lse)
+      if (!packed) MDG_TA4(0); else if (D == 24) MDG_TA4(24); else if (D == 16) MDG_TA4(16); else MDG_TA4(8);
+#undef MDG_TA4
     } else {
       dim3 grid((unsigned)((T + 255) / 256 * H * B * L));
-      hipLaunchKernelGGL((attn_temporal_bf16_kernel<8, 128>), grid, dim3(512), 0, s, (const bf16_t*)qkv_t, kbias, kvb,
-                         (bf16_t*)out, T, L, H, D, B * L, lse);
+#define MDG_TA8(PD_)                                                                                      \
+  hipLaunchKernelGGL((attn_temporal_bf16_kernel<8, 128, PD_>), grid, dim3(512), 0, s, (const bf16_t*)qkv_t, kbias, \
+                     kvb, (bf16_t*)out, T, L, H, D, B * L, lse)
+      if (!packed) MDG_TA8(0); else if (D == 24) MDG_TA8(24); else if (D == 16) MDG_TA8(16); else MDG_TA8(8);
+#undef MDG_TA8
     }
     return hipGetLastError();
   }

@@ -20,7 +20,7 @@ GemmPlan gemm_plan(const mdg_gemm_desc& p);
 hipError_t gemm_launch(const mdg_gemm_desc& p, const GemmPlan& g, hipStream_t s);
 hipError_t attn_temporal_launch(int dtype, int B, int T, int L, int H, int D, const void* qkv_t,
                                 const float* kbias, const float* kvb, void* out, hipStream_t s,
-                                float* lse = nullptr);
+                                float* lse = nullptr, bool packed = false);
 hipError_t attn_spatial_launch(int dtype, int nf, int L, int H, int D, const void* qkv,
                                const float* kvb, const float* mask, void* out, hipStream_t s);
 hipError_t embed_launch(int N, int T, int L, int C, int K, const float* x, const float* W,
@@ -108,6 +108,16 @@ bool fuse_spatial_attn(const mdg_dims& d) {
     return !(e && e[0] == '0');
   }();
   return on && d.dtype == MDG_BF16 && d.L == 4 && d.D == 24 && d.H % 2 == 0;
+}
+
+// bf16, head_dim % 8 == 0: temporal attention planes stored packed (row stride D);
+// MDG_PACKED_PLANES=0 keeps the padded planes (A/B knob)
+bool packed_planes(const mdg_dims& d) {
+  static const bool on = [] {
+    const char* e = getenv("MDG_PACKED_PLANES");
+    return !(e && e[0] == '0');
+  }();
+  return on && d.dtype == MDG_BF16 && d.D % 8 == 0 && d.D < MDG_DP;
 }
 
 struct WsLayout {
@@ -226,6 +236,10 @@ int mdg_gemm(const mdg_gemm_desc* g, void* stream) {
       }
       break;
     case MDG_EPI_QKV:
+      if (g->qkv_layout == MDG_QKV_TEMPORAL_PACKED && (g->D % 8 || g->D >= MDG_DP))
+        return fail(MDG_E_SHAPE, "gemm QKV packed: D=%d (multiple of 8, < %d)", g->D, MDG_DP);
+      if (g->qkv_layout < MDG_QKV_SPATIAL || g->qkv_layout > MDG_QKV_TEMPORAL_PACKED)
+        return fail(MDG_E_ARG, "gemm QKV: layout %d", g->qkv_layout);
       if (!g->qkv_out || g->D <= 0 || g->D % 4 || g->D >= MDG_DP_WIDE || g->N != 3 * g->H * g->D)
         return fail(MDG_E_SHAPE, "gemm QKV: N=%d H=%d D=%d", g->N, g->H, g->D);
       if (g->T <= 0 || g->L <= 0 || g->M % (g->T * g->L))
@@ -279,6 +293,19 @@ int mdg_attn_temporal(int32_t dtype, int32_t B, int32_t T, int32_t L, int32_t H,
   return hip_check(mdg::attn_temporal_launch(dtype, B, T, L, H, D, qkv_t, kbias, kvb, out,
                                              (hipStream_t)stream),
                    "attn_temporal");
+}
+
+int mdg_attn_temporal_packed(int32_t dtype, int32_t B, int32_t T, int32_t L, int32_t H, int32_t D,
+                             const void* qkv_t, const float* kbias, const float* kvb, void* out, void* stream) {
+  if (dtype != MDG_BF16) return fail(MDG_E_DTYPE, "attn_temporal_packed: bf16 only (dtype %d)", dtype);
+  if (!qkv_t || !kbias || !kvb || !out) return fail(MDG_E_ARG, "attn_temporal_packed: null pointer");
+  if (B <= 0 || T <= 0 || L <= 0 || H <= 0 || D <= 0 || D % 8 || D >= MDG_DP)
+    return fail(MDG_E_SHAPE, "attn_temporal_packed: B=%d T=%d L=%d H=%d D=%d (D multiple of 8, < %d)", B, T, L, H, D,
+                MDG_DP);
+  if (H > 65535 || B * L > 65535) return fail(MDG_E_SHAPE, "attn_temporal_packed: grid too large");
+  return hip_check(mdg::attn_temporal_launch(dtype, B, T, L, H, D, qkv_t, kbias, kvb, out, (hipStream_t)stream,
+                                             nullptr, true),
+                   "attn_temporal_packed");
 }
 
 int mdg_attn_temporal_lse(int32_t dtype, int32_t B, int32_t T, int32_t L, int32_t H, int32_t D,
@@ -379,15 +406,23 @@ static int layer_fwd_impl(const mdg_dims* d, const mdg_layer_weights* w, const f
   q.epi = MDG_EPI_QKV;
   q.N = 3 * C; q.K = C; q.A = xn; q.lda = C; q.W = w->wqkv[0]; q.ldw = C; q.bias = w->bqkv[0];
   q.rope = rope_l; q.rope_rows = L + 1;
+  // bf16 with D % 8 == 0: the attention planes are stored packed (row stride D, 24 of the padded
+  // 32 columns); the attention kernel synthesises the pad column while staging
+  const bool packed = packed_planes(*d);
+  auto attn_t = [&](int Bq, int Tq, int Lq, const float* kb, const float* kvb) -> int {
+    return packed ? mdg_attn_temporal_packed(d->dtype, Bq, Tq, Lq, H, D, qkv_t, kb, kvb, o, stream)
+                  : mdg_attn_temporal(d->dtype, Bq, Tq, Lq, H, D, qkv_t, kb, kvb, o, stream);
+  };
+  const int tlayout = packed ? MDG_QKV_TEMPORAL_PACKED : MDG_QKV_TEMPORAL;
   if (L >= kSpatialMfmaMinL && (size_t)B * T <= 65535) {
     // long residue axis (ATLAS crop 256): every frame is one attention sequence of L tokens;
     // the temporal MFMA kernel runs it with (B', T', L') = (B*T, L, 1) — same token order
-    q.qkv_layout = MDG_QKV_TEMPORAL; q.qkv_out = qkv_t; q.qscale = qs * 1.4426950408889634f;
+    q.qkv_layout = tlayout; q.qkv_out = qkv_t; q.qscale = qs * 1.4426950408889634f;
     q.T = L; q.L = 1;
     if (int e = mdg_gemm(&q, stream)) return e;
     q.T = T; q.L = L;
     const float* kbias_s = (const float*)(wsb + lay.kbias_s);
-    if (int e = mdg_attn_temporal(d->dtype, B * T, L, 1, H, D, qkv_t, kbias_s, w->kvb[0], o, stream)) return e;
+    if (int e = attn_t(B * T, L, 1, kbias_s, w->kvb[0])) return e;
   } else if (fuse_spatial_attn(*d)) {
     // q|k|v of the 4 residues stay on chip: projection + attention -> o in one launch
     q.epi = MDG_EPI_ATTN_SPATIAL; q.qscale = qs;
@@ -413,10 +448,10 @@ static int layer_fwd_impl(const mdg_dims* d, const mdg_layer_weights* w, const f
     if (int e = ln(3 * C, 4 * C)) return e;
   q.epi = MDG_EPI_QKV;  // (the spatial launch above may have been the fused ATTN_SPATIAL form)
   q.W = w->wqkv[1]; q.bias = w->bqkv[1];
-  q.qkv_layout = MDG_QKV_TEMPORAL; q.qkv_out = qkv_t; q.qscale = qs * 1.4426950408889634f;
+  q.qkv_layout = tlayout; q.qkv_out = qkv_t; q.qscale = qs * 1.4426950408889634f;
   q.rope = rope_t; q.rope_rows = T + 1;
   if (int e = mdg_gemm(&q, stream)) return e;
-  if (int e = mdg_attn_temporal(d->dtype, B, T, L, H, D, qkv_t, kbias, w->kvb[1], o, stream)) return e;
+  if (int e = attn_t(B, T, L, kbias, w->kvb[1])) return e;
   r.W = w->wo[1]; r.bias = w->bo[1]; r.gate_off = 5 * C;
   if (fuse) {  // + LN_mlp(h) -> xn
     r.xn_shift_off = 6 * C; r.xn_scale_off = 7 * C;
@@ -530,12 +565,14 @@ int mdg_describe_plan(const mdg_dims* d, char* buf, size_t n) {
     spatial = "qkv_gemm(spatial layout)+attn_spatial(valu)";
   snprintf(buf, n,
            "{\"dtype\": \"%s\", \"spatial\": \"%s\", \"ln_handoff\": \"%s\", "
-           "\"temporal\": \"qkv_gemm+%s\", \"mlp\": \"fc1_gemm(gelu)+%s\", \"final\": \"euler_epilogue_gemm\"}",
+           "\"temporal\": \"qkv_gemm+%s\", \"planes\": \"%s\", \"mlp\": \"fc1_gemm(gelu)+%s\", "
+           "\"final\": \"euler_epilogue_gemm\"}",
            d->dtype == MDG_BF16 ? "bf16" : "f32", spatial,
            fuse ? "fused into gated-residual row-LN GEMM epilogues" : "stand-alone ln_mod pass",
            d->D >= MDG_DP ? (d->dtype == MDG_BF16 ? "attn_temporal(wide heads: bf16 16x16x32 mfma, 64-col rows)"
                                                   : "attn_temporal(wide heads: f32 16x16x4 mfma, 64-col rows)")
            : d->dtype == MDG_BF16 ? "attn_temporal_bf16(32x32x16 mfma)" : "attn_temporal(f32 16x16x4 mfma)",
+           packed_planes(*d) ? "packed (row stride = head_dim)" : "padded (row stride MDG_HEAD_STRIDE)",
            fuse ? "fc2_rowln_gemm" : "fc2_gate_res_gemm");
   return MDG_OK;
 }

@@ -107,7 +107,7 @@ __device__ __forceinline__ void epi4(const mdg_gemm_desc& p, int m, int n, float
       dst = reinterpret_cast<CT*>(p.qkv_out) + ((size_t)(m * 3 + which) * p.H + head) * D + cp;
     } else {
       const int BL = (M / (p.T * p.L)) * p.L, seq = mt * p.L + l;
-      const int dp = dp_of(p.D);
+      const int dp = p.qkv_layout == MDG_QKV_TEMPORAL_PACKED ? p.D : dp_of(p.D);
       dst = reinterpret_cast<CT*>(p.qkv_out) + (size_t)which * BL * p.H * p.T * dp +
             ((size_t)(seq * p.H + head) * p.T + t) * dp + cp;
     }
@@ -496,7 +496,7 @@ __device__ __forceinline__ void epi_tile(const mdg_gemm_desc& p, const float* __
     const int BL = (M / (p.T * p.L)) * p.L;
     bf16_t* qo = reinterpret_cast<bf16_t*>(p.qkv_out);
     const size_t colS = (size_t)(which * p.H + head) * D + cp;               // spatial: + m*3*H*D
-    const int dp = dp_of(D);
+    const int dp = p.qkv_layout == MDG_QKV_TEMPORAL_PACKED ? D : dp_of(D);
     const size_t colT = (size_t)which * BL * p.H * p.T * dp + (size_t)head * p.T * dp + cp;
 #pragma unroll
     for (int u0 = 0; u0 < RPT; u0 += U) {

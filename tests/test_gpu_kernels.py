@@ -223,6 +223,64 @@ def test_attn_temporal(lib, dt, T):
         torch.testing.assert_close(got[0, :, :, h].permute(1, 0, 2), ref, rtol=rtol * 2, atol=atol * 2)
 
 
+@pytest.mark.parametrize("T,D", [(1, 24), (63, 24), (1000, 24), (1300, 16), (129, 8)])
+def test_attn_temporal_packed_equals_padded(lib, T, D):
+    """Packed planes (row stride D, pad column synthesised while staging) give the padded
+    kernel's output bit for bit; the packed q|k|v GEMM layout is the padded one minus the pads."""
+    from mdgen_finetune_amd import _lib
+
+    B, L, H = 1, 3, 4
+    BL = B * L
+    g = torch.Generator(device="cuda").manual_seed(T + D)
+    pad = torch.zeros(3, BL, H, T, 32, device="cuda")
+    pad[..., :D] = torch.randn(3, BL, H, T, D, device="cuda", generator=g)
+    pad[1:, ..., D] = 1.0
+    pad = pad.to(torch.bfloat16)
+    packed = pad[..., :D].contiguous()
+    mask = torch.ones(B, T, L, device="cuda")
+    if T > 3:
+        mask[:, T // 3: T // 2, 1] = 0
+        mask[:, :, 2] = 0
+    kvb = torch.zeros(H, 2, 32, device="cuda")
+    kvb[:, :, :D] = torch.randn(H, 2, D, device="cuda", generator=g)
+    kvb[:, 1, D] = 1.0
+    kbias = torch.where(mask.permute(0, 2, 1).reshape(BL, T) != 0, 0.0, float("-inf")).contiguous()
+    o1 = torch.zeros(B * T * L, H * D, device="cuda", dtype=torch.bfloat16)
+    o2 = torch.zeros_like(o1)
+    _lib.check(lib.mdg_attn_temporal(1, B, T, L, H, D, pad.data_ptr(), kbias.data_ptr(), kvb.data_ptr(),
+                                     o1.data_ptr(), _s()), "attn_temporal")
+    _lib.check(lib.mdg_attn_temporal_packed(1, B, T, L, H, D, packed.data_ptr(), kbias.data_ptr(), kvb.data_ptr(),
+                                            o2.data_ptr(), _s()), "attn_temporal_packed")
+    torch.cuda.synchronize()
+    assert torch.equal(o1, o2)
+    assert lib.mdg_attn_temporal_packed(1, B, T, L, H, 20, packed.data_ptr(), kbias.data_ptr(), kvb.data_ptr(),
+                                        o2.data_ptr(), _s()) == 1001  # D % 8 != 0: refused
+
+
+def test_gemm_qkv_packed_layout_is_padded_minus_pads(lib):
+    from mdgen_finetune_amd import _lib
+
+    B, T, L, H, D = 2, 37, 4, 16, 24
+    C, M = H * D, B * T * L
+    g = torch.Generator(device="cuda").manual_seed(77)
+    A = torch.randn(M, C, device="cuda", generator=g).to(torch.bfloat16)
+    W = (torch.randn(3 * C, C, device="cuda", generator=g) / math.sqrt(C)).to(torch.bfloat16)
+    bias = torch.randn(3 * C, device="cuda", generator=g)
+    inv = 1.0 / (10000 ** (torch.arange(0, D, 2).float() / D))
+    f = torch.arange(T + 1).float()[:, None] * inv
+    table = torch.cat([f.cos().reshape(-1), f.sin().reshape(-1)]).cuda()
+    outs = []
+    for layout, shape in ((1, (3, B * L, H, T, 32)), (2, (3, B * L, H, T, D))):
+        out = torch.zeros(*shape, device="cuda", dtype=torch.bfloat16)
+        d = _desc(dtype=1, a_mode=0, epi=2, M=M, N=3 * C, K=C, A=A.data_ptr(), lda=C, W=W.data_ptr(), ldw=C,
+                  bias=bias.data_ptr(), qkv_layout=layout, qkv_out=out.data_ptr(), H=H, D=D, T=T, L=L, qscale=0.3,
+                  rope=table.data_ptr(), rope_rows=T + 1)
+        _lib.check(lib.mdg_gemm(ctypes.byref(d), _s()), "mdg_gemm")
+        outs.append(out)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][..., :D], outs[1])
+
+
 @pytest.mark.parametrize("dt", ["f32", "bf16"])
 @pytest.mark.parametrize("L,D", [(5, 24), (4, 24), (4, 16)])   # L == 4: DPP quad kernel
 def test_attn_spatial(lib, dt, L, D):
