@@ -883,8 +883,31 @@ __global__ __launch_bounds__(kRowThreads, BM == 64 ? 4 : 1) void gemm_rowln_kern
       for (int e = 0; e < NE; ++e) hv[rr][e] = *reinterpret_cast<const float2*>(hr + 2 * lane + 128 * e);
     }
   };
+  // Fast epilogue (BM 128, the tile spans <= 2 trajectory entries -- every tile when
+  // rows_per_mod >= 128): the adaLN rows go to LDS once and each wave processes its rows as
+  // PAIRS, one row per half-wave, 4 consecutive columns per lane, so every h load / store is a
+  // 16-B-per-lane access (1 KiB per wave instruction) and every xn store 8 B per lane: half the
+  // memory instructions of the float2 layout.  Unit u = (band u, the wave's 4 rows as 2 pairs).
+  int b_lo = 0, b_hi = 1 << 30;
+  if (BM == 128) {
+    b_lo = fdiv(m0, p.rows_per_mod, inv_rpm);
+    b_hi = fdiv(min(m0 + BM - 1, M - 1), p.rows_per_mod, inv_rpm);
+  }
+  const bool fast = BM == 128 && b_hi - b_lo < 2;
+  const int half = lane >> 5, hl = lane & 31;
+  auto load_unit4 = [&](int u, float4 (&h4)[2][NE]) {
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr) {
+      const int m = min(m0 + u * 32 + wave * 4 + 2 * pr + half, M - 1);
+      const float* hr = p.resid + (size_t)m * p.ldr + 4 * hl;
+#pragma unroll
+      for (int e = 0; e < NE; ++e) h4[pr][e] = *reinterpret_cast<const float4*>(hr + 128 * e);
+    }
+  };
+  float4 h4[2][NE];
   float2 hv[RG][NE], gv[NE];
-  load_unit(0, hv, gv);
+  if (fast) load_unit4(0, h4);
+  else if (BM == 64) load_unit(0, hv, gv);
 
   f32x4 acc[4][NT];
 #pragma unroll
@@ -940,14 +963,10 @@ __global__ __launch_bounds__(kRowThreads, BM == 64 ? 4 : 1) void gemm_rowln_kern
   // trajectory -- made the compiler drain every outstanding store and prefetch with
   // s_waitcnt vmcnt(0) on every row.)  The band barriers are raw s_barrier after an LDS wait:
   // they order the stage buffer only, so the h / xn stores stay in flight across them.
-  int b_lo = 0, b_hi = 0;
-  if (BM == 128) {
-    b_lo = fdiv(m0, p.rows_per_mod, inv_rpm);
-    b_hi = fdiv(min(m0 + BM - 1, M - 1), p.rows_per_mod, inv_rpm);
-  }
-  if (BM == 128 && b_hi - b_lo < 2) {
+  if (fast) {
     float* emods = stage + 32 * LDS_ST;  // [2][3][NCOL]: gate | xn scale | xn shift
     static_assert(BM != 128 || (32 * LDS_ST + 6 * NCOL) * 4 <= kRowStages * STAGE * 2, "adaLN rows fit the ring");
+    static_assert(LDS_ST % 4 == 0, "16-B aligned stage rows");
     __builtin_amdgcn_s_barrier();  // every wave is done reading the ring (its loads were all waited)
     for (int i = tid; i < 6 * NCOL; i += kRowThreads) {
       const int eb = i / (3 * NCOL), w = (i / NCOL) % 3, k = i % NCOL;
@@ -958,7 +977,10 @@ __global__ __launch_bounds__(kRowThreads, BM == 64 ? 4 : 1) void gemm_rowln_kern
       else v = p.xn_out ? p.xn_mods[b * p.xn_mod_stride + p.xn_shift_off + k] : 0.0f;
       emods[i] = v;
     }
-    // h rows of unit 0 were loaded before the K loop (with its gate row, unused here)
+    float4 b4[NE];
+#pragma unroll
+    for (int e = 0; e < NE; ++e)
+      b4[e] = p.bias ? *reinterpret_cast<const float4*>(p.bias + 4 * hl + 128 * e) : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll 1
     for (int band = 0; band < BM / 32; ++band) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -976,83 +998,83 @@ __global__ __launch_bounds__(kRowThreads, BM == 64 ? 4 : 1) void gemm_rowln_kern
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
-#pragma unroll 1
-      for (int g0 = 0; g0 < 4; g0 += RG) {
-        const int u = band * UPB + g0 / RG;
-        float2 hn[RG][NE], gn[NE];
-        if (u + 1 < NU) load_unit(u + 1, hn, gn);
-        float sum[RG];
-        int eb[RG];
+      float4 hn[2][NE];
+      if (band + 1 < BM / 32) load_unit4(band + 1, hn);
+      float sum[2];
+      int eb[2];
 #pragma unroll
-        for (int rr = 0; rr < RG; ++rr) {
-          const int m = m0 + band * 32 + wave * 4 + g0 + rr;
-          eb[rr] = fdiv(min(m, M - 1), p.rows_per_mod, inv_rpm) - b_lo;
-          const float* srow = stage + (wave * 4 + g0 + rr) * LDS_ST;
-          const float* gr = emods + eb[rr] * 3 * NCOL;
-          float s = 0.f;
+      for (int pr = 0; pr < 2; ++pr) {
+        const int m = m0 + band * 32 + wave * 4 + 2 * pr + half;
+        eb[pr] = fdiv(min(m, M - 1), p.rows_per_mod, inv_rpm) - b_lo;
+        const float* srow = stage + (wave * 4 + 2 * pr + half) * LDS_ST + 4 * hl;
+        const float* gr = emods + eb[pr] * 3 * NCOL + 4 * hl;
+        float sacc = 0.f;
+#pragma unroll
+        for (int e = 0; e < NE; ++e) {
+          const float4 v = *reinterpret_cast<const float4*>(srow + 128 * e);
+          const float4 g = *reinterpret_cast<const float4*>(gr + 128 * e);
+          float4& h = h4[pr][e];
+          h.x += g.x * (v.x + b4[e].x);
+          h.y += g.y * (v.y + b4[e].y);
+          h.z += g.z * (v.z + b4[e].z);
+          h.w += g.w * (v.w + b4[e].w);
+          sacc += (h.x + h.y) + (h.z + h.w);
+        }
+        sum[pr] = sacc;
+        if (m < M) {
+          float* hr = p.resid + (size_t)m * p.ldr + 4 * hl;
+#pragma unroll
+          for (int e = 0; e < NE; ++e) *reinterpret_cast<float4*>(hr + 128 * e) = h4[pr][e];
+        }
+      }
+      if (p.xn_out) {
+        // row sums over each half-wave (32 lanes)
+#pragma unroll
+        for (int o = 16; o >= 1; o >>= 1)
+#pragma unroll
+          for (int pr = 0; pr < 2; ++pr) sum[pr] += __shfl_xor(sum[pr], o, 64);
+        float ss[2];
+#pragma unroll
+        for (int pr = 0; pr < 2; ++pr) {
+          sum[pr] *= invN;  // mean
+          float t = 0.f;
 #pragma unroll
           for (int e = 0; e < NE; ++e) {
-            const int k = 2 * lane + 128 * e;
-            const float2 v = *reinterpret_cast<const float2*>(srow + k);
-            const float2 g2 = *reinterpret_cast<const float2*>(gr + k);
-            hv[rr][e].x += g2.x * (v.x + bb[e].x);
-            hv[rr][e].y += g2.y * (v.y + bb[e].y);
-            s += hv[rr][e].x + hv[rr][e].y;
+            const float4 h = h4[pr][e];
+            const float a0 = h.x - sum[pr], a1 = h.y - sum[pr], a2 = h.z - sum[pr], a3 = h.w - sum[pr];
+            t += (a0 * a0 + a1 * a1) + (a2 * a2 + a3 * a3);
           }
-          sum[rr] = s;
-          if (m < M) {
-#pragma unroll
-            for (int e = 0; e < NE; ++e)
-              *reinterpret_cast<float2*>(p.resid + (size_t)m * p.ldr + 2 * lane + 128 * e) = hv[rr][e];
-          }
-        }
-        if (p.xn_out) {
-#pragma unroll
-          for (int o = 32; o >= 1; o >>= 1)
-#pragma unroll
-            for (int rr = 0; rr < RG; ++rr) sum[rr] += __shfl_xor(sum[rr], o, 64);
-          float ss[RG];
-#pragma unroll
-          for (int rr = 0; rr < RG; ++rr) {
-            sum[rr] *= invN;  // mean
-            float t = 0.f;
-#pragma unroll
-            for (int e = 0; e < NE; ++e) {
-              const float a0 = hv[rr][e].x - sum[rr], a1 = hv[rr][e].y - sum[rr];
-              t += a0 * a0 + a1 * a1;
-            }
-            ss[rr] = t;
-          }
-#pragma unroll
-          for (int o = 32; o >= 1; o >>= 1)
-#pragma unroll
-            for (int rr = 0; rr < RG; ++rr) ss[rr] += __shfl_xor(ss[rr], o, 64);
-#pragma unroll
-          for (int rr = 0; rr < RG; ++rr) {
-            const int m = m0 + band * 32 + wave * 4 + g0 + rr;
-            const float rs = 1.0f / sqrtf(ss[rr] * invN + p.ln_eps);
-            const float* mr = emods + eb[rr] * 3 * NCOL;
-#pragma unroll
-            for (int e = 0; e < NE; ++e) {
-              const int k = 2 * lane + 128 * e;
-              const float2 xs = *reinterpret_cast<const float2*>(mr + NCOL + k);
-              const float2 xh = *reinterpret_cast<const float2*>(mr + 2 * NCOL + k);
-              typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
-              bf16x2 pr;
-              pr[0] = (bf16_t)((hv[rr][e].x - sum[rr]) * rs * (1.0f + xs.x) + xh.x);
-              pr[1] = (bf16_t)((hv[rr][e].y - sum[rr]) * rs * (1.0f + xs.y) + xh.y);
-              if (m < M) *reinterpret_cast<bf16x2*>(reinterpret_cast<bf16_t*>(p.xn_out) + (size_t)m * NCOL + k) = pr;
-            }
-          }
+          ss[pr] = t;
         }
 #pragma unroll
-        for (int e = 0; e < NE; ++e)
+        for (int o = 16; o >= 1; o >>= 1)
 #pragma unroll
-          for (int rr = 0; rr < RG; ++rr) hv[rr][e] = hn[rr][e];
+          for (int pr = 0; pr < 2; ++pr) ss[pr] += __shfl_xor(ss[pr], o, 64);
+#pragma unroll
+        for (int pr = 0; pr < 2; ++pr) {
+          const int m = m0 + band * 32 + wave * 4 + 2 * pr + half;
+          const float rs = 1.0f / sqrtf(ss[pr] * invN + p.ln_eps);
+          const float* mr = emods + eb[pr] * 3 * NCOL + 4 * hl;
+#pragma unroll
+          for (int e = 0; e < NE; ++e) {
+            const float4 xs = *reinterpret_cast<const float4*>(mr + NCOL + 128 * e);
+            const float4 xh = *reinterpret_cast<const float4*>(mr + 2 * NCOL + 128 * e);
+            const float4 h = h4[pr][e];
+            if (m < M)
+              st4<bf16_t>(reinterpret_cast<bf16_t*>(p.xn_out) + (size_t)m * NCOL + 4 * hl + 128 * e,
+                          (h.x - sum[pr]) * rs * (1.0f + xs.x) + xh.x, (h.y - sum[pr]) * rs * (1.0f + xs.y) + xh.y,
+                          (h.z - sum[pr]) * rs * (1.0f + xs.z) + xh.z, (h.w - sum[pr]) * rs * (1.0f + xs.w) + xh.w);
+          }
+        }
       }
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr)
+#pragma unroll
+        for (int e = 0; e < NE; ++e) h4[pr][e] = hn[pr][e];
     }
     return;
   }
+  if (BM == 128) load_unit(0, hv, gv);  // the rare tile over > 2 entries: no prefetch under the K loop
   __syncthreads();  // all waves are done with the ring
 #pragma unroll 1
   for (int band = 0; band < BM / 32; ++band) {
