@@ -549,7 +549,130 @@ __device__ __forceinline__ void epi_tile(const mdg_gemm_desc& p, const float* __
   }
 }
 
-template <int EPI, int BK>
+// Wide-store variant of epi_tile for the bf16 STORE (fc1 + GELU, plain projections) and QKV
+// (q|k|v + RoPE scatter, head dim a multiple of 8) epilogues: a thread owns 8 consecutive
+// columns (16 threads per 128-column row), so every output store is a 16-B bf16x8 (was 8 B):
+// half the store instructions, which bound these epilogues, for the same bytes.
+template <int EPI, int NT, int BM>
+__device__ __forceinline__ void epi_tile8(const mdg_gemm_desc& p, const float* __restrict__ stage, int m0, int n0,
+                                          int tid) {
+  constexpr int LDS_ST = 128 + 4;
+  const int M = p.M;
+  const int c = (tid & 15) * 8, n = n0 + c, r0 = tid >> 4;
+  constexpr int RS = NT / 16, RPT = BM / RS, U = 2;
+  static_assert(RPT % U == 0, "rows per thread");
+  float bb[8];
+#pragma unroll
+  for (int j = 0; j < 8; j += 4) {
+    const float4 b = p.bias ? *reinterpret_cast<const float4*>(p.bias + n + j) : make_float4(0.f, 0.f, 0.f, 0.f);
+    bb[j] = b.x; bb[j + 1] = b.y; bb[j + 2] = b.z; bb[j + 3] = b.w;
+  }
+  auto ld8s = [&](int row, float (&v)[8]) {
+    const float4 a = *reinterpret_cast<const float4*>(stage + row * LDS_ST + c);
+    const float4 b = *reinterpret_cast<const float4*>(stage + row * LDS_ST + c + 4);
+    v[0] = a.x + bb[0]; v[1] = a.y + bb[1]; v[2] = a.z + bb[2]; v[3] = a.w + bb[3];
+    v[4] = b.x + bb[4]; v[5] = b.y + bb[5]; v[6] = b.z + bb[6]; v[7] = b.w + bb[7];
+  };
+  auto st8 = [&](bf16_t* dst, const float (&v)[8]) {
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (bf16_t)v[j];
+    *reinterpret_cast<bf16x8*>(dst) = o;
+  };
+  if constexpr (EPI == MDG_EPI_STORE) {
+#pragma unroll
+    for (int u0 = 0; u0 < RPT; u0 += U) {
+      float v[U][8];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int row = r0 + RS * (u0 + u), m = m0 + row;
+        ld8s(row, v[u]);
+        if (p.act == MDG_ACT_GELU) {
+          if (p.aux && m < M) st8(reinterpret_cast<bf16_t*>(p.aux) + (size_t)m * p.ldaux + n, v[u]);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[u][j] = gelu_fast(v[u][j]);
+        } else if (p.act == MDG_ACT_DGELU) {
+          const bf16x8 a = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const bf16_t*>(p.aux) +
+                                                            (size_t)min(m, M - 1) * p.ldaux + n);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[u][j] *= gelu_grad_fast((float)a[j]);
+        } else if (p.act == MDG_ACT_SILU) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[u][j] = silu(v[u][j]);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int m = m0 + r0 + RS * (u0 + u);
+        if (m >= M) break;
+        if (p.out_f32) {
+          float* o = reinterpret_cast<float*>(p.out) + (size_t)m * p.ldo + n;
+          *reinterpret_cast<float4*>(o) = make_float4(v[u][0], v[u][1], v[u][2], v[u][3]);
+          *reinterpret_cast<float4*>(o + 4) = make_float4(v[u][4], v[u][5], v[u][6], v[u][7]);
+        } else {
+          st8(reinterpret_cast<bf16_t*>(p.out) + (size_t)m * p.ldo + n, v[u]);
+        }
+      }
+    }
+  } else {  // MDG_EPI_QKV, D % 8 == 0: the 8 columns lie in one head of one of q | k | v
+    const int Cm = p.N / 3, D = p.D, half = D >> 1;
+    const int which = (n >= Cm) + (n >= 2 * Cm), w = n - which * Cm;
+    const int head = w / D, cp = w - head * D, pi = cp >> 1;  // 4 RoPE pairs pi .. pi+3
+    const float sc = (which == 0) ? p.qscale : 1.0f;
+    const bool rope = p.rope && which < 2, spatial = p.qkv_layout == MDG_QKV_SPATIAL;
+    const float invL = 1.0f / (float)p.L, invT = 1.0f / (float)p.T;
+    const int BL = (M / (p.T * p.L)) * p.L;
+    const int dp = p.qkv_layout == MDG_QKV_TEMPORAL_PACKED ? D : dp_of(D);
+    bf16_t* qo = reinterpret_cast<bf16_t*>(p.qkv_out);
+    const size_t colS = (size_t)(which * p.H + head) * D + cp;
+    const size_t colT = (size_t)which * BL * p.H * p.T * dp + (size_t)head * p.T * dp + cp;
+#pragma unroll
+    for (int u0 = 0; u0 < RPT; u0 += U) {
+      float4 cs[U], sn[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int m = min(m0 + r0 + RS * (u0 + u), M - 1);
+        const int ml = fdiv(m, p.L, invL), l = m - ml * p.L;
+        const int t = ml - fdiv(ml, p.T, invT) * p.T;
+        const int pos = spatial ? l : t;
+        cs[u] = sn[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (rope) {  // cos / sin of pairs pi..pi+3 (16-B aligned: half and pi are multiples of 4)
+          cs[u] = *reinterpret_cast<const float4*>(p.rope + (size_t)pos * half + pi);
+          sn[u] = *reinterpret_cast<const float4*>(p.rope + (size_t)(p.rope_rows + pos) * half + pi);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int row = r0 + RS * (u0 + u), m = m0 + row;
+        if (m >= M) break;
+        float v[8];
+        ld8s(row, v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] *= sc;
+        if (rope) {
+          const float cc[4] = {cs[u].x, cs[u].y, cs[u].z, cs[u].w}, ss[4] = {sn[u].x, sn[u].y, sn[u].z, sn[u].w};
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const float x = v[2 * k], y = v[2 * k + 1];
+            v[2 * k] = x * cc[k] - y * ss[k];
+            v[2 * k + 1] = y * cc[k] + x * ss[k];
+          }
+        }
+        size_t off;
+        if (spatial) {
+          off = (size_t)m * 3 * p.H * D + colS;
+        } else {
+          const int ml = fdiv(m, p.L, invL), l = m - ml * p.L;
+          const int b = fdiv(ml, p.T, invT), t = ml - b * p.T;
+          off = colT + ((size_t)(b * p.L + l) * p.H * p.T + t) * dp;
+        }
+        st8(qo + off, v);
+      }
+    }
+  }
+}
+
+template <int EPI, int BK, bool WIDE = false>  // WIDE: the 16-B-store epilogue (epi_tile8)
 __global__ __launch_bounds__(kB4Threads) void gemm_bf16_b4_kernel(const mdg_gemm_desc p) {
   constexpr int BM = kB4Tile, BN = kB4Tile, TILE = BM * BK, LDS_ST = BN + 4;
   constexpr int CPR = BK / 8;      // 16-B chunks per tile row
@@ -645,7 +768,10 @@ __global__ __launch_bounds__(kB4Threads) void gemm_bf16_b4_kernel(const mdg_gemm
             stage[((BANDS == 1 ? wm * 64 : 0) + i * 16 + lg * 4 + r) * LDS_ST + wn * 64 + j * 16 + lr] = acc[i][j][r];
     }
     __syncthreads();
-    epi_tile<EPI, kB4Threads, BROWS>(p, stage, m0 + band * BROWS, n0, tid);
+    if constexpr (WIDE && (EPI == MDG_EPI_STORE || EPI == MDG_EPI_QKV))
+      epi_tile8<EPI, kB4Threads, BROWS>(p, stage, m0 + band * BROWS, n0, tid);
+    else
+      epi_tile<EPI, kB4Threads, BROWS>(p, stage, m0 + band * BROWS, n0, tid);
     if (band + 1 < BANDS) __syncthreads();
   }
 }
@@ -655,18 +781,33 @@ __host__ __device__ constexpr size_t b4_smem() {
   return BK == 64 ? (size_t)kB4Tile * (kB4Tile + 4) * 4 : (size_t)(kB4Tile / 2) * (kB4Tile + 4) * 4;
 }
 
-template <int EPI, int BK>
-static hipError_t launch_b4(const mdg_gemm_desc& p, hipStream_t s) {
+template <int EPI, int BK, bool WIDE>
+static hipError_t launch_b4_v(const mdg_gemm_desc& p, hipStream_t s) {
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_bf16_b4_kernel<EPI, BK>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_bf16_b4_kernel<EPI, BK, WIDE>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)b4_smem<BK>());
     if (e != hipSuccess) return e;
     attr_set = true;
   }
   const int nwg = (p.N / kB4Tile) * ((p.M + kB4Tile - 1) / kB4Tile);
-  hipLaunchKernelGGL((gemm_bf16_b4_kernel<EPI, BK>), dim3(nwg), dim3(kB4Threads), b4_smem<BK>(), s, p);
+  hipLaunchKernelGGL((gemm_bf16_b4_kernel<EPI, BK, WIDE>), dim3(nwg), dim3(kB4Threads), b4_smem<BK>(), s, p);
   return hipGetLastError();
+}
+
+// the 16-B-store epilogue where its alignment holds (MDG_WIDE_EPI=0: the 8-B one, A/B knob)
+template <int EPI, int BK>
+static hipError_t launch_b4(const mdg_gemm_desc& p, hipStream_t s) {
+  static const bool knob = [] {
+    const char* e = getenv("MDG_WIDE_EPI");
+    return !(e && e[0] == '0');
+  }();
+  bool wide = false;
+  if constexpr (EPI == MDG_EPI_STORE) wide = p.ldo % 8 == 0 && (!p.aux || p.ldaux % 8 == 0);
+  if constexpr (EPI == MDG_EPI_QKV) wide = p.D % 8 == 0;
+  if constexpr (EPI == MDG_EPI_STORE || EPI == MDG_EPI_QKV)
+    if (wide && knob) return launch_b4_v<EPI, BK, true>(p, s);
+  return launch_b4_v<EPI, BK, false>(p, s);
 }
 
 // ---------------------------------------------------------------------------------------
