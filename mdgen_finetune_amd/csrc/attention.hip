@@ -277,15 +277,20 @@ __global__ __launch_bounds__(256) void attn_temporal_kernel(const CT* __restrict
 //   P = exp2(S^T) converted pairwise to bf16 IS the B operand of O^T = V^T P (the
 //     accumulator-as-operand map: element j of k-step s is key 16s + 8(j>>2) + 4h + (j&3)),
 //     and the matching V^T fragment is two ds_read_b64_tr_b16 of the plain [key][32] image;
-//   the softmax offset rides in the QK MFMA (K pad column D = 1, Q pad element = -mt) and is
-//   raised only when a score outgrows it by kGrow, so the common path is one v_exp_f32 per
-//   score plus a local max for the growth test; the row sum is O^T row D (V pad column = 1).
+//   the softmax offset rides in the QK MFMA (K pad column D = 1, Q pad element = -mt, mt =
+//   the bias key's score); the row sum is O^T row D (V pad column = 1).
+// Optimistic pass first: the offset is never raised and no score is tested, so the common
+// path is one v_exp_f32 and half a v_cvt_pk per score.  P is floating point, so a lagging
+// offset costs no precision unless something overflows (a score 128 above the bias key's, or
+// the f32 accumulators); the pass ends with a block-wide finiteness test of O^T and, when it
+// fails, the block reruns with the growth-tested offset (raised whenever a score outgrows it
+// by kGrow), the only path whose P stay bounded.
 typedef __attribute__((ext_vector_type(16))) float f32x16;
 
 // One 64-key sub-chunk of the bf16 temporal attention (K / V images of its 64 rows at Kc /
 // Vc, key-padding bias at kbsub): S^T = K Q^T (4 MFMAs), growth test / rare offset raise,
 // P = exp2(S^T) -> bf16 B operand, O^T += V^T P (4 MFMAs with tr-read V^T fragments).
-__device__ __forceinline__ void ta_subchunk(const bf16_t* Kc, const bf16_t* Vc, const float* kbsub, bool masked,
+__device__ __forceinline__ void ta_subchunk(const bf16_t* Kc, const bf16_t* Vc, const float* kbsub, bool masked, bool GROW,
                                             int r, int h, int grow, int gcol, int padS, int padH, int padJ,
                                             bf16x8 (&qf)[2], float& mt, f32x16& o) {
   constexpr int DP = MDG_DP;
@@ -310,11 +315,13 @@ __device__ __forceinline__ void ta_subchunk(const bf16_t* Kc, const bf16_t* Vc, 
       for (int i = 0; i < 16; ++i) sacc[kt][i] += kbsub[kt * 32 + (i & 3) + 8 * (i >> 2) + 4 * h];
   }
   float lm = sacc[0][0];
+  if (GROW) {  // block-uniform
 #pragma unroll
-  for (int kt = 0; kt < 2; ++kt)
+    for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-    for (int i = 0; i < 16; ++i) lm = fmaxf(lm, sacc[kt][i]);
-  if (__builtin_expect(__any(lm > kGrow), 0)) {
+      for (int i = 0; i < 16; ++i) lm = fmaxf(lm, sacc[kt][i]);
+  }
+  if (GROW && __builtin_expect(__any(lm > kGrow), 0)) {
     const float mx = fmaxf(lm, __shfl_xor(lm, 32, 64));
     const float nm = (mx > kGrow) ? (float)(bf16_t)(mt + mx) : mt;
     const float delta = nm - mt;
@@ -428,50 +435,59 @@ __global__ __launch_bounds__(kTW * 64, 4) void attn_temporal_bf16_kernel(const b
   __shared__ float kbs[2][KC];
   __shared__ int kflag[2][KC / 64];
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int r = lane & 31, h = lane >> 5;
-  // XCD-aware order (bijective remap of the 1-D grid): the query blocks of one (sequence,
-  // head) are consecutive on one XCD, so its K / V are fetched into that XCD's L2 once
-  const int nqb = (T + kTW * 32 - 1) / (kTW * 32), nwg = nqb * H * BL;
-  const int xcd = blockIdx.x & 7, loc = blockIdx.x >> 3, qq = nwg >> 3, r8 = nwg & 7;
-  const int wg = (xcd < r8 ? xcd * (qq + 1) : r8 * (qq + 1) + (xcd - r8) * qq) + loc;
-  const int qb = wg % nqb, head = (wg / nqb) % H, seq = wg / (nqb * H);
-  const int q0 = qb * (kTW * 32) + wave * 32;
-  const size_t plane = (size_t)BL * H * T * RS;
-  const bf16_t* Qg = qkv + ((size_t)seq * H + head) * T * RS;
-  const bf16_t* Kg = Qg + plane;
-  const bf16_t* Vg = Qg + 2 * plane;
-  const float* kb = kbias + (size_t)seq * T;
+  __shared__ int s_bad;
+  if (threadIdx.x == 0) s_bad = 0;  // published by the first chunk barrier
+  // The optimistic pass, and (rarely, block-uniform) the growth-tested rerun.  Every per-thread
+  // value is derived from an opaque copy of the thread index inside the attempt loop, so
+  // nothing but the loop counter lives across attempts (hoisted addresses spilled).
+  for (int attempt = 0;; ++attempt) {
+    const bool grow = attempt > 0;
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    const int lane = tid & 63, wave = tid >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    // XCD-aware order (bijective remap of the 1-D grid): the query blocks of one (sequence,
+    // head) are consecutive on one XCD, so its K / V are fetched into that XCD's L2 once
+    const int nqb = (T + kTW * 32 - 1) / (kTW * 32), nwg = nqb * H * BL;
+    const int xcd = blockIdx.x & 7, loc = blockIdx.x >> 3, qq = nwg >> 3, r8 = nwg & 7;
+    const int wg = (xcd < r8 ? xcd * (qq + 1) : r8 * (qq + 1) + (xcd - r8) * qq) + loc;
+    const int qb = wg % nqb, head = (wg / nqb) % H, seq = wg / (nqb * H);
+    const int q0 = qb * (kTW * 32) + wave * 32;
+    const size_t plane = (size_t)BL * H * T * RS;
+    const bf16_t* Qg = qkv + ((size_t)seq * H + head) * T * RS;
+    const bf16_t* Kg = Qg + plane;
+    const bf16_t* Vg = Qg + 2 * plane;
+    const float* kb = kbias + (size_t)seq * T;
 
-  const int q = q0 + r;
-  bf16x8 qf[2];
-  float mt;
-  f32x16 o;
-  ta_setup(Qg, kvb + head * 2 * DP, q, T, D, RS, r, h, qf, mt, o);
-  const int padS = D >> 4, padH = (D >> 3) & 1, padJ = D & 7;  // Q element holding -mt
+    const int q = q0 + r;
+    bf16x8 qf[2];
+    float mt;
+    f32x16 o;
+    ta_setup(Qg, kvb + head * 2 * DP, q, T, D, RS, r, h, qf, mt, o);
+    const int padS = D >> 4, padH = (D >> 3) & 1, padJ = D & 7;  // Q element holding -mt
 
-  // chunk staging: thread -> key row tid/4, 16-B piece tid%4 of K and of V
-  const int srow = tid >> 2, spc = tid & 3;
-  u32x4 kreg, vreg;
-  float kbreg = 0.f;
-  // packed planes: the pieces at and after column D are not in memory.  Their LDS slots (fixed
-  // per thread) are written once here -- 1.0 at column D for k (softmax offset) and v (row sum),
-  // zeros elsewhere, exactly the padded rows' content -- and never restaged (rows past T are
-  // masked by the -inf key bias, so their constant pad is harmless).
-  const bool real = !PACKED || spc * 8 < D;
-  if (PACKED && !real) {
-    u32x4 synth = u32x4{0u, 0u, 0u, 0u};
-    if (spc == (D >> 3)) {
-      const int e = D & 7;  // bf16 1.0 = 0x3F80 in half e & 1 of dword e >> 1
+    // chunk staging: thread -> key row tid/4, 16-B piece tid%4 of K and of V
+    const int srow = tid >> 2, spc = tid & 3;
+    u32x4 kreg, vreg;
+    float kbreg = 0.f;
+    // packed planes: the pieces at and after column D are not in memory.  Their LDS slots (fixed
+    // per thread) hold 1.0 at column D for k (softmax offset) and v (row sum), zeros elsewhere --
+    // exactly the padded rows' content -- written before the first chunk and never restaged
+    // (rows past T are masked by the -inf key bias, so their constant pad is harmless).
+    const bool real = !PACKED || spc * 8 < D;
+    if (PACKED && !real && !grow) {
+      u32x4 synth = u32x4{0u, 0u, 0u, 0u};
+      if (spc == (D >> 3)) {
+        const int e = D & 7;  // bf16 1.0 = 0x3F80 in half e & 1 of dword e >> 1
 #pragma unroll
-      for (int w = 0; w < 4; ++w) synth[w] = (w == (e >> 1)) ? (0x3F80u << (16 * (e & 1))) : 0u;
-    }
+        for (int w = 0; w < 4; ++w) synth[w] = (w == (e >> 1)) ? (0x3F80u << (16 * (e & 1))) : 0u;
+      }
 #pragma unroll
-    for (int bf = 0; bf < 2; ++bf) {
-      *reinterpret_cast<u32x4*>(&Ks[bf][srow * DP + ((spc ^ ((srow >> 3) & 3)) * 8)]) = synth;
-      *reinterpret_cast<u32x4*>(&Vs[bf][srow * DP + spc * 8]) = synth;
+      for (int bf = 0; bf < 2; ++bf) {
+        *reinterpret_cast<u32x4*>(&Ks[bf][srow * DP + ((spc ^ ((srow >> 3) & 3)) * 8)]) = synth;
+        *reinterpret_cast<u32x4*>(&Vs[bf][srow * DP + spc * 8]) = synth;
+      }
     }
-  }
 #define MDG_TA_GLOAD(c_)                                                                      \
   {                                                                                           \
     const int key = (c_) * KC + srow;                                                         \
@@ -498,32 +514,42 @@ __global__ __launch_bounds__(kTW * 64, 4) void attn_temporal_bf16_kernel(const b
     }                                                                                         \
   }
 
-  const int nchunks = (T + KC - 1) / KC;
-  MDG_TA_GLOAD(0);
-  MDG_TA_LSTORE(0);
-  __syncthreads();
-  // V^T tr-read lane geometry: 16-lane group g reads keys (+4h + i>>2), columns 16(g&1) + 4(i&3)
-  const int gi = lane & 15, gcol = 16 * ((lane >> 4) & 1) + 4 * (gi & 3), grow = 4 * h + (gi >> 2);
-  for (int c = 0; c < nchunks; ++c) {
-    const int cur = c & 1;
-    if (c + 1 < nchunks) MDG_TA_GLOAD(c + 1);
-    int mflag = 0;
-#pragma unroll
-    for (int f = 0; f < KC / 64; ++f) mflag |= kflag[cur][f];
-    const bool masked = mflag != 0;
-    const bf16_t* Kc = Ks[cur];
-    const bf16_t* Vc = Vs[cur];
-#pragma unroll
-    for (int sub = 0; sub < KC / 64; ++sub)
-      ta_subchunk(Kc + sub * 64 * DP, Vc + sub * 64 * DP, kbs[cur] + sub * 64, masked, r, h, grow, gcol, padS, padH,
-                  padJ, qf, mt, o);
-    if (c + 1 < nchunks) MDG_TA_LSTORE(cur ^ 1);
+    const int nchunks = (T + KC - 1) / KC;
+    // V^T tr-read lane geometry: 16-lane group g reads keys (+4h + i>>2), columns 16(g&1) + 4(i&3)
+    const int gi = lane & 15, gcol = 16 * ((lane >> 4) & 1) + 4 * (gi & 3), grow_r = 4 * h + (gi >> 2);
+    MDG_TA_GLOAD(0);
+    MDG_TA_LSTORE(0);
     __syncthreads();
-  }
+    for (int c = 0; c < nchunks; ++c) {
+      const int cur = c & 1;
+      if (c + 1 < nchunks) MDG_TA_GLOAD(c + 1);
+      int mflag = 0;
+#pragma unroll
+      for (int f = 0; f < KC / 64; ++f) mflag |= kflag[cur][f];
+      const bool masked = mflag != 0;
+      const bf16_t* Kc = Ks[cur];
+      const bf16_t* Vc = Vs[cur];
+#pragma unroll
+      for (int sub = 0; sub < KC / 64; ++sub)
+        ta_subchunk(Kc + sub * 64 * DP, Vc + sub * 64 * DP, kbs[cur] + sub * 64, masked, grow, r, h, grow_r, gcol,
+                    padS, padH, padJ, qf, mt, o);
+      if (c + 1 < nchunks) MDG_TA_LSTORE(cur ^ 1);
+      __syncthreads();
+    }
 #undef MDG_TA_GLOAD
 #undef MDG_TA_LSTORE
-
-  ta_store(o, out, q, T, L, H, D, seq, head, h, mt, lse);
+    if (!grow) {
+      bool bad = false;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) bad |= !__builtin_isfinite(o[i]);
+      if (__any(bad) && lane == 0) s_bad = 1;
+      __syncthreads();
+    }
+    if (grow || !s_bad) {  // block-uniform
+      ta_store(o, out, q, T, L, H, D, seq, head, h, mt, lse);
+      return;
+    }
+  }
 }
 
 

@@ -223,6 +223,38 @@ def test_attn_temporal(lib, dt, T):
         torch.testing.assert_close(got[0, :, :, h].permute(1, 0, 2), ref, rtol=rtol * 2, atol=atol * 2)
 
 
+@pytest.mark.parametrize("qmul", [4.0, 40.0])
+def test_attn_temporal_large_scores(lib, qmul):
+    """Scores far above the bias key's: x4 (up to ~100 in log2 units: the optimistic pass,
+    P up to ~2^100, stays finite) and x40 (overflows: the block reruns with the growth-tested
+    offset).  Both against the fp32 softmax of the same bf16 operands."""
+    from mdgen_finetune_amd import _lib
+
+    B, L, H, D, T = 1, 2, 4, 24, 700
+    BL = B * L
+    g = torch.Generator(device="cuda").manual_seed(int(qmul))
+    qkv = torch.zeros(3, BL, H, T, 32, device="cuda")
+    qkv[..., :D] = torch.randn(3, BL, H, T, D, device="cuda", generator=g)
+    qkv[0, ..., :D] *= qmul
+    qkv[1:, ..., D] = 1.0
+    qkv = qkv.to(torch.bfloat16)
+    kvb = torch.zeros(H, 2, 32, device="cuda")
+    kvb[:, :, :D] = 0.1 * torch.randn(H, 2, D, device="cuda", generator=g)
+    kvb[:, 1, D] = 1.0
+    kbias = torch.zeros(BL, T, device="cuda")
+    out = torch.zeros(B * T * L, H * D, device="cuda", dtype=torch.bfloat16)
+    _lib.check(lib.mdg_attn_temporal(1, B, T, L, H, D, qkv.data_ptr(), kbias.data_ptr(), kvb.data_ptr(),
+                                     out.data_ptr(), _s()), "attn_temporal")
+    qf = qkv.float()
+    got = out.float().reshape(B, T, L, H, D)
+    assert torch.isfinite(got).all()
+    for h in range(H):
+        ref = _attn_ref(qf[0, :, h, :, :D], qf[1, :, h, :, :D], qf[2, :, h, :, :D], kvb[h, 0, :D], kvb[h, 1, :D], torch.ones(BL, T, dtype=torch.bool, device="cuda"),
+                        base2=True)
+        rtol, atol = _tol("bf16")
+        torch.testing.assert_close(got[0, :, :, h].permute(1, 0, 2), ref, rtol=rtol * 2, atol=atol * 2)
+
+
 @pytest.mark.parametrize("T,D", [(1, 24), (63, 24), (1000, 24), (1300, 16), (129, 8)])
 def test_attn_temporal_packed_equals_padded(lib, T, D):
     """Packed planes (row stride D, pad column synthesised while staging) give the padded
