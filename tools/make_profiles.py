@@ -7,7 +7,9 @@
                                   reports half the bytes of 16-B/lane streaming reads,
                                   MI355X_MICROARCH.md §HBM); mean of the last 50 dispatches
                                   (the roofline timing loop).
-Usage: python tools/make_profiles.py RR [B T L]"""
+Usage: python tools/make_profiles.py RR [B T L]
+With a non-default B T L only the traffic of that shape (gpurun_out/pmc_roof_B_T_L, from
+ROOF_ARGS="B T L" bash tools/roof_pmc.sh) is merged into traffic_rRR.json."""
 import collections
 import csv
 import json
@@ -21,8 +23,10 @@ B, T, L = (int(a) for a in sys.argv[2:5]) if len(sys.argv) > 4 else (8, 1000, 4)
 out = os.path.join(REPO, "profiles")
 os.makedirs(out, exist_ok=True)
 
+default_shape = (B, T, L) == (8, 1000, 4)
+pmc_dir = os.path.join(REPO, "gpurun_out", "pmc_roof" if default_shape else f"pmc_roof_{B}_{T}_{L}")
 stats = os.path.join(REPO, "gpurun_out", "prof", "run_kernel_stats.csv")
-if os.path.exists(stats):
+if os.path.exists(stats) and default_shape:
     shutil.copy(stats, os.path.join(out, f"r{rr}_kernel_stats.csv"))
     rows = list(csv.DictReader(open(stats)))
     lines = [f"# r{rr}: rocprofv3 --kernel-trace --stats, `python bench.py --steps 3 --warmup 1 --no-cpu-baseline`",
@@ -74,10 +78,10 @@ KMAP = {"gemm_bf16_b4_kernel<2": "gemm_qkv_temporal", "attn_temporal_bf16": "att
         "gemm_rowln_kernel": "gemm_fc2_rowln"}
 res = collections.defaultdict(dict)
 for cname, scale in (("FETCH_SIZE", 2 * 1024), ("WRITE_SIZE", 1024)):
-    p = os.path.join(REPO, "gpurun_out", "pmc_roof", f"{cname}_counter_collection.csv")
+    p = os.path.join(pmc_dir, f"{cname}_counter_collection.csv")
     if not os.path.exists(p):
         continue
-    shutil.copy(p, os.path.join(out, f"r{rr}_pmc_{cname}.csv"))
+    shutil.copy(p, os.path.join(out, f"r{rr}_pmc_{cname}{'' if default_shape else f'_B{B}_T{T}_L{L}'}.csv"))
     by = collections.defaultdict(list)
     for r in csv.DictReader(open(p)):
         for pat, name in KMAP.items():
@@ -87,11 +91,14 @@ for cname, scale in (("FETCH_SIZE", 2 * 1024), ("WRITE_SIZE", 1024)):
         v.sort()
         last = [x[1] for x in v[-50:]]
         res[name][cname] = sum(last) / len(last) * scale
-traffic = {}
+tpath = os.path.join(out, f"traffic_r{rr}.json")
+traffic = {} if default_shape or not os.path.exists(tpath) else json.load(open(tpath))
 for name, d in res.items():
     if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
-        traffic[name] = {f"B{B}_T{T}_L{L}_bf16": round(d["FETCH_SIZE"] + d["WRITE_SIZE"]),
-                         "read_bytes": round(d["FETCH_SIZE"]), "write_bytes": round(d["WRITE_SIZE"])}
+        e = traffic.setdefault(name, {})
+        e[f"B{B}_T{T}_L{L}_bf16"] = round(d["FETCH_SIZE"] + d["WRITE_SIZE"])
+        sfx = "" if default_shape else f"_B{B}_T{T}_L{L}"
+        e["read_bytes" + sfx], e["write_bytes" + sfx] = round(d["FETCH_SIZE"]), round(d["WRITE_SIZE"])
 if traffic:
-    json.dump(traffic, open(os.path.join(out, f"traffic_r{rr}.json"), "w"), indent=1)
+    json.dump(traffic, open(tpath, "w"), indent=1)
 print(json.dumps(traffic, indent=1))

@@ -4,10 +4,12 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-mkdir -p gpurun_out/pmc_roof
+# ROOF_ARGS="B T L" selects another shape (e.g. "1 250 256", ATLAS), written to pmc_roof_B_T_L
+D=gpurun_out/pmc_roof${ROOF_ARGS:+_${ROOF_ARGS// /_}}
+mkdir -p $D
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 400 rocprofv3 --pmc $C --kernel-include-regex "gemm_bf16_b4|attn_temporal_bf16|gemm_rowln" \
-    --output-format csv -d gpurun_out/pmc_roof -o $C -- python tools/roof_kernels.py \
-    > gpurun_out/pmc_roof/log_$C.txt 2>&1 || exit $?
+    --output-format csv -d $D -o $C -- python tools/roof_kernels.py ${ROOF_ARGS:-} \
+    > $D/log_$C.txt 2>&1 || exit $?
 done
 echo done
