@@ -1122,7 +1122,9 @@ __global__ __launch_bounds__(kRowThreads, BM == 64 ? 4 : 1) void gemm_rowln_kern
 #pragma unroll
     for (int e = 0; e < NE; ++e)
       b4[e] = p.bias ? *reinterpret_cast<const float4*>(p.bias + 4 * hl + 128 * e) : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll 1
+#pragma unroll
+    // unrolled: a rolled band loop made the next band's prefetch conditional, and on the merged
+    // path the compiler drained it with s_waitcnt vmcnt(0) before the current band's first use
     for (int band = 0; band < BM / 32; ++band) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();  // previous band's stage reads (and the adaLN rows) are done
