@@ -74,8 +74,8 @@ __global__ void add_inplace_kernel(size_t n, float* __restrict__ y, const float*
   if (i < n) y[i] += x[i];
 }
 
-// One block (one wave) per (sample r, head h); thread = query residue, keys staged in LDS in
-// chunks of 64 with an online softmax.  proj row layout (ldp floats per residue, ipa.py:113-152):
+// One block (one wave) per (sample r, head h, group of 64 query residues); thread = query
+// residue, keys staged in LDS in chunks of 64 with an online softmax.  proj row layout (ldp floats per residue, ipa.py:113-152):
 //   q [h*CH + i] | kv [H*CH + h*2CH + {0..CH-1: k, CH..2CH-1: v}] |
 //   q_pts raw [3][H*PQ] (x block, y block, z block; point j = h*PQ + p) |
 //   kv_pts raw [3][H*(PQ+PV)] (point j = h*(PQ+PV) + p; p < PQ: k, else v)
@@ -89,7 +89,9 @@ __global__ __launch_bounds__(64) void ipa_attn_kernel(int R, int B, int L, int H
   constexpr int KW = 2 * CH + 3 * PQ + 3 * PV;  // floats per staged key
   __shared__ float ks[64][KW + 1];
   __shared__ float mk[64];
-  const int r = blockIdx.x / H, h = blockIdx.x - r * H, b = r % B, tid = threadIdx.x;
+  const int nqg = (L + 63) / 64;
+  const int r = blockIdx.x / (H * nqg), hq = blockIdx.x - r * (H * nqg), h = hq / nqg, b = r % B, tid = threadIdx.x;
+  const int i0 = (hq - h * nqg) * 64;
   const int HPq = H * PQ, HPkv = H * (PQ + PV);
   const int oqp = 3 * H * CH, okvp = oqp + 3 * HPq;
   // softplus(head_weights) * sqrt(1 / (3 * (P_q * 9 / 2)))  (ipa.py:180-185)
@@ -100,7 +102,7 @@ __global__ __launch_bounds__(64) void ipa_attn_kernel(int R, int B, int L, int H
   const float* tr_b = trans + (size_t)b * L * 3;
   const float* mask_r = mask + (size_t)r * L;  // sample-replicated frame mask [R][L]
 
-  for (int i0 = 0; i0 < L; i0 += 64) {
+  {
     const int i = i0 + tid;
     const bool qv = i < L;
     const int ii = qv ? i : L - 1;
@@ -242,7 +244,7 @@ bool ipa_attn_supported(int c, int pq, int pv) {
 hipError_t ipa_attn_launch(int R, int B, int L, int H, int c, int pq, int pv, const float* proj, int ldp,
                            const float* rots, const float* trans, const float* mask, const float* head_weights,
                            float* out, int ldc, hipStream_t s) {
-  const dim3 grid((unsigned)(R * H)), block(64);
+  const dim3 grid((unsigned)(R * H * ((L + 63) / 64))), block(64);
 #define MDG_IPA(CH_, PQ_, PV_)                                                                              \
   if (c == CH_ && pq == PQ_ && pv == PV_) {                                                                 \
     hipLaunchKernelGGL((ipa_attn_kernel<CH_, PQ_, PV_>), grid, block, 0, s, R, B, L, H, proj, ldp, rots, trans, \
