@@ -2,8 +2,10 @@
 95-114) restated in mdgen_finetune_amd/transport/integrators.py.  torchdiffeq is absent, so
 parity with torchdiffeq itself is unpinned; these tests pin the algorithm's properties:
 convergence to analytic solutions at the solver's order, the saved grid, the step-size
-controller, and the drop-in Sampler wiring with the model on the eager backend (the HIP
-side is in tests/test_gpu_parity.py)."""
+controller, the drop-in Sampler wiring with the model on the eager backend (the HIP side is
+in tests/test_gpu_parity.py), and agreement with scipy's independent Runge-Kutta
+implementations (RK45 = the same Dormand-Prince pair, DOP853 as the tight reference) on a
+nonlinear system and on the model's own velocity field."""
 import functools
 import math
 
@@ -117,3 +119,63 @@ def test_sampler_dopri5_with_model_matches_tight_solve():
 def test_unknown_sampler_is_refused():
     with pytest.raises(NotImplementedError):
         Sampler(create_transport(None, "GVP")).sample_ode(sampling_method="rk4")
+
+
+def _vdp(t, y, mu=1.5):
+    # Van der Pol, y = [..., 2]: a nonlinear, mildly stiff test problem
+    x, v = y[..., 0], y[..., 1]
+    return torch.stack([v, mu * (1 - x * x) * v - x], -1)
+
+
+@pytest.mark.parametrize("rtol", [1e-5, 1e-8])
+def test_matches_scipy_runge_kutta_on_van_der_pol(rtol):
+    """An independent implementation of the same Dormand-Prince 5(4) pair (scipy RK45) and a
+    higher-order one (DOP853) at tight tolerance: the restated solver lands on the same
+    trajectory to its tolerance (float64, 3 initial states, 40 saved points)."""
+    from scipy.integrate import solve_ivp
+
+    y0 = torch.tensor([[2.0, 0.0], [0.5, -1.0], [-1.5, 0.7]], dtype=torch.float64)
+    t = torch.linspace(0, 3, 40, dtype=torch.float64)
+    ours = odeint_dopri5(_vdp, y0, t, rtol=rtol, atol=rtol * 1e-2)
+    for b in range(3):
+        ref = solve_ivp(lambda tt, yy: _vdp(tt, torch.from_numpy(yy)).numpy(), (0.0, 3.0), y0[b].numpy(),
+                        method="DOP853", t_eval=t.numpy(), rtol=1e-12, atol=1e-14)
+        rk45 = solve_ivp(lambda tt, yy: _vdp(tt, torch.from_numpy(yy)).numpy(), (0.0, 3.0), y0[b].numpy(),
+                         method="RK45", t_eval=t.numpy(), rtol=rtol, atol=rtol * 1e-2)
+        err_ours = np.abs(ours[:, b].numpy() - ref.y.T).max()
+        err_rk45 = np.abs(rk45.y.T - ref.y.T).max()
+        # same pair, same tolerance: same accuracy class as scipy's RK45 (within 10x either way)
+        assert err_ours < 50 * rtol, (err_ours, rtol)
+        assert err_ours < 10 * max(err_rk45, 1e-3 * rtol), (err_ours, err_rk45)
+
+
+def test_model_field_matches_scipy_dop853():
+    """dopri5 at the reference's tolerances (rtol 1e-3, atol 1e-6; transport.py:410-413) on the
+    model's own velocity field (eager backend, float64) against scipy's DOP853 at rtol 1e-8
+    (~1000 field evaluations, ~8 s)."""
+    from scipy.integrate import solve_ivp
+
+    d, cfg = load_golden("small_sim_T8")
+    m, _ = build_model(cfg)
+    m.backend = "torch"
+    m = m.double()
+    from tests.test_model_cpu import _kw
+
+    kw = {k: (v.double() if torch.is_tensor(v) and v.is_floating_point() else v) for k, v in _kw(d).items()}
+    zs = torch.from_numpy(d["in_zs"]).double()
+    shape = zs.shape
+    t = torch.linspace(0, 1, 50, dtype=torch.float64)
+
+    def field(tt, y):
+        return m.forward_inference(y, torch.ones(shape[0], dtype=torch.float64) * tt, **kw)
+
+    with torch.no_grad():
+        ours = odeint_dopri5(field, zs, t, rtol=1e-3, atol=1e-6)
+        assert ours.shape[0] == 50
+        ref = solve_ivp(lambda tt, yy: field(torch.tensor(tt, dtype=torch.float64),
+                                             torch.from_numpy(yy).reshape(shape)).reshape(-1).numpy(),
+                        (0.0, 1.0), zs.reshape(-1).numpy(), method="DOP853", rtol=1e-8, atol=1e-10)
+    ref_end = torch.from_numpy(ref.y[:, -1]).reshape(shape)
+    scale = ref_end.abs().max().item()
+    err = (ours[-1] - ref_end).abs().max().item()
+    assert err < 1e-2 * max(scale, 1.0), (err, scale)
