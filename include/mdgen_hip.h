@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define MDG_ABI_VERSION 12
+#define MDG_ABI_VERSION 13
 #define MDG_MAX_LAYERS 16
 #define MDG_DP 32      /* padded head dim of the attention operand buffers for head_dim <= 31 */
 #define MDG_DP_WIDE 64 /* ... and for 32 <= head_dim <= 63 (column head_dim of the padded k / v rows
@@ -198,6 +198,12 @@ int mdg_describe_plan(const mdg_dims* d, char* buf, size_t n);
 
 /* Building blocks (exposed for unit tests and for the conditioning precompute). */
 int mdg_gemm(const mdg_gemm_desc* g, void* stream);
+/* The block's MLP as ONE kernel (latent_model.py:488-491): fc1 = PLAIN STORE + GELU (its out is
+   not written: the hidden activation stays on chip), fc2 = PLAIN GATE_RES (+ the LayerNorm
+   hand-off; its A is not read), the descriptors exactly as for mdg_gemm(fc1) then
+   mdg_gemm(fc2).  bf16, C == fc1.K == fc2.N == 384, F == fc1.N == fc2.K a multiple of 128,
+   fc2.rows_per_mod >= 128, no training outputs; MDG_E_SHAPE otherwise. */
+int mdg_mlp_fused(const mdg_gemm_desc* fc1, const mdg_gemm_desc* fc2, void* stream);
 /* qkv: CT [n_frames*L][3][H][D] (unpadded q | k | v rows of each token) */
 int mdg_attn_spatial(int32_t dtype, int32_t n_frames, int32_t L, int32_t H, int32_t D,
                      const void* qkv, const float* kvb, const float* mask, void* out,

@@ -18,6 +18,8 @@ struct GemmPlan {
 };
 GemmPlan gemm_plan(const mdg_gemm_desc& p);
 hipError_t gemm_launch(const mdg_gemm_desc& p, const GemmPlan& g, hipStream_t s);
+bool mlp_fused_supported(const mdg_gemm_desc& f1, const mdg_gemm_desc& f2);
+hipError_t mlp_fused_launch(const mdg_gemm_desc& f1, const mdg_gemm_desc& f2, hipStream_t s);
 hipError_t attn_temporal_launch(int dtype, int B, int T, int L, int H, int D, const void* qkv_t,
                                 const float* kbias, const float* kvb, void* out, hipStream_t s,
                                 float* lse = nullptr, bool packed = false);
@@ -118,6 +120,16 @@ bool packed_planes(const mdg_dims& d) {
     return !(e && e[0] == '0');
   }();
   return on && d.dtype == MDG_BF16 && d.D % 8 == 0 && d.D < MDG_DP;
+}
+
+// bf16, C = 384: the block's MLP as one kernel (hidden activation on chip); MDG_FUSED_MLP=0
+// keeps fc1 + fc2 (A/B knob)
+bool fused_mlp_on() {
+  static const bool on = [] {
+    const char* e = getenv("MDG_FUSED_MLP");
+    return !(e && e[0] == '0');
+  }();
+  return on;
 }
 
 struct WsLayout {
@@ -465,7 +477,6 @@ static int layer_fwd_impl(const mdg_dims* d, const mdg_layer_weights* w, const f
   f1.epi = MDG_EPI_STORE; f1.act = MDG_ACT_GELU;
   f1.N = F; f1.K = C; f1.A = xn; f1.lda = C; f1.W = w->w1; f1.ldw = C; f1.bias = w->b1;
   f1.out = hid; f1.ldo = F;
-  if (int e = mdg_gemm(&f1, stream)) return e;
   mdg_gemm_desc f2 = g;
   f2.epi = MDG_EPI_GATE_RES;
   f2.N = C; f2.K = F; f2.A = hid; f2.lda = F; f2.W = w->w2; f2.ldw = F; f2.bias = w->b2;
@@ -474,7 +485,19 @@ static int layer_fwd_impl(const mdg_dims* d, const mdg_layer_weights* w, const f
     f2.xn_out = xn; f2.xn_mods = ho.next_mods; f2.xn_mod_stride = ho.next_stride;
     f2.xn_shift_off = ho.next_shift; f2.xn_scale_off = ho.next_scale; f2.ln_eps = 1e-6f;
   }
+  if (fuse && fused_mlp_on() && mdg::mlp_fused_supported(f1, f2))
+    return hip_check(mdg::mlp_fused_launch(f1, f2, (hipStream_t)stream), "mlp fused launch");
+  if (int e = mdg_gemm(&f1, stream)) return e;
   return mdg_gemm(&f2, stream);
+}
+
+int mdg_mlp_fused(const mdg_gemm_desc* f1, const mdg_gemm_desc* f2, void* stream) {
+  if (!f1 || !f2) return fail(MDG_E_ARG, "mlp_fused: null descriptor");
+  if (!f1->A || !f1->W || !f2->W || !f2->resid) return fail(MDG_E_ARG, "mlp_fused: null pointer");
+  if (!mdg::mlp_fused_supported(*f1, *f2))
+    return fail(MDG_E_SHAPE, "mlp_fused: outside the envelope (bf16, K=N=384, F %% 128, rows_per_mod >= 128) "
+                "M=%d C=%d F=%d", f1->M, f1->K, f1->N);
+  return hip_check(mdg::mlp_fused_launch(*f1, *f2, (hipStream_t)stream), "mlp fused launch");
 }
 
 int mdg_layer_fwd(const mdg_dims* d, const mdg_layer_weights* w, const float* rope_l,
@@ -565,7 +588,7 @@ int mdg_describe_plan(const mdg_dims* d, char* buf, size_t n) {
     spatial = "qkv_gemm(spatial layout)+attn_spatial(valu)";
   snprintf(buf, n,
            "{\"dtype\": \"%s\", \"spatial\": \"%s\", \"ln_handoff\": \"%s\", "
-           "\"temporal\": \"qkv_gemm+%s\", \"planes\": \"%s\", \"mlp\": \"fc1_gemm(gelu)+%s\", "
+           "\"temporal\": \"qkv_gemm+%s\", \"planes\": \"%s\", \"mlp\": \"%s\", "
            "\"final\": \"euler_epilogue_gemm\"}",
            d->dtype == MDG_BF16 ? "bf16" : "f32", spatial,
            fuse ? "fused into gated-residual row-LN GEMM epilogues" : "stand-alone ln_mod pass",
@@ -573,7 +596,10 @@ int mdg_describe_plan(const mdg_dims* d, char* buf, size_t n) {
                                                   : "attn_temporal(wide heads: f32 16x16x4 mfma, 64-col rows)")
            : d->dtype == MDG_BF16 ? "attn_temporal_bf16(32x32x16 mfma)" : "attn_temporal(f32 16x16x4 mfma)",
            packed_planes(*d) ? "packed (row stride = head_dim)" : "padded (row stride MDG_HEAD_STRIDE)",
-           fuse ? "fc2_rowln_gemm" : "fc2_gate_res_gemm");
+           (fuse && fused_mlp_on() && d->dtype == MDG_BF16 && d->C == 384 && d->T * d->L >= 128)
+               ? "mlp_fused(fc1+gelu+fc2+gated residual+LN in one kernel, hidden on chip)"
+           : fuse ? "fc1_gemm(gelu)+fc2_rowln_gemm"
+                  : "fc1_gemm(gelu)+fc2_gate_res_gemm");
   return MDG_OK;
 }
 

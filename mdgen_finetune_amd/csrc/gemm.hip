@@ -956,6 +956,146 @@ __host__ __device__ constexpr size_t rowln_smem() {
   return (size_t)RowCfg<BM>::STAGES * (BM + NCOL) * 32 * 2;
 }
 
+// The row-LN fast epilogue (BM 128, 8 waves as 2 x 4, the tile spans <= 2 adaLN entries):
+// shared by gemm_rowln_kernel and the fused MLP kernel.  acc = the waves' 64 x NCOL/4
+// accumulator tiles; h4 = band 0's residual rows (rowln_load_band), already in flight.
+template <int NCOL>
+__device__ __forceinline__ void rowln_load_band(const mdg_gemm_desc& p, int m0, int u, float4 (&h4)[2][NCOL / 128]) {
+  constexpr int NE = NCOL / 128;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, half = lane >> 5, hl = lane & 31;
+#pragma unroll
+  for (int pr = 0; pr < 2; ++pr) {
+    const int m = min(m0 + u * 32 + wave * 4 + 2 * pr + half, p.M - 1);
+    const float* hr = p.resid + (size_t)m * p.ldr + 4 * hl;
+#pragma unroll
+    for (int e = 0; e < NE; ++e) h4[pr][e] = *reinterpret_cast<const float4*>(hr + 128 * e);
+  }
+}
+
+template <int NCOL>
+__device__ __forceinline__ void rowln_fast_epilogue(const mdg_gemm_desc& p, f32x4 (&acc)[4][NCOL / 64],
+                                                    float4 (&h4)[2][NCOL / 128], unsigned char* smem, int m0,
+                                                    int b_lo, float inv_rpm) {
+  constexpr int BM = 128, WTN = NCOL / 4, NT = WTN / 16, LDS_ST = NCOL + 4, NE = NCOL / 128;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wm = wave / 4, wn = wave % 4;
+  const int lr = lane & 15, lg = lane >> 4, half = lane >> 5, hl = lane & 31;
+  const int M = p.M;
+  const int b_hi = fdiv(min(m0 + BM - 1, M - 1), p.rows_per_mod, inv_rpm);
+  float* stage = reinterpret_cast<float*>(smem);
+  const float invN = 1.0f / (float)NCOL;
+  auto load_unit4 = [&](int u, float4 (&hb)[2][NE]) { rowln_load_band<NCOL>(p, m0, u, hb); };
+  float* emods = stage + 32 * LDS_ST;  // [2][3][NCOL]: gate | xn scale | xn shift
+  // the caller's smem holds (32 * LDS_ST + 6 * NCOL) floats: the band stage + the adaLN rows
+  static_assert(LDS_ST % 4 == 0, "16-B aligned stage rows");
+  __builtin_amdgcn_s_barrier();  // every wave is done reading the ring (its loads were all waited)
+  for (int i = tid; i < 6 * NCOL; i += kRowThreads) {
+    const int eb = i / (3 * NCOL), w = (i / NCOL) % 3, k = i % NCOL;
+    const size_t b = (size_t)min(b_lo + eb, b_hi);
+    float v;
+    if (w == 0) v = p.gate ? p.gate[b * p.mod_stride + p.gate_off + k] : 1.0f;
+    else if (w == 1) v = p.xn_out ? p.xn_mods[b * p.xn_mod_stride + p.xn_scale_off + k] : 0.0f;
+    else v = p.xn_out ? p.xn_mods[b * p.xn_mod_stride + p.xn_shift_off + k] : 0.0f;
+    emods[i] = v;
+  }
+  float4 b4[NE];
+#pragma unroll
+  for (int e = 0; e < NE; ++e)
+    b4[e] = p.bias ? *reinterpret_cast<const float4*>(p.bias + 4 * hl + 128 * e) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  // unrolled: a rolled band loop made the next band's prefetch conditional, and on the merged
+  // path the compiler drained it with s_waitcnt vmcnt(0) before the current band's first use
+  for (int band = 0; band < BM / 32; ++band) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // previous band's stage reads (and the adaLN rows) are done
+    if (wm == (band >> 1)) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if ((i >> 1) != (band & 1)) continue;
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            stage[((i & 1) * 16 + lg * 4 + r) * LDS_ST + wn * WTN + j * 16 + lr] = acc[i][j][r];
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    float4 hn[2][NE];
+    if (band + 1 < BM / 32) load_unit4(band + 1, hn);
+    float sum[2];
+    int eb[2];
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr) {
+      const int m = m0 + band * 32 + wave * 4 + 2 * pr + half;
+      eb[pr] = fdiv(min(m, M - 1), p.rows_per_mod, inv_rpm) - b_lo;
+      const float* srow = stage + (wave * 4 + 2 * pr + half) * LDS_ST + 4 * hl;
+      const float* gr = emods + eb[pr] * 3 * NCOL + 4 * hl;
+      float sacc = 0.f;
+#pragma unroll
+      for (int e = 0; e < NE; ++e) {
+        const float4 v = *reinterpret_cast<const float4*>(srow + 128 * e);
+        const float4 g = *reinterpret_cast<const float4*>(gr + 128 * e);
+        float4& h = h4[pr][e];
+        h.x += g.x * (v.x + b4[e].x);
+        h.y += g.y * (v.y + b4[e].y);
+        h.z += g.z * (v.z + b4[e].z);
+        h.w += g.w * (v.w + b4[e].w);
+        sacc += (h.x + h.y) + (h.z + h.w);
+      }
+      sum[pr] = sacc;
+      if (m < M) {
+        float* hr = p.resid + (size_t)m * p.ldr + 4 * hl;
+#pragma unroll
+        for (int e = 0; e < NE; ++e) *reinterpret_cast<float4*>(hr + 128 * e) = h4[pr][e];
+      }
+    }
+    if (p.xn_out) {
+      // row sums over each half-wave (32 lanes)
+#pragma unroll
+      for (int o = 16; o >= 1; o >>= 1)
+#pragma unroll
+        for (int pr = 0; pr < 2; ++pr) sum[pr] += __shfl_xor(sum[pr], o, 64);
+      float ss[2];
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr) {
+        sum[pr] *= invN;  // mean
+        float t = 0.f;
+#pragma unroll
+        for (int e = 0; e < NE; ++e) {
+          const float4 h = h4[pr][e];
+          const float a0 = h.x - sum[pr], a1 = h.y - sum[pr], a2 = h.z - sum[pr], a3 = h.w - sum[pr];
+          t += (a0 * a0 + a1 * a1) + (a2 * a2 + a3 * a3);
+        }
+        ss[pr] = t;
+      }
+#pragma unroll
+      for (int o = 16; o >= 1; o >>= 1)
+#pragma unroll
+        for (int pr = 0; pr < 2; ++pr) ss[pr] += __shfl_xor(ss[pr], o, 64);
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr) {
+        const int m = m0 + band * 32 + wave * 4 + 2 * pr + half;
+        const float rs = 1.0f / sqrtf(ss[pr] * invN + p.ln_eps);
+        const float* mr = emods + eb[pr] * 3 * NCOL + 4 * hl;
+#pragma unroll
+        for (int e = 0; e < NE; ++e) {
+          const float4 xs = *reinterpret_cast<const float4*>(mr + NCOL + 128 * e);
+          const float4 xh = *reinterpret_cast<const float4*>(mr + 2 * NCOL + 128 * e);
+          const float4 h = h4[pr][e];
+          if (m < M)
+            st4<bf16_t>(reinterpret_cast<bf16_t*>(p.xn_out) + (size_t)m * NCOL + 4 * hl + 128 * e,
+                        (h.x - sum[pr]) * rs * (1.0f + xs.x) + xh.x, (h.y - sum[pr]) * rs * (1.0f + xs.y) + xh.y,
+                        (h.z - sum[pr]) * rs * (1.0f + xs.z) + xh.z, (h.w - sum[pr]) * rs * (1.0f + xs.w) + xh.w);
+        }
+      }
+    }
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr)
+#pragma unroll
+      for (int e = 0; e < NE; ++e) h4[pr][e] = hn[pr][e];
+  }
+}
+
 template <int NCOL, int BM>
 __global__ __launch_bounds__(kRowThreads, BM == 64 ? 4 : 1) void gemm_rowln_kernel(const mdg_gemm_desc p) {
   constexpr int kRowStages = RowCfg<BM>::STAGES, WMW = RowCfg<BM>::WMW, WNW = 8 / WMW;
@@ -1035,19 +1175,9 @@ __global__ __launch_bounds__(kRowThreads, BM == 64 ? 4 : 1) void gemm_rowln_kern
     b_hi = fdiv(min(m0 + BM - 1, M - 1), p.rows_per_mod, inv_rpm);
   }
   const bool fast = BM == 128 && b_hi - b_lo < 2;
-  const int half = lane >> 5, hl = lane & 31;
-  auto load_unit4 = [&](int u, float4 (&h4)[2][NE]) {
-#pragma unroll
-    for (int pr = 0; pr < 2; ++pr) {
-      const int m = min(m0 + u * 32 + wave * 4 + 2 * pr + half, M - 1);
-      const float* hr = p.resid + (size_t)m * p.ldr + 4 * hl;
-#pragma unroll
-      for (int e = 0; e < NE; ++e) h4[pr][e] = *reinterpret_cast<const float4*>(hr + 128 * e);
-    }
-  };
   float4 h4[2][NE];
   float2 hv[RG][NE], gv[NE];
-  if (fast) load_unit4(0, h4);
+  if (fast) rowln_load_band<NCOL>(p, m0, 0, h4);
   else if (BM == 64) load_unit(0, hv, gv);
 
   f32x4 acc[4][NT];
@@ -1104,118 +1234,12 @@ __global__ __launch_bounds__(kRowThreads, BM == 64 ? 4 : 1) void gemm_rowln_kern
   // trajectory -- made the compiler drain every outstanding store and prefetch with
   // s_waitcnt vmcnt(0) on every row.)  The band barriers are raw s_barrier after an LDS wait:
   // they order the stage buffer only, so the h / xn stores stay in flight across them.
-  if (fast) {
-    float* emods = stage + 32 * LDS_ST;  // [2][3][NCOL]: gate | xn scale | xn shift
-    static_assert(BM != 128 || (32 * LDS_ST + 6 * NCOL) * 4 <= kRowStages * STAGE * 2, "adaLN rows fit the ring");
-    static_assert(LDS_ST % 4 == 0, "16-B aligned stage rows");
-    __builtin_amdgcn_s_barrier();  // every wave is done reading the ring (its loads were all waited)
-    for (int i = tid; i < 6 * NCOL; i += kRowThreads) {
-      const int eb = i / (3 * NCOL), w = (i / NCOL) % 3, k = i % NCOL;
-      const size_t b = (size_t)min(b_lo + eb, b_hi);
-      float v;
-      if (w == 0) v = p.gate ? p.gate[b * p.mod_stride + p.gate_off + k] : 1.0f;
-      else if (w == 1) v = p.xn_out ? p.xn_mods[b * p.xn_mod_stride + p.xn_scale_off + k] : 0.0f;
-      else v = p.xn_out ? p.xn_mods[b * p.xn_mod_stride + p.xn_shift_off + k] : 0.0f;
-      emods[i] = v;
+  if constexpr (BM == 128) {
+    static_assert((32 * LDS_ST + 6 * NCOL) * 4 <= kRowStages * STAGE * 2, "adaLN rows fit the ring");
+    if (fast) {
+      rowln_fast_epilogue<NCOL>(p, acc, h4, smem, m0, b_lo, inv_rpm);
+      return;
     }
-    float4 b4[NE];
-#pragma unroll
-    for (int e = 0; e < NE; ++e)
-      b4[e] = p.bias ? *reinterpret_cast<const float4*>(p.bias + 4 * hl + 128 * e) : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-    // unrolled: a rolled band loop made the next band's prefetch conditional, and on the merged
-    // path the compiler drained it with s_waitcnt vmcnt(0) before the current band's first use
-    for (int band = 0; band < BM / 32; ++band) {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();  // previous band's stage reads (and the adaLN rows) are done
-      if (wm == (band >> 1)) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          if ((i >> 1) != (band & 1)) continue;
-#pragma unroll
-          for (int j = 0; j < NT; ++j)
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-              stage[((i & 1) * 16 + lg * 4 + r) * LDS_ST + wn * WTN + j * 16 + lr] = acc[i][j][r];
-        }
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      float4 hn[2][NE];
-      if (band + 1 < BM / 32) load_unit4(band + 1, hn);
-      float sum[2];
-      int eb[2];
-#pragma unroll
-      for (int pr = 0; pr < 2; ++pr) {
-        const int m = m0 + band * 32 + wave * 4 + 2 * pr + half;
-        eb[pr] = fdiv(min(m, M - 1), p.rows_per_mod, inv_rpm) - b_lo;
-        const float* srow = stage + (wave * 4 + 2 * pr + half) * LDS_ST + 4 * hl;
-        const float* gr = emods + eb[pr] * 3 * NCOL + 4 * hl;
-        float sacc = 0.f;
-#pragma unroll
-        for (int e = 0; e < NE; ++e) {
-          const float4 v = *reinterpret_cast<const float4*>(srow + 128 * e);
-          const float4 g = *reinterpret_cast<const float4*>(gr + 128 * e);
-          float4& h = h4[pr][e];
-          h.x += g.x * (v.x + b4[e].x);
-          h.y += g.y * (v.y + b4[e].y);
-          h.z += g.z * (v.z + b4[e].z);
-          h.w += g.w * (v.w + b4[e].w);
-          sacc += (h.x + h.y) + (h.z + h.w);
-        }
-        sum[pr] = sacc;
-        if (m < M) {
-          float* hr = p.resid + (size_t)m * p.ldr + 4 * hl;
-#pragma unroll
-          for (int e = 0; e < NE; ++e) *reinterpret_cast<float4*>(hr + 128 * e) = h4[pr][e];
-        }
-      }
-      if (p.xn_out) {
-        // row sums over each half-wave (32 lanes)
-#pragma unroll
-        for (int o = 16; o >= 1; o >>= 1)
-#pragma unroll
-          for (int pr = 0; pr < 2; ++pr) sum[pr] += __shfl_xor(sum[pr], o, 64);
-        float ss[2];
-#pragma unroll
-        for (int pr = 0; pr < 2; ++pr) {
-          sum[pr] *= invN;  // mean
-          float t = 0.f;
-#pragma unroll
-          for (int e = 0; e < NE; ++e) {
-            const float4 h = h4[pr][e];
-            const float a0 = h.x - sum[pr], a1 = h.y - sum[pr], a2 = h.z - sum[pr], a3 = h.w - sum[pr];
-            t += (a0 * a0 + a1 * a1) + (a2 * a2 + a3 * a3);
-          }
-          ss[pr] = t;
-        }
-#pragma unroll
-        for (int o = 16; o >= 1; o >>= 1)
-#pragma unroll
-          for (int pr = 0; pr < 2; ++pr) ss[pr] += __shfl_xor(ss[pr], o, 64);
-#pragma unroll
-        for (int pr = 0; pr < 2; ++pr) {
-          const int m = m0 + band * 32 + wave * 4 + 2 * pr + half;
-          const float rs = 1.0f / sqrtf(ss[pr] * invN + p.ln_eps);
-          const float* mr = emods + eb[pr] * 3 * NCOL + 4 * hl;
-#pragma unroll
-          for (int e = 0; e < NE; ++e) {
-            const float4 xs = *reinterpret_cast<const float4*>(mr + NCOL + 128 * e);
-            const float4 xh = *reinterpret_cast<const float4*>(mr + 2 * NCOL + 128 * e);
-            const float4 h = h4[pr][e];
-            if (m < M)
-              st4<bf16_t>(reinterpret_cast<bf16_t*>(p.xn_out) + (size_t)m * NCOL + 4 * hl + 128 * e,
-                          (h.x - sum[pr]) * rs * (1.0f + xs.x) + xh.x, (h.y - sum[pr]) * rs * (1.0f + xs.y) + xh.y,
-                          (h.z - sum[pr]) * rs * (1.0f + xs.z) + xh.z, (h.w - sum[pr]) * rs * (1.0f + xs.w) + xh.w);
-          }
-        }
-      }
-#pragma unroll
-      for (int pr = 0; pr < 2; ++pr)
-#pragma unroll
-        for (int e = 0; e < NE; ++e) h4[pr][e] = hn[pr][e];
-    }
-    return;
   }
   if (BM == 128) load_unit(0, hv, gv);  // the rare tile over > 2 entries: no prefetch under the K loop
   __syncthreads();  // all waves are done with the ring
@@ -1352,6 +1376,201 @@ static hipError_t launch_rowln(const mdg_gemm_desc& p, hipStream_t s) {
   }
   hipLaunchKernelGGL((gemm_rowln_kernel<NCOL, BM>), dim3((p.M + BM - 1) / BM), dim3(kRowThreads),
                      (rowln_smem<NCOL, BM>()), s, p);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// Fused MLP (latent_model.py:488-491): x += gate_m * fc2(gelu(fc1(xn))) and the next LN, the
+// hidden activation never leaving the CU.  Block = 128 token rows (one block per CU, 8 waves),
+// the hidden dimension in chunks of 128: per chunk 12 fc1 K-steps (Hc^T = W1c . xn^T, 64
+// hidden x 32 tokens per wave, acc1) -> bias + GELU -> bf16 chunk Hc [128 tokens][128] in LDS
+// -> 4 fc2 K-steps (acc2 += Hc . W2c^T, 64 tokens x 96 outputs per wave, the row-LN layout)
+// -> after the last chunk the row-LN epilogue.  Every K-step's operand slice (xn + W1c rows,
+// or W2 rows) streams through one 4-slot global_load_lds ring with counted vmcnt (2 or 3
+// pieces per wave per step).  The fc1 product is computed transposed so a lane's accumulator
+// holds 4 consecutive hidden units of one token: one 8-B LDS write per 4 GELU outputs.  The
+// K order of both products is the unfused GEMMs' (ascending in 32s).
+struct MlpArgs {
+  mdg_gemm_desc f1, f2;
+};
+constexpr int kMlpThreads = 512, kMlpHC = 128, kMlpStages = 4, kMlpSlot = 384 * 32;
+
+__host__ __device__ constexpr size_t mlp_smem(int F) {
+  return (size_t)kMlpStages * kMlpSlot * 2 + (size_t)128 * kMlpHC * 2 + (size_t)F * 4;
+}
+
+// s_waitcnt vmcnt(n) for a wave-uniform n in [0, 6]
+__device__ __forceinline__ void vm_wait_upto6(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+  }
+}
+
+template <int NCOL>
+__global__ __launch_bounds__(kMlpThreads, 1) void mlp_rowln_kernel(const MlpArgs args) {
+  static_assert(NCOL == 384, "the ring slot holds 384 W2 rows");
+  constexpr int BM = 128, BK = 32, HC = kMlpHC, STAGES = kMlpStages, SLOT = kMlpSlot;
+  constexpr int WTN = NCOL / 4, NT = WTN / 16, NE = NCOL / 128, LDS_ST = NCOL + 4;
+  static_assert((32 * LDS_ST + 6 * NCOL) * 4 <= STAGES * SLOT * 2, "epilogue stage + adaLN rows fit the ring");
+  typedef __attribute__((address_space(3))) void* lds_ptr_t;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const mdg_gemm_desc& q = args.f1;  // xn, W1, b1
+  const mdg_gemm_desc& p = args.f2;  // W2, b2 and the row-LN epilogue
+  bf16_t* ring = reinterpret_cast<bf16_t*>(smem);
+  bf16_t* Hs = ring + STAGES * SLOT;                    // [BM][HC]: 16-B chunk c of row r at c ^ (r & 15)
+  float* b1s = reinterpret_cast<float*>(Hs + BM * HC);  // [F]
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / 4, wn = wave % 4;    // fc2: 64 tokens x WTN outputs
+  const int wah = wave / 4, wat = wave % 4;  // fc1: 64 hidden x 32 tokens
+  const int lr = lane & 15, lg = lane >> 4;
+  const int M = p.M, F = p.K;
+  const int NS = (F / HC) * 16;  // 12 fc1 + 4 fc2 K-steps per hidden chunk
+  const int nwg = (M + BM - 1) / BM;
+  const int xcd = blockIdx.x & 7, loc = blockIdx.x >> 3, q8 = nwg >> 3, r8 = nwg & 7;
+  const int m0 = ((xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc) * BM;
+
+  for (int i = tid; i < F; i += kMlpThreads) b1s[i] = q.bias ? q.bias[i] : 0.f;
+  // ring loader: slot row r's 16-B chunk c at c ^ ((-(r >> 2)) & 3); a 16-row piece per glds
+  const int cswz = ((lane & 3) ^ ((-(lane >> 4)) & 3)) * 8;
+  const bf16_t* X = reinterpret_cast<const bf16_t*>(q.A);
+  const bf16_t* W1 = reinterpret_cast<const bf16_t*>(q.W);
+  const bf16_t* W2 = reinterpret_cast<const bf16_t*>(p.W);
+  // fc1 step: waves 0-3 stage xn rows 16(2w + i) + lane/4, waves 4-7 the chunk's W1 rows (slot
+  // rows 128 + ...); fc2 step: wave w stages W2 rows 16(3w + i) + lane/4
+  // (element offsets from wave-uniform bases: one 64-bit address per lane is rebuilt per issue
+  // instead of five held across the loop)
+  const bool xw = wave < 4;
+  const bf16_t* abase = xw ? X : W1;
+  const int ald = xw ? q.lda : q.ldw;
+  int aoff[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r = 16 * (2 * (wave & 3) + i) + (lane >> 2);
+    aoff[i] = (xw ? min(m0 + r, M - 1) : r) * ald + cswz;
+  }
+  const int boff = (16 * 3 * wave + (lane >> 2)) * p.ldw + cswz, bstep = 16 * p.ldw;
+  auto issue = [&](int s) {
+    bf16_t* sl = ring + (s % STAGES) * SLOT;
+    const int j = s >> 4, t = s & 15;
+    if (t < 12) {
+      const bf16_t* base = abase + (size_t)t * BK + (xw ? (size_t)0 : (size_t)j * HC * q.ldw);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        __builtin_amdgcn_global_load_lds((const void*)(base + aoff[i]),
+                                         (lds_ptr_t)(sl + ((xw ? 0 : BM) + 16 * (2 * (wave & 3) + i)) * BK), 16, 0, 0);
+    } else {
+      const bf16_t* base = W2 + j * HC + (t - 12) * BK;
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+        __builtin_amdgcn_global_load_lds((const void*)(base + boff + i * bstep), (lds_ptr_t)(sl + 16 * (3 * wave + i) * BK),
+                                         16, 0, 0);
+    }
+  };
+
+  f32x4 acc2[4][NT], acc1[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc2[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc1[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  const int ch = (lg ^ ((-(lr >> 2)) & 3)) * 8;
+#pragma unroll
+  for (int s0 = 0; s0 < STAGES - 1; ++s0)
+    if (s0 < NS) issue(s0);
+  // step s landed: leave the (up to 2) younger steps' pieces in flight; then refill the slot
+  // every wave has finished reading (step s - 1's) with step s + 3
+  auto step_begin = [&](int s) {
+    const int y1 = s + 1 < NS ? (((s + 1) & 15) < 12 ? 2 : 3) : 0;
+    const int y2 = s + 2 < NS ? (((s + 2) & 15) < 12 ? 2 : 3) : 0;
+    vm_wait_upto6(y1 + y2);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (s + STAGES - 1 < NS) issue(s + STAGES - 1);
+    return ring + (s % STAGES) * SLOT;
+  };
+  // (the fc1 and fc2 step bodies are separate loops: one loop with a branch per step made the
+  // compiler give the accumulators different registers on the two paths)
+  for (int j = 0; j < NS / 16; ++j) {
+    for (int t = 0; t < 12; ++t) {
+      const bf16_t* sl = step_begin(j * 16 + t);
+      bf16x8 a[4], b[2];
+#pragma unroll
+      for (int hi = 0; hi < 4; ++hi) a[hi] = *reinterpret_cast<const bf16x8*>(sl + (BM + wah * 64 + hi * 16 + lr) * BK + ch);
+#pragma unroll
+      for (int ti = 0; ti < 2; ++ti) b[ti] = *reinterpret_cast<const bf16x8*>(sl + (wat * 32 + ti * 16 + lr) * BK + ch);
+#pragma unroll
+      for (int hi = 0; hi < 4; ++hi)
+#pragma unroll
+        for (int ti = 0; ti < 2; ++ti) acc1[hi][ti] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[hi], b[ti], acc1[hi][ti], 0, 0, 0);
+    }
+    // the chunk's fc1 is complete: + b1, GELU, bf16 -> Hs; restart acc1.  (Hs was last read by
+    // chunk j - 1's fc2 steps, which every wave finished before this chunk's first barrier.)
+    const float* b1c = b1s + j * HC;
+#pragma unroll
+    for (int hi = 0; hi < 4; ++hi)
+#pragma unroll
+      for (int ti = 0; ti < 2; ++ti) {
+        const int hb = wah * 64 + hi * 16 + lg * 4, tok = wat * 32 + ti * 16 + lr;
+        bf16x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = (bf16_t)gelu_fast(acc1[hi][ti][r] + b1c[hb + r]);
+        *reinterpret_cast<bf16x4*>(Hs + tok * HC + (((hb >> 3) ^ (tok & 15)) * 8) + (hb & 7)) = o;
+        acc1[hi][ti] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // Hs complete before the next barrier
+    for (int kb = 0; kb < 4; ++kb) {
+      const bf16_t* sl = step_begin(j * 16 + 12 + kb);
+      bf16x8 a[4], b[NT];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = wm * 64 + i * 16 + lr;
+        a[i] = *reinterpret_cast<const bf16x8*>(Hs + row * HC + (((kb * 4 + lg) ^ (row & 15)) * 8));
+      }
+#pragma unroll
+      for (int jn = 0; jn < NT; ++jn) b[jn] = *reinterpret_cast<const bf16x8*>(sl + (wn * WTN + jn * 16 + lr) * BK + ch);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int jn = 0; jn < NT; ++jn) acc2[i][jn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[jn], acc2[i][jn], 0, 0, 0);
+    }
+  }
+  const float inv_rpm = 1.0f / (float)p.rows_per_mod;
+  float4 h4[2][NE];
+  rowln_load_band<NCOL>(p, m0, 0, h4);  // band 0's residual rows
+  rowln_fast_epilogue<NCOL>(p, acc2, h4, smem, m0, fdiv(m0, p.rows_per_mod, inv_rpm), inv_rpm);
+}
+
+// The fused MLP's shape envelope: bf16, C = 384, F % 128 == 0, fc1 = PLAIN STORE + GELU, fc2 =
+// PLAIN GATE_RES whose tiles span <= 2 adaLN entries (rows_per_mod >= 128), no training outputs.
+bool mlp_fused_supported(const mdg_gemm_desc& f1, const mdg_gemm_desc& f2) {
+  return f1.dtype == MDG_BF16 && f2.dtype == MDG_BF16 && f1.a_mode == MDG_A_PLAIN && f2.a_mode == MDG_A_PLAIN &&
+         f1.epi == MDG_EPI_STORE && f1.act == MDG_ACT_GELU && f2.epi == MDG_EPI_GATE_RES && f1.K == 384 &&
+         f2.N == 384 && f1.N == f2.K && f1.N % kMlpHC == 0 && f1.N >= kMlpHC && f1.M == f2.M && f1.M > 0 &&
+         f2.rows_per_mod >= 128 && f2.resid && !f2.resid_in && !f2.aux && !f1.aux && f1.lda % 8 == 0 &&
+         f1.ldw % 8 == 0 && f2.ldw % 8 == 0 && f2.ldr % 4 == 0 && (!f2.xn_out || f2.xn_mods) && mlp_smem(f1.N) <= 160 * 1024;
+}
+
+hipError_t mlp_fused_launch(const mdg_gemm_desc& f1, const mdg_gemm_desc& f2, hipStream_t s) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&mlp_rowln_kernel<384>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  MlpArgs a;
+  a.f1 = f1;
+  a.f2 = f2;
+  hipLaunchKernelGGL((mlp_rowln_kernel<384>), dim3((f1.M + 127) / 128), dim3(kMlpThreads), mlp_smem(f1.N), s, a);
   return hipGetLastError();
 }
 

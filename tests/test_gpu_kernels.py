@@ -118,6 +118,69 @@ def test_gemm_gate_res_fused_layernorm(lib, N, K, M):
     torch.testing.assert_close(xn.float(), xref, rtol=2e-2, atol=2e-2)
 
 
+@pytest.mark.parametrize("M,TL,with_ln", [(512, 256, True), (4000, 4000, True), (300, 150, True), (1000, 200, False)])
+def test_mlp_fused_equals_fc1_then_fc2(lib, M, TL, with_ln):
+    """mdg_mlp_fused (fc1 + GELU + fc2 + gated residual + next LN in one kernel, the hidden
+    activation on chip) against the same two descriptors through mdg_gemm: h and xn
+    bit-identical (same K order, same GELU, same bf16 rounding of the hidden activation), and
+    against torch.  Partial last tiles (M % 128 != 0) and tiles spanning two trajectories."""
+    from mdgen_finetune_amd import _lib
+
+    C, F = 384, 1536
+    g = torch.Generator(device="cuda").manual_seed(M + TL)
+    xn = torch.randn(M, C, device="cuda", generator=g).to(torch.bfloat16)
+    W1 = (torch.randn(F, C, device="cuda", generator=g) / math.sqrt(C)).to(torch.bfloat16)
+    b1 = torch.randn(F, device="cuda", generator=g) * 0.5
+    W2 = (torch.randn(C, F, device="cuda", generator=g) / math.sqrt(F)).to(torch.bfloat16)
+    b2 = torch.randn(C, device="cuda", generator=g)
+    nb = (M + TL - 1) // TL
+    mods = torch.randn(nb, 9 * C, device="cuda", generator=g) * 0.5
+    nmods = torch.randn(nb, 2 * C, device="cuda", generator=g) * 0.5
+    h0 = torch.randn(M, C, device="cuda", generator=g) * 2
+    hid = torch.zeros(M, F, device="cuda", dtype=torch.bfloat16)
+    outs = []
+    for fused in (False, True):
+        h = h0.clone()
+        xo = torch.zeros(M, C, device="cuda", dtype=torch.bfloat16)
+        f1 = _desc(dtype=1, a_mode=0, epi=0, act=1, M=M, N=F, K=C, A=xn.data_ptr(), lda=C, W=W1.data_ptr(), ldw=C,
+                   bias=b1.data_ptr(), out=hid.data_ptr(), ldo=F)
+        kw = dict(xn_out=xo.data_ptr(), xn_mods=nmods.data_ptr(), xn_mod_stride=2 * C, xn_shift_off=0,
+                  xn_scale_off=C, ln_eps=1e-6) if with_ln else {}
+        f2 = _desc(dtype=1, a_mode=0, epi=1, M=M, N=C, K=F, A=hid.data_ptr(), lda=F, W=W2.data_ptr(), ldw=F,
+                   bias=b2.data_ptr(), mod_stride=9 * C, rows_per_mod=TL, resid=h.data_ptr(), ldr=C,
+                   gate=mods.data_ptr(), gate_off=8 * C, **kw)
+        if fused:
+            _lib.check(lib.mdg_mlp_fused(ctypes.byref(f1), ctypes.byref(f2), _s()), "mdg_mlp_fused")
+        else:
+            _lib.check(lib.mdg_gemm(ctypes.byref(f1), _s()), "fc1")
+            _lib.check(lib.mdg_gemm(ctypes.byref(f2), _s()), "fc2")
+        outs.append((h, xo))
+    torch.cuda.synchronize()
+    (h_ref, x_ref), (h_f, x_f) = outs
+    b = torch.arange(M, device="cuda") // TL
+    pre = xn.float() @ W1.float().T + b1
+    hidden = (pre * 0.5 * (1 + torch.erf(pre / math.sqrt(2)))).to(torch.bfloat16).float()
+    href = h0 + mods[b, 8 * C:9 * C] * (hidden @ W2.float().T + b2)
+    torch.testing.assert_close(h_f, href, rtol=5e-3, atol=5e-3)
+    if with_ln:  # the unfused fc2 ran the same row-LN epilogue
+        assert torch.equal(h_f, h_ref), (h_f - h_ref).abs().max().item()
+        assert torch.equal(x_f, x_ref), (x_f.float() - x_ref.float()).abs().max().item()
+    else:  # (without the LN hand-off the unfused fc2 takes the tile GEMM's gated-residual epilogue)
+        torch.testing.assert_close(h_f, h_ref, rtol=1e-6, atol=1e-5)
+        assert not x_f.any()
+
+
+def test_mlp_fused_rejects_unsupported_shapes(lib):
+    d1 = _desc(dtype=1, a_mode=0, epi=0, act=1, M=256, N=1536, K=256, A=1, lda=256, W=1, ldw=256)
+    d2 = _desc(dtype=1, a_mode=0, epi=1, M=256, N=256, K=1536, A=1, lda=1536, W=1, ldw=1536, resid=1, ldr=256,
+               rows_per_mod=256)
+    assert lib.mdg_mlp_fused(ctypes.byref(d1), ctypes.byref(d2), _s()) == 1001  # MDG_E_SHAPE: C != 384
+    d1.K = d2.N = 384
+    d1.lda = d2.ldr = 384
+    d2.rows_per_mod = 64  # tiles over > 2 trajectories
+    assert lib.mdg_mlp_fused(ctypes.byref(d1), ctypes.byref(d2), _s()) == 1001
+
+
 def _rope_ref(x, pos, inv_freq):
     # x [..., D] at integer positions pos [...]
     half = x.shape[-1] // 2
