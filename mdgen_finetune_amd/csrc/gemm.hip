@@ -1382,18 +1382,19 @@ static hipError_t launch_rowln(const mdg_gemm_desc& p, hipStream_t s) {
 // ---------------------------------------------------------------------------------------
 // Fused MLP (latent_model.py:488-491): x += gate_m * fc2(gelu(fc1(xn))) and the next LN, the
 // hidden activation never leaving the CU.  Block = 128 token rows (one block per CU, 8 waves),
-// the hidden dimension in chunks of 128: per chunk 12 fc1 K-steps (Hc^T = W1c . xn^T, 64
-// hidden x 32 tokens per wave, acc1) -> bias + GELU -> bf16 chunk Hc [128 tokens][128] in LDS
-// -> 4 fc2 K-steps (acc2 += Hc . W2c^T, 64 tokens x 96 outputs per wave, the row-LN layout)
-// -> after the last chunk the row-LN epilogue.  Every K-step's operand slice (xn + W1c rows,
-// or W2 rows) streams through one 4-slot global_load_lds ring with counted vmcnt (2 or 3
-// pieces per wave per step).  The fc1 product is computed transposed so a lane's accumulator
-// holds 4 consecutive hidden units of one token: one 8-B LDS write per 4 GELU outputs.  The
-// K order of both products is the unfused GEMMs' (ascending in 32s).
+// the hidden dimension in chunks of 128: per chunk 6 fc1 K-steps of 64 (Hc^T = W1c . xn^T,
+// 64 hidden x 32 tokens per wave, acc1) -> bias + GELU -> bf16 chunk Hc [128 tokens][128] in
+// LDS -> 4 fc2 K-steps of 32 (acc2 += Hc . W2c^T, 64 tokens x 96 outputs per wave, the row-LN
+// layout) -> after the last chunk the row-LN epilogue.  Every K-step's operand slice (xn +
+// W1c rows as two 32-wide images, or W2 rows) streams through one 3-slot global_load_lds ring
+// with counted vmcnt (4 or 3 pieces per wave per step, one barrier per step).  The fc1 product
+// is computed transposed so a lane's accumulator holds 4 consecutive hidden units of one
+// token: one 8-B LDS write per 4 GELU outputs.  The K order of both products is the unfused
+// GEMMs' (ascending in 32s), so the result equals fc1 then fc2 bit for bit.
 struct MlpArgs {
   mdg_gemm_desc f1, f2;
 };
-constexpr int kMlpThreads = 512, kMlpHC = 128, kMlpStages = 4, kMlpSlot = 384 * 32;
+constexpr int kMlpThreads = 512, kMlpHC = 128, kMlpStages = 3, kMlpSlot = 512 * 32;
 
 __host__ __device__ constexpr size_t mlp_smem(int F) {
   return (size_t)kMlpStages * kMlpSlot * 2 + (size_t)128 * kMlpHC * 2 + (size_t)F * 4;
@@ -1431,7 +1432,7 @@ __global__ __launch_bounds__(kMlpThreads, 1) void mlp_rowln_kernel(const MlpArgs
   const int wah = wave / 4, wat = wave % 4;  // fc1: 64 hidden x 32 tokens
   const int lr = lane & 15, lg = lane >> 4;
   const int M = p.M, F = p.K;
-  const int NS = (F / HC) * 16;  // 12 fc1 + 4 fc2 K-steps per hidden chunk
+  const int NS = (F / HC) * 10;  // 6 fc1 (K 64) + 4 fc2 (K 32) steps per hidden chunk
   const int nwg = (M + BM - 1) / BM;
   const int xcd = blockIdx.x & 7, loc = blockIdx.x >> 3, q8 = nwg >> 3, r8 = nwg & 7;
   const int m0 = ((xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc) * BM;
@@ -1442,10 +1443,10 @@ __global__ __launch_bounds__(kMlpThreads, 1) void mlp_rowln_kernel(const MlpArgs
   const bf16_t* X = reinterpret_cast<const bf16_t*>(q.A);
   const bf16_t* W1 = reinterpret_cast<const bf16_t*>(q.W);
   const bf16_t* W2 = reinterpret_cast<const bf16_t*>(p.W);
-  // fc1 step: waves 0-3 stage xn rows 16(2w + i) + lane/4, waves 4-7 the chunk's W1 rows (slot
-  // rows 128 + ...); fc2 step: wave w stages W2 rows 16(3w + i) + lane/4
-  // (element offsets from wave-uniform bases: one 64-bit address per lane is rebuilt per issue
-  // instead of five held across the loop)
+  // fc1 step (k0 = 64 t): two 32-wide images of 256 slot rows each (xn rows, then the chunk's
+  // W1 rows): waves 0-3 stage xn rows 16(2w + i) + lane/4, waves 4-7 W1 rows (slot rows
+  // 128 + ...), in both images; fc2 step: wave w stages W2 rows 16(3w + i) + lane/4.
+  // (Element offsets from wave-uniform bases: one 64-bit address per lane is rebuilt per issue.)
   const bool xw = wave < 4;
   const bf16_t* abase = xw ? X : W1;
   const int ald = xw ? q.lda : q.ldw;
@@ -1456,17 +1457,21 @@ __global__ __launch_bounds__(kMlpThreads, 1) void mlp_rowln_kernel(const MlpArgs
     aoff[i] = (xw ? min(m0 + r, M - 1) : r) * ald + cswz;
   }
   const int boff = (16 * 3 * wave + (lane >> 2)) * p.ldw + cswz, bstep = 16 * p.ldw;
+  constexpr int IMG = 2 * BM * BK;  // one 32-wide image of the fc1 step (xn + W1c rows)
   auto issue = [&](int s) {
     bf16_t* sl = ring + (s % STAGES) * SLOT;
-    const int j = s >> 4, t = s & 15;
-    if (t < 12) {
-      const bf16_t* base = abase + (size_t)t * BK + (xw ? (size_t)0 : (size_t)j * HC * q.ldw);
+    const int j = s / 10, t = s % 10;
+    if (t < 6) {
+      const bf16_t* base = abase + (size_t)t * 2 * BK + (xw ? (size_t)0 : (size_t)j * HC * q.ldw);
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
-        __builtin_amdgcn_global_load_lds((const void*)(base + aoff[i]),
-                                         (lds_ptr_t)(sl + ((xw ? 0 : BM) + 16 * (2 * (wave & 3) + i)) * BK), 16, 0, 0);
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          __builtin_amdgcn_global_load_lds((const void*)(base + h * BK + aoff[i]),
+                                           (lds_ptr_t)(sl + h * IMG + ((xw ? 0 : BM) + 16 * (2 * (wave & 3) + i)) * BK),
+                                           16, 0, 0);
     } else {
-      const bf16_t* base = W2 + j * HC + (t - 12) * BK;
+      const bf16_t* base = W2 + j * HC + (t - 6) * BK;
 #pragma unroll
       for (int i = 0; i < 3; ++i)
         __builtin_amdgcn_global_load_lds((const void*)(base + boff + i * bstep), (lds_ptr_t)(sl + 16 * (3 * wave + i) * BK),
@@ -1486,12 +1491,11 @@ __global__ __launch_bounds__(kMlpThreads, 1) void mlp_rowln_kernel(const MlpArgs
 #pragma unroll
   for (int s0 = 0; s0 < STAGES - 1; ++s0)
     if (s0 < NS) issue(s0);
-  // step s landed: leave the (up to 2) younger steps' pieces in flight; then refill the slot
-  // every wave has finished reading (step s - 1's) with step s + 3
+  // step s landed: leave step s+1's pieces in flight; then refill the slot every wave has
+  // finished reading (step s-1's) with step s+2
   auto step_begin = [&](int s) {
-    const int y1 = s + 1 < NS ? (((s + 1) & 15) < 12 ? 2 : 3) : 0;
-    const int y2 = s + 2 < NS ? (((s + 2) & 15) < 12 ? 2 : 3) : 0;
-    vm_wait_upto6(y1 + y2);
+    const int y1 = s + 1 < NS ? ((s + 1) % 10 < 6 ? 4 : 3) : 0;
+    vm_wait_upto6(y1);
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (s + STAGES - 1 < NS) issue(s + STAGES - 1);
@@ -1499,18 +1503,22 @@ __global__ __launch_bounds__(kMlpThreads, 1) void mlp_rowln_kernel(const MlpArgs
   };
   // (the fc1 and fc2 step bodies are separate loops: one loop with a branch per step made the
   // compiler give the accumulators different registers on the two paths)
-  for (int j = 0; j < NS / 16; ++j) {
-    for (int t = 0; t < 12; ++t) {
-      const bf16_t* sl = step_begin(j * 16 + t);
-      bf16x8 a[4], b[2];
+  for (int j = 0; j < NS / 10; ++j) {
+    for (int t = 0; t < 6; ++t) {
+      const bf16_t* sl = step_begin(j * 10 + t);
 #pragma unroll
-      for (int hi = 0; hi < 4; ++hi) a[hi] = *reinterpret_cast<const bf16x8*>(sl + (BM + wah * 64 + hi * 16 + lr) * BK + ch);
+      for (int h = 0; h < 2; ++h) {
+        bf16x8 a[4], b[2];
 #pragma unroll
-      for (int ti = 0; ti < 2; ++ti) b[ti] = *reinterpret_cast<const bf16x8*>(sl + (wat * 32 + ti * 16 + lr) * BK + ch);
+        for (int hi = 0; hi < 4; ++hi)
+          a[hi] = *reinterpret_cast<const bf16x8*>(sl + h * IMG + (BM + wah * 64 + hi * 16 + lr) * BK + ch);
 #pragma unroll
-      for (int hi = 0; hi < 4; ++hi)
+        for (int ti = 0; ti < 2; ++ti) b[ti] = *reinterpret_cast<const bf16x8*>(sl + h * IMG + (wat * 32 + ti * 16 + lr) * BK + ch);
 #pragma unroll
-        for (int ti = 0; ti < 2; ++ti) acc1[hi][ti] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[hi], b[ti], acc1[hi][ti], 0, 0, 0);
+        for (int hi = 0; hi < 4; ++hi)
+#pragma unroll
+          for (int ti = 0; ti < 2; ++ti) acc1[hi][ti] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[hi], b[ti], acc1[hi][ti], 0, 0, 0);
+      }
     }
     // the chunk's fc1 is complete: + b1, GELU, bf16 -> Hs; restart acc1.  (Hs was last read by
     // chunk j - 1's fc2 steps, which every wave finished before this chunk's first barrier.)
@@ -1528,7 +1536,7 @@ __global__ __launch_bounds__(kMlpThreads, 1) void mlp_rowln_kernel(const MlpArgs
       }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // Hs complete before the next barrier
     for (int kb = 0; kb < 4; ++kb) {
-      const bf16_t* sl = step_begin(j * 16 + 12 + kb);
+      const bf16_t* sl = step_begin(j * 10 + 6 + kb);
       bf16x8 a[4], b[NT];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {

@@ -56,8 +56,38 @@ def run(M, N, K, a_mode, epi, dt="bf16", act=0, rowln=False):
           f"torch.matmul {ref:8.1f} us ({fl/ref/1e6:7.1f} TF/s)", flush=True)
 
 
+def run_mlp(M, C=384, F=1536, rpm=4000):
+    """mdg_mlp_fused vs mdg_gemm(fc1) + mdg_gemm(fc2) (row-LN hand-off) on one lane's shape."""
+    A = (torch.randn(M, C, device="cuda") * 0.5).to(torch.bfloat16)
+    W1 = (torch.randn(F, C, device="cuda") / C ** 0.5).to(torch.bfloat16)
+    W2 = (torch.randn(C, F, device="cuda") / F ** 0.5).to(torch.bfloat16)
+    b1, b2 = torch.randn(F, device="cuda"), torch.randn(C, device="cuda")
+    hid = torch.empty(M, F, device="cuda", dtype=torch.bfloat16)
+    resid, xn = torch.zeros(M, C, device="cuda"), torch.empty(M, C, device="cuda", dtype=torch.bfloat16)
+    mods = torch.randn(M // rpm + 1, 9 * C, device="cuda") * 0.1
+    f1, f2 = _lib.MdgGemmDesc(), _lib.MdgGemmDesc()
+    f1.dtype, f1.a_mode, f1.epi, f1.act, f1.M, f1.N, f1.K = 1, 0, 0, 1, M, F, C
+    f1.A, f1.lda, f1.W, f1.ldw, f1.bias, f1.out, f1.ldo = A.data_ptr(), C, W1.data_ptr(), C, b1.data_ptr(), hid.data_ptr(), F
+    f2.dtype, f2.a_mode, f2.epi, f2.M, f2.N, f2.K = 1, 0, 1, M, C, F
+    f2.A, f2.lda, f2.W, f2.ldw, f2.bias = hid.data_ptr(), F, W2.data_ptr(), F, b2.data_ptr()
+    f2.resid, f2.ldr, f2.gate, f2.gate_off, f2.mod_stride, f2.rows_per_mod = resid.data_ptr(), C, mods.data_ptr(), 0, 9 * C, rpm
+    f2.xn_out, f2.xn_mods, f2.xn_mod_stride, f2.xn_shift_off, f2.xn_scale_off, f2.ln_eps = (xn.data_ptr(), mods.data_ptr(),
+                                                                                           9 * C, 0, C, 1e-6)
+    s = torch.cuda.current_stream().cuda_stream
+    fused = tm(lambda: _lib.check(lib.mdg_mlp_fused(ctypes.byref(f1), ctypes.byref(f2), s), "mlp"))
+    t1 = tm(lambda: _lib.check(lib.mdg_gemm(ctypes.byref(f1), s), "fc1"))
+    t2 = tm(lambda: _lib.check(lib.mdg_gemm(ctypes.byref(f2), s), "fc2"))
+    fl = 4.0 * M * C * F
+    print(f"mlp M={M}: mdg fused {fused:8.1f} us ({fl / fused / 1e6:7.1f} TF/s)   fc1 {t1:7.1f} + fc2 {t2:7.1f} = "
+          f"{t1 + t2:7.1f} us", flush=True)
+
+
 if __name__ == "__main__":
     import sys as _s
+    if len(_s.argv) > 1 and _s.argv[1] == "mlp":
+        for M in (32000, 64000):
+            run_mlp(M)
+        _s.exit(0)
     if len(_s.argv) > 1 and _s.argv[1] == "rowln":  # fused gated residual + LN (out_proj / fc2)
         for M in (32000, 64000):
             for K in (384, 1536):
