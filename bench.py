@@ -17,10 +17,11 @@ Multi-GPU: inference does not shard (temporal attention couples all T frames of 
 trajectory), so N ranks run N independent replicas of the window ("replicas only",
 scaling "weak"); no collective on the data path.
 
-Extra fields: "roofline" for the dominant kernel (gemm_rowln_kernel, the gated-residual +
-LayerNorm-epilogue GEMM, 34 % of the step per profiles/; quoted on its largest launch, fc2;
-live HIP-event timing on the stream the kernel runs on), "roofline_more" for the next two
-(temporal q|k|v GEMM, temporal attention), "cpu_baseline" (the oracle restatement timed on
+Extra fields: "roofline" for the dominant kernel (the fused MLP, mlp_rowln_kernel: fc1 +
+GELU + fc2 + gated residual + next LN in one launch, the largest share of the step per
+profiles/; live HIP-event timing on the stream the kernel runs on; with MDG_FUSED_MLP=0 the
+fc2 row-LN GEMM instead), "roofline_more" for the next ones (the out_proj row-LN GEMM, the
+temporal q|k|v GEMM, the temporal attention), "cpu_baseline" (the oracle restatement timed on
 this host's cores).  Each roofline entry is priced against its BINDING roof: algorithmic
 FLOPs / 2.5 PF vs algorithmic bytes / 8 TB/s, whichever is longer ("bound"); both fractions
 are reported ("mfma_frac", "hbm_frac") with the kernel's arithmetic intensity.
@@ -119,7 +120,10 @@ def roofline(eng, st, dtype, B, T, L):
       * attn_temporal — the largest launch type per step (profiles/r01_summary.md):
         4*B*L*H*T*(T+1)*D FLOPs (QK^T and PV over T+1 keys incl. the bias row, unpadded D);
       * gemm_qkv_temporal — 2*M*N*K with M = B*T*L, N = 3C, K = C (+ RoPE/scatter epilogue);
-      * gemm_fc2_rowln — fc2 with the gated residual + LayerNorm epilogue, 2*M*C*4C."""
+      * gemm_fc2_rowln — fc2 with the gated residual + LayerNorm epilogue, 2*M*C*4C (the
+        MLP's second GEMM when the MLP is not fused);
+      * mlp_fused — fc1 + GELU + fc2 + gated residual + LN in one kernel, 4*M*C*4C;
+      * gemm_out_proj_rowln — out_proj + gated residual + LN, 2*M*C*C."""
     from mdgen_finetune_amd import _lib
 
     lib, P = eng.lib, eng._packed
@@ -165,6 +169,25 @@ def roofline(eng, st, dtype, B, T, L):
     def fc2():
         _lib.check(lib.mdg_gemm(ctypes.byref(f), s), "fc2 rowln gemm")
 
+    # the fused MLP with the same fc2 descriptor and the fc1 one the step builds
+    f1 = _lib.MdgGemmDesc()
+    f1.dtype, f1.a_mode, f1.epi, f1.act, f1.M, f1.N, f1.K = eng.mdg_dtype, _lib.MDG_A_PLAIN, _lib.MDG_EPI_STORE, 1, N, 4 * C, C
+    f1.A, f1.lda = ws + off["xn"], C
+    f1.W, f1.ldw, f1.bias = P["layers"][0]["w1"].data_ptr(), C, P["layers"][0]["b1"].data_ptr()
+    f1.out, f1.ldo = ws + off["hid"], 4 * C
+
+    def mlp():
+        _lib.check(lib.mdg_mlp_fused(ctypes.byref(f1), ctypes.byref(f), s), "mlp fused")
+
+    # out_proj + gated residual + LN (K = C), the same row-LN kernel as fc2
+    o = _lib.MdgGemmDesc()
+    ctypes.memmove(ctypes.byref(o), ctypes.byref(f), ctypes.sizeof(f))
+    o.K, o.A, o.lda = C, ws + off["o"], C
+    o.W, o.ldw, o.bias = P["layers"][0]["wo1"].data_ptr(), C, P["layers"][0]["bo1"].data_ptr()
+
+    def out_proj():
+        _lib.check(lib.mdg_gemm(ctypes.byref(o), s), "out_proj rowln gemm")
+
     # algorithmic bytes per launch: every operand read once + every output written once, in the
     # path's storage types (bf16 activations / weights, fp32 residual stream), head dim UNPADDED
     # (D = 24; the kernels' 32-wide pad is not counted), adaLN rows / biases / RoPE tables omitted
@@ -173,12 +196,18 @@ def roofline(eng, st, dtype, B, T, L):
     bytes_fc2 = N * 4 * C * cb + 2 * N * C * 4 + N * C * cb + 4 * C * C * cb   # hid, h r+w, xn, W2
     bytes_qkv = N * C * cb + 3 * N * HD * cb + 3 * C * C * cb                     # xn, q|k|v, Wqkv
     bytes_attn = 3 * N * HD * cb + N * HD * cb                                    # q|k|v, o
+    bytes_mlp = N * C * cb + 2 * N * C * 4 + N * C * cb + 8 * C * C * cb          # xn, h r+w, xn out, W1+W2
+    bytes_op = N * C * cb + 2 * N * C * 4 + N * C * cb + C * C * cb               # o, h r+w, xn out, Wo
     # (the bf16 step stores the planes packed: these are also the bytes it moves; the f32 path
     # pads D to 32 columns)
     out = {}
-    for name, fn, flops, nbytes in (("gemm_fc2_rowln", fc2, 2.0 * N * C * 4 * C, bytes_fc2),
-                                    ("gemm_qkv_temporal", gemm, 2.0 * N * 3 * C * C, bytes_qkv),
-                                    ("attn_temporal", attn, 4.0 * B * L * H * T * (T + 1) * D, bytes_attn)):
+    fused = eng.describe_plan(B, T, L).get("mlp", "").startswith("mlp_fused")
+    kernels = [("mlp_fused", mlp, 4.0 * N * C * 4 * C, bytes_mlp)] if fused else \
+        [("gemm_fc2_rowln", fc2, 2.0 * N * C * 4 * C, bytes_fc2)]
+    kernels += [("gemm_out_proj_rowln", out_proj, 2.0 * N * C * C, bytes_op),
+                ("gemm_qkv_temporal", gemm, 2.0 * N * 3 * C * C, bytes_qkv),
+                ("attn_temporal", attn, 4.0 * B * L * H * T * (T + 1) * D, bytes_attn)]
+    for name, fn, flops, nbytes in kernels:
         sec = time_kernel(fn, 50)
         # the binding roof: whichever of the MFMA time and the HBM time of the algorithmic work
         # is longer (arithmetic intensity below / above the ridge 2.5 PF / 8 TB/s = 312 FLOP/B)
@@ -213,7 +242,7 @@ def job_value(world, B, T, n_euler, steps, el):
     return world * B * T * n_euler * steps / el
 
 
-def step_model(B, T, L, C=384, H=16, nl=5, lat=21, dtype="bf16"):
+def step_model(B, T, L, C=384, H=16, nl=5, lat=21, dtype="bf16", fused_mlp=False):
     """Algorithmic work of ONE denoise step (forward + Euler update) of B trajectories, from the
     model dims (counted 2*M*N*K per GEMM, 4*S*(S+1)*D per attention head-sequence):
       flops        — GEMMs 32*C^2 per token per layer + temporal attention 4*(T+1)*C per token
@@ -236,6 +265,8 @@ def step_model(B, T, L, C=384, H=16, nl=5, lat=21, dtype="bf16"):
     attn = N * 4 * C * cb
     fc1 = N * (C * cb + 4 * C * cb)
     fc2 = N * (4 * C * cb + 8 * C + C * cb)
+    if fused_mlp:  # the hidden activation never reaches HBM: xn in, h r+w, xn out
+        fc1, fc2 = 0, N * (C * cb + 8 * C + C * cb)
     final = N * (C * cb + 3 * lat * 4)
     design = emb + nl * (spatial + 2 * rowln + qkv + attn + fc1 + fc2) + final
     params = nl * 16 * C * C + 2 * lat * C
@@ -243,10 +274,10 @@ def step_model(B, T, L, C=384, H=16, nl=5, lat=21, dtype="bf16"):
     return {"flops": flops, "design_bytes": design, "floor_bytes": floor, "D": D}
 
 
-def step_roofline(B, T, L, dtype, sec_per_denoise):
+def step_roofline(B, T, L, dtype, sec_per_denoise, fused_mlp=False):
     """Whole-step position against both roofs (not one kernel): achieved TFLOP/s of the step's
     algorithmic FLOPs vs the dense MFMA peak, and achieved GB/s of the design's data flow vs HBM."""
-    sm = step_model(B, T, L, dtype=dtype)
+    sm = step_model(B, T, L, dtype=dtype, fused_mlp=fused_mlp)
     tf = sm["flops"] / sec_per_denoise / 1e12
     gbs = sm["design_bytes"] / sec_per_denoise / 1e9
     t_mfma = sm["flops"] / (PEAK_TFLOPS[dtype] * 1e12)
@@ -291,7 +322,8 @@ def sweep_line(dev, T, L, B, dtype, lanes, num_steps, steps, seed):
     out = {"batch": B, "dtype": dtype, "lanes": eng.lanes, "value": round(B * T * n_euler / sec, 1),
            "unit": "frames/s", "ms_per_window": round(sec * 1e3, 3),
            "us_per_denoise_step": round(sec / n_euler * 1e6, 2),
-           "step_roofline": step_roofline(B, T, L, dtype, sec / n_euler)}
+           "step_roofline": step_roofline(B, T, L, dtype, sec / n_euler,
+                                          eng.describe_plan(B // eng.lanes, T, L).get("mlp", "").startswith("mlp_fused"))}
     del eng, m
     torch.cuda.empty_cache()
     return out
@@ -431,11 +463,12 @@ def main():
                        "parallelism": f"replicas{world}", "hipgraph": not a.no_graph,
                        "lanes": a.lanes},
             "us_per_denoise_step": round(el / a.steps / n_euler * 1e6, 2),
-            "step_roofline": step_roofline(B, T, L, a.dtype, el / a.steps / n_euler / world),
+            "step_roofline": step_roofline(B, T, L, a.dtype, el / a.steps / n_euler / world,
+                                           plan.get("mlp", "").startswith("mlp_fused")),
             "kernel_plan": plan,
             "batch_sweep": sweep,
-            "roofline": roofs["gemm_fc2_rowln"] if roofs else None,
-            "roofline_more": [roofs["gemm_qkv_temporal"], roofs["attn_temporal"]] if roofs else None,
+            "roofline": list(roofs.values())[0] if roofs else None,
+            "roofline_more": list(roofs.values())[1:] if roofs else None,
             "cpu_baseline": cpu,
         }
         if share:  # rehearsal: every rank on cuda:0 — not a multi-GPU measurement

@@ -39,8 +39,8 @@ if os.path.exists(stats) and default_shape:
         # bench.roofline times each roofline kernel in a loop of 50 launches after the timed
         # windows (plus one warm-up launch): those are the last 50 dispatches of its name; the
         # rest ran inside the hipGraph windows.
-        pats = (("gemm_rowln_kernel", "gemm_fc2_rowln"), ("gemm_bf16_b4_kernel<2", "gemm_qkv_temporal"),
-                ("attn_temporal_bf16", "attn_temporal"))
+        pats = (("mlp_rowln_kernel", "mlp_fused"), ("gemm_rowln_kernel", "gemm_out_proj_rowln"),
+                ("gemm_bf16_b4_kernel<2", "gemm_qkv_temporal"), ("attn_temporal_bf16", "attn_temporal"))
         per = collections.defaultdict(list)
         for r in csv.DictReader(open(trace)):
             for pat, name in pats:
@@ -65,17 +65,15 @@ if os.path.exists(stats) and default_shape:
                 continue
             loop = [x[1] for x in v[-50:]]
             graph = [x[1] for x in v[:-51]]
-            # gemm_rowln_kernel serves out_proj (x2 per layer) AND fc2 (x1) at one grid size:
-            # fc2 (K = 4C) is the slowest third of the family's in-graph launches
-            own = sorted(graph)[-len(graph) // 3:] if name == "gemm_fc2_rowln" else graph
+            # (with the fused MLP the row-LN kernel serves only out_proj, x2 per layer)
             lines.append(f"| {name} | {sum(loop) / len(loop):.1f} | {bench_live.get(name, 'n/a')} | "
-                         f"{sum(graph) / len(graph):.1f} | {sum(own) / len(own):.1f}"
-                         f"{' (fc2 = slowest third of the family)' if own is not graph else ''} |")
+                         f"{sum(graph) / len(graph):.1f} | {sum(graph) / len(graph):.1f} |")
     open(os.path.join(out, f"r{rr}_summary.md"), "w").write("\n".join(lines) + "\n")
 
-# the rowln family's last 50 dispatches are bench.roofline's fc2 timing loop
+# each roofline kernel's last 50 dispatches are its bench.roofline timing loop (the row-LN
+# family's: the out_proj one; the fc2 one when the MLP is not fused)
 KMAP = {"gemm_bf16_b4_kernel<2": "gemm_qkv_temporal", "attn_temporal_bf16": "attn_temporal",
-        "gemm_rowln_kernel": "gemm_fc2_rowln"}
+        "gemm_rowln_kernel": "gemm_out_proj_rowln", "mlp_rowln_kernel": "mlp_fused"}
 res = collections.defaultdict(dict)
 for cname, scale in (("FETCH_SIZE", 2 * 1024), ("WRITE_SIZE", 1024)):
     p = os.path.join(pmc_dir, f"{cname}_counter_collection.csv")
