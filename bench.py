@@ -123,7 +123,9 @@ def roofline(eng, st, dtype, B, T, L):
       * gemm_fc2_rowln — fc2 with the gated residual + LayerNorm epilogue, 2*M*C*4C (the
         MLP's second GEMM when the MLP is not fused);
       * mlp_fused — fc1 + GELU + fc2 + gated residual + LN in one kernel, 4*M*C*4C;
-      * gemm_out_proj_rowln — out_proj + gated residual + LN, 2*M*C*C."""
+      * gemm_out_proj_rowln — out_proj + gated residual + LN, 2*M*C*C;
+      * rowln_qkv — the spatial out_proj + gated residual + LN_t and the temporal q|k|v in one
+        kernel (LN_t(h) on chip), 2*M*C*C + 2*M*3C*C."""
     from mdgen_finetune_amd import _lib
 
     lib, P = eng.lib, eng._packed
@@ -188,6 +190,9 @@ def roofline(eng, st, dtype, B, T, L):
     def out_proj():
         _lib.check(lib.mdg_gemm(ctypes.byref(o), s), "out_proj rowln gemm")
 
+    def rowln_qkv():
+        _lib.check(lib.mdg_rowln_qkv(ctypes.byref(o), ctypes.byref(g), s), "rowln_qkv")
+
     # algorithmic bytes per launch: every operand read once + every output written once, in the
     # path's storage types (bf16 activations / weights, fp32 residual stream), head dim UNPADDED
     # (D = 24; the kernels' 32-wide pad is not counted), adaLN rows / biases / RoPE tables omitted
@@ -198,15 +203,19 @@ def roofline(eng, st, dtype, B, T, L):
     bytes_attn = 3 * N * HD * cb + N * HD * cb                                    # q|k|v, o
     bytes_mlp = N * C * cb + 2 * N * C * 4 + N * C * cb + 8 * C * C * cb          # xn, h r+w, xn out, W1+W2
     bytes_op = N * C * cb + 2 * N * C * 4 + N * C * cb + C * C * cb               # o, h r+w, xn out, Wo
+    bytes_rq = N * C * cb + 2 * N * C * 4 + 3 * N * HD * cb + 4 * C * C * cb      # o, h r+w, q|k|v, Wo+Wqkv
     # (the bf16 step stores the planes packed: these are also the bytes it moves; the f32 path
     # pads D to 32 columns)
     out = {}
-    fused = eng.describe_plan(B, T, L).get("mlp", "").startswith("mlp_fused")
+    fused, fused_qkv = _fusions(eng.describe_plan(B, T, L))
     kernels = [("mlp_fused", mlp, 4.0 * N * C * 4 * C, bytes_mlp)] if fused else \
         [("gemm_fc2_rowln", fc2, 2.0 * N * C * 4 * C, bytes_fc2)]
-    kernels += [("gemm_out_proj_rowln", out_proj, 2.0 * N * C * C, bytes_op),
-                ("gemm_qkv_temporal", gemm, 2.0 * N * 3 * C * C, bytes_qkv),
-                ("attn_temporal", attn, 4.0 * B * L * H * T * (T + 1) * D, bytes_attn)]
+    if fused_qkv:  # (the temporal out_proj stays a row-LN GEMM)
+        kernels += [("rowln_qkv", rowln_qkv, 8.0 * N * C * C, bytes_rq)]
+    kernels += [("gemm_out_proj_rowln", out_proj, 2.0 * N * C * C, bytes_op)]
+    if not fused_qkv:
+        kernels += [("gemm_qkv_temporal", gemm, 2.0 * N * 3 * C * C, bytes_qkv)]
+    kernels += [("attn_temporal", attn, 4.0 * B * L * H * T * (T + 1) * D, bytes_attn)]
     for name, fn, flops, nbytes in kernels:
         sec = time_kernel(fn, 50)
         # the binding roof: whichever of the MFMA time and the HBM time of the algorithmic work
@@ -242,7 +251,7 @@ def job_value(world, B, T, n_euler, steps, el):
     return world * B * T * n_euler * steps / el
 
 
-def step_model(B, T, L, C=384, H=16, nl=5, lat=21, dtype="bf16", fused_mlp=False):
+def step_model(B, T, L, C=384, H=16, nl=5, lat=21, dtype="bf16", fused_mlp=False, fused_qkv=False):
     """Algorithmic work of ONE denoise step (forward + Euler update) of B trajectories, from the
     model dims (counted 2*M*N*K per GEMM, 4*S*(S+1)*D per attention head-sequence):
       flops        — GEMMs 32*C^2 per token per layer + temporal attention 4*(T+1)*C per token
@@ -267,17 +276,24 @@ def step_model(B, T, L, C=384, H=16, nl=5, lat=21, dtype="bf16", fused_mlp=False
     fc2 = N * (4 * C * cb + 8 * C + C * cb)
     if fused_mlp:  # the hidden activation never reaches HBM: xn in, h r+w, xn out
         fc1, fc2 = 0, N * (C * cb + 8 * C + C * cb)
+    if fused_qkv:  # spatial out_proj + LN_t + temporal q|k|v in one kernel: LN_t(h) stays on chip
+        qkv -= N * C * cb  # (and the out_proj's xn write, below)
     final = N * (C * cb + 3 * lat * 4)
-    design = emb + nl * (spatial + 2 * rowln + qkv + attn + fc1 + fc2) + final
+    design = emb + nl * (spatial + 2 * rowln - (N * C * cb if fused_qkv else 0) + qkv + attn + fc1 + fc2) + final
     params = nl * 16 * C * C + 2 * lat * C
     floor = params * cb + N * lat * 4 * 2
     return {"flops": flops, "design_bytes": design, "floor_bytes": floor, "D": D}
 
 
-def step_roofline(B, T, L, dtype, sec_per_denoise, fused_mlp=False):
+def _fusions(plan):
+    """(fused MLP, fused out_proj + q|k|v) of a kernel plan (mdg_describe_plan)."""
+    return plan.get("mlp", "").startswith("mlp_fused"), plan.get("temporal", "").startswith("rowln_qkv")
+
+
+def step_roofline(B, T, L, dtype, sec_per_denoise, fused_mlp=False, fused_qkv=False):
     """Whole-step position against both roofs (not one kernel): achieved TFLOP/s of the step's
     algorithmic FLOPs vs the dense MFMA peak, and achieved GB/s of the design's data flow vs HBM."""
-    sm = step_model(B, T, L, dtype=dtype, fused_mlp=fused_mlp)
+    sm = step_model(B, T, L, dtype=dtype, fused_mlp=fused_mlp, fused_qkv=fused_qkv)
     tf = sm["flops"] / sec_per_denoise / 1e12
     gbs = sm["design_bytes"] / sec_per_denoise / 1e9
     t_mfma = sm["flops"] / (PEAK_TFLOPS[dtype] * 1e12)
@@ -322,8 +338,7 @@ def sweep_line(dev, T, L, B, dtype, lanes, num_steps, steps, seed):
     out = {"batch": B, "dtype": dtype, "lanes": eng.lanes, "value": round(B * T * n_euler / sec, 1),
            "unit": "frames/s", "ms_per_window": round(sec * 1e3, 3),
            "us_per_denoise_step": round(sec / n_euler * 1e6, 2),
-           "step_roofline": step_roofline(B, T, L, dtype, sec / n_euler,
-                                          eng.describe_plan(B // eng.lanes, T, L).get("mlp", "").startswith("mlp_fused"))}
+           "step_roofline": step_roofline(B, T, L, dtype, sec / n_euler, *_fusions(eng.describe_plan(B // eng.lanes, T, L)))}
     del eng, m
     torch.cuda.empty_cache()
     return out
@@ -463,8 +478,7 @@ def main():
                        "parallelism": f"replicas{world}", "hipgraph": not a.no_graph,
                        "lanes": a.lanes},
             "us_per_denoise_step": round(el / a.steps / n_euler * 1e6, 2),
-            "step_roofline": step_roofline(B, T, L, a.dtype, el / a.steps / n_euler / world,
-                                           plan.get("mlp", "").startswith("mlp_fused")),
+            "step_roofline": step_roofline(B, T, L, a.dtype, el / a.steps / n_euler / world, *_fusions(plan)),
             "kernel_plan": plan,
             "batch_sweep": sweep,
             "roofline": list(roofs.values())[0] if roofs else None,

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define MDG_ABI_VERSION 13
+#define MDG_ABI_VERSION 14
 #define MDG_MAX_LAYERS 16
 #define MDG_DP 32      /* padded head dim of the attention operand buffers for head_dim <= 31 */
 #define MDG_DP_WIDE 64 /* ... and for 32 <= head_dim <= 63 (column head_dim of the padded k / v rows
@@ -204,6 +204,13 @@ int mdg_gemm(const mdg_gemm_desc* g, void* stream);
    mdg_gemm(fc2).  bf16, C == fc1.K == fc2.N == 384, F == fc1.N == fc2.K a multiple of 128,
    fc2.rows_per_mod >= 128, no training outputs; MDG_E_SHAPE otherwise. */
 int mdg_mlp_fused(const mdg_gemm_desc* fc1, const mdg_gemm_desc* fc2, void* stream);
+/* The spatial attention's out_proj + gated residual + temporal LayerNorm and the temporal
+   q|k|v projection as ONE kernel (latent_model.py:471-477): out_proj = PLAIN GATE_RES with
+   the LN hand-off (xn_out is NOT written: LN_t(h) stays on chip), qkv = the QKV epilogue into
+   MDG_QKV_TEMPORAL_PACKED planes (its A is not read), the descriptors exactly as for
+   mdg_gemm(out_proj) then mdg_gemm(qkv).  bf16, C == 384, head_dim % 8 == 0 and <= 48,
+   out_proj.rows_per_mod >= 128, no training outputs; MDG_E_SHAPE otherwise. */
+int mdg_rowln_qkv(const mdg_gemm_desc* out_proj, const mdg_gemm_desc* qkv, void* stream);
 /* qkv: CT [n_frames*L][3][H][D] (unpadded q | k | v rows of each token) */
 int mdg_attn_spatial(int32_t dtype, int32_t n_frames, int32_t L, int32_t H, int32_t D,
                      const void* qkv, const float* kvb, const float* mask, void* out,

@@ -120,6 +120,7 @@ SIGNATURES = [
     ("mdg_describe_plan", _i32, [ctypes.POINTER(MdgDims), ctypes.c_char_p, ctypes.c_size_t]),
     ("mdg_gemm", _i32, [ctypes.POINTER(MdgGemmDesc), _vp]),
     ("mdg_mlp_fused", _i32, [ctypes.POINTER(MdgGemmDesc), ctypes.POINTER(MdgGemmDesc), _vp]),
+    ("mdg_rowln_qkv", _i32, [ctypes.POINTER(MdgGemmDesc), ctypes.POINTER(MdgGemmDesc), _vp]),
     ("mdg_attn_spatial", _i32, [_i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
     ("mdg_attn_temporal", _i32, [_i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
     ("mdg_attn_temporal_packed", _i32, [_i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
@@ -144,7 +145,7 @@ SIGNATURES = [
                                     _vp]),
 ]
 
-ABI_VERSION = 13
+ABI_VERSION = 14
 _LIB = None
 
 

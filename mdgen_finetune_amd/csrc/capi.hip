@@ -20,6 +20,8 @@ GemmPlan gemm_plan(const mdg_gemm_desc& p);
 hipError_t gemm_launch(const mdg_gemm_desc& p, const GemmPlan& g, hipStream_t s);
 bool mlp_fused_supported(const mdg_gemm_desc& f1, const mdg_gemm_desc& f2);
 hipError_t mlp_fused_launch(const mdg_gemm_desc& f1, const mdg_gemm_desc& f2, hipStream_t s);
+bool rowln_qkv_supported(const mdg_gemm_desc& r, const mdg_gemm_desc& q);
+hipError_t rowln_qkv_launch(const mdg_gemm_desc& r, const mdg_gemm_desc& q, hipStream_t s);
 hipError_t attn_temporal_launch(int dtype, int B, int T, int L, int H, int D, const void* qkv_t,
                                 const float* kbias, const float* kvb, void* out, hipStream_t s,
                                 float* lse = nullptr, bool packed = false);
@@ -127,6 +129,16 @@ bool packed_planes(const mdg_dims& d) {
 bool fused_mlp_on() {
   static const bool on = [] {
     const char* e = getenv("MDG_FUSED_MLP");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+// bf16, C = 384, packed planes: the spatial out_proj row-LN and the temporal q|k|v projection
+// as one kernel (LN_t(h) stays on chip); MDG_FUSED_QKV=0 keeps the two launches (A/B knob)
+bool fused_qkv_on() {
+  static const bool on = [] {
+    const char* e = getenv("MDG_FUSED_QKV");
     return !(e && e[0] == '0');
   }();
   return on;
@@ -453,16 +465,21 @@ static int layer_fwd_impl(const mdg_dims* d, const mdg_layer_weights* w, const f
     r.xn_out = xn; r.xn_mods = mods; r.xn_mod_stride = ms; r.xn_shift_off = 3 * C; r.xn_scale_off = 4 * C;
     r.ln_eps = 1e-6f;
   }
-  if (int e = mdg_gemm(&r, stream)) return e;
 
   // ---- temporal attention: x += gate_t * mha_t(mod(LN x))     (latent_model.py:474-486)
-  if (!fuse)
-    if (int e = ln(3 * C, 4 * C)) return e;
   q.epi = MDG_EPI_QKV;  // (the spatial launch above may have been the fused ATTN_SPATIAL form)
   q.W = w->wqkv[1]; q.bias = w->bqkv[1];
   q.qkv_layout = tlayout; q.qkv_out = qkv_t; q.qscale = qs * 1.4426950408889634f;
   q.rope = rope_t; q.rope_rows = T + 1;
-  if (int e = mdg_gemm(&q, stream)) return e;
+  if (fuse && fused_qkv_on() && mdg::rowln_qkv_supported(r, q)) {
+    // out_proj + gated residual + LN_t + q|k|v in one launch (xn is not written)
+    if (int e = hip_check(mdg::rowln_qkv_launch(r, q, s), "rowln_qkv launch")) return e;
+  } else {
+    if (int e = mdg_gemm(&r, stream)) return e;
+    if (!fuse)
+      if (int e = ln(3 * C, 4 * C)) return e;
+    if (int e = mdg_gemm(&q, stream)) return e;
+  }
   if (int e = attn_t(B, T, L, kbias, w->kvb[1])) return e;
   r.W = w->wo[1]; r.bias = w->bo[1]; r.gate_off = 5 * C;
   if (fuse) {  // + LN_mlp(h) -> xn
@@ -498,6 +515,15 @@ int mdg_mlp_fused(const mdg_gemm_desc* f1, const mdg_gemm_desc* f2, void* stream
     return fail(MDG_E_SHAPE, "mlp_fused: outside the envelope (bf16, K=N=384, F %% 128, rows_per_mod >= 128) "
                 "M=%d C=%d F=%d", f1->M, f1->K, f1->N);
   return hip_check(mdg::mlp_fused_launch(*f1, *f2, (hipStream_t)stream), "mlp fused launch");
+}
+
+int mdg_rowln_qkv(const mdg_gemm_desc* r, const mdg_gemm_desc* q, void* stream) {
+  if (!r || !q) return fail(MDG_E_ARG, "rowln_qkv: null descriptor");
+  if (!r->A || !r->W || !r->resid || !q->W || !q->qkv_out) return fail(MDG_E_ARG, "rowln_qkv: null pointer");
+  if (!mdg::rowln_qkv_supported(*r, *q))
+    return fail(MDG_E_SHAPE, "rowln_qkv: outside the envelope (bf16, C=384, LN output, packed temporal planes, "
+                "head_dim %% 8 == 0 and <= 48, rows_per_mod >= 128) M=%d D=%d", r->M, q->D);
+  return hip_check(mdg::rowln_qkv_launch(*r, *q, (hipStream_t)stream), "rowln_qkv launch");
 }
 
 int mdg_layer_fwd(const mdg_dims* d, const mdg_layer_weights* w, const float* rope_l,
@@ -588,10 +614,13 @@ int mdg_describe_plan(const mdg_dims* d, char* buf, size_t n) {
     spatial = "qkv_gemm(spatial layout)+attn_spatial(valu)";
   snprintf(buf, n,
            "{\"dtype\": \"%s\", \"spatial\": \"%s\", \"ln_handoff\": \"%s\", "
-           "\"temporal\": \"qkv_gemm+%s\", \"planes\": \"%s\", \"mlp\": \"%s\", "
+           "\"temporal\": \"%s+%s\", \"planes\": \"%s\", \"mlp\": \"%s\", "
            "\"final\": \"euler_epilogue_gemm\"}",
            d->dtype == MDG_BF16 ? "bf16" : "f32", spatial,
            fuse ? "fused into gated-residual row-LN GEMM epilogues" : "stand-alone ln_mod pass",
+           (fuse && fused_qkv_on() && C == 384 && packed_planes(*d) && d->D <= 48 && d->T * d->L >= 128)
+               ? "rowln_qkv(spatial out_proj+gated residual+LN_t+q|k|v in one kernel, LN_t on chip)"
+               : "qkv_gemm",
            d->D >= MDG_DP ? (d->dtype == MDG_BF16 ? "attn_temporal(wide heads: bf16 16x16x32 mfma, 64-col rows)"
                                                   : "attn_temporal(wide heads: f32 16x16x4 mfma, 64-col rows)")
            : d->dtype == MDG_BF16 ? "attn_temporal_bf16(32x32x16 mfma)" : "attn_temporal(f32 16x16x4 mfma)",

@@ -652,10 +652,10 @@ __device__ __forceinline__ void epi_tile8(const mdg_gemm_desc& p, const float* _
         if (rope) {
           const float cc[4] = {cs[u].x, cs[u].y, cs[u].z, cs[u].w}, ss[4] = {sn[u].x, sn[u].y, sn[u].z, sn[u].w};
 #pragma unroll
-          for (int k = 0; k < 4; ++k) {
+          for (int k = 0; k < 4; ++k) {  // explicit fma: the fused rowln_qkv epilogue rounds alike
             const float x = v[2 * k], y = v[2 * k + 1];
-            v[2 * k] = x * cc[k] - y * ss[k];
-            v[2 * k + 1] = y * cc[k] + x * ss[k];
+            v[2 * k] = __builtin_fmaf(x, cc[k], -(y * ss[k]));
+            v[2 * k + 1] = __builtin_fmaf(y, cc[k], x * ss[k]);
           }
         }
         size_t off;
@@ -973,9 +973,15 @@ __device__ __forceinline__ void rowln_load_band(const mdg_gemm_desc& p, int m0, 
 }
 
 template <int NCOL>
+// xlds: write the normalised rows (xn) not to p.xn_out but into LDS, as K-slice images of 32
+// columns ([NCOL / 32][BM][32] bf16, 16-B chunk c of row r at c ^ ((-(r >> 2)) & 3)): the
+// A operand of a following GEMM in the same block.
 __device__ __forceinline__ void rowln_fast_epilogue(const mdg_gemm_desc& p, f32x4 (&acc)[4][NCOL / 64],
                                                     float4 (&h4)[2][NCOL / 128], unsigned char* smem, int m0,
-                                                    int b_lo, float inv_rpm) {
+                                                    int b_lo, float inv_rpm, bf16_t* xlds = nullptr) {
+  // no fp contraction: every kernel that inlines this epilogue (the row-LN GEMM, the fused MLP,
+  // the fused out_proj + q|k|v) rounds h and xn identically
+#pragma clang fp contract(off)
   constexpr int BM = 128, WTN = NCOL / 4, NT = WTN / 16, LDS_ST = NCOL + 4, NE = NCOL / 128;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wm = wave / 4, wn = wave % 4;
   const int lr = lane & 15, lg = lane >> 4, half = lane >> 5, hl = lane & 31;
@@ -1082,10 +1088,15 @@ __device__ __forceinline__ void rowln_fast_epilogue(const mdg_gemm_desc& p, f32x
           const float4 xs = *reinterpret_cast<const float4*>(mr + NCOL + 128 * e);
           const float4 xh = *reinterpret_cast<const float4*>(mr + 2 * NCOL + 128 * e);
           const float4 h = h4[pr][e];
-          if (m < M)
-            st4<bf16_t>(reinterpret_cast<bf16_t*>(p.xn_out) + (size_t)m * NCOL + 4 * hl + 128 * e,
-                        (h.x - sum[pr]) * rs * (1.0f + xs.x) + xh.x, (h.y - sum[pr]) * rs * (1.0f + xs.y) + xh.y,
-                        (h.z - sum[pr]) * rs * (1.0f + xs.z) + xh.z, (h.w - sum[pr]) * rs * (1.0f + xs.w) + xh.w);
+          const float o0 = (h.x - sum[pr]) * rs * (1.0f + xs.x) + xh.x, o1 = (h.y - sum[pr]) * rs * (1.0f + xs.y) + xh.y;
+          const float o2 = (h.z - sum[pr]) * rs * (1.0f + xs.z) + xh.z, o3 = (h.w - sum[pr]) * rs * (1.0f + xs.w) + xh.w;
+          if (xlds) {
+            const int r = m - m0, col = 4 * hl + 128 * e, cw = col & 31;
+            st4<bf16_t>(xlds + (col >> 5) * (BM * 32) + r * 32 + (((cw >> 3) ^ ((-(r >> 2)) & 3)) * 8) + (cw & 7), o0, o1,
+                        o2, o3);
+          } else if (m < M) {
+            st4<bf16_t>(reinterpret_cast<bf16_t*>(p.xn_out) + (size_t)m * NCOL + 4 * hl + 128 * e, o0, o1, o2, o3);
+          }
         }
       }
     }
@@ -1400,6 +1411,44 @@ __host__ __device__ constexpr size_t mlp_smem(int F) {
   return (size_t)kMlpStages * kMlpSlot * 2 + (size_t)128 * kMlpHC * 2 + (size_t)F * 4;
 }
 
+// LDS accesses the compiler's wait-count pass does not see.  It makes every LDS access that
+// follows a global_load_lds wait for ALL outstanding LDS DMA (s_waitcnt vmcnt(0): it cannot
+// tell the ring slots from the other LDS arrays), which drains the ring ahead of the
+// epilogues' bias / RoPE reads; these kernels order their LDS by their own barriers instead.
+// Each read group is ONE asm statement ending in s_waitcnt lgkmcnt(0), with early-clobber
+// outputs: with the wait in a separate statement the compiler copied a destination register
+// before the data had arrived.
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+typedef __attribute__((ext_vector_type(2))) float f32x2;
+__device__ __forceinline__ void lds_ld4x4_raw(const float* p0, const float* p1, const float* p2, const float* p3,
+                                              f32x4& v0, f32x4& v1, f32x4& v2, f32x4& v3) {
+  asm volatile(
+      "ds_read_b128 %0, %4\n\tds_read_b128 %1, %5\n\tds_read_b128 %2, %6\n\tds_read_b128 %3, %7\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(v0), "=&v"(v1), "=&v"(v2), "=&v"(v3)
+      : "v"(lds_addr(p0)), "v"(lds_addr(p1)), "v"(lds_addr(p2)), "v"(lds_addr(p3)));
+}
+__device__ __forceinline__ f32x4 lds_ld4_raw(const float* p) {
+  f32x4 v;
+  asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=&v"(v) : "v"(lds_addr(p)));
+  return v;
+}
+// one float4 + four float2 (the bias and the RoPE cos / sin pairs of two tokens)
+__device__ __forceinline__ void lds_ld4_2x4_raw(const float* pb, const float* pc0, const float* ps0, const float* pc1,
+                                                const float* ps1, f32x4& b, f32x2& c0, f32x2& s0, f32x2& c1,
+                                                f32x2& s1) {
+  asm volatile(
+      "ds_read_b128 %0, %5\n\tds_read_b64 %1, %6\n\tds_read_b64 %2, %7\n\tds_read_b64 %3, %8\n\t"
+      "ds_read_b64 %4, %9\n\ts_waitcnt lgkmcnt(0)"
+      : "=&v"(b), "=&v"(c0), "=&v"(s0), "=&v"(c1), "=&v"(s1)
+      : "v"(lds_addr(pb)), "v"(lds_addr(pc0)), "v"(lds_addr(ps0)), "v"(lds_addr(pc1)), "v"(lds_addr(ps1)));
+}
+__device__ __forceinline__ void lds_st1_raw(float* p, float v) {
+  asm volatile("ds_write_b32 %0, %1" ::"v"(lds_addr(p)), "v"(v) : "memory");
+}
+
 // s_waitcnt vmcnt(n) for a wave-uniform n in [0, 6]
 __device__ __forceinline__ void vm_wait_upto6(int n) {
   switch (n) {
@@ -1523,6 +1572,11 @@ __global__ __launch_bounds__(kMlpThreads, 1) void mlp_rowln_kernel(const MlpArgs
     // the chunk's fc1 is complete: + b1, GELU, bf16 -> Hs; restart acc1.  (Hs was last read by
     // chunk j - 1's fc2 steps, which every wave finished before this chunk's first barrier.)
     const float* b1c = b1s + j * HC;
+    f32x4 b1v[4];
+    {
+      const float* bp = b1c + wah * 64 + lg * 4;
+      lds_ld4x4_raw(bp, bp + 16, bp + 32, bp + 48, b1v[0], b1v[1], b1v[2], b1v[3]);
+    }
 #pragma unroll
     for (int hi = 0; hi < 4; ++hi)
 #pragma unroll
@@ -1530,7 +1584,7 @@ __global__ __launch_bounds__(kMlpThreads, 1) void mlp_rowln_kernel(const MlpArgs
         const int hb = wah * 64 + hi * 16 + lg * 4, tok = wat * 32 + ti * 16 + lr;
         bf16x4 o;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = (bf16_t)gelu_fast(acc1[hi][ti][r] + b1c[hb + r]);
+        for (int r = 0; r < 4; ++r) o[r] = (bf16_t)gelu_fast(acc1[hi][ti][r] + b1v[hi][r]);
         *reinterpret_cast<bf16x4*>(Hs + tok * HC + (((hb >> 3) ^ (tok & 15)) * 8) + (hb & 7)) = o;
         acc1[hi][ti] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
@@ -1579,6 +1633,300 @@ hipError_t mlp_fused_launch(const mdg_gemm_desc& f1, const mdg_gemm_desc& f2, hi
   a.f1 = f1;
   a.f2 = f2;
   hipLaunchKernelGGL((mlp_rowln_kernel<384>), dim3((f1.M + 127) / 128), dim3(kMlpThreads), mlp_smem(f1.N), s, a);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// Spatial out_proj + gated residual + temporal LN, then the temporal q|k|v projection, in one
+// kernel (latent_model.py:471-477): LN_t(h) never leaves the CU.  Block = 128 token rows, one
+// block per CU.  Phase 1 is gemm_rowln_kernel<384, 128> (4-stage ring, fast epilogue) with the
+// normalised rows written into LDS as twelve 32-wide K-slice images; each wave then moves its
+// 32 token rows x 384 of them into registers (the MFMA B operand for the whole phase).  Phase 2
+// streams W_qkv in 9 chunks of 128 output columns x 3 K-steps of 128 through a 4-slot
+// global_load_lds ring (counted vmcnt, one barrier per step); wave = 64 output columns x 32
+// tokens, computed transposed (q|k|v^T = W . xn^T) so a lane holds 4 consecutive columns of one
+// token: + bias, x qscale (q), RoPE at the frame position (q, k), one 8-B store into the packed
+// temporal planes.  The K order is the unfused GEMM's, so q|k|v equal it up to the epilogue's
+// fp contraction.  LDS: phase-1 ring [0, 128K) | epilogue stage [0, 58K) + xn images [64K, 160K)
+// | phase-2 ring [0, 128K) + RoPE rows of the block's tokens + bias [128K, ...).
+struct RqArgs {
+  mdg_gemm_desc r, q;
+};
+constexpr int kRqThreads = 512;
+constexpr int kRqSmem = 160 * 1024;
+
+// s_waitcnt vmcnt(n) for a wave-uniform n in {0, 4, 8, 12, 16} (anything else: vmcnt(0))
+__device__ __forceinline__ void vm_wait_4x(int n) {
+  switch (n) {
+    case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
+__global__ __launch_bounds__(kRqThreads, 1) void rowln_qkv_kernel(const RqArgs args) {
+  constexpr int NCOL = 384, BM = 128, BK = 32, STAGES = 4, WTN = NCOL / 4, NT = WTN / 16, NE = NCOL / 128;
+  constexpr int STAGE = (BM + NCOL) * BK, ATILE = BM * BK, WLD = NCOL / 128;
+  constexpr int NCH = 3 * NCOL / 128, KS = NCOL / BK, QSTEPS = NCH * 3, IMG = 128 * BK, QSLOT = 4 * IMG;
+  static_assert(STAGES * STAGE * 2 == 131072 && 4 * QSLOT * 2 == 131072, "rings");
+  static_assert((32 * (NCOL + 4) + 6 * NCOL) * 4 <= 65536 && KS * BM * BK * 2 + 65536 == kRqSmem, "LDS plan");
+  typedef __attribute__((address_space(3))) void* lds_ptr_t;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const mdg_gemm_desc& p = args.r;  // out_proj + gated residual + LN_t
+  const mdg_gemm_desc& q = args.q;  // temporal q|k|v
+  bf16_t* lds = reinterpret_cast<bf16_t*>(smem);
+  bf16_t* Xs = reinterpret_cast<bf16_t*>(smem + 65536);
+  const int D = q.D, half = D >> 1;
+  float* Rs = reinterpret_cast<float*>(smem + 131072);  // [BM][D]: cos | sin of each token's pairs
+  float* Bq = Rs + BM * D;                               // [3 * NCOL]
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int M = p.M;
+  const int nwg = (M + BM - 1) / BM;
+  const int xcd = blockIdx.x & 7, loc = blockIdx.x >> 3, q8 = nwg >> 3, r8 = nwg & 7;
+  const int m0 = ((xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc) * BM;
+  const int ch = (lg ^ ((-(lr >> 2)) & 3)) * 8;
+
+  // ---------------------------------------------------------------- phase 1: out_proj row-LN
+  {
+    const int wm = wave / 4, wn = wave % 4;
+    const bf16_t* A = reinterpret_cast<const bf16_t*>(p.A);
+    const bf16_t* W = reinterpret_cast<const bf16_t*>(p.W);
+    const int arow = 16 * wave + (lane >> 2);
+    const bf16_t* asrc = A + (size_t)min(m0 + arow, M - 1) * p.lda + (((lane & 3) ^ ((-(arow >> 2)) & 3)) * 8);
+    const bf16_t* bsrc[WLD];
+#pragma unroll
+    for (int i = 0; i < WLD; ++i) {
+      const int row = 16 * (wave * WLD + i) + (lane >> 2);
+      bsrc[i] = W + (size_t)row * p.ldw + (((lane & 3) ^ ((-(row >> 2)) & 3)) * 8);
+    }
+    auto load = [&](int st, int k0) {
+      bf16_t* sa = lds + st * STAGE;
+      __builtin_amdgcn_global_load_lds((const void*)(asrc + k0), (lds_ptr_t)(sa + 16 * wave * BK), 16, 0, 0);
+#pragma unroll
+      for (int i = 0; i < WLD; ++i)
+        __builtin_amdgcn_global_load_lds((const void*)(bsrc[i] + k0), (lds_ptr_t)(sa + ATILE + 16 * (wave * WLD + i) * BK),
+                                         16, 0, 0);
+    };
+    float4 h4[2][NE];
+    rowln_load_band<NCOL>(p, m0, 0, h4);
+    f32x4 acc[4][NT];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    constexpr int nk = NCOL / BK;
+#pragma unroll
+    for (int s0 = 0; s0 < STAGES - 1; ++s0) load(s0, s0 * BK);
+    for (int kt = 0; kt < nk; ++kt) {
+      const int younger = min(STAGES - 2, nk - 1 - kt);
+      if (younger >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (1 + WLD)) : "memory");
+      else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(1 + WLD) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (kt + STAGES - 1 < nk) load((kt + STAGES - 1) % STAGES, (kt + STAGES - 1) * BK);
+      const bf16_t* As = lds + (kt % STAGES) * STAGE;
+      const bf16_t* Bs = As + ATILE;
+      bf16x8 a[4], b[NT];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = *reinterpret_cast<const bf16x8*>(As + (wm * 64 + i * 16 + lr) * BK + ch);
+#pragma unroll
+      for (int j = 0; j < NT; ++j) b[j] = *reinterpret_cast<const bf16x8*>(Bs + (wn * WTN + j * 16 + lr) * BK + ch);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    const float inv_rpm = 1.0f / (float)p.rows_per_mod;
+    rowln_fast_epilogue<NCOL>(p, acc, h4, smem, m0, fdiv(m0, p.rows_per_mod, inv_rpm), inv_rpm, Xs);
+  }
+
+  // ---------------------------------------------------------------- phase 2: temporal q|k|v
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();  // xn images complete; the epilogue stage is free
+  const int wah = wave >> 2, wat = wave & 3;  // 64 output columns x 32 tokens
+  const int T = q.T, L = q.L;
+  const float invL = 1.0f / (float)L, invT = 1.0f / (float)T, invD = 1.0f / (float)D;
+  // the RoPE rows of the block's tokens and the bias, into registers first (LDS after the xn
+  // images are read), issued before the ring so the ring's pieces stay the youngest loads
+  constexpr int RMAX = (BM * 48) / kRqThreads, BMAX = (3 * NCOL + kRqThreads - 1) / kRqThreads;
+  const int nR = q.rope ? BM * D : 0;
+  float rv[RMAX], bv[BMAX];
+  // (unpredicated loads of clamped indices: exec-masked ones made the compiler drain vmcnt)
+#pragma unroll
+  for (int k = 0; k < RMAX; ++k) rv[k] = 0.f;
+  if (nR) {
+#pragma unroll
+    for (int k = 0; k < RMAX; ++k) {
+      const int i = min(tid + k * kRqThreads, nR - 1);
+      const int tok = fdiv(i, D, invD), j = i - tok * D, hj = j < half ? j : j - half;
+      const int m = min(m0 + tok, M - 1), ml = fdiv(m, L, invL), t = ml - fdiv(ml, T, invT) * T;
+      rv[k] = q.rope[(size_t)((j < half ? 0 : q.rope_rows) + t) * half + hj];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < BMAX; ++k) bv[k] = q.bias ? q.bias[min(tid + k * kRqThreads, 3 * NCOL - 1)] : 0.f;
+  const bf16_t* Wq = reinterpret_cast<const bf16_t*>(q.W);
+  const int gimg = wave >> 1;
+  const int cswz = ((lane & 3) ^ ((-(lane >> 4)) & 3)) * 8;
+  int woff[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) woff[i] = (16 * (4 * (wave & 1) + i) + (lane >> 2)) * q.ldw + cswz;
+  // step s = (chunk s / 3, K rows 128 (s % 3) ..): image g = wave / 2, 16-row pieces 4 (wave & 1) + i
+  auto qissue = [&](int s) {
+    const int n = s / 3, kk = s - 3 * n;
+    bf16_t* sl = lds + (s & 3) * QSLOT + gimg * IMG;
+    const bf16_t* base = Wq + (size_t)n * 128 * q.ldw + (4 * kk + gimg) * BK;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(base + woff[i]), (lds_ptr_t)(sl + 16 * (4 * (wave & 1) + i) * BK), 16,
+                                       0, 0);
+  };
+  qissue(0);
+  qissue(1);  // slots 0, 1 = the dead ring / epilogue stage region
+  bf16x8 xr[2][KS];
+#pragma unroll
+  for (int ti = 0; ti < 2; ++ti)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+      xr[ti][ks] = *reinterpret_cast<const bf16x8*>(Xs + ks * (BM * BK) + (wat * 32 + ti * 16 + lr) * BK + ch);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  vm_wait_4x(4);  // step 0's pieces (and the RoPE / bias loads before them) landed
+  __builtin_amdgcn_s_barrier();  // every wave holds its xn rows: the image region is free
+  asm volatile("" ::: "memory");
+#pragma unroll
+  for (int k = 0; k < RMAX; ++k) {
+    const int i = tid + k * kRqThreads;
+    if (i < nR) lds_st1_raw(Rs + i, rv[k]);
+  }
+#pragma unroll
+  for (int k = 0; k < BMAX; ++k) {
+    const int i = tid + k * kRqThreads;
+    if (i < 3 * NCOL) lds_st1_raw(Bq + i, bv[k]);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // before step 1's barrier
+  qissue(2);
+  qissue(3);
+
+  // per-token plane row offsets: token m = (b T + t) L + l -> ((b L + l) H + head) T + t
+  const int H = q.H, BL = (M / (T * L)) * L;
+  const size_t plane = (size_t)BL * H * T * D;
+  size_t toff[2];
+#pragma unroll
+  for (int ti = 0; ti < 2; ++ti) {
+    const int m = min(m0 + wat * 32 + ti * 16 + lr, M - 1);
+    const int ml = fdiv(m, L, invL), l = m - ml * L, b = fdiv(ml, T, invT), t = ml - b * T;
+    toff[ti] = ((size_t)(b * L + l) * H * T + t) * D;
+  }
+  const bool full = m0 + BM <= M;  // every epilogue store is issued (the counted waits rely on it)
+  bf16_t* qo = reinterpret_cast<bf16_t*>(q.qkv_out);
+  for (int n = 0; n < NCH; ++n) {
+    f32x4 acc[4][2];
+#pragma unroll
+    for (int hi = 0; hi < 4; ++hi)
+#pragma unroll
+      for (int ti = 0; ti < 2; ++ti) acc[hi][ti] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < 3; ++kk) {
+      const int s = 3 * n + kk;
+      if (s > 0) {
+        // step s landed: leave the younger steps' pieces and (after chunk 0) the previous
+        // chunk's 8 stores in flight; then refill the slot step s - 1 used with step s + 3
+        const int younger = min(2, QSTEPS - 1 - s);
+        vm_wait_4x(4 * younger + (full && n > 0 ? 8 : 0));
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (s + 3 < QSTEPS) qissue(s + 3);
+      }
+      const bf16_t* sl = lds + (s & 3) * QSLOT + (wah * 64 + lr) * BK + ch;
+      // image g + 1's fragments are read while image g's MFMAs run
+      bf16x8 a[2][4];
+#pragma unroll
+      for (int hi = 0; hi < 4; ++hi) a[0][hi] = *reinterpret_cast<const bf16x8*>(sl + hi * 16 * BK);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        if (g < 3)
+#pragma unroll
+          for (int hi = 0; hi < 4; ++hi)
+            a[(g + 1) & 1][hi] = *reinterpret_cast<const bf16x8*>(sl + (g + 1) * IMG + hi * 16 * BK);
+        __builtin_amdgcn_sched_barrier(0);  // (keeps the scheduler from sinking the reads)
+#pragma unroll
+        for (int hi = 0; hi < 4; ++hi)
+#pragma unroll
+          for (int ti = 0; ti < 2; ++ti)
+            acc[hi][ti] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[g & 1][hi], xr[ti][4 * kk + g], acc[hi][ti], 0, 0, 0);
+      }
+    }
+    // chunk n = 128 columns of one of q | k | v
+    const int which = n / 3;
+    const float sc = which == 0 ? q.qscale : 1.0f;
+    const bool rope = q.rope && which < 2;
+#pragma unroll
+    for (int hi = 0; hi < 4; ++hi) {
+      const int col0 = n * 128 + wah * 64 + hi * 16 + lg * 4, w = col0 - which * NCOL;
+      const int head = fdiv(w, D, invD), cp = w - head * D;
+      f32x4 bb;
+      f32x2 cc[2], ss[2];
+      if (rope) {
+        const float* r0 = Rs + (wat * 32 + lr) * D + (cp >> 1);
+        const float* r1 = r0 + 16 * D;
+        lds_ld4_2x4_raw(Bq + col0, r0, r0 + half, r1, r1 + half, bb, cc[0], ss[0], cc[1], ss[1]);
+      } else {
+        bb = lds_ld4_raw(Bq + col0);
+        cc[0] = cc[1] = ss[0] = ss[1] = f32x2{0.f, 0.f};
+      }
+      bf16_t* dst = qo + which * plane + (size_t)head * T * D + cp;
+#pragma unroll
+      for (int ti = 0; ti < 2; ++ti) {
+        const int tok = wat * 32 + ti * 16 + lr;
+        float v0 = acc[hi][ti][0] + bb[0], v1 = acc[hi][ti][1] + bb[1], v2 = acc[hi][ti][2] + bb[2],
+              v3 = acc[hi][ti][3] + bb[3];
+        v0 *= sc; v1 *= sc; v2 *= sc; v3 *= sc;
+        if (rope) {
+          const f32x2 c2 = cc[ti], s2 = ss[ti];
+          // (explicit fma, as epi_tile8: the two paths round alike)
+          const float x0 = __builtin_fmaf(v0, c2[0], -(v1 * s2[0])), y0 = __builtin_fmaf(v1, c2[0], v0 * s2[0]);
+          const float x1 = __builtin_fmaf(v2, c2[1], -(v3 * s2[1])), y1 = __builtin_fmaf(v3, c2[1], v2 * s2[1]);
+          v0 = x0; v1 = y0; v2 = x1; v3 = y1;
+        }
+        if (full || m0 + tok < M) {
+          bf16x4 o;
+          o[0] = (bf16_t)v0; o[1] = (bf16_t)v1; o[2] = (bf16_t)v2; o[3] = (bf16_t)v3;
+          *reinterpret_cast<bf16x4*>(dst + toff[ti]) = o;
+        }
+      }
+    }
+  }
+}
+
+// Envelope: bf16; out_proj = PLAIN GATE_RES, K = N = 384, LN output on, tiles over <= 2 adaLN
+// entries; q|k|v = the temporal QKV epilogue into packed planes, N = 1152, head_dim D % 8 == 0
+// and <= 48 (the RoPE rows of 128 tokens fit next to the ring), no training outputs.
+bool rowln_qkv_supported(const mdg_gemm_desc& r, const mdg_gemm_desc& q) {
+  return r.dtype == MDG_BF16 && q.dtype == MDG_BF16 && r.a_mode == MDG_A_PLAIN && r.epi == MDG_EPI_GATE_RES &&
+         r.K == 384 && r.N == 384 && r.M > 0 && r.rows_per_mod >= 128 && r.resid && !r.resid_in && !r.aux &&
+         r.xn_out && r.xn_mods && r.lda % 8 == 0 && r.ldw % 8 == 0 && r.ldr % 4 == 0 && q.epi == MDG_EPI_QKV &&
+         q.qkv_layout == MDG_QKV_TEMPORAL_PACKED && q.qkv_out && q.W && q.M == r.M && q.N == 3 * 384 && q.K == 384 &&
+         q.ldw % 8 == 0 && !q.aux && q.D > 0 && q.D % 8 == 0 && q.D <= 48 && q.H * q.D == 384 && q.T > 0 && q.L > 0 &&
+         r.M % (q.T * q.L) == 0 && (!q.rope || q.rope_rows >= q.T);
+}
+
+hipError_t rowln_qkv_launch(const mdg_gemm_desc& r, const mdg_gemm_desc& q, hipStream_t s) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&rowln_qkv_kernel),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, kRqSmem);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  RqArgs a;
+  a.r = r;
+  a.q = q;
+  hipLaunchKernelGGL(rowln_qkv_kernel, dim3((r.M + 127) / 128), dim3(kRqThreads), kRqSmem, s, a);
   return hipGetLastError();
 }
 

@@ -181,6 +181,72 @@ def test_mlp_fused_rejects_unsupported_shapes(lib):
     assert lib.mdg_mlp_fused(ctypes.byref(d1), ctypes.byref(d2), _s()) == 1001
 
 
+@pytest.mark.parametrize("B,T,L,rope", [(2, 37, 4, True), (8, 250, 4, True), (1, 32, 4, False), (3, 64, 5, True)])
+def test_rowln_qkv_equals_out_proj_then_qkv(lib, B, T, L, rope):
+    """mdg_rowln_qkv (spatial out_proj + gated residual + LN_t, then the temporal q|k|v into
+    packed planes, LN_t(h) on chip) against the same two descriptors through mdg_gemm: h
+    bit-identical (the same row-LN epilogue); q|k|v bit-identical too (the same bf16 LN rows,
+    the same K order, the same epilogue arithmetic).  Partial last tiles
+    (M % 128 != 0), tiles over two trajectories, with and without RoPE; xn is not written."""
+    from mdgen_finetune_amd import _lib
+
+    H, D = 16, 24
+    C, M, TL = H * D, B * T * L, T * L
+    g = torch.Generator(device="cuda").manual_seed(M + T)
+    o = torch.randn(M, C, device="cuda", generator=g).to(torch.bfloat16)
+    Wo = (torch.randn(C, C, device="cuda", generator=g) / math.sqrt(C)).to(torch.bfloat16)
+    bo = torch.randn(C, device="cuda", generator=g) * 0.5
+    Wq = (torch.randn(3 * C, C, device="cuda", generator=g) / math.sqrt(C)).to(torch.bfloat16)
+    bq = torch.randn(3 * C, device="cuda", generator=g) * 0.5
+    mods = torch.randn(B, 9 * C, device="cuda", generator=g) * 0.5
+    h0 = torch.randn(M, C, device="cuda", generator=g) * 2
+    inv = 1.0 / (10000 ** (torch.arange(0, D, 2).float() / D))
+    f = torch.arange(T + 1).float()[:, None] * inv
+    table = torch.cat([f.cos().reshape(-1), f.sin().reshape(-1)]).cuda()
+    outs = []
+    for fused in (False, True):
+        h = h0.clone()
+        xo = torch.zeros(M, C, device="cuda", dtype=torch.bfloat16)
+        planes = torch.zeros(3, B * L, H, T, D, device="cuda", dtype=torch.bfloat16)
+        r = _desc(dtype=1, a_mode=0, epi=1, M=M, N=C, K=C, A=o.data_ptr(), lda=C, W=Wo.data_ptr(), ldw=C,
+                  bias=bo.data_ptr(), mod_stride=9 * C, rows_per_mod=TL, resid=h.data_ptr(), ldr=C,
+                  gate=mods.data_ptr(), gate_off=2 * C, xn_out=xo.data_ptr(), xn_mods=mods.data_ptr(),
+                  xn_mod_stride=9 * C, xn_shift_off=3 * C, xn_scale_off=4 * C, ln_eps=1e-6)
+        q = _desc(dtype=1, a_mode=0, epi=2, M=M, N=3 * C, K=C, A=xo.data_ptr(), lda=C, W=Wq.data_ptr(), ldw=C,
+                  bias=bq.data_ptr(), qkv_layout=2, qkv_out=planes.data_ptr(), H=H, D=D, T=T, L=L, qscale=0.3,
+                  rope=table.data_ptr() if rope else 0, rope_rows=T + 1)
+        if fused:
+            _lib.check(lib.mdg_rowln_qkv(ctypes.byref(r), ctypes.byref(q), _s()), "mdg_rowln_qkv")
+        else:
+            _lib.check(lib.mdg_gemm(ctypes.byref(r), _s()), "out_proj")
+            _lib.check(lib.mdg_gemm(ctypes.byref(q), _s()), "qkv")
+        outs.append((h, xo, planes))
+    torch.cuda.synchronize()
+    (h_ref, x_ref, p_ref), (h_f, x_f, p_f) = outs
+    b = torch.arange(M, device="cuda") // TL
+    href = h0 + mods[b, 2 * C:3 * C] * (o.float() @ Wo.float().T + bo)
+    torch.testing.assert_close(h_f, href, rtol=5e-3, atol=5e-3)
+    assert torch.equal(h_f, h_ref), (h_f - h_ref).abs().max().item()
+    assert not x_f.any()  # LN_t(h) stayed on chip
+    assert x_ref.any()
+    # (both epilogues: + bias, x qscale, RoPE with explicit fma -> bf16)
+    assert torch.equal(p_f, p_ref), ((p_f.float() - p_ref.float()).abs().max().item(), int((p_f != p_ref).sum()))
+
+
+def test_rowln_qkv_rejects_unsupported_shapes(lib):
+    r = _desc(dtype=1, a_mode=0, epi=1, M=256, N=384, K=384, A=1, lda=384, W=1, ldw=384, resid=1, ldr=384,
+              rows_per_mod=256, xn_out=1, xn_mods=1)
+    q = _desc(dtype=1, a_mode=0, epi=2, M=256, N=3 * 384, K=384, A=1, lda=384, W=1, ldw=384, qkv_layout=1,
+              qkv_out=1, H=16, D=24, T=64, L=4)
+    assert lib.mdg_rowln_qkv(ctypes.byref(r), ctypes.byref(q), _s()) == 1001  # padded planes
+    q.qkv_layout = 2
+    r.rows_per_mod = 64  # tiles over > 2 trajectories
+    assert lib.mdg_rowln_qkv(ctypes.byref(r), ctypes.byref(q), _s()) == 1001
+    r.rows_per_mod = 256
+    q.H, q.D = 6, 64  # head_dim > 48
+    assert lib.mdg_rowln_qkv(ctypes.byref(r), ctypes.byref(q), _s()) == 1001
+
+
 def _rope_ref(x, pos, inv_freq):
     # x [..., D] at integer positions pos [...]
     half = x.shape[-1] // 2

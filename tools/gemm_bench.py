@@ -82,8 +82,39 @@ def run_mlp(M, C=384, F=1536, rpm=4000):
           f"{t1 + t2:7.1f} us", flush=True)
 
 
+def run_rq(B=8, T=1000, L=4, H=16, D=24):
+    """mdg_rowln_qkv vs mdg_gemm(out_proj row-LN) + mdg_gemm(temporal q|k|v) on one lane's shape."""
+    C, M = H * D, B * T * L
+    o = (torch.randn(M, C, device="cuda") * 0.5).to(torch.bfloat16)
+    Wo = (torch.randn(C, C, device="cuda") / C ** 0.5).to(torch.bfloat16)
+    Wq = (torch.randn(3 * C, C, device="cuda") / C ** 0.5).to(torch.bfloat16)
+    bo, bq = torch.randn(C, device="cuda"), torch.randn(3 * C, device="cuda")
+    resid, xn = torch.zeros(M, C, device="cuda"), torch.empty(M, C, device="cuda", dtype=torch.bfloat16)
+    planes = torch.empty(3 * M * C, device="cuda", dtype=torch.bfloat16)
+    mods = torch.randn(B, 9 * C, device="cuda") * 0.1
+    rope = torch.randn(2 * (T + 1) * (D // 2), device="cuda")
+    r, q = _lib.MdgGemmDesc(), _lib.MdgGemmDesc()
+    r.dtype, r.a_mode, r.epi, r.M, r.N, r.K = 1, 0, 1, M, C, C
+    r.A, r.lda, r.W, r.ldw, r.bias = o.data_ptr(), C, Wo.data_ptr(), C, bo.data_ptr()
+    r.resid, r.ldr, r.gate, r.gate_off, r.mod_stride, r.rows_per_mod = resid.data_ptr(), C, mods.data_ptr(), 2 * C, 9 * C, T * L
+    r.xn_out, r.xn_mods, r.xn_mod_stride, r.xn_shift_off, r.xn_scale_off, r.ln_eps = (xn.data_ptr(), mods.data_ptr(),
+                                                                                       9 * C, 3 * C, 4 * C, 1e-6)
+    q.dtype, q.a_mode, q.epi, q.M, q.N, q.K = 1, 0, 2, M, 3 * C, C
+    q.A, q.lda, q.W, q.ldw, q.bias = xn.data_ptr(), C, Wq.data_ptr(), C, bq.data_ptr()
+    q.qkv_layout, q.qkv_out, q.H, q.D, q.T, q.L, q.qscale = 2, planes.data_ptr(), H, D, T, L, 0.3
+    q.rope, q.rope_rows = rope.data_ptr(), T + 1
+    s = torch.cuda.current_stream().cuda_stream
+    fused = tm(lambda: _lib.check(lib.mdg_rowln_qkv(ctypes.byref(r), ctypes.byref(q), s), "rq"))
+    t1 = tm(lambda: _lib.check(lib.mdg_gemm(ctypes.byref(r), s), "out_proj"))
+    t2 = tm(lambda: _lib.check(lib.mdg_gemm(ctypes.byref(q), s), "qkv"))
+    print(f"rq M={M}: mdg fused {fused:8.1f} us   out_proj {t1:7.1f} + qkv {t2:7.1f} = {t1 + t2:7.1f} us", flush=True)
+
+
 if __name__ == "__main__":
     import sys as _s
+    if len(_s.argv) > 1 and _s.argv[1] == "rq":
+        run_rq()
+        _s.exit(0)
     if len(_s.argv) > 1 and _s.argv[1] == "mlp":
         for M in (32000, 64000):
             run_mlp(M)

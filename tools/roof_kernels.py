@@ -1,5 +1,5 @@
-"""Launch the roofline kernels of bench.py (fc2 row-LN GEMM, temporal q|k|v GEMM, temporal
-attention) at the bench's per-lane shape after one eager sampling window, for rocprofv3 counter passes
+"""Launch the roofline kernels of bench.py (fused MLP, fused out_proj + q|k|v, row-LN GEMM,
+temporal attention) at the bench's per-lane shape after one eager sampling window, for rocprofv3 counter passes
 (tools/roof_pmc.sh).  Usage: python tools/roof_kernels.py [B T L]"""
 import os
 import sys

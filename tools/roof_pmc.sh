@@ -8,7 +8,7 @@ cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 D=gpurun_out/pmc_roof${ROOF_ARGS:+_${ROOF_ARGS// /_}}
 mkdir -p $D
 for C in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 400 rocprofv3 --pmc $C --kernel-include-regex "gemm_bf16_b4|attn_temporal_bf16|gemm_rowln|mlp_rowln" \
+  timeout -k 10 400 rocprofv3 --pmc $C --kernel-include-regex "gemm_bf16_b4|attn_temporal_bf16|gemm_rowln|mlp_rowln|rowln_qkv" \
     --output-format csv -d $D -o $C -- python tools/roof_kernels.py ${ROOF_ARGS:-} \
     > $D/log_$C.txt 2>&1 || exit $?
 done
