@@ -90,7 +90,7 @@ for cname, scale in (("FETCH_SIZE", 2 * 1024), ("WRITE_SIZE", 1024)):
         last = [x[1] for x in v[-50:]]
         res[name][cname] = sum(last) / len(last) * scale
 tpath = os.path.join(out, f"traffic_r{rr}.json")
-traffic = {} if default_shape or not os.path.exists(tpath) else json.load(open(tpath))
+traffic = json.load(open(tpath)) if os.path.exists(tpath) else {}  # (other shapes' entries kept)
 for name, d in res.items():
     if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
         e = traffic.setdefault(name, {})
