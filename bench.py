@@ -232,7 +232,10 @@ def roofline(eng, st, dtype, B, T, L):
                      "avg_launch_us": round(sec * 1e6, 2), "flops_per_launch": flops, "bytes_per_launch": nbytes,
                      "intensity_flop_per_byte": round(flops / nbytes, 1),
                      "mfma_frac": round(mfma_ach / PEAK_TFLOPS[dtype], 4),
-                     "hbm_frac": round(hbm_ach / PEAK_HBM_GBS, 4), "shape": f"B={B} T={T} L={L}"}
+                     "hbm_frac": round(hbm_ach / PEAK_HBM_GBS, 4), "shape": f"B={B} T={T} L={L}",
+                     "timing": "standalone: 50 back-to-back launches outside the graph, one lane's shape, the "
+                               "step's workspace activations and layer-0 weights, zero adaLN rows; in the graph two "
+                               "lanes share the chip and each launch takes longer (profiles/r02_summary.md)"}
     return out
 
 
