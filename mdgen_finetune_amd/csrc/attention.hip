@@ -286,6 +286,11 @@ __global__ __launch_bounds__(256) void attn_temporal_kernel(const CT* __restrict
 // fails, the block reruns with the growth-tested offset (raised whenever a score outgrows it
 // by kGrow), the only path whose P stay bounded.
 typedef __attribute__((ext_vector_type(16))) float f32x16;
+// timing diagnostics only (tools/diag_mlp_attn.sh): 1 = exp2 replaced by the identity, 2 = no
+// K / V chunk restaged after the first.  Results are wrong in every diagnostic build.
+#ifndef MDG_DIAG_ATTN
+#define MDG_DIAG_ATTN 0
+#endif
 
 // One 64-key sub-chunk of the bf16 temporal attention (K / V images of its 64 rows at Kc /
 // Vc, key-padding bias at kbsub): S^T = K Q^T (4 MFMAs), growth test / rare offset raise,
@@ -345,7 +350,8 @@ __device__ __forceinline__ void ta_subchunk(const bf16_t* Kc, const bf16_t* Vc, 
     for (int s2 = 0; s2 < 2; ++s2) {
       bf16x8 pf;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) pf[j] = (bf16_t)__builtin_amdgcn_exp2f(sacc[kt][8 * s2 + j]);
+      for (int j = 0; j < 8; ++j)
+        pf[j] = (bf16_t)(MDG_DIAG_ATTN == 1 ? sacc[kt][8 * s2 + j] : __builtin_amdgcn_exp2f(sacc[kt][8 * s2 + j]));
       const bf16_t* vb = Vc + (kt * 32 + 16 * s2 + grow) * DP + gcol;
       const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(vb));
       const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(vb + 8 * DP));
@@ -522,7 +528,7 @@ __global__ __launch_bounds__(kTW * 64, 4) void attn_temporal_bf16_kernel(const b
     __syncthreads();
     for (int c = 0; c < nchunks; ++c) {
       const int cur = c & 1;
-      if (c + 1 < nchunks) MDG_TA_GLOAD(c + 1);
+      if (c + 1 < nchunks && MDG_DIAG_ATTN != 2) MDG_TA_GLOAD(c + 1);
       int mflag = 0;
 #pragma unroll
       for (int f = 0; f < KC / 64; ++f) mflag |= kflag[cur][f];
@@ -533,7 +539,7 @@ __global__ __launch_bounds__(kTW * 64, 4) void attn_temporal_bf16_kernel(const b
       for (int sub = 0; sub < KC / 64; ++sub)
         ta_subchunk(Kc + sub * 64 * DP, Vc + sub * 64 * DP, kbs[cur] + sub * 64, masked, grow, r, h, grow_r, gcol,
                     padS, padH, padJ, qf, mt, o);
-      if (c + 1 < nchunks) MDG_TA_LSTORE(cur ^ 1);
+      if (c + 1 < nchunks && MDG_DIAG_ATTN != 2) MDG_TA_LSTORE(cur ^ 1);
       __syncthreads();
     }
 #undef MDG_TA_GLOAD

@@ -20,6 +20,8 @@ GemmPlan gemm_plan(const mdg_gemm_desc& p);
 hipError_t gemm_launch(const mdg_gemm_desc& p, const GemmPlan& g, hipStream_t s);
 bool mlp_fused_supported(const mdg_gemm_desc& f1, const mdg_gemm_desc& f2);
 hipError_t mlp_fused_launch(const mdg_gemm_desc& f1, const mdg_gemm_desc& f2, hipStream_t s);
+bool final_euler_supported(const mdg_gemm_desc& p);
+hipError_t final_euler_launch(const mdg_gemm_desc& p, hipStream_t s);
 bool rowln_qkv_supported(const mdg_gemm_desc& r, const mdg_gemm_desc& q);
 hipError_t rowln_qkv_launch(const mdg_gemm_desc& r, const mdg_gemm_desc& q, hipStream_t s);
 hipError_t attn_temporal_launch(int dtype, int B, int T, int L, int H, int D, const void* qkv_t,
@@ -139,6 +141,16 @@ bool fused_mlp_on() {
 bool fused_qkv_on() {
   static const bool on = [] {
     const char* e = getenv("MDG_FUSED_QKV");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+// bf16, latent <= 32: the FinalLayer + Euler update as its own one-pass kernel;
+// MDG_FAST_FINAL=0 keeps the generic EULER GEMM (A/B knob)
+bool fast_final_on() {
+  static const bool on = [] {
+    const char* e = getenv("MDG_FAST_FINAL");
     return !(e && e[0] == '0');
   }();
   return on;
@@ -287,6 +299,8 @@ int mdg_gemm(const mdg_gemm_desc* g, void* stream) {
     default:
       return fail(MDG_E_ARG, "gemm: epi %d", g->epi);
   }
+  if (g->epi == MDG_EPI_EULER && fast_final_on() && mdg::final_euler_supported(*g))
+    return hip_check(mdg::final_euler_launch(*g, (hipStream_t)stream), "final euler launch");
   const mdg::GemmPlan plan = mdg::gemm_plan(*g);
   if (plan.cfg < 0) return fail(MDG_E_SHAPE, "gemm: no tile fits N=%d", g->N);
   if (plan.smem > 160 * 1024)
@@ -587,7 +601,7 @@ static int denoise_range(const mdg_model* m, const mdg_step_io* io, const float*
   g.A = xn; g.lda = d->C; g.W = m->w_final; g.ldw = d->C; g.bias = m->b_final;
   g.out = io->x_out; g.ldo = d->latent; g.x_in = io->x_in; g.v_out = io->v_out; g.dt = io->dt;
   g.n_valid = d->latent;
-  return mdg_gemm(&g, stream);
+  return mdg_gemm(&g, stream);  // bf16: the one-pass final_euler_kernel
 }
 
 int mdg_denoise_step(const mdg_model* m, const mdg_step_io* io, const float* mask, void* ws, void* stream) {

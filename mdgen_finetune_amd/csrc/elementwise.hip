@@ -234,13 +234,11 @@ __global__ __launch_bounds__(256, 4) void embed_ln_kernel(int N, int TL, int L, 
   const int K = KC ? KC : Kr;
   extern __shared__ __attribute__((aligned(16))) float wl[];  // [K][C]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  for (int i = tid; i < K * C / 4; i += 256) reinterpret_cast<float4*>(wl)[i] = reinterpret_cast<const float4*>(Wt)[i];
-  __syncthreads();
   const float invC = 1.0f / (float)C;
   const int groups = (N + 16 - 1) / 16;
   for (int gi = blockIdx.x; gi < groups; gi += gridDim.x) {
     const int r0 = gi * 16 + wave * R;
-    float2 hv[R][NE], sv[NE], cv[NE];
+    float2 hv[R][NE], uv[R][NE], sv[NE], cv[NE];
     float xv[R];
     // shift / scale of the first row's batch entry; a row of another entry (a group that
     // straddles a trajectory boundary) reloads its own below
@@ -260,13 +258,32 @@ __global__ __launch_bounds__(256, 4) void embed_ln_kernel(int N, int TL, int L, 
 #pragma unroll
       for (int e = 0; e < NE; ++e) {
         const int k = 2 * lane + 128 * e;
-        float2 t = *reinterpret_cast<const float2*>(base + (size_t)n * C + k);
-        if (ipa) {
-          const float2 u = *reinterpret_cast<const float2*>(ipa + ((size_t)b * L + l) * C + k);
-          t.x += u.x; t.y += u.y;
-        }
-        hv[rr][e] = t;
+        hv[rr][e] = *reinterpret_cast<const float2*>(base + (size_t)n * C + k);
+        uv[rr][e] = ipa ? *reinterpret_cast<const float2*>(ipa + ((size_t)b * L + l) * C + k) : make_float2(0.f, 0.f);
       }
+    }
+    // W_l2e^T is staged after the first group's row loads are issued, so its L2 round trip
+    // and the block barrier overlap their HBM latency instead of preceding it
+    // (LDS DMA: all of a thread's pieces in flight at once, next to the row loads)
+    if (gi == (int)blockIdx.x) {
+      typedef __attribute__((address_space(3))) void* lds_ptr_t;
+      const int n4 = K * C / 4;
+      for (int u = 0; u * 256 < n4; ++u) {
+        const int i0 = u * 256 + wave * 64;  // this wave's 64 float4 pieces
+        if (i0 + lane < n4)
+          __builtin_amdgcn_global_load_lds((const void*)(Wt + 4 * (size_t)(i0 + lane)), (lds_ptr_t)(wl + 4 * i0), 16, 0, 0);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+    if (ipa) {
+#pragma unroll
+      for (int rr = 0; rr < R; ++rr)
+#pragma unroll
+        for (int e = 0; e < NE; ++e) {
+          hv[rr][e].x += uv[rr][e].x;
+          hv[rr][e].y += uv[rr][e].y;
+        }
     }
     float2 a[R][NE];
 #pragma unroll

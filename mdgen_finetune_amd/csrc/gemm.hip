@@ -41,6 +41,15 @@ namespace mdg {
 
 constexpr int kThreads = 512;
 
+// x + dt * v rounded twice, as torchdiffeq's Euler step computes it (integrators.py:106-113:
+// dt * f, then y0 + that).  hipcc's __fmul_rn / __fadd_rn are plain operations that the
+// default -ffp-contract=fast fuses into one v_fma (one rounding); contraction is off here.
+__device__ __forceinline__ float euler_update(float x, float dt, float v) {
+#pragma clang fp contract(off)
+  const float dv = dt * v;
+  return x + dv;
+}
+
 // floor(a / d) for 0 <= a < 2^24 with a float reciprocal + one-step fix-up
 __device__ __forceinline__ int fdiv(int a, int d, float inv) {
   int q = (int)((float)a * inv);
@@ -120,7 +129,7 @@ __device__ __forceinline__ void epi4(const mdg_gemm_desc& p, int m, int n, float
       if (n + e < p.n_valid) {
         if (p.v_out) p.v_out[rowoff + n + e] = vv[e];
         float* xo = reinterpret_cast<float*>(p.out);
-        if (xo) xo[rowoff + n + e] = __fadd_rn(p.x_in[rowoff + n + e], __fmul_rn(p.dt, vv[e]));
+        if (xo) xo[rowoff + n + e] = euler_update(p.x_in[rowoff + n + e], p.dt, vv[e]);
       }
     }
   }
@@ -1405,6 +1414,12 @@ static hipError_t launch_rowln(const mdg_gemm_desc& p, hipStream_t s) {
 struct MlpArgs {
   mdg_gemm_desc f1, f2;
 };
+// timing diagnostics only (tools/diag_mlp_attn.sh builds them into separate libraries): 1 = xn
+// staged for the first hidden chunk only, 2 = GELU replaced by the identity, 3 = nothing staged
+// after the first chunk.  Results are wrong in every diagnostic build.
+#ifndef MDG_DIAG_MLP
+#define MDG_DIAG_MLP 0
+#endif
 constexpr int kMlpThreads = 512, kMlpHC = 128, kMlpStages = 3, kMlpSlot = 512 * 32;
 
 __host__ __device__ constexpr size_t mlp_smem(int F) {
@@ -1510,6 +1525,7 @@ __global__ __launch_bounds__(kMlpThreads, 1) void mlp_rowln_kernel(const MlpArgs
   auto issue = [&](int s) {
     bf16_t* sl = ring + (s % STAGES) * SLOT;
     const int j = s / 10, t = s % 10;
+    if ((MDG_DIAG_MLP == 1 && xw && t < 6 && j > 0) || (MDG_DIAG_MLP == 3 && j > 0)) return;
     if (t < 6) {
       const bf16_t* base = abase + (size_t)t * 2 * BK + (xw ? (size_t)0 : (size_t)j * HC * q.ldw);
 #pragma unroll
@@ -1584,7 +1600,8 @@ __global__ __launch_bounds__(kMlpThreads, 1) void mlp_rowln_kernel(const MlpArgs
         const int hb = wah * 64 + hi * 16 + lg * 4, tok = wat * 32 + ti * 16 + lr;
         bf16x4 o;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = (bf16_t)gelu_fast(acc1[hi][ti][r] + b1v[hi][r]);
+        for (int r = 0; r < 4; ++r)
+          o[r] = (bf16_t)(MDG_DIAG_MLP == 2 ? acc1[hi][ti][r] + b1v[hi][r] : gelu_fast(acc1[hi][ti][r] + b1v[hi][r]));
         *reinterpret_cast<bf16x4*>(Hs + tok * HC + (((hb >> 3) ^ (tok & 15)) * 8) + (hb & 7)) = o;
         acc1[hi][ti] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
@@ -1609,6 +1626,89 @@ __global__ __launch_bounds__(kMlpThreads, 1) void mlp_rowln_kernel(const MlpArgs
   float4 h4[2][NE];
   rowln_load_band<NCOL>(p, m0, 0, h4);  // band 0's residual rows
   rowln_fast_epilogue<NCOL>(p, acc2, h4, smem, m0, fdiv(m0, p.rows_per_mod, inv_rpm), inv_rpm);
+}
+
+// ---------------------------------------------------------------------------------------
+// FinalLayer + Euler update of the bf16 denoise step (layers.py:58-75 then
+// integrators.py:106-113): v = xn . W^T + b, x_out = x_in + dt * v for latent <= 32 columns.
+// The generic 64x32 GEMM took ~35 us for 25 MB (six barrier-separated register-staged
+// K-steps per 64 rows: latency, not bandwidth).  Here one wave owns 16 token rows and loads
+// them straight into its MFMA A fragments, every K at once (one HBM round trip per wave);
+// W^T (32 x C, pad rows 0) is staged once per block in LDS (rows padded by 16 B, so the
+// 16-lane fragment reads hit distinct bank slots), issued beside the row loads.  The
+// v_mfma_f32_16x16x32_bf16 chain runs in ascending K like the generic GEMM's, so v is equal
+// to it bit for bit.
+template <int KC>
+__global__ __launch_bounds__(256) void final_euler_kernel(const mdg_gemm_desc p) {
+  constexpr int KS = KC / 32, LDW = KC + 8, WCH = 32 * KC / 8;  // 16-B chunks of W
+  constexpr int WPT = (WCH + 255) / 256;
+  __shared__ __attribute__((aligned(16))) bf16_t Ws[32 * LDW];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int M = p.M;
+  const int m0 = blockIdx.x * 64 + wave * 16;
+  const bf16_t* A = reinterpret_cast<const bf16_t*>(p.A) + (size_t)min(m0 + lr, M - 1) * p.lda + 8 * lg;
+  bf16x8 a[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) a[ks] = *reinterpret_cast<const bf16x8*>(A + 32 * ks);
+  const bf16_t* W = reinterpret_cast<const bf16_t*>(p.W);
+  u32x4 wr[WPT];
+#pragma unroll
+  for (int u = 0; u < WPT; ++u) {
+    const int c = tid + 256 * u;
+    if (c < WCH) wr[u] = *reinterpret_cast<const u32x4*>(W + (size_t)(c / (KC / 8)) * p.ldw + 8 * (c % (KC / 8)));
+  }
+#pragma unroll
+  for (int u = 0; u < WPT; ++u) {
+    const int c = tid + 256 * u;
+    if (c < WCH) *reinterpret_cast<u32x4*>(Ws + (c / (KC / 8)) * LDW + 8 * (c % (KC / 8))) = wr[u];
+  }
+  __syncthreads();
+  f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      const bf16x8 b = *reinterpret_cast<const bf16x8*>(Ws + (16 * nt + lr) * LDW + 32 * ks + 8 * lg);
+      acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ks], b, acc[nt], 0, 0, 0);
+    }
+  }
+  // lane: rows 4 lg + r, column 16 nt + lr
+  float* xo = reinterpret_cast<float*>(p.out);
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) {
+    const int n = 16 * nt + lr;
+    if (n >= p.n_valid) continue;
+    const float bn = p.bias ? p.bias[n] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = m0 + 4 * lg + r;
+      if (m >= M) continue;
+      const size_t o = (size_t)m * p.ldo + n;
+      const float v = acc[nt][r] + bn;
+      if (p.v_out) p.v_out[o] = v;
+      if (xo) xo[o] = euler_update(p.x_in[o], p.dt, v);
+    }
+  }
+}
+
+// bf16 EULER GEMM with plain A, latent <= 32 (N = 32 with the pad rows), C in {128 .. 512}
+// (mdg_gemm routes such a descriptor here; MDG_FAST_FINAL=0 keeps the generic GEMM)
+bool final_euler_supported(const mdg_gemm_desc& p) {
+  return p.dtype == MDG_BF16 && p.a_mode == MDG_A_PLAIN && p.epi == MDG_EPI_EULER && p.N == 32 && p.n_valid <= 32 &&
+         (p.K == 128 || p.K == 256 || p.K == 384 || p.K == 512) && p.lda % 8 == 0 && p.ldw % 8 == 0 && p.M > 0 &&
+         (p.out || p.v_out);
+}
+
+hipError_t final_euler_launch(const mdg_gemm_desc& p, hipStream_t s) {
+  const dim3 grid((p.M + 63) / 64);
+  switch (p.K) {
+    case 128: hipLaunchKernelGGL((final_euler_kernel<128>), grid, dim3(256), 0, s, p); break;
+    case 256: hipLaunchKernelGGL((final_euler_kernel<256>), grid, dim3(256), 0, s, p); break;
+    case 384: hipLaunchKernelGGL((final_euler_kernel<384>), grid, dim3(256), 0, s, p); break;
+    default: hipLaunchKernelGGL((final_euler_kernel<512>), grid, dim3(256), 0, s, p); break;
+  }
+  return hipGetLastError();
 }
 
 // The fused MLP's shape envelope: bf16, C = 384, F % 128 == 0, fc1 = PLAIN STORE + GELU, fc2 =

@@ -575,3 +575,46 @@ def test_gemm_attn_spatial_rejects_unsupported_shapes(lib):
     d = _desc(dtype=1, a_mode=0, epi=_lib.MDG_EPI_ATTN_SPATIAL, M=8, N=3 * 64, K=64, A=x.data_ptr(), lda=64,
               W=x.data_ptr(), ldw=64, H=4, D=16, L=4, out=x.data_ptr(), ldo=64, kvb=x.data_ptr())
     assert lib.mdg_gemm(ctypes.byref(d), _s()) == 1001  # D != 24: the two-launch path covers it
+
+
+def _euler_desc(xn, W, b, xin, xo, vo, latent, dt):
+    from mdgen_finetune_amd import _lib
+
+    d = _lib.MdgGemmDesc()
+    M, C = xn.shape
+    d.dtype, d.a_mode, d.epi, d.M, d.N, d.K = 1, 0, 3, M, W.shape[0], C
+    d.A, d.lda, d.W, d.ldw, d.bias = xn.data_ptr(), C, W.data_ptr(), C, b.data_ptr()
+    d.out, d.ldo, d.x_in, d.v_out, d.dt, d.n_valid = xo.data_ptr(), latent, xin.data_ptr(), vo.data_ptr(), dt, latent
+    return d
+
+
+@pytest.mark.parametrize("M,C,latent", [(37, 384, 21), (1000, 384, 21), (32000, 384, 21), (4100, 384, 28),
+                                        (640, 128, 32), (333, 512, 21), (96, 256, 7)])
+def test_final_euler_plain_bf16(lib, M, C, latent):
+    """bf16 FinalLayer + Euler on the LN'd operand (the denoise step's last launch:
+    final_euler_kernel via mdg_gemm): equal bit for bit to the generic EULER GEMM (forced by
+    an N = 64 descriptor: the same K order on the same MFMA), and to the fp32 product of the
+    bf16 operands within accumulation-order rounding; x_out = x_in + dt * v exactly."""
+    from mdgen_finetune_amd import _lib
+
+    g = torch.Generator(device="cuda").manual_seed(M + C + latent)
+    xn = torch.randn(M, C, device="cuda", generator=g).to(torch.bfloat16)
+    W = torch.zeros(64, C, device="cuda")
+    W[:latent] = torch.randn(latent, C, device="cuda", generator=g) / C ** 0.5
+    W = W.to(torch.bfloat16)
+    b = torch.zeros(64, device="cuda")
+    b[:latent] = torch.randn(latent, device="cuda", generator=g)
+    xin = torch.randn(M, latent, device="cuda", generator=g)
+    outs = []
+    for n in (32, 64):  # 32: final_euler_kernel; 64: the generic GEMM
+        xo = torch.full_like(xin, float("nan"))
+        vo = torch.full_like(xin, float("nan"))
+        d = _euler_desc(xn, W[:n].contiguous(), b[:n].contiguous(), xin, xo, vo, latent, 0.375)
+        _lib.check(lib.mdg_gemm(ctypes.byref(d), _s()), "euler gemm")
+        outs.append((xo, vo))
+    torch.cuda.synchronize()
+    (xo, vo), (xo_g, vo_g) = outs
+    assert torch.equal(vo, vo_g) and torch.equal(xo, xo_g)
+    vref = xn.float() @ W.float()[:latent].T + b[:latent]
+    torch.testing.assert_close(vo, vref, rtol=1e-5, atol=1e-5)
+    assert torch.equal(xo, xin + 0.375 * vo)
