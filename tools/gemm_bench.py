@@ -110,8 +110,33 @@ def run_rq(B=8, T=1000, L=4, H=16, D=24):
     print(f"rq M={M}: mdg fused {fused:8.1f} us   out_proj {t1:7.1f} + qkv {t2:7.1f} = {t1 + t2:7.1f} us", flush=True)
 
 
+def run_final(M=32000, C=384, latent=21):
+    """The denoise step's FinalLayer + Euler (mdg_gemm EULER, N = 32: final_euler_kernel) vs
+    the generic 64x32 GEMM (an N = 64 descriptor)."""
+    xn = torch.randn(M, C, device="cuda").to(torch.bfloat16)
+    W = torch.zeros(64, C, device="cuda")
+    W[:latent] = torch.randn(latent, C, device="cuda") / C ** 0.5
+    W = W.to(torch.bfloat16)
+    b = torch.zeros(64, device="cuda")
+    xin, xo, vo = (torch.randn(M, latent, device="cuda") for _ in range(3))
+    s = torch.cuda.current_stream().cuda_stream
+    res = []
+    for n in (32, 64):
+        d = _lib.MdgGemmDesc()
+        d.dtype, d.a_mode, d.epi, d.M, d.N, d.K = 1, 0, 3, M, n, C
+        Wn, bn = W[:n].contiguous(), b[:n].contiguous()
+        d.A, d.lda, d.W, d.ldw, d.bias = xn.data_ptr(), C, Wn.data_ptr(), C, bn.data_ptr()
+        d.out, d.ldo, d.x_in, d.v_out, d.dt, d.n_valid = xo.data_ptr(), latent, xin.data_ptr(), vo.data_ptr(), 0.02, latent
+        res.append(tm(lambda: _lib.check(lib.mdg_gemm(ctypes.byref(d), s), "euler")))
+    mb = (M * C * 2 + 3 * M * latent * 4) / 1e6
+    print(f"final M={M}: final_euler {res[0]:7.1f} us ({mb / res[0]:6.2f} TB/s)   generic {res[1]:7.1f} us", flush=True)
+
+
 if __name__ == "__main__":
     import sys as _s
+    if len(_s.argv) > 1 and _s.argv[1] == "final":
+        run_final()
+        _s.exit(0)
     if len(_s.argv) > 1 and _s.argv[1] == "rq":
         run_rq()
         _s.exit(0)
