@@ -2083,14 +2083,18 @@ static int rowln_bm() {
 constexpr int kSpaThreads = 256;
 constexpr int kSpaBN = 144;                                   // 2 heads x q|k|v x 24
 constexpr int kSpaLdsSt = kSpaBN + 4;                         // fp32 epilogue row stride
-constexpr size_t kSpaSmem = (size_t)64 * kSpaLdsSt * 4;       // 37888 B (>= 2 x (128+144) x 32 x 2)
-static_assert(2 * (128 + kSpaBN) * 32 * 2 <= kSpaSmem, "ring fits the epilogue stage");
+constexpr size_t kSpaStage = (size_t)(128 + kSpaBN) * 32 * 2;  // one K-step's A + B image, 17408 B
+// ring of S K-steps (S - 1 in flight while one is read); the epilogue stage reuses it
+__host__ __device__ constexpr size_t spa_smem(int S) {
+  return (size_t)S * kSpaStage > (size_t)64 * kSpaLdsSt * 4 ? (size_t)S * kSpaStage : (size_t)64 * kSpaLdsSt * 4;
+}
 
 template <int I>
 __device__ __forceinline__ float quad_bc(float x) {
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), I | (I << 2) | (I << 4) | (I << 6), 0xF, 0xF, true));
 }
 
+template <int S>  // ring depth (K-steps)
 __global__ __launch_bounds__(kSpaThreads) void gemm_qkv_attn_spatial_kernel(const mdg_gemm_desc p) {
   constexpr int D = 24, HP = 2, BM = 128, BN = kSpaBN, BK = 32, NF = BN / 16, HD = HP * D;
   constexpr int ATILE = BM * BK, STAGE = (BM + BN) * BK, LDS_ST = kSpaLdsSt;
@@ -2144,14 +2148,26 @@ __global__ __launch_bounds__(kSpaThreads) void gemm_qkv_attn_spatial_kernel(cons
 #pragma unroll
     for (int j = 0; j < NF; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  MDG_SPA_LOAD(0, 0);
   const int nk = K / BK;
+#pragma unroll
+  for (int s0 = 0; s0 < S - 1; ++s0)
+    if (s0 < nk) MDG_SPA_LOAD(s0, s0 * BK);
   const int ch = (lg ^ swz_of(lr)) * 8;  // fragment rows are lr mod 16
   for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int cur = kt % S;
+    // step kt landed: leave the younger steps' pieces (4 per step, 5 on wave 0) in flight
+    const int younger = min(S - 2, nk - 1 - kt);
+    if (S > 2 && younger >= 2) {
+      if (wave == 0) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    } else if (S > 2 && younger == 1) {
+      if (wave == 0) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     __syncthreads();
-    if (kt + 1 < nk) MDG_SPA_LOAD(cur ^ 1, (kt + 1) * BK);
+    if (kt + S - 1 < nk) MDG_SPA_LOAD((kt + S - 1) % S, (kt + S - 1) * BK);
     const bf16_t* As = lds + cur * STAGE;
     const bf16_t* Bs = As + ATILE;
     bf16x8 a[2], b[NF];
@@ -2247,9 +2263,34 @@ __global__ __launch_bounds__(kSpaThreads) void gemm_qkv_attn_spatial_kernel(cons
   }
 }
 
+// ring depth: MDG_SPA_STAGES (2, 3 or 4; A/B knob).  Measured standalone at M = 32000: 52.7 /
+// 53.5 / 59.5 us: more co-resident blocks (4 per CU at 2 stages) beat a deeper ring
+static int spa_stages() {
+  static const int st = [] {
+    const char* e = getenv("MDG_SPA_STAGES");
+    const int v = e ? atoi(e) : 2;
+    return (v == 3 || v == 4) ? v : 2;
+  }();
+  return st;
+}
+
 static hipError_t launch_spatial(const mdg_gemm_desc& p, hipStream_t s) {
   const int nwg = (p.H / 2) * ((p.M + 127) / 128);
-  hipLaunchKernelGGL(gemm_qkv_attn_spatial_kernel, dim3(nwg), dim3(kSpaThreads), kSpaSmem, s, p);
+  switch (spa_stages()) {
+    case 2: hipLaunchKernelGGL((gemm_qkv_attn_spatial_kernel<2>), dim3(nwg), dim3(kSpaThreads), spa_smem(2), s, p); break;
+    case 4: {
+      static bool attr_set = false;
+      if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_qkv_attn_spatial_kernel<4>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)spa_smem(4));
+        if (e != hipSuccess) return e;
+        attr_set = true;
+      }
+      hipLaunchKernelGGL((gemm_qkv_attn_spatial_kernel<4>), dim3(nwg), dim3(kSpaThreads), spa_smem(4), s, p);
+      break;
+    }
+    default: hipLaunchKernelGGL((gemm_qkv_attn_spatial_kernel<3>), dim3(nwg), dim3(kSpaThreads), spa_smem(3), s, p); break;
+  }
   return hipGetLastError();
 }
 
@@ -2339,7 +2380,7 @@ GemmPlan gemm_plan(const mdg_gemm_desc& p) {
   int cfg = -1;
   if (p.epi == MDG_EPI_ATTN_SPATIAL) {  // validated by mdg_gemm: bf16 PLAIN, L 4, D 24, H even
     g.cfg = kCfgSpa;
-    g.smem = kSpaSmem;
+    g.smem = spa_smem(spa_stages());
     g.bm = 128;
     g.bn = kSpaBN;
     return g;

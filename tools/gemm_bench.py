@@ -110,6 +110,29 @@ def run_rq(B=8, T=1000, L=4, H=16, D=24):
     print(f"rq M={M}: mdg fused {fused:8.1f} us   out_proj {t1:7.1f} + qkv {t2:7.1f} = {t1 + t2:7.1f} us", flush=True)
 
 
+def run_spa(B=8, T=1000, L=4, H=16, D=24):
+    """The fused spatial q|k|v projection + 4-residue attention (MDG_EPI_ATTN_SPATIAL) on one
+    lane's shape."""
+    C, M = H * D, B * T * L
+    xn = (torch.randn(M, C, device="cuda") * 0.5).to(torch.bfloat16)
+    W = (torch.randn(3 * C, C, device="cuda") / C ** 0.5).to(torch.bfloat16)
+    bq = torch.randn(3 * C, device="cuda")
+    kvb = torch.zeros(H, 2, 32, device="cuda")
+    kvb[:, :, :D] = torch.randn(H, 2, D, device="cuda")
+    rope = torch.randn(2 * L * (D // 2), device="cuda")
+    o = torch.empty(M, C, device="cuda", dtype=torch.bfloat16)
+    d = _lib.MdgGemmDesc()
+    d.dtype, d.a_mode, d.epi, d.M, d.N, d.K = 1, 0, 4, M, 3 * C, C
+    d.A, d.lda, d.W, d.ldw, d.bias = xn.data_ptr(), C, W.data_ptr(), C, bq.data_ptr()
+    d.H, d.D, d.T, d.L, d.qscale, d.rope, d.rope_rows = H, D, T, L, D ** -0.5, rope.data_ptr(), L
+    d.out, d.ldo, d.kvb = o.data_ptr(), C, kvb.data_ptr()
+    s = torch.cuda.current_stream().cuda_stream
+    us = tm(lambda: _lib.check(lib.mdg_gemm(ctypes.byref(d), s), "spa"))
+    fl = 2.0 * M * 3 * C * C
+    print(f"spa M={M}: {us:7.1f} us ({fl / us / 1e6:6.1f} TF/s)  MDG_SPA_STAGES={os.environ.get('MDG_SPA_STAGES', '3')}",
+          flush=True)
+
+
 def run_final(M=32000, C=384, latent=21):
     """The denoise step's FinalLayer + Euler (mdg_gemm EULER, N = 32: final_euler_kernel) vs
     the generic 64x32 GEMM (an N = 64 descriptor)."""
@@ -134,6 +157,9 @@ def run_final(M=32000, C=384, latent=21):
 
 if __name__ == "__main__":
     import sys as _s
+    if len(_s.argv) > 1 and _s.argv[1] == "spa":
+        run_spa()
+        _s.exit(0)
     if len(_s.argv) > 1 and _s.argv[1] == "final":
         run_final()
         _s.exit(0)
