@@ -2094,6 +2094,38 @@ __device__ __forceinline__ float quad_bc(float x) {
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), I | (I << 2) | (I << 4) | (I << 6), 0xF, 0xF, true));
 }
 
+// Quad-broadcast FMAs with the DPP riding on the FMA (v_fmac_f32_dpp, src0 read from quad lane j):
+// half the VALU of the v_mov_b32_dpp + v_fmac pair the compiler emits for quad_bc(x) * y (it
+// does not fold the broadcast).  A DPP source written by a VALU needs two wait states, which
+// the hazard recognizer does not provide across inline asm: each block starts with s_nop 1.
+// s_j += sum_{c < 6} q[c] * k_j[c]   (k_j = quad lane j's k), c ascending per key
+__device__ __forceinline__ void quad_dots6(const float* q, const float* k, float& s0, float& s1, float& s2, float& s3) {
+  asm volatile("s_nop 1\n\t"
+               "v_fmac_f32_dpp %0, %10, %4 quad_perm:[0,0,0,0] row_mask:0xf bank_mask:0xf\n\t" "v_fmac_f32_dpp %1, %10, %4 quad_perm:[1,1,1,1] row_mask:0xf bank_mask:0xf\n\t" "v_fmac_f32_dpp %2, %10, %4 quad_perm:[2,2,2,2] row_mask:0xf bank_mask:0xf\n\t" "v_fmac_f32_dpp %3, %10, %4 quad_perm:[3,3,3,3] row_mask:0xf bank_mask:0xf\n\t"
+               "v_fmac_f32_dpp %0, %11, %5 quad_perm:[0,0,0,0] row_mask:0xf bank_mask:0xf\n\t" "v_fmac_f32_dpp %1, %11, %5 quad_perm:[1,1,1,1] row_mask:0xf bank_mask:0xf\n\t" "v_fmac_f32_dpp %2, %11, %5 quad_perm:[2,2,2,2] row_mask:0xf bank_mask:0xf\n\t" "v_fmac_f32_dpp %3, %11, %5 quad_perm:[3,3,3,3] row_mask:0xf bank_mask:0xf\n\t"
+               "v_fmac_f32_dpp %0, %12, %6 quad_perm:[0,0,0,0] row_mask:0xf bank_mask:0xf\n\t" "v_fmac_f32_dpp %1, %12, %6 quad_perm:[1,1,1,1] row_mask:0xf bank_mask:0xf\n\t" "v_fmac_f32_dpp %2, %12, %6 quad_perm:[2,2,2,2] row_mask:0xf bank_mask:0xf\n\t" "v_fmac_f32_dpp %3, %12, %6 quad_perm:[3,3,3,3] row_mask:0xf bank_mask:0xf\n\t"
+               "v_fmac_f32_dpp %0, %13, %7 quad_perm:[0,0,0,0] row_mask:0xf bank_mask:0xf\n\t" "v_fmac_f32_dpp %1, %13, %7 quad_perm:[1,1,1,1] row_mask:0xf bank_mask:0xf\n\t" "v_fmac_f32_dpp %2, %13, %7 quad_perm:[2,2,2,2] row_mask:0xf bank_mask:0xf\n\t" "v_fmac_f32_dpp %3, %13, %7 quad_perm:[3,3,3,3] row_mask:0xf bank_mask:0xf\n\t"
+               "v_fmac_f32_dpp %0, %14, %8 quad_perm:[0,0,0,0] row_mask:0xf bank_mask:0xf\n\t" "v_fmac_f32_dpp %1, %14, %8 quad_perm:[1,1,1,1] row_mask:0xf bank_mask:0xf\n\t" "v_fmac_f32_dpp %2, %14, %8 quad_perm:[2,2,2,2] row_mask:0xf bank_mask:0xf\n\t" "v_fmac_f32_dpp %3, %14, %8 quad_perm:[3,3,3,3] row_mask:0xf bank_mask:0xf\n\t"
+               "v_fmac_f32_dpp %0, %15, %9 quad_perm:[0,0,0,0] row_mask:0xf bank_mask:0xf\n\t" "v_fmac_f32_dpp %1, %15, %9 quad_perm:[1,1,1,1] row_mask:0xf bank_mask:0xf\n\t" "v_fmac_f32_dpp %2, %15, %9 quad_perm:[2,2,2,2] row_mask:0xf bank_mask:0xf\n\t" "v_fmac_f32_dpp %3, %15, %9 quad_perm:[3,3,3,3] row_mask:0xf bank_mask:0xf\n\t"
+               : "+v"(s0), "+v"(s1), "+v"(s2), "+v"(s3)
+               : "v"(q[0]), "v"(q[1]), "v"(q[2]), "v"(q[3]), "v"(q[4]), "v"(q[5]),
+                 "v"(k[0]), "v"(k[1]), "v"(k[2]), "v"(k[3]), "v"(k[4]), "v"(k[5]));
+}
+// o[c] += sum_j p_j * v_j[c] for c < 6, keys j ascending
+__device__ __forceinline__ void quad_pv6(float* o, const float* v, float p0, float p1, float p2, float p3) {
+  asm volatile("s_nop 1\n\t"
+               "v_fmac_f32_dpp %0, %10, %6 quad_perm:[0,0,0,0] row_mask:0xf bank_mask:0xf\n\t" "v_fmac_f32_dpp %0, %10, %7 quad_perm:[1,1,1,1] row_mask:0xf bank_mask:0xf\n\t" "v_fmac_f32_dpp %0, %10, %8 quad_perm:[2,2,2,2] row_mask:0xf bank_mask:0xf\n\t" "v_fmac_f32_dpp %0, %10, %9 quad_perm:[3,3,3,3] row_mask:0xf bank_mask:0xf\n\t"
+               "v_fmac_f32_dpp %1, %11, %6 quad_perm:[0,0,0,0] row_mask:0xf bank_mask:0xf\n\t" "v_fmac_f32_dpp %1, %11, %7 quad_perm:[1,1,1,1] row_mask:0xf bank_mask:0xf\n\t" "v_fmac_f32_dpp %1, %11, %8 quad_perm:[2,2,2,2] row_mask:0xf bank_mask:0xf\n\t" "v_fmac_f32_dpp %1, %11, %9 quad_perm:[3,3,3,3] row_mask:0xf bank_mask:0xf\n\t"
+               "v_fmac_f32_dpp %2, %12, %6 quad_perm:[0,0,0,0] row_mask:0xf bank_mask:0xf\n\t" "v_fmac_f32_dpp %2, %12, %7 quad_perm:[1,1,1,1] row_mask:0xf bank_mask:0xf\n\t" "v_fmac_f32_dpp %2, %12, %8 quad_perm:[2,2,2,2] row_mask:0xf bank_mask:0xf\n\t" "v_fmac_f32_dpp %2, %12, %9 quad_perm:[3,3,3,3] row_mask:0xf bank_mask:0xf\n\t"
+               "v_fmac_f32_dpp %3, %13, %6 quad_perm:[0,0,0,0] row_mask:0xf bank_mask:0xf\n\t" "v_fmac_f32_dpp %3, %13, %7 quad_perm:[1,1,1,1] row_mask:0xf bank_mask:0xf\n\t" "v_fmac_f32_dpp %3, %13, %8 quad_perm:[2,2,2,2] row_mask:0xf bank_mask:0xf\n\t" "v_fmac_f32_dpp %3, %13, %9 quad_perm:[3,3,3,3] row_mask:0xf bank_mask:0xf\n\t"
+               "v_fmac_f32_dpp %4, %14, %6 quad_perm:[0,0,0,0] row_mask:0xf bank_mask:0xf\n\t" "v_fmac_f32_dpp %4, %14, %7 quad_perm:[1,1,1,1] row_mask:0xf bank_mask:0xf\n\t" "v_fmac_f32_dpp %4, %14, %8 quad_perm:[2,2,2,2] row_mask:0xf bank_mask:0xf\n\t" "v_fmac_f32_dpp %4, %14, %9 quad_perm:[3,3,3,3] row_mask:0xf bank_mask:0xf\n\t"
+               "v_fmac_f32_dpp %5, %15, %6 quad_perm:[0,0,0,0] row_mask:0xf bank_mask:0xf\n\t" "v_fmac_f32_dpp %5, %15, %7 quad_perm:[1,1,1,1] row_mask:0xf bank_mask:0xf\n\t" "v_fmac_f32_dpp %5, %15, %8 quad_perm:[2,2,2,2] row_mask:0xf bank_mask:0xf\n\t" "v_fmac_f32_dpp %5, %15, %9 quad_perm:[3,3,3,3] row_mask:0xf bank_mask:0xf\n\t"
+               : "+v"(o[0]), "+v"(o[1]), "+v"(o[2]), "+v"(o[3]), "+v"(o[4]), "+v"(o[5])
+               : "v"(p0), "v"(p1), "v"(p2), "v"(p3), "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]),
+                 "v"(v[5]));
+}
+
+
 template <int S>  // ring depth (K-steps)
 __global__ __launch_bounds__(kSpaThreads) void gemm_qkv_attn_spatial_kernel(const mdg_gemm_desc p) {
   constexpr int D = 24, HP = 2, BM = 128, BN = kSpaBN, BK = 32, NF = BN / 16, HD = HP * D;
@@ -2230,13 +2262,9 @@ __global__ __launch_bounds__(kSpaThreads) void gemm_qkv_attn_spatial_kernel(cons
     const float kvalid = (!p.key_mask || p.key_mask[min(m, M - 1)] != 0.f) ? 1.f : 0.f;
     float sb = 0.f, s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
 #pragma unroll
-    for (int c = 0; c < 12; ++c) {
-      sb += q[c] * kbh[c0 + c];
-      s0 += q[c] * quad_bc<0>(k[c]);
-      s1 += q[c] * quad_bc<1>(k[c]);
-      s2 += q[c] * quad_bc<2>(k[c]);
-      s3 += q[c] * quad_bc<3>(k[c]);
-    }
+    for (int c = 0; c < 12; ++c) sb += q[c] * kbh[c0 + c];
+    quad_dots6(q, k, s0, s1, s2, s3);
+    quad_dots6(q + 6, k + 6, s0, s1, s2, s3);
     sb += __shfl_xor(sb, 4, 64); s0 += __shfl_xor(s0, 4, 64); s1 += __shfl_xor(s1, 4, 64);
     s2 += __shfl_xor(s2, 4, 64); s3 += __shfl_xor(s3, 4, 64);
     const float v0 = quad_bc<0>(kvalid), v1 = quad_bc<1>(kvalid), v2 = quad_bc<2>(kvalid), v3 = quad_bc<3>(kvalid);
@@ -2251,9 +2279,11 @@ __global__ __launch_bounds__(kSpaThreads) void gemm_qkv_attn_spatial_kernel(cons
     const float inv = 1.0f / (pb + p0 + p1 + p2 + p3);
     float o[12];
 #pragma unroll
-    for (int c = 0; c < 12; ++c)
-      o[c] = (pb * kbh[MDG_DP + c0 + c] + p0 * quad_bc<0>(v[c]) + p1 * quad_bc<1>(v[c]) + p2 * quad_bc<2>(v[c]) +
-              p3 * quad_bc<3>(v[c])) * inv;
+    for (int c = 0; c < 12; ++c) o[c] = pb * kbh[MDG_DP + c0 + c];
+    quad_pv6(o, v, p0, p1, p2, p3);
+    quad_pv6(o + 6, v + 6, p0, p1, p2, p3);
+#pragma unroll
+    for (int c = 0; c < 12; ++c) o[c] *= inv;
     if (m < M) {
       bf16_t* op = reinterpret_cast<bf16_t*>(p.out) + (size_t)m * p.ldo + gh * D + c0;
 #pragma unroll
