@@ -629,7 +629,7 @@ int mdg_describe_plan(const mdg_dims* d, char* buf, size_t n) {
   snprintf(buf, n,
            "{\"dtype\": \"%s\", \"spatial\": \"%s\", \"ln_handoff\": \"%s\", "
            "\"temporal\": \"%s+%s\", \"planes\": \"%s\", \"mlp\": \"%s\", "
-           "\"final\": \"euler_epilogue_gemm\"}",
+           "\"final\": \"%s\"}",
            d->dtype == MDG_BF16 ? "bf16" : "f32", spatial,
            fuse ? "fused into gated-residual row-LN GEMM epilogues" : "stand-alone ln_mod pass",
            (fuse && fused_qkv_on() && C == 384 && packed_planes(*d) && d->D <= 48 && d->T * d->L >= 128)
@@ -642,7 +642,10 @@ int mdg_describe_plan(const mdg_dims* d, char* buf, size_t n) {
            (fuse && fused_mlp_on() && d->dtype == MDG_BF16 && d->C == 384 && d->T * d->L >= 128)
                ? "mlp_fused(fc1+gelu+fc2+gated residual+LN in one kernel, hidden on chip)"
            : fuse ? "fc1_gemm(gelu)+fc2_rowln_gemm"
-                  : "fc1_gemm(gelu)+fc2_gate_res_gemm");
+                  : "fc1_gemm(gelu)+fc2_gate_res_gemm",
+           (d->dtype == MDG_BF16 && fast_final_on() && d->latent <= 32 && (C == 128 || C == 256 || C == 384 || C == 512))
+               ? "final_euler_kernel(one pass, W in LDS)"
+               : "euler_epilogue_gemm");
   return MDG_OK;
 }
 
