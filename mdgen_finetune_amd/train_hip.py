@@ -17,8 +17,9 @@ backward  per sublayer, top down:
                                 step); fc1's with the GELU-derivative epilogue (MDG_ACT_DGELU);
             mdg_attn_*_bwd      flash-style attention backward (P recomputed from the saved lse),
                                 RoPE / q-scale undone in the epilogue, bias_k / bias_v partials;
-            torch.mm            the weight gradients dW = dY^T X (plain GEMMs, hipBLASLt) —
-                                the only library calls on the path.
+            torch.bmm           the weight gradients dW = dY^T X (plain GEMMs, hipBLASLt, split
+                                over token chunks + a sum of fp32 partials) — the only
+                                library calls on the path.
 The adaLN modulation vectors enter as a [B, 9C] input of the Function, so the t-embedding /
 adaLN linears upstream stay ordinary autograd modules (x-independent, tiny).
 
@@ -47,6 +48,24 @@ def _mm_f32(a, b):
         return torch.mm(a, b, out_dtype=torch.float32)
     except (RuntimeError, TypeError):
         return (a @ b).float()
+
+
+def _dw(dy, x):
+    """dW = dy^T x (fp32 result) over the N token rows.  With bf16 operands the reduction is
+    split into S token chunks (one batched GEMM, then a sum of the S fp32 partials): the output
+    is only [Nout][Kin] (e.g. 1536 x 384 = 48 tiles), so one GEMM over all N = 32 000 rows ran
+    on a fifth of the CUs (hipBLASLt picks no split-K here; 209 us for fc1's 37.7 GF)."""
+    n = dy.shape[0]
+    if dy.dtype != torch.float32:
+        for S in (16, 8, 4, 2):
+            if n % S == 0 and n // S >= 1024:
+                a = dy.view(S, n // S, dy.shape[1]).transpose(1, 2)
+                b = x.view(S, n // S, x.shape[1])
+                try:
+                    return torch.bmm(a, b, out_dtype=torch.float32).sum(0)
+                except (RuntimeError, TypeError, NotImplementedError):
+                    break
+    return _mm_f32(dy.t(), x)
 
 
 class LayerHelper:
@@ -260,11 +279,11 @@ class _HipLayerFn(torch.autograd.Function):
         # ---- MLP: h3 = h2 + g_m * (fc2(gelu(fc1(xn3))))
         dy_m = e(N, C)
         part_m = lngate(None, None, None, 0, 0, dh3, dh3, sv["y"][2], 8 * C, dy_m)
-        grads["w2"] = _mm_f32(dy_m.t(), sv["act"])
+        grads["w2"] = _dw(dy_m, sv["act"])
         grads["b2"] = part_m[:, :, 3].sum((0, 1))
         du = dx_gemm(dy_m, P["w2"].t().contiguous(), C, F, _lib.MDG_ACT_DGELU, sv["u"])
-        grads["w1"] = _mm_f32(du.t(), sv["xn"][2])
-        grads["b1"] = du.float().sum(0)
+        grads["w1"] = _dw(du, sv["xn"][2])
+        grads["b1"] = du.sum(0, dtype=torch.float32)
         dxn3 = dx_gemm(du, P["w1"].t().contiguous(), F, C)
         dh2 = e(N, C, dtp=torch.float32)
         dy_t = e(N, C)
@@ -272,7 +291,7 @@ class _HipLayerFn(torch.autograd.Function):
 
         def attention(i, dy, o, xn, qkv, lse):
             """out_proj + attention backward of attention i (0 spatial, 1 temporal); returns dxn."""
-            grads[f"wo{i}"] = _mm_f32(dy.t(), o)
+            grads[f"wo{i}"] = _dw(dy, o)
             do = dx_gemm(dy, P[f"wo{i}"].t().contiguous(), C, C)
             dqkv = e(N, 3 * C)
             if i == 1 or L >= 16:
@@ -296,8 +315,8 @@ class _HipLayerFn(torch.autograd.Function):
                                                     dqkv.data_ptr(), bpart.data_ptr(), qscale, s),
                            "mdg_attn_spatial_bwd")
             grads[f"kvb{i}"] = bpart.sum(1)
-            grads[f"wqkv{i}"] = _mm_f32(dqkv.t(), xn)
-            grads[f"bqkv{i}"] = dqkv.float().sum(0)
+            grads[f"wqkv{i}"] = _dw(dqkv, xn)
+            grads[f"bqkv{i}"] = dqkv.sum(0, dtype=torch.float32)
             return dx_gemm(dqkv, P[f"wqkv{i}"].t().contiguous(), 3 * C, C)
 
         dxn2 = attention(1, dy_t, sv["o"][1], sv["xn"][1], sv["qkv_t"], sv["lse_t"])
