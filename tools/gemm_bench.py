@@ -129,7 +129,7 @@ def run_spa(B=8, T=1000, L=4, H=16, D=24):
     s = torch.cuda.current_stream().cuda_stream
     us = tm(lambda: _lib.check(lib.mdg_gemm(ctypes.byref(d), s), "spa"))
     fl = 2.0 * M * 3 * C * C
-    print(f"spa M={M}: {us:7.1f} us ({fl / us / 1e6:6.1f} TF/s)  MDG_SPA_STAGES={os.environ.get('MDG_SPA_STAGES', '3')}",
+    print(f"spa M={M}: {us:7.1f} us ({fl / us / 1e6:6.1f} TF/s)  MDG_SPA_STAGES={os.environ.get('MDG_SPA_STAGES', '2')}",
           flush=True)
 
 

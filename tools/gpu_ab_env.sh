@@ -17,7 +17,7 @@ for rep in 1 2; do
     if [ $L = old ]; then ENVSET="env $AB_ENV"; else ENVSET="env"; fi
     if [ -n "${AB_MODE:-}" ]; then
       $ENVSET timeout -k 10 100 python tools/gemm_bench.py $AB_MODE > gpurun_out/gemm_ab.log 2>&1 || exit $?
-      grep mdg gpurun_out/gemm_ab.log | cut -c1-75
+      grep -E "mdg|spa M|final M" gpurun_out/gemm_ab.log | cut -c1-90
     fi
     $ENVSET timeout -k 10 300 python -u bench.py --steps 4 --warmup 1 --no-cpu-baseline --sweep-batches "" --no-f32-line \
       > gpurun_out/bench_ab.log 2>&1 || exit $?
