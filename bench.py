@@ -61,10 +61,13 @@ def parse():
                     help="extra per-GPU batch sizes timed beside the headline (comma list, '' = none)")
     ap.add_argument("--no-f32-line", action="store_true", help="skip the fp32-operand (parity path) line")
     ap.add_argument("--sweep-steps", type=int, default=2, help="timed windows per sweep / f32 line")
+    ap.add_argument("--tps", action="store_true",
+                    help="TPS / interpolation model (BASELINE config 4: --tps_condition, latent 28, start + end "
+                         "frames conditioned; use with --frames 100); an evidence line, not the headline")
     return ap.parse_args()
 
 
-def make_model(T, L, seed=0):
+def make_model(T, L, seed=0, tps=False):
     import argparse as ap_
 
     from mdgen_finetune_amd import synthetic
@@ -72,20 +75,22 @@ def make_model(T, L, seed=0):
 
     args = ap_.Namespace(embed_dim=384, mha_heads=16, num_layers=5, ipa_heads=4, ipa_head_dim=32, ipa_qk=8,
                          ipa_v=8, dropout=0.0, no_rope=False, prepend_ipa=True, abs_pos_emb=True, crop=L,
-                         num_frames=T, time_multiplier=100.0, sim_condition=True, tps_condition=False)
-    m = LatentMDGenModel(args, 21).eval()
+                         num_frames=T, time_multiplier=100.0, sim_condition=not tps, tps_condition=tps)
+    m = LatentMDGenModel(args, 28 if tps else 21).eval()
     synthetic.fill_module_(m, seed)
     return m
 
 
-def inputs(B, T, L, seed, device):
+def inputs(B, T, L, seed, device, tps=False):
     from mdgen_finetune_amd import synthetic
     from mdgen_finetune_amd.rigid_utils import Rigid, Rotation
 
-    inp = synthetic.make_inputs(seed, B, T, L, 21)
+    inp = synthetic.make_inputs(seed, B, T, L, 28 if tps else 21, tps=tps)
     g = lambda k: torch.from_numpy(inp[k]).to(device)  # noqa: E731
     kw = dict(mask=g("mask"), start_frames=Rigid(Rotation(rot_mats=g("rots")), g("trans")), x_cond=g("x_cond"),
               x_cond_mask=g("x_cond_mask"), aatype=g("aatype"))
+    if tps:
+        kw["end_frames"] = Rigid(Rotation(rot_mats=g("end_rots")), g("end_trans"))
     return g("x"), kw, inp
 
 
@@ -410,11 +415,11 @@ def main():
     from mdgen_finetune_amd.engine import get_engine
 
     B, T, L = a.batch, a.frames, a.crop
-    m = make_model(T, L).to(dev)
+    m = make_model(T, L, tps=a.tps).to(dev)
     m.hip_dtype = a.dtype
     eng = get_engine(m)
     eng.lanes = a.lanes
-    zs, kw, _ = inputs(B, T, L, seed=100 + rank, device=dev)
+    zs, kw, _ = inputs(B, T, L, seed=100 + rank, device=dev, tps=a.tps)
 
     def window():
         return eng.sample_euler(zs, num_steps=a.num_steps, use_graph=not a.no_graph, **kw)
@@ -444,13 +449,13 @@ def main():
         nl = a.lanes if (a.lanes > 1 and B % a.lanes == 0) else 1
         Bl = B // nl
         st = eng._state(Bl, T, L, lane=1 if nl > 1 else 0)
-        roofs = roofline(eng, st, a.dtype, Bl, T, L) if rank == 0 else None
+        roofs = roofline(eng, st, a.dtype, Bl, T, L) if rank == 0 and not a.tps else None
         plan = eng.describe_plan(Bl, T, L)
 
     # extra lines (rank 0, single process): the B sweep SURVEY §8(d) asks for and the fp32
     # parity-path throughput, each with its own step-level roofline
     sweep = []
-    if rank == 0 and world == 1:
+    if rank == 0 and world == 1 and not a.tps:
         for Bs in [int(b) for b in a.sweep_batches.split(",") if b.strip()]:
             if Bs != B:
                 sweep.append(sweep_line(dev, T, L, Bs, a.dtype, a.lanes, a.num_steps, a.sweep_steps, 300 + Bs))
@@ -459,7 +464,7 @@ def main():
 
     out = None
     if rank == 0:
-        cpu = None if (a.no_cpu_baseline or world > 1) else cpu_baseline(T, L, a.cpu_seconds)
+        cpu = None if (a.no_cpu_baseline or world > 1 or a.tps) else cpu_baseline(T, L, a.cpu_seconds)
         out = {
             "metric": "denoised frames/sec, 1000-frame x crop4 forward-sim step, 1/2/4/8 MI355X",
             "value": round(value, 1),
@@ -488,6 +493,11 @@ def main():
             "roofline_more": list(roofs.values())[1:] if roofs else None,
             "cpu_baseline": cpu,
         }
+        if a.tps:  # BASELINE config 4 evidence line (tps_inference.py path), not the headline metric
+            out["config"]["workload"] = (f"tps_inference window: Euler ODE {n_euler} denoising steps x B={B} "
+                                         f"interpolations x T={T} frames x L={L} residues, start + end frames "
+                                         "conditioned (+ per-window dual-IPA conditioning), per GPU")
+            out["config"]["model"] = "LatentMDGenModel --tps_condition (latent 28, 5 layers, C=384, 16 heads, IPA prepend)"
         if share:  # rehearsal: every rank on cuda:0 — not a multi-GPU measurement
             out["shared_gpu"] = True
             out["ranks_sharing_gpu"] = world
