@@ -19,7 +19,8 @@ struct GemmPlan {
 GemmPlan gemm_plan(const mdg_gemm_desc& p);
 hipError_t gemm_launch(const mdg_gemm_desc& p, const GemmPlan& g, hipStream_t s);
 bool mlp_fused_supported(const mdg_gemm_desc& f1, const mdg_gemm_desc& f2);
-hipError_t mlp_fused_launch(const mdg_gemm_desc& f1, const mdg_gemm_desc& f2, hipStream_t s);
+hipError_t mlp_fused_launch(const mdg_gemm_desc& f1, const mdg_gemm_desc& f2, hipStream_t s, float* part);
+int mlp_split_factor(int M, int F);
 bool final_euler_supported(const mdg_gemm_desc& p);
 hipError_t final_euler_launch(const mdg_gemm_desc& p, hipStream_t s);
 bool rowln_qkv_supported(const mdg_gemm_desc& r, const mdg_gemm_desc& q);
@@ -157,7 +158,7 @@ bool fast_final_on() {
 }
 
 struct WsLayout {
-  size_t qkv_s, qkv_t, o, hid, xn, kbias, kbias_s, total;
+  size_t qkv_s, qkv_t, o, hid, xn, kbias, kbias_s, mlp_part, total;
 };
 
 WsLayout ws_layout(const mdg_dims& d) {
@@ -172,6 +173,9 @@ WsLayout ws_layout(const mdg_dims& d) {
   w.xn = off;    off += align256(N * d.C * cs);
   w.kbias = off; off += align256((size_t)d.B * d.L * d.T * sizeof(float));
   w.kbias_s = off; off += align256(N * sizeof(float));
+  // the small-M fused MLP's fc2 partials ([split][N][C] fp32; bf16 C = 384 only, else empty)
+  const int split = (d.dtype == MDG_BF16 && d.C == 384 && d.F % 128 == 0) ? mdg::mlp_split_factor((int)N, d.F) : 1;
+  w.mlp_part = off; off += split > 1 ? align256((size_t)split * N * d.C * sizeof(float)) : 0;
   w.total = off;
   return w;
 }
@@ -517,7 +521,8 @@ static int layer_fwd_impl(const mdg_dims* d, const mdg_layer_weights* w, const f
     f2.xn_shift_off = ho.next_shift; f2.xn_scale_off = ho.next_scale; f2.ln_eps = 1e-6f;
   }
   if (fuse && fused_mlp_on() && mdg::mlp_fused_supported(f1, f2))
-    return hip_check(mdg::mlp_fused_launch(f1, f2, (hipStream_t)stream), "mlp fused launch");
+    return hip_check(mdg::mlp_fused_launch(f1, f2, (hipStream_t)stream, (float*)(wsb + lay.mlp_part)),
+                     "mlp fused launch");
   if (int e = mdg_gemm(&f1, stream)) return e;
   return mdg_gemm(&f2, stream);
 }
@@ -528,7 +533,7 @@ int mdg_mlp_fused(const mdg_gemm_desc* f1, const mdg_gemm_desc* f2, void* stream
   if (!mdg::mlp_fused_supported(*f1, *f2))
     return fail(MDG_E_SHAPE, "mlp_fused: outside the envelope (bf16, K=N=384, F %% 128, rows_per_mod >= 128) "
                 "M=%d C=%d F=%d", f1->M, f1->K, f1->N);
-  return hip_check(mdg::mlp_fused_launch(*f1, *f2, (hipStream_t)stream), "mlp fused launch");
+  return hip_check(mdg::mlp_fused_launch(*f1, *f2, (hipStream_t)stream, nullptr), "mlp fused launch");
 }
 
 int mdg_rowln_qkv(const mdg_gemm_desc* r, const mdg_gemm_desc* q, void* stream) {

@@ -1413,6 +1413,8 @@ static hipError_t launch_rowln(const mdg_gemm_desc& p, hipStream_t s) {
 // GEMMs' (ascending in 32s), so the result equals fc1 then fc2 bit for bit.
 struct MlpArgs {
   mdg_gemm_desc f1, f2;
+  float* part;  // split form: [nsplit][M][NCOL] fp32 fc2 partials (no epilogue in the kernel)
+  int nsplit;   // hidden chunks are divided over gridDim.y = nsplit blocks per row tile
 };
 // timing diagnostics only (tools/diag_mlp_attn.sh builds them into separate libraries): 1 = xn
 // staged for the first hidden chunk only, 2 = GELU replaced by the identity, 3 = nothing staged
@@ -1477,7 +1479,7 @@ __device__ __forceinline__ void vm_wait_upto6(int n) {
   }
 }
 
-template <int NCOL>
+template <int NCOL, bool SPLIT>  // SPLIT: chunks [y * cps, (y + 1) * cps) only, fp32 partials out
 __global__ __launch_bounds__(kMlpThreads, 1) void mlp_rowln_kernel(const MlpArgs args) {
   static_assert(NCOL == 384, "the ring slot holds 384 W2 rows");
   constexpr int BM = 128, BK = 32, HC = kMlpHC, STAGES = kMlpStages, SLOT = kMlpSlot;
@@ -1496,7 +1498,8 @@ __global__ __launch_bounds__(kMlpThreads, 1) void mlp_rowln_kernel(const MlpArgs
   const int wah = wave / 4, wat = wave % 4;  // fc1: 64 hidden x 32 tokens
   const int lr = lane & 15, lg = lane >> 4;
   const int M = p.M, F = p.K;
-  const int NS = (F / HC) * 10;  // 6 fc1 (K 64) + 4 fc2 (K 32) steps per hidden chunk
+  const int cps = SPLIT ? (F / HC) / args.nsplit : F / HC, j0 = SPLIT ? (int)blockIdx.y * cps : 0;
+  const int NS = cps * 10;  // 6 fc1 (K 64) + 4 fc2 (K 32) steps per hidden chunk
   const int nwg = (M + BM - 1) / BM;
   const int xcd = blockIdx.x & 7, loc = blockIdx.x >> 3, q8 = nwg >> 3, r8 = nwg & 7;
   const int m0 = ((xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc) * BM;
@@ -1524,7 +1527,7 @@ __global__ __launch_bounds__(kMlpThreads, 1) void mlp_rowln_kernel(const MlpArgs
   constexpr int IMG = 2 * BM * BK;  // one 32-wide image of the fc1 step (xn + W1c rows)
   auto issue = [&](int s) {
     bf16_t* sl = ring + (s % STAGES) * SLOT;
-    const int j = s / 10, t = s % 10;
+    const int j = j0 + s / 10, t = s % 10;  // hidden chunk, step within it
     if ((MDG_DIAG_MLP == 1 && xw && t < 6 && j > 0) || (MDG_DIAG_MLP == 3 && j > 0)) return;
     if (t < 6) {
       const bf16_t* base = abase + (size_t)t * 2 * BK + (xw ? (size_t)0 : (size_t)j * HC * q.ldw);
@@ -1587,7 +1590,7 @@ __global__ __launch_bounds__(kMlpThreads, 1) void mlp_rowln_kernel(const MlpArgs
     }
     // the chunk's fc1 is complete: + b1, GELU, bf16 -> Hs; restart acc1.  (Hs was last read by
     // chunk j - 1's fc2 steps, which every wave finished before this chunk's first barrier.)
-    const float* b1c = b1s + j * HC;
+    const float* b1c = b1s + (j0 + j) * HC;
     f32x4 b1v[4];
     {
       const float* bp = b1c + wah * 64 + lg * 4;
@@ -1622,10 +1625,89 @@ __global__ __launch_bounds__(kMlpThreads, 1) void mlp_rowln_kernel(const MlpArgs
         for (int jn = 0; jn < NT; ++jn) acc2[i][jn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[jn], acc2[i][jn], 0, 0, 0);
     }
   }
-  const float inv_rpm = 1.0f / (float)p.rows_per_mod;
-  float4 h4[2][NE];
-  rowln_load_band<NCOL>(p, m0, 0, h4);  // band 0's residual rows
-  rowln_fast_epilogue<NCOL>(p, acc2, h4, smem, m0, fdiv(m0, p.rows_per_mod, inv_rpm), inv_rpm);
+  if constexpr (SPLIT) {
+    // this block's fc2 partial sum: 16 consecutive columns (64 B) per 16-lane group and register
+    float* pp = args.part + (size_t)blockIdx.y * M * NCOL;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * 64 + i * 16 + lg * 4 + r;
+        if (m < M)
+#pragma unroll
+          for (int jn = 0; jn < NT; ++jn) pp[(size_t)m * NCOL + wn * WTN + jn * 16 + lr] = acc2[i][jn][r];
+      }
+  } else {
+    const float inv_rpm = 1.0f / (float)p.rows_per_mod;
+    float4 h4[2][NE];
+    rowln_load_band<NCOL>(p, m0, 0, h4);  // band 0's residual rows
+    rowln_fast_epilogue<NCOL>(p, acc2, h4, smem, m0, fdiv(m0, p.rows_per_mod, inv_rpm), inv_rpm);
+  }
+}
+
+// The split MLP's second pass: v = sum of the nsplit fc2 partials (split order), then exactly
+// the row-LN epilogue's arithmetic: h += gate * (v + b2), LayerNorm + adaLN modulate -> xn.
+// One wave per row, lane = columns 2 lane + 128 e.
+template <int NCOL>
+__global__ __launch_bounds__(256) void mlp_split_reduce_kernel(const mdg_gemm_desc p, const float* __restrict__ part,
+                                                               int nsplit) {
+#pragma clang fp contract(off)
+  constexpr int NE = NCOL / 128;
+  const int lane = threadIdx.x & 63, m = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int M = p.M;
+  if (m >= M) return;
+  const size_t b = (size_t)(m / p.rows_per_mod);
+  float2 v[NE];
+#pragma unroll
+  for (int e = 0; e < NE; ++e) v[e] = make_float2(0.f, 0.f);
+  for (int s = 0; s < nsplit; ++s)
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+      const float2 t = *reinterpret_cast<const float2*>(part + ((size_t)s * M + m) * NCOL + 2 * lane + 128 * e);
+      v[e].x += t.x;
+      v[e].y += t.y;
+    }
+  float2 h[NE];
+  float sum = 0.f;
+  float* hr = p.resid + (size_t)m * p.ldr;
+#pragma unroll
+  for (int e = 0; e < NE; ++e) {
+    const int k = 2 * lane + 128 * e;
+    const float2 hv = *reinterpret_cast<const float2*>(hr + k);
+    const float2 bb = p.bias ? *reinterpret_cast<const float2*>(p.bias + k) : make_float2(0.f, 0.f);
+    const float2 gg = p.gate ? *reinterpret_cast<const float2*>(p.gate + b * p.mod_stride + p.gate_off + k)
+                             : make_float2(1.f, 1.f);
+    h[e].x = hv.x + gg.x * (v[e].x + bb.x);
+    h[e].y = hv.y + gg.y * (v[e].y + bb.y);
+    sum += h[e].x + h[e].y;
+    *reinterpret_cast<float2*>(hr + k) = h[e];
+  }
+  if (!p.xn_out) return;
+  const float invN = 1.0f / (float)NCOL;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) sum += __shfl_xor(sum, o, 64);
+  const float mean = sum * invN;
+  float ss = 0.f;
+#pragma unroll
+  for (int e = 0; e < NE; ++e) {
+    const float a0 = h[e].x - mean, a1 = h[e].y - mean;
+    ss += a0 * a0 + a1 * a1;
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) ss += __shfl_xor(ss, o, 64);
+  const float rs = 1.0f / sqrtf(ss * invN + p.ln_eps);
+  const float* mr = p.xn_mods + b * p.xn_mod_stride;
+#pragma unroll
+  for (int e = 0; e < NE; ++e) {
+    const int k = 2 * lane + 128 * e;
+    const float2 xs = *reinterpret_cast<const float2*>(mr + p.xn_scale_off + k);
+    const float2 xh = *reinterpret_cast<const float2*>(mr + p.xn_shift_off + k);
+    typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+    bf16x2 pr;
+    pr[0] = (bf16_t)((h[e].x - mean) * rs * (1.0f + xs.x) + xh.x);
+    pr[1] = (bf16_t)((h[e].y - mean) * rs * (1.0f + xs.y) + xh.y);
+    *reinterpret_cast<bf16x2*>(reinterpret_cast<bf16_t*>(p.xn_out) + (size_t)m * NCOL + k) = pr;
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1743,18 +1825,46 @@ bool mlp_fused_supported(const mdg_gemm_desc& f1, const mdg_gemm_desc& f2) {
          f1.ldw % 8 == 0 && f2.ldw % 8 == 0 && f2.ldr % 4 == 0 && (!f2.xn_out || f2.xn_mods) && mlp_smem(f1.N) <= 160 * 1024;
 }
 
-hipError_t mlp_fused_launch(const mdg_gemm_desc& f1, const mdg_gemm_desc& f2, hipStream_t s) {
+// Hidden-chunk split for small M (fewer row tiles than the chip has CUs: each block would stream
+// all of W1 and W2 for one tile): the largest divisor of the chunk count that keeps the grid
+// within ~1.25 blocks per CU; 1 = no split.  MDG_MLP_SPLIT=0 disables it (A/B knob).
+int mlp_split_factor(int M, int F) {
+  static const bool on = [] {
+    const char* e = getenv("MDG_MLP_SPLIT");
+    return !(e && e[0] == '0');
+  }();
+  const int tiles = (M + 127) / 128, nch = F / kMlpHC;
+  if (!on || tiles >= 128 || nch < 2) return 1;
+  int best = 1;
+  for (int d = 2; d <= nch; ++d)
+    if (nch % d == 0 && tiles * d <= 320) best = d;
+  return best;
+}
+
+hipError_t mlp_fused_launch(const mdg_gemm_desc& f1, const mdg_gemm_desc& f2, hipStream_t s, float* part) {
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&mlp_rowln_kernel<384>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (e != hipSuccess) return e;
+    for (const void* k : {reinterpret_cast<const void*>(&mlp_rowln_kernel<384, false>),
+                          reinterpret_cast<const void*>(&mlp_rowln_kernel<384, true>)}) {
+      hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      if (e != hipSuccess) return e;
+    }
     attr_set = true;
   }
   MlpArgs a;
   a.f1 = f1;
   a.f2 = f2;
-  hipLaunchKernelGGL((mlp_rowln_kernel<384>), dim3((f1.M + 127) / 128), dim3(kMlpThreads), mlp_smem(f1.N), s, a);
+  a.part = part;
+  a.nsplit = part ? mlp_split_factor(f1.M, f1.N) : 1;
+  const int tiles = (f1.M + 127) / 128;
+  if (a.nsplit > 1) {
+    hipLaunchKernelGGL((mlp_rowln_kernel<384, true>), dim3(tiles, a.nsplit), dim3(kMlpThreads), mlp_smem(f1.N), s, a);
+    if (hipError_t e = hipGetLastError()) return e;
+    hipLaunchKernelGGL((mlp_split_reduce_kernel<384>), dim3((f1.M + 3) / 4), dim3(256), 0, s, f2, (const float*)part,
+                       a.nsplit);
+    return hipGetLastError();
+  }
+  hipLaunchKernelGGL((mlp_rowln_kernel<384, false>), dim3(tiles), dim3(kMlpThreads), mlp_smem(f1.N), s, a);
   return hipGetLastError();
 }
 
