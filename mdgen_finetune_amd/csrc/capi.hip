@@ -137,8 +137,12 @@ bool fused_mlp_on() {
   return on;
 }
 
+// fewer than 128 row tiles of 128: a one-block-per-tile kernel would leave most CUs idle
+bool small_m(long long N) { return (N + 127) / 128 < 128; }
+
 // bf16, C = 384, packed planes: the spatial out_proj row-LN and the temporal q|k|v projection
-// as one kernel (LN_t(h) stays on chip); MDG_FUSED_QKV=0 keeps the two launches (A/B knob)
+// as one kernel (LN_t(h) stays on chip); MDG_FUSED_QKV=0 keeps the two launches (A/B knob).
+// Small M takes the two launches (the q|k|v GEMM then runs on 9x the blocks).
 bool fused_qkv_on() {
   static const bool on = [] {
     const char* e = getenv("MDG_FUSED_QKV");
@@ -489,7 +493,7 @@ static int layer_fwd_impl(const mdg_dims* d, const mdg_layer_weights* w, const f
   q.W = w->wqkv[1]; q.bias = w->bqkv[1];
   q.qkv_layout = tlayout; q.qkv_out = qkv_t; q.qscale = qs * 1.4426950408889634f;
   q.rope = rope_t; q.rope_rows = T + 1;
-  if (fuse && fused_qkv_on() && mdg::rowln_qkv_supported(r, q)) {
+  if (fuse && fused_qkv_on() && !small_m(N) && mdg::rowln_qkv_supported(r, q)) {
     // out_proj + gated residual + LN_t + q|k|v in one launch (xn is not written)
     if (int e = hip_check(mdg::rowln_qkv_launch(r, q, s), "rowln_qkv launch")) return e;
   } else {
@@ -637,7 +641,8 @@ int mdg_describe_plan(const mdg_dims* d, char* buf, size_t n) {
            "\"final\": \"%s\"}",
            d->dtype == MDG_BF16 ? "bf16" : "f32", spatial,
            fuse ? "fused into gated-residual row-LN GEMM epilogues" : "stand-alone ln_mod pass",
-           (fuse && fused_qkv_on() && C == 384 && packed_planes(*d) && d->D <= 48 && d->T * d->L >= 128)
+           (fuse && fused_qkv_on() && C == 384 && packed_planes(*d) && d->D <= 48 && d->T * d->L >= 128 &&
+            !small_m((long long)d->B * d->T * d->L))
                ? "rowln_qkv(spatial out_proj+gated residual+LN_t+q|k|v in one kernel, LN_t on chip)"
                : "qkv_gemm",
            d->D >= MDG_DP ? (d->dtype == MDG_BF16 ? "attn_temporal(wide heads: bf16 16x16x32 mfma, 64-col rows)"
@@ -645,7 +650,9 @@ int mdg_describe_plan(const mdg_dims* d, char* buf, size_t n) {
            : d->dtype == MDG_BF16 ? "attn_temporal_bf16(32x32x16 mfma)" : "attn_temporal(f32 16x16x4 mfma)",
            packed_planes(*d) ? "packed (row stride = head_dim)" : "padded (row stride MDG_HEAD_STRIDE)",
            (fuse && fused_mlp_on() && d->dtype == MDG_BF16 && d->C == 384 && d->T * d->L >= 128)
-               ? "mlp_fused(fc1+gelu+fc2+gated residual+LN in one kernel, hidden on chip)"
+               ? (mdg::mlp_split_factor(d->B * d->T * d->L, d->F) > 1
+                      ? "mlp_fused(small M: hidden chunks split over blocks, fp32 partials + row-LN pass)"
+                      : "mlp_fused(fc1+gelu+fc2+gated residual+LN in one kernel, hidden on chip)")
            : fuse ? "fc1_gemm(gelu)+fc2_rowln_gemm"
                   : "fc1_gemm(gelu)+fc2_gate_res_gemm",
            (d->dtype == MDG_BF16 && fast_final_on() && d->latent <= 32 && (C == 128 || C == 256 || C == 384 || C == 512))

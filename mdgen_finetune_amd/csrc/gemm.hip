@@ -2164,8 +2164,10 @@ hipError_t rowln_qkv_launch(const mdg_gemm_desc& r, const mdg_gemm_desc& q, hipS
 
 // row-tile height of the fused gated-residual + LN GEMM (MDG_ROWLN_BM=64 knob; default 128:
 // measured at M = 32000 / 64000, 64-row tiles at two blocks per CU tie on out_proj and lose
-// 20 % on fc2 — the extra W re-reads from L2 outweigh the epilogue / main-loop overlap)
-static int rowln_bm() {
+// 20 % on fc2 — the extra W re-reads from L2 outweigh the epilogue / main-loop overlap.  Not
+// chosen automatically for small M either: its epilogue rounds h 1 ulp differently from the
+// 128-row one, which the fused kernels' bit-identity to this GEMM relies on)
+static int rowln_bm(int) {
   static const int bm = [] {
     const char* e = getenv("MDG_ROWLN_BM");
     return (e && atoi(e) == 64) ? 64 : 128;
@@ -2530,7 +2532,7 @@ GemmPlan gemm_plan(const mdg_gemm_desc& p) {
   else if (bf && !ext && p.epi == MDG_EPI_GATE_RES && p.xn_out && p.K % 64 == 0 && p.lda % 8 == 0 && p.ldw % 8 == 0 &&
            (p.N == 128 || p.N == 256 || p.N == 384 || p.N == 512)) {
     g.cfg = kCfgRow;  // full-row gated residual + LayerNorm
-    const bool b64 = rowln_bm() == 64 && p.N <= 384;
+    const bool b64 = rowln_bm(p.M) == 64 && p.N <= 384;
 #define MDG_ROWSM(n) (b64 ? rowln_smem<n, 64>() : rowln_smem<n, 128>())
     g.smem = p.N == 128 ? MDG_ROWSM(128) : p.N == 256 ? MDG_ROWSM(256) : p.N == 384 ? MDG_ROWSM(384) : MDG_ROWSM(512);
 #undef MDG_ROWSM
