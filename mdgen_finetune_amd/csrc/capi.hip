@@ -21,6 +21,8 @@ hipError_t gemm_launch(const mdg_gemm_desc& p, const GemmPlan& g, hipStream_t s)
 bool mlp_fused_supported(const mdg_gemm_desc& f1, const mdg_gemm_desc& f2);
 hipError_t mlp_fused_launch(const mdg_gemm_desc& f1, const mdg_gemm_desc& f2, hipStream_t s, float* part);
 int mlp_split_factor(int M, int F);
+bool rowln_splitk_supported(const mdg_gemm_desc& r, int S);
+hipError_t rowln_splitk_launch(const mdg_gemm_desc& r, hipStream_t s, float* part, int S);
 bool final_euler_supported(const mdg_gemm_desc& p);
 hipError_t final_euler_launch(const mdg_gemm_desc& p, hipStream_t s);
 bool rowln_qkv_supported(const mdg_gemm_desc& r, const mdg_gemm_desc& q);
@@ -163,6 +165,7 @@ bool fast_final_on() {
 
 struct WsLayout {
   size_t qkv_s, qkv_t, o, hid, xn, kbias, kbias_s, mlp_part, total;
+  int mlp_split;  // > 1: [mlp_split][N][C] fp32 partials at mlp_part (small-M MLP / out_proj)
 };
 
 WsLayout ws_layout(const mdg_dims& d) {
@@ -180,6 +183,7 @@ WsLayout ws_layout(const mdg_dims& d) {
   // the small-M fused MLP's fc2 partials ([split][N][C] fp32; bf16 C = 384 only, else empty)
   const int split = (d.dtype == MDG_BF16 && d.C == 384 && d.F % 128 == 0) ? mdg::mlp_split_factor((int)N, d.F) : 1;
   w.mlp_part = off; off += split > 1 ? align256((size_t)split * N * d.C * sizeof(float)) : 0;
+  w.mlp_split = split;
   w.total = off;
   return w;
 }
@@ -426,6 +430,23 @@ static int layer_fwd_impl(const mdg_dims* d, const mdg_layer_weights* w, const f
   void* xn = wsb + lay.xn;
   hipStream_t s = (hipStream_t)stream;
   const int TL = T * L, ms = 9 * C;
+  // out_proj row-LN GEMMs: split-K over the workspace's partials when M is small
+  auto rowln_gemm = [&](const mdg_gemm_desc& g) -> int {
+    // at most MDG_ROWLN_SPLITK K pieces of the 12 K-steps (default 1 = off).  Measured: a B = 1
+    // window (one chain, 32 tiles) +7 % at 2-4 pieces, but a TPS B = 16 window (two lanes of 25
+    // tiles sharing the chip) -9 % at 2 and -26 % at 12: the fp32 partials' write + re-read cost
+    // more than the CUs the other lane leaves idle.  The library cannot see the lane count.
+    static const int smax = [] {
+      const char* e = getenv("MDG_ROWLN_SPLITK");
+      return e ? atoi(e) : 1;
+    }();
+    int S = 1;
+    for (int d2 = 2; d2 <= smax && d2 <= lay.mlp_split; ++d2)
+      if (12 % d2 == 0 && ((N + 127) / 128) * d2 <= 320) S = d2;
+    if (small_m(N) && mdg::rowln_splitk_supported(g, S))
+      return hip_check(mdg::rowln_splitk_launch(g, s, (float*)(wsb + lay.mlp_part), S), "rowln split-K launch");
+    return mdg_gemm(&g, stream);
+  };
   // LN + adaLN modulate into the CT activation buffer (latent_model.py:467/475/489)
   // fused hand-off: the bf16 path with C in {128..512} produces each LN input inside the
   // preceding gated-residual GEMM (gemm_rowln_kernel); otherwise a stand-alone ln_mod pass
@@ -497,7 +518,7 @@ static int layer_fwd_impl(const mdg_dims* d, const mdg_layer_weights* w, const f
     // out_proj + gated residual + LN_t + q|k|v in one launch (xn is not written)
     if (int e = hip_check(mdg::rowln_qkv_launch(r, q, s), "rowln_qkv launch")) return e;
   } else {
-    if (int e = mdg_gemm(&r, stream)) return e;
+    if (int e = rowln_gemm(r)) return e;
     if (!fuse)
       if (int e = ln(3 * C, 4 * C)) return e;
     if (int e = mdg_gemm(&q, stream)) return e;
@@ -507,7 +528,7 @@ static int layer_fwd_impl(const mdg_dims* d, const mdg_layer_weights* w, const f
   if (fuse) {  // + LN_mlp(h) -> xn
     r.xn_shift_off = 6 * C; r.xn_scale_off = 7 * C;
   }
-  if (int e = mdg_gemm(&r, stream)) return e;
+  if (int e = rowln_gemm(r)) return e;
 
   // ---- MLP: x += gate_m * fc2(gelu(fc1(mod(LN x))))           (latent_model.py:488-491)
   if (!fuse)

@@ -1116,7 +1116,9 @@ __device__ __forceinline__ void rowln_fast_epilogue(const mdg_gemm_desc& p, f32x
   }
 }
 
-template <int NCOL, int BM>
+// PART: split-K form for small M — block (tile, y) runs K-steps [y nk, (y + 1) nk) and writes its
+// fp32 partial tile to (float*)p.aux + y * M * NCOL; mlp_split_reduce_kernel finishes the rows
+template <int NCOL, int BM, bool PART = false>
 __global__ __launch_bounds__(kRowThreads, BM == 64 ? 4 : 1) void gemm_rowln_kernel(const mdg_gemm_desc p) {
   constexpr int kRowStages = RowCfg<BM>::STAGES, WMW = RowCfg<BM>::WMW, WNW = 8 / WMW;
   constexpr int BK = 32, WTN = NCOL / WNW, NT = WTN / 16, ATILE = BM * BK, STAGE = (BM + NCOL) * BK;
@@ -1197,8 +1199,10 @@ __global__ __launch_bounds__(kRowThreads, BM == 64 ? 4 : 1) void gemm_rowln_kern
   const bool fast = BM == 128 && b_hi - b_lo < 2;
   float4 h4[2][NE];
   float2 hv[RG][NE], gv[NE];
-  if (fast) rowln_load_band<NCOL>(p, m0, 0, h4);
-  else if (BM == 64) load_unit(0, hv, gv);
+  if (!PART) {
+    if (fast) rowln_load_band<NCOL>(p, m0, 0, h4);
+    else if (BM == 64) load_unit(0, hv, gv);
+  }
 
   f32x4 acc[4][NT];
 #pragma unroll
@@ -1206,10 +1210,10 @@ __global__ __launch_bounds__(kRowThreads, BM == 64 ? 4 : 1) void gemm_rowln_kern
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = K / BK;
+  const int nk = (PART ? K / (int)gridDim.y : K) / BK, kbeg = PART ? (int)blockIdx.y * nk * BK : 0;
 #pragma unroll
   for (int s0 = 0; s0 < kRowStages - 1; ++s0)
-    if (s0 < nk) MDG_ROW_LOAD(s0, s0 * BK);
+    if (s0 < nk) MDG_ROW_LOAD(s0, kbeg + s0 * BK);
   const int swz = (-(lr >> 2)) & 3;
   for (int kt = 0; kt < nk; ++kt) {
     // stage kt landed: leave the (up to 2) younger stages' loads in flight
@@ -1225,7 +1229,7 @@ __global__ __launch_bounds__(kRowThreads, BM == 64 ? 4 : 1) void gemm_rowln_kern
     }
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (kt + kRowStages - 1 < nk) MDG_ROW_LOAD((kt + kRowStages - 1) % kRowStages, (kt + kRowStages - 1) * BK);
+    if (kt + kRowStages - 1 < nk) MDG_ROW_LOAD((kt + kRowStages - 1) % kRowStages, kbeg + (kt + kRowStages - 1) * BK);
     const bf16_t* As = lds + (kt % kRowStages) * STAGE;
     const bf16_t* Bs = As + ATILE;
     const int ch = (lg ^ swz) * 8;
@@ -1240,6 +1244,21 @@ __global__ __launch_bounds__(kRowThreads, BM == 64 ? 4 : 1) void gemm_rowln_kern
       for (int j = 0; j < NT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
   }
 #undef MDG_ROW_LOAD
+
+  if constexpr (PART) {
+    static_assert(BM == 128, "split-K form: 128-row tiles");
+    float* pp = reinterpret_cast<float*>(p.aux) + (size_t)blockIdx.y * M * NCOL;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * 64 + i * 16 + lg * 4 + r;
+        if (m < M)
+#pragma unroll
+          for (int j = 0; j < NT; ++j) pp[(size_t)m * NCOL + wn * WTN + j * 16 + lr] = acc[i][j][r];
+      }
+    return;
+  }
 
   // ------------------------------------------------------------------ epilogue
   float* stage = reinterpret_cast<float*>(smem);
@@ -1865,6 +1884,33 @@ hipError_t mlp_fused_launch(const mdg_gemm_desc& f1, const mdg_gemm_desc& f2, hi
     return hipGetLastError();
   }
   hipLaunchKernelGGL((mlp_rowln_kernel<384, false>), dim3(tiles), dim3(kMlpThreads), mlp_smem(f1.N), s, a);
+  return hipGetLastError();
+}
+
+// Split-K row-LN GEMM for small M (the out_proj launches of a B = 1 window: 32 row tiles):
+// S = the MLP's split factor (a divisor of the 12 K-steps), fp32 partials in `part` ([S][M][384]), then
+// the split MLP's reduction pass (sum, + bias, gated residual, LN + modulate -> xn).  Same
+// envelope as the fast row-LN path: bf16 PLAIN, K = N = 384, rows_per_mod >= 128, xn out.
+bool rowln_splitk_supported(const mdg_gemm_desc& r, int S) {
+  return S > 1 && (384 / 32) % S == 0 && r.dtype == MDG_BF16 && r.a_mode == MDG_A_PLAIN &&
+         r.epi == MDG_EPI_GATE_RES && r.N == 384 && r.K == 384 && r.rows_per_mod >= 128 && r.resid && !r.resid_in &&
+         !r.aux && r.xn_out && r.xn_mods && r.lda % 8 == 0 && r.ldw % 8 == 0 && r.ldr % 4 == 0;
+}
+
+hipError_t rowln_splitk_launch(const mdg_gemm_desc& r, hipStream_t s, float* part, int S) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_rowln_kernel<384, 128, true>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)rowln_smem<384, 128>());
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  mdg_gemm_desc rp = r;
+  rp.aux = part;
+  hipLaunchKernelGGL((gemm_rowln_kernel<384, 128, true>), dim3((r.M + 127) / 128, S), dim3(kRowThreads),
+                     (rowln_smem<384, 128>()), s, rp);
+  if (hipError_t e = hipGetLastError()) return e;
+  hipLaunchKernelGGL((mlp_split_reduce_kernel<384>), dim3((r.M + 3) / 4), dim3(256), 0, s, r, (const float*)part, S);
   return hipGetLastError();
 }
 
