@@ -139,8 +139,9 @@ bool fused_mlp_on() {
   return on;
 }
 
-// fewer than 128 row tiles of 128: a one-block-per-tile kernel would leave most CUs idle
-bool small_m(long long N) { return (N + 127) / 128 < 128; }
+// fewer than 64 row tiles of 128: a one-block-per-tile kernel would leave most CUs idle even
+// with a second lane beside it (the engine runs 2 lanes from B = 8; a B = 8 lane has 125 tiles)
+bool small_m(long long N) { return (N + 127) / 128 < 64; }
 
 // bf16, C = 384, packed planes: the spatial out_proj row-LN and the temporal q|k|v projection
 // as one kernel (LN_t(h) stays on chip); MDG_FUSED_QKV=0 keeps the two launches (A/B knob).

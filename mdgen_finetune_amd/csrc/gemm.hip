@@ -1844,7 +1844,7 @@ bool mlp_fused_supported(const mdg_gemm_desc& f1, const mdg_gemm_desc& f2) {
          f1.ldw % 8 == 0 && f2.ldw % 8 == 0 && f2.ldr % 4 == 0 && (!f2.xn_out || f2.xn_mods) && mlp_smem(f1.N) <= 160 * 1024;
 }
 
-// Hidden-chunk split for small M (fewer row tiles than the chip has CUs: each block would stream
+// Hidden-chunk split for small M (< 64 row tiles, a quarter of the CUs: each block would stream
 // all of W1 and W2 for one tile): the largest divisor of the chunk count that keeps the grid
 // within ~1.25 blocks per CU; 1 = no split.  MDG_MLP_SPLIT=0 disables it (A/B knob).
 int mlp_split_factor(int M, int F) {
@@ -1853,7 +1853,7 @@ int mlp_split_factor(int M, int F) {
     return !(e && e[0] == '0');
   }();
   const int tiles = (M + 127) / 128, nch = F / kMlpHC;
-  if (!on || tiles >= 128 || nch < 2) return 1;
+  if (!on || tiles >= 64 || nch < 2) return 1;
   int best = 1;
   for (int d = 2; d <= nch; ++d)
     if (nch % d == 0 && tiles * d <= 320) best = d;
