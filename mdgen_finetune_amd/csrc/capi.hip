@@ -436,7 +436,9 @@ static int layer_fwd_impl(const mdg_dims* d, const mdg_layer_weights* w, const f
     // at most MDG_ROWLN_SPLITK K pieces of the 12 K-steps (default 1 = off).  Measured: a B = 1
     // window (one chain, 32 tiles) +7 % at 2-4 pieces, but a TPS B = 16 window (two lanes of 25
     // tiles sharing the chip) -9 % at 2 and -26 % at 12: the fp32 partials' write + re-read cost
-    // more than the CUs the other lane leaves idle.  The library cannot see the lane count.
+    // more than the CUs the other lane leaves idle.  Keying it on the launch's B (< 4: a chain
+    // alone on the chip) broke the lanes' bit-identity to one chain (a 2-lane window of B = 4
+    // would split, the single chain would not), so it stays an explicit choice.
     static const int smax = [] {
       const char* e = getenv("MDG_ROWLN_SPLITK");
       return e ? atoi(e) : 1;

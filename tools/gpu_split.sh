@@ -13,8 +13,8 @@ line() {  # $1 = env, rest = bench args
     > gpurun_out/bench_split.log 2>&1 || exit 1
   python -c "import json;d=json.loads(open('gpurun_out/bench_split.log').read().strip().splitlines()[-1]);print('$env', '$*', d['value'], d['us_per_denoise_step'])"
 }
-for rep in 1; do
-  for e in MDG_X=1 MDG_ROWLN_SPLITK=2 MDG_ROWLN_SPLITK=1; do
+for rep in 1 2; do
+  for e in MDG_X=1 MDG_ROWLN_SPLITK=1; do
     line $e --batch 1 --lanes 1
     line $e --tps --frames 100 --batch 16
   done
