@@ -14,7 +14,7 @@ line() {  # $1 = env, rest = bench args
   python -c "import json;d=json.loads(open('gpurun_out/bench_split.log').read().strip().splitlines()[-1]);print('$env', '$*', d['value'], d['us_per_denoise_step'])"
 }
 for rep in 1 2; do
-  for e in MDG_X=1 MDG_ROWLN_SPLITK=1; do
+  for e in MDG_X=1 MDG_ROWLN64_SMALL=0; do
     line $e --batch 1 --lanes 1
     line $e --tps --frames 100 --batch 16
   done
