@@ -1846,17 +1846,25 @@ bool mlp_fused_supported(const mdg_gemm_desc& f1, const mdg_gemm_desc& f2) {
 
 // Hidden-chunk split for small M (< 64 row tiles, a quarter of the CUs: each block would stream
 // all of W1 and W2 for one tile): the largest divisor of the chunk count that keeps the grid
-// within ~1.25 blocks per CU; 1 = no split.  MDG_MLP_SPLIT=0 disables it (A/B knob).
+// within the cap below; 1 = no split.  MDG_MLP_SPLIT=0 disables it (A/B knob).
 int mlp_split_factor(int M, int F) {
   static const bool on = [] {
     const char* e = getenv("MDG_MLP_SPLIT");
     return !(e && e[0] == '0');
   }();
+  // MDG_MLP_SPLIT_BLOCKS: grid cap (default 320).  Measured: 160 gives a two-lane TPS window
+  // (25 tiles per lane) 6 pieces instead of 12, +12.7 %, and a B = 1 window 4 instead of 6,
+  // -3.6 %; 240 (6 and 6) made test_concurrent_lanes_equal_single_chain[3-1] fail in 2 of 3
+  // full GPU suites (graph replay != single chain) — not understood, so 320 stays
+  static const int cap = [] {
+    const char* e = getenv("MDG_MLP_SPLIT_BLOCKS");
+    return e ? atoi(e) : 320;
+  }();
   const int tiles = (M + 127) / 128, nch = F / kMlpHC;
   if (!on || tiles >= 64 || nch < 2) return 1;
   int best = 1;
   for (int d = 2; d <= nch; ++d)
-    if (nch % d == 0 && tiles * d <= 320) best = d;
+    if (nch % d == 0 && tiles * d <= cap) best = d;
   return best;
 }
 

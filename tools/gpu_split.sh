@@ -3,7 +3,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests -m gpu -q -x --timeout 200 --timeout-method thread -p no:cacheprovider \
+[ -n "${SKIP_SUITE:-}" ] || timeout -k 10 600 python -u -m pytest tests -m gpu -q -x --timeout 200 --timeout-method thread -p no:cacheprovider \
   > gpurun_out/pytest_split.log 2>&1; rc=$?
 echo "suite rc=$rc"; tail -2 gpurun_out/pytest_split.log
 [ $rc -ne 0 ] && exit $rc
@@ -14,7 +14,7 @@ line() {  # $1 = env, rest = bench args
   python -c "import json;d=json.loads(open('gpurun_out/bench_split.log').read().strip().splitlines()[-1]);print('$env', '$*', d['value'], d['us_per_denoise_step'])"
 }
 for rep in 1 2; do
-  for e in MDG_X=1 MDG_ROWLN64_SMALL=0; do
+  for e in MDG_X=1 MDG_MLP_SPLIT_BLOCKS=160 MDG_MLP_SPLIT_BLOCKS=400; do
     line $e --batch 1 --lanes 1
     line $e --tps --frames 100 --batch 16
   done
