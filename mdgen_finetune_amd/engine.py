@@ -263,10 +263,15 @@ class HipEngine:
         if nbytes == 0:
             _lib.check(1001, f"workspace for B={B} T={T} L={L}")
         st.ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        if os.environ.get("MDG_POISON_WS") == "1":  # debugging: NaN bytes expose reads of unwritten memory
+            st.ws.fill_(0xFF)
         _lib.check(lib.mdg_workspace_init(ctypes.byref(st.dims), st.ws.data_ptr(), _lib.stream_handle()),
                    "mdg_workspace_init")
         st.h = torch.empty(st.N, self.C, device=dev)
         st.base = torch.empty(st.N, self.C, device=dev)
+        if os.environ.get("MDG_POISON_WS") == "1":
+            st.h.fill_(float("nan"))
+            st.base.fill_(float("nan"))
         st.rope_l = self._rope_table(L + 1) if self.rope else None
         st.rope_t = self._rope_table(T + 1) if self.rope else None
         st.kvb = []
