@@ -61,6 +61,14 @@ def parse():
                     help="extra per-GPU batch sizes timed beside the headline (comma list, '' = none)")
     ap.add_argument("--no-f32-line", action="store_true", help="skip the fp32-operand (parity path) line")
     ap.add_argument("--sweep-steps", type=int, default=2, help="timed windows per sweep / f32 line")
+    ap.add_argument("--sampler", default="euler", choices=["euler", "dopri5"],
+                    help="dopri5: an evidence line for the reference's DEFAULT sampler (parsing.py:102): one "
+                         "window = Sampler.sample_ode() (adaptive dopri5, atol 1e-6 / rtol 1e-3, 50 saved points) "
+                         "with every adaptive step one hipGraph replay; reports NFE and accepted / rejected steps")
+    ap.add_argument("--train", action="store_true",
+                    help="BASELINE config 3 evidence line: the GVP training step (forward + loss + backward + "
+                         "clip + Adam + EMA, the HIP block stack, graphed) at B trajectories x T frames per GPU "
+                         "(use --batch 8); ranks average gradients over RCCL")
     ap.add_argument("--tps", action="store_true",
                     help="TPS / interpolation model (BASELINE config 4: --tps_condition, latent 28, start + end "
                          "frames conditioned; use with --frames 100); an evidence line, not the headline")
@@ -393,6 +401,143 @@ def cpu_baseline(T, L, seconds):
                       f"{el:.1f} s on {threads} threads of {cpu}"}
 
 
+def cpu_train_baseline(T, L, seconds):
+    """The eager CPU training step (the reference's arithmetic: the build's torch backend on the
+    CPU, fp32, autograd + Adam) at B=1, T frames, timed until `seconds` of CPU work."""
+    from mdgen_finetune_amd.parsing import parse_train_args
+    from mdgen_finetune_amd.train import Trainer
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    threads = max(1, min(threads, os.cpu_count() or 1))
+    torch.set_num_threads(threads)
+    args = parse_train_args(["--synthetic", "--sim_condition", "--prepend_ipa", "--abs_pos_emb", "--num_frames",
+                             str(T), "--crop", str(L), "--batch_size", "1", "--synthetic_size", "1"])
+    tr = Trainer(args)
+    b = next(iter(tr.loader))
+    tr.step([b], log=False)  # warm
+    n, t0 = 0, time.perf_counter()
+    while True:
+        tr.step([b], log=False)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= seconds or n >= 20:
+            break
+    return {"value": round(T * n / el, 1), "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": f"{n} eager training steps (torch CPU autograd + Adam, the reference's fp32 arithmetic), "
+                      f"B=1 T={T} L={L}, {el:.1f} s on {threads} threads"}
+
+
+def train_main(a, world, rank, dev, share):
+    """Config 3 (BASELINE.json configs[2]): training frames/s = world * B * T * steps / time of
+    `steps` optimizer steps (GraphedStep replays; the batch is on the device)."""
+    from mdgen_finetune_amd.parsing import parse_train_args
+    from mdgen_finetune_amd.train import Trainer
+
+    B, T, L = a.batch, a.frames, a.crop
+    args = parse_train_args(["--synthetic", "--sim_condition", "--prepend_ipa", "--abs_pos_emb", "--num_frames",
+                             str(T), "--crop", str(L), "--batch_size", str(B), "--synthetic_size", str(B * world),
+                             "--hip_dtype", a.dtype, "--seed", "137"])
+    torch.set_float32_matmul_precision("medium")  # train.py:13
+    tr = Trainer(args, rank, world, dev)
+    batch = {k: (v.to(dev) if torch.is_tensor(v) else v) for k, v in next(iter(tr.loader)).items()}
+    for _ in range(max(1, a.warmup)):
+        loss, _ = tr.step([batch], log=False)
+    torch.cuda.synchronize()
+    assert torch.isfinite(loss).all(), "non-finite loss"
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        loss, _ = tr.step([batch], log=False)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    el = max_over_ranks(time.perf_counter() - t0, world, torch.device("cpu") if share else dev)
+    if rank != 0:
+        return
+    sec = el / a.steps
+    sm = step_model(B, T, L, dtype=a.dtype)
+    flops = 3.0 * sm["flops"]  # forward + backward (2x) of the block stack per optimizer step
+    tf = flops / sec / 1e12
+    cpu = None if (a.no_cpu_baseline or world > 1) else cpu_train_baseline(T, L, a.cpu_seconds)
+    out = {"metric": "training frames/sec (GVP flow-matching optimizer step), 1000-frame x crop4 forward-sim, "
+                     "1/2/4/8 MI355X",
+           "value": round(world * B * T * a.steps / el, 1), "unit": "frames/s", "n_gpus": 1 if share else world,
+           "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(sec * 1e3, 3), "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": a.dtype,
+           "data": "synthetic (seeded weights and tetrapeptide trajectories; no dataset offline)",
+           "config": {"workload": f"training step: prep_batch + GVP loss + backward + grad clip + Adam + EMA, "
+                                  f"B={B} trajectories x T={T} frames x L={L} per GPU",
+                      "model": "LatentMDGenModel default (5 layers, C=384, 16 heads, IPA prepend, abs pos emb)",
+                      "global_batch": B * world, "seq_len": T, "crop": L,
+                      "parallelism": f"dp{world}" + (" (flat RCCL all-reduce between graphs)" if world > 1 else ""),
+                      "hipgraph": bool(tr.graph_mode)},
+           "step_roofline": {"flops_per_step": flops, "flops_basis": "3 x forward FLOPs of the block stack + "
+                                                                     "embedding / FinalLayer (step_model), B per GPU",
+                             "achieved_tflops": round(tf, 1), "peak_tflops": PEAK_TFLOPS[a.dtype],
+                             "mfma_frac": round(tf / PEAK_TFLOPS[a.dtype], 4)},
+           "loss": float(loss), "max_mem_gb": round(torch.cuda.max_memory_allocated() / 2 ** 30, 2),
+           "cpu_baseline": cpu}
+    if share:
+        out["shared_gpu"] = True
+        out["ranks_sharing_gpu"] = world
+    print(json.dumps(out), flush=True)
+
+
+def dopri5_main(a, world, rank, dev, share):
+    """The reference's default sampler: frames/s = world * B * T * windows / time, where a
+    window is Sampler(transport).sample_ode() (dopri5) from x0 ~ N(0, I) to t = 1 through the
+    drop-in call (wrapper.py:472-478), every adaptive step one hipGraph replay
+    (integrators.odeint_dopri5_graphed) and one host read."""
+    import functools
+
+    from mdgen_finetune_amd.transport import Dopri5Stats, Sampler, create_transport
+
+    B, T, L = a.batch, a.frames, a.crop
+    m = make_model(T, L).to(dev)
+    m.hip_dtype = a.dtype
+    zs, kw, _ = inputs(B, T, L, seed=100 + rank, device=dev)
+    sampler = Sampler(create_transport(m.args, "GVP", "velocity"))
+    fn = sampler.sample_ode()  # dopri5 (parsing.py:102)
+    model = functools.partial(m.forward_inference, **kw)
+    with torch.no_grad():
+        for _ in range(max(1, a.warmup)):
+            ys = fn(zs, model)
+        torch.cuda.synchronize()
+        assert torch.isfinite(ys[-1]).all(), "non-finite samples"
+        if world > 1:
+            torch.distributed.barrier()
+        stats = []
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            sampler.dopri5_stats = Dopri5Stats()
+            fn(zs, model)
+            stats.append(sampler.dopri5_stats)
+        torch.cuda.synchronize()
+        if world > 1:
+            torch.distributed.barrier()
+        el = max_over_ranks(time.perf_counter() - t0, world, torch.device("cpu") if share else dev)
+    if rank != 0:
+        return
+    nfe = sum(s.nfe for s in stats) / len(stats)
+    sec = el / a.steps
+    out = {"metric": "denoised frames/sec, 1000-frame x crop4 forward-sim window, dopri5 (the reference's default "
+                     "sampler), 1/2/4/8 MI355X",
+           "value": round(world * B * T * a.steps / el, 1), "unit": "frames/s", "n_gpus": 1 if share else world,
+           "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(sec * 1e3, 3), "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": a.dtype,
+           "data": "synthetic (seed-derived weights and tetrapeptide latents/frames; no checkpoint offline)",
+           "config": {"workload": f"sim_inference rollout window: adaptive dopri5 (atol 1e-6, rtol 1e-3, 50 saved "
+                                  f"points) x B={B} trajectories x T={T} frames x L={L}, per GPU",
+                      "global_batch": B * world, "seq_len": T, "crop": L, "parallelism": f"replicas{world}"},
+           "nfe_per_window": nfe, "accepted_steps": [s.accepted for s in stats],
+           "rejected_steps": [s.rejected for s in stats],
+           "ms_per_evaluation": round(sec / nfe * 1e3, 3),
+           "forward_frames_per_s": round(world * B * T * nfe * a.steps / el, 1)}  # comparable to the Euler line
+    print(json.dumps(out), flush=True)
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -412,6 +557,16 @@ def main():
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=dev)
+    if a.train:
+        train_main(a, world, rank, dev, share)
+        if world > 1:
+            torch.distributed.destroy_process_group()
+        return
+    if a.sampler == "dopri5":
+        dopri5_main(a, world, rank, dev, share)
+        if world > 1:
+            torch.distributed.destroy_process_group()
+        return
     from mdgen_finetune_amd.engine import get_engine
 
     B, T, L = a.batch, a.frames, a.crop

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define MDG_ABI_VERSION 14
+#define MDG_ABI_VERSION 15
 #define MDG_MAX_LAYERS 16
 #define MDG_DP 32      /* padded head dim of the attention operand buffers for head_dim <= 31 */
 #define MDG_DP_WIDE 64 /* ... and for 32 <= head_dim <= 63 (column head_dim of the padded k / v rows
@@ -422,6 +422,18 @@ int mdg_attn_temporal_bwd(int32_t dtype, int32_t B, int32_t T, int32_t L, int32_
 int mdg_attn_spatial_bwd(int32_t dtype, int32_t n_frames, int32_t L, int32_t H, int32_t D, const void* qkv,
                          const float* kvb, const float* mask, const void* dout, const float* rope, int32_t rope_rows,
                          void* dqkv, float* bpart, float qscale, void* stream);
+
+/* Weight / bias gradients of a linear layer from token-major operands (the nn.Linear backward
+   inside LatentMDGenLayer under loss.backward(): transport.py:137-222, latent_model.py:456-493):
+     dw[m][k] = sum_n dy[n][m] x[n][k]   (fp32, ld lddw; null = skip)
+     db[m]    = sum_n dy[n][m]           (fp32; null = skip)
+   dy CT [N][ldy] (columns 0..M-1), x CT [N][ldx] (columns 0..K-1); the reduction is split over
+   token chunks whose fp32 partials (in ws) are summed in chunk order: deterministic.  bf16 needs
+   N % 32 == 0 (pad the token rows with zeros); M, K, ldy, ldx multiples of 8; 16-B aligned
+   operands.  ws: mdg_wgrad_workspace_bytes(dtype, N, M, K, need_dw, need_db) bytes. */
+size_t mdg_wgrad_workspace_bytes(int32_t dtype, int32_t N, int32_t M, int32_t K, int32_t need_dw, int32_t need_db);
+int mdg_wgrad(int32_t dtype, int32_t N, int32_t M, int32_t K, const void* dy, int32_t ldy, const void* x, int32_t ldx,
+              float* dw, int32_t lddw, float* db, void* ws, size_t ws_bytes, void* stream);
 
 #ifdef __cplusplus
 }

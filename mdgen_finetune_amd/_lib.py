@@ -143,9 +143,11 @@ SIGNATURES = [
                                      _vp, _vp, _i32, _vp, _f32, _f32, _i32, _vp]),
     ("mdg_attn_spatial_bwd", _i32, [_i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _f32,
                                     _vp]),
+    ("mdg_wgrad_workspace_bytes", ctypes.c_size_t, [_i32, _i32, _i32, _i32, _i32, _i32]),
+    ("mdg_wgrad", _i32, [_i32, _i32, _i32, _i32, _vp, _i32, _vp, _i32, _vp, _i32, _vp, _vp, ctypes.c_size_t, _vp]),
 ]
 
-ABI_VERSION = 14
+ABI_VERSION = 15
 _LIB = None
 
 

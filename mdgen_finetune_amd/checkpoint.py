@@ -23,7 +23,8 @@ def _safe_load(path, map_location="cpu"):
         return torch.load(path, map_location=map_location, weights_only=True)
 
 
-def save_checkpoint(path, wrapper, optimizer=None, epoch=0, global_step=0, epoch_complete=True, batches_done=0):
+def save_checkpoint(path, wrapper, optimizer=None, epoch=0, global_step=0, epoch_complete=True, batches_done=0,
+                    grad_scaler=None):
     """Lightning layout; ``args`` is stored as a Namespace of plain values.  ``loops`` records
     where in the epoch the save happened (a mid-epoch save, e.g. at --max_steps, resumes the
     same epoch after its ``batches_done`` consumed batches, as Lightning's fit loop does)."""
@@ -41,6 +42,8 @@ def save_checkpoint(path, wrapper, optimizer=None, epoch=0, global_step=0, epoch
         "lr_schedulers": [],
         "loops": {"fit_loop": {"epoch_complete": bool(epoch_complete), "batches_done": int(batches_done)}},
     }
+    if grad_scaler is not None:  # --precision 16-mixed: the loss-scale state (Lightning's precision-plugin entry)
+        ckpt["MixedPrecision"] = grad_scaler
     if wrapper.ema is not None:
         ema = wrapper.ema.state_dict()
         ckpt["ema"] = {"params": {k: v.detach().cpu() for k, v in ema["params"].items()},

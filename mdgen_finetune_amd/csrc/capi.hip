@@ -81,6 +81,10 @@ hipError_t ipa_attn_launch(int R, int B, int L, int H, int c, int pq, int pv, co
                            float* out, int ldc, hipStream_t s);
 hipError_t tps_rel7_launch(int B, int L, const float* rots, const float* trans, const float* erots,
                            const float* etrans, float* out, hipStream_t s);
+// wgrad.hip
+size_t wgrad_ws_bytes(int dtype, int N, int M, int K, bool need_w, bool need_b);
+hipError_t wgrad_launch(int dtype, int N, int M, int K, const void* dy, int ldy, const void* x, int ldx, float* dw,
+                        int lddw, float* db, float* ws, hipStream_t s);
 }  // namespace mdg
 
 namespace {
@@ -1102,6 +1106,26 @@ int mdg_precompute_cond(const mdg_cond_model* m, const mdg_cond_io* io, void* ws
   if (d.tps)  // x_r + x_f (latent_model.py:211)
     if (int e = hip_check(mdg::add_inplace_launch((size_t)M * C, io->ipa, F(c.x2), s), "ipa add")) return e;
   return MDG_OK;
+}
+
+size_t mdg_wgrad_workspace_bytes(int32_t dtype, int32_t N, int32_t M, int32_t K, int32_t need_dw, int32_t need_db) {
+  if ((dtype != MDG_F32 && dtype != MDG_BF16) || N <= 0 || M <= 0 || K <= 0) return 0;
+  return mdg::wgrad_ws_bytes(dtype, N, M, K, need_dw != 0, need_db != 0);
+}
+
+int mdg_wgrad(int32_t dtype, int32_t N, int32_t M, int32_t K, const void* dy, int32_t ldy, const void* x, int32_t ldx,
+              float* dw, int32_t lddw, float* db, void* ws, size_t ws_bytes, void* stream) {
+  if (dtype != MDG_F32 && dtype != MDG_BF16) return fail(MDG_E_DTYPE, "wgrad: dtype %d", dtype);
+  if (!dy || (dw && !x) || (!dw && !db)) return fail(MDG_E_ARG, "wgrad: null dy / x / outputs");
+  if (N <= 0 || M < 8 || K < 8 || M % 8 || K % 8 || ldy < M || ldy % 8 || (dw && (ldx < K || ldx % 8 || lddw < K)))
+    return fail(MDG_E_SHAPE, "wgrad: N=%d M=%d K=%d ldy=%d ldx=%d lddw=%d (M, K, ld multiples of 8)", N, M, K, ldy, ldx,
+                lddw);
+  if (dtype == MDG_BF16 && N % 32) return fail(MDG_E_SHAPE, "wgrad bf16: N=%d not a multiple of 32 (pad with zero rows)", N);
+  if (!aligned16(dy) || (dw && !aligned16(x))) return fail(MDG_E_SHAPE, "wgrad: operands must be 16-B aligned");
+  const size_t need = mdg::wgrad_ws_bytes(dtype, N, M, K, dw != nullptr, db != nullptr);
+  if (!ws || ws_bytes < need) return fail(MDG_E_ARG, "wgrad: workspace %zu < %zu bytes", ws_bytes, need);
+  return hip_check(mdg::wgrad_launch(dtype, N, M, K, dy, ldy, x, ldx, dw, lddw, db, (float*)ws, (hipStream_t)stream),
+                   "wgrad");
 }
 
 }  // extern "C"

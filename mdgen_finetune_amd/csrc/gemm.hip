@@ -2292,8 +2292,15 @@ __device__ __forceinline__ void quad_pv6(float* o, const float* v, float p0, flo
 }
 
 
+// diagnostics of the lane-offset graph divergence (tools/gpu_lane_race.sh): 1 = agent-scope
+// acquire fence at kernel start, 2 = the DPP products through the compiler's quad_bc instead
+// of the inline v_fmac_f32_dpp blocks.  Never set in the product build.
+#ifndef MDG_DIAG_SPA
+#define MDG_DIAG_SPA 0
+#endif
 template <int S>  // ring depth (K-steps)
 __global__ __launch_bounds__(kSpaThreads) void gemm_qkv_attn_spatial_kernel(const mdg_gemm_desc p) {
+  if (MDG_DIAG_SPA == 1) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   constexpr int D = 24, HP = 2, BM = 128, BN = kSpaBN, BK = 32, NF = BN / 16, HD = HP * D;
   constexpr int ATILE = BM * BK, STAGE = (BM + BN) * BK, LDS_ST = kSpaLdsSt;
   typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -2305,7 +2312,7 @@ __global__ __launch_bounds__(kSpaThreads) void gemm_qkv_attn_spatial_kernel(cons
   const int M = p.M, K = p.K, C = p.H * D;
   const int n_tiles = p.H / HP, m_tiles = (M + BM - 1) / BM, nwg = n_tiles * m_tiles;
   const int xcd = blockIdx.x & 7, loc = blockIdx.x >> 3, q8 = nwg >> 3, r8 = nwg & 7;
-  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+  const int wg = p.ln_eps < 0.f ? (int)blockIdx.x : (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
   const int mt = wg / n_tiles, pair = wg - mt * n_tiles;
   const int m0 = mt * BM;
   // tile column r -> packed weight row: segment r / 48 (q, k, v), head pair `pair`
@@ -2429,8 +2436,16 @@ __global__ __launch_bounds__(kSpaThreads) void gemm_qkv_attn_spatial_kernel(cons
     float sb = 0.f, s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
 #pragma unroll
     for (int c = 0; c < 12; ++c) sb += q[c] * kbh[c0 + c];
-    quad_dots6(q, k, s0, s1, s2, s3);
-    quad_dots6(q + 6, k + 6, s0, s1, s2, s3);
+    if (MDG_DIAG_SPA == 2) {
+#pragma unroll
+      for (int c = 0; c < 12; ++c) {
+        s0 = fmaf(quad_bc<0>(k[c]), q[c], s0); s1 = fmaf(quad_bc<1>(k[c]), q[c], s1);
+        s2 = fmaf(quad_bc<2>(k[c]), q[c], s2); s3 = fmaf(quad_bc<3>(k[c]), q[c], s3);
+      }
+    } else {
+      quad_dots6(q, k, s0, s1, s2, s3);
+      quad_dots6(q + 6, k + 6, s0, s1, s2, s3);
+    }
     sb += __shfl_xor(sb, 4, 64); s0 += __shfl_xor(s0, 4, 64); s1 += __shfl_xor(s1, 4, 64);
     s2 += __shfl_xor(s2, 4, 64); s3 += __shfl_xor(s3, 4, 64);
     const float v0 = quad_bc<0>(kvalid), v1 = quad_bc<1>(kvalid), v2 = quad_bc<2>(kvalid), v3 = quad_bc<3>(kvalid);
@@ -2446,8 +2461,16 @@ __global__ __launch_bounds__(kSpaThreads) void gemm_qkv_attn_spatial_kernel(cons
     float o[12];
 #pragma unroll
     for (int c = 0; c < 12; ++c) o[c] = pb * kbh[MDG_DP + c0 + c];
-    quad_pv6(o, v, p0, p1, p2, p3);
-    quad_pv6(o + 6, v + 6, p0, p1, p2, p3);
+    if (MDG_DIAG_SPA == 2) {
+#pragma unroll
+      for (int c = 0; c < 12; ++c) {
+        o[c] = fmaf(quad_bc<0>(v[c]), p0, o[c]); o[c] = fmaf(quad_bc<1>(v[c]), p1, o[c]);
+        o[c] = fmaf(quad_bc<2>(v[c]), p2, o[c]); o[c] = fmaf(quad_bc<3>(v[c]), p3, o[c]);
+      }
+    } else {
+      quad_pv6(o, v, p0, p1, p2, p3);
+      quad_pv6(o + 6, v + 6, p0, p1, p2, p3);
+    }
 #pragma unroll
     for (int c = 0; c < 12; ++c) o[c] *= inv;
     if (m < M) {
@@ -2470,7 +2493,14 @@ static int spa_stages() {
   return st;
 }
 
-static hipError_t launch_spatial(const mdg_gemm_desc& p, hipStream_t s) {
+static hipError_t launch_spatial(const mdg_gemm_desc& p0, hipStream_t s) {
+  // MDG_SPA_XCD=0: plain block order (diagnostic; carried in the unused ln_eps field)
+  static const bool xcd_map = [] {
+    const char* e = getenv("MDG_SPA_XCD");
+    return !(e && e[0] == '0');
+  }();
+  mdg_gemm_desc p = p0;
+  p.ln_eps = xcd_map ? 0.f : -1.f;
   const int nwg = (p.H / 2) * ((p.M + 127) / 128);
   switch (spa_stages()) {
     case 2: hipLaunchKernelGGL((gemm_qkv_attn_spatial_kernel<2>), dim3(nwg), dim3(kSpaThreads), spa_smem(2), s, p); break;

@@ -1,0 +1,314 @@
+// Weight and bias gradients of the block's linear layers (the backward of nn.Linear inside
+// LatentMDGenLayer, latent_model.py:456-493 under loss.backward(), transport.py:137-222):
+//     dW[m][k] = sum_n dY[n][m] X[n][k]        db[m] = sum_n dY[n][m]
+// over the N token rows.  Both operands are token-major ([N][features], as the forward saved
+// them and the backward produced them), so the reduction runs along the SLOW axis of both.
+//
+// bf16 (the training default): one block = a 128 x 128 tile of dW and one chunk of tokens
+// (split over gridDim.z; each split writes an fp32 partial, mdg_wgrad sums the partials in
+// split order, so the result is deterministic).  Per K-step of 32 tokens the block stages a
+// [32 tokens][128 features] image of each operand through a 3-slot global_load_lds ring
+// (256-B rows, 16-B chunk c of row r at c ^ (((r&3)<<2) | ((r>>2)&3)), the XOR applied to the
+// per-lane SOURCE address since LDS-DMA writes lane-linearly) and every MFMA operand is read
+// TRANSPOSED out of it with ds_read_b64_tr_b16: lane 4q+p of a 16-lane group supplies row q
+// (a token), columns 4p..4p+3; lane i receives column i of the 4 rows — the token axis lands
+// in the registers, which is the k axis of v_mfma_f32_32x32x16_bf16 for BOTH operands (the k
+// order inside a step is the same permutation for A and B, so the sum is unchanged).
+// 4 waves, each a 64 x 64 quarter (2 x 2 tiles of 32 x 32, 64 accumulator VGPRs).
+//
+// fp32 (the parity path): a plain 64 x 64 LDS-tiled FMA kernel, same split / reduce.
+#include "common.h"
+
+namespace mdg {
+
+namespace {
+
+constexpr int kWgThreads = 256, kWgTile = 128, kWgBK = 32, kWgStages = 3;
+constexpr int kWgImg = kWgBK * kWgTile;  // bf16 elements of one operand image
+constexpr int kWgSlot = 2 * kWgImg;      // dY image + X image
+
+__device__ __forceinline__ int wg_swz(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
+// element offset of (token row r, feature column c) in an image
+__device__ __forceinline__ int wg_off(int r, int c) { return r * kWgTile + (((c >> 3) ^ wg_swz(r)) << 3) + (c & 7); }
+
+struct WgArgs {
+  const void* dy;
+  const void* x;
+  float* part;  // [S][M][K] fp32 (S == 1 with direct = true: dW itself)
+  int N, M, K, ldy, ldx, ldp, chunk;
+};
+
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+__device__ __forceinline__ void wg_vm_wait(int n) {
+  if (n >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// The 8-token A or B operand of one 32 x 32 x 16 MFMA: features cbase + (lane & 31), the
+// k-step's tokens {16 s2 + 4h + q} and {16 s2 + 8 + 4h + q} (h = lane >> 5, q = 0..3).
+__device__ __forceinline__ bf16x8 wg_frag(const bf16_t* img, int cbase, int s2, int lane) {
+  const int h = lane >> 5, gi = lane & 15;
+  const int col = cbase + 16 * ((lane >> 4) & 1) + 4 * (gi & 3);
+  const int row = 16 * s2 + 4 * h + (gi >> 2);
+  const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(img + wg_off(row, col)));
+  const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(img + wg_off(row + 8, col)));
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    r[j] = lo[j];
+    r[4 + j] = hi[j];
+  }
+  return r;
+}
+
+__global__ __launch_bounds__(kWgThreads, 2) void wgrad_bf16_kernel(const WgArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  bf16_t* ring = reinterpret_cast<bf16_t*>(smem);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int m0 = blockIdx.x * kWgTile, k0 = blockIdx.y * kWgTile, z = blockIdx.z;
+  const int nbeg = z * a.chunk;
+  const int nsteps = (min(a.N, nbeg + a.chunk) - nbeg) / kWgBK;
+  const bf16_t* DY = reinterpret_cast<const bf16_t*>(a.dy);
+  const bf16_t* X = reinterpret_cast<const bf16_t*>(a.x);
+  // loader: piece j (0..3) of wave w = image j >> 1, token rows 4 (2w + (j & 1)) + lane / 16,
+  // chunk position lane & 15 holding logical chunk (lane & 15) ^ swz(row); columns past the
+  // matrix edge are clamped into it (they only feed dW entries that are never stored)
+  const int r_lo = lane >> 4, cpos = lane & 15;
+  size_t src[4];
+  int dst[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int img = j >> 1, rb = 4 * (2 * wave + (j & 1)), r = rb + r_lo;
+    const int lim = img ? a.K : a.M;
+    const int col = min((img ? k0 : m0) + 8 * (cpos ^ wg_swz(r)), lim - 8);
+    src[j] = (size_t)(nbeg + r) * (img ? a.ldx : a.ldy) + col;
+    dst[j] = img * kWgImg + rb * kWgTile;
+  }
+  auto issue = [&](int s) {
+    bf16_t* sl = ring + (s % kWgStages) * kWgSlot;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const bf16_t* base = (j >> 1) ? X : DY;
+      const size_t step = (size_t)s * kWgBK * ((j >> 1) ? a.ldx : a.ldy);
+      __builtin_amdgcn_global_load_lds((const void*)(base + src[j] + step), (lds_ptr_t)(sl + dst[j]), 16, 0, 0);
+    }
+  };
+  const int wm = wave >> 1, wk = wave & 1;
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[t][u][i] = 0.f;
+
+  for (int s0 = 0; s0 < kWgStages - 1; ++s0)
+    if (s0 < nsteps) issue(s0);
+  for (int s = 0; s < nsteps; ++s) {
+    // step s landed (step s+1's pieces stay in flight); every wave's reads of step s-1 are
+    // retired (lgkmcnt) before the barrier, so the slot can be refilled with step s+2
+    wg_vm_wait(s + 1 < nsteps ? 4 : 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (s + kWgStages - 1 < nsteps) issue(s + kWgStages - 1);
+    const bf16_t* A = ring + (s % kWgStages) * kWgSlot;
+    const bf16_t* B = A + kWgImg;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      bf16x8 af[2], bfr[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) af[t] = wg_frag(A, 64 * wm + 32 * t, s2, lane);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) bfr[u] = wg_frag(B, 64 * wk + 32 * u, s2, lane);
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[t], bfr[u], acc[t][u], 0, 0, 0);
+    }
+  }
+  // D[m][k]: k = lane & 31, m = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
+  float* P = a.part + (size_t)z * a.M * a.ldp;
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int k = k0 + 64 * wk + 32 * u + (lane & 31);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + 64 * wm + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (m < a.M && k < a.K) P[(size_t)m * a.ldp + k] = acc[t][u][r];
+      }
+    }
+}
+
+// fp32 parity path: 64 x 64 tile, 16 tokens per LDS step, 4 x 4 outputs per thread.
+__global__ __launch_bounds__(256) void wgrad_f32_kernel(const WgArgs a) {
+  __shared__ float As[16][64], Bs[16][64];
+  const int tid = threadIdx.x, tm = tid >> 4, tk = tid & 15;
+  const int m0 = blockIdx.x * 64, k0 = blockIdx.y * 64, z = blockIdx.z;
+  const int nbeg = z * a.chunk, nend = min(a.N, nbeg + a.chunk);
+  const float* DY = reinterpret_cast<const float*>(a.dy);
+  const float* X = reinterpret_cast<const float*>(a.x);
+  float acc[4][4] = {};
+  for (int n = nbeg; n < nend; n += 16) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = tid + 256 * i, r = e >> 6, c = e & 63;
+      const bool ok = n + r < nend;
+      As[r][c] = (ok && m0 + c < a.M) ? DY[(size_t)(n + r) * a.ldy + m0 + c] : 0.f;
+      Bs[r][c] = (ok && k0 + c < a.K) ? X[(size_t)(n + r) * a.ldx + k0 + c] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      float av[4], bv[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) av[i] = As[r][tm + 16 * i];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bv[j] = Bs[r][tk + 16 * j];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(av[i], bv[j], acc[i][j]);
+    }
+    __syncthreads();
+  }
+  float* P = a.part + (size_t)z * a.M * a.ldp;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int m = m0 + tm + 16 * i, k = k0 + tk + 16 * j;
+      if (m < a.M && k < a.K) P[(size_t)m * a.ldp + k] = acc[i][j];
+    }
+}
+
+// Column sums of dY over a token chunk: thread = 8 consecutive columns (one 16-B bf16 load /
+// two float4), 4 waves over interleaved rows, reduced through LDS -> part[z][M].
+template <typename CT>
+__global__ __launch_bounds__(256) void colsum_kernel(const CT* __restrict__ dy, int N, int M, int ldy, int chunk,
+                                                     float* __restrict__ part) {
+  __shared__ float red[4][64 * 8];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c0 = (blockIdx.x * 64 + lane) * 8, z = blockIdx.y;
+  const int nbeg = z * chunk, nend = min(N, nbeg + chunk);
+  float s[8] = {};
+  if (c0 < M) {
+    for (int n = nbeg + wave; n < nend; n += 4) {
+      const CT* p = dy + (size_t)n * ldy + c0;
+      if constexpr (is_bf16<CT>()) {
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(p);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s[j] += (float)v[j];
+      } else {
+        const float4 v0 = reinterpret_cast<const float4*>(p)[0], v1 = reinterpret_cast<const float4*>(p)[1];
+        s[0] += v0.x; s[1] += v0.y; s[2] += v0.z; s[3] += v0.w;
+        s[4] += v1.x; s[5] += v1.y; s[6] += v1.z; s[7] += v1.w;
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[wave][lane * 8 + j] = s[j];
+  __syncthreads();
+  for (int e = threadIdx.x; e < 64 * 8; e += 256) {
+    const int c = blockIdx.x * 512 + e;
+    if (c < M) part[(size_t)z * M + c] = ((red[0][e] + red[1][e]) + red[2][e]) + red[3][e];
+  }
+}
+
+// out[m][k] (ld ldo) = sum over z in order of part[z][m][k] (ld ldp)
+__global__ __launch_bounds__(256) void split_sum_kernel(const float* __restrict__ part, int S, int M, int K, int ldp,
+                                                        float* __restrict__ out, int ldo) {
+  const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (long long)M * K) return;
+  const int m = (int)(e / K), k = (int)(e % K);
+  const size_t zs = (size_t)M * ldp;
+  const float* p = part + (size_t)m * ldp + k;
+  float s = p[0];
+  for (int z = 1; z < S; ++z) s += p[z * zs];
+  out[(size_t)m * ldo + k] = s;
+}
+
+}  // namespace
+
+// Split plan shared by the workspace query and the launch.
+struct WgPlan {
+  int S, chunk, cs_S, cs_chunk;
+  size_t part_elems, cs_elems;
+};
+
+WgPlan wgrad_plan(int dtype, int N, int M, int K, bool need_w, bool need_b) {
+  WgPlan p{};
+  const int tile = dtype == MDG_BF16 ? kWgTile : 64;
+  const int tiles = ((M + tile - 1) / tile) * ((K + tile - 1) / tile);
+  const int quantum = dtype == MDG_BF16 ? kWgBK : 16;
+  const int nq = (N + quantum - 1) / quantum;
+  // ~2 blocks per CU over the 256 CUs, each split at least 8 K-steps long
+  int S = need_w ? (512 + tiles - 1) / tiles : 1;
+  S = max(1, min(S, nq / 8));
+  p.chunk = ((nq + S - 1) / S) * quantum;
+  p.S = (N + p.chunk - 1) / p.chunk;
+  p.part_elems = need_w ? (size_t)p.S * M * K : 0;
+  const int cblocks = (M + 511) / 512;
+  int cs = need_b ? max(1, min(256 / cblocks, N / 64)) : 0;
+  p.cs_chunk = need_b ? (N + cs - 1) / cs : 0;
+  p.cs_S = need_b ? (N + p.cs_chunk - 1) / p.cs_chunk : 0;
+  p.cs_elems = need_b ? (size_t)p.cs_S * M : 0;
+  return p;
+}
+
+hipError_t wgrad_launch(int dtype, int N, int M, int K, const void* dy, int ldy, const void* x, int ldx, float* dw,
+                        int lddw, float* db, float* ws, hipStream_t s) {
+  const WgPlan p = wgrad_plan(dtype, N, M, K, dw != nullptr, db != nullptr);
+  if (dw) {
+    WgArgs a;
+    a.dy = dy; a.x = x; a.N = N; a.M = M; a.K = K; a.ldy = ldy; a.ldx = ldx; a.chunk = p.chunk;
+    const bool direct = p.S == 1;
+    a.part = direct ? dw : ws;
+    a.ldp = direct ? lddw : K;
+    if (dtype == MDG_BF16) {
+      static bool attr = false;
+      if (!attr) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_bf16_kernel),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, kWgStages * kWgSlot * 2);
+        if (e != hipSuccess) return e;
+        attr = true;
+      }
+      hipLaunchKernelGGL(wgrad_bf16_kernel, dim3((M + 127) / 128, (K + 127) / 128, p.S), dim3(kWgThreads),
+                         kWgStages * kWgSlot * 2, s, a);
+    } else {
+      hipLaunchKernelGGL(wgrad_f32_kernel, dim3((M + 63) / 64, (K + 63) / 64, p.S), dim3(256), 0, s, a);
+    }
+    if (hipError_t e = hipGetLastError()) return e;
+    if (!direct) {
+      const long long n = (long long)M * K;
+      hipLaunchKernelGGL(split_sum_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, (const float*)ws, p.S, M,
+                         K, K, dw, lddw);
+      if (hipError_t e = hipGetLastError()) return e;
+    }
+  }
+  if (db) {
+    float* cp = ws + (p.S > 1 ? p.part_elems : 0);
+    const dim3 grid((M + 511) / 512, p.cs_S);
+    if (dtype == MDG_BF16)
+      hipLaunchKernelGGL(colsum_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)dy, N, M, ldy, p.cs_chunk, cp);
+    else
+      hipLaunchKernelGGL(colsum_kernel<float>, grid, dim3(256), 0, s, (const float*)dy, N, M, ldy, p.cs_chunk, cp);
+    if (hipError_t e = hipGetLastError()) return e;
+    hipLaunchKernelGGL(split_sum_kernel, dim3((M + 255) / 256), dim3(256), 0, s, (const float*)cp, p.cs_S, 1, M, M, db,
+                       M);
+    if (hipError_t e = hipGetLastError()) return e;
+  }
+  return hipSuccess;
+}
+
+size_t wgrad_ws_bytes(int dtype, int N, int M, int K, bool need_w, bool need_b) {
+  const WgPlan p = wgrad_plan(dtype, N, M, K, need_w, need_b);
+  return ((p.S > 1 ? p.part_elems : 0) + p.cs_elems) * sizeof(float) + 256;
+}
+
+}  // namespace mdg

@@ -76,7 +76,10 @@ class HipEngine:
 
     # ------------------------------------------------------------------ packing
     def _param_key(self):
-        return tuple((p.data_ptr(), p._version) for p in self.model.parameters())
+        # _weights_gen: bumped by updates that bypass autograd's version counters (the graphed
+        # training step's Adam runs inside a hipGraph replay: train.GraphedStep.run)
+        return (getattr(self.model, "_weights_gen", 0),) + tuple(
+            (p.data_ptr(), p._version) for p in self.model.parameters())
 
     def _pack(self):
         key = self._param_key()
@@ -263,10 +266,18 @@ class HipEngine:
         if nbytes == 0:
             _lib.check(1001, f"workspace for B={B} T={T} L={L}")
         st.ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-        if os.environ.get("MDG_POISON_WS") == "1":  # debugging: NaN bytes expose reads of unwritten memory
-            st.ws.fill_(0xFF)
         _lib.check(lib.mdg_workspace_init(ctypes.byref(st.dims), st.ws.data_ptr(), _lib.stream_handle()),
                    "mdg_workspace_init")
+        if os.environ.get("MDG_POISON_WS") == "1":
+            # debugging: NaN bytes (0xFF) in every region the step must write before reading it,
+            # applied AFTER mdg_workspace_init (which zeroes the workspace and sets the padded
+            # planes' 1.0 columns): q|k|v (spatial), o, hidden, xn, key-padding biases, the split
+            # partials, and the temporal planes when they are packed (no init-time pad column)
+            off = _lib.workspace_offsets(st.dims)
+            st.ws[off["qkv_s"]:off["qkv_t"]].fill_(0xFF)
+            st.ws[off["o"]:].fill_(0xFF)
+            if self.describe_plan_dims(st.dims).get("planes", "").startswith("packed"):
+                st.ws[off["qkv_t"]:off["o"]].fill_(0xFF)
         st.h = torch.empty(st.N, self.C, device=dev)
         st.base = torch.empty(st.N, self.C, device=dev)
         if os.environ.get("MDG_POISON_WS") == "1":
@@ -301,11 +312,13 @@ class HipEngine:
 
     def describe_plan(self, B, T, L):
         """The kernel route mdg_denoise_step takes for (B, T, L) at this dtype (mdg_describe_plan)."""
+        return self.describe_plan_dims(self._state(B, T, L).dims)
+
+    def describe_plan_dims(self, dims):
         import json
 
-        st = self._state(B, T, L)
         buf = ctypes.create_string_buffer(1024)
-        _lib.check(self.lib.mdg_describe_plan(ctypes.byref(st.dims), buf, 1024), "mdg_describe_plan")
+        _lib.check(self.lib.mdg_describe_plan(ctypes.byref(dims), buf, 1024), "mdg_describe_plan")
         return json.loads(buf.value.decode())
 
     # ------------------------------------------------------------------ conditioning
@@ -338,10 +351,13 @@ class HipEngine:
         return mods, mods_f, ipa
 
     def _prepare_tps(self, rots, trans, erots, etrans):
-        """TPS relative 7-vectors: None = computed on the device inside mdg_precompute_cond
-        (quaternion sign w >= 0).  ``rel7_override`` (tests: the reference's own vectors, whose
-        eigenvector sign LAPACK chose) or MDG_TPS_REL7=host (the reference's host arithmetic,
-        rot_to_quat by CPU eigh) instead stage a [2][B][L][7] tensor outside any graph."""
+        """TPS relative 7-vectors, staged as a [2][B][L][7] tensor outside any graph.  Default:
+        the reference's host arithmetic (relative_tensor7: rot_to_quat by CPU eigh, whose
+        eigenvector sign is LAPACK's), the same function the training path and the eager torch
+        backend use, so sampling conditions exactly as training did.  ``rel7_override`` (tests:
+        the reference's own vectors) replaces it; MDG_TPS_REL7=device computes them inside
+        mdg_precompute_cond instead (no host round trip; quaternion sign fixed to w >= 0, a
+        documented deviation from the reference's arbitrary sign)."""
         from .model.latent_model import relative_tensor7
 
         self._rel7 = None
@@ -350,7 +366,7 @@ class HipEngine:
         ov = getattr(self, "rel7_override", None)
         if ov is not None:
             self._rel7 = torch.stack([t.to(rots.device, torch.float32) for t in ov]).contiguous()
-        elif os.environ.get("MDG_TPS_REL7") == "host":
+        elif os.environ.get("MDG_TPS_REL7") != "device":
             self._rel7 = torch.stack([relative_tensor7(rots, trans, erots, etrans),
                                       relative_tensor7(erots, etrans, rots, trans)]).contiguous()
 
@@ -515,7 +531,16 @@ class HipEngine:
                     vs.graph = g
             return vs.v.clone()
 
+        def f_capturable(t, y):
+            """The same evaluation as device work only (no replay, no host read of t): for a
+            caller that captures several evaluations into its own graph (the graphed dopri5)."""
+            vs.x.copy_(y)
+            vs.t.copy_(t.to(torch.float32).reshape(1, 1).expand(1, B))
+            program()
+            return vs.v.clone()
+
         f.state = vs
+        f.capturable = f_capturable
         return f
 
     def _copy_opt(self, gs, name, val):

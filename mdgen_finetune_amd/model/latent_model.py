@@ -41,6 +41,26 @@ def get_1d_sincos_pos_embed_from_grid(embed_dim, pos):
     return np.concatenate([np.sin(out), np.cos(out)], axis=1)
 
 
+class _SmallTableEmbedding(torch.autograd.Function):
+    """weight[idx] for a table of a few rows (mask_to_emb: 2 rows, indexed per token).  The
+    forward is the plain gather; the backward is one [E, N] x [N, C] GEMM of the one-hot
+    indices, instead of autograd's sort-based embedding_dense_backward (0.5 ms per call over
+    the 32 000 tokens of a training step on MI355X)."""
+
+    @staticmethod
+    def forward(ctx, weight, idx):
+        ctx.save_for_backward(idx)
+        ctx.E = weight.shape[0]
+        return weight[idx]
+
+    @staticmethod
+    def backward(ctx, g):
+        (idx,) = ctx.saved_tensors
+        g2 = g.reshape(-1, g.shape[-1])
+        onehot = F.one_hot(idx.reshape(-1), ctx.E).to(g2.dtype)
+        return onehot.t() @ g2, None
+
+
 UNSUPPORTED_FLAGS = ("design", "mpnn", "dynamic_mpnn", "hyena", "interleave_ipa", "inpainting")
 
 
@@ -245,7 +265,9 @@ class LatentMDGenModel(nn.Module):
         if getattr(self.args, "abs_time_emb", False):
             h = h + self.time_embed[:, :, None]
         if x_cond is not None:
-            h = h + self.cond_to_emb(x_cond) + self.mask_to_emb(x_cond_mask)
+            emb = (_SmallTableEmbedding.apply(self.mask_to_emb.weight, x_cond_mask) if torch.is_grad_enabled()
+                   else self.mask_to_emb(x_cond_mask))
+            h = h + self.cond_to_emb(x_cond) + emb
         c = self.embed_time(t)[:, None]
         if self.args.prepend_ipa:
             h = h + self.run_ipa(c[:, 0], mask[:, 0], start_frames, end_frames, aatype)[:, None]
@@ -253,8 +275,14 @@ class LatentMDGenModel(nn.Module):
         if hip_layers:
             from ..train_hip import hip_layer_forward
             hl = self._train_helper()
+        ckpt = bool(getattr(self.args, "grad_checkpointing", False)) and self.training
         for layer in self.layers:
-            if hip_layers:  # block forward + backward in libmdgen_hip.so (train_hip.py)
+            if hip_layers and ckpt:  # --grad_checkpointing: the HIP Function re-runs in backward
+                # (reentrant form: the first forward runs without autograd, so the Function's
+                # saved activations of every layer but the one being differentiated are freed)
+                h = torch.utils.checkpoint.checkpoint(hip_layer_forward, hl, layer, h,
+                                                      layer.adaLN_modulation(c[:, 0]), mask, use_reentrant=True)
+            elif hip_layers:  # block forward + backward in libmdgen_hip.so (train_hip.py)
                 h = hip_layer_forward(hl, layer, h, layer.adaLN_modulation(c[:, 0]), mask)
             elif getattr(self.args, "grad_checkpointing", False) and self.training:
                 h = torch.utils.checkpoint.checkpoint(layer, h, c, mask, use_reentrant=False)
@@ -294,8 +322,10 @@ def relative_tensor7(rots_a, trans_a, rots_b, trans_b):
 
     The quaternion comes from an eigenvector (rot_to_quat, rigid_utils.py:191-210) whose sign
     flips under 1-ulp changes of the composed rotation for a sizeable fraction of residues, and
-    latent_to_emb_f/_r are linear in it — so this x-independent, once-per-window precompute must
-    reproduce the reference's arithmetic bit for bit; it is not done on the device."""
+    latent_to_emb_f/_r are linear in it — so this x-independent, once-per-window precompute
+    reproduces the reference's host arithmetic (CPU eigh).  The HIP engine uses this same
+    function by default (engine._prepare_tps), so training and sampling condition alike; its
+    device alternative (MDG_TPS_REL7=device, mdg_tps_rel7) fixes the sign to w >= 0 instead."""
     dev = rots_a.device
     ra, ta, rb, tb = (z.detach().float().cpu() for z in (rots_a, trans_a, rots_b, trans_b))
     ra_inv = ra.transpose(-1, -2)

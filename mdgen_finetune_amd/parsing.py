@@ -61,6 +61,9 @@ _EXTRA = [
                                  "libmdgen_hip.so (train_hip.py); 'torch': eager autograd"),
     ("hip_dtype", _S, "bf16", "operand type of the HIP GEMM / attention kernels: 'bf16' (fp32 accumulate, "
                               "the reference's matmul precision 'medium') or 'f32' (exact fp32)"),
+    ("train_graph", _I, 1, "1: on a ROCm device the optimizer step replays hipGraphs (forward + loss + "
+                           "backward [+ RCCL gradient all-reduce between two graphs] + clip + Adam + EMA); "
+                           "0: eager step (also used for grad accumulation > 1 and 16-mixed)"),
 ]
 
 _REQUIRED = ("train_split", "val_split", "data_dir")

@@ -64,17 +64,21 @@ def get_log_mean(log):
 
 
 def setup_distributed():
-    """Rank/world from the torch.distributed.run environment; RCCL on GPUs, gloo on CPU."""
+    """Rank/world from the torch.distributed.run environment; RCCL on GPUs, gloo on CPU.
+    MDG_SHARE_GPU=1 puts every rank on cuda:0 with gloo (rehearsing N ranks on a one-GPU box:
+    RCCL refuses two ranks on one device)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     use_cuda = torch.cuda.is_available()
-    device = torch.device("cuda", local) if use_cuda else torch.device("cpu")
+    share = os.environ.get("MDG_SHARE_GPU") == "1"
+    device = torch.device("cuda", 0 if share else local) if use_cuda else torch.device("cpu")
     if use_cuda:
         torch.cuda.set_device(device)
     if world > 1 and not dist.is_initialized():
-        dist.init_process_group("nccl" if use_cuda else "gloo", rank=rank, world_size=world,
-                                **({"device_id": device} if use_cuda else {}))
+        nccl = use_cuda and not share
+        dist.init_process_group("nccl" if nccl else "gloo", rank=rank, world_size=world,
+                                **({"device_id": device} if nccl else {}))
     return rank, world, device
 
 
@@ -91,14 +95,19 @@ class Trainer:
         else:
             m.backend = "torch"
         torch.manual_seed(args.seed + 1 + 1000 * rank)  # independent (t, x0) draws per rank
-        self.model = self.wrapper.model
-        if world > 1:
-            self.model = DDP(self.wrapper.model, device_ids=[self.device.index] if self.device.type == "cuda" else None,
-                             bucket_cap_mb=args.bucket_cap_mb, gradient_as_bucket_view=True, static_graph=True)
-        self.optimizer = self.wrapper.configure_optimizers()
-        self.epoch, self.global_step, self.skip_batches = 0, 0, 0
         self.precision = resolve_precision(args.precision, self.device)
         self.scaler = torch.amp.GradScaler(self.device.type) if self.precision == torch.float16 else None
+        # the graphed step (GraphedStep): ROCm device, HIP block stack, one micro-batch per step,
+        # no loss scaler; gradients averaged by this class's flat all-reduce instead of DDP
+        self.graph_mode = bool(self.device.type == "cuda" and int(getattr(args, "train_graph", 0))
+                               and m.backend == "hip" and self.scaler is None and max(1, args.accumulate_grad) == 1)
+        self._graphed = None
+        self.model = self.wrapper.model
+        if world > 1 and not self.graph_mode:
+            self.model = DDP(self.wrapper.model, device_ids=[self.device.index] if self.device.type == "cuda" else None,
+                             bucket_cap_mb=args.bucket_cap_mb, gradient_as_bucket_view=True, static_graph=True)
+        self.optimizer = self.wrapper.configure_optimizers(capturable=self.graph_mode)
+        self.epoch, self.global_step, self.skip_batches = 0, 0, 0
         if dataset is None:
             if not args.synthetic:
                 raise NotImplementedError("only --synthetic data is available offline (the reference's "
@@ -114,10 +123,13 @@ class Trainer:
 
     # ------------------------------------------------------------------ checkpoint
     def resume(self, path):
+        self._graphed = None  # static buffers / captured optimizer state are re-made from the restored state
         ck = load_checkpoint(path, map_location=self.device)
         self.wrapper.model.load_state_dict(model_state_dict(ck))
         if ck.get("optimizer_states"):
             self.optimizer.load_state_dict(ck["optimizer_states"][0])
+        if self.scaler is not None and ck.get("MixedPrecision"):  # the loss-scale state (16-mixed)
+            self.scaler.load_state_dict(ck["MixedPrecision"])
         if self.wrapper.ema is not None and "ema" in ck:
             self.wrapper.ema.load_state_dict(ck["ema"])
             self.wrapper.ema.to(self.device)
@@ -133,17 +145,48 @@ class Trainer:
             return None
         path = os.path.join(self.args.model_dir, f"epoch={self.epoch}-step={self.global_step}.ckpt")
         save_checkpoint(path, self.wrapper, self.optimizer, self.epoch, self.global_step,
-                        epoch_complete=epoch_complete, batches_done=batches_done)
+                        epoch_complete=epoch_complete, batches_done=batches_done,
+                        grad_scaler=self.scaler.state_dict() if self.scaler is not None else None)
         return path
 
     # ------------------------------------------------------------------ one optimizer step
     def _to_device(self, batch):
         return {k: (v.to(self.device, non_blocking=True) if torch.is_tensor(v) else v) for k, v in batch.items()}
 
-    @torch.enable_grad()
-    def step(self, micro_batches):
+    def step(self, micro_batches, log=True):
         """One optimizer step over ``len(micro_batches)`` accumulated micro-batches; returns the
-        mean loss (rank-local) and the global grad norm before clipping."""
+        mean loss (rank-local) and the global grad norm before clipping.  In graph mode the step
+        is a replay of GraphedStep's graphs with the batch copied into its static buffers."""
+        if self.graph_mode and len(micro_batches) == 1:
+            if self._graphed is None:
+                self._graphed = GraphedStep(self, micro_batches[0])
+            loss, gnorm = self._graphed.run(micro_batches[0], log=log)
+            self.global_step += 1
+            return loss, gnorm
+        return self._eager_step(micro_batches, log=log)
+
+    def allreduce_grads(self, flat=None):
+        """Average the gradients over ranks (graph mode; DDP does it in the eager mode): one
+        all-reduce of the flat fp32 buffer (RCCL over xGMI; gloo on CPU)."""
+        if self.world == 1:
+            return
+        params = [p for p in self.wrapper.model.parameters() if p.requires_grad]
+        own = flat is None
+        if own:
+            flat = torch.cat([(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1) for p in params])
+        dist.all_reduce(flat)
+        flat.div_(self.world)
+        if own:
+            off = 0
+            for p in params:
+                n = p.numel()
+                if p.grad is None:
+                    p.grad = torch.zeros_like(p)
+                p.grad.copy_(flat[off:off + n].view_as(p))
+                off += n
+
+    @torch.enable_grad()
+    def _eager_step(self, micro_batches, log=True, update=True):
         a = self.args
         n = len(micro_batches)
         self.wrapper.train()
@@ -156,10 +199,13 @@ class Trainer:
             ctx = self.model.no_sync() if (not sync and isinstance(self.model, DDP)) else _null()
             with ctx:
                 with autocast:
-                    loss = self.wrapper.general_step(batch, "train", model=self.model)
+                    out = self.wrapper.general_step(batch, "train", model=self.model, log=log)
+                loss = out if log else out[0]
                 scaled = loss / n
                 (self.scaler.scale(scaled) if self.scaler is not None else scaled).backward()
             losses.append(loss.detach())
+        if self.graph_mode:
+            self.allreduce_grads()
         if self.scaler is not None:
             self.scaler.unscale_(self.optimizer)
         gnorm = torch.nn.utils.clip_grad_norm_(self.wrapper.model.parameters(), a.grad_clip) if a.grad_clip else None
@@ -170,7 +216,8 @@ class Trainer:
             self.optimizer.step()
         self.wrapper.on_before_zero_grad()
         self.optimizer.zero_grad(set_to_none=True)
-        self.global_step += 1
+        if update:
+            self.global_step += 1
         return torch.stack(losses).mean(), gnorm
 
     def print_log(self, prefix="iter"):
@@ -214,6 +261,105 @@ class Trainer:
             if (self.epoch + 1) % a.ckpt_freq == 0:
                 self.save()
             self.epoch += 1
+
+
+class GraphedStep:
+    """The optimizer step as hipGraph replays (Trainer.graph_mode).
+
+    The eager step launches ~2 300 kernels from the host (the IPA / t-MLP / loss autograd, the
+    per-layer weight packing, the HIP layer kernels): 33 ms of CPU against ~25 ms of GPU work per
+    step on MI355X, so the device idles.  Here, after two warm-up steps on a side
+    stream (autograd buffers, optimizer / EMA state, RoPE tables; the parameters, optimizer
+    state and EMA are restored afterwards, so warm-up trains nothing), one capture records
+      world 1: prep_batch -> GVP loss -> backward -> grad clip -> Adam (capturable) -> EMA
+    and each step is: copy the batch into the static buffers, replay.  With world > 1 the step
+    is two graphs around an eager RCCL all-reduce of the flat gradient buffer (graph 1 ends by
+    packing the gradients into it; graph 2's clip / Adam read them through views of it):
+      graph 1: prep_batch -> loss -> backward -> cat(grads) | all_reduce(flat) / world |
+      graph 2: clip -> Adam -> EMA.
+    The (t, x0) draws come from the CUDA generator's graph-safe philox offsets, so every replay
+    draws fresh noise, as the eager step does."""
+
+    def __init__(self, tr, batch, warmup=2):
+        self.tr = tr
+        dev = tr.device
+        self.static = {k: (v.to(dev).clone() if torch.is_tensor(v) else v) for k, v in batch.items()}
+        self.params = [p for p in tr.wrapper.model.parameters() if p.requires_grad]
+        self.split = tr.world > 1
+        model = tr.wrapper.model
+        snap = [p.detach().clone() for p in model.parameters()]
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(warmup):
+                tr._eager_step([self.static], log=False, update=False)
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        with torch.no_grad():  # warm-up trains nothing: restore weights, optimizer state, EMA
+            for p, v in zip(model.parameters(), snap):
+                p.copy_(v)
+            for st in tr.optimizer.state.values():
+                for v in st.values():
+                    if torch.is_tensor(v):
+                        v.zero_()
+            if tr.wrapper.ema is not None:
+                for k, v in model.state_dict().items():
+                    tr.wrapper.ema.params[k].copy_(v)
+        tr.optimizer.zero_grad(set_to_none=True)
+        n = sum(p.numel() for p in self.params)
+        self.flat = torch.empty(n, device=dev) if self.split else None
+        self.g1 = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.g1):
+            self.loss, self.losses, self.t = self._fwd_bwd()
+            if self.split:
+                self.grads_g1 = [p.grad for p in self.params]  # graph-1 memory, kept referenced
+                torch.cat([g.reshape(-1) for g in self.grads_g1], out=self.flat)
+            else:
+                self.gnorm = self._update()
+        if self.split:
+            off = 0
+            for p in self.params:  # graph 2 reads the averaged gradients in place
+                p.grad = self.flat[off:off + p.numel()].view_as(p)
+                off += p.numel()
+            self.g2 = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.g2):
+                self.gnorm = self._update()
+
+    def _fwd_bwd(self):
+        tr = self.tr
+        tr.wrapper.train()
+        autocast = (torch.autocast("cuda", dtype=tr.precision) if tr.precision is not None
+                    else torch.autocast("cuda", enabled=False))
+        with torch.enable_grad():
+            with autocast:
+                loss, losses, t = tr.wrapper.general_step(self.static, "train", model=tr.wrapper.model, log=False)
+            loss.backward()
+        return loss.detach(), losses.detach(), t.detach()
+
+    def _update(self):
+        tr = self.tr
+        gnorm = torch.nn.utils.clip_grad_norm_(self.params, tr.args.grad_clip) if tr.args.grad_clip else None
+        tr.optimizer.step()
+        tr.wrapper.on_before_zero_grad()
+        return gnorm
+
+    def run(self, batch, log=True):
+        for k, v in batch.items():
+            if torch.is_tensor(v):
+                self.static[k].copy_(v, non_blocking=True)
+        self.g1.replay()
+        if self.split:
+            self.tr.allreduce_grads(self.flat)
+            self.g2.replay()
+        model = self.tr.wrapper.model  # the replayed Adam bumps no version counters: tell the engine
+        model._weights_gen = getattr(model, "_weights_gen", 0) + 1
+        if log:
+            w = self.tr.wrapper
+            w.stage = "train"
+            w.iter_step += 1
+            w.log("loss", self.losses)
+            w.log("time", self.t)
+        return self.loss, self.gnorm
 
 
 # Lightning precision strings the reference passes to pl.Trainer(precision=...) (train.py:52)

@@ -17,9 +17,10 @@ backward  per sublayer, top down:
                                 step); fc1's with the GELU-derivative epilogue (MDG_ACT_DGELU);
             mdg_attn_*_bwd      flash-style attention backward (P recomputed from the saved lse),
                                 RoPE / q-scale undone in the epilogue, bias_k / bias_v partials;
-            torch.bmm           the weight gradients dW = dY^T X (plain GEMMs, hipBLASLt, split
-                                over token chunks + a sum of fp32 partials) — the only
-                                library calls on the path.
+            mdg_wgrad           the weight and bias gradients dW = dY^T X, db = colsum(dY) from
+                                the token-major operands (MFMA tiles fed by transposing LDS
+                                reads, split over token chunks, fp32 partials summed in
+                                chunk order: deterministic; csrc/wgrad.hip).
 The adaLN modulation vectors enter as a [B, 9C] input of the Function, so the t-embedding /
 adaLN linears upstream stay ordinary autograd modules (x-independent, tiny).
 
@@ -40,32 +41,34 @@ from . import _lib
 _LN2 = math.log(2.0)
 
 
-def _mm_f32(a, b):
-    """a @ b with fp32 output (fp32 accumulate) for bf16 operands."""
-    if a.dtype == torch.float32:
-        return a @ b
-    try:
-        return torch.mm(a, b, out_dtype=torch.float32)
-    except (RuntimeError, TypeError):
-        return (a @ b).float()
+def pad_tokens(n):
+    """Token rows of every buffer the weight-gradient kernel reads: a multiple of 32 (its
+    bf16 K-step); the rows past n are zero."""
+    return (n + 31) // 32 * 32
 
 
-def _dw(dy, x):
-    """dW = dy^T x (fp32 result) over the N token rows.  With bf16 operands the reduction is
-    split into S token chunks (one batched GEMM, then a sum of the S fp32 partials): the output
-    is only [Nout][Kin] (e.g. 1536 x 384 = 48 tiles), so one GEMM over all N = 32 000 rows ran
-    on a fifth of the CUs (hipBLASLt picks no split-K here; 209 us for fc1's 37.7 GF)."""
-    n = dy.shape[0]
-    if dy.dtype != torch.float32:
-        for S in (16, 8, 4, 2):
-            if n % S == 0 and n // S >= 1024:
-                a = dy.view(S, n // S, dy.shape[1]).transpose(1, 2)
-                b = x.view(S, n // S, x.shape[1])
-                try:
-                    return torch.bmm(a, b, out_dtype=torch.float32).sum(0)
-                except (RuntimeError, TypeError, NotImplementedError):
-                    break
-    return _mm_f32(dy.t(), x)
+def _rows(n, cols, dtype, dev):
+    """[pad_tokens(n)][cols] buffer whose pad rows are zero (kernels write rows < n)."""
+    t = torch.empty(pad_tokens(n), cols, device=dev, dtype=dtype)
+    if t.shape[0] > n:
+        t[n:].zero_()
+    return t
+
+
+def wgrad(lib, mdg_dtype, dy, x, need_b=False):
+    """(dW = dy^T x, db = colsum(dy)) in fp32 through mdg_wgrad; dy [Np][M], x [Np][K] token
+    rows (pad rows zero), x None -> only db."""
+    n, M = dy.shape
+    K = x.shape[1] if x is not None else 8
+    need_w = x is not None
+    wsb = lib.mdg_wgrad_workspace_bytes(mdg_dtype, n, M, K, int(need_w), int(need_b))
+    ws = torch.empty(wsb, device=dy.device, dtype=torch.uint8)
+    dw = torch.empty(M, K, device=dy.device) if need_w else None
+    db = torch.empty(M, device=dy.device) if need_b else None
+    _lib.check(lib.mdg_wgrad(mdg_dtype, n, M, K, dy.data_ptr(), dy.stride(0), _lib.ptr(x),
+                             x.stride(0) if need_w else 0, _lib.ptr(dw), K, _lib.ptr(db), ws.data_ptr(), wsb,
+                             _lib.stream_handle()), "mdg_wgrad")
+    return dw, db
 
 
 class LayerHelper:
@@ -209,12 +212,13 @@ class _HipLayerFn(torch.autograd.Function):
         kb_s = torch.empty(B * T, L, device=dev)
         _lib.check(lib.mdg_mask_bias(B, T, L, mask.data_ptr(), kb_t.data_ptr(), kb_s.data_ptr(), s), "mdg_mask_bias")
         e = lambda *shape, dt=ct: torch.empty(*shape, device=dev, dtype=dt)  # noqa: E731
-        sv = {"xn": [e(N, C) for _ in range(3)], "stats": [e(N, 2, dt=torch.float32) for _ in range(3)],
+        r = lambda cols: _rows(N, cols, ct, dev)  # noqa: E731  (operands of the weight gradients)
+        sv = {"xn": [r(C) for _ in range(3)], "stats": [e(N, 2, dt=torch.float32) for _ in range(3)],
               "qkv_s": e(3, B * T, H, L, _lib.MDG_DP) if long_l else e(N, 3 * C),
               "lse_s": e(B * T, H, L, dt=torch.float32) if long_l else None,
               "qkv_t": e(3, B * L, H, T, _lib.MDG_DP), "lse_t": e(B * L, H, T, dt=torch.float32),
-              "o": [e(N, C), e(N, C)], "y": [e(N, C) for _ in range(3)],
-              "h1": e(N, C, dt=torch.float32), "h2": e(N, C, dt=torch.float32), "u": e(N, F), "act": e(N, F)}
+              "o": [r(C), r(C)], "y": [e(N, C) for _ in range(3)],
+              "h1": e(N, C, dt=torch.float32), "h2": e(N, C, dt=torch.float32), "u": e(N, F), "act": r(F)}
         cs = _lib.MdgLayerSaved()
         for i in range(3):
             cs.xn[i], cs.stats[i], cs.y[i] = sv["xn"][i].data_ptr(), sv["stats"][i].data_ptr(), sv["y"][i].data_ptr()
@@ -253,6 +257,8 @@ class _HipLayerFn(torch.autograd.Function):
         nblk = lib.mdg_ln_gate_bwd_blocks(TL)
         qscale = D ** -0.5
         e = lambda *shape, dtp=ct: torch.empty(*shape, device=dev, dtype=dtp)  # noqa: E731
+        r = lambda cols: _rows(N, cols, ct, dev)  # noqa: E731
+        wg = lambda dy, x, need_b=False: wgrad(lib, dt, dy, x, need_b)  # noqa: E731
 
         def lngate(dxn, h_ln, stats, shift_off, scale_off, dh_res, dh_out, y, gate_off, dy):
             part = torch.empty(B, nblk, 4, C, device=dev)
@@ -264,7 +270,7 @@ class _HipLayerFn(torch.autograd.Function):
 
         def dx_gemm(dy, w_t, K, Nout, act=_lib.MDG_ACT_NONE, aux=None):
             """out [N][Nout] (CT) = dy [N][K] . w_t^T with w_t = W^T [Nout][K]."""
-            out = e(N, Nout)
+            out = r(Nout)
             g = _lib.MdgGemmDesc()
             g.dtype, g.a_mode, g.epi, g.act = dt, _lib.MDG_A_PLAIN, _lib.MDG_EPI_STORE, act
             g.M, g.N, g.K = N, Nout, K
@@ -277,23 +283,22 @@ class _HipLayerFn(torch.autograd.Function):
 
         grads = {}
         # ---- MLP: h3 = h2 + g_m * (fc2(gelu(fc1(xn3))))
-        dy_m = e(N, C)
+        dy_m = r(C)
         part_m = lngate(None, None, None, 0, 0, dh3, dh3, sv["y"][2], 8 * C, dy_m)
-        grads["w2"] = _dw(dy_m, sv["act"])
+        grads["w2"], _ = wg(dy_m, sv["act"])
         grads["b2"] = part_m[:, :, 3].sum((0, 1))
         du = dx_gemm(dy_m, P["w2"].t().contiguous(), C, F, _lib.MDG_ACT_DGELU, sv["u"])
-        grads["w1"] = _dw(du, sv["xn"][2])
-        grads["b1"] = du.sum(0, dtype=torch.float32)
+        grads["w1"], grads["b1"] = wg(du, sv["xn"][2], True)
         dxn3 = dx_gemm(du, P["w1"].t().contiguous(), F, C)
         dh2 = e(N, C, dtp=torch.float32)
-        dy_t = e(N, C)
+        dy_t = r(C)
         part_t = lngate(dxn3, sv["h2"], sv["stats"][2], 6 * C, 7 * C, dh3, dh2, sv["y"][1], 5 * C, dy_t)
 
         def attention(i, dy, o, xn, qkv, lse):
             """out_proj + attention backward of attention i (0 spatial, 1 temporal); returns dxn."""
-            grads[f"wo{i}"] = _dw(dy, o)
+            grads[f"wo{i}"], _ = wg(dy, o)
             do = dx_gemm(dy, P[f"wo{i}"].t().contiguous(), C, C)
-            dqkv = e(N, 3 * C)
+            dqkv = r(3 * C)
             if i == 1 or L >= 16:
                 Bq, Tq, Lq = (B, T, L) if i == 1 else (B * T, L, 1)
                 rope, rows = (rope_t, T + 1) if i == 1 else (rope_l, L + 1)
@@ -315,13 +320,12 @@ class _HipLayerFn(torch.autograd.Function):
                                                     dqkv.data_ptr(), bpart.data_ptr(), qscale, s),
                            "mdg_attn_spatial_bwd")
             grads[f"kvb{i}"] = bpart.sum(1)
-            grads[f"wqkv{i}"] = _dw(dqkv, xn)
-            grads[f"bqkv{i}"] = dqkv.sum(0, dtype=torch.float32)
+            grads[f"wqkv{i}"], grads[f"bqkv{i}"] = wg(dqkv, xn, True)
             return dx_gemm(dqkv, P[f"wqkv{i}"].t().contiguous(), 3 * C, C)
 
         dxn2 = attention(1, dy_t, sv["o"][1], sv["xn"][1], sv["qkv_t"], sv["lse_t"])
         dh1 = e(N, C, dtp=torch.float32)
-        dy_s = e(N, C)
+        dy_s = r(C)
         part_s = lngate(dxn2, sv["h1"], sv["stats"][1], 3 * C, 4 * C, dh2, dh1, sv["y"][0], 2 * C, dy_s)
         dxn1 = attention(0, dy_s, sv["o"][0], sv["xn"][0], sv["qkv_s"], sv["lse_s"])
         dh0 = e(N, C, dtp=torch.float32)

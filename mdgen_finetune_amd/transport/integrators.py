@@ -17,8 +17,11 @@ dopri5.py) — parity against torchdiffeq itself is unpinned:
     ``num_steps`` is the number of *saved* points, not of integration steps.
 
 ``func(t, y)`` receives t as a 0-dim tensor of y's dtype (torchdiffeq's ``_PerturbFunc``
-casts it) and must return dy/dt shaped like y.  The host decides accept / reject after every
-step (one device→host read of the error ratio), as torchdiffeq does.
+casts it) and must return dy/dt shaped like y.  ``odeint_dopri5`` decides accept / reject on
+the host after every step, as torchdiffeq does.  ``odeint_dopri5_graphed`` runs the same
+arithmetic with the whole step — six stage evaluations, the error ratio, accept / reject
+(``torch.where``) and the next step size — captured in ONE hipGraph, so a step is one replay
+and one device→host read (the new t / dt, to decide whether the next output time is reached).
 """
 from __future__ import annotations
 
@@ -192,4 +195,109 @@ def odeint_dopri5(func, y0, t, rtol=1e-3, atol=1e-6, max_num_steps=2 ** 31 - 1, 
             dt = _optimal_step_size(dt, ratio)
             n_steps += 1
         sol[i] = _interp_evaluate(coeffs, t_lo, t_hi, nt)
+    return sol
+
+
+def odeint_dopri5_graphed(func, y0, t, rtol=1e-3, atol=1e-6, max_num_steps=2 ** 31 - 1, stats=None, f0_func=None):
+    """``odeint_dopri5`` with the adaptive step on the device: ``func(t, y)`` must be
+    stream-capturable (device work only, t a 0-dim tensor of y's dtype; e.g. the HIP
+    velocity field's ``capturable`` program).  The initial step selection runs once, eagerly
+    (``f0_func``, default func); every later step is one replay of the captured step graph and
+    one host read of (t_hi, dt).  Same tableau, error norm, step-size control and dense output
+    as ``odeint_dopri5``, so the accepted step sequence and the solution are the same."""
+    if not torch.is_floating_point(y0):
+        raise TypeError("y0 must be floating point")
+    dev, dty = y0.device, y0.dtype
+    t = torch.as_tensor(t).to(device=dev, dtype=torch.float64)
+    if t.dim() != 1 or not bool((t[1:] > t[:-1]).all()):
+        raise ValueError("t must be strictly increasing")
+    rtol = float(torch.as_tensor(rtol, dtype=torch.float64).reshape(-1)[0])
+    atol = float(torch.as_tensor(atol, dtype=torch.float64).reshape(-1)[0])
+    st = stats if stats is not None else Dopri5Stats()
+    ef = f0_func or func
+
+    def f_eager(tt, yy):
+        st.nfe += 1
+        return ef(tt.to(yy.dtype), yy)
+
+    beta = [_weights(b, y0) for b in _BETA]
+    c_err = _weights(_C_ERROR, y0)
+    c_mid = _weights(_C_MID, y0)
+    sol = torch.empty(len(t), *y0.shape, dtype=dty, device=dev)
+    sol[0] = y0
+    f0 = f_eager(t[0], y0)
+    # static state of the captured step
+    S = {"y": y0.clone(), "fy": f0.clone(), "t_lo": t[0].clone(), "t_hi": t[0].clone(),
+         "dt": _select_initial_step(f_eager, t[0], y0, f0, rtol, atol).reshape(()).clone(),
+         "coeffs": [y0.clone() for _ in range(5)], "acc": torch.zeros((), dtype=torch.int64, device=dev),
+         "tries": torch.zeros((), dtype=torch.int64, device=dev)}
+
+    def step():
+        y, fy, t_hi, dt = S["y"], S["fy"], S["t_hi"], S["dt"]
+        t1 = t_hi + dt
+        dt_y = dt.to(dty)
+        ks = [fy]
+        for a_i, b_i in zip(_ALPHA, beta):
+            yi = _combine(y, ks, b_i, dt_y)
+            if a_i == 1.0:
+                tt = t1.to(dty)
+                tt = torch.nextafter(tt, tt - 1)
+            else:
+                tt = (t_hi + a_i * dt).to(dty)
+            ks.append(func(tt, yi))
+        y1 = yi
+        err = _combine(None, ks, c_err, dt_y)
+        tol = atol + rtol * torch.max(y.abs(), y1.abs())
+        ratio = rms_norm(err / tol)
+        ok = ratio <= 1
+        y_mid = _combine(y, ks, c_mid, dt_y)
+        new = _interp_fit(y, y1, y_mid, ks[0], ks[-1], dt_y)
+        for c, n in zip(S["coeffs"], new):
+            c.copy_(torch.where(ok, n, c))
+        S["t_lo"].copy_(torch.where(ok, t_hi, S["t_lo"]))
+        y.copy_(torch.where(ok, y1, y))
+        fy.copy_(torch.where(ok, ks[-1], fy))
+        er = ratio.to(dt.dtype)  # _optimal_step_size; ratio == 0 gives min(inf, ifactor) = ifactor
+        dmin = torch.where(ok, torch.ones_like(er), torch.full_like(er, 0.2))
+        new_dt = dt * torch.clamp(0.9 / er ** (1.0 / ORDER), min=dmin, max=torch.full_like(er, 10.0))
+        t_hi.copy_(torch.where(ok, t1, t_hi))
+        dt.copy_(new_dt)
+        S["acc"].add_(ok.to(torch.int64))
+        S["tries"].add_(1)
+
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(side):
+        torch.cuda.synchronize()
+        with torch.cuda.graph(g, stream=side):
+            step()
+    torch.cuda.current_stream().wait_stream(side)
+    n_steps = 0
+    th_dt = torch.stack([S["t_hi"], S["dt"]])
+    for i in range(1, len(t)):
+        nt = float(t[i])
+        while True:
+            torch.stack([S["t_hi"], S["dt"]], out=th_dt)
+            t_hi_v, dt_v = th_dt.tolist()
+            if not nt > t_hi_v:
+                break
+            if n_steps >= max_num_steps:
+                raise AssertionError(f"max_num_steps exceeded ({n_steps}>={max_num_steps})")
+            if not t_hi_v + dt_v > t_hi_v:
+                raise AssertionError(f"underflow in dt {dt_v}")
+            g.replay()
+            n_steps += 1
+        x = ((t[i] - S["t_lo"]) / (S["t_hi"] - S["t_lo"])).to(dty)
+        c = S["coeffs"]
+        total = c[0] + x * c[1]
+        xp = x
+        for cc in c[2:]:
+            xp = xp * x
+            total = total + xp * cc
+        sol[i] = total
+    acc, tries = int(S["acc"]), int(S["tries"])
+    st.accepted += acc
+    st.rejected += tries - acc
+    st.nfe += 6 * tries
     return sol

@@ -95,10 +95,16 @@ class Transport:
         return t0, t1
 
     def sample(self, x1):
-        """transport.py:125-135 (RNG order: x0 = randn_like(x1), then t)."""
+        """transport.py:125-135 (RNG order: x0 = randn_like(x1), then t).  The reference draws t
+        on the CPU generator and copies it over; inside a graph capture (the graphed training
+        step) a host-to-device copy cannot be recorded, so t is drawn on x1's device there
+        (same distribution, the device generator's graph-safe stream)."""
         x0 = th.randn_like(x1)
         t0, t1 = self.check_interval(self.train_eps, self.sample_eps)
-        t = th.rand((x1.shape[0],)) * (t1 - t0) + t0
+        if x1.is_cuda and th.cuda.is_current_stream_capturing():
+            t = th.rand((x1.shape[0],), device=x1.device) * (t1 - t0) + t0
+        else:
+            t = th.rand((x1.shape[0],)) * (t1 - t0) + t0
         return t.to(x1), x0, x1
 
     def training_losses(self, model, x1, aatype1=None, mask=None, model_kwargs=None):
@@ -166,6 +172,12 @@ class Sampler:
                     fn = get_engine(m).velocity_field(
                         x, mask=mask, start_frames=kw.get("start_frames"), end_frames=kw.get("end_frames"),
                         x_cond=kw.get("x_cond"), x_cond_mask=kw.get("x_cond_mask"), aatype=kw.get("aatype"))
+                    from .integrators import odeint_dopri5_graphed
+
+                    ts = th.linspace(t0, t1, num_steps).to(x.device)
+                    # the whole adaptive step (6 evaluations + accept / reject) is one hipGraph
+                    return odeint_dopri5_graphed(fn.capturable, x, ts, rtol=rtol, atol=atol, f0_func=fn,
+                                                 stats=getattr(self, "dopri5_stats", None))
                 else:
                     def fn(t, y):  # integrators.py:98-101
                         return drift(y, th.ones(y.size(0)).to(y.device) * t, model, **model_kwargs)

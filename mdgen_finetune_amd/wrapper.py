@@ -174,9 +174,11 @@ class NewMDGenWrapper(nn.Module):
         }
 
     # ------------------------------------------------------------------ training step
-    def general_step(self, batch, stage="train", model=None):
+    def general_step(self, batch, stage="train", model=None, log=True):
         """wrapper.py:367-403.  ``model`` is the module the loss differentiates through (the
-        DDP wrapper of ``self.model`` in data-parallel training)."""
+        DDP wrapper of ``self.model`` in data-parallel training).  ``log=False`` (inside a graph
+        capture, where .item() cannot sync) returns (batch-mean loss, per-sample losses, t)
+        and leaves the logging to the caller (Trainer.log_step)."""
         self.iter_step += 1
         self.stage = stage
         start1 = time.time()
@@ -186,6 +188,8 @@ class NewMDGenWrapper(nn.Module):
                                              x1=prep["latents"], aatype1=None, mask=prep["loss_mask"],
                                              model_kwargs=prep["model_kwargs"])
         loss = out["loss"]
+        if not log:
+            return loss.mean(), loss, out["t"]
         self.log("model_dur", time.time() - start)
         self.log("loss", loss)
         self.log("time", out["t"])
@@ -236,11 +240,12 @@ class NewMDGenWrapper(nn.Module):
         return atom14, aa
 
     # ------------------------------------------------------------------ optimizer / EMA / ckpt
-    def configure_optimizers(self, params=None):
-        """wrapper.py:167-173."""
+    def configure_optimizers(self, params=None, capturable=False):
+        """wrapper.py:167-173 (capturable: the step count on the device, for a graphed step)."""
         cls = torch.optim.AdamW if self.args.adamW else torch.optim.Adam
         params = params if params is not None else self.model.parameters()
-        return cls([p for p in params if p.requires_grad], lr=self.args.lr)
+        kw = {"capturable": True} if capturable else {}
+        return cls([p for p in params if p.requires_grad], lr=self.args.lr, **kw)
 
     def on_before_zero_grad(self):
         """wrapper.py:78-80."""

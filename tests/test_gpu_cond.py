@@ -126,11 +126,12 @@ def test_device_tps_rel7_matches_reference_up_to_eigen_sign(name):
         assert (out[k, ..., 0] >= 0).all()
 
 
-def test_tps_window_with_device_rel7_matches_sign_fixed_oracle():
-    """The TPS sampler path with the device relative frames (no override) equals the same
-    window computed with the reference's 7-vectors sign-fixed to w >= 0."""
+def test_tps_window_with_device_rel7_matches_sign_fixed_oracle(monkeypatch):
+    """The TPS sampler path with the device relative frames (MDG_TPS_REL7=device, no override)
+    equals the same window computed with the reference's 7-vectors sign-fixed to w >= 0."""
     from mdgen_finetune_amd.engine import get_engine
 
+    monkeypatch.setenv("MDG_TPS_REL7", "device")
     d, cfg = load_golden("small_tps_T8")
     m, _ = build_model(cfg, "cuda", T=8)
     eng = get_engine(m)
@@ -159,3 +160,29 @@ def test_tps_window_with_device_rel7_matches_sign_fixed_oracle():
     torch.cuda.synchronize()
     _close(ipa_dev, ipa_fix, 1e-4, "tps ipa: device rel7 vs sign-fixed reference rel7")
     assert np.isfinite(ipa_dev.cpu().numpy()).all()
+
+
+def test_tps_default_engine_conditions_like_training_path():
+    """No override, default environment: the HIP engine's TPS forward stages the relative frames
+    from relative_tensor7 (the host eigen-solve the training / eager path uses), so it equals the
+    eager torch-backend forward of the same module (f32 tolerance) — sampling conditions exactly
+    as training did (one sign convention)."""
+    import os
+
+    from mdgen_finetune_amd.rigid_utils import Rigid, Rotation
+
+    assert os.environ.get("MDG_TPS_REL7") is None
+    d, cfg = load_golden("small_tps_T8")
+    m, _ = build_model(cfg, "cuda", T=8)
+    m.hip_dtype = "f32"
+    dev = torch.device("cuda")
+    f = lambda k: torch.from_numpy(d["in_" + k]).to(dev)  # noqa: E731
+    kw = dict(mask=f("mask"), start_frames=Rigid(Rotation(rot_mats=f("rots")), f("trans")),
+              end_frames=Rigid(Rotation(rot_mats=f("end_rots")), f("end_trans")), x_cond=f("x_cond"),
+              x_cond_mask=f("x_cond_mask"), aatype=f("aatype"))
+    with torch.no_grad():
+        v_hip = m(f("x"), f("t"), **kw)
+        m.backend = "torch"
+        v_eager = m(f("x"), f("t"), **kw)
+        m.backend = "hip"
+    _close(v_hip, v_eager, 1e-4, "tps forward: HIP engine (default rel7) vs eager torch backend")

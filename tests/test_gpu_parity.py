@@ -252,6 +252,30 @@ def test_dopri5_solve_matches_cpu_solve(dtype):
 
 
 @pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_graphed_dopri5_equals_host_controlled_dopri5(dtype):
+    """odeint_dopri5_graphed (the whole adaptive step — 6 evaluations, error ratio, accept /
+    reject, next dt — as one hipGraph, one host read per step) against odeint_dopri5 (host
+    accept / reject) on the same HIP velocity field: the same accepted / rejected step counts
+    and the same solution bit for bit."""
+    from mdgen_finetune_amd.engine import get_engine
+    from mdgen_finetune_amd.transport import Dopri5Stats
+    from mdgen_finetune_amd.transport import integrators as I
+
+    d, cfg = load_golden("small_sim_T8")
+    m, _ = build_model(cfg, "cuda")
+    m.hip_dtype = dtype
+    zs = torch.from_numpy(d["in_zs"]).cuda()
+    f = get_engine(m).velocity_field(zs, **_kw(d))
+    ts = torch.linspace(0, 1, 50)
+    s1, s2 = Dopri5Stats(), Dopri5Stats()
+    ref = I.odeint_dopri5(f, zs, ts, stats=s1)
+    got = I.odeint_dopri5_graphed(f.capturable, zs, ts, stats=s2, f0_func=f)
+    assert (s1.accepted, s1.rejected) == (s2.accepted, s2.rejected), (vars(s1), vars(s2))
+    assert s1.nfe == s2.nfe
+    assert torch.equal(got, ref), float((got - ref).abs().max())
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
 @pytest.mark.parametrize("T,L,n_pad", [(16, 256, 51), (40, 24, 3), (8, 16, 0)])
 def test_long_residue_axis_atlas_matches_oracle(T, L, n_pad, dtype):
     """ATLAS shape (BASELINE config 5: crop 256, ~20% padded residues): L >= 16 routes the
@@ -267,6 +291,56 @@ def test_long_residue_axis_atlas_matches_oracle(T, L, n_pad, dtype):
         v = m(g("x"), g("t"), g("mask"), start_frames=Rigid(Rotation(rot_mats=g("rots")), g("trans")),
               x_cond=g("x_cond"), x_cond_mask=g("x_cond_mask"), aatype=g("aatype"))
     _check(v, ref, dtype, valid=inp["mask"][0, 0] > 0)
+
+
+@pytest.mark.parametrize("B,lanes", [(16, 2), (8, 1)])
+def test_headline_route_T1000_matches_oracle(B, lanes):
+    """The bench's own route (bf16, T=1000, L=4; B=16 as two lanes of 8, and B=8 as one chain):
+    the 250-tile launches take the fused MLP (mlp_rowln_kernel) and the fused out_proj + q|k|v
+    (rowln_qkv_kernel).  One Euler step (num_steps=2, dt=1) through the captured window,
+    v = x_1 - x_0 against the oracle forward at t=0 for every trajectory, at the bf16 bounds."""
+    from mdgen_finetune_amd.engine import get_engine
+    from mdgen_finetune_amd.rigid_utils import Rigid, Rotation
+
+    from mdgen_finetune_amd import synthetic
+    from oracle import mdgen_oracle as O
+
+    T = 1000
+    cfg = dict(flags=[], latent_dim=21, L=4, T=T, tps=False, weights_seed=21)
+    inp = synthetic.make_inputs(22, B, T, 4, 21)
+    f = lambda k: torch.from_numpy(inp[k])  # noqa: E731
+    c = O.Cfg(crop=4)
+    P = O.seeded_params(c, 21)
+    torch.set_num_threads(16)
+    with torch.no_grad():
+        v_ref = O.forward(P, c, f("x"), torch.zeros(B), f("mask"), f("rots"), f("trans"), x_cond=f("x_cond"),
+                          x_cond_mask=f("x_cond_mask"), aatype=f("aatype")).numpy()
+    m, _ = build_model(cfg, "cuda", T=T)
+    m.hip_dtype = "bf16"
+    eng = get_engine(m)
+    eng.lanes = lanes
+    plan = eng.describe_plan(B // lanes, T, 4)
+    assert plan["mlp"].startswith("mlp_fused(fc1+gelu+fc2"), plan
+    assert plan["temporal"].startswith("rowln_qkv"), plan
+    g = lambda k: f(k).cuda()  # noqa: E731
+    kw = dict(mask=g("mask"), start_frames=Rigid(Rotation(rot_mats=g("rots")), g("trans")), x_cond=g("x_cond"),
+              x_cond_mask=g("x_cond_mask"), aatype=g("aatype"))
+    for _ in range(2):  # capture + replay, then a second replay
+        ys = eng.sample_euler(g("x"), num_steps=2, use_graph=True, **kw)
+        v = (ys[1] - ys[0]).cpu().numpy()
+        _check(v, v_ref, "bf16")
+    eng.lanes = 0
+
+
+def _first_mismatch(got, ref, Bl):
+    """Locus of the first differing element: (state index, lane, b, t, l, channel, |d|)."""
+    d = (got - ref).abs()
+    idx = (d > 0).nonzero()
+    if idx.numel() == 0:
+        return None
+    s, b, t, l, ch = idx[0].tolist()
+    return dict(step=s, lane=b // Bl, b=b, t=t, l=l, channel=ch, abs=float(d[s, b, t, l, ch]),
+                n_bad=int(idx.shape[0]), max_abs=float(d.max()))
 
 
 @pytest.mark.parametrize("lanes,offset", [(2, 0), (2, 2), (3, 1)])
@@ -294,8 +368,9 @@ def test_concurrent_lanes_equal_single_chain(lanes, offset):
     got_replay = eng.sample_euler(g("x"), num_steps=6, use_graph=True, **kw)
     eng.lanes, eng.lane_offset = 1, 0
     eng._graphs.clear()
-    assert torch.equal(got_eager, ref)
-    assert torch.equal(got_graph, ref) and torch.equal(got_replay, ref)
+    Bl = ref.shape[1] // lanes
+    for name, got in (("eager", got_eager), ("graph", got_graph), ("replay", got_replay)):
+        assert torch.equal(got, ref), (name, _first_mismatch(got, ref, Bl))
 
 
 @pytest.mark.parametrize("dtype", ["f32", "bf16"])

@@ -184,3 +184,196 @@ def test_hip_layer_backward_matches_eager_autograd(dtype, T, L, n_pad):
     _log_train({"test": "layer_bwd", "dtype": dtype, "T": T, "L": L, "n_pad": n_pad, "fwd_rel": fwd,
                 "worst_rel": worst[0], "worst": worst[1]})
     assert worst[0] <= tol, worst
+
+
+def _default_dims_case(B=2, T=64, L=4, seed=31):
+    """Inputs of config 3's loss at the reference's training dims (parsing.py:86-97: embed_dim
+    384, 16 heads -> head_dim 24, 5 layers, IPA prepend): seeded latents, noise, t, mask."""
+    from mdgen_finetune_amd import synthetic
+
+    inp = synthetic.make_inputs(seed, B, T, L, 21)
+    rng = np.random.default_rng(seed + 1)
+    inp["x0"] = rng.standard_normal(inp["x"].shape).astype(np.float32)
+    inp["t_loss"] = rng.uniform(0.05, 0.95, B).astype(np.float32)
+    inp["loss_mask"] = np.broadcast_to(inp["mask"][..., None], inp["x"].shape).astype(np.float32).copy()
+    cfg = dict(flags=[], latent_dim=21, L=L, T=T, tps=False, weights_seed=seed + 2)
+    return inp, cfg
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_default_dims_training_grads_match_oracle(dtype):
+    """The HIP training path at the dims config 3 trains (C=384, H=16, D=24, 5 layers, T=64):
+    the GVP loss and EVERY parameter gradient against the oracle under autograd (CPU fp32).
+    Bounds: f32 loss rel 1e-5, grads 1e-4; bf16 loss 1e-2, grads BF16_DEFAULT_GRAD (~2x the
+    worst observed, profiles/r03_parity_train.jsonl)."""
+    from mdgen_finetune_amd.rigid_utils import Rigid, Rotation
+    from mdgen_finetune_amd.transport import create_transport
+    from mdgen_finetune_amd.transport.transport import mean_flat
+    from oracle import mdgen_oracle as O
+
+    inp, cfg = _default_dims_case()
+    f = lambda k: torch.from_numpy(np.ascontiguousarray(inp[k]))  # noqa: E731
+    c = O.Cfg(crop=4)
+    P = O.seeded_params(c, cfg["weights_seed"])
+    for v in P.values():
+        v.requires_grad_(True)
+    torch.set_num_threads(16)
+    kw_cpu = dict(mask=f("mask"), rots=f("rots"), trans=f("trans"), x_cond=f("x_cond"), x_cond_mask=f("x_cond_mask"),
+                  aatype=f("aatype"))
+    loss_ref, _ = O.gvp_training_loss(P, c, f("x"), f("x0"), f("t_loss"), f("loss_mask"), **kw_cpu)
+    loss_ref.mean().backward()
+
+    m, _ = build_model(cfg, "cuda", T=64)
+    m.train()
+    m.hip_dtype = dtype
+    g = lambda k: f(k).cuda()  # noqa: E731
+    kw = dict(mask=g("mask"), start_frames=Rigid(Rotation(rot_mats=g("rots")), g("trans")), x_cond=g("x_cond"),
+              x_cond_mask=g("x_cond_mask"), aatype=g("aatype"))
+    assert m._use_hip_layers(torch.zeros(1, device="cuda", requires_grad=True))
+    tr = create_transport(m.args, "GVP", "velocity")
+    t, xt, ut = tr.path_sampler.plan(g("t_loss"), g("x0"), g("x"))
+    v = m(xt, t, **kw)
+    loss = mean_flat((v - ut) ** 2, g("loss_mask"))
+    loss.mean().backward()
+    lrel = float((loss.detach().cpu() - loss_ref.detach()).abs().max() / loss_ref.detach().abs().max())
+    names = dict(m.named_parameters())
+    worst, checked = (0.0, None), 0
+    for k, p in P.items():
+        if p.grad is None or k not in names or float(p.grad.norm()) < 1e-8:
+            continue
+        gg = names[k].grad
+        assert gg is not None, k
+        rel = float((gg.detach().float().cpu() - p.grad).norm()) / float(p.grad.norm())
+        worst = max(worst, (rel, k))
+        checked += 1
+    _log_train({"test": "default_dims_grads", "dtype": dtype, "loss_rel": lrel, "worst_grad_rel": worst[0],
+                "worst_param": worst[1], "checked": checked})
+    loss_tol, grad_tol = (1e-5, 1e-4) if dtype == "f32" else (1e-2, BF16_DEFAULT_GRAD)
+    assert lrel <= loss_tol, lrel
+    assert worst[0] <= grad_tol, worst
+    assert checked > 250
+
+
+BF16_DEFAULT_GRAD = 5e-2
+
+
+def _fixed_noise(tr, B, shape, seed=5):
+    """Replace the transport's (t, x0) draw with fixed device tensors (graph-safe)."""
+    gen = torch.Generator().manual_seed(seed)
+    x0 = torch.randn(*shape, generator=gen).cuda()
+    t = (0.05 + 0.9 * torch.rand(B, generator=gen)).cuda()
+    tr.wrapper.transport.sample = lambda x1: (t, x0, x1)
+
+
+def test_graphed_step_equals_eager_step():
+    """Trainer.graph_mode (GraphedStep: forward + loss + backward + clip + Adam + EMA replayed
+    from one hipGraph) against the eager step on the same batch and noise: the updated
+    parameters, the loss and the grad norm agree; later replays keep training (the loss moves)."""
+    from mdgen_finetune_amd.train import Trainer
+
+    res = {}
+    for mode in (0, 1):
+        a = _args(["--lr", "1e-3", "--embed_dim", "96", "--mha_heads", "4", "--ema", "--train_graph", str(mode)])
+        tr = Trainer(a, device=torch.device("cuda"))
+        assert tr.graph_mode == bool(mode)
+        b = _batch(a, B=2)
+        _fixed_noise(tr, 2, (2, a.num_frames, a.crop, 21))
+        loss, gnorm = tr.step([b], log=False)
+        res[mode] = (float(loss), float(gnorm), torch.cat([p.detach().flatten() for p in tr.wrapper.model.parameters()]),
+                     torch.cat([v.flatten() for v in tr.wrapper.ema.params.values() if v.is_floating_point()]))
+        if mode:
+            losses = [float(tr.step([b], log=False)[0]) for _ in range(3)]
+            assert len(set(losses)) > 1 and np.isfinite(losses).all()
+    (l0, g0, p0, e0), (l1, g1, p1, e1) = res[0], res[1]
+    assert abs(l0 - l1) <= 1e-5 * abs(l0), (l0, l1)
+    assert abs(g0 - g1) <= 1e-4 * abs(g0), (g0, g1)
+    assert float((p0 - p1).abs().max()) <= 1e-6, float((p0 - p1).abs().max())
+    assert float((e0 - e1).abs().max()) <= 1e-6
+
+
+def _share_worker(rank, world, port, graph, out):
+    import os
+
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), MDG_SHARE_GPU="1")
+    from mdgen_finetune_amd.train import Trainer, setup_distributed
+
+    r, w, dev = setup_distributed()
+    a = _args(["--grad_clip", "0", "--embed_dim", "96", "--mha_heads", "4", "--train_graph", str(graph),
+               "--bucket_cap_mb", "0.25"])
+    tr = Trainer(a, r, w, dev)
+    assert tr.graph_mode == bool(graph)
+    b = _batch(a, B=2, seed=100 + rank)
+    _fixed_noise(tr, 2, (2, a.num_frames, a.crop, 21), seed=7 + rank)
+    m = tr.wrapper.model
+    params = [p for p in m.parameters() if p.requires_grad]
+    prep = tr.wrapper.prep_batch({k: (v.cuda() if torch.is_tensor(v) else v) for k, v in b.items()})
+    loss = tr.wrapper.transport.training_losses(m, prep["latents"], mask=prep["loss_mask"],
+                                                model_kwargs=prep["model_kwargs"])["loss"].mean()
+    local = torch.autograd.grad(loss, params, allow_unused=True)
+    local = torch.cat([(x if x is not None else torch.zeros_like(p)).flatten() for x, p in zip(local, params)])
+    ref = local.clone()
+    dist.all_reduce(ref)
+    ref /= w
+    seen = []
+    orig = tr.optimizer.step
+    tr.optimizer.step = lambda *a_, **k_: (seen.append(torch.cat([p.grad.flatten().clone() for p in params])),
+                                           orig())[1]
+    if graph:
+        tr.step([b], log=False)
+        got = tr._graphed.flat.clone()
+    else:
+        for _ in range(2):  # DDP's bucketed path from its third iteration (static graph)
+            tr.wrapper.general_step({k: (v.cuda() if torch.is_tensor(v) else v) for k, v in b.items()},
+                                    model=tr.model).backward()
+            tr.optimizer.zero_grad(set_to_none=True)
+        tr.step([b], log=False)
+        got = seen[-1]
+    pall = torch.cat([p.detach().flatten() for p in params])
+    gathered = [torch.zeros_like(pall) for _ in range(w)]
+    dist.all_gather(gathered, pall)
+    out[rank] = (float((got - ref).abs().max()), float(ref.abs().max()), float((gathered[0] - gathered[1]).abs().max()),
+                 float((local - ref).abs().max()))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("graph", [0, 1])
+def test_world2_on_one_gpu_allreduce_matches_local_mean(graph):
+    """Two ranks on cuda:0 over gloo (MDG_SHARE_GPU=1), each running the HIP training Function:
+    graph=0 through DistributedDataParallel (bucketed all-reduce during backward), graph=1
+    through GraphedStep (flat all-reduce between its two graphs).  The averaged gradient equals
+    the mean of the ranks' local gradients and the replicas stay identical after Adam."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_share_worker, args=(2, port, graph, out), nprocs=2, join=True)
+    for r in range(2):
+        err, scale, drift, spread = out[r]
+        assert err <= 1e-5 * max(1.0, scale), (r, err, scale)
+        assert drift == 0.0
+        assert spread > 0.0
+
+
+def test_grad_checkpointing_on_hip_layers_same_grads():
+    """--grad_checkpointing with the HIP training Function (reentrant checkpoint: the layer's
+    forward re-runs in backward) gives the same gradients as the stored-activation path."""
+    d, cfg = load_golden("small_loss")
+    grads = []
+    for ck in (False, True):
+        m, _ = build_model(cfg, "cuda")
+        m.train()
+        m.args.grad_checkpointing = ck
+        loss, _ = _model_loss(m, d, "cuda")
+        loss.mean().backward()
+        grads.append(torch.cat([p.grad.flatten() for p in m.parameters() if p.grad is not None]))
+    assert grads[0].shape == grads[1].shape
+    assert torch.equal(grads[0], grads[1]), float((grads[0] - grads[1]).abs().max())

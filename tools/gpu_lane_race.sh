@@ -1,0 +1,22 @@
+#!/bin/bash
+# Lane-divergence locus hunt (tools/lane_race.py), one process per variant.
+# Round-3 results: gpurun_out/lane_race/*.log; DESIGN.md §2 records the cause.
+set -u -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+OUT=gpurun_out/lane_race
+mkdir -p $OUT
+R=${R:-300}
+run() { local name=$1; shift; echo "== $name"; env "$@" timeout -k 10 150 python -u tools/lane_race.py $LA > $OUT/$name.log 2>&1; local rc=$?; tail -1 $OUT/$name.log; return $rc; }
+VARIANTS=${VARIANTS:-"default spa3 spa4 xcd0 fence dppc nomlp"}
+for v in $VARIANTS; do
+  case $v in
+    default) LA="3 1 $R" run default MDG_X=1 ;;
+    spa3) LA="3 1 $R" run spa3 MDG_SPA_STAGES=3 ;;
+    spa4) LA="3 1 $R" run spa4 MDG_SPA_STAGES=4 ;;
+    xcd0) LA="3 1 $R" run xcd0 MDG_SPA_XCD=0 ;;
+    fence) LA="3 1 $R" run fence MDG_LIB_PATH=$PWD/diaglib/spa1.so ;;
+    dppc) LA="3 1 $R" run dppc MDG_LIB_PATH=$PWD/diaglib/spa2.so ;;
+    nomlp) LA="3 1 $R" run nomlp MDG_FUSED_MLP=0 ;;
+    *) echo "unknown $v"; false ;;
+  esac || exit 1
+done
