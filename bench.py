@@ -360,22 +360,25 @@ def sweep_line(dev, T, L, B, dtype, lanes, num_steps, steps, seed):
     return out
 
 
-def cpu_baseline(T, L, seconds):
+def cpu_baseline(T, L, seconds, tps=False):
     """The oracle (oracle/mdgen_oracle.py, fp32 PyTorch-CPU restatement pinned to the
-    reference) timed on this host: forward + Euler update at B=1 T=1000 L=4, repeated until
-    `seconds` of CPU work."""
+    reference) timed on this host: forward + Euler update at B=1, T frames, L=4 (the TPS model
+    with start + end frames for tps), repeated until `seconds` of CPU work."""
     from mdgen_finetune_amd import synthetic
     from oracle import mdgen_oracle as O
 
     threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     threads = max(1, min(threads, os.cpu_count() or 1))
     torch.set_num_threads(threads)
-    c = O.Cfg(crop=L)
+    lat = 28 if tps else 21
+    c = O.Cfg(crop=L, latent_dim=lat, tps=tps)
     P = O.seeded_params(c, 0)
-    inp = synthetic.make_inputs(1, 1, T, L, 21)
+    inp = synthetic.make_inputs(1, 1, T, L, lat, tps=tps)
     f = lambda k: torch.from_numpy(inp[k])  # noqa: E731
     kw = dict(mask=f("mask"), rots=f("rots"), trans=f("trans"), x_cond=f("x_cond"), x_cond_mask=f("x_cond_mask"),
               aatype=f("aatype"))
+    if tps:
+        kw.update(end_rots=f("end_rots"), end_trans=f("end_trans"))
     x = f("x")
     dt = float(torch.linspace(0, 1, 50)[1])
     with torch.no_grad():
@@ -397,8 +400,38 @@ def cpu_baseline(T, L, seconds):
     except OSError:
         pass
     return {"value": round(T * n / el, 1), "unit": "frames/s", "cores": threads, "kind": "port",
-            "sample": f"{n} denoising steps (oracle forward + Euler update), B=1 T={T} L={L}, fp32, "
-                      f"{el:.1f} s on {threads} threads of {cpu}"}
+            "sample": f"{n} denoising steps (oracle forward + Euler update{', TPS model' if tps else ''}), B=1 "
+                      f"T={T} L={L}, fp32, {el:.1f} s on {threads} threads of {cpu}"}
+
+
+def step_kernel_roofline(eng, B, T, L, dtype, lanes, zs, kw):
+    """Small-M shapes (TPS T=100, B=1 windows) have no single dominant launch type (every
+    launch is a few tiles; the MLP runs split over blocks with a reduction pass): the roofline
+    unit is one whole denoise step (all its launches) of one lane, timed with HIP events on its
+    stream, replayed standalone from the engine's state, priced at the step's algorithmic FLOPs."""
+    from mdgen_finetune_amd import _lib
+
+    Bl = B // lanes
+    st = eng._state(Bl, T, L, lane=1 if lanes > 1 else 0)
+    gs = next(iter(eng._graphs.values()))
+    mods, mods_f, ipa = gs.cond
+    lane_mods = mods[0] if lanes > 1 else mods
+    io = eng._step_io(st, gs.states[0].data_ptr(), gs.states[1].data_ptr(), None,
+                      None if ipa is None else ipa[0].data_ptr(), lane_mods[0].data_ptr(), mods_f[0].data_ptr(),
+                      gs.dts[0], base=eng._states[(B, T, L, 0)].base.data_ptr())
+    s = _lib.stream_handle()
+
+    def step():
+        _lib.check(eng.lib.mdg_denoise_step(ctypes.byref(st.model_struct), ctypes.byref(io), gs.mask.data_ptr(),
+                                            st.ws.data_ptr(), s), "mdg_denoise_step")
+
+    sec = time_kernel(step, 50)
+    sm = step_model(Bl, T, L, dtype=dtype, lat=eng.lat)
+    tf = sm["flops"] / sec / 1e12
+    return {"kernel": "denoise_step (every launch of one step of one lane)", "bound": "mfma", "achieved": round(tf, 2),
+            "peak": PEAK_TFLOPS[dtype], "unit": "TFLOP/s", "frac": round(tf / PEAK_TFLOPS[dtype], 4), "traffic": None,
+            "avg_launch_us": round(sec * 1e6, 2), "flops_per_launch": sm["flops"], "shape": f"B={Bl} T={T} L={L}",
+            "timing": "standalone: 50 back-to-back steps of one lane from the window's state (HIP events)"}
 
 
 def cpu_train_baseline(T, L, seconds):
@@ -605,6 +638,8 @@ def main():
         Bl = B // nl
         st = eng._state(Bl, T, L, lane=1 if nl > 1 else 0)
         roofs = roofline(eng, st, a.dtype, Bl, T, L) if rank == 0 and not a.tps else None
+        if rank == 0 and a.tps:
+            roofs = {"step": step_kernel_roofline(eng, B, T, L, a.dtype, nl, zs, kw)}
         plan = eng.describe_plan(Bl, T, L)
 
     # extra lines (rank 0, single process): the B sweep SURVEY §8(d) asks for and the fp32
@@ -619,7 +654,7 @@ def main():
 
     out = None
     if rank == 0:
-        cpu = None if (a.no_cpu_baseline or world > 1 or a.tps) else cpu_baseline(T, L, a.cpu_seconds)
+        cpu = None if (a.no_cpu_baseline or world > 1) else cpu_baseline(T, L, a.cpu_seconds, tps=a.tps)
         out = {
             "metric": "denoised frames/sec, 1000-frame x crop4 forward-sim step, 1/2/4/8 MI355X",
             "value": round(value, 1),

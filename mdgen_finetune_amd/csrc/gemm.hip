@@ -39,6 +39,13 @@
 
 namespace mdg {
 
+// kRingWaitNote — every raw s_barrier after which a wave refills a ring slot (LDS DMA) is
+// preceded by an explicit s_waitcnt lgkmcnt(0): the compiler may otherwise leave the previous
+// step's last ds_reads of THAT slot in flight across the barrier (it moves their MFMAs, and the
+// waits guarding them, below it), and an LDS-DMA write issued by another wave after the barrier
+// then races those reads.  Found in round 3 by scanning the ISA of every kernel for LDS
+// operations pending at a barrier (mlp_rowln_kernel<384, false>, rowln_qkv_kernel); DESIGN.md §4.
+
 constexpr int kThreads = 512;
 
 // x + dt * v rounded twice, as torchdiffeq's Euler step computes it (integrators.py:106-113:
@@ -890,6 +897,7 @@ __global__ __launch_bounds__(kB8Threads) void gemm_bf16_b8_kernel(const mdg_gemm
     // finished reading stage kt-1, whose buffer the loads below overwrite)
     if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // ring reads retired (see kRingWaitNote)
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (kt + 2 < nk) {
@@ -981,27 +989,34 @@ __device__ __forceinline__ void rowln_load_band(const mdg_gemm_desc& p, int m0, 
   }
 }
 
-template <int NCOL>
 // xlds: write the normalised rows (xn) not to p.xn_out but into LDS, as K-slice images of 32
 // columns ([NCOL / 32][BM][32] bf16, 16-B chunk c of row r at c ^ ((-(r >> 2)) & 3)): the
 // A operand of a following GEMM in the same block.
-__device__ __forceinline__ void rowln_fast_epilogue(const mdg_gemm_desc& p, f32x4 (&acc)[4][NCOL / 64],
-                                                    float4 (&h4)[2][NCOL / 128], unsigned char* smem, int m0,
-                                                    int b_lo, float inv_rpm, bf16_t* xlds = nullptr) {
+// stage_band(band, stage) writes the block's fp32 accumulator rows [32 band, 32 band + 32)
+// into stage (row stride LDS_ST floats); the kernels differ only in where their accumulators live.
+// NREG stage regions: band b is read from region b % NREG, so a caller with NREG = 3 may write
+// bands 0-2 at once (at band 0's call; band 3 at its own) and free their registers early.
+// LATE_H: h4 is not loaded yet; band 0's residual rows are read right after band 0's staging (a
+// caller whose accumulators fill the registers until then).
+template <int NCOL, int NREG = 1, bool LATE_H = false, typename StageBand>
+__device__ __forceinline__ void rowln_fast_epilogue_impl(const mdg_gemm_desc& p, StageBand stage_band,
+                                                         float4 (&h4)[2][NCOL / 128], unsigned char* smem, int m0,
+                                                         int b_lo, float inv_rpm, bf16_t* xlds = nullptr) {
   // no fp contraction: every kernel that inlines this epilogue (the row-LN GEMM, the fused MLP,
   // the fused out_proj + q|k|v) rounds h and xn identically
 #pragma clang fp contract(off)
-  constexpr int BM = 128, WTN = NCOL / 4, NT = WTN / 16, LDS_ST = NCOL + 4, NE = NCOL / 128;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wm = wave / 4, wn = wave % 4;
-  const int lr = lane & 15, lg = lane >> 4, half = lane >> 5, hl = lane & 31;
+  constexpr int BM = 128, LDS_ST = NCOL + 4, NE = NCOL / 128;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int half = lane >> 5, hl = lane & 31;
   const int M = p.M;
   const int b_hi = fdiv(min(m0 + BM - 1, M - 1), p.rows_per_mod, inv_rpm);
   float* stage = reinterpret_cast<float*>(smem);
   const float invN = 1.0f / (float)NCOL;
   auto load_unit4 = [&](int u, float4 (&hb)[2][NE]) { rowln_load_band<NCOL>(p, m0, u, hb); };
-  float* emods = stage + 32 * LDS_ST;  // [2][3][NCOL]: gate | xn scale | xn shift
+  float* emods = stage + NREG * 32 * LDS_ST;  // [2][3][NCOL]: gate | xn scale | xn shift
   // the caller's smem holds (32 * LDS_ST + 6 * NCOL) floats: the band stage + the adaLN rows
   static_assert(LDS_ST % 4 == 0, "16-B aligned stage rows");
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the last K-step's ring reads (kRingWaitNote)
   __builtin_amdgcn_s_barrier();  // every wave is done reading the ring (its loads were all waited)
   for (int i = tid; i < 6 * NCOL; i += kRowThreads) {
     const int eb = i / (3 * NCOL), w = (i / NCOL) % 3, k = i % NCOL;
@@ -1022,18 +1037,10 @@ __device__ __forceinline__ void rowln_fast_epilogue(const mdg_gemm_desc& p, f32x
   for (int band = 0; band < BM / 32; ++band) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // previous band's stage reads (and the adaLN rows) are done
-    if (wm == (band >> 1)) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        if ((i >> 1) != (band & 1)) continue;
-#pragma unroll
-        for (int j = 0; j < NT; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-            stage[((i & 1) * 16 + lg * 4 + r) * LDS_ST + wn * WTN + j * 16 + lr] = acc[i][j][r];
-      }
-    }
+    stage_band(band, stage);
+    if (LATE_H && band == 0) rowln_load_band<NCOL>(p, m0, 0, h4);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const float* bstage = stage + (band % NREG) * 32 * LDS_ST;
     __builtin_amdgcn_s_barrier();
     float4 hn[2][NE];
     if (band + 1 < BM / 32) load_unit4(band + 1, hn);
@@ -1043,7 +1050,7 @@ __device__ __forceinline__ void rowln_fast_epilogue(const mdg_gemm_desc& p, f32x
     for (int pr = 0; pr < 2; ++pr) {
       const int m = m0 + band * 32 + wave * 4 + 2 * pr + half;
       eb[pr] = fdiv(min(m, M - 1), p.rows_per_mod, inv_rpm) - b_lo;
-      const float* srow = stage + (wave * 4 + 2 * pr + half) * LDS_ST + 4 * hl;
+      const float* srow = bstage + (wave * 4 + 2 * pr + half) * LDS_ST + 4 * hl;
       const float* gr = emods + eb[pr] * 3 * NCOL + 4 * hl;
       float sacc = 0.f;
 #pragma unroll
@@ -1114,6 +1121,31 @@ __device__ __forceinline__ void rowln_fast_epilogue(const mdg_gemm_desc& p, f32x
 #pragma unroll
       for (int e = 0; e < NE; ++e) h4[pr][e] = hn[pr][e];
   }
+}
+
+// The 8-wave (2 x 4) accumulator layout of the row-LN GEMM / fused MLP / fused out_proj + qkv:
+// wave (wm, wn) holds rows wm * 64 + 16 i + 4 lg + r, columns wn * NCOL / 4 + 16 j + lr.
+template <int NCOL>
+__device__ __forceinline__ void rowln_fast_epilogue(const mdg_gemm_desc& p, f32x4 (&acc)[4][NCOL / 64],
+                                                    float4 (&h4)[2][NCOL / 128], unsigned char* smem, int m0,
+                                                    int b_lo, float inv_rpm, bf16_t* xlds = nullptr) {
+  constexpr int WTN = NCOL / 4, NT = WTN / 16, LDS_ST = NCOL + 4;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, wm = wave / 4, wn = wave % 4;
+  const int lr = lane & 15, lg = lane >> 4;
+  auto stage_band = [&](int band, float* stage) {
+    if (wm == (band >> 1)) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if ((i >> 1) != (band & 1)) continue;
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            stage[((i & 1) * 16 + lg * 4 + r) * LDS_ST + wn * WTN + j * 16 + lr] = acc[i][j][r];
+      }
+    }
+  };
+  rowln_fast_epilogue_impl<NCOL>(p, stage_band, h4, smem, m0, b_lo, inv_rpm, xlds);
 }
 
 // PART: split-K form for small M — block (tile, y) runs K-steps [y nk, (y + 1) nk) and writes its
@@ -1227,6 +1259,7 @@ __global__ __launch_bounds__(kRowThreads, BM == 64 ? 4 : 1) void gemm_rowln_kern
       else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WLD) : "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // ring reads retired (see kRingWaitNote)
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (kt + kRowStages - 1 < nk) MDG_ROW_LOAD((kt + kRowStages - 1) % kRowStages, kbeg + (kt + kRowStages - 1) * BK);
@@ -1583,6 +1616,7 @@ __global__ __launch_bounds__(kMlpThreads, 1) void mlp_rowln_kernel(const MlpArgs
   auto step_begin = [&](int s) {
     const int y1 = s + 1 < NS ? ((s + 1) % 10 < 6 ? 4 : 3) : 0;
     vm_wait_upto6(y1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // ring reads retired (see kRingWaitNote)
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (s + STAGES - 1 < NS) issue(s + STAGES - 1);
@@ -1661,6 +1695,217 @@ __global__ __launch_bounds__(kMlpThreads, 1) void mlp_rowln_kernel(const MlpArgs
     float4 h4[2][NE];
     rowln_load_band<NCOL>(p, m0, 0, h4);  // band 0's residual rows
     rowln_fast_epilogue<NCOL>(p, acc2, h4, smem, m0, fdiv(m0, p.rows_per_mod, inv_rpm), inv_rpm);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Fused MLP, wave-specialised (round 3; large M, one 128-token tile per block, 8 waves).
+// The lock-step kernel above runs fc1 -> GELU -> fc2 in every wave, so the GELU's vector issue
+// (~3 800 cycles per wave and hidden chunk) sits on the MFMA critical path.  Here the two halves
+// of a SIMD's pair of waves do different work at the same time:
+//   P waves 0-3 ("producers"): Hc^T = W1c . xn^T for chunk t (32 tokens each, the 128 hidden
+//     units of the chunk), + b1, GELU, bf16 -> H[t % 2] in LDS.  Each P wave keeps its 32 xn rows
+//     x 384 in registers for the whole kernel (the fc1 B operand: 96 VGPRs), so xn is read from
+//     HBM exactly once per tile (the lock-step kernel re-staged it per chunk: 1.11x traffic).
+//   Q waves 4-7 ("consumers"): acc2 += H[t-1] . W2c^T for chunk t-1 (128 tokens x 96 outputs
+//     each, 192 accumulator VGPRs), then the row-LN epilogue.
+// Wave w and w + 4 share SIMD w, so a P wave's GELU issues beside a Q wave's MFMAs.  A chunk is
+// 4 phases separated by one block barrier: per phase P does 3 fc1 K-steps of 32 (W1 slice 128
+// rows x 96, 24 KiB), Q one fc2 K-step of 32 (W2 slice 384 rows x 32, 24 KiB); both slices of
+// phase p+1 stream into the other slot of a 2-slot global_load_lds ring during phase p (6 pieces
+// per wave, waited with vmcnt(0) before the phase's barrier).  LDS: H 2 x 32 KiB + ring 2 x 48
+// KiB = 160 KiB.  The K orders of both products equal the lock-step kernel's, so h and xn are
+// bit-identical to it (tests/test_gpu_kernels.py).
+constexpr int kWsThreads = 512, kWsHC = 128, kWsW1Img = 128 * 32;
+constexpr int kWsSlot = 3 * kWsW1Img + 384 * 32;                                 // bf16 elements
+constexpr size_t kWsSmem = (size_t)2 * 128 * kWsHC * 2 + (size_t)2 * kWsSlot * 2;  // 160 KiB
+
+template <int NCOL>
+__global__ __launch_bounds__(kWsThreads, 1) void mlp_ws_kernel(const MlpArgs args) {
+  static_assert(NCOL == 384, "the ring's W2 slice holds 384 rows");
+  constexpr int BM = 128, HC = kWsHC, BK = 32, NQ = 6, LDS_ST = NCOL + 4;
+  typedef __attribute__((address_space(3))) void* lds_ptr_t;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  bf16_t* Hb = reinterpret_cast<bf16_t*>(smem);  // [2][BM][HC]: 16-B chunk c of row r at c ^ (r & 15)
+  bf16_t* ring = Hb + 2 * BM * HC;               // [2][kWsSlot]
+  const mdg_gemm_desc& q = args.f1;              // xn, W1, b1
+  const mdg_gemm_desc& p = args.f2;              // W2, b2 and the row-LN epilogue
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wq = wave & 3;
+  const bool isP = wave < 4;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int M = p.M, F = p.K, NCH = F / HC, NPH = 4 * (NCH + 1);
+  const int nwg = (M + BM - 1) / BM;
+  const int xcd = blockIdx.x & 7, loc = blockIdx.x >> 3, q8 = nwg >> 3, r8 = nwg & 7;
+  const int m0 = ((xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc) * BM;
+  const bf16_t* X = reinterpret_cast<const bf16_t*>(q.A);
+  const bf16_t* W1 = reinterpret_cast<const bf16_t*>(q.W);
+  const bf16_t* W2 = reinterpret_cast<const bf16_t*>(p.W);
+  // ring pieces (16 rows x 64 B each, lane-linear destination, swizzle on the source chunk):
+  // P wave wq stages W1 pieces 6wq..6wq+5 (image k3 = id / 8, row block id % 8), Q wave wq W2
+  // row blocks 6wq..6wq+5
+  // the row swizzle of row 16 rb + prow depends on prow only: one per-lane offset for all pieces
+  const int prow = lane >> 2, pch = lane & 3;
+  const int ldw = isP ? q.ldw : p.ldw;
+  const int voff = prow * ldw + ((pch ^ ((-(prow >> 2)) & 3)) * 8);
+  auto issue = [&](int ph) {
+    if (ph >= NPH) return;
+    bf16_t* sl = ring + (ph & 1) * kWsSlot;
+    if (isP) {
+      if (ph >= 4 * NCH) return;
+      const bf16_t* base = W1 + (size_t)(ph >> 2) * HC * ldw + 96 * (ph & 3) + voff;
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        const int id = 6 * wq + i;
+        __builtin_amdgcn_global_load_lds((const void*)(base + 32 * (id >> 3) + 16 * (id & 7) * ldw),
+                                         (lds_ptr_t)(sl + (id >> 3) * kWsW1Img + 16 * (id & 7) * BK), 16, 0, 0);
+      }
+    } else {
+      if (ph < 4) return;
+      const bf16_t* base = W2 + (size_t)((ph >> 2) - 1) * HC + 32 * (ph & 3) + voff;
+#pragma unroll
+      for (int i = 0; i < 6; ++i)
+        __builtin_amdgcn_global_load_lds((const void*)(base + 16 * (6 * wq + i) * ldw),
+                                         (lds_ptr_t)(sl + 3 * kWsW1Img + 16 * (6 * wq + i) * BK), 16, 0, 0);
+    }
+  };
+  const int ch = (lg ^ ((-(lr >> 2)) & 3)) * 8;  // fragment rows are lr mod 16
+  issue(0);
+  if (isP) {
+    // P: the wave's 32 xn rows as the fc1 B operand, k-step kk, token tile ni
+    bf16x8 xf[12][2];
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni) {
+      const bf16_t* xr = X + (size_t)min(m0 + 32 * wq + 16 * ni + lr, M - 1) * q.lda + 8 * lg;
+#pragma unroll
+      for (int kk = 0; kk < 12; ++kk) xf[kk][ni] = *reinterpret_cast<const bf16x8*>(xr + 32 * kk);
+    }
+    f32x4 acc1[8][2];
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) acc1[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    // (the chunk's 4 phases unrolled: xf is indexed by compile-time k-steps only, so it stays in
+    // registers)
+    for (int t = 0; t < NCH; ++t) {
+#pragma unroll
+      for (int sub = 0; sub < 4; ++sub) {
+        const int ph = 4 * t + sub;
+        asm volatile("" ::: "memory");
+        issue(ph + 1);
+        const bf16_t* img = ring + (ph & 1) * kWsSlot;
+        f32x4 b1v[8];
+        if (sub == 3) {
+#pragma unroll
+          for (int mi = 0; mi < 8; ++mi)
+            b1v[mi] = q.bias ? *reinterpret_cast<const f32x4*>(q.bias + t * HC + 16 * mi + 4 * lg)
+                             : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int k3 = 0; k3 < 3; ++k3) {
+#pragma unroll
+          for (int mi = 0; mi < 8; ++mi) {
+            const bf16x8 a = *reinterpret_cast<const bf16x8*>(img + k3 * kWsW1Img + (16 * mi + lr) * BK + ch);
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni)
+              acc1[mi][ni] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, xf[3 * sub + k3][ni], acc1[mi][ni], 0, 0, 0);
+          }
+          __builtin_amdgcn_sched_barrier(0);  // keep the next k-step's fragment reads out of this one
+        }
+        if (sub == 3) {  // the chunk's fc1 is complete: + b1, GELU, bf16 -> H[t % 2]
+          bf16_t* Hs = Hb + (t & 1) * BM * HC;
+#pragma unroll
+          for (int mi = 0; mi < 8; ++mi) {
+#pragma unroll
+            for (int ni = 0; ni < 2; ++ni) {
+              const int hb = 16 * mi + 4 * lg, tok = 32 * wq + 16 * ni + lr;
+              bf16x4 o;
+#pragma unroll
+              for (int r = 0; r < 4; ++r) o[r] = (bf16_t)gelu_fast(acc1[mi][ni][r] + b1v[mi][r]);
+              *reinterpret_cast<bf16x4*>(Hs + tok * HC + (((hb >> 3) ^ (tok & 15)) * 8) + (hb & 7)) = o;
+              acc1[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+            __builtin_amdgcn_sched_barrier(0);  // one tile pair at a time: bounded temporaries
+          }
+        }
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+      }
+    }
+    for (int ph = 4 * NCH; ph < NPH; ++ph) {  // the Q waves' last chunk
+      asm volatile("" ::: "memory");
+      issue(ph + 1);
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+    const float inv_rpm = 1.0f / (float)p.rows_per_mod;
+    float4 h4[2][NCOL / 128];
+    auto no_stage = [&](int, float*) {};
+    rowln_fast_epilogue_impl<NCOL, 3, true>(p, no_stage, h4, smem, m0, fdiv(m0, p.rows_per_mod, inv_rpm), inv_rpm);
+  } else {
+    f32x4 acc2[8][NQ];
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+      for (int nj = 0; nj < NQ; ++nj) acc2[mi][nj] = f32x4{0.f, 0.f, 0.f, 0.f};
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    for (int ph = 0; ph < 4; ++ph) {  // the P waves' first chunk
+      asm volatile("" ::: "memory");
+      issue(ph + 1);
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+    for (int u = 0; u < NCH; ++u) {
+#pragma unroll
+      for (int sub = 0; sub < 4; ++sub) {
+        const int ph = 4 * (u + 1) + sub;
+        asm volatile("" ::: "memory");
+        issue(ph + 1);
+        const bf16_t* Hs = Hb + (u & 1) * BM * HC;
+        const bf16_t* img = ring + (ph & 1) * kWsSlot + 3 * kWsW1Img;
+        // two halves of 4 token tiles (fewer live fragment registers beside the 192 accumulators)
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+          bf16x8 a[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int row = 16 * (4 * hf + i) + lr;
+            a[i] = *reinterpret_cast<const bf16x8*>(Hs + row * HC + (((sub * 4 + lg) ^ (row & 15)) * 8));
+          }
+#pragma unroll
+          for (int nj = 0; nj < NQ; ++nj) {
+            const bf16x8 b = *reinterpret_cast<const bf16x8*>(img + (96 * wq + 16 * nj + lr) * BK + ch);
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+              acc2[4 * hf + i][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b, acc2[4 * hf + i][nj], 0, 0, 0);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+      }
+    }
+    const float inv_rpm = 1.0f / (float)p.rows_per_mod;
+    float4 h4[2][NCOL / 128];
+    // band b = accumulator rows 16 mi + 4 lg + r with mi in {2b, 2b+1}; columns 96 wq + 16 nj + lr.
+    // Bands 0-2 go to stage regions 0-2 at band 0 (144 accumulator VGPRs freed before the row
+    // work), band 3 to region 0 once band 0 is done
+    auto stage_band = [&](int band, float* stage) {
+      if (band == 1 || band == 2) return;
+#pragma unroll
+      for (int mi = 0; mi < 8; ++mi) {
+        if (band == 0 ? mi >= 6 : mi < 6) continue;
+        float* rg = stage + ((mi >> 1) % 3) * 32 * LDS_ST;
+#pragma unroll
+        for (int nj = 0; nj < NQ; ++nj)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            rg[((mi & 1) * 16 + lg * 4 + r) * LDS_ST + 96 * wq + 16 * nj + lr] = acc2[mi][nj][r];
+      }
+    };
+    rowln_fast_epilogue_impl<NCOL, 3, true>(p, stage_band, h4, smem, m0, fdiv(m0, p.rows_per_mod, inv_rpm), inv_rpm);
   }
 }
 
@@ -1868,11 +2113,24 @@ int mlp_split_factor(int M, int F) {
   return best;
 }
 
+// MDG_MLP_WS=1 selects the wave-specialised kernel for large M (A/B knob; off by default: it
+// measured 168 vs 130 us at M = 32 000 — each phase's 48 KiB ring slot is issued only one
+// phase (~0.7 us) ahead of its use while an LDS-DMA fill takes ~1.1 us to land, and LDS has no
+// room for a third slot beside the double-buffered H)
+static bool mlp_ws_on() {
+  static const bool on = [] {
+    const char* e = getenv("MDG_MLP_WS");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
 hipError_t mlp_fused_launch(const mdg_gemm_desc& f1, const mdg_gemm_desc& f2, hipStream_t s, float* part) {
   static bool attr_set = false;
   if (!attr_set) {
     for (const void* k : {reinterpret_cast<const void*>(&mlp_rowln_kernel<384, false>),
-                          reinterpret_cast<const void*>(&mlp_rowln_kernel<384, true>)}) {
+                          reinterpret_cast<const void*>(&mlp_rowln_kernel<384, true>),
+                          reinterpret_cast<const void*>(&mlp_ws_kernel<384>)}) {
       hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       if (e != hipSuccess) return e;
     }
@@ -1889,6 +2147,10 @@ hipError_t mlp_fused_launch(const mdg_gemm_desc& f1, const mdg_gemm_desc& f2, hi
     if (hipError_t e = hipGetLastError()) return e;
     hipLaunchKernelGGL((mlp_split_reduce_kernel<384>), dim3((f1.M + 3) / 4), dim3(256), 0, s, f2, (const float*)part,
                        a.nsplit);
+    return hipGetLastError();
+  }
+  if (mlp_ws_on()) {
+    hipLaunchKernelGGL((mlp_ws_kernel<384>), dim3(tiles), dim3(kWsThreads), kWsSmem, s, a);
     return hipGetLastError();
   }
   hipLaunchKernelGGL((mlp_rowln_kernel<384, false>), dim3(tiles), dim3(kMlpThreads), mlp_smem(f1.N), s, a);
@@ -2012,6 +2274,7 @@ __global__ __launch_bounds__(kRqThreads, 1) void rowln_qkv_kernel(const RqArgs a
       if (younger >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * (1 + WLD)) : "memory");
       else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(1 + WLD) : "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // ring reads retired (see kRingWaitNote)
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       if (kt + STAGES - 1 < nk) load((kt + STAGES - 1) % STAGES, (kt + STAGES - 1) * BK);
@@ -2124,6 +2387,7 @@ __global__ __launch_bounds__(kRqThreads, 1) void rowln_qkv_kernel(const RqArgs a
         // chunk's 8 stores in flight; then refill the slot step s - 1 used with step s + 3
         const int younger = min(2, QSTEPS - 1 - s);
         vm_wait_4x(4 * younger + (full && n > 0 ? 8 : 0));
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // ring reads retired (see kRingWaitNote)
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         if (s + 3 < QSTEPS) qissue(s + 3);

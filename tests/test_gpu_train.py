@@ -85,7 +85,7 @@ def _model_loss(m, d, device):
 
 
 # grad tolerance per train path: ||g - g_ref|| / ||g_ref|| per parameter (and for the loss)
-TRAIN_TOL = {"torch": (1e-5, 1e-4), "hip-f32": (1e-5, 1e-4), "hip-bf16": (1e-2, 5e-2)}
+TRAIN_TOL = {"torch": (1e-5, 1e-4), "hip-f32": (1e-5, 1e-4), "hip-bf16": (1e-3, 2.5e-2)}
 
 
 def _log_train(rec):
@@ -146,7 +146,8 @@ def test_hip_layer_backward_matches_eager_autograd(dtype, T, L, n_pad):
     module on the same inputs (random upstream gradient): d h_in, d mods (adaLN) and every
     parameter gradient.  Covers the L = 4 quad spatial kernels, a query tail (T = 70), padded
     residues (key-padding), the generic spatial path (L = 6) and the L >= 16 route (spatial
-    attention on the temporal MFMA kernel).  f32: rel <= 1e-4; bf16: rel <= 5e-2."""
+    attention on the temporal MFMA kernel).  f32: rel <= 1e-4; bf16: rel <= 4.5e-2 (2x the worst
+    observed, 2.24e-2: profiles/r03_parity_train.jsonl)."""
     import argparse
 
     from mdgen_finetune_amd import synthetic
@@ -172,7 +173,7 @@ def test_hip_layer_backward_matches_eager_autograd(dtype, T, L, n_pad):
     # HIP Function (mods from the same adaLN module)
     out = hip_layer_forward(hl, layer, h, layer.adaLN_modulation(c), mask)
     gots = torch.autograd.grad(out, [h, c] + list(layer.parameters()), gout)
-    tol = 1e-4 if dtype == "f32" else 5e-2
+    tol = 1e-4 if dtype == "f32" else 4.5e-2
     fwd = float((out - out_ref).norm() / out_ref.norm())
     names = ["h", "c"] + [n for n, _ in layer.named_parameters()]
     worst = (fwd, "forward")
@@ -254,7 +255,7 @@ def test_default_dims_training_grads_match_oracle(dtype):
     assert checked > 250
 
 
-BF16_DEFAULT_GRAD = 5e-2
+BF16_DEFAULT_GRAD = 3.5e-2  # 2x the worst observed (1.63e-2, layers.4.mha_t.attn.k_proj.bias)
 
 
 def _fixed_noise(tr, B, shape, seed=5):
@@ -273,7 +274,7 @@ def test_graphed_step_equals_eager_step():
 
     res = {}
     for mode in (0, 1):
-        a = _args(["--lr", "1e-3", "--embed_dim", "96", "--mha_heads", "4", "--ema", "--train_graph", str(mode)])
+        a = _args(["--lr", "1e-3", "--embed_dim", "192", "--mha_heads", "8", "--ema", "--train_graph", str(mode)])
         tr = Trainer(a, device=torch.device("cuda"))
         assert tr.graph_mode == bool(mode)
         b = _batch(a, B=2)
@@ -301,7 +302,7 @@ def _share_worker(rank, world, port, graph, out):
     from mdgen_finetune_amd.train import Trainer, setup_distributed
 
     r, w, dev = setup_distributed()
-    a = _args(["--grad_clip", "0", "--embed_dim", "96", "--mha_heads", "4", "--train_graph", str(graph),
+    a = _args(["--grad_clip", "0", "--embed_dim", "192", "--mha_heads", "8", "--train_graph", str(graph),
                "--bucket_cap_mb", "0.25"])
     tr = Trainer(a, r, w, dev)
     assert tr.graph_mode == bool(graph)

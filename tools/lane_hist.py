@@ -44,19 +44,29 @@ class HistLib:
                 return st
         raise KeyError(ws)
 
+    def regions(self, st):
+        """name -> (byte offset, bytes) of the workspace regions a layer writes (bf16 packed planes)."""
+        off = _lib.workspace_offsets(st.dims)
+        N, C, d = st.N, self._eng.C, st.dims
+        a = lambda x: (x + 255) // 256 * 256  # noqa: E731
+        part = off["kbias"] + a(d.B * d.L * d.T * 4) + a(N * 4)
+        return {"xn": (off["xn"], N * C * 2), "o": (off["o"], N * C * 2),
+                "qkv_t": (off["qkv_t"], 3 * d.B * d.L * d.H * d.T * d.D * 2), "mlp_part": (part, 12 * N * C * 4)}
+
     def _snap(self, ws, stream):
         st = self._state(ws)
-        off = _lib.workspace_offsets(st.dims)
-        N, C = st.N, self._eng.C
         i = self.count.get(ws, 0)
         self.count[ws] = i + 1
         lst = self.hist.setdefault(ws, [])
+        regs = self.regions(st)
         if i == len(lst):
-            lst.append((torch.empty(N, C, device="cuda"), torch.empty(N * C, dtype=torch.bfloat16, device="cuda")))
-        h, xn = lst[i]
+            lst.append({"h": torch.empty(st.N, self._eng.C, device="cuda"),
+                        **{k: torch.empty(n, dtype=torch.uint8, device="cuda") for k, (o, n) in regs.items()}})
+        snap = lst[i]
         with torch.cuda.stream(torch.cuda.ExternalStream(stream)):
-            h.copy_(st.h)
-            xn.copy_(st.ws[off["xn"]:off["xn"] + N * C * 2].view(torch.bfloat16))
+            snap["h"].copy_(st.h)
+            for k, (o, n) in regs.items():
+                snap[k].copy_(st.ws[o:o + n])
 
     def _layers(self, m, io, mask, ws, first, last, stream):
         for k in range(first, last):
@@ -78,7 +88,8 @@ def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 200
     lanes = int(sys.argv[2]) if len(sys.argv) > 2 else 3
     offset = int(sys.argv[3]) if len(sys.argv) > 3 else 1
-    B, T, L = 6, 64, 4
+    B = int(sys.argv[4]) if len(sys.argv) > 4 else 6
+    T, L = 64, 4
     cfg = dict(flags=[], latent_dim=21, L=L, T=T, tps=False, weights_seed=3)
     m, _ = build_model(cfg, "cuda", T=T)
     m.hip_dtype = "bf16"
@@ -94,7 +105,7 @@ def main():
     ref = eng.sample_euler(g("x"), num_steps=6, use_graph=False, **kw)
     torch.cuda.synchronize()
     chain_ws = [ws for ws in hl.hist][0]
-    chain = [(h.clone(), x.clone()) for h, x in hl.hist[chain_ws]]
+    chain = [{k: v.clone() for k, v in snap.items()} for snap in hl.hist[chain_ws]]
     eng.lanes, eng.lane_offset = lanes, offset
     eng._graphs.clear()
     cap = eng._capture
@@ -122,17 +133,32 @@ def main():
             k = st_lane = [key for key, v in eng._states.items() if v is st][0][3] - 1
             rows = slice(k * Bl * T * L, (k + 1) * Bl * T * L)
             first = None
-            for i, (h, xn) in enumerate(lst[: len(chain)]):
-                hc, xc = chain[i]
-                dh = (h - hc[rows]).abs()
-                dx = (xn.float().view(-1, eng.C) - xc.float().view(-1, eng.C)[rows]).abs()
-                if bool((dh > 0).any()) or bool((dx > 0).any()):
-                    bad_rows = ((dh > 0).any(1) | (dx > 0).any(1)).nonzero().flatten()
-                    frames = sorted({int(x) // L for x in bad_rows.tolist()})
-                    first = {"call": i, "step": i // nl, "layer": i % nl, "h_max": float(dh.max()),
-                             "xn_max": float(dx.max()), "n_rows": int(bad_rows.numel()),
-                             "frames_lo_hi": [frames[0], frames[-1]], "n_frames": len(frames),
-                             "h_rows": int((dh > 0).any(1).sum()), "xn_rows": int((dx > 0).any(1).sum())}
+            C, H, D = eng.C, eng.H, eng.D
+            NL = Bl * T * L
+            for i, snap in enumerate(lst[: len(chain)]):
+                ref_s = chain[i]
+                diff = {}
+                # row regions: lane rows <-> chain rows [k NL, (k+1) NL)
+                for name, width, dt in (("h", C, torch.float32), ("xn", C, torch.bfloat16), ("o", C, torch.bfloat16)):
+                    a = snap[name].view(dt).view(-1, width) if name != "h" else snap[name]
+                    b = (ref_s[name].view(dt).view(-1, width) if name != "h" else ref_s[name])[k * NL:(k + 1) * NL]
+                    bad = (a != b).any(1).nonzero().flatten()
+                    if bad.numel():
+                        diff[name] = {"rows": int(bad.numel()), "lo": int(bad[0]), "hi": int(bad[-1]),
+                                      "max": float((a.float() - b.float()).abs().max())}
+                # planes [3][seq][H][T*D]: lane seq s <-> chain seq k*Bl*L + s
+                pa = snap["qkv_t"].view(torch.bfloat16).view(3, Bl * L, H, T * D)
+                pb = ref_s["qkv_t"].view(torch.bfloat16).view(3, B * L, H, T * D)[:, k * Bl * L:(k + 1) * Bl * L]
+                bad = (pa != pb).any(-1).nonzero()
+                if bad.numel():
+                    diff["qkv_t"] = {"n": int(bad.shape[0]), "which_seq_head": bad[:6].tolist()}
+                ma = snap["mlp_part"].view(torch.float32).view(12, NL, C)
+                mb = ref_s["mlp_part"].view(torch.float32).view(12, B * T * L, C)[:, k * NL:(k + 1) * NL]
+                bad = (ma != mb).any(-1).nonzero()
+                if bad.numel():
+                    diff["mlp_part"] = {"n": int(bad.shape[0]), "split_row": bad[:6].tolist()}
+                if diff:
+                    first = {"call": i, "step": i // nl, "layer": i % nl, "diff": diff}
                     break
             rep["lanes"].append({"lane": st_lane, "first": first})
         print(json.dumps(rep), flush=True)
