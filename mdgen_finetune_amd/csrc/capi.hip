@@ -6,6 +6,7 @@
 #include <string.h>
 
 #include <string>
+#include <vector>
 
 #include "../../include/mdgen_hip.h"
 #include "common.h"
@@ -102,8 +103,66 @@ int fail(int code, const char* fmt, ...) {
   return code;
 }
 
+// Diagnostic (MDG_DEBUG_COHERENCE, tools/lane_hist.py): inside a denoise step every checked
+// launch is followed by a small kernel on the same stream.  =1: each of its waves performs an
+// agent-scope release + acquire (L2 write-back + invalidate on the XCD it runs on, L1 invalidate
+// on its CU); =2: the same launch with an empty body (timing control).
+__global__ void coherence_kernel(int fence) {
+  if (fence) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+}
+
+thread_local hipStream_t g_dbg_stream = nullptr;  // the denoise step's stream (may be the null stream)
+thread_local bool g_dbg_in_step = false;
+
+// Diagnostic (tools/lane_snap.py): with a snapshot buffer set (mdg_debug_snapshots), every
+// checked launch inside a denoise step is followed by device copies of the step's workspace,
+// residual h and latents x into the next free slot of the buffer, on the launch's stream (so a
+// captured graph replays them).  Slots are labelled with the launch and the workspace pointer.
+struct DbgRegion {
+  const void* p;
+  size_t n;
+};
+thread_local DbgRegion g_dbg_regions[3];
+struct DbgSnap {
+  char* dst = nullptr;
+  size_t cap = 0, used = 0;
+  std::vector<std::string> label;
+  std::vector<size_t> off;
+  std::vector<const void*> ws;
+};
+DbgSnap g_snap;
+
+void debug_snapshot(const char* what) {
+  size_t need = 0;
+  for (const DbgRegion& r : g_dbg_regions) need += (r.n + 255) & ~(size_t)255;
+  if (!g_snap.dst || g_snap.used + need > g_snap.cap) return;
+  g_snap.label.push_back(what);
+  g_snap.off.push_back(g_snap.used);
+  g_snap.ws.push_back(g_dbg_regions[0].p);
+  for (const DbgRegion& r : g_dbg_regions) {
+    if (r.n) (void)hipMemcpyAsync(g_snap.dst + g_snap.used, r.p, r.n, hipMemcpyDeviceToDevice, g_dbg_stream);
+    g_snap.used += (r.n + 255) & ~(size_t)255;
+  }
+}
+
+int debug_coherence() {
+  static const int v = [] {
+    const char* e = getenv("MDG_DEBUG_COHERENCE");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
 int hip_check(hipError_t e, const char* what) {
-  if (e == hipSuccess) return MDG_OK;
+  if (e == hipSuccess) {
+    if (g_dbg_in_step && debug_coherence())
+      hipLaunchKernelGGL(coherence_kernel, dim3(1024), dim3(64), 0, g_dbg_stream, debug_coherence() == 1 ? 1 : 0);
+    if (g_dbg_in_step && g_snap.dst) debug_snapshot(what);
+    return MDG_OK;
+  }
   return fail((int)e, "%s: %s", what, hipGetErrorString(e));
 }
 
@@ -501,6 +560,7 @@ static int layer_fwd_impl(const mdg_dims* d, const mdg_layer_weights* w, const f
     // q|k|v of the 4 residues stay on chip: projection + attention -> o in one launch
     q.epi = MDG_EPI_ATTN_SPATIAL; q.qscale = qs;
     q.out = o; q.ldo = C; q.kvb = w->kvb[0]; q.key_mask = mask;
+    q.qkv_out = qkv_s;  // unused by the product kernel (a diagnostic build dumps its q|k|v tile there)
     if (int e = mdg_gemm(&q, stream)) return e;
   } else {
     q.qkv_layout = MDG_QKV_SPATIAL; q.qkv_out = qkv_s; q.qscale = qs;
@@ -641,14 +701,31 @@ static int denoise_range(const mdg_model* m, const mdg_step_io* io, const float*
   return mdg_gemm(&g, stream);  // bf16: the one-pass final_euler_kernel
 }
 
+static int denoise_range_dbg(const mdg_model* m, const mdg_step_io* io, const float* mask, void* ws, int first,
+                             int last, void* stream) {
+  g_dbg_stream = (hipStream_t)stream;
+  g_dbg_in_step = true;
+  if (m && io && g_snap.dst) {
+    const mdg_dims& d = m->dims;
+    const size_t N = (size_t)d.B * d.T * d.L;
+    g_dbg_regions[0] = {ws, ws_layout(d).total};
+    g_dbg_regions[1] = {io->h, N * d.C * sizeof(float)};
+    g_dbg_regions[2] = {io->x_out ? io->x_out : io->x_in, N * d.latent * sizeof(float)};
+  }
+  const int e = denoise_range(m, io, mask, ws, first, last, stream);
+  g_dbg_stream = nullptr;
+  g_dbg_in_step = false;
+  return e;
+}
+
 int mdg_denoise_step(const mdg_model* m, const mdg_step_io* io, const float* mask, void* ws, void* stream) {
   if (!m) return fail(MDG_E_ARG, "denoise_step: null model/io");
-  return denoise_range(m, io, mask, ws, 0, m->dims.num_layers, stream);
+  return denoise_range_dbg(m, io, mask, ws, 0, m->dims.num_layers, stream);
 }
 
 int mdg_denoise_step_layers(const mdg_model* m, const mdg_step_io* io, const float* mask, void* ws,
                             int32_t first_layer, int32_t last_layer, void* stream) {
-  return denoise_range(m, io, mask, ws, first_layer, last_layer, stream);
+  return denoise_range_dbg(m, io, mask, ws, first_layer, last_layer, stream);
 }
 
 int mdg_describe_plan(const mdg_dims* d, char* buf, size_t n) {
@@ -1129,3 +1206,23 @@ int mdg_wgrad(int32_t dtype, int32_t N, int32_t M, int32_t K, const void* dy, in
 }
 
 }  // extern "C"
+
+// ---- diagnostics (not part of the ABI in include/mdgen_hip.h; tools/lane_snap.py)
+extern "C" int mdg_debug_snapshots(void* dst, size_t cap) {
+  g_snap.dst = (char*)dst;
+  g_snap.cap = dst ? cap : 0;
+  g_snap.used = 0;
+  g_snap.label.clear();
+  g_snap.off.clear();
+  g_snap.ws.clear();
+  return 0;
+}
+// i < 0: the number of snapshots taken; else slot i's byte offset, workspace and label
+extern "C" int mdg_debug_snapshot_info(int i, size_t* off, void** ws, char* label, size_t n) {
+  if (i < 0) return (int)g_snap.off.size();
+  if (i >= (int)g_snap.off.size()) return -1;
+  *off = g_snap.off[i];
+  *ws = (void*)g_snap.ws[i];
+  snprintf(label, n, "%s", g_snap.label[i].c_str());
+  return 0;
+}

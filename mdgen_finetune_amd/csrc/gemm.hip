@@ -1912,6 +1912,25 @@ __global__ __launch_bounds__(kWsThreads, 1) void mlp_ws_kernel(const MlpArgs arg
 // The split MLP's second pass: v = sum of the nsplit fc2 partials (split order), then exactly
 // the row-LN epilogue's arithmetic: h += gate * (v + b2), LayerNorm + adaLN modulate -> xn.
 // One wave per row, lane = columns 2 lane + 128 e.
+// Diagnostic build (MDG_DIAG_ORDER=1, tools/gpu_lane_race.sh "order"): launch-order check of
+// the split-MLP reduction -> next layer's fused spatial kernel hand-off.  Per xn buffer (hashed
+// slot) the reduction's blocks count their completion after a release fence, and every block of
+// the spatial kernel, before its first load, compares that count with the number the stream
+// order implies (spatial launch j of a lane follows j reductions of (M + 3) / 4 blocks).
+#ifndef MDG_DIAG_ORDER
+#define MDG_DIAG_ORDER 0
+#endif
+#if MDG_DIAG_ORDER
+struct OrderSlot {
+  unsigned long long key;
+  unsigned red, spa, err, worst;
+};
+__device__ OrderSlot g_order[61];
+__device__ __forceinline__ OrderSlot& order_slot(const void* xn) {
+  return g_order[((uintptr_t)xn >> 8) % 61];
+}
+#endif
+
 template <int NCOL>
 __global__ __launch_bounds__(256) void mlp_split_reduce_kernel(const mdg_gemm_desc p, const float* __restrict__ part,
                                                                int nsplit) {
@@ -1919,6 +1938,21 @@ __global__ __launch_bounds__(256) void mlp_split_reduce_kernel(const mdg_gemm_de
   constexpr int NE = NCOL / 128;
   const int lane = threadIdx.x & 63, m = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int M = p.M;
+#if MDG_DIAG_ORDER
+  struct Done {
+    const mdg_gemm_desc& p;
+    __device__ ~Done() {
+      if (!p.xn_out) return;
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        __threadfence();
+        OrderSlot& o = order_slot(p.xn_out);
+        o.key = (unsigned long long)(uintptr_t)p.xn_out;
+        atomicAdd(&o.red, 1u);
+      }
+    }
+  } done_{p};
+#endif
   if (m >= M) return;
   const size_t b = (size_t)(m / p.rows_per_mod);
   float2 v[NE];
@@ -2097,13 +2131,14 @@ int mlp_split_factor(int M, int F) {
     const char* e = getenv("MDG_MLP_SPLIT");
     return !(e && e[0] == '0');
   }();
-  // MDG_MLP_SPLIT_BLOCKS: grid cap (default 320).  Measured: 160 gives a two-lane TPS window
-  // (25 tiles per lane) 6 pieces instead of 12, +12.7 %, and a B = 1 window 4 instead of 6,
-  // -3.6 %; 240 (6 and 6) made test_concurrent_lanes_equal_single_chain[3-1] fail in 2 of 3
-  // full GPU suites (graph replay != single chain) — not understood, so 320 stays
+  // MDG_MLP_SPLIT_BLOCKS: grid cap (default 240).  Measured (round 2): 160 gives a two-lane TPS
+  // window (25 tiles per lane) 6 pieces instead of 12, +12.7 %, and a B = 1 window 4 instead of
+  // 6, -3.6 %; 240 gives 6 and 6.  (240 was held back in round 2 by a rare concurrent-lane
+  // divergence; its cause was the fused spatial kernel's misaligned RoPE loads, fixed in round 3,
+  // DESIGN.md §4.)
   static const int cap = [] {
     const char* e = getenv("MDG_MLP_SPLIT_BLOCKS");
-    return e ? atoi(e) : 320;
+    return e ? atoi(e) : 240;
   }();
   const int tiles = (M + 127) / 128, nch = F / kMlpHC;
   if (!on || tiles >= 64 || nch < 2) return 1;
@@ -2556,15 +2591,34 @@ __device__ __forceinline__ void quad_pv6(float* o, const float* v, float p0, flo
 }
 
 
-// diagnostics of the lane-offset graph divergence (tools/gpu_lane_race.sh): 1 = agent-scope
-// acquire fence at kernel start, 2 = the DPP products through the compiler's quad_bc instead
-// of the inline v_fmac_f32_dpp blocks.  Never set in the product build.
+// diagnostic builds of the fused spatial kernel (tools/gpu_lane_race.sh, tools/lane_snap.py;
+// DESIGN.md §4 "Concurrent-lane divergence"), never set in the product build: 2 = the DPP
+// products through the compiler's quad_bc instead of the inline v_fmac_f32_dpp blocks; 8 = each
+// band's q|k|v tile also written to p.qkv_out (the spatial q|k|v workspace region, unused on
+// this path); 9 = every lane's attention evaluated a second time (same code, the stage address
+// made opaque) with both traces logged where the results differ.
 #ifndef MDG_DIAG_SPA
 #define MDG_DIAG_SPA 0
 #endif
+#if MDG_DIAG_SPA == 9
+__device__ unsigned g_spa_diag[4 + 32 * 128];  // [0] = mismatching lanes, then 32-word records
+#endif
 template <int S>  // ring depth (K-steps)
 __global__ __launch_bounds__(kSpaThreads) void gemm_qkv_attn_spatial_kernel(const mdg_gemm_desc p) {
-  if (MDG_DIAG_SPA == 1) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#if MDG_DIAG_ORDER
+  if (threadIdx.x == 0) {
+    OrderSlot& o = order_slot(p.A);
+    const unsigned nwg_ = (unsigned)((p.H / 2) * ((p.M + 127) / 128));
+    const unsigned j = atomicAdd(&o.spa, 1u) / nwg_;
+    const unsigned red = __hip_atomic_load(&o.red, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned want = j * (unsigned)((p.M + 3) / 4);
+    if (red < want) {
+      atomicAdd(&o.err, 1u);
+      atomicMax(&o.worst, want - red);
+    }
+  }
+  __syncthreads();
+#endif
   constexpr int D = 24, HP = 2, BM = 128, BN = kSpaBN, BK = 32, NF = BN / 16, HD = HP * D;
   constexpr int ATILE = BM * BK, STAGE = (BM + BN) * BK, LDS_ST = kSpaLdsSt;
   typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -2673,70 +2727,150 @@ __global__ __launch_bounds__(kSpaThreads) void gemm_qkv_attn_spatial_kernel(cons
       for (int r = 0; r < 4; ++r)
         stage[(16 * wave + lg * 4 + r) * LDS_ST + j * 16 + lr] = (acc[band][j][r] + bcol[j]) * scol[j];
     __syncthreads();
+    if (MDG_DIAG_SPA == 8 && p.qkv_out) {  // the band's q|k|v tile (before RoPE) -> [M][H / 2][144] bf16
+      for (int i = tid; i < 64 * BN; i += kSpaThreads) {
+        const int rr = i / BN, cc = i - rr * BN, mm = m0 + band * 64 + rr;
+        if (mm < M) reinterpret_cast<bf16_t*>(p.qkv_out)[(size_t)mm * (p.H / 2) * BN + pair * BN + cc] = (bf16_t)stage[rr * LDS_ST + cc];
+      }
+    }
     const int row = f * 4 + jr, m = m0 + band * 64 + row;
-    const float* srow = stage + row * LDS_ST + hh * D + c0;
-    float q[12], k[12], v[12];
+    // the band's attention for this lane (a lambda so the diagnostic build can evaluate it twice)
+    auto attend = [&](auto vol, float (&o)[12], int rowx, unsigned* trace) {
+      constexpr bool VOL = decltype(vol)::value;
+      typedef typename std::conditional<VOL, const volatile float, const float>::type cf;
+      cf* srow = stage + rowx * LDS_ST + hh * D + c0;
+      const bool rope = p.rope != nullptr;
+      cf* kb = kbh;
+      cf* kmask = p.key_mask;
+      float q[12], k[12], v[12];
+      if constexpr (VOL) {
 #pragma unroll
-    for (int c = 0; c < 12; c += 4) {
-      const float4 a4 = *reinterpret_cast<const float4*>(srow + c);
-      const float4 b4 = *reinterpret_cast<const float4*>(srow + HD + c);
-      const float4 v4 = *reinterpret_cast<const float4*>(srow + 2 * HD + c);
-      q[c] = a4.x; q[c + 1] = a4.y; q[c + 2] = a4.z; q[c + 3] = a4.w;
-      k[c] = b4.x; k[c + 1] = b4.y; k[c + 2] = b4.z; k[c + 3] = b4.w;
-      v[c] = v4.x; v[c + 1] = v4.y; v[c + 2] = v4.z; v[c + 3] = v4.w;
-    }
-    if (p.rope) {  // fair-esm rotate-half on the pair-interleaved columns, position l = jr
-      constexpr int half = D / 2;
+        for (int c = 0; c < 12; ++c) {
+          q[c] = srow[c];
+          k[c] = srow[HD + c];
+          v[c] = srow[2 * HD + c];
+        }
+      } else {
 #pragma unroll
-      for (int i = 0; i < 6; ++i) {
-        const int pi = dh * 6 + i;
-        const float cs = p.rope[jr * half + pi], sn = p.rope[(p.rope_rows + jr) * half + pi];
-        const float q0 = q[2 * i], q1 = q[2 * i + 1], k0 = k[2 * i], k1 = k[2 * i + 1];
-        q[2 * i] = q0 * cs - q1 * sn; q[2 * i + 1] = q1 * cs + q0 * sn;
-        k[2 * i] = k0 * cs - k1 * sn; k[2 * i + 1] = k1 * cs + k0 * sn;
+        for (int c = 0; c < 12; c += 4) {
+          const float4 a4 = *reinterpret_cast<const float4*>(srow + c);
+          const float4 b4 = *reinterpret_cast<const float4*>(srow + HD + c);
+          const float4 v4 = *reinterpret_cast<const float4*>(srow + 2 * HD + c);
+          q[c] = a4.x; q[c + 1] = a4.y; q[c + 2] = a4.z; q[c + 3] = a4.w;
+          k[c] = b4.x; k[c + 1] = b4.y; k[c + 2] = b4.z; k[c + 3] = b4.w;
+          v[c] = v4.x; v[c + 1] = v4.y; v[c + 2] = v4.z; v[c + 3] = v4.w;
+        }
       }
-    }
-    const float kvalid = (!p.key_mask || p.key_mask[min(m, M - 1)] != 0.f) ? 1.f : 0.f;
-    float sb = 0.f, s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+      if (MDG_DIAG_SPA == 9 && trace) {
+        unsigned hq = 0, hk = 0, hv = 0;
 #pragma unroll
-    for (int c = 0; c < 12; ++c) sb += q[c] * kbh[c0 + c];
-    if (MDG_DIAG_SPA == 2) {
-#pragma unroll
-      for (int c = 0; c < 12; ++c) {
-        s0 = fmaf(quad_bc<0>(k[c]), q[c], s0); s1 = fmaf(quad_bc<1>(k[c]), q[c], s1);
-        s2 = fmaf(quad_bc<2>(k[c]), q[c], s2); s3 = fmaf(quad_bc<3>(k[c]), q[c], s3);
+        for (int c = 0; c < 12; ++c) {
+          hq = hq * 31u + __float_as_uint(q[c]); hk = hk * 31u + __float_as_uint(k[c]); hv = hv * 31u + __float_as_uint(v[c]);
+        }
+        trace[0] = hq; trace[1] = hk; trace[2] = hv;
       }
-    } else {
-      quad_dots6(q, k, s0, s1, s2, s3);
-      quad_dots6(q + 6, k + 6, s0, s1, s2, s3);
-    }
-    sb += __shfl_xor(sb, 4, 64); s0 += __shfl_xor(s0, 4, 64); s1 += __shfl_xor(s1, 4, 64);
-    s2 += __shfl_xor(s2, 4, 64); s3 += __shfl_xor(s3, 4, 64);
-    const float v0 = quad_bc<0>(kvalid), v1 = quad_bc<1>(kvalid), v2 = quad_bc<2>(kvalid), v3 = quad_bc<3>(kvalid);
-    float mx = sb;  // the bias key is never masked (mha.py:273-280)
-    if (v0 != 0.f) mx = fmaxf(mx, s0);
-    if (v1 != 0.f) mx = fmaxf(mx, s1);
-    if (v2 != 0.f) mx = fmaxf(mx, s2);
-    if (v3 != 0.f) mx = fmaxf(mx, s3);
-    const float pb = expf(sb - mx);
-    const float p0 = v0 != 0.f ? expf(s0 - mx) : 0.f, p1 = v1 != 0.f ? expf(s1 - mx) : 0.f;
-    const float p2 = v2 != 0.f ? expf(s2 - mx) : 0.f, p3 = v3 != 0.f ? expf(s3 - mx) : 0.f;
-    const float inv = 1.0f / (pb + p0 + p1 + p2 + p3);
+      if (rope) {  // fair-esm rotate-half on the pair-interleaved columns, position l = jr
+        // The lane's 6 cos and 6 sin values start at float (jr * 12 + dh * 6): 8-B aligned, not
+        // 16-B.  Read as scalar floats, the compiler merged them into global_load_dwordx4 at that
+        // 8-B alignment, and such loads returned wrong data for lanes 48-63 of a wave, rarely and
+        // only with another kernel's blocks on the CU (the concurrent-lane divergence of
+        // DESIGN.md §4; this change alone: 0 vs 46 divergent replays of 1 200).  Each lane now
+        // reads its position's whole 12-float row as three 16-B-aligned float4 and keeps its half.
+        constexpr int half = D / 2;
+        static_assert(half == 12, "row = 3 float4");
+        const float4* rc = reinterpret_cast<const float4*>(p.rope + jr * half);
+        const float4* rs = reinterpret_cast<const float4*>(p.rope + (p.rope_rows + jr) * half);
+        const float4 c4[3] = {rc[0], rc[1], rc[2]}, s4[3] = {rs[0], rs[1], rs[2]};
+        auto pick = [&](const float4 (&r)[3], int e) {  // element e of the 12-float row
+          const float4 w = r[e >> 2];
+          return (e & 3) == 0 ? w.x : (e & 3) == 1 ? w.y : (e & 3) == 2 ? w.z : w.w;
+        };
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+          const float cs = dh ? pick(c4, 6 + i) : pick(c4, i), sn = dh ? pick(s4, 6 + i) : pick(s4, i);
+          const float q0 = q[2 * i], q1 = q[2 * i + 1], k0 = k[2 * i], k1 = k[2 * i + 1];
+          q[2 * i] = q0 * cs - q1 * sn; q[2 * i + 1] = q1 * cs + q0 * sn;
+          k[2 * i] = k0 * cs - k1 * sn; k[2 * i + 1] = k1 * cs + k0 * sn;
+        }
+      }
+      const float kvalid = (!kmask || kmask[min(m, M - 1)] != 0.f) ? 1.f : 0.f;
+      float sb = 0.f, s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+#pragma unroll
+      for (int c = 0; c < 12; ++c) sb += q[c] * kb[c0 + c];
+      if (MDG_DIAG_SPA == 2) {
+#pragma unroll
+        for (int c = 0; c < 12; ++c) {
+          s0 = fmaf(quad_bc<0>(k[c]), q[c], s0); s1 = fmaf(quad_bc<1>(k[c]), q[c], s1);
+          s2 = fmaf(quad_bc<2>(k[c]), q[c], s2); s3 = fmaf(quad_bc<3>(k[c]), q[c], s3);
+        }
+      } else {
+        quad_dots6(q, k, s0, s1, s2, s3);
+        quad_dots6(q + 6, k + 6, s0, s1, s2, s3);
+      }
+      if (MDG_DIAG_SPA == 9 && trace) {
+        trace[3] = __float_as_uint(sb); trace[4] = __float_as_uint(s0); trace[5] = __float_as_uint(s3);
+      }
+      sb += __shfl_xor(sb, 4, 64); s0 += __shfl_xor(s0, 4, 64); s1 += __shfl_xor(s1, 4, 64);
+      s2 += __shfl_xor(s2, 4, 64); s3 += __shfl_xor(s3, 4, 64);
+      if (MDG_DIAG_SPA == 9 && trace) {
+        trace[6] = __float_as_uint(sb); trace[7] = __float_as_uint(s0); trace[8] = __float_as_uint(s3);
+      }
+      const float v0 = quad_bc<0>(kvalid), v1 = quad_bc<1>(kvalid), v2 = quad_bc<2>(kvalid), v3 = quad_bc<3>(kvalid);
+      float mx = sb;  // the bias key is never masked (mha.py:273-280)
+      if (v0 != 0.f) mx = fmaxf(mx, s0);
+      if (v1 != 0.f) mx = fmaxf(mx, s1);
+      if (v2 != 0.f) mx = fmaxf(mx, s2);
+      if (v3 != 0.f) mx = fmaxf(mx, s3);
+      const float pb = expf(sb - mx);
+      const float p0 = v0 != 0.f ? expf(s0 - mx) : 0.f, p1 = v1 != 0.f ? expf(s1 - mx) : 0.f;
+      const float p2 = v2 != 0.f ? expf(s2 - mx) : 0.f, p3 = v3 != 0.f ? expf(s3 - mx) : 0.f;
+      const float inv = 1.0f / (pb + p0 + p1 + p2 + p3);
+      if (MDG_DIAG_SPA == 9 && trace) {
+        trace[9] = __float_as_uint(pb); trace[10] = __float_as_uint(p0); trace[11] = __float_as_uint(inv);
+      }
+#pragma unroll
+      for (int c = 0; c < 12; ++c) o[c] = pb * kb[MDG_DP + c0 + c];
+      if (MDG_DIAG_SPA == 2) {
+#pragma unroll
+        for (int c = 0; c < 12; ++c) {
+          o[c] = fmaf(quad_bc<0>(v[c]), p0, o[c]); o[c] = fmaf(quad_bc<1>(v[c]), p1, o[c]);
+          o[c] = fmaf(quad_bc<2>(v[c]), p2, o[c]); o[c] = fmaf(quad_bc<3>(v[c]), p3, o[c]);
+        }
+      } else {
+        quad_pv6(o, v, p0, p1, p2, p3);
+        quad_pv6(o + 6, v + 6, p0, p1, p2, p3);
+      }
+#pragma unroll
+      for (int c = 0; c < 12; ++c) o[c] *= inv;
+    };
     float o[12];
+#if MDG_DIAG_SPA == 9
+    unsigned tr1[12], tr2[12];
+    attend(std::false_type{}, o, row, tr1);
+    {  // evaluate again (same code, the stage row address made opaque so every LDS read is
+       // reissued) and log any lane whose result differs bit for bit, with both traces
+      float o2[12];
+      int row2 = row;
+      asm volatile("" : "+v"(row2));
+      attend(std::false_type{}, o2, row2, tr2);
+      int bad = -1;
 #pragma unroll
-    for (int c = 0; c < 12; ++c) o[c] = pb * kbh[MDG_DP + c0 + c];
-    if (MDG_DIAG_SPA == 2) {
+      for (int c = 0; c < 12; ++c)
+        if (__float_as_uint(o[c]) != __float_as_uint(o2[c]) && bad < 0) bad = c;
+      if (bad >= 0) {
+        const unsigned i = atomicAdd(&g_spa_diag[0], 1u);
+        if (i < 128) {
+          unsigned* e = g_spa_diag + 4 + 32 * i;
+          e[0] = blockIdx.x; e[1] = tid; e[2] = band; e[3] = bad;
+          e[4] = __float_as_uint(o[bad]); e[5] = __float_as_uint(o2[bad]); e[6] = (unsigned)m; e[7] = pair;
 #pragma unroll
-      for (int c = 0; c < 12; ++c) {
-        o[c] = fmaf(quad_bc<0>(v[c]), p0, o[c]); o[c] = fmaf(quad_bc<1>(v[c]), p1, o[c]);
-        o[c] = fmaf(quad_bc<2>(v[c]), p2, o[c]); o[c] = fmaf(quad_bc<3>(v[c]), p3, o[c]);
+          for (int t = 0; t < 12; ++t) { e[8 + t] = tr1[t]; e[20 + t] = tr2[t]; }
+        }
       }
-    } else {
-      quad_pv6(o, v, p0, p1, p2, p3);
-      quad_pv6(o + 6, v + 6, p0, p1, p2, p3);
     }
-#pragma unroll
-    for (int c = 0; c < 12; ++c) o[c] *= inv;
+#else
+    attend(std::false_type{}, o, row, nullptr);
+#endif
     if (m < M) {
       bf16_t* op = reinterpret_cast<bf16_t*>(p.out) + (size_t)m * p.ldo + gh * D + c0;
 #pragma unroll
@@ -2970,3 +3104,23 @@ hipError_t gemm_launch(const mdg_gemm_desc& p, const GemmPlan& g, hipStream_t s)
 }
 
 }  // namespace mdg
+
+#if MDG_DIAG_ORDER
+extern "C" int mdg_debug_order_counters(unsigned long long* out, int n) {
+  mdg::OrderSlot h[61];
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(mdg::g_order), sizeof(h)) != hipSuccess) return -1;
+  int k = 0;
+  for (int i = 0; i < 61 && k + 5 <= n; ++i)
+    if (h[i].key) {
+      out[k++] = h[i].key; out[k++] = h[i].red; out[k++] = h[i].spa; out[k++] = h[i].err; out[k++] = h[i].worst;
+    }
+  return k / 5;
+}
+#endif
+
+#if MDG_DIAG_SPA == 9
+extern "C" int mdg_debug_spa_diag(unsigned* out, int n) {
+  if (n < 4 + 32 * 128) return -1;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(mdg::g_spa_diag), sizeof(unsigned) * (4 + 32 * 128)) == hipSuccess ? 0 : -1;
+}
+#endif

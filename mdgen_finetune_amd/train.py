@@ -174,7 +174,14 @@ class Trainer:
         own = flat is None
         if own:
             flat = torch.cat([(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1) for p in params])
-        dist.all_reduce(flat)
+        if flat.is_cuda and dist.get_backend() == "gloo":
+            # gloo (the world-2 on-one-GPU tests, MDG_SHARE_GPU) reduces host memory: stage the
+            # buffer explicitly so no gloo worker thread touches the device between the graphs
+            host = flat.cpu()
+            dist.all_reduce(host)
+            flat.copy_(host)
+        else:
+            dist.all_reduce(flat)
         flat.div_(self.world)
         if own:
             off = 0

@@ -293,7 +293,10 @@ def test_graphed_step_equals_eager_step():
 
 
 def _share_worker(rank, world, port, graph, out):
+    import faulthandler
     import os
+
+    faulthandler.enable()
 
     import torch.distributed as dist
 
@@ -310,11 +313,15 @@ def _share_worker(rank, world, port, graph, out):
     _fixed_noise(tr, 2, (2, a.num_frames, a.crop, 21), seed=7 + rank)
     m = tr.wrapper.model
     params = [p for p in m.parameters() if p.requires_grad]
-    prep = tr.wrapper.prep_batch({k: (v.cuda() if torch.is_tensor(v) else v) for k, v in b.items()})
-    loss = tr.wrapper.transport.training_losses(m, prep["latents"], mask=prep["loss_mask"],
-                                                model_kwargs=prep["model_kwargs"])["loss"].mean()
-    local = torch.autograd.grad(loss, params, allow_unused=True)
-    local = torch.cat([(x if x is not None else torch.zeros_like(p)).flatten() for x, p in zip(local, params)])
+    def local_grads():  # returns no autograd state: the graph (and its AccumulateGrad nodes,
+        # created on this stream) must be gone before GraphedStep warms up on its side stream
+        prep = tr.wrapper.prep_batch({k: (v.cuda() if torch.is_tensor(v) else v) for k, v in b.items()})
+        loss = tr.wrapper.transport.training_losses(m, prep["latents"], mask=prep["loss_mask"],
+                                                    model_kwargs=prep["model_kwargs"])["loss"].mean()
+        g = torch.autograd.grad(loss, params, allow_unused=True)
+        return torch.cat([(x if x is not None else torch.zeros_like(p)).flatten() for x, p in zip(g, params)])
+
+    local = local_grads()
     ref = local.clone()
     dist.all_reduce(ref)
     ref /= w

@@ -17,6 +17,19 @@ for v in $VARIANTS; do
     fence) LA="3 1 $R" run fence MDG_LIB_PATH=$PWD/diaglib/spa1.so ;;
     dppc) LA="3 1 $R" run dppc MDG_LIB_PATH=$PWD/diaglib/spa2.so ;;
     nomlp) LA="3 1 $R" run nomlp MDG_FUSED_MLP=0 ;;
+    acq) LA="3 1 $R" run acq MDG_LIB_PATH=$PWD/diaglib/spa3.so ;;
+    sys) LA="3 1 $R" run sys MDG_LIB_PATH=$PWD/diaglib/spa4.so ;;
+    areg) LA="3 1 $R" run areg MDG_LIB_PATH=$PWD/diaglib/spa5.so ;;
+    sleep) LA="3 1 $R" run sleep MDG_LIB_PATH=$PWD/diaglib/spa6.so ;;
+    twice) LA="3 1 $R" run twice MDG_LIB_PATH=$PWD/diaglib/spa9.so ;;
+    vh) LA="3 1 $R" run vh MDG_LIB_PATH=$PWD/diaglib/vh.so ;;
+    vT) LA="3 1 $R" run vT MDG_LIB_PATH=$PWD/diaglib/vT.so ;;
+    vP) LA="3 1 $R" run vP MDG_LIB_PATH=$PWD/diaglib/vP.so ;;
+    vX) LA="3 1 $R" run vX MDG_LIB_PATH=$PWD/diaglib/vX.so ;;
+    o2) LA="3 2 $R" run o2 MDG_X=1 ;;
+    l2o1) LA="2 1 $R 4" run l2o1 MDG_X=1 ;;
+    vR) LA="3 1 $R" run vR MDG_LIB_PATH=$PWD/diaglib/vR.so ;;
+    order) LA="3 1 $R" run order MDG_LIB_PATH=$PWD/diaglib/order.so ;;
     *) echo "unknown $v"; false ;;
   esac || exit 1
 done

@@ -39,6 +39,49 @@ def locus(got, ref, Bl):
             "cs_first_step": sorted({int(i) for i in idx[:, 3].tolist()})[:24]}
 
 
+def order_counters():
+    """The MDG_DIAG_ORDER build's launch-order counters (xn buffer, reductions done, spatial
+    blocks started, blocks that started early, worst deficit), or None in other builds."""
+    import ctypes
+
+    from mdgen_finetune_amd import _lib
+
+    lib = _lib.load()
+    if not hasattr(lib, "mdg_debug_order_counters"):
+        return None
+    buf = (ctypes.c_ulonglong * 320)()
+    n = lib.mdg_debug_order_counters(buf, 320)
+    return [{"xn": hex(buf[5 * i]), "red": buf[5 * i + 1], "spa": buf[5 * i + 2], "early": buf[5 * i + 3],
+             "worst": buf[5 * i + 4]} for i in range(max(n, 0))]
+
+
+def spa_diag():
+    """The MDG_DIAG_SPA=9 build's log: lanes whose second evaluation of the fused spatial
+    attention differed from the first (block, thread, band, column, bits 1, bits 2, row, pair)."""
+    import ctypes
+
+    from mdgen_finetune_amd import _lib
+
+    lib = _lib.load()
+    if not hasattr(lib, "mdg_debug_spa_diag"):
+        return None
+    buf = (ctypes.c_uint * (4 + 32 * 128))()
+    lib.mdg_debug_spa_diag(buf, 4 + 32 * 128)
+    n = buf[0]
+    import struct
+
+    f = lambda u: struct.unpack("f", struct.pack("I", u))[0]  # noqa: E731
+    names = ["hq", "hk", "hv", "sb", "s0", "s3", "sb_x", "s0_x", "s3_x", "pb", "p0", "inv"]
+    recs = [list(buf[4 + 32 * i: 36 + 32 * i]) for i in range(min(n, 128))]
+    out = []
+    for r in recs:
+        t1, t2 = r[8:20], r[20:32]
+        out.append({"block": r[0], "tid": r[1], "band": r[2], "c": r[3], "o1": f(r[4]), "o2": f(r[5]), "m": r[6],
+                    "pair": r[7], "first_diff": next((names[i] for i in range(12) if t1[i] != t2[i]), None),
+                    "diffs": [names[i] for i in range(12) if t1[i] != t2[i]]})
+    return {"n": n, "records": out[:48]}
+
+
 def main():
     lanes, offset, reps = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3])
     B = int(sys.argv[4]) if len(sys.argv) > 4 else 6
@@ -64,11 +107,15 @@ def main():
         loc = locus(got, ref, Bl)
         if loc is not None:
             loc["replay"] = r
+            oc = order_counters()
+            if oc is not None:
+                loc["order"] = oc
             bad.append(loc)
             print(json.dumps(loc), flush=True)
     env = {k: v for k, v in os.environ.items() if k.startswith("MDG_")}
     print(json.dumps({"summary": True, "lanes": lanes, "offset": offset, "B": B, "T": T, "mode": mode, "reps": reps,
-                      "n_mismatch": len(bad), "env": env}), flush=True)
+                      "n_mismatch": len(bad), "env": env, "order": order_counters(), "spa_diag": spa_diag()}),
+          flush=True)
 
 
 if __name__ == "__main__":
