@@ -117,9 +117,9 @@ def time_kernel(fn, iters=20):
 
 
 def _traffic(kernel, B, T, L, dtype):
-    """HBM bytes per launch from the committed PMC pass (profiles/traffic_r02.json, FETCH_SIZE x2
+    """HBM bytes per launch from the committed PMC pass (profiles/traffic_r03.json, FETCH_SIZE x2
     + WRITE_SIZE per the gfx950 correction of MI355X_MICROARCH.md §HBM), or None."""
-    prof = os.path.join(REPO, "profiles", "traffic_r02.json")  # this round's PMC passes
+    prof = os.path.join(REPO, "profiles", "traffic_r03.json")  # this round's PMC passes
     try:
         return json.load(open(prof))[kernel].get(f"B{B}_T{T}_L{L}_{dtype}")
     except Exception:
