@@ -976,13 +976,30 @@ __host__ __device__ constexpr size_t rowln_smem() {
 // The row-LN fast epilogue (BM 128, 8 waves as 2 x 4, the tile spans <= 2 adaLN entries):
 // shared by gemm_rowln_kernel and the fused MLP kernel.  acc = the waves' 64 x NCOL/4
 // accumulator tiles; h4 = band 0's residual rows (rowln_load_band), already in flight.
-template <int NCOL>
-__device__ __forceinline__ void rowln_load_band(const mdg_gemm_desc& p, int m0, int u, float4 (&h4)[2][NCOL / 128]) {
+// Token row of a row-LN tile's local row r (0 .. 127).  RowsLinear: rows m0 .. m0 + 127 (every
+// kernel but one).  RowsFrames: 8 consecutive frames x 16 consecutive residues, r = 16 f + l
+// (the fused out_proj + q|k|v for the long residue axis, L % 16 == 0: each (residue, head)
+// plane then receives 8 consecutive 48-B rows from one block instead of one row from each of 8
+// blocks); rows of frames past the last map to M (invalid: loads clamp, stores skip).
+struct RowsLinear {
+  int m0;
+  __device__ int operator()(int r) const { return m0 + r; }
+};
+struct RowsFrames {
+  int f0, l0, L, nf, M;
+  __device__ int operator()(int r) const {
+    const int f = f0 + (r >> 4);
+    return f < nf ? f * L + l0 + (r & 15) : M;
+  }
+};
+
+template <int NCOL, typename RM>
+__device__ __forceinline__ void rowln_load_band(const mdg_gemm_desc& p, RM rows, int u, float4 (&h4)[2][NCOL / 128]) {
   constexpr int NE = NCOL / 128;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, half = lane >> 5, hl = lane & 31;
 #pragma unroll
   for (int pr = 0; pr < 2; ++pr) {
-    const int m = min(m0 + u * 32 + wave * 4 + 2 * pr + half, p.M - 1);
+    const int m = min(rows(u * 32 + wave * 4 + 2 * pr + half), p.M - 1);
     const float* hr = p.resid + (size_t)m * p.ldr + 4 * hl;
 #pragma unroll
     for (int e = 0; e < NE; ++e) h4[pr][e] = *reinterpret_cast<const float4*>(hr + 128 * e);
@@ -998,9 +1015,9 @@ __device__ __forceinline__ void rowln_load_band(const mdg_gemm_desc& p, int m0, 
 // bands 0-2 at once (at band 0's call; band 3 at its own) and free their registers early.
 // LATE_H: h4 is not loaded yet; band 0's residual rows are read right after band 0's staging (a
 // caller whose accumulators fill the registers until then).
-template <int NCOL, int NREG = 1, bool LATE_H = false, typename StageBand>
+template <int NCOL, int NREG = 1, bool LATE_H = false, typename StageBand, typename RM = RowsLinear>
 __device__ __forceinline__ void rowln_fast_epilogue_impl(const mdg_gemm_desc& p, StageBand stage_band,
-                                                         float4 (&h4)[2][NCOL / 128], unsigned char* smem, int m0,
+                                                         float4 (&h4)[2][NCOL / 128], unsigned char* smem, RM rows,
                                                          int b_lo, float inv_rpm, bf16_t* xlds = nullptr) {
   // no fp contraction: every kernel that inlines this epilogue (the row-LN GEMM, the fused MLP,
   // the fused out_proj + q|k|v) rounds h and xn identically
@@ -1009,10 +1026,10 @@ __device__ __forceinline__ void rowln_fast_epilogue_impl(const mdg_gemm_desc& p,
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int half = lane >> 5, hl = lane & 31;
   const int M = p.M;
-  const int b_hi = fdiv(min(m0 + BM - 1, M - 1), p.rows_per_mod, inv_rpm);
+  const int b_hi = fdiv(min(rows(BM - 1), M - 1), p.rows_per_mod, inv_rpm);
   float* stage = reinterpret_cast<float*>(smem);
   const float invN = 1.0f / (float)NCOL;
-  auto load_unit4 = [&](int u, float4 (&hb)[2][NE]) { rowln_load_band<NCOL>(p, m0, u, hb); };
+  auto load_unit4 = [&](int u, float4 (&hb)[2][NE]) { rowln_load_band<NCOL>(p, rows, u, hb); };
   float* emods = stage + NREG * 32 * LDS_ST;  // [2][3][NCOL]: gate | xn scale | xn shift
   // the caller's smem holds (32 * LDS_ST + 6 * NCOL) floats: the band stage + the adaLN rows
   static_assert(LDS_ST % 4 == 0, "16-B aligned stage rows");
@@ -1038,7 +1055,7 @@ __device__ __forceinline__ void rowln_fast_epilogue_impl(const mdg_gemm_desc& p,
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // previous band's stage reads (and the adaLN rows) are done
     stage_band(band, stage);
-    if (LATE_H && band == 0) rowln_load_band<NCOL>(p, m0, 0, h4);
+    if (LATE_H && band == 0) rowln_load_band<NCOL>(p, rows, 0, h4);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     const float* bstage = stage + (band % NREG) * 32 * LDS_ST;
     __builtin_amdgcn_s_barrier();
@@ -1048,7 +1065,7 @@ __device__ __forceinline__ void rowln_fast_epilogue_impl(const mdg_gemm_desc& p,
     int eb[2];
 #pragma unroll
     for (int pr = 0; pr < 2; ++pr) {
-      const int m = m0 + band * 32 + wave * 4 + 2 * pr + half;
+      const int m = rows(band * 32 + wave * 4 + 2 * pr + half);
       eb[pr] = fdiv(min(m, M - 1), p.rows_per_mod, inv_rpm) - b_lo;
       const float* srow = bstage + (wave * 4 + 2 * pr + half) * LDS_ST + 4 * hl;
       const float* gr = emods + eb[pr] * 3 * NCOL + 4 * hl;
@@ -1096,7 +1113,7 @@ __device__ __forceinline__ void rowln_fast_epilogue_impl(const mdg_gemm_desc& p,
         for (int pr = 0; pr < 2; ++pr) ss[pr] += __shfl_xor(ss[pr], o, 64);
 #pragma unroll
       for (int pr = 0; pr < 2; ++pr) {
-        const int m = m0 + band * 32 + wave * 4 + 2 * pr + half;
+        const int rl = band * 32 + wave * 4 + 2 * pr + half, m = rows(rl);
         const float rs = 1.0f / sqrtf(ss[pr] * invN + p.ln_eps);
         const float* mr = emods + eb[pr] * 3 * NCOL + 4 * hl;
 #pragma unroll
@@ -1107,7 +1124,7 @@ __device__ __forceinline__ void rowln_fast_epilogue_impl(const mdg_gemm_desc& p,
           const float o0 = (h.x - sum[pr]) * rs * (1.0f + xs.x) + xh.x, o1 = (h.y - sum[pr]) * rs * (1.0f + xs.y) + xh.y;
           const float o2 = (h.z - sum[pr]) * rs * (1.0f + xs.z) + xh.z, o3 = (h.w - sum[pr]) * rs * (1.0f + xs.w) + xh.w;
           if (xlds) {
-            const int r = m - m0, col = 4 * hl + 128 * e, cw = col & 31;
+            const int r = rl, col = 4 * hl + 128 * e, cw = col & 31;
             st4<bf16_t>(xlds + (col >> 5) * (BM * 32) + r * 32 + (((cw >> 3) ^ ((-(r >> 2)) & 3)) * 8) + (cw & 7), o0, o1,
                         o2, o3);
           } else if (m < M) {
@@ -1125,9 +1142,9 @@ __device__ __forceinline__ void rowln_fast_epilogue_impl(const mdg_gemm_desc& p,
 
 // The 8-wave (2 x 4) accumulator layout of the row-LN GEMM / fused MLP / fused out_proj + qkv:
 // wave (wm, wn) holds rows wm * 64 + 16 i + 4 lg + r, columns wn * NCOL / 4 + 16 j + lr.
-template <int NCOL>
+template <int NCOL, typename RM = RowsLinear>
 __device__ __forceinline__ void rowln_fast_epilogue(const mdg_gemm_desc& p, f32x4 (&acc)[4][NCOL / 64],
-                                                    float4 (&h4)[2][NCOL / 128], unsigned char* smem, int m0,
+                                                    float4 (&h4)[2][NCOL / 128], unsigned char* smem, RM rows,
                                                     int b_lo, float inv_rpm, bf16_t* xlds = nullptr) {
   constexpr int WTN = NCOL / 4, NT = WTN / 16, LDS_ST = NCOL + 4;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, wm = wave / 4, wn = wave % 4;
@@ -1145,7 +1162,7 @@ __device__ __forceinline__ void rowln_fast_epilogue(const mdg_gemm_desc& p, f32x
       }
     }
   };
-  rowln_fast_epilogue_impl<NCOL>(p, stage_band, h4, smem, m0, b_lo, inv_rpm, xlds);
+  rowln_fast_epilogue_impl<NCOL>(p, stage_band, h4, smem, rows, b_lo, inv_rpm, xlds);
 }
 
 // PART: split-K form for small M — block (tile, y) runs K-steps [y nk, (y + 1) nk) and writes its
@@ -1232,7 +1249,7 @@ __global__ __launch_bounds__(kRowThreads, BM == 64 ? 4 : 1) void gemm_rowln_kern
   float4 h4[2][NE];
   float2 hv[RG][NE], gv[NE];
   if (!PART) {
-    if (fast) rowln_load_band<NCOL>(p, m0, 0, h4);
+    if (fast) rowln_load_band<NCOL>(p, RowsLinear{m0}, 0, h4);
     else if (BM == 64) load_unit(0, hv, gv);
   }
 
@@ -1309,7 +1326,7 @@ __global__ __launch_bounds__(kRowThreads, BM == 64 ? 4 : 1) void gemm_rowln_kern
   if constexpr (BM == 128) {
     static_assert((32 * LDS_ST + 6 * NCOL) * 4 <= kRowStages * STAGE * 2, "adaLN rows fit the ring");
     if (fast) {
-      rowln_fast_epilogue<NCOL>(p, acc, h4, smem, m0, b_lo, inv_rpm);
+      rowln_fast_epilogue<NCOL>(p, acc, h4, smem, RowsLinear{m0}, b_lo, inv_rpm);
       return;
     }
   }
@@ -1693,8 +1710,8 @@ __global__ __launch_bounds__(kMlpThreads, 1) void mlp_rowln_kernel(const MlpArgs
   } else {
     const float inv_rpm = 1.0f / (float)p.rows_per_mod;
     float4 h4[2][NE];
-    rowln_load_band<NCOL>(p, m0, 0, h4);  // band 0's residual rows
-    rowln_fast_epilogue<NCOL>(p, acc2, h4, smem, m0, fdiv(m0, p.rows_per_mod, inv_rpm), inv_rpm);
+    rowln_load_band<NCOL>(p, RowsLinear{m0}, 0, h4);  // band 0's residual rows
+    rowln_fast_epilogue<NCOL>(p, acc2, h4, smem, RowsLinear{m0}, fdiv(m0, p.rows_per_mod, inv_rpm), inv_rpm);
   }
 }
 
@@ -1842,7 +1859,8 @@ __global__ __launch_bounds__(kWsThreads, 1) void mlp_ws_kernel(const MlpArgs arg
     const float inv_rpm = 1.0f / (float)p.rows_per_mod;
     float4 h4[2][NCOL / 128];
     auto no_stage = [&](int, float*) {};
-    rowln_fast_epilogue_impl<NCOL, 3, true>(p, no_stage, h4, smem, m0, fdiv(m0, p.rows_per_mod, inv_rpm), inv_rpm);
+    rowln_fast_epilogue_impl<NCOL, 3, true>(p, no_stage, h4, smem, RowsLinear{m0}, fdiv(m0, p.rows_per_mod, inv_rpm),
+                                            inv_rpm);
   } else {
     f32x4 acc2[8][NQ];
 #pragma unroll
@@ -1905,7 +1923,8 @@ __global__ __launch_bounds__(kWsThreads, 1) void mlp_ws_kernel(const MlpArgs arg
             rg[((mi & 1) * 16 + lg * 4 + r) * LDS_ST + 96 * wq + 16 * nj + lr] = acc2[mi][nj][r];
       }
     };
-    rowln_fast_epilogue_impl<NCOL, 3, true>(p, stage_band, h4, smem, m0, fdiv(m0, p.rows_per_mod, inv_rpm), inv_rpm);
+    rowln_fast_epilogue_impl<NCOL, 3, true>(p, stage_band, h4, smem, RowsLinear{m0}, fdiv(m0, p.rows_per_mod, inv_rpm),
+                                            inv_rpm);
   }
 }
 
@@ -2234,6 +2253,7 @@ hipError_t rowln_splitk_launch(const mdg_gemm_desc& r, hipStream_t s, float* par
 // | phase-2 ring [0, 128K) + RoPE rows of the block's tokens + bias [128K, ...).
 struct RqArgs {
   mdg_gemm_desc r, q;
+  int frames;  // 1: RowsFrames tiles (q.L % 16 == 0, q.T >= 8), 0: RowsLinear
 };
 constexpr int kRqThreads = 512;
 constexpr int kRqSmem = 160 * 1024;
@@ -2249,6 +2269,7 @@ __device__ __forceinline__ void vm_wait_4x(int n) {
   }
 }
 
+template <bool FRAMES>
 __global__ __launch_bounds__(kRqThreads, 1) void rowln_qkv_kernel(const RqArgs args) {
   constexpr int NCOL = 384, BM = 128, BK = 32, STAGES = 4, WTN = NCOL / 4, NT = WTN / 16, NE = NCOL / 128;
   constexpr int STAGE = (BM + NCOL) * BK, ATILE = BM * BK, WLD = NCOL / 128;
@@ -2268,9 +2289,18 @@ __global__ __launch_bounds__(kRqThreads, 1) void rowln_qkv_kernel(const RqArgs a
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lr = lane & 15, lg = lane >> 4;
   const int M = p.M;
-  const int nwg = (M + BM - 1) / BM;
+  const int nlg = q.L / 16, nf = M / q.L;  // (FRAMES) residue groups per frame, frames
+  const int nwg = FRAMES ? ((nf + 7) / 8) * nlg : (M + BM - 1) / BM;
   const int xcd = blockIdx.x & 7, loc = blockIdx.x >> 3, q8 = nwg >> 3, r8 = nwg & 7;
-  const int m0 = ((xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc) * BM;
+  const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+  typedef typename std::conditional<FRAMES, RowsFrames, RowsLinear>::type RM;
+  RM rows;
+  if constexpr (FRAMES) {
+    const int fg = tile / nlg;
+    rows = RowsFrames{8 * fg, 16 * (tile - fg * nlg), q.L, nf, M};
+  } else {
+    rows = RowsLinear{tile * BM};
+  }
   const int ch = (lg ^ ((-(lr >> 2)) & 3)) * 8;
 
   // ---------------------------------------------------------------- phase 1: out_proj row-LN
@@ -2279,7 +2309,7 @@ __global__ __launch_bounds__(kRqThreads, 1) void rowln_qkv_kernel(const RqArgs a
     const bf16_t* A = reinterpret_cast<const bf16_t*>(p.A);
     const bf16_t* W = reinterpret_cast<const bf16_t*>(p.W);
     const int arow = 16 * wave + (lane >> 2);
-    const bf16_t* asrc = A + (size_t)min(m0 + arow, M - 1) * p.lda + (((lane & 3) ^ ((-(arow >> 2)) & 3)) * 8);
+    const bf16_t* asrc = A + (size_t)min(rows(arow), M - 1) * p.lda + (((lane & 3) ^ ((-(arow >> 2)) & 3)) * 8);
     const bf16_t* bsrc[WLD];
 #pragma unroll
     for (int i = 0; i < WLD; ++i) {
@@ -2295,7 +2325,7 @@ __global__ __launch_bounds__(kRqThreads, 1) void rowln_qkv_kernel(const RqArgs a
                                          16, 0, 0);
     };
     float4 h4[2][NE];
-    rowln_load_band<NCOL>(p, m0, 0, h4);
+    rowln_load_band<NCOL>(p, rows, 0, h4);
     f32x4 acc[4][NT];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -2326,7 +2356,7 @@ __global__ __launch_bounds__(kRqThreads, 1) void rowln_qkv_kernel(const RqArgs a
         for (int j = 0; j < NT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
     }
     const float inv_rpm = 1.0f / (float)p.rows_per_mod;
-    rowln_fast_epilogue<NCOL>(p, acc, h4, smem, m0, fdiv(m0, p.rows_per_mod, inv_rpm), inv_rpm, Xs);
+    rowln_fast_epilogue<NCOL>(p, acc, h4, smem, rows, fdiv(rows(0), p.rows_per_mod, inv_rpm), inv_rpm, Xs);
   }
 
   // ---------------------------------------------------------------- phase 2: temporal q|k|v
@@ -2348,7 +2378,7 @@ __global__ __launch_bounds__(kRqThreads, 1) void rowln_qkv_kernel(const RqArgs a
     for (int k = 0; k < RMAX; ++k) {
       const int i = min(tid + k * kRqThreads, nR - 1);
       const int tok = fdiv(i, D, invD), j = i - tok * D, hj = j < half ? j : j - half;
-      const int m = min(m0 + tok, M - 1), ml = fdiv(m, L, invL), t = ml - fdiv(ml, T, invT) * T;
+      const int m = min(rows(tok), M - 1), ml = fdiv(m, L, invL), t = ml - fdiv(ml, T, invT) * T;
       rv[k] = q.rope[(size_t)((j < half ? 0 : q.rope_rows) + t) * half + hj];
     }
   }
@@ -2402,11 +2432,11 @@ __global__ __launch_bounds__(kRqThreads, 1) void rowln_qkv_kernel(const RqArgs a
   size_t toff[2];
 #pragma unroll
   for (int ti = 0; ti < 2; ++ti) {
-    const int m = min(m0 + wat * 32 + ti * 16 + lr, M - 1);
+    const int m = min(rows(wat * 32 + ti * 16 + lr), M - 1);
     const int ml = fdiv(m, L, invL), l = m - ml * L, b = fdiv(ml, T, invT), t = ml - b * T;
     toff[ti] = ((size_t)(b * L + l) * H * T + t) * D;
   }
-  const bool full = m0 + BM <= M;  // every epilogue store is issued (the counted waits rely on it)
+  const bool full = rows(BM - 1) < M;  // every epilogue store is issued (the counted waits rely on it)
   bf16_t* qo = reinterpret_cast<bf16_t*>(q.qkv_out);
   for (int n = 0; n < NCH; ++n) {
     f32x4 acc[4][2];
@@ -2478,7 +2508,7 @@ __global__ __launch_bounds__(kRqThreads, 1) void rowln_qkv_kernel(const RqArgs a
           const float x1 = __builtin_fmaf(v2, c2[1], -(v3 * s2[1])), y1 = __builtin_fmaf(v3, c2[1], v2 * s2[1]);
           v0 = x0; v1 = y0; v2 = x1; v3 = y1;
         }
-        if (full || m0 + tok < M) {
+        if (full || rows(tok) < M) {
           bf16x4 o;
           o[0] = (bf16_t)v0; o[1] = (bf16_t)v1; o[2] = (bf16_t)v2; o[3] = (bf16_t)v3;
           *reinterpret_cast<bf16x4*>(dst + toff[ti]) = o;
@@ -2500,18 +2530,38 @@ bool rowln_qkv_supported(const mdg_gemm_desc& r, const mdg_gemm_desc& q) {
          r.M % (q.T * q.L) == 0 && (!q.rope || q.rope_rows >= q.T);
 }
 
+// MDG_RQ_FRAMES=1: frame tiles (8 frames x 16 residues) for L % 16 == 0 and T >= 8 (a tile
+// then spans <= 2 trajectories).  Off by default: at the ATLAS shape (B 1, T 250, L 256) the
+// kernel wrote 246.6 vs 257 MB (PMC WRITE_SIZE; h 98.3 + planes 147.5 MB algorithmic — the
+// plane rows were not partial-line writes after all) and took 144 vs 139 us (same box).
+static bool rq_frames(const mdg_gemm_desc& q) {
+  static const bool on = [] {
+    const char* e = getenv("MDG_RQ_FRAMES");
+    return e && e[0] == '1';
+  }();
+  return on && q.L % 16 == 0 && q.T >= 8;
+}
+
 hipError_t rowln_qkv_launch(const mdg_gemm_desc& r, const mdg_gemm_desc& q, hipStream_t s) {
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&rowln_qkv_kernel),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, kRqSmem);
-    if (e != hipSuccess) return e;
+    for (const void* k : {reinterpret_cast<const void*>(&rowln_qkv_kernel<false>),
+                          reinterpret_cast<const void*>(&rowln_qkv_kernel<true>)}) {
+      hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kRqSmem);
+      if (e != hipSuccess) return e;
+    }
     attr_set = true;
   }
   RqArgs a;
   a.r = r;
   a.q = q;
-  hipLaunchKernelGGL(rowln_qkv_kernel, dim3((r.M + 127) / 128), dim3(kRqThreads), kRqSmem, s, a);
+  a.frames = rq_frames(q) ? 1 : 0;
+  if (a.frames) {
+    const int nf = r.M / q.L;
+    hipLaunchKernelGGL(rowln_qkv_kernel<true>, dim3(((nf + 7) / 8) * (q.L / 16)), dim3(kRqThreads), kRqSmem, s, a);
+  } else {
+    hipLaunchKernelGGL(rowln_qkv_kernel<false>, dim3((r.M + 127) / 128), dim3(kRqThreads), kRqSmem, s, a);
+  }
   return hipGetLastError();
 }
 

@@ -3,6 +3,7 @@
 mdg_final_euler)."""
 import ctypes
 import math
+import os
 
 import pytest
 import torch
@@ -181,13 +182,36 @@ def test_mlp_fused_rejects_unsupported_shapes(lib):
     assert lib.mdg_mlp_fused(ctypes.byref(d1), ctypes.byref(d2), _s()) == 1001
 
 
-@pytest.mark.parametrize("B,T,L,rope", [(2, 37, 4, True), (8, 250, 4, True), (1, 32, 4, False), (3, 64, 5, True)])
+@pytest.mark.parametrize("B,T,L,rope", [(2, 37, 4, True), (8, 250, 4, True), (1, 32, 4, False), (3, 64, 5, True),
+                                        (2, 37, 32, True), (3, 9, 16, True), (1, 250, 256, True), (1, 12, 48, False)])
 def test_rowln_qkv_equals_out_proj_then_qkv(lib, B, T, L, rope):
+    _rowln_qkv_check(lib, B, T, L, rope)
+
+
+def test_rowln_qkv_frame_tiles():
+    """MDG_RQ_FRAMES=1 (frame tiles, read once per process): the L % 16 == 0 cases in a child
+    process, each against the two-launch path bit for bit."""
+    import subprocess
+    import sys
+
+    code = ("import sys; sys.path.insert(0, %r); from tests.test_gpu_kernels import _rowln_qkv_check; "
+            "from mdgen_finetune_amd import _lib; lib = _lib.load(); "
+            "[_rowln_qkv_check(lib, *c) for c in [(2, 37, 32, True), (3, 9, 16, True), (1, 250, 256, True), "
+            "(1, 12, 48, False)]]; print('ok')") % os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MDG_RQ_FRAMES="1")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-2000:]
+
+
+def _rowln_qkv_check(lib, B, T, L, rope):
     """mdg_rowln_qkv (spatial out_proj + gated residual + LN_t, then the temporal q|k|v into
     packed planes, LN_t(h) on chip) against the same two descriptors through mdg_gemm: h
     bit-identical (the same row-LN epilogue); q|k|v bit-identical too (the same bf16 LN rows,
     the same K order, the same epilogue arithmetic).  Partial last tiles
-    (M % 128 != 0), tiles over two trajectories, with and without RoPE; xn is not written."""
+    (M % 128 != 0), tiles over two trajectories, with and without RoPE; xn is not written.
+    With MDG_RQ_FRAMES=1 (test_rowln_qkv_frame_tiles), L % 16 == 0 takes the frame tiles (8
+    frames x 16 residues; a ragged last frame group when B T % 8 != 0, groups across trajectory
+    boundaries when T % 8 != 0)."""
     from mdgen_finetune_amd import _lib
 
     H, D = 16, 24
