@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define MDG_ABI_VERSION 15
+#define MDG_ABI_VERSION 16
 #define MDG_MAX_LAYERS 16
 #define MDG_DP 32      /* padded head dim of the attention operand buffers for head_dim <= 31 */
 #define MDG_DP_WIDE 64 /* ... and for 32 <= head_dim <= 63 (column head_dim of the padded k / v rows
@@ -434,6 +434,24 @@ int mdg_attn_spatial_bwd(int32_t dtype, int32_t n_frames, int32_t L, int32_t H, 
 size_t mdg_wgrad_workspace_bytes(int32_t dtype, int32_t N, int32_t M, int32_t K, int32_t need_dw, int32_t need_db);
 int mdg_wgrad(int32_t dtype, int32_t N, int32_t M, int32_t K, const void* dy, int32_t ldy, const void* x, int32_t ldx,
               float* dw, int32_t lddw, float* db, void* ws, size_t ws_bytes, void* stream);
+
+/* Invariant point attention core of the IPA prepend under autograd (reference
+   src/mdgen/model/ipa.py:92-255, c_z = 0; latent_model.py:179-214), fp32, L <= 32, c = 32,
+   8 query/key points and 8 value points (the reference's defaults; other shapes: MDG_E_SHAPE).
+   Operands per token b*L + i, head h:  q [..][H][c], kv [..][H][2c] (k | v), qp [..][H][Pq][3]
+   and kvp [..][H][Pq + Pv][3] (points already in the global frame), mask [B][L], rots
+   [B][L][3][3], trans [B][L][3], hw [H] = softplus(head_weights) * sqrt(1 / (3 Pq 9/2)),
+   wc = sqrt(1 / (3c)).
+   fwd: out [B*L][H*c + 4*H*Pv] = [o | ol_x | ol_y | ol_z | |ol|], the linear_out input.
+   bwd: from dout (same layout): dq, dkv, dqp, dkvp (same layouts as the operands) and
+   dhw_part [B][H] (sum over B = d hw). */
+int mdg_ipa_core_fwd(int32_t B, int32_t L, int32_t H, int32_t c, int32_t Pq, int32_t Pv, const float* q,
+                     const float* kv, const float* qp, const float* kvp, const float* mask, const float* rots,
+                     const float* trans, const float* hw, float wc, float* out, void* stream);
+int mdg_ipa_core_bwd(int32_t B, int32_t L, int32_t H, int32_t c, int32_t Pq, int32_t Pv, const float* q,
+                     const float* kv, const float* qp, const float* kvp, const float* mask, const float* rots,
+                     const float* trans, const float* hw, float wc, const float* dout, float* dq, float* dkv,
+                     float* dqp, float* dkvp, float* dhw_part, void* stream);
 
 #ifdef __cplusplus
 }

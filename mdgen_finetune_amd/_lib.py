@@ -145,9 +145,11 @@ SIGNATURES = [
                                     _vp]),
     ("mdg_wgrad_workspace_bytes", ctypes.c_size_t, [_i32, _i32, _i32, _i32, _i32, _i32]),
     ("mdg_wgrad", _i32, [_i32, _i32, _i32, _i32, _vp, _i32, _vp, _i32, _vp, _i32, _vp, _vp, ctypes.c_size_t, _vp]),
+    ("mdg_ipa_core_fwd", _i32, [_i32] * 6 + [_vp] * 8 + [_f32, _vp, _vp]),
+    ("mdg_ipa_core_bwd", _i32, [_i32] * 6 + [_vp] * 8 + [_f32] + [_vp] * 7),
 ]
 
-ABI_VERSION = 15
+ABI_VERSION = 16
 _LIB = None
 
 

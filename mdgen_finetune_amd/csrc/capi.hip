@@ -22,6 +22,14 @@ hipError_t gemm_launch(const mdg_gemm_desc& p, const GemmPlan& g, hipStream_t s)
 bool mlp_fused_supported(const mdg_gemm_desc& f1, const mdg_gemm_desc& f2);
 hipError_t mlp_fused_launch(const mdg_gemm_desc& f1, const mdg_gemm_desc& f2, hipStream_t s, float* part);
 int mlp_split_factor(int M, int F);
+bool ipa_core_supported(int L, int c, int Pq, int Pv);
+hipError_t ipa_core_fwd_launch(int B, int L, int H, const float* q, const float* kv, const float* qp, const float* kvp,
+                               const float* mask, const float* rots, const float* trans, const float* hw, float wc,
+                               float* out, hipStream_t s);
+hipError_t ipa_core_bwd_launch(int B, int L, int H, const float* q, const float* kv, const float* qp, const float* kvp,
+                               const float* mask, const float* rots, const float* trans, const float* hw, float wc,
+                               const float* dout, float* dq, float* dkv, float* dqp, float* dkvp, float* dhw_part,
+                               hipStream_t s);
 bool rowln_splitk_supported(const mdg_gemm_desc& r, int S);
 hipError_t rowln_splitk_launch(const mdg_gemm_desc& r, hipStream_t s, float* part, int S);
 bool final_euler_supported(const mdg_gemm_desc& p);
@@ -957,6 +965,33 @@ int mdg_attn_spatial_bwd(int32_t dtype, int32_t n_frames, int32_t L, int32_t H, 
   return hip_check(mdg::attn_spatial_bwd_launch(dtype, n_frames, L, H, D, qkv, kvb, mask, dout, rope, rope_rows, dqkv,
                                                 bpart, qscale, (hipStream_t)stream),
                    "attn_spatial_bwd");
+}
+
+int mdg_ipa_core_fwd(int32_t B, int32_t L, int32_t H, int32_t c, int32_t Pq, int32_t Pv, const float* q,
+                     const float* kv, const float* qp, const float* kvp, const float* mask, const float* rots,
+                     const float* trans, const float* hw, float wc, float* out, void* stream) {
+  if (!q || !kv || !qp || !kvp || !mask || !rots || !trans || !hw || !out) return fail(MDG_E_ARG, "ipa_core_fwd: null");
+  if (B <= 0 || H <= 0 || !mdg::ipa_core_supported(L, c, Pq, Pv))
+    return fail(MDG_E_SHAPE, "ipa_core_fwd: B=%d L=%d H=%d c=%d Pq=%d Pv=%d (L <= 32, c = 32, 8 + 8 points)", B, L, H,
+                c, Pq, Pv);
+  return hip_check(mdg::ipa_core_fwd_launch(B, L, H, q, kv, qp, kvp, mask, rots, trans, hw, wc, out,
+                                            (hipStream_t)stream),
+                   "ipa_core_fwd");
+}
+
+int mdg_ipa_core_bwd(int32_t B, int32_t L, int32_t H, int32_t c, int32_t Pq, int32_t Pv, const float* q,
+                     const float* kv, const float* qp, const float* kvp, const float* mask, const float* rots,
+                     const float* trans, const float* hw, float wc, const float* dout, float* dq, float* dkv,
+                     float* dqp, float* dkvp, float* dhw_part, void* stream) {
+  if (!q || !kv || !qp || !kvp || !mask || !rots || !trans || !hw || !dout || !dq || !dkv || !dqp || !dkvp ||
+      !dhw_part)
+    return fail(MDG_E_ARG, "ipa_core_bwd: null");
+  if (B <= 0 || H <= 0 || !mdg::ipa_core_supported(L, c, Pq, Pv))
+    return fail(MDG_E_SHAPE, "ipa_core_bwd: B=%d L=%d H=%d c=%d Pq=%d Pv=%d (L <= 32, c = 32, 8 + 8 points)", B, L, H,
+                c, Pq, Pv);
+  return hip_check(mdg::ipa_core_bwd_launch(B, L, H, q, kv, qp, kvp, mask, rots, trans, hw, wc, dout, dq, dkv, dqp,
+                                            dkvp, dhw_part, (hipStream_t)stream),
+                   "ipa_core_bwd");
 }
 
 }  // extern "C"

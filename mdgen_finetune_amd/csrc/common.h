@@ -81,6 +81,17 @@ __device__ __forceinline__ void st4(CT* p, float a, float b, float c, float d) {
   }
 }
 
+// Store 8 CT (16 B for bf16, 32 B for f32); p aligned accordingly.
+template <typename CT>
+__device__ __forceinline__ void st8(CT* p, const typename V8<CT>::T& v) {
+  if constexpr (is_bf16<CT>()) {
+    *reinterpret_cast<bf16x8*>(p) = v;
+  } else {
+    reinterpret_cast<float4*>(p)[0] = make_float4(v[0], v[1], v[2], v[3]);
+    reinterpret_cast<float4*>(p)[1] = make_float4(v[4], v[5], v[6], v[7]);
+  }
+}
+
 template <typename CT>
 __device__ __forceinline__ float4 ld4f(const CT* p) {
   if constexpr (is_bf16<CT>()) {

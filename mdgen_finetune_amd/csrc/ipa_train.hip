@@ -1,0 +1,323 @@
+// Invariant point attention core for the training step (the IPA prepend under loss.backward():
+// reference src/mdgen/model/ipa.py:92-255 with c_z = 0, called from latent_model.py:179-214).
+//
+// The projections (linear_q / _kv / _q_points / _kv_points and the frame application of the
+// points) and linear_out stay ordinary autograd ops; between them sits the attention core,
+// which eager PyTorch runs as ~25 forward and ~45 backward kernels of a few microseconds each
+// on B * L = 32 tokens -- launch-bound, and five IPA layers deep on the step's critical path.
+// Here it is one kernel each way, fp32 throughout.  One block (one wave) per (sample, head);
+// lane i = query i (L <= 32):
+//   logit_ij = wc q_i.k_j - 1/2 hw_h sum_p |qp_ip - kp_jp|^2 + 1e5 (m_i m_j - 1)
+//   a_ij = softmax_j(logit_ij)
+//   o_i = sum_j a_ij v_j,  og_i = sum_j a_ij vp_j,  ol_i = R_i^T (og_i - t_i),  n_i = sqrt(|ol_i|^2 + eps)
+// written as the linear_out input row [o | ol_x | ol_y | ol_z | n] (ipa.py:226-250's concat order).
+// Backward (lane i, then lane j over the block's LDS copies):
+//   dol = d ol + dn ol / n,  dog_i = R_i dol,  da_ij = do_i.v_j + dog_i.vp_j,
+//   dl_ij = a_ij (da_ij - sum_j' a_ij' da_ij'),
+//   dq_i = wc sum_j dl_ij k_j,  dqp_i = -hw sum_j dl_ij (qp_i - kp_j),
+//   dk_j = wc sum_i dl_ij q_i,  dkp_j = hw sum_i dl_ij (qp_i - kp_j),
+//   dv_j = sum_i a_ij do_i,  dvp_j = sum_i a_ij dog_i,
+//   d hw_h = -1/2 sum_ij dl_ij sum_p |qp_ip - kp_jp|^2  (per-sample partials: no atomics).
+#include "../../include/mdgen_hip.h"
+#include "common.h"
+
+namespace mdg {
+namespace {
+
+constexpr int kIpaMaxL = 32;  // the tetrapeptide crop and small proteins; longer crops take the eager path
+constexpr float kIpaInf = 1e5f, kIpaEps = 1e-8f;
+
+template <int CH, int PQ, int PV>
+struct IpaShape {
+  static constexpr int KV = 2 * CH;          // k | v per head
+  static constexpr int PKV = (PQ + PV) * 3;  // k points | v points per head
+};
+
+// logits of query row i against every key, softmax -> P[i][*] (LDS); returns nothing
+template <int CH, int PQ>
+__device__ __forceinline__ void ipa_row_softmax(const float (&q)[CH], const float (&qp)[PQ * 3], float mi, int L,
+                                                const float* Ks, const float* KPs, const float* Ms, float wc, float hwh,
+                                                float* Prow) {
+  float mx = -INFINITY;
+  for (int j = 0; j < L; ++j) {
+    float s = 0.f;
+#pragma unroll
+    for (int d = 0; d < CH; ++d) s += q[d] * Ks[j * CH + d];
+    float d2 = 0.f;
+#pragma unroll
+    for (int p = 0; p < PQ; ++p) {
+      float e = 0.f;
+#pragma unroll
+      for (int x = 0; x < 3; ++x) {
+        const float u = qp[3 * p + x] - KPs[j * PQ * 3 + 3 * p + x];
+        e += u * u;
+      }
+      d2 += e * hwh;
+    }
+    const float lg = s * wc + d2 * -0.5f + kIpaInf * (mi * Ms[j] - 1.0f);
+    Prow[j] = lg;
+    mx = fmaxf(mx, lg);
+  }
+  float sum = 0.f;
+  for (int j = 0; j < L; ++j) {
+    const float e = expf(Prow[j] - mx);
+    Prow[j] = e;
+    sum += e;
+  }
+  const float inv = 1.0f / sum;
+  for (int j = 0; j < L; ++j) Prow[j] *= inv;
+}
+
+template <int CH, int PQ, int PV>
+struct IpaSmem {
+  float K[kIpaMaxL * CH], V[kIpaMaxL * CH], KP[kIpaMaxL * PQ * 3], VP[kIpaMaxL * PV * 3], M[kIpaMaxL];
+  float P[kIpaMaxL * (kIpaMaxL + 1)];
+};
+
+// stage the block's keys (k, v, key points, value points, mask) of sample b, head h
+template <int CH, int PQ, int PV>
+__device__ __forceinline__ void ipa_stage_keys(IpaSmem<CH, PQ, PV>& S, int b, int h, int L, int H, const float* kv,
+                                               const float* kvp, const float* mask) {
+  using SH = IpaShape<CH, PQ, PV>;
+  for (int e = threadIdx.x; e < L * CH; e += blockDim.x) {
+    const int j = e / CH, d = e % CH;
+    const float* row = kv + (((size_t)b * L + j) * H + h) * SH::KV;
+    S.K[e] = row[d];
+    S.V[e] = row[CH + d];
+  }
+  for (int e = threadIdx.x; e < L * PQ * 3; e += blockDim.x) {
+    const int j = e / (PQ * 3), r = e % (PQ * 3);
+    S.KP[e] = kvp[(((size_t)b * L + j) * H + h) * SH::PKV + r];
+  }
+  for (int e = threadIdx.x; e < L * PV * 3; e += blockDim.x) {
+    const int j = e / (PV * 3), r = e % (PV * 3);
+    S.VP[e] = kvp[(((size_t)b * L + j) * H + h) * SH::PKV + PQ * 3 + r];
+  }
+  for (int j = threadIdx.x; j < L; j += blockDim.x) S.M[j] = mask[(size_t)b * L + j];
+}
+
+template <int CH, int PQ, int PV>
+__global__ __launch_bounds__(64) void ipa_core_fwd_kernel(int L, int H, const float* __restrict__ q,
+                                                          const float* __restrict__ kv, const float* __restrict__ qpts,
+                                                          const float* __restrict__ kvp, const float* __restrict__ mask,
+                                                          const float* __restrict__ rots,
+                                                          const float* __restrict__ trans,
+                                                          const float* __restrict__ hw, float wc,
+                                                          float* __restrict__ out) {
+  __shared__ IpaSmem<CH, PQ, PV> S;
+  const int b = blockIdx.x / H, h = blockIdx.x % H, i = threadIdx.x;
+  ipa_stage_keys<CH, PQ, PV>(S, b, h, L, H, kv, kvp, mask);
+  __syncthreads();
+  if (i >= L) return;
+  const size_t tok = (size_t)b * L + i;
+  float qr[CH], qpr[PQ * 3];
+#pragma unroll
+  for (int d = 0; d < CH; ++d) qr[d] = q[(tok * H + h) * CH + d];
+#pragma unroll
+  for (int r = 0; r < PQ * 3; ++r) qpr[r] = qpts[(tok * H + h) * PQ * 3 + r];
+  float* Prow = S.P + i * (kIpaMaxL + 1);
+  ipa_row_softmax<CH, PQ>(qr, qpr, S.M[i], L, S.K, S.KP, S.M, wc, hw[h], Prow);
+  const int W = H * CH + 4 * H * PV;
+  float* orow = out + tok * W;
+  // o_i
+  for (int d = 0; d < CH; ++d) {
+    float acc = 0.f;
+    for (int j = 0; j < L; ++j) acc += Prow[j] * S.V[j * CH + d];
+    orow[h * CH + d] = acc;
+  }
+  // points: global sum - t_i, then R_i^T, norm
+  const float* R = rots + tok * 9;
+  const float* t = trans + tok * 3;
+  for (int p = 0; p < PV; ++p) {
+    float g[3];
+#pragma unroll
+    for (int x = 0; x < 3; ++x) {
+      float acc = 0.f;
+      for (int j = 0; j < L; ++j) acc += Prow[j] * S.VP[j * PV * 3 + 3 * p + x];
+      g[x] = acc - t[x];
+    }
+    float l[3], nn = 0.f;
+#pragma unroll
+    for (int x = 0; x < 3; ++x) {
+      l[x] = R[0 * 3 + x] * g[0] + R[1 * 3 + x] * g[1] + R[2 * 3 + x] * g[2];
+      nn += l[x] * l[x];
+      orow[H * CH + x * H * PV + h * PV + p] = l[x];
+    }
+    orow[H * CH + 3 * H * PV + h * PV + p] = sqrtf(nn + kIpaEps);
+  }
+}
+
+template <int CH, int PQ, int PV>
+struct IpaBwdSmem {
+  IpaSmem<CH, PQ, PV> s;
+  float Q[kIpaMaxL * CH], QP[kIpaMaxL * PQ * 3], DO[kIpaMaxL * CH], DOG[kIpaMaxL * PV * 3];
+  float DL[kIpaMaxL * (kIpaMaxL + 1)];
+  float red[64];
+};
+
+template <int CH, int PQ, int PV>
+__global__ __launch_bounds__(64) void ipa_core_bwd_kernel(int L, int H, const float* __restrict__ q,
+                                                          const float* __restrict__ kv, const float* __restrict__ qpts,
+                                                          const float* __restrict__ kvp, const float* __restrict__ mask,
+                                                          const float* __restrict__ rots,
+                                                          const float* __restrict__ trans,
+                                                          const float* __restrict__ hw, float wc,
+                                                          const float* __restrict__ dout, float* __restrict__ dq,
+                                                          float* __restrict__ dkv, float* __restrict__ dqp,
+                                                          float* __restrict__ dkvp, float* __restrict__ dhw_part) {
+  using SH = IpaShape<CH, PQ, PV>;
+  __shared__ IpaBwdSmem<CH, PQ, PV> S;
+  const int b = blockIdx.x / H, h = blockIdx.x % H, i = threadIdx.x;
+  ipa_stage_keys<CH, PQ, PV>(S.s, b, h, L, H, kv, kvp, mask);
+  for (int e = threadIdx.x; e < L * CH; e += blockDim.x) {
+    const int j = e / CH, d = e % CH;
+    S.Q[e] = q[(((size_t)b * L + j) * H + h) * CH + d];
+  }
+  for (int e = threadIdx.x; e < L * PQ * 3; e += blockDim.x) {
+    const int j = e / (PQ * 3), r = e % (PQ * 3);
+    S.QP[e] = qpts[(((size_t)b * L + j) * H + h) * PQ * 3 + r];
+  }
+  __syncthreads();
+  const float hwh = hw[h];
+  float dhw = 0.f;
+  if (i < L) {
+    const size_t tok = (size_t)b * L + i;
+    float qr[CH], qpr[PQ * 3];
+#pragma unroll
+    for (int d = 0; d < CH; ++d) qr[d] = S.Q[i * CH + d];
+#pragma unroll
+    for (int r = 0; r < PQ * 3; ++r) qpr[r] = S.QP[i * PQ * 3 + r];
+    float* Prow = S.s.P + i * (kIpaMaxL + 1);
+    ipa_row_softmax<CH, PQ>(qr, qpr, S.s.M[i], L, S.s.K, S.s.KP, S.s.M, wc, hwh, Prow);
+    const int W = H * CH + 4 * H * PV;
+    const float* grow = dout + tok * W;
+    const float* R = rots + tok * 9;
+    const float* t = trans + tok * 3;
+    // d o_i -> LDS; d(point outputs) -> d og_i = R_i (d ol + dn ol / n)
+    for (int d = 0; d < CH; ++d) S.DO[i * CH + d] = grow[h * CH + d];
+    for (int p = 0; p < PV; ++p) {
+      float g[3];
+#pragma unroll
+      for (int x = 0; x < 3; ++x) {
+        float acc = 0.f;
+        for (int j = 0; j < L; ++j) acc += Prow[j] * S.s.VP[j * PV * 3 + 3 * p + x];
+        g[x] = acc - t[x];
+      }
+      float l[3], nn = 0.f;
+#pragma unroll
+      for (int x = 0; x < 3; ++x) {
+        l[x] = R[0 * 3 + x] * g[0] + R[1 * 3 + x] * g[1] + R[2 * 3 + x] * g[2];
+        nn += l[x] * l[x];
+      }
+      const float n = sqrtf(nn + kIpaEps), dn = grow[H * CH + 3 * H * PV + h * PV + p];
+      float dl[3];
+#pragma unroll
+      for (int x = 0; x < 3; ++x) dl[x] = grow[H * CH + x * H * PV + h * PV + p] + dn * l[x] / n;
+#pragma unroll
+      for (int x = 0; x < 3; ++x)
+        S.DOG[i * PV * 3 + 3 * p + x] = R[x * 3 + 0] * dl[0] + R[x * 3 + 1] * dl[1] + R[x * 3 + 2] * dl[2];
+    }
+    // da_ij, row dot, dl_ij
+    float* DLrow = S.DL + i * (kIpaMaxL + 1);
+    float rs = 0.f;
+    for (int j = 0; j < L; ++j) {
+      float da = 0.f;
+#pragma unroll
+      for (int d = 0; d < CH; ++d) da += S.DO[i * CH + d] * S.s.V[j * CH + d];
+#pragma unroll
+      for (int r = 0; r < PV * 3; ++r) da += S.DOG[i * PV * 3 + r] * S.s.VP[j * PV * 3 + r];
+      DLrow[j] = da;
+      rs += Prow[j] * da;
+    }
+    float gq[CH], gqp[PQ * 3];
+#pragma unroll
+    for (int d = 0; d < CH; ++d) gq[d] = 0.f;
+#pragma unroll
+    for (int r = 0; r < PQ * 3; ++r) gqp[r] = 0.f;
+    for (int j = 0; j < L; ++j) {
+      const float dlj = Prow[j] * (DLrow[j] - rs);
+      DLrow[j] = dlj;
+#pragma unroll
+      for (int d = 0; d < CH; ++d) gq[d] += dlj * S.s.K[j * CH + d];
+      float d2 = 0.f;
+#pragma unroll
+      for (int r = 0; r < PQ * 3; ++r) {
+        const float u = qpr[r] - S.s.KP[j * PQ * 3 + r];
+        gqp[r] += dlj * u;
+        d2 += u * u;
+      }
+      dhw += dlj * d2;
+    }
+    float* dqr = dq + (tok * H + h) * CH;
+#pragma unroll
+    for (int d = 0; d < CH; ++d) dqr[d] = wc * gq[d];
+    float* dqpr = dqp + (tok * H + h) * PQ * 3;
+#pragma unroll
+    for (int r = 0; r < PQ * 3; ++r) dqpr[r] = -hwh * gqp[r];
+  }
+  // d hw_h of this sample: -1/2 sum_ij dl_ij d2_ij
+  S.red[threadIdx.x] = dhw;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float s = 0.f;
+    for (int k = 0; k < L; ++k) s += S.red[k];
+    dhw_part[(size_t)b * H + h] = -0.5f * s;
+  }
+  // key side: lane j
+  const int j = threadIdx.x;
+  if (j >= L) return;
+  const size_t tok = (size_t)b * L + j;
+  float gk[CH], gv[CH], gkp[PQ * 3], gvp[PV * 3];
+#pragma unroll
+  for (int d = 0; d < CH; ++d) gk[d] = gv[d] = 0.f;
+#pragma unroll
+  for (int r = 0; r < PQ * 3; ++r) gkp[r] = 0.f;
+#pragma unroll
+  for (int r = 0; r < PV * 3; ++r) gvp[r] = 0.f;
+  for (int ii = 0; ii < L; ++ii) {
+    const float dl = S.DL[ii * (kIpaMaxL + 1) + j], a = S.s.P[ii * (kIpaMaxL + 1) + j];
+#pragma unroll
+    for (int d = 0; d < CH; ++d) {
+      gk[d] += dl * S.Q[ii * CH + d];
+      gv[d] += a * S.DO[ii * CH + d];
+    }
+#pragma unroll
+    for (int r = 0; r < PQ * 3; ++r) gkp[r] += dl * (S.QP[ii * PQ * 3 + r] - S.s.KP[j * PQ * 3 + r]);
+#pragma unroll
+    for (int r = 0; r < PV * 3; ++r) gvp[r] += a * S.DOG[ii * PV * 3 + r];
+  }
+  float* dkvr = dkv + (tok * H + h) * SH::KV;
+#pragma unroll
+  for (int d = 0; d < CH; ++d) {
+    dkvr[d] = wc * gk[d];
+    dkvr[CH + d] = gv[d];
+  }
+  float* dkvpr = dkvp + (tok * H + h) * SH::PKV;
+#pragma unroll
+  for (int r = 0; r < PQ * 3; ++r) dkvpr[r] = hwh * gkp[r];
+#pragma unroll
+  for (int r = 0; r < PV * 3; ++r) dkvpr[PQ * 3 + r] = gvp[r];
+}
+
+}  // namespace
+
+bool ipa_core_supported(int L, int c, int Pq, int Pv) { return L >= 1 && L <= kIpaMaxL && c == 32 && Pq == 8 && Pv == 8; }
+
+hipError_t ipa_core_fwd_launch(int B, int L, int H, const float* q, const float* kv, const float* qp, const float* kvp,
+                               const float* mask, const float* rots, const float* trans, const float* hw, float wc,
+                               float* out, hipStream_t s) {
+  hipLaunchKernelGGL((ipa_core_fwd_kernel<32, 8, 8>), dim3(B * H), dim3(64), 0, s, L, H, q, kv, qp, kvp, mask, rots,
+                     trans, hw, wc, out);
+  return hipGetLastError();
+}
+
+hipError_t ipa_core_bwd_launch(int B, int L, int H, const float* q, const float* kv, const float* qp, const float* kvp,
+                               const float* mask, const float* rots, const float* trans, const float* hw, float wc,
+                               const float* dout, float* dq, float* dkv, float* dqp, float* dkvp, float* dhw_part,
+                               hipStream_t s) {
+  hipLaunchKernelGGL((ipa_core_bwd_kernel<32, 8, 8>), dim3(B * H), dim3(64), 0, s, L, H, q, kv, qp, kvp, mask, rots,
+                     trans, hw, wc, dout, dq, dkv, dqp, dkvp, dhw_part);
+  return hipGetLastError();
+}
+
+}  // namespace mdg

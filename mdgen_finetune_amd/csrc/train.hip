@@ -65,65 +65,80 @@ __global__ __launch_bounds__(256) void ln_gate_bwd_kernel(int M, int C, int TL, 
       for (int a = 0; a < 4; ++a) acc[a][e][w] = 0.f;
     }
   const float invC = 1.0f / (float)C;
-  for (int m = r0 + wave; m < r1; m += 4) {
-    float d[E][W];
+  // R rows of the wave per iteration (rows m + 4i): every row's loads are issued before any
+  // row's reduction, so R HBM round trips overlap (one row per iteration left the loop
+  // latency-bound at 2 waves per SIMD).  Rows are accumulated in the same order as one at a time.
+  constexpr int R = 4;
+  for (int m0 = r0 + wave; m0 < r1; m0 += 4 * R) {
+    float d[R][E][W], dx[R][E][W], hv[R][E][W], yv[R][E][W];
+    float2 st[R];
 #pragma unroll
-    for (int e = 0; e < E; ++e)
-#pragma unroll
-      for (int w = 0; w < W; ++w) d[e][w] = (e < nE) ? dh_res[(size_t)m * C + W * lane + 64 * W * e + w] : 0.f;
-    if (dxn) {
-      const float2 st = *reinterpret_cast<const float2*>(stats + 2 * (size_t)m);
-      float g[E][W], xh[E][W], s1 = 0.f, s2 = 0.f;
+    for (int i = 0; i < R; ++i) {
+      const int m = m0 + 4 * i;
+      const bool rv = m < r1;
+      st[i] = (dxn && rv) ? *reinterpret_cast<const float2*>(stats + 2 * (size_t)m) : make_float2(0.f, 0.f);
 #pragma unroll
       for (int e = 0; e < E; ++e)
 #pragma unroll
         for (int w = 0; w < W; ++w) {
-          const int k = W * lane + 64 * W * e + w;
-          float dx = 0.f, hv = st.x;
-          if (e < nE) {
-            dx = (float)dxn[(size_t)m * C + k];
-            hv = hln[(size_t)m * C + k];
-          }
-          xh[e][w] = (hv - st.x) * st.y;
-          g[e][w] = dx * sc1[e][w];
-          acc[0][e][w] += dx;
-          acc[1][e][w] += dx * xh[e][w];
-          s1 += g[e][w];
-          s2 += g[e][w] * xh[e][w];
+          const bool ok = rv && e < nE;
+          const size_t k = (size_t)m * C + W * lane + 64 * W * e + w;
+          d[i][e][w] = ok ? dh_res[k] : 0.f;
+          dx[i][e][w] = (ok && dxn) ? (float)dxn[k] : 0.f;
+          hv[i][e][w] = (ok && dxn) ? hln[k] : st[i].x;
+          yv[i][e][w] = (ok && y) ? (float)y[k] : 0.f;
         }
+    }
 #pragma unroll
-      for (int o = 32; o >= 1; o >>= 1) {
-        s1 += __shfl_xor(s1, o, 64);
-        s2 += __shfl_xor(s2, o, 64);
+    for (int i = 0; i < R; ++i) {
+      const int m = m0 + 4 * i;
+      if (m >= r1) break;  // wave-uniform
+      if (dxn) {
+        float g[E][W], xh[E][W], s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int e = 0; e < E; ++e)
+#pragma unroll
+          for (int w = 0; w < W; ++w) {
+            xh[e][w] = (hv[i][e][w] - st[i].x) * st[i].y;
+            g[e][w] = dx[i][e][w] * sc1[e][w];
+            acc[0][e][w] += dx[i][e][w];
+            acc[1][e][w] += dx[i][e][w] * xh[e][w];
+            s1 += g[e][w];
+            s2 += g[e][w] * xh[e][w];
+          }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+          s1 += __shfl_xor(s1, o, 64);
+          s2 += __shfl_xor(s2, o, 64);
+        }
+        s1 *= invC;
+        s2 *= invC;
+#pragma unroll
+        for (int e = 0; e < E; ++e)
+#pragma unroll
+          for (int w = 0; w < W; ++w) d[i][e][w] += st[i].y * (g[e][w] - s1 - xh[e][w] * s2);
       }
-      s1 *= invC;
-      s2 *= invC;
+      if (y) {
 #pragma unroll
-      for (int e = 0; e < E; ++e)
+        for (int e = 0; e < E; ++e)
 #pragma unroll
-        for (int w = 0; w < W; ++w) d[e][w] += st.y * (g[e][w] - s1 - xh[e][w] * s2);
-    }
-    if (y) {
-#pragma unroll
-      for (int e = 0; e < E; ++e)
-#pragma unroll
-        for (int w = 0; w < W; ++w) {
-          if (e < nE) {
-            const size_t i = (size_t)m * C + W * lane + 64 * W * e + w;
-            const float yv = (float)y[i];
-            const float dyv = d[e][w] * gt[e][w];
-            dy[i] = (CT)dyv;
-            acc[2][e][w] += d[e][w] * yv;
-            acc[3][e][w] += dyv;
+          for (int w = 0; w < W; ++w) {
+            if (e < nE) {
+              const size_t k = (size_t)m * C + W * lane + 64 * W * e + w;
+              const float dyv = d[i][e][w] * gt[e][w];
+              dy[k] = (CT)dyv;
+              acc[2][e][w] += d[i][e][w] * yv[i][e][w];
+              acc[3][e][w] += dyv;
+            }
           }
-        }
-    }
-    if (dxn || dh_out != dh_res) {
+      }
+      if (dxn || dh_out != dh_res) {
 #pragma unroll
-      for (int e = 0; e < E; ++e)
+        for (int e = 0; e < E; ++e)
 #pragma unroll
-        for (int w = 0; w < W; ++w)
-          if (e < nE) dh_out[(size_t)m * C + W * lane + 64 * W * e + w] = d[e][w];
+          for (int w = 0; w < W; ++w)
+            if (e < nE) dh_out[(size_t)m * C + W * lane + 64 * W * e + w] = d[i][e][w];
+      }
     }
   }
 #pragma unroll
@@ -142,6 +157,137 @@ __global__ __launch_bounds__(256) void ln_gate_bwd_kernel(int M, int C, int TL, 
   }
 }
 
+// C = 384 form: half a wave per row (lane: 4 consecutive columns in each of the three 128-wide
+// chunks, so every access is one 16-B f32 / 8-B bf16 vector), two rows per wave, two row pairs
+// in flight per iteration, and the operand presence as template flags: the generic kernel
+// above branches per element on them and issues dword / short loads one wait at a time.
+template <typename CT, bool DXN, bool Y, bool DHW>
+__global__ __launch_bounds__(256) void ln_gate_bwd384_kernel(int M, int TL, const CT* __restrict__ dxn,
+                                                             const float* __restrict__ hln,
+                                                             const float* __restrict__ stats,
+                                                             const float* __restrict__ mods, int mod_stride,
+                                                             int scale_off, const float* dh_res, float* dh_out,
+                                                             const CT* __restrict__ y, int gate_off,
+                                                             CT* __restrict__ dy, float* __restrict__ part) {
+  constexpr int C = 384, E = 3, R = 2;
+  __shared__ float red[4][4][C];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hl = lane & 31, half = lane >> 5;
+  const int b = blockIdx.y, jb = blockIdx.x;
+  const int r0 = b * TL + jb * kLnbRows;
+  const int r1 = min(b * TL + min((jb + 1) * kLnbRows, TL), M);
+  const float* mr = mods + (size_t)b * mod_stride;
+  float4 sc1[E], gt[E];
+  float acc[4][E][4];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int k = 128 * e + 4 * hl;
+    sc1[e] = DXN ? *reinterpret_cast<const float4*>(mr + scale_off + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+    if (DXN) sc1[e] = make_float4(1.f + sc1[e].x, 1.f + sc1[e].y, 1.f + sc1[e].z, 1.f + sc1[e].w);
+    gt[e] = Y ? *reinterpret_cast<const float4*>(mr + gate_off + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[a][e][j] = 0.f;
+  }
+  auto f4 = [](const float4& v, int j) { return j == 0 ? v.x : j == 1 ? v.y : j == 2 ? v.z : v.w; };
+  const float invC = 1.0f / (float)C;
+  // rows of this half-wave: r0 + 2 wave + half + 8 i, i = 0 .. 7
+  for (int i0 = 0; i0 < kLnbRows / 8; i0 += R) {
+    float d[R][E][4], dx[R][E][4], hv[R][E][4], yv[R][E][4];
+    float2 st[R];
+    bool ok[R];
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      const int m = r0 + 2 * wave + half + 8 * (i0 + u);
+      ok[u] = m < r1;
+      const size_t row = (size_t)min(m, r1 - 1) * C;
+      st[u] = DXN ? *reinterpret_cast<const float2*>(stats + 2 * (row / C)) : make_float2(0.f, 0.f);
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const size_t k = row + 128 * e + 4 * hl;
+        const float4 dv = *reinterpret_cast<const float4*>(dh_res + k);
+        d[u][e][0] = dv.x; d[u][e][1] = dv.y; d[u][e][2] = dv.z; d[u][e][3] = dv.w;
+        if constexpr (DXN) {
+          const float4 xv = ld4f<CT>(dxn + k), hh = *reinterpret_cast<const float4*>(hln + k);
+          dx[u][e][0] = xv.x; dx[u][e][1] = xv.y; dx[u][e][2] = xv.z; dx[u][e][3] = xv.w;
+          hv[u][e][0] = hh.x; hv[u][e][1] = hh.y; hv[u][e][2] = hh.z; hv[u][e][3] = hh.w;
+        }
+        if constexpr (Y) {
+          const float4 yy = ld4f<CT>(y + k);
+          yv[u][e][0] = yy.x; yv[u][e][1] = yy.y; yv[u][e][2] = yy.z; yv[u][e][3] = yy.w;
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      const int m = r0 + 2 * wave + half + 8 * (i0 + u);
+      const float vm = ok[u] ? 1.f : 0.f;
+      if constexpr (DXN) {
+        float g[E][4], xh[E][4], s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int e = 0; e < E; ++e)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            xh[e][j] = (hv[u][e][j] - st[u].x) * st[u].y;
+            g[e][j] = dx[u][e][j] * f4(sc1[e], j);
+            acc[0][e][j] += vm * dx[u][e][j];
+            acc[1][e][j] += vm * (dx[u][e][j] * xh[e][j]);
+            s1 += g[e][j];
+            s2 += g[e][j] * xh[e][j];
+          }
+#pragma unroll
+        for (int o = 16; o >= 1; o >>= 1) {
+          s1 += __shfl_xor(s1, o, 64);
+          s2 += __shfl_xor(s2, o, 64);
+        }
+        s1 *= invC;
+        s2 *= invC;
+#pragma unroll
+        for (int e = 0; e < E; ++e)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) d[u][e][j] += st[u].y * (g[e][j] - s1 - xh[e][j] * s2);
+      }
+      if (!ok[u]) continue;
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const size_t k = (size_t)m * C + 128 * e + 4 * hl;
+        if constexpr (Y) {
+          float dyv[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            dyv[j] = d[u][e][j] * f4(gt[e], j);
+            acc[2][e][j] += d[u][e][j] * yv[u][e][j];
+            acc[3][e][j] += dyv[j];
+          }
+          st4<CT>(dy + k, dyv[0], dyv[1], dyv[2], dyv[3]);
+        }
+        if constexpr (DHW)
+          *reinterpret_cast<float4*>(dh_out + k) = make_float4(d[u][e][0], d[u][e][1], d[u][e][2], d[u][e][3]);
+      }
+    }
+  }
+  // the two half-waves' partials, then the block's four waves
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int e = 0; e < E; ++e)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[a][e][j] += __shfl_xor(acc[a][e][j], 32, 64);
+  if (half == 0)
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int e = 0; e < E; ++e)
+        *reinterpret_cast<float4*>(&red[wave][a][128 * e + 4 * hl]) =
+            make_float4(acc[a][e][0], acc[a][e][1], acc[a][e][2], acc[a][e][3]);
+  __syncthreads();
+  const int nb = gridDim.x;
+  for (int i = threadIdx.x; i < 4 * C; i += 256) {
+    const int a = i / C, c = i - a * C;
+    part[(((size_t)b * nb + jb) * 4 + a) * C + c] = red[0][a][c] + red[1][a][c] + red[2][a][c] + red[3][a][c];
+  }
+}
+
 int ln_gate_bwd_blocks(int TL) { return (TL + kLnbRows - 1) / kLnbRows; }
 
 hipError_t ln_gate_bwd_launch(int dtype, int M, int C, int TL, const void* dxn, const float* hln, const float* stats,
@@ -149,6 +295,19 @@ hipError_t ln_gate_bwd_launch(int dtype, int M, int C, int TL, const void* dxn, 
                               float* dh_out, const void* y, int gate_off, void* dy, float* part, hipStream_t s) {
   const int B = M / TL;
   dim3 grid(ln_gate_bwd_blocks(TL), B);
+  if (C == 384 && ((uintptr_t)mods & 15) == 0 && mod_stride % 4 == 0 && scale_off % 4 == 0 && gate_off % 4 == 0) {
+    const bool dhw = dxn || dh_out != dh_res;
+#define MDG_LNB384(CTT, X_, Y_, W_)                                                                                hipLaunchKernelGGL((ln_gate_bwd384_kernel<CTT, X_, Y_, W_>), grid, dim3(256), 0, s, M, TL, (const CTT*)dxn, hln,                      stats, mods, mod_stride, scale_off, dh_res, dh_out, (const CTT*)y, gate_off, (CTT*)dy, part)
+#define MDG_LNB384_T(CTT)                                                                      if (dxn && y) MDG_LNB384(CTT, true, true, true);                                             else if (dxn) MDG_LNB384(CTT, true, false, true);                                            else if (y) { if (dhw) MDG_LNB384(CTT, false, true, true); else MDG_LNB384(CTT, false, true, false); }   else { if (dhw) MDG_LNB384(CTT, false, false, true); else MDG_LNB384(CTT, false, false, false); }
+    if (dtype == MDG_BF16) {
+      MDG_LNB384_T(bf16_t)
+    } else {
+      MDG_LNB384_T(float)
+    }
+#undef MDG_LNB384_T
+#undef MDG_LNB384
+    return hipGetLastError();
+  }
   const bool w2 = C % 128 == 0;
 #define MDG_LNB(CTT, W)                                                                                         \
   hipLaunchKernelGGL((ln_gate_bwd_kernel<CTT, W>), grid, dim3(256), 0, s, M, C, TL, (const CTT*)dxn, hln, stats, \
@@ -768,19 +927,24 @@ __global__ __launch_bounds__(256) void attn_spatial_bwd_quad_kernel(const CT* __
   const int C = H * D;
   const CT* base = qkv + (size_t)tok * 3 * C + head * D;
   float q[DM], k[DM], v[DM], g[DM];
+  // 16-B (bf16) row pieces: D % 8 == 0 on this route (each lane's rows are 2.3 KB apart, so
+  // every vector-memory instruction touches 64 lines: the instruction count is the cost)
 #pragma unroll
-  for (int d = 0; d < DM; d += 4) {
-    float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a, c = a, e = a;
+  for (int d = 0; d < DM; d += 8) {
+    typename V8<CT>::T a = zero8<CT>(), b = a, c = a, e = a;
     if (d < D) {
-      a = ld4f<CT>(base + d);
-      b = ld4f<CT>(base + C + d);
-      c = ld4f<CT>(base + 2 * C + d);
-      e = ld4f<CT>(dout + (size_t)tok * C + head * D + d);
+      a = ld8<CT>(base + d);
+      b = ld8<CT>(base + C + d);
+      c = ld8<CT>(base + 2 * C + d);
+      e = ld8<CT>(dout + (size_t)tok * C + head * D + d);
     }
-    q[d] = a.x; q[d + 1] = a.y; q[d + 2] = a.z; q[d + 3] = a.w;
-    k[d] = b.x; k[d + 1] = b.y; k[d + 2] = b.z; k[d + 3] = b.w;
-    v[d] = c.x; v[d + 1] = c.y; v[d + 2] = c.z; v[d + 3] = c.w;
-    g[d] = e.x; g[d + 1] = e.y; g[d + 2] = e.z; g[d + 3] = e.w;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      q[d + u] = (float)a[u];
+      k[d + u] = (float)b[u];
+      v[d + u] = (float)c[u];
+      g[d + u] = (float)e[u];
+    }
   }
   const float kvalid = (!mask || mask[tok] != 0.f) ? 1.f : 0.f;
   const float* bk = kvb + head * 2 * kDP;
@@ -826,63 +990,89 @@ __global__ __launch_bounds__(256) void attn_spatial_bwd_quad_kernel(const CT* __
   float ds[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) ds[i] = p[i] * (dp[i] - dl);
-  // dq = ds_b bk + sum_i ds_i k_i;  as key j: dk = sum_J ds_J[j] q_J, dv = sum_J p_J[j] dO_J
-  float dq[DM], dk[DM], dv[DM];
-#pragma unroll
-  for (int d = 0; d < DM; ++d) {
-    dq[d] = dsb * bk[d];
-    dk[d] = 0.f;
-    dv[d] = 0.f;
-  }
+  // dq = ds_b bk + sum_i ds_i k_i;  as key j: dk = sum_J ds_J[j] q_J, dv = sum_J p_J[j] dO_J.
+  // One output row at a time, each stored before the next is formed, so k / v / the finished
+  // gradient rows die early (all three at once held 256 VGPRs: one wave per SIMD).
+  CT* oq = dqkv + (size_t)tok * 3 * C + head * D;
+  const int half = D >> 1;
+  // lane J = i's ds / p for key j (this lane's residue)
+  float dsJ[4], pJ[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-#pragma unroll
-    for (int d = 0; d < DM; ++d) dq[d] += ds[i] * qbi(k[d], i);
-    // lane J = i's ds / p for key j (this lane's residue)
-    float dsJ = 0.f, pJ = 0.f;
+    dsJ[i] = 0.f;
+    pJ[i] = 0.f;
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) {
       const float a = qbi(ds[jj], i), b = qbi(p[jj], i);
       if (jj == j) {
-        dsJ = a;
-        pJ = b;
+        dsJ[i] = a;
+        pJ[i] = b;
       }
     }
+  }
+  auto store_row = [&](int which, const float (&r)[DM], bool rot, float scl) {
 #pragma unroll
-    for (int d = 0; d < DM; ++d) {
-      dk[d] += dsJ * qbi(q[d], i);
-      dv[d] += pJ * qbi(g[d], i);
+    for (int d0 = 0; d0 < DM; d0 += 8) {
+      if (d0 < D) {
+        typename V8<CT>::T w8;
+#pragma unroll
+        for (int d = d0; d < d0 + 8; d += 2) {
+          float a = r[d] * scl, b = r[d + 1] * scl;
+          if (rot) rope_inv(a, b, rope, rope_rows, half, j, d >> 1);
+          w8[d - d0] = (CT)a;
+          w8[d - d0 + 1] = (CT)b;
+        }
+        if (live) st8<CT>(oq + which * C + d0, w8);
+      }
     }
+  };
+  {
+    float dq[DM];
+#pragma unroll
+    for (int d = 0; d < DM; ++d) dq[d] = dsb * bk[d];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int d = 0; d < DM; ++d) dq[d] += ds[i] * qbi(k[d], i);
+    store_row(0, dq, rope != nullptr, qscale);
   }
 #pragma unroll
   for (int d = 0; d < DM; ++d) {
     red[threadIdx.x][d] = live ? dsb * q[d] : 0.f;
     red[threadIdx.x][DM + d] = live ? pb * g[d] : 0.f;
   }
-  if (live) {
-    CT* oq = dqkv + (size_t)tok * 3 * C + head * D;
-    const int half = D >> 1;
+  {
+    float dk[DM];
 #pragma unroll
-    for (int d = 0; d < DM; d += 2) {
-      if (d < D) {
-        float a = dq[d] * qscale, b = dq[d + 1] * qscale, c = dk[d], e = dk[d + 1];
-        if (rope) {
-          rope_inv(a, b, rope, rope_rows, half, j, d >> 1);
-          rope_inv(c, e, rope, rope_rows, half, j, d >> 1);
-        }
-        oq[d] = (CT)a;
-        oq[d + 1] = (CT)b;
-        oq[C + d] = (CT)c;
-        oq[C + d + 1] = (CT)e;
-        oq[2 * C + d] = (CT)dv[d];
-        oq[2 * C + d + 1] = (CT)dv[d + 1];
-      }
-    }
+    for (int d = 0; d < DM; ++d) dk[d] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int d = 0; d < DM; ++d) dk[d] += dsJ[i] * qbi(q[d], i);
+    store_row(1, dk, rope != nullptr, 1.0f);
   }
+  {
+    float dv[DM];
+#pragma unroll
+    for (int d = 0; d < DM; ++d) dv[d] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int d = 0; d < DM; ++d) dv[d] += pJ[i] * qbi(g[d], i);
+    store_row(2, dv, false, 1.0f);
+  }
+  // bias_k / bias_v partials of the block: 4 row groups of 64 in parallel, then the 4 sums
+  // (a 256-long serial LDS chain per column before)
+  __syncthreads();
+  const int col = threadIdx.x % (2 * DM), grp = threadIdx.x / (2 * DM);
+  float s4 = 0.f;
+  if (grp < 4)
+    for (int i = 64 * grp; i < 64 * grp + 64; ++i) s4 += red[i][col];
+  __syncthreads();
+  if (grp < 4) red[grp][col] = s4;
   __syncthreads();
   if (threadIdx.x < 2 * DM) {
-    float s = 0.f;
-    for (int i = 0; i < 256; ++i) s += red[i][threadIdx.x];
+    const float s = (red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x]);
     const int which = threadIdx.x / DM, d = threadIdx.x % DM;
     if (d < kDP) bpart[((size_t)head * gridDim.x + blockIdx.x) * 2 * kDP + which * kDP + d] = s;
   }

@@ -203,6 +203,12 @@ class LatentMDGenModel(nn.Module):
         C = self.args.embed_dim
         rots, trans = frames_to_tensors(start_frames, mask_b.device)
         use_aa = aatype is not None and hasattr(self, "aatype_to_emb")
+        # differentiable calls on a ROCm device: the IPA attention core runs the HIP training
+        # kernels (mdg_ipa_core_fwd / _bwd) between the autograd projections
+        hip_core = (self.backend == "hip" and getattr(self, "train_backend", "hip") == "hip" and mask_b.is_cuda
+                    and torch.is_grad_enabled())
+        for layer in self.ipa_layers:
+            layer.ipa.hip_core = hip_core
         if not self.tps:
             x = torch.zeros(B, L, C, device=mask_b.device)
             if use_aa:

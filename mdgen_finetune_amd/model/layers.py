@@ -79,11 +79,23 @@ class RotaryEmbedding(nn.Module):
         freqs = torch.einsum("i,j->ij", pos, self.inv_freq)
         return freqs.cos().to(device), freqs.sin().to(device)
 
+    def tables2(self, n, device):
+        """cat([cos, cos]), cat([sin, sin]) [n, dim] (fair-esm's doubled tables), cached per
+        (n, device): inv_freq is a constant buffer, and rebuilding the tables took ~8 small
+        kernels per attention call in the training step's eager conditioning."""
+        cache = self.__dict__.setdefault("_tab2", {})
+        key = (n, str(device), self.inv_freq.data_ptr())
+        t = cache.get(key)
+        if t is None:
+            cos, sin = self.tables(n, device)
+            t = cache[key] = (torch.cat([cos, cos], -1), torch.cat([sin, sin], -1))
+        return t
 
-def apply_rope(x, cos, sin):
+
+def apply_rope(x, cos, sin, doubled=False):
     n, h = x.shape[-2], x.shape[-1] // 2
-    c = torch.cat([cos[:n], cos[:n]], -1)
-    s = torch.cat([sin[:n], sin[:n]], -1)
+    c = cos[:n] if doubled else torch.cat([cos[:n], cos[:n]], -1)
+    s = sin[:n] if doubled else torch.cat([sin[:n], sin[:n]], -1)
     rot = torch.cat((-x[..., h:], x[..., :h]), dim=-1)
     return x * c + rot * s
 
@@ -133,12 +145,11 @@ class MultiheadAttention(nn.Module):
         k = k.reshape(N, Sk, H, d).transpose(1, 2)
         v = v.reshape(N, Sk, H, d).transpose(1, 2)
         if self.rot_emb is not None:
-            cos, sin = self.rot_emb.tables(Sk, x.device)
-            q, k = apply_rope(q, cos, sin), apply_rope(k, cos, sin)
+            cos2, sin2 = self.rot_emb.tables2(Sk, x.device)
+            q, k = apply_rope(q, cos2, sin2, doubled=True), apply_rope(k, cos2, sin2, doubled=True)
         # softmax(q k^T masked) v (mha.py:359-389) as one fused SDPA call: the [N,H,S,Sk] score
         # tensor of the reference is never materialised (forward or backward)
-        bias = torch.zeros(N, 1, 1, Sk, dtype=q.dtype, device=x.device).masked_fill(
-            ~kvalid[:, None, None, :], float("-inf"))
+        bias = torch.where(kvalid[:, None, None, :], 0.0, float("-inf")).to(q.dtype)
         o = F.scaled_dot_product_attention(q, k, v, attn_mask=bias, scale=1.0,
                                            dropout_p=self.dropout if self.training else 0.0)
         o = o.transpose(1, 2).reshape(N, S, C)
@@ -156,6 +167,45 @@ class AttentionWithRoPE(nn.Module):
         return self.attn(x, mask)
 
 
+class _IpaCoreFn(torch.autograd.Function):
+    """The IPA attention core (logits, softmax, value / point aggregation, inverse frame, point
+    norms: ipa.py:149-250) as one HIP kernel each way (csrc/ipa_train.hip, mdg_ipa_core_fwd /
+    _bwd); the projections around it stay autograd ops.  Returns the linear_out input
+    [B, L, H*c + 4*H*Pv]."""
+
+    @staticmethod
+    def forward(ctx, q, kv, qp, kvp, mask, rots, trans, hw, wc):
+        from .. import _lib
+
+        lib = _lib.load()
+        B, L, H, c = q.shape
+        Pq, Pv = qp.shape[3], kvp.shape[3] - qp.shape[3]
+        ops = [t.detach().float().contiguous() for t in (q, kv, qp, kvp, mask, rots, trans, hw)]
+        out = torch.empty(B, L, H * c + 4 * H * Pv, device=q.device)
+        _lib.check(lib.mdg_ipa_core_fwd(B, L, H, c, Pq, Pv, *[t.data_ptr() for t in ops], wc, out.data_ptr(),
+                                        _lib.stream_handle()), "mdg_ipa_core_fwd")
+        ctx.save_for_backward(*ops)
+        ctx.wc = wc
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        from .. import _lib
+
+        lib = _lib.load()
+        ops = ctx.saved_tensors
+        q, kv, qp, kvp = ops[:4]
+        B, L, H, c = q.shape
+        Pq, Pv = qp.shape[3], kvp.shape[3] - qp.shape[3]
+        dq, dkv, dqp, dkvp = (torch.empty_like(t) for t in (q, kv, qp, kvp))
+        dhw = torch.empty(B, H, device=q.device)
+        _lib.check(lib.mdg_ipa_core_bwd(B, L, H, c, Pq, Pv, *[t.data_ptr() for t in ops], ctx.wc,
+                                        dout.float().contiguous().data_ptr(), dq.data_ptr(), dkv.data_ptr(),
+                                        dqp.data_ptr(), dkvp.data_ptr(), dhw.data_ptr(), _lib.stream_handle()),
+                   "mdg_ipa_core_bwd")
+        return dq, dkv, dqp, dkvp, None, None, None, dhw.sum(0), None
+
+
 class InvariantPointAttention(nn.Module):
     """Parameters of ipa.py:34-90 (c_z = 0) and the eager forward of ipa.py:92-255."""
 
@@ -165,6 +215,7 @@ class InvariantPointAttention(nn.Module):
         self.c_s, self.c_hidden, self.no_heads = c_s, c_hidden, no_heads
         self.no_qk_points, self.no_v_points = no_qk_points, no_v_points
         self.inf, self.eps = inf, eps
+        self.hip_core = False  # set per call by LatentMDGenModel.run_ipa (HIP training path)
         hc = c_hidden * no_heads
         self.linear_q = nn.Linear(c_s, hc)
         self.linear_kv = nn.Linear(c_s, 2 * hc)
@@ -182,28 +233,29 @@ class InvariantPointAttention(nn.Module):
         kv = self.linear_kv(s).reshape(B, L, H, 2 * c)
         k, v = kv[..., :c], kv[..., c:]
 
+        # Frame applications as one broadcast product + a 3-term sum each (r x: sum_j r_ij x_j;
+        # the per-component form of rigid_utils.py:64-86 costs ~17 kernels forward and ~40
+        # backward per application, and the training step runs 4 per IPA layer)
         def points(lin, n):
-            raw = lin(s)
-            pts = torch.stack(torch.split(raw, n, dim=-1), dim=-1)
-            r = rots[:, :, None]
-            x, y, z = pts.unbind(-1)
-            rp = torch.stack([r[..., i, 0] * x + r[..., i, 1] * y + r[..., i, 2] * z for i in range(3)], -1)
+            pts = lin(s).reshape(B, L, 3, n).transpose(-1, -2)  # stack(split(raw, n), -1)
+            rp = (rots[:, :, None] * pts[..., None, :]).sum(-1)
             return rp + trans[:, :, None]
 
         q_pts = points(self.linear_q_points, H * Pq).reshape(B, L, H, Pq, 3)
         kv_pts = points(self.linear_kv_points, H * (Pq + Pv)).reshape(B, L, H, Pq + Pv, 3)
+        hw = F.softplus(self.head_weights) * math.sqrt(1.0 / (3 * (Pq * 9.0 / 2)))
+        if self.hip_core and s.is_cuda and L <= 32 and c == 32 and Pq == 8 and Pv == 8:
+            return self.linear_out(_IpaCoreFn.apply(q, kv, q_pts, kv_pts, mask, rots, trans, hw,
+                                                    math.sqrt(1.0 / (3 * c))))
         k_pts, v_pts = kv_pts[..., :Pq, :], kv_pts[..., Pq:, :]
         a = torch.einsum("bihc,bjhc->bhij", q, k) * math.sqrt(1.0 / (3 * c))
         d2 = ((q_pts[:, :, None] - k_pts[:, None, :]) ** 2).sum(-1)
-        hw = F.softplus(self.head_weights) * math.sqrt(1.0 / (3 * (Pq * 9.0 / 2)))
         pt = (d2 * hw[:, None]).sum(-1) * (-0.5)
         sq = self.inf * (mask[:, :, None] * mask[:, None, :] - 1)
         a = torch.softmax(a + pt.permute(0, 3, 1, 2) + sq[:, None], dim=-1)
         o = torch.einsum("bhij,bjhc->bihc", a, v).reshape(B, L, H * c)
         opt = torch.einsum("bhij,bjhpx->bihpx", a, v_pts) - trans[:, :, None, None]
-        r = rots[:, :, None, None]
-        x, y, z = opt.unbind(-1)
-        opt = torch.stack([r[..., 0, i] * x + r[..., 1, i] * y + r[..., 2, i] * z for i in range(3)], -1)
+        opt = (rots.transpose(-1, -2)[:, :, None, None] * opt[..., None, :]).sum(-1)  # r^T x
         nrm = torch.sqrt((opt ** 2).sum(-1) + self.eps).reshape(B, L, H * Pv)
         opt = opt.reshape(B, L, H * Pv, 3)
         return self.linear_out(torch.cat([o, opt[..., 0], opt[..., 1], opt[..., 2], nrm], -1))

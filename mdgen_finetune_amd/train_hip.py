@@ -102,6 +102,21 @@ class LayerHelper:
             self._perm = (torch.arange(self.H)[:, None] * D + within[None]).reshape(-1).to(device)
         return self._perm
 
+    def perm3(self, device):
+        """Row order of the packed [3C] q|k|v weight from cat([q, k, v]) (q / k rows
+        pair-interleaved per head, v natural) and its inverse: one gather each way instead of
+        one per projection."""
+        key = ("perm3", device)
+        t = self._tables.get(key)
+        if t is None:
+            C = self.C
+            p = self.perm(device)
+            fwd = torch.cat([p, C + p, 2 * C + torch.arange(C, device=device)])
+            inv = torch.empty_like(fwd)
+            inv[fwd] = torch.arange(3 * C, device=device)
+            t = self._tables[key] = (fwd, inv)
+        return t
+
     def table(self, n_rows, inv_freq):
         """cos | sin [n_rows][D/2] (fair-esm: fp32 outer product on the CPU, then cos / sin)."""
         key = (n_rows, inv_freq.device)
@@ -119,11 +134,16 @@ class LayerHelper:
 
     # -------------------------------------------------------------- bias-key rotation
     def _rot(self, S, n_rows, inv_freq, dev):
-        half = self.D // 2
-        tab = self.table(n_rows, inv_freq)
-        cos = tab[: n_rows * half].reshape(n_rows, half)[S]
-        sin = tab[n_rows * half:].reshape(n_rows, half)[S]
-        return torch.cat([cos, cos]), torch.cat([sin, sin])
+        """(cat(cos, cos), cat(sin, sin)) of position S, cached (a constant of the table)."""
+        key = ("rot", S, n_rows, inv_freq.device)
+        t = self._tables.get(key)
+        if t is None:
+            half = self.D // 2
+            tab = self.table(n_rows, inv_freq)
+            cos = tab[: n_rows * half].reshape(n_rows, half)[S]
+            sin = tab[n_rows * half:].reshape(n_rows, half)[S]
+            t = self._tables[key] = (torch.cat([cos, cos]), torch.cat([sin, sin]))
+        return t
 
     def kvb(self, bias_k, bias_v, S, n_rows, inv_freq):
         """[H][2][32] as the kernels read it (engine._kvb): bias_k RoPE-rotated at position S in
@@ -186,12 +206,14 @@ class _HipLayerFn(torch.autograd.Function):
         perm = hl.perm(dev) if hl.rope else None
         P = {}
         with torch.no_grad():
+            p3 = hl.perm3(dev)[0] if perm is not None else None
             for i in range(2):
                 wq, bq, wk, bk, wv, bv, wo, bo, bias_k, bias_v = params[10 * i:10 * i + 10]
-                if perm is not None:
-                    wq, wk, bq, bk = wq[perm], wk[perm], bq[perm], bk[perm]
-                P[f"wqkv{i}"] = torch.cat([wq, wk, wv]).to(ct).contiguous()
-                P[f"bqkv{i}"] = torch.cat([bq, bk, bv]).float().contiguous()
+                w3, b3 = torch.cat([wq, wk, wv]), torch.cat([bq, bk, bv])
+                if p3 is not None:
+                    w3, b3 = w3[p3], b3[p3]
+                P[f"wqkv{i}"] = w3.to(ct).contiguous()
+                P[f"bqkv{i}"] = b3.float().contiguous()
                 P[f"wo{i}"] = wo.to(ct).contiguous()
                 P[f"bo{i}"] = bo.float().contiguous()
                 S, rows = (L, L + 1) if i == 0 else (T, T + 1)
@@ -286,7 +308,6 @@ class _HipLayerFn(torch.autograd.Function):
         dy_m = r(C)
         part_m = lngate(None, None, None, 0, 0, dh3, dh3, sv["y"][2], 8 * C, dy_m)
         grads["w2"], _ = wg(dy_m, sv["act"])
-        grads["b2"] = part_m[:, :, 3].sum((0, 1))
         du = dx_gemm(dy_m, P["w2"].t().contiguous(), C, F, _lib.MDG_ACT_DGELU, sv["u"])
         grads["w1"], grads["b1"] = wg(du, sv["xn"][2], True)
         dxn3 = dx_gemm(du, P["w1"].t().contiguous(), F, C)
@@ -331,27 +352,23 @@ class _HipLayerFn(torch.autograd.Function):
         dh0 = e(N, C, dtp=torch.float32)
         part_0 = lngate(dxn1, h.reshape(N, C), sv["stats"][0], 0, C, dh1, dh0, None, 0, None)
 
-        # adaLN chunks, latent_model.py:459-461 order
-        red = lambda part, k: part[:, :, k].sum(1)  # noqa: E731
-        dmods = torch.cat([red(part_0, 0), red(part_0, 1), red(part_s, 2), red(part_s, 0), red(part_s, 1),
-                           red(part_t, 2), red(part_t, 0), red(part_t, 1), red(part_m, 2)], -1)
-        grads["bo0"] = part_s[:, :, 3].sum((0, 1))
-        grads["bo1"] = part_t[:, :, 3].sum((0, 1))
+        # adaLN chunks, latent_model.py:459-461 order (each part tensor reduced over its row
+        # blocks once: [B, 4, C] = d shift, d scale, d gate, bias partial)
+        p0, ps, pt, pm = part_0.sum(1), part_s.sum(1), part_t.sum(1), part_m.sum(1)
+        dmods = torch.cat([p0[:, 0:2], ps[:, 2:3], ps[:, 0:2], pt[:, 2:3], pt[:, 0:2], pm[:, 2:3]], 1).reshape(B, 9 * C)
+        grads["bo0"] = ps[:, 3].sum(0)
+        grads["bo1"] = pt[:, 3].sum(0)
+        grads["b2"] = pm[:, 3].sum(0)
 
-        # packed -> parameter layout
-        perm = hl.perm(dev) if hl.rope else None
+        # packed -> parameter layout (one gather per tensor undoes the q / k row interleave)
+        inv3 = hl.perm3(dev)[1] if hl.rope else None
         out = []
         for i in range(2):
             gw, gb = grads[f"wqkv{i}"], grads[f"bqkv{i}"]
+            if inv3 is not None:
+                gw, gb = gw[inv3], gb[inv3]
             gq, gk, gv = gw[:C], gw[C:2 * C], gw[2 * C:]
             bq, bk, bv = gb[:C], gb[C:2 * C], gb[2 * C:]
-            if perm is not None:
-                def unperm(x):
-                    y = torch.empty_like(x)
-                    y[perm] = x
-                    return y
-
-                gq, gk, bq, bk = unperm(gq), unperm(gk), unperm(bq), unperm(bk)
             S, rows = (L, L + 1) if i == 0 else (T, T + 1)
             gbk, gbv = hl.kvb_grad(grads[f"kvb{i}"], S, rows, ctx.inv_freq)
             out += [gq, bq, gk, bk, gv, bv, grads[f"wo{i}"], grads[f"bo{i}"], gbk, gbv]

@@ -241,10 +241,16 @@ class NewMDGenWrapper(nn.Module):
 
     # ------------------------------------------------------------------ optimizer / EMA / ckpt
     def configure_optimizers(self, params=None, capturable=False):
-        """wrapper.py:167-173 (capturable: the step count on the device, for a graphed step)."""
+        """wrapper.py:167-173 (capturable: the step count on the device, for a graphed step).
+
+        The graphed step uses the fused Adam kernel (a handful of multi-tensor launches): the
+        capturable foreach form falls back to per-tensor kernels for its 0-d step / bias-correction
+        arithmetic, ~600 launches per step for the model's 289 tensors (profiles/r03_train_kernels.md).
+        The fused update does not bump the parameters' version counters; GraphedStep.run tells the
+        inference engine's weight cache instead (model._weights_gen)."""
         cls = torch.optim.AdamW if self.args.adamW else torch.optim.Adam
         params = params if params is not None else self.model.parameters()
-        kw = {"capturable": True} if capturable else {}
+        kw = {"capturable": True, "fused": True} if capturable else {}
         return cls([p for p in params if p.requires_grad], lr=self.args.lr, **kw)
 
     def on_before_zero_grad(self):
