@@ -15,6 +15,41 @@ import torch.nn.functional as F
 from torch import nn
 
 
+class _TokenLinear(torch.autograd.Function):
+    """nn.Linear over the B*T*L token rows with a tiny in or out width (latent 21 <-> C): the
+    weight gradient dY^T X has K = 32 000 tokens and an output of a few tiles, which hipBLASLt
+    ran as one long-K kernel (120 us each in the training step); here it is split over 16 token
+    chunks (one batched GEMM + a sum of the fp32 partials)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        ctx.save_for_backward(x, weight)
+        ctx.has_bias = bias is not None
+        return F.linear(x, weight, bias)
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w = ctx.saved_tensors
+        g2 = g.reshape(-1, g.shape[-1])
+        x2 = x.reshape(-1, x.shape[-1])
+        dx = (g2 @ w.to(g2.dtype)).reshape(x.shape) if ctx.needs_input_grad[0] else None
+        n, S = g2.shape[0], 16
+        if n % S == 0 and n >= 64 * S:
+            dw = torch.bmm(g2.reshape(S, n // S, -1).transpose(1, 2), x2.to(g2.dtype).reshape(S, n // S, -1)).sum(0)
+        else:
+            dw = g2.t() @ x2.to(g2.dtype)
+        db = g2.sum(0) if ctx.has_bias else None
+        return dx, dw.to(w.dtype), db
+
+
+def token_linear(lin, x):
+    """lin(x), with the split-K weight gradient of _TokenLinear when autograd records a call on
+    the GPU over many token rows."""
+    if x.is_cuda and torch.is_grad_enabled() and x.numel() >= 4096 * x.shape[-1]:
+        return _TokenLinear.apply(x, lin.weight, lin.bias)
+    return lin(x)
+
+
 def modulate(x, shift, scale):
     return x * (1 + scale.unsqueeze(1)) + shift.unsqueeze(1)
 
@@ -63,7 +98,7 @@ class FinalLayer(nn.Module):
 
     def forward(self, x, c):
         shift, scale = self.adaLN_modulation(c).chunk(2, dim=-1)
-        return self.linear(modulate(self.norm_final(x), shift, scale))
+        return token_linear(self.linear, modulate(self.norm_final(x), shift, scale))
 
 
 class RotaryEmbedding(nn.Module):
