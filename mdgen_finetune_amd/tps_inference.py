@@ -55,6 +55,9 @@ def parse_args(argv=None):
     p.add_argument("--synthetic", type=str, default=None,
                    help="peptide sequence: sample between two frames of a synthetic trajectory (no dataset)")
     p.add_argument("--seed", type=int, default=137)
+    p.add_argument("--batches_per_pass", type=int, default=1,
+                   help="sample this many consecutive batches in one GPU pass (same windows, files and metadata "
+                        "as one at a time; the reference's batch of 10 leaves most of an MI355X idle)")
     return p.parse_args(argv)
 
 
@@ -104,19 +107,24 @@ def sample_batches(model, name, arr, aatype, start_idxs, end_idxs, args, device,
     together; returns the metadata records and the atom14 windows written."""
     rng = np.random.RandomState(args.seed)
     metadata, outs = [], []
-    for i in range(args.num_batches):
-        batch = collate_samples([get_sample(arr, aatype, start_idxs, end_idxs, start_state, end_state,
-                                            args.num_frames, rng, device) for _ in range(args.batch_size)])
-        atom14s, _ = model.inference({k: v.to(device) for k, v in batch.items()},
-                                     zs0=None if zs0 is None else zs0[i].to(device))
-        outs.append(atom14s)
-        for j in range(args.batch_size):
-            idx = i * args.batch_size + j
-            path = os.path.join(args.out_dir, f"{name}_{idx}.pdb")
-            atom14_to_pdb(atom14s[j].cpu().numpy(), batch["seqres"][0].cpu().numpy(), path)
-            metadata.append({"name": name, "start_idx": int(batch["start_idx"][j]), "end_idx": int(batch["end_idx"][j]),
-                             "start_state": int(batch["start_state"][j]), "end_state": int(batch["end_state"][j]),
-                             "path": path})
+    bs, k = args.batch_size, max(1, int(getattr(args, "batches_per_pass", 1) or 1))
+    for i0 in range(0, args.num_batches, k):
+        ids = list(range(i0, min(i0 + k, args.num_batches)))
+        # the windows are drawn batch by batch in the reference's order, then stacked
+        batches = [collate_samples([get_sample(arr, aatype, start_idxs, end_idxs, start_state, end_state,
+                                               args.num_frames, rng, device) for _ in range(bs)]) for _ in ids]
+        batch = {key: torch.cat([b[key] for b in batches]) for key in batches[0]}
+        z = None if zs0 is None else torch.cat([zs0[i] for i in ids]).to(device)
+        atom14s, _ = model.inference({key: v.to(device) for key, v in batch.items()}, zs0=z)
+        for n, i in enumerate(ids):
+            outs.append(atom14s[n * bs:(n + 1) * bs])
+            for j in range(bs):
+                idx, row = i * bs + j, n * bs + j
+                path = os.path.join(args.out_dir, f"{name}_{idx}.pdb")
+                atom14_to_pdb(atom14s[row].cpu().numpy(), batch["seqres"][0].cpu().numpy(), path)
+                metadata.append({"name": name, "start_idx": int(batch["start_idx"][row]),
+                                 "end_idx": int(batch["end_idx"][row]), "start_state": int(batch["start_state"][row]),
+                                 "end_state": int(batch["end_state"][row]), "path": path})
     return metadata, outs
 
 

@@ -1,5 +1,6 @@
 """Rollout geometry (torch restatement) and the PDB writer against the reference's own
 geometry.py / utils.atom14_to_pdb outputs (tests/golden/geometry.npz, oracle/gen_golden.py)."""
+import os
 import numpy as np
 import torch
 
@@ -94,6 +95,39 @@ def test_tps_inference_cpu_writes_paths_and_metadata(tmp_path):
     for m in meta:
         txt = open(m["path"]).read()
         assert txt.count("ENDMDL") == 6 and "nan" not in txt.lower()
+
+
+def test_tps_batches_per_pass_equals_one_batch_at_a_time(tmp_path):
+    """--batches_per_pass k stacks k reference batches into one sampler call: the same windows
+    (start / end draws in the reference's order), files and metadata; with fixed noise the same
+    paths as sampling the batches one at a time (eager CPU backend)."""
+    import json
+    import types
+
+    import numpy as np
+
+    from mdgen_finetune_amd.checkpoint import load_from_checkpoint
+    from mdgen_finetune_amd.tps_inference import _synthetic_traj, sample_batches
+
+    ck = _small_ckpt(tmp_path, T=6, tps=True)
+    model = load_from_checkpoint(ck, map_location="cpu").eval()
+    model.model.backend = "torch"
+    arr, aat = _synthetic_traj("AKDW", 64, 5)
+    zs0 = torch.randn(3, 2, 6, 4, model.model.latent_dim, generator=torch.Generator().manual_seed(1))
+    res = {}
+    for k in (1, 2):
+        out = tmp_path / f"k{k}"
+        out.mkdir()
+        args = types.SimpleNamespace(num_batches=3, batch_size=2, num_frames=6, seed=4, out_dir=str(out),
+                                     batches_per_pass=k)
+        with torch.no_grad():
+            meta, outs = sample_batches(model, "AKDW", arr, aat, [0, 1, 2], [40, 50], args, torch.device("cpu"),
+                                        zs0=zs0)
+        res[k] = ([{kk: v for kk, v in m.items() if kk != "path"} for m in meta], torch.cat(outs),
+                  [os.path.basename(m["path"]) for m in meta])
+    assert res[1][0] == res[2][0] and res[1][2] == res[2][2]
+    assert torch.allclose(res[1][1], res[2][1], atol=1e-4), float((res[1][1] - res[2][1]).abs().max())
+    assert np.isfinite(res[2][1].numpy()).all() and json.dumps(res[2][0])
 
 
 def test_tps_get_sample_window_layout():
