@@ -101,6 +101,10 @@ typedef struct {
   const float* mods_final; /* [B][2C] FinalLayer adaLN (shift, scale) */
   float dt;                /* t_{i+1} - t_i */
   float* h;                /* [N][C] fp32 residual-stream scratch */
+  int32_t chain_alone;     /* 1: this step is the only chain on the device (no concurrent lane);
+                              small-M launches may then split the out_proj row-LN GEMM over K
+                              (fp32 partials + a reduction pass), which pays only when the other
+                              CUs are idle.  0: the lane-invariant routes only. */
 } mdg_step_io;
 
 typedef struct {
@@ -452,6 +456,38 @@ int mdg_ipa_core_bwd(int32_t B, int32_t L, int32_t H, int32_t c, int32_t Pq, int
                      const float* kv, const float* qp, const float* kvp, const float* mask, const float* rots,
                      const float* trans, const float* hw, float wc, const float* dout, float* dq, float* dkv,
                      float* dqp, float* dkvp, float* dhw_part, void* stream);
+
+/* Per-step weight packing / gradient unpacking of one training layer (train_hip._HipLayerFn;
+   latent_model.py:456-493 parameters, mha.py:245-247 projections, fair-esm RoPE of bias_k at
+   the bias key's position S).  All sources fp32 in nn.Linear / nn.Parameter layout; the packed
+   outputs are the mdg_layer_weights operands plus the transposes the input-gradient GEMMs read.
+   rope_tab[i]: [rope_rows][D/2] cos then [rope_rows][D/2] sin; rope_pos[i] = S (L or T). */
+typedef struct {
+  int32_t C, H, D, F, rope, dtype;
+  const float* wq[2]; const float* wk[2]; const float* wv[2];
+  const float* bq[2]; const float* bk[2]; const float* bv[2];
+  const float* wo[2]; const float* bias_k[2]; const float* bias_v[2];
+  const float* w1; const float* w2;
+  const float* rope_tab[2]; int32_t rope_rows[2]; int32_t rope_pos[2];
+  void* wqkv[2]; void* wqkv_t[2]; float* bqkv[2]; void* wo_p[2]; void* wo_t[2]; float* kvb[2];
+  void* w1_p; void* w1_t; void* w2_p; void* w2_t;
+} mdg_train_pack;
+/* gwqkv / gbqkv: packed-order fp32 gradients ([3C][C], [3C]); bpart[i]: [H][parts[i]][2][32]
+   bias-key / value partials; part[0..3]: the ln_gate_bwd partials [B][nblk][4][C] of the
+   layer-input LN, the spatial, temporal and MLP sublayers.  Outputs fp32 in parameter layout;
+   dmods [B][9C] in latent_model.py:459-461 chunk order. */
+typedef struct {
+  int32_t C, H, D, B, nblk, rope;
+  const float* gwqkv[2]; const float* gbqkv[2];
+  const float* bpart[2]; int32_t parts[2];
+  const float* rope_tab[2]; int32_t rope_rows[2]; int32_t rope_pos[2];
+  const float* part[4];
+  float* gq[2]; float* gk[2]; float* gv[2]; float* gbq[2]; float* gbk[2]; float* gbv[2];
+  float* gbias_k[2]; float* gbias_v[2];
+  float* dmods; float* gbo[2]; float* gb2;
+} mdg_train_unpack;
+int mdg_train_pack_layer(const mdg_train_pack* p, void* stream);
+int mdg_train_unpack_layer(const mdg_train_unpack* u, void* stream);
 
 #ifdef __cplusplus
 }

@@ -51,7 +51,7 @@ class MdgModel(ctypes.Structure):
 
 class MdgStepIO(ctypes.Structure):
     _fields_ = [("x_in", _vp), ("x_out", _vp), ("v_out", _vp), ("base", _vp), ("ipa", _vp),
-                ("mods", _vp), ("mods_final", _vp), ("dt", _f32), ("h", _vp)]
+                ("mods", _vp), ("mods_final", _vp), ("dt", _f32), ("h", _vp), ("chain_alone", _i32)]
 
 
 class MdgGemmDesc(ctypes.Structure):
@@ -101,6 +101,22 @@ class MdgCondIO(ctypes.Structure):
         ("lanes", _i32), ("mods", _vp), ("mods_final", _vp), ("ipa", _vp)]
 
 
+class MdgTrainPack(ctypes.Structure):
+    _fields_ = [(n, _i32) for n in ("C", "H", "D", "F", "rope", "dtype")] + [
+        (n, _vp * 2) for n in ("wq", "wk", "wv", "bq", "bk", "bv", "wo", "bias_k", "bias_v")] + [
+        ("w1", _vp), ("w2", _vp), ("rope_tab", _vp * 2), ("rope_rows", _i32 * 2), ("rope_pos", _i32 * 2)] + [
+        (n, _vp * 2) for n in ("wqkv", "wqkv_t", "bqkv", "wo_p", "wo_t", "kvb")] + [
+        (n, _vp) for n in ("w1_p", "w1_t", "w2_p", "w2_t")]
+
+
+class MdgTrainUnpack(ctypes.Structure):
+    _fields_ = [(n, _i32) for n in ("C", "H", "D", "B", "nblk", "rope")] + [
+        ("gwqkv", _vp * 2), ("gbqkv", _vp * 2), ("bpart", _vp * 2), ("parts", _i32 * 2), ("rope_tab", _vp * 2),
+        ("rope_rows", _i32 * 2), ("rope_pos", _i32 * 2), ("part", _vp * 4)] + [
+        (n, _vp * 2) for n in ("gq", "gk", "gv", "gbq", "gbk", "gbv", "gbias_k", "gbias_v")] + [
+        ("dmods", _vp), ("gbo", _vp * 2), ("gb2", _vp)]
+
+
 # (name, restype, argtypes) of every exported entry point — the test suite checks that the
 # built library exports exactly these and that include/mdgen_hip.h declares them.
 SIGNATURES = [
@@ -147,6 +163,8 @@ SIGNATURES = [
     ("mdg_wgrad", _i32, [_i32, _i32, _i32, _i32, _vp, _i32, _vp, _i32, _vp, _i32, _vp, _vp, ctypes.c_size_t, _vp]),
     ("mdg_ipa_core_fwd", _i32, [_i32] * 6 + [_vp] * 8 + [_f32, _vp, _vp]),
     ("mdg_ipa_core_bwd", _i32, [_i32] * 6 + [_vp] * 8 + [_f32] + [_vp] * 7),
+    ("mdg_train_pack_layer", _i32, [ctypes.POINTER(MdgTrainPack), _vp]),
+    ("mdg_train_unpack_layer", _i32, [ctypes.POINTER(MdgTrainUnpack), _vp]),
 ]
 
 ABI_VERSION = 16

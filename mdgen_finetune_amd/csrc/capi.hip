@@ -22,6 +22,8 @@ hipError_t gemm_launch(const mdg_gemm_desc& p, const GemmPlan& g, hipStream_t s)
 bool mlp_fused_supported(const mdg_gemm_desc& f1, const mdg_gemm_desc& f2);
 hipError_t mlp_fused_launch(const mdg_gemm_desc& f1, const mdg_gemm_desc& f2, hipStream_t s, float* part);
 int mlp_split_factor(int M, int F);
+hipError_t train_pack_launch(const mdg_train_pack& p, hipStream_t s);
+hipError_t train_unpack_launch(const mdg_train_unpack& u, hipStream_t s);
 bool ipa_core_supported(int L, int c, int Pq, int Pv);
 hipError_t ipa_core_fwd_launch(int B, int L, int H, const float* q, const float* kv, const float* qp, const float* kvp,
                                const float* mask, const float* rots, const float* trans, const float* hw, float wc,
@@ -483,6 +485,7 @@ struct LnHandoff {
   bool xn_ready;
   const float* next_mods;
   int next_stride, next_shift, next_scale;
+  bool alone = false;  // mdg_step_io.chain_alone: the small-M split-K out_proj route may run
 };
 
 static int layer_fwd_impl(const mdg_dims* d, const mdg_layer_weights* w, const float* rope_l, const float* rope_t,
@@ -510,10 +513,13 @@ static int layer_fwd_impl(const mdg_dims* d, const mdg_layer_weights* w, const f
     // more than the CUs the other lane leaves idle.  Keying it on the launch's B (< 4: a chain
     // alone on the chip) broke the lanes' bit-identity to one chain (a 2-lane window of B = 4
     // would split, the single chain would not), so it stays an explicit choice.
-    static const int smax = [] {
+    static const int smax_env = [] {
       const char* e = getenv("MDG_ROWLN_SPLITK");
       return e ? atoi(e) : 1;
     }();
+    // a chain alone on the chip (mdg_step_io.chain_alone): up to 4 pieces (round 3, B = 1
+    // window +8 %: 1.51 -> 1.64 M frames/s in round 2's measurement)
+    const int smax = smax_env > 1 ? smax_env : (ho.alone ? 4 : 1);
     int S = 1;
     for (int d2 = 2; d2 <= smax && d2 <= lay.mlp_split; ++d2)
       if (12 % d2 == 0 && ((N + 127) / 128) * d2 <= 320) S = d2;
@@ -684,7 +690,7 @@ static int denoise_range(const mdg_model* m, const mdg_step_io* io, const float*
   for (int i = first; i < last; ++i) {
     const bool final_next = i + 1 == d->num_layers;  // the next LN input is the FinalLayer's
     const LnHandoff ho{fuse, final_next ? io->mods_final : io->mods + (i + 1) * mstride, final_next ? 2 * C : 9 * C,
-                       0, C};
+                       0, C, io->chain_alone != 0};
     if (!m->layers[i].wqkv[0]) return fail(MDG_E_ARG, "denoise_step: layer %d weights missing", i);
     if (int e = layer_fwd_impl(d, &m->layers[i], m->rope_l, m->rope_t, io->mods + i * mstride, mask, io->h, ws,
                                stream, ho))
@@ -992,6 +998,40 @@ int mdg_ipa_core_bwd(int32_t B, int32_t L, int32_t H, int32_t c, int32_t Pq, int
   return hip_check(mdg::ipa_core_bwd_launch(B, L, H, q, kv, qp, kvp, mask, rots, trans, hw, wc, dout, dq, dkv, dqp,
                                             dkvp, dhw_part, (hipStream_t)stream),
                    "ipa_core_bwd");
+}
+
+int mdg_train_pack_layer(const mdg_train_pack* p, void* stream) {
+  if (!p) return fail(MDG_E_ARG, "train_pack: null");
+  if (p->dtype != MDG_F32 && p->dtype != MDG_BF16) return fail(MDG_E_DTYPE, "train_pack: dtype %d", p->dtype);
+  if (p->C <= 0 || p->H <= 0 || p->D <= 0 || p->C != p->H * p->D || p->D % 2 || p->D >= MDG_DP || p->F <= 0)
+    return fail(MDG_E_SHAPE, "train_pack: C=%d H=%d D=%d F=%d", p->C, p->H, p->D, p->F);
+  for (int i = 0; i < 2; ++i) {
+    if (!p->wq[i] || !p->wk[i] || !p->wv[i] || !p->bq[i] || !p->bk[i] || !p->bv[i] || !p->wo[i] || !p->bias_k[i] ||
+        !p->bias_v[i] || !p->wqkv[i] || !p->wqkv_t[i] || !p->bqkv[i] || !p->wo_p[i] || !p->wo_t[i] || !p->kvb[i])
+      return fail(MDG_E_ARG, "train_pack: null pointer (attention %d)", i);
+    if (p->rope && (!p->rope_tab[i] || p->rope_pos[i] < 0 || p->rope_pos[i] >= p->rope_rows[i]))
+      return fail(MDG_E_SHAPE, "train_pack: rope table %d (pos %d rows %d)", i, p->rope_pos[i], p->rope_rows[i]);
+  }
+  if (!p->w1 || !p->w2 || !p->w1_p || !p->w1_t || !p->w2_p || !p->w2_t) return fail(MDG_E_ARG, "train_pack: MLP");
+  return hip_check(mdg::train_pack_launch(*p, (hipStream_t)stream), "train_pack");
+}
+
+int mdg_train_unpack_layer(const mdg_train_unpack* u, void* stream) {
+  if (!u) return fail(MDG_E_ARG, "train_unpack: null");
+  if (u->C <= 0 || u->H <= 0 || u->D <= 0 || u->C != u->H * u->D || u->D % 2 || u->D >= MDG_DP || u->B <= 0 ||
+      u->nblk <= 0)
+    return fail(MDG_E_SHAPE, "train_unpack: C=%d H=%d D=%d B=%d nblk=%d", u->C, u->H, u->D, u->B, u->nblk);
+  for (int i = 0; i < 2; ++i) {
+    if (!u->gwqkv[i] || !u->gbqkv[i] || !u->bpart[i] || u->parts[i] <= 0 || !u->gq[i] || !u->gk[i] || !u->gv[i] ||
+        !u->gbq[i] || !u->gbk[i] || !u->gbv[i] || !u->gbias_k[i] || !u->gbias_v[i])
+      return fail(MDG_E_ARG, "train_unpack: null pointer (attention %d)", i);
+    if (u->rope && (!u->rope_tab[i] || u->rope_pos[i] < 0 || u->rope_pos[i] >= u->rope_rows[i]))
+      return fail(MDG_E_SHAPE, "train_unpack: rope table %d", i);
+  }
+  for (int k = 0; k < 4; ++k)
+    if (!u->part[k]) return fail(MDG_E_ARG, "train_unpack: part %d", k);
+  if (!u->dmods || !u->gbo[0] || !u->gbo[1] || !u->gb2) return fail(MDG_E_ARG, "train_unpack: outputs");
+  return hip_check(mdg::train_unpack_launch(*u, (hipStream_t)stream), "train_unpack");
 }
 
 }  // extern "C"

@@ -1,0 +1,204 @@
+// Weight packing and gradient unpacking of the HIP training layer (train_hip._HipLayerFn), one
+// launch each per layer and step.  Done with PyTorch ops they were ~75 small kernels per layer
+// (concatenations, row gathers for the q / k pair interleave, casts, transposes for the input-
+// gradient GEMMs, the bias-key RoPE rotation and its transpose, the adaLN partial sums):
+// 390 launches and 2.9 ms of a 20 ms training step on MI355X (profiles/r03_train_kernels.md).
+//
+// pack   (forward):  wqkv[i] = CT [3C][C] rows q | k | v, q and k rows pair-interleaved per head
+//                    (row 2j = dim j, 2j+1 = dim j + D/2) when RoPE is on; its transpose; bqkv[i];
+//                    wo[i], w1, w2 as CT and transposed; kvb[i] = [H][2][32]: bias_k RoPE-rotated at
+//                    the bias key's position S (fair-esm: x cos + rotate_half(x) sin) in the
+//                    interleaved order, bias_v with 1.0 in pad column D.
+// unpack (backward): the packed-order fp32 q|k|v weight / bias gradients back to q_proj / k_proj /
+//                    v_proj order; bias-key gradient partials summed over parts, un-interleaved and
+//                    rotated back (the transpose of the rotation); the adaLN gradient [B][9C]
+//                    (latent_model.py:459-461 chunk order) and the out_proj / fc2 bias gradients
+//                    from the LN/gate-backward per-block partials.
+#include "../../include/mdgen_hip.h"
+#include "common.h"
+
+namespace mdg {
+namespace {
+
+// natural (q_proj row order) index of packed row r of one head-major q or k block
+__device__ __forceinline__ int nat_of_packed(int r, int D) {
+  const int h = r / D, j = r - h * D;
+  return h * D + ((j & 1) ? (j >> 1) + D / 2 : (j >> 1));
+}
+__device__ __forceinline__ int packed_of_nat(int n, int D) {
+  const int h = n / D, j = n - h * D, half = D / 2;
+  return h * D + (j < half ? 2 * j : 2 * (j - half) + 1);
+}
+
+// One 32 x 32 tile of a weight: source row gathered by `src_row`, written cast to CT row-major
+// and transposed, both coalesced (the transpose goes through LDS: scattered 2-byte stores made
+// this launch 1 ms per layer).
+template <typename CT, typename SrcRow>
+__device__ __forceinline__ void pack_tile(float (*tile)[33], SrcRow src_row, void* dst, void* dst_t, int R, int K,
+                                          int r0, int k0) {
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8 threads
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int r = r0 + ty + 8 * u, k = k0 + tx;
+    const float v = (r < R && k < K) ? src_row(r)[k] : 0.f;
+    tile[ty + 8 * u][tx] = v;
+    if (r < R && k < K) reinterpret_cast<CT*>(dst)[(size_t)r * K + k] = (CT)v;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int k = k0 + ty + 8 * u, r = r0 + tx;
+    if (r < R && k < K) reinterpret_cast<CT*>(dst_t)[(size_t)k * R + r] = (CT)tile[tx][ty + 8 * u];
+  }
+  __syncthreads();
+}
+
+template <typename CT, typename SrcRow>
+__device__ __forceinline__ void pack_matrix(float (*tile)[33], SrcRow src_row, void* dst, void* dst_t, int R, int K) {
+  const int tr = (R + 31) / 32, tk = (K + 31) / 32;
+  for (int t = blockIdx.x; t < tr * tk; t += gridDim.x) pack_tile<CT>(tile, src_row, dst, dst_t, R, K, (t / tk) * 32,
+                                                                      (t % tk) * 32);
+}
+
+template <typename CT>
+__global__ __launch_bounds__(256) void pack_kernel(const mdg_train_pack p) {
+#pragma clang fp contract(off)
+  __shared__ float tile[32][33];
+  const int C = p.C, D = p.D, F = p.F, H = p.H, half = D / 2;
+  const int job = blockIdx.y;
+  const int stride = gridDim.x * blockDim.x;
+  const int t0 = blockIdx.x * blockDim.x + threadIdx.x;
+  if (job < 2) {  // q|k|v weight of attention `job`
+    const int i = job;
+    auto row = [&](int r) -> const float* {
+      if (r < C) return p.wq[i] + (size_t)(p.rope ? nat_of_packed(r, D) : r) * C;
+      if (r < 2 * C) return p.wk[i] + (size_t)(p.rope ? nat_of_packed(r - C, D) : r - C) * C;
+      return p.wv[i] + (size_t)(r - 2 * C) * C;
+    };
+    pack_matrix<CT>(tile, row, p.wqkv[i], p.wqkv_t[i], 3 * C, C);
+  } else if (job < 4) {  // out_proj weight
+    const int i = job - 2;
+    pack_matrix<CT>(tile, [&](int r) { return p.wo[i] + (size_t)r * C; }, p.wo_p[i], p.wo_t[i], C, C);
+  } else if (job == 4) {  // fc1 [F][C]
+    pack_matrix<CT>(tile, [&](int r) { return p.w1 + (size_t)r * C; }, p.w1_p, p.w1_t, F, C);
+  } else if (job == 5) {  // fc2 [C][F]
+    pack_matrix<CT>(tile, [&](int r) { return p.w2 + (size_t)r * F; }, p.w2_p, p.w2_t, C, F);
+  } else {  // q|k|v bias and the bias key / value rows of attention job - 6
+    const int i = job - 6;
+    for (int e = t0; e < 3 * C; e += stride) {
+      float v;
+      if (e < C) v = p.bq[i][p.rope ? nat_of_packed(e, D) : e];
+      else if (e < 2 * C) v = p.bk[i][p.rope ? nat_of_packed(e - C, D) : e - C];
+      else v = p.bv[i][e - 2 * C];
+      p.bqkv[i][e] = v;
+    }
+    const float* tab = p.rope_tab[i];
+    const int S = p.rope_pos[i], rows = p.rope_rows[i];
+    for (int e = t0; e < H * 2 * MDG_DP; e += stride) {
+      const int h = e / (2 * MDG_DP), which = (e / MDG_DP) & 1, d = e % MDG_DP;
+      float v = 0.f;
+      if (which == 1) {
+        v = d < D ? p.bias_v[i][h * D + d] : (d == D ? 1.0f : 0.f);
+      } else if (d < D) {
+        if (p.rope) {
+          const int j = (d & 1) ? (d >> 1) + half : (d >> 1);  // natural dim of interleaved column d
+          const float* kb = p.bias_k[i] + h * D;
+          const float c = tab[S * half + (j % half)], s = tab[rows * half + S * half + (j % half)];
+          const float rot = j < half ? -kb[j + half] : kb[j - half];
+          v = __fadd_rn(__fmul_rn(kb[j], c), __fmul_rn(rot, s));
+        } else {
+          v = p.bias_k[i][h * D + d];
+        }
+      }
+      p.kvb[i][e] = v;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void unpack_kernel(const mdg_train_unpack u) {
+#pragma clang fp contract(off)
+  const int C = u.C, D = u.D, H = u.H, B = u.B, nb = u.nblk, half = D / 2;
+  const int job = blockIdx.y;
+  const int stride = gridDim.x * blockDim.x;
+  const int t0 = blockIdx.x * blockDim.x + threadIdx.x;
+  if (job < 2) {  // q|k|v weight + bias gradients of attention `job`, natural row order
+    const int i = job;
+    for (int e = t0; e < 3 * C * C; e += stride) {
+      const int n = e / C, k = e - n * C;  // natural row n of [q; k; v]
+      const int blk = n / C, nn = n - blk * C;
+      const int r = blk * C + (blk < 2 && u.rope ? packed_of_nat(nn, D) : nn);
+      const float v = u.gwqkv[i][(size_t)r * C + k];
+      float* dst = blk == 0 ? u.gq[i] : blk == 1 ? u.gk[i] : u.gv[i];
+      dst[(size_t)nn * C + k] = v;
+      if (k == 0) {
+        const float bv = u.gbqkv[i][r];
+        float* db = blk == 0 ? u.gbq[i] : blk == 1 ? u.gbk[i] : u.gbv[i];
+        db[nn] = bv;
+      }
+    }
+  } else if (job < 4) {  // bias_k / bias_v gradients of attention job - 2
+    const int i = job - 2, np = u.parts[i];
+    const float* bp = u.bpart[i];  // [H][parts][2][32]
+    const float* tab = u.rope_tab[i];
+    const int S = u.rope_pos[i], rows = u.rope_rows[i];
+    auto g = [&](int h, int which, int d) {
+      float s = 0.f;
+      for (int q = 0; q < np; ++q) s += bp[(((size_t)h * np + q) * 2 + which) * MDG_DP + d];
+      return s;
+    };
+    for (int e = t0; e < H * D; e += stride) {
+      const int h = e / D, j = e - h * D;
+      u.gbias_v[i][e] = g(h, 1, j);
+      if (!u.rope) {
+        u.gbias_k[i][e] = g(h, 0, j);
+        continue;
+      }
+      // gradient w.r.t. the rotated bias key, natural order; then the transpose of x c + rot(x) s
+      const int jp = j < half ? j + half : j - half;
+      const float gr = g(h, 0, j < half ? 2 * j : 2 * (j - half) + 1);
+      const float grp = g(h, 0, jp < half ? 2 * jp : 2 * (jp - half) + 1);
+      const float c = tab[S * half + (j % half)], sp = tab[rows * half + S * half + (jp % half)];
+      const float z = __fmul_rn(grp, sp);
+      u.gbias_k[i][e] = __fadd_rn(__fmul_rn(gr, c), j < half ? z : -z);
+    }
+  } else if (job == 4) {  // adaLN gradient [B][9C]
+    // chunk -> (part tensor, row): shift_l, scale_l | gate_l | shift_t, scale_t | gate_t | shift_m,
+    // scale_m | gate_m  (latent_model.py:459-461)
+    const int src[9] = {0, 0, 1, 1, 1, 2, 2, 2, 3}, row[9] = {0, 1, 2, 0, 1, 2, 0, 1, 2};
+    for (int e = t0; e < B * 9 * C; e += stride) {
+      const int b = e / (9 * C), ck = e - b * 9 * C, c9 = ck / C, k = ck - c9 * C;
+      const float* pp = u.part[src[c9]];
+      float s = 0.f;
+      for (int q = 0; q < nb; ++q) s += pp[(((size_t)b * nb + q) * 4 + row[c9]) * C + k];
+      u.dmods[e] = s;
+    }
+  } else {  // out_proj (spatial, temporal) and fc2 bias gradients: row 3 of part_s / part_t / part_m
+    for (int e = t0; e < 3 * C; e += stride) {
+      const int w = e / C, k = e - w * C;
+      const float* pp = u.part[w + 1];
+      float s = 0.f;
+      for (int b = 0; b < B; ++b) {
+        float sb = 0.f;
+        for (int q = 0; q < nb; ++q) sb += pp[(((size_t)b * nb + q) * 4 + 3) * C + k];
+        s += sb;
+      }
+      (w == 0 ? u.gbo[0] : w == 1 ? u.gbo[1] : u.gb2)[k] = s;
+    }
+  }
+}
+
+}  // namespace
+
+hipError_t train_pack_launch(const mdg_train_pack& p, hipStream_t s) {
+  const dim3 grid(256, 8);
+  if (p.dtype == MDG_BF16) hipLaunchKernelGGL(pack_kernel<bf16_t>, grid, dim3(256), 0, s, p);
+  else hipLaunchKernelGGL(pack_kernel<float>, grid, dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
+hipError_t train_unpack_launch(const mdg_train_unpack& u, hipStream_t s) {
+  hipLaunchKernelGGL(unpack_kernel, dim3(128, 6), dim3(256), 0, s, u);
+  return hipGetLastError();
+}
+
+}  // namespace mdg

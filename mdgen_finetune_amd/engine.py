@@ -71,6 +71,8 @@ class HipEngine:
         # concurrent sub-batch chains per window; 0 = auto: 2 lanes once a window has >= 8
         # trajectories (even count) — measured best at B = 16, bit-identical to 1
         self.lanes = int(os.environ.get("MDG_LANES", "0"))
+        # a single chain (no concurrent lane) may use the small-M split-K out_proj route
+        self.split_alone = os.environ.get("MDG_SPLIT_ALONE", "1") != "0"
         # layers of lane k-1's first step that run before lane k starts (0 = lanes in lock-step)
         self.lane_offset = int(os.environ.get("MDG_LANE_OFFSET", "0"))
 
@@ -409,13 +411,17 @@ class HipEngine:
         aa = None if aatype is None else aatype.to(x.device, torch.int64).contiguous()
         return B, T, L, mask, rots, trans, erots, etrans, aa
 
-    def _step_io(self, st, x_in, x_out, v_out, ipa, mods, mods_f, dt, base=None):
+    def _step_io(self, st, x_in, x_out, v_out, ipa, mods, mods_f, dt, base=None, alone=False):
+        """alone: this chain has the device to itself (no concurrent lane), so the library may
+        take the small-M split-K out_proj route (mdg_step_io.chain_alone; self.split_alone
+        False keeps every chain on the lane-invariant routes)."""
         io = _lib.MdgStepIO()
         io.x_in, io.x_out, io.v_out = x_in, x_out, v_out
         io.base, io.ipa = st.base.data_ptr() if base is None else base, ipa
         io.mods, io.mods_final = mods, mods_f
         io.dt = dt
         io.h = st.h.data_ptr()
+        io.chain_alone = int(bool(alone) and self.split_alone)
         return io
 
     # ------------------------------------------------------------------ one forward
@@ -433,7 +439,7 @@ class HipEngine:
         _lib.check(self.lib.mdg_prepare_mask(ctypes.byref(st.dims), mask.data_ptr(), st.ws.data_ptr(), s),
                    "mdg_prepare_mask")
         io = self._step_io(st, xin.data_ptr(), None, v.data_ptr(), _lib.ptr(ipa), mods.data_ptr(),
-                           mods_f.data_ptr(), 0.0)
+                           mods_f.data_ptr(), 0.0, alone=True)
         _lib.check(self.lib.mdg_denoise_step(ctypes.byref(st.model_struct), ctypes.byref(io), mask.data_ptr(),
                                              st.ws.data_ptr(), s), "mdg_denoise_step")
         return v
@@ -512,7 +518,7 @@ class HipEngine:
                        "mdg_prepare_mask")
             vs.io = self._step_io(st, vs.x.data_ptr(), None, vs.v.data_ptr(),
                                   None if ipa is None else ipa[0].data_ptr(), mods[0].data_ptr(),
-                                  mods_f[0].data_ptr(), 0.0)
+                                  mods_f[0].data_ptr(), 0.0, alone=True)
             _lib.check(self.lib.mdg_denoise_step(ctypes.byref(st.model_struct), ctypes.byref(vs.io),
                                                  vs.mask.data_ptr(), st.ws.data_ptr(), s), "mdg_denoise_step")
 
@@ -593,7 +599,7 @@ class HipEngine:
         for i in range(gs.S):
             io = self._step_io(st, gs.states[i].data_ptr(), gs.states[i + 1].data_ptr(), None,
                                None if ipa is None else ipa[i].data_ptr(), mods[i].data_ptr(),
-                               mods_f[i].data_ptr(), gs.dts[i])
+                               mods_f[i].data_ptr(), gs.dts[i], alone=True)
             ios.append(io)
             _lib.check(self.lib.mdg_denoise_step(ctypes.byref(st.model_struct), ctypes.byref(io),
                                                  gs.mask.data_ptr(), st.ws.data_ptr(), s), "mdg_denoise_step")

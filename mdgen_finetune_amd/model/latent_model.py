@@ -84,8 +84,8 @@ class IPALayer(nn.Module):
         self.fc2 = nn.Linear(ffn_embed_dim, embed_dim)
         self.final_layer_norm = nn.LayerNorm(embed_dim, elementwise_affine=False, eps=1e-6)
 
-    def forward(self, x, t, mask, rots, trans):
-        sh_l, sc_l, g_l, sh_m, sc_m, g_m = self.adaLN_modulation(t).chunk(6, dim=-1)
+    def forward(self, x, t, mask, rots, trans, mods=None):
+        sh_l, sc_l, g_l, sh_m, sc_m, g_m = (self.adaLN_modulation(t) if mods is None else mods).chunk(6, dim=-1)
         x = x + self.ipa(self.ipa_norm(x), rots, trans, mask)
         x = x + g_l.unsqueeze(1) * self.mha_l(modulate(self.mha_layer_norm(x), sh_l, sc_l), mask)
         h = modulate(self.final_layer_norm(x), sh_m, sc_m)
@@ -200,8 +200,9 @@ class LatentMDGenModel(nn.Module):
         """c = TEmb(t * time_multiplier)  [B, C]  (latent_model.py:252)."""
         return self.t_embedder(t * self.args.time_multiplier)
 
-    def run_ipa(self, c, mask_b, start_frames, end_frames, aatype):
-        """latent_model.py:179-214 (sim / TPS branches); c [B, C], mask_b [B, L]."""
+    def run_ipa(self, c, mask_b, start_frames, end_frames, aatype, ada=None):
+        """latent_model.py:179-214 (sim / TPS branches); c [B, C], mask_b [B, L]; ada: the IPA
+        layers' adaLN outputs precomputed by _stacked_adaln (None: each layer computes its own)."""
         B, L = mask_b.shape
         C = self.args.embed_dim
         rots, trans = frames_to_tensors(start_frames, mask_b.device)
@@ -216,8 +217,8 @@ class LatentMDGenModel(nn.Module):
             x = torch.zeros(B, L, C, device=mask_b.device)
             if use_aa:
                 x = x + self.aatype_to_emb(aatype)
-            for layer in self.ipa_layers:
-                x = layer(x, c, mask_b, rots, trans)
+            for k, layer in enumerate(self.ipa_layers):
+                x = layer(x, c, mask_b, rots, trans, mods=None if ada is None else ada[k])
             return x
         erots, etrans = frames_to_tensors(end_frames, mask_b.device)
         x_f = self.latent_to_emb_f(relative_tensor7(rots, trans, erots, etrans))
@@ -225,9 +226,10 @@ class LatentMDGenModel(nn.Module):
         if use_aa:
             x_f = x_f + self.aatype_to_emb(aatype)
             x_r = x_r + self.aatype_to_emb(aatype)
-        for layer in self.ipa_layers:
-            x_r = layer(x_r, c, mask_b, rots, trans)
-            x_f = layer(x_f, c, mask_b, erots, etrans)
+        for k, layer in enumerate(self.ipa_layers):
+            m = None if ada is None else ada[k]
+            x_r = layer(x_r, c, mask_b, rots, trans, mods=m)
+            x_f = layer(x_f, c, mask_b, erots, etrans, mods=m)
         return x_r + x_f
 
     # ------------------------------------------------------------------ forward
@@ -278,26 +280,42 @@ class LatentMDGenModel(nn.Module):
                    else self.mask_to_emb(x_cond_mask))
             h = h + token_linear(self.cond_to_emb, x_cond) + emb
         c = self.embed_time(t)[:, None]
-        if self.args.prepend_ipa:
-            h = h + self.run_ipa(c[:, 0], mask[:, 0], start_frames, end_frames, aatype)[:, None]
         hip_layers = self._use_hip_layers(h)
+        ckpt = bool(getattr(self.args, "grad_checkpointing", False)) and self.training
+        # the HIP training path: every adaLN linear of the model as one stacked GEMM
+        ada = self._stacked_adaln(c[:, 0]) if hip_layers and not ckpt else None
+        if self.args.prepend_ipa:
+            h = h + self.run_ipa(c[:, 0], mask[:, 0], start_frames, end_frames, aatype,
+                                 ada=None if ada is None else ada[0])[:, None]
         if hip_layers:
             from ..train_hip import hip_layer_forward
             hl = self._train_helper()
-        ckpt = bool(getattr(self.args, "grad_checkpointing", False)) and self.training
-        for layer in self.layers:
+        for k, layer in enumerate(self.layers):
             if hip_layers and ckpt:  # --grad_checkpointing: the HIP Function re-runs in backward
                 # (reentrant form: the first forward runs without autograd, so the Function's
                 # saved activations of every layer but the one being differentiated are freed)
                 h = torch.utils.checkpoint.checkpoint(hip_layer_forward, hl, layer, h,
                                                       layer.adaLN_modulation(c[:, 0]), mask, use_reentrant=True)
             elif hip_layers:  # block forward + backward in libmdgen_hip.so (train_hip.py)
-                h = hip_layer_forward(hl, layer, h, layer.adaLN_modulation(c[:, 0]), mask)
+                h = hip_layer_forward(hl, layer, h, ada[1][k], mask)
             elif getattr(self.args, "grad_checkpointing", False) and self.training:
                 h = torch.utils.checkpoint.checkpoint(layer, h, c, mask, use_reentrant=False)
             else:
                 h = layer(h, c, mask)
-        return self.emb_to_latent(h, c)
+        return self.emb_to_latent(h, c, mods=None if ada is None else ada[2][:, None])
+
+    def _stacked_adaln(self, c0):
+        """Every adaLN linear (IPA layers 6C, blocks 9C, FinalLayer 2C: latent_model.py:341-493,
+        layers.py:58-75) over SiLU(c) as ONE GEMM of the concatenated weights; returns
+        ([IPA layer mods], [block mods], final mods).  The 11 separate SiLU + Linear pairs were
+        ~70 forward + backward kernels of the training step on 8 rows."""
+        ipa = list(self.ipa_layers) if self.args.prepend_ipa else []
+        mods = [l.adaLN_modulation for l in ipa] + [l.adaLN_modulation for l in self.layers] + \
+            [self.emb_to_latent.adaLN_modulation]
+        lin = [m[-1] for m in mods]
+        y = F.linear(F.silu(c0), torch.cat([l.weight for l in lin]), torch.cat([l.bias for l in lin]))
+        parts = torch.split(y, [l.out_features for l in lin], -1)
+        return list(parts[:len(ipa)]), list(parts[len(ipa):len(ipa) + len(self.layers)]), parts[-1]
 
     def _use_hip_layers(self, h):
         """Differentiable calls on a ROCm device run the block stack through the HIP training

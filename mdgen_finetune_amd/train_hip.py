@@ -13,14 +13,17 @@ backward  per sublayer, top down:
             mdg_ln_gate_bwd     LN/modulate backward of sublayer k fused with the gated-residual
                                 backward of sublayer k-1 (dh, dy = dh * gate, adaLN and bias
                                 gradient partials);
-            mdg_gemm            input gradients dX = dY W through the HIP GEMM (Wt packed once per
-                                step); fc1's with the GELU-derivative epilogue (MDG_ACT_DGELU);
+            mdg_gemm            input gradients dX = dY W through the HIP GEMM (W^T from the
+                                forward's mdg_train_pack_layer); fc1's with the GELU-derivative
+                                epilogue (MDG_ACT_DGELU);
             mdg_attn_*_bwd      flash-style attention backward (P recomputed from the saved lse),
                                 RoPE / q-scale undone in the epilogue, bias_k / bias_v partials;
             mdg_wgrad           the weight and bias gradients dW = dY^T X, db = colsum(dY) from
                                 the token-major operands (MFMA tiles fed by transposing LDS
                                 reads, split over token chunks, fp32 partials summed in
                                 chunk order: deterministic; csrc/wgrad.hip).
+mdg_train_pack_layer (forward) / mdg_train_unpack_layer (backward) move the parameters into
+the kernels' layouts and the gradients back (csrc/pack_train.hip), one launch each.
 The adaLN modulation vectors enter as a [B, 9C] input of the Function, so the t-embedding /
 adaLN linears upstream stay ordinary autograd modules (x-independent, tiny).
 
@@ -55,6 +58,14 @@ def _rows(n, cols, dtype, dev):
     return t
 
 
+def _src(t):
+    """Device pointer of an fp32 contiguous parameter (the pack kernel's source layout)."""
+    if t.dtype != torch.float32 or not t.is_contiguous():
+        raise RuntimeError(f"HIP training layer: parameter of dtype {t.dtype} / strides {t.stride()} "
+                           "(fp32 contiguous expected)")
+    return t.data_ptr()
+
+
 def wgrad(lib, mdg_dtype, dy, x, need_b=False):
     """(dW = dy^T x, db = colsum(dy)) in fp32 through mdg_wgrad; dy [Np][M], x [Np][K] token
     rows (pad rows zero), x None -> only db."""
@@ -72,8 +83,7 @@ def wgrad(lib, mdg_dtype, dy, x, need_b=False):
 
 
 class LayerHelper:
-    """Per-model state of the HIP training path: ctypes library, RoPE tables per length, the
-    pair-interleave permutation, dtype."""
+    """Per-model state of the HIP training path: ctypes library, RoPE tables per length, dtype."""
 
     def __init__(self, model, dtype="bf16"):
         self.model = model
@@ -85,7 +95,6 @@ class LayerHelper:
         self.rope = not a.no_rope
         self.set_dtype(dtype)
         self._tables = {}
-        self._perm = None
 
     def set_dtype(self, dtype):
         if dtype not in ("bf16", "f32"):
@@ -93,29 +102,6 @@ class LayerHelper:
         self.dtype_name = dtype
         self.mdg_dtype = _lib.MDG_BF16 if dtype == "bf16" else _lib.MDG_F32
         self.ct = torch.bfloat16 if dtype == "bf16" else torch.float32
-
-    def perm(self, device):
-        if self._perm is None or self._perm.device != device:
-            D, half = self.D, self.D // 2
-            idx = torch.arange(D)
-            within = torch.where(idx % 2 == 0, idx // 2, idx // 2 + half)
-            self._perm = (torch.arange(self.H)[:, None] * D + within[None]).reshape(-1).to(device)
-        return self._perm
-
-    def perm3(self, device):
-        """Row order of the packed [3C] q|k|v weight from cat([q, k, v]) (q / k rows
-        pair-interleaved per head, v natural) and its inverse: one gather each way instead of
-        one per projection."""
-        key = ("perm3", device)
-        t = self._tables.get(key)
-        if t is None:
-            C = self.C
-            p = self.perm(device)
-            fwd = torch.cat([p, C + p, 2 * C + torch.arange(C, device=device)])
-            inv = torch.empty_like(fwd)
-            inv[fwd] = torch.arange(3 * C, device=device)
-            t = self._tables[key] = (fwd, inv)
-        return t
 
     def table(self, n_rows, inv_freq):
         """cos | sin [n_rows][D/2] (fair-esm: fp32 outer product on the CPU, then cos / sin)."""
@@ -131,49 +117,6 @@ class LayerHelper:
     def dims(self, B, T, L):
         return _lib.MdgDims(B=B, T=T, L=L, C=self.C, H=self.H, D=self.D, F=self.F, latent=self.model.latent_dim,
                             num_layers=self.model.args.num_layers, dtype=self.mdg_dtype)
-
-    # -------------------------------------------------------------- bias-key rotation
-    def _rot(self, S, n_rows, inv_freq, dev):
-        """(cat(cos, cos), cat(sin, sin)) of position S, cached (a constant of the table)."""
-        key = ("rot", S, n_rows, inv_freq.device)
-        t = self._tables.get(key)
-        if t is None:
-            half = self.D // 2
-            tab = self.table(n_rows, inv_freq)
-            cos = tab[: n_rows * half].reshape(n_rows, half)[S]
-            sin = tab[n_rows * half:].reshape(n_rows, half)[S]
-            t = self._tables[key] = (torch.cat([cos, cos]), torch.cat([sin, sin]))
-        return t
-
-    def kvb(self, bias_k, bias_v, S, n_rows, inv_freq):
-        """[H][2][32] as the kernels read it (engine._kvb): bias_k RoPE-rotated at position S in
-        the pair-interleaved order, bias_v natural with 1.0 in pad column D."""
-        H, D, half = self.H, self.D, self.D // 2
-        kb = bias_k.detach().float().reshape(H, D)
-        if self.rope:
-            c2, s2 = self._rot(S, n_rows, inv_freq, kb.device)
-            kb = kb * c2 + torch.cat([-kb[:, half:], kb[:, :half]], -1) * s2
-            kb = kb.reshape(-1)[self.perm(kb.device)].reshape(H, D)
-        out = torch.zeros(H, 2, _lib.MDG_DP, device=kb.device)
-        out[:, 0, :D] = kb
-        out[:, 1, :D] = bias_v.detach().float().reshape(H, D)
-        out[:, 1, D] = 1.0
-        return out
-
-    def kvb_grad(self, g, S, n_rows, inv_freq):
-        """Map the kernels' [H][2][32] bias-key gradient (w.r.t. the rotated, interleaved rows)
-        back to d bias_k, d bias_v [1, 1, C] of the parameters."""
-        H, D, half = self.H, self.D, self.D // 2
-        gk = g[:, 0, :D].reshape(-1)
-        if self.rope:
-            nat = torch.empty_like(gk)
-            nat[self.perm(gk.device)] = gk
-            gk = nat.reshape(H, D)
-            c2, s2 = self._rot(S, n_rows, inv_freq, gk.device)
-            z = gk * s2
-            gk = gk * c2 + torch.cat([z[:, half:], -z[:, :half]], -1)  # transpose of rotate_half
-        gv = g[:, 1, :D]
-        return gk.reshape(1, 1, -1), gv.reshape(1, 1, -1)
 
 
 def _layer_params(layer):
@@ -203,26 +146,36 @@ class _HipLayerFn(torch.autograd.Function):
         h = h.contiguous().float()
         mods = mods.contiguous().float()
         mask = mask.contiguous().float()
-        perm = hl.perm(dev) if hl.rope else None
+        # the layer's operands in the kernels' layouts (q / k rows pair-interleaved, CT casts, the
+        # transposes the backward's input-gradient GEMMs read, RoPE-rotated bias key): one launch
+        # (mdg_train_pack_layer; ~35 PyTorch kernels per layer before)
+        ee = lambda *shape, dt=ct: torch.empty(*shape, device=dev, dtype=dt)  # noqa: E731
         P = {}
-        with torch.no_grad():
-            p3 = hl.perm3(dev)[0] if perm is not None else None
-            for i in range(2):
-                wq, bq, wk, bk, wv, bv, wo, bo, bias_k, bias_v = params[10 * i:10 * i + 10]
-                w3, b3 = torch.cat([wq, wk, wv]), torch.cat([bq, bk, bv])
-                if p3 is not None:
-                    w3, b3 = w3[p3], b3[p3]
-                P[f"wqkv{i}"] = w3.to(ct).contiguous()
-                P[f"bqkv{i}"] = b3.float().contiguous()
-                P[f"wo{i}"] = wo.to(ct).contiguous()
-                P[f"bo{i}"] = bo.float().contiguous()
-                S, rows = (L, L + 1) if i == 0 else (T, T + 1)
-                P[f"kvb{i}"] = hl.kvb(bias_k, bias_v, S, rows, inv_freq)
-            w1, b1, w2, b2 = params[20:24]
-            P["w1"], P["b1"] = w1.to(ct).contiguous(), b1.float().contiguous()
-            P["w2"], P["b2"] = w2.to(ct).contiguous(), b2.float().contiguous()
-            rope_l = hl.table(L + 1, inv_freq) if hl.rope else None
-            rope_t = hl.table(T + 1, inv_freq) if hl.rope else None
+        pk = _lib.MdgTrainPack(C=C, H=H, D=D, F=F, rope=int(hl.rope), dtype=hl.mdg_dtype)
+        tabs = []
+        for i in range(2):
+            wq, bq, wk, bk, wv, bv, wo, bo, bias_k, bias_v = [t.detach() for t in params[10 * i:10 * i + 10]]
+            for name, t in (("wq", wq), ("wk", wk), ("wv", wv), ("bq", bq), ("bk", bk), ("bv", bv), ("wo", wo),
+                            ("bias_k", bias_k), ("bias_v", bias_v)):
+                getattr(pk, name)[i] = _src(t)
+            P[f"wqkv{i}"], P[f"wqkv_t{i}"], P[f"bqkv{i}"] = ee(3 * C, C), ee(C, 3 * C), ee(3 * C, dt=torch.float32)
+            P[f"wo{i}"], P[f"wo_t{i}"] = ee(C, C), ee(C, C)
+            P[f"bo{i}"] = bo.float().contiguous()
+            P[f"kvb{i}"] = ee(H, 2, _lib.MDG_DP, dt=torch.float32)
+            S, rows = (L, L + 1) if i == 0 else (T, T + 1)
+            tab = hl.table(rows, inv_freq) if hl.rope else None
+            tabs.append(tab)
+            pk.rope_tab[i], pk.rope_rows[i], pk.rope_pos[i] = _lib.ptr(tab), rows, S
+            pk.wqkv[i], pk.wqkv_t[i], pk.bqkv[i] = P[f"wqkv{i}"].data_ptr(), P[f"wqkv_t{i}"].data_ptr(), \
+                P[f"bqkv{i}"].data_ptr()
+            pk.wo_p[i], pk.wo_t[i], pk.kvb[i] = P[f"wo{i}"].data_ptr(), P[f"wo_t{i}"].data_ptr(), P[f"kvb{i}"].data_ptr()
+        w1, b1, w2, b2 = [t.detach() for t in params[20:24]]
+        pk.w1, pk.w2 = _src(w1), _src(w2)
+        P["w1"], P["w1_t"], P["w2"], P["w2_t"] = ee(F, C), ee(C, F), ee(C, F), ee(F, C)
+        P["b1"], P["b2"] = b1.float().contiguous(), b2.float().contiguous()
+        pk.w1_p, pk.w1_t, pk.w2_p, pk.w2_t = (P[k].data_ptr() for k in ("w1", "w1_t", "w2", "w2_t"))
+        _lib.check(lib.mdg_train_pack_layer(ctypes.byref(pk), s), "mdg_train_pack_layer")
+        rope_l, rope_t = tabs
         lw = _lib.MdgLayerWeights()
         for i in range(2):
             lw.wqkv[i], lw.bqkv[i] = P[f"wqkv{i}"].data_ptr(), P[f"bqkv{i}"].data_ptr()
@@ -308,9 +261,9 @@ class _HipLayerFn(torch.autograd.Function):
         dy_m = r(C)
         part_m = lngate(None, None, None, 0, 0, dh3, dh3, sv["y"][2], 8 * C, dy_m)
         grads["w2"], _ = wg(dy_m, sv["act"])
-        du = dx_gemm(dy_m, P["w2"].t().contiguous(), C, F, _lib.MDG_ACT_DGELU, sv["u"])
+        du = dx_gemm(dy_m, P["w2_t"], C, F, _lib.MDG_ACT_DGELU, sv["u"])
         grads["w1"], grads["b1"] = wg(du, sv["xn"][2], True)
-        dxn3 = dx_gemm(du, P["w1"].t().contiguous(), F, C)
+        dxn3 = dx_gemm(du, P["w1_t"], F, C)
         dh2 = e(N, C, dtp=torch.float32)
         dy_t = r(C)
         part_t = lngate(dxn3, sv["h2"], sv["stats"][2], 6 * C, 7 * C, dh3, dh2, sv["y"][1], 5 * C, dy_t)
@@ -318,7 +271,7 @@ class _HipLayerFn(torch.autograd.Function):
         def attention(i, dy, o, xn, qkv, lse):
             """out_proj + attention backward of attention i (0 spatial, 1 temporal); returns dxn."""
             grads[f"wo{i}"], _ = wg(dy, o)
-            do = dx_gemm(dy, P[f"wo{i}"].t().contiguous(), C, C)
+            do = dx_gemm(dy, P[f"wo_t{i}"], C, C)
             dqkv = r(3 * C)
             if i == 1 or L >= 16:
                 Bq, Tq, Lq = (B, T, L) if i == 1 else (B * T, L, 1)
@@ -340,9 +293,9 @@ class _HipLayerFn(torch.autograd.Function):
                                                     ctx.mask.data_ptr(), do.data_ptr(), _lib.ptr(rope_l), L + 1,
                                                     dqkv.data_ptr(), bpart.data_ptr(), qscale, s),
                            "mdg_attn_spatial_bwd")
-            grads[f"kvb{i}"] = bpart.sum(1)
+            grads[f"kvb{i}"] = bpart
             grads[f"wqkv{i}"], grads[f"bqkv{i}"] = wg(dqkv, xn, True)
-            return dx_gemm(dqkv, P[f"wqkv{i}"].t().contiguous(), 3 * C, C)
+            return dx_gemm(dqkv, P[f"wqkv_t{i}"], 3 * C, C)
 
         dxn2 = attention(1, dy_t, sv["o"][1], sv["xn"][1], sv["qkv_t"], sv["lse_t"])
         dh1 = e(N, C, dtp=torch.float32)
@@ -352,26 +305,30 @@ class _HipLayerFn(torch.autograd.Function):
         dh0 = e(N, C, dtp=torch.float32)
         part_0 = lngate(dxn1, h.reshape(N, C), sv["stats"][0], 0, C, dh1, dh0, None, 0, None)
 
-        # adaLN chunks, latent_model.py:459-461 order (each part tensor reduced over its row
-        # blocks once: [B, 4, C] = d shift, d scale, d gate, bias partial)
-        p0, ps, pt, pm = part_0.sum(1), part_s.sum(1), part_t.sum(1), part_m.sum(1)
-        dmods = torch.cat([p0[:, 0:2], ps[:, 2:3], ps[:, 0:2], pt[:, 2:3], pt[:, 0:2], pm[:, 2:3]], 1).reshape(B, 9 * C)
-        grads["bo0"] = ps[:, 3].sum(0)
-        grads["bo1"] = pt[:, 3].sum(0)
-        grads["b2"] = pm[:, 3].sum(0)
-
-        # packed -> parameter layout (one gather per tensor undoes the q / k row interleave)
-        inv3 = hl.perm3(dev)[1] if hl.rope else None
+        # packed -> parameter layout, the bias-key rotation undone, adaLN / bias gradients from the
+        # per-block partials: one launch (mdg_train_unpack_layer)
+        f32 = lambda *shape: torch.empty(*shape, device=dev)  # noqa: E731
+        up = _lib.MdgTrainUnpack(C=C, H=H, D=D, B=B, nblk=nblk, rope=int(hl.rope))
+        g = {}
+        for i in range(2):
+            up.gwqkv[i], up.gbqkv[i] = grads[f"wqkv{i}"].data_ptr(), grads[f"bqkv{i}"].data_ptr()
+            up.bpart[i], up.parts[i] = grads[f"kvb{i}"].data_ptr(), grads[f"kvb{i}"].shape[1]
+            S, rows = (L, L + 1) if i == 0 else (T, T + 1)
+            up.rope_tab[i], up.rope_rows[i], up.rope_pos[i] = _lib.ptr(ctx.rope[i]), rows, S
+            for name, shape in (("gq", (C, C)), ("gk", (C, C)), ("gv", (C, C)), ("gbq", (C,)), ("gbk", (C,)),
+                                ("gbv", (C,)), ("gbias_k", (1, 1, C)), ("gbias_v", (1, 1, C))):
+                g[name, i] = f32(*shape)
+                getattr(up, name)[i] = g[name, i].data_ptr()
+        for k, part in enumerate((part_0, part_s, part_t, part_m)):
+            up.part[k] = part.data_ptr()
+        dmods, gbo0, gbo1, gb2 = f32(B, 9 * C), f32(C), f32(C), f32(C)
+        up.dmods, up.gbo[0], up.gbo[1], up.gb2 = dmods.data_ptr(), gbo0.data_ptr(), gbo1.data_ptr(), gb2.data_ptr()
+        _lib.check(lib.mdg_train_unpack_layer(ctypes.byref(up), s), "mdg_train_unpack_layer")
+        grads["bo0"], grads["bo1"], grads["b2"] = gbo0, gbo1, gb2
         out = []
         for i in range(2):
-            gw, gb = grads[f"wqkv{i}"], grads[f"bqkv{i}"]
-            if inv3 is not None:
-                gw, gb = gw[inv3], gb[inv3]
-            gq, gk, gv = gw[:C], gw[C:2 * C], gw[2 * C:]
-            bq, bk, bv = gb[:C], gb[C:2 * C], gb[2 * C:]
-            S, rows = (L, L + 1) if i == 0 else (T, T + 1)
-            gbk, gbv = hl.kvb_grad(grads[f"kvb{i}"], S, rows, ctx.inv_freq)
-            out += [gq, bq, gk, bk, gv, bv, grads[f"wo{i}"], grads[f"bo{i}"], gbk, gbv]
+            out += [g["gq", i], g["gbq", i], g["gk", i], g["gbk", i], g["gv", i], g["gbv", i], grads[f"wo{i}"],
+                    grads[f"bo{i}"], g["gbias_k", i], g["gbias_v", i]]
         out += [grads["w1"], grads["b1"], grads["w2"], grads["b2"]]
         del ctx.sv, ctx.P
         return (dh0.reshape(B, T, L, C), dmods, None, None, None, *out)

@@ -360,6 +360,7 @@ def test_concurrent_lanes_equal_single_chain(lanes, offset):
     kw = dict(mask=g("mask"), start_frames=Rigid(Rotation(rot_mats=g("rots")), g("trans")), x_cond=g("x_cond"),
               x_cond_mask=g("x_cond_mask"), aatype=g("aatype"))
     eng.lanes = 1
+    eng.split_alone = False  # the lane-invariant routes only (a lone chain may split the out_proj over K)
     ref = eng.sample_euler(g("x"), num_steps=6, use_graph=False, **kw)
     eng.lanes, eng.lane_offset = lanes, offset
     eng._graphs.clear()
@@ -367,6 +368,7 @@ def test_concurrent_lanes_equal_single_chain(lanes, offset):
     got_graph = eng.sample_euler(g("x"), num_steps=6, use_graph=True, **kw)
     got_replay = eng.sample_euler(g("x"), num_steps=6, use_graph=True, **kw)
     eng.lanes, eng.lane_offset = 1, 0
+    eng.split_alone = True
     eng._graphs.clear()
     Bl = ref.shape[1] // lanes
     for name, got in (("eager", got_eager), ("graph", got_graph), ("replay", got_replay)):

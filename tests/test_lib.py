@@ -57,6 +57,9 @@ int main(void){
  printf("%zu %zu %zu %zu %zu %zu %zu\n", sizeof(mdg_cond_dims), sizeof(mdg_ipa_layer_weights),
         sizeof(mdg_cond_model), sizeof(mdg_cond_io), offsetof(mdg_cond_model, time_multiplier),
         offsetof(mdg_cond_model, t_freqs), offsetof(mdg_cond_model, ipa));
+ printf("%zu %zu %zu %zu %zu %zu %zu\n", sizeof(mdg_train_pack), offsetof(mdg_train_pack, rope_rows),
+        offsetof(mdg_train_pack, w1_t), sizeof(mdg_train_unpack), offsetof(mdg_train_unpack, part),
+        offsetof(mdg_train_unpack, gb2), offsetof(mdg_step_io, chain_alone));
  printf("%zu %zu %zu %zu %zu %zu %zu\n", offsetof(mdg_step_io, dt), offsetof(mdg_step_io, h),
         offsetof(mdg_gemm_desc, qscale), offsetof(mdg_gemm_desc, rope_rows), offsetof(mdg_gemm_desc, aux),
         offsetof(mdg_gemm_desc, ldaux), offsetof(mdg_layer_saved, init_planes));
@@ -70,7 +73,11 @@ int main(void){
         out = subprocess.check_output([exe]).decode().split()
     sizes = [int(v) for v in out[:6]]
     cond = [int(v) for v in out[6:13]]
-    offs = [int(v) for v in out[13:]]
+    train = [int(v) for v in out[13:20]]
+    offs = [int(v) for v in out[20:]]
+    assert train == [ctypes.sizeof(_lib.MdgTrainPack), _lib.MdgTrainPack.rope_rows.offset, _lib.MdgTrainPack.w1_t.offset,
+                     ctypes.sizeof(_lib.MdgTrainUnpack), _lib.MdgTrainUnpack.part.offset,
+                     _lib.MdgTrainUnpack.gb2.offset, _lib.MdgStepIO.chain_alone.offset]
     assert cond == [ctypes.sizeof(_lib.MdgCondDims), ctypes.sizeof(_lib.MdgIpaLayerWeights),
                     ctypes.sizeof(_lib.MdgCondModel), ctypes.sizeof(_lib.MdgCondIO),
                     _lib.MdgCondModel.time_multiplier.offset, _lib.MdgCondModel.t_freqs.offset,
