@@ -31,8 +31,8 @@ __device__ __forceinline__ int packed_of_nat(int n, int D) {
 }
 
 // One 32 x 32 tile of a weight: source row gathered by `src_row`, written cast to CT row-major
-// and transposed, both coalesced (the transpose goes through LDS: scattered 2-byte stores made
-// this launch 1 ms per layer).
+// and transposed, both coalesced (the transpose goes through LDS); the whole pack launch takes
+// ~12 us per layer (rocprofv3, B = 8 training step).
 template <typename CT, typename SrcRow>
 __device__ __forceinline__ void pack_tile(float (*tile)[33], SrcRow src_row, void* dst, void* dst_t, int R, int K,
                                           int r0, int k0) {
@@ -136,7 +136,8 @@ __global__ __launch_bounds__(256) void unpack_kernel(const mdg_train_unpack u) {
         db[nn] = bv;
       }
     }
-  } else if (job < 4) {  // bias_k / bias_v gradients of attention job - 2
+  } else if (job < 4) {  // bias_k / bias_v gradients of attention job - 2 (the caller passes the
+    // partials already summed over their slots: parts = 1 in the training Function)
     const int i = job - 2, np = u.parts[i];
     const float* bp = u.bpart[i];  // [H][parts][2][32]
     const float* tab = u.rope_tab[i];
@@ -163,26 +164,32 @@ __global__ __launch_bounds__(256) void unpack_kernel(const mdg_train_unpack u) {
     }
   } else if (job == 4) {  // adaLN gradient [B][9C]
     // chunk -> (part tensor, row): shift_l, scale_l | gate_l | shift_t, scale_t | gate_t | shift_m,
-    // scale_m | gate_m  (latent_model.py:459-461)
+    // scale_m | gate_m  (latent_model.py:459-461).  8 lanes per element split the row blocks
+    // (a serial sum over them per element was latency-bound), combined by shuffles in lane order.
     const int src[9] = {0, 0, 1, 1, 1, 2, 2, 2, 3}, row[9] = {0, 1, 2, 0, 1, 2, 0, 1, 2};
-    for (int e = t0; e < B * 9 * C; e += stride) {
-      const int b = e / (9 * C), ck = e - b * 9 * C, c9 = ck / C, k = ck - c9 * C;
+    const int g = t0 & 7;
+    for (int e0 = t0 >> 3; e0 < B * 9 * C; e0 += stride >> 3) {
+      const int b = e0 / (9 * C), ck = e0 - b * 9 * C, c9 = ck / C, k = ck - c9 * C;
       const float* pp = u.part[src[c9]];
       float s = 0.f;
-      for (int q = 0; q < nb; ++q) s += pp[(((size_t)b * nb + q) * 4 + row[c9]) * C + k];
-      u.dmods[e] = s;
+      for (int q = g; q < nb; q += 8) s += pp[(((size_t)b * nb + q) * 4 + row[c9]) * C + k];
+      s += __shfl_xor(s, 1, 64);
+      s += __shfl_xor(s, 2, 64);
+      s += __shfl_xor(s, 4, 64);
+      if (g == 0) u.dmods[e0] = s;
     }
   } else {  // out_proj (spatial, temporal) and fc2 bias gradients: row 3 of part_s / part_t / part_m
-    for (int e = t0; e < 3 * C; e += stride) {
-      const int w = e / C, k = e - w * C;
+    const int g = t0 & 7;
+    for (int e0 = t0 >> 3; e0 < 3 * C; e0 += stride >> 3) {
+      const int w = e0 / C, k = e0 - w * C;
       const float* pp = u.part[w + 1];
       float s = 0.f;
-      for (int b = 0; b < B; ++b) {
-        float sb = 0.f;
-        for (int q = 0; q < nb; ++q) sb += pp[(((size_t)b * nb + q) * 4 + 3) * C + k];
-        s += sb;
-      }
-      (w == 0 ? u.gbo[0] : w == 1 ? u.gbo[1] : u.gb2)[k] = s;
+      for (int b = 0; b < B; ++b)
+        for (int q = g; q < nb; q += 8) s += pp[(((size_t)b * nb + q) * 4 + 3) * C + k];
+      s += __shfl_xor(s, 1, 64);
+      s += __shfl_xor(s, 2, 64);
+      s += __shfl_xor(s, 4, 64);
+      if (g == 0) (w == 0 ? u.gbo[0] : w == 1 ? u.gbo[1] : u.gb2)[k] = s;
     }
   }
 }

@@ -84,9 +84,16 @@ class IPALayer(nn.Module):
         self.fc2 = nn.Linear(ffn_embed_dim, embed_dim)
         self.final_layer_norm = nn.LayerNorm(embed_dim, elementwise_affine=False, eps=1e-6)
 
+    hip_hl = None  # train_hip.LayerHelper while LatentMDGenModel.run_ipa runs the HIP training path
+
     def forward(self, x, t, mask, rots, trans, mods=None):
-        sh_l, sc_l, g_l, sh_m, sc_m, g_m = (self.adaLN_modulation(t) if mods is None else mods).chunk(6, dim=-1)
+        m6 = self.adaLN_modulation(t) if mods is None else mods
         x = x + self.ipa(self.ipa_norm(x), rots, trans, mask)
+        if self.hip_hl is not None:  # MHA + MLP sublayers on the HIP training kernels
+            from ..train_hip import hip_ipa_layer_tail
+
+            return hip_ipa_layer_tail(self.hip_hl, self, x, m6, mask)
+        sh_l, sc_l, g_l, sh_m, sc_m, g_m = m6.chunk(6, dim=-1)
         x = x + g_l.unsqueeze(1) * self.mha_l(modulate(self.mha_layer_norm(x), sh_l, sc_l), mask)
         h = modulate(self.final_layer_norm(x), sh_m, sc_m)
         return x + g_m.unsqueeze(1) * self.fc2(gelu(self.fc1(h)))
@@ -211,8 +218,12 @@ class LatentMDGenModel(nn.Module):
         # kernels (mdg_ipa_core_fwd / _bwd) between the autograd projections
         hip_core = (self.backend == "hip" and getattr(self, "train_backend", "hip") == "hip" and mask_b.is_cuda
                     and torch.is_grad_enabled())
+        # the MHA + MLP of each IPA layer on the HIP layer Function (the block stack's kernels)
+        # wherever the block stack itself takes them
+        hl = self._train_helper() if hip_core and self._use_hip_layers(mask_b) else None
         for layer in self.ipa_layers:
             layer.ipa.hip_core = hip_core
+            layer.hip_hl = hl
         if not self.tps:
             x = torch.zeros(B, L, C, device=mask_b.device)
             if use_aa:
@@ -283,7 +294,7 @@ class LatentMDGenModel(nn.Module):
         hip_layers = self._use_hip_layers(h)
         ckpt = bool(getattr(self.args, "grad_checkpointing", False)) and self.training
         # the HIP training path: every adaLN linear of the model as one stacked GEMM
-        ada = self._stacked_adaln(c[:, 0]) if hip_layers and not ckpt else None
+        ada = self._stacked_adaln(c[:, 0]) if hip_layers else None
         if self.args.prepend_ipa:
             h = h + self.run_ipa(c[:, 0], mask[:, 0], start_frames, end_frames, aatype,
                                  ada=None if ada is None else ada[0])[:, None]
@@ -294,8 +305,8 @@ class LatentMDGenModel(nn.Module):
             if hip_layers and ckpt:  # --grad_checkpointing: the HIP Function re-runs in backward
                 # (reentrant form: the first forward runs without autograd, so the Function's
                 # saved activations of every layer but the one being differentiated are freed)
-                h = torch.utils.checkpoint.checkpoint(hip_layer_forward, hl, layer, h,
-                                                      layer.adaLN_modulation(c[:, 0]), mask, use_reentrant=True)
+                h = torch.utils.checkpoint.checkpoint(hip_layer_forward, hl, layer, h, ada[1][k], mask,
+                                                      use_reentrant=True)
             elif hip_layers:  # block forward + backward in libmdgen_hip.so (train_hip.py)
                 h = hip_layer_forward(hl, layer, h, ada[1][k], mask)
             elif getattr(self.args, "grad_checkpointing", False) and self.training:

@@ -135,6 +135,24 @@ def hip_layer_forward(hl, layer, h, mods, mask):
     return _HipLayerFn.apply(h, mods, mask, hl, inv_freq, *_layer_params(layer))
 
 
+def hip_ipa_layer_tail(hl, layer, x1, mods6, mask_b):
+    """IPALayer (latent_model.py:341-394) after its IPA sublayer: x1 + g_l MHA_L(mod(LN x1)),
+    then + g_m MLP(mod(LN .)), on the HIP training Function as a T = 1 block whose temporal
+    sublayer has gate 0: adaLN rows [sh_l, sc_l, g_l, 0, 0, 0, sh_m, sc_m, g_m].  With g_t = 0
+    the temporal branch adds exactly 0 forward and passes exactly 0 gradient back (dy_t = dh * 0),
+    so this is the IPA layer's arithmetic; its stand-in weights (mha_l's again) receive zero
+    gradients.  x1 [B, L, C], mods6 [B, 6C], mask_b [B, L]."""
+    C = hl.C
+    inv_freq = layer.mha_l.attn.rot_emb.inv_freq if hl.rope else None
+    mods9 = torch.cat([mods6[:, :3 * C], mods6.new_zeros(mods6.shape[0], 3 * C), mods6[:, 3 * C:]], -1)
+    mha = layer.mha_l.attn
+    att = [mha.q_proj.weight, mha.q_proj.bias, mha.k_proj.weight, mha.k_proj.bias, mha.v_proj.weight, mha.v_proj.bias,
+           mha.out_proj.weight, mha.out_proj.bias, mha.bias_k, mha.bias_v]
+    params = att + att + [layer.fc1.weight, layer.fc1.bias, layer.fc2.weight, layer.fc2.bias]
+    out = _HipLayerFn.apply(x1[:, None], mods9, mask_b[:, None], hl, inv_freq, *params)
+    return out[:, 0]
+
+
 class _HipLayerFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, h, mods, mask, hl, inv_freq, *params):
@@ -293,7 +311,9 @@ class _HipLayerFn(torch.autograd.Function):
                                                     ctx.mask.data_ptr(), do.data_ptr(), _lib.ptr(rope_l), L + 1,
                                                     dqkv.data_ptr(), bpart.data_ptr(), qscale, s),
                            "mdg_attn_spatial_bwd")
-            grads[f"kvb{i}"] = bpart
+            # [H][1][2][32]: the partials summed over their slots by one reduction kernel (the
+            # unpack launch summing 1 024 temporal slots per element serially took 1 ms)
+            grads[f"kvb{i}"] = bpart.sum(1, keepdim=True)
             grads[f"wqkv{i}"], grads[f"bqkv{i}"] = wg(dqkv, xn, True)
             return dx_gemm(dqkv, P[f"wqkv_t{i}"], 3 * C, C)
 
