@@ -103,3 +103,41 @@ def test_unsupported_flags_raise():
             LatentMDGenModel(a, 21)
 
 
+
+
+def test_token_linear_split_k_backward_matches_linear():
+    """_TokenLinear (the training step's token-wide linears: split-K weight gradient over 16 token
+    chunks, layers.py) against nn.Linear's autograd, on the CPU."""
+    from mdgen_finetune_amd.model.layers import _TokenLinear
+
+    gen = torch.Generator().manual_seed(0)
+    lin = torch.nn.Linear(21, 384)
+    x = torch.randn(2, 1000, 4, 21, generator=gen, requires_grad=True)
+    g = torch.randn(2, 1000, 4, 384, generator=gen)
+    grads = []
+    for split in (False, True):
+        lin.zero_grad(set_to_none=True)
+        x.grad = None
+        y = _TokenLinear.apply(x, lin.weight, lin.bias) if split else lin(x)
+        (y * g).sum().backward()
+        grads.append((x.grad.clone(), lin.weight.grad.clone(), lin.bias.grad.clone()))
+    for a, b in zip(*grads):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-4)
+
+
+def test_stacked_adaln_equals_per_module_adaln():
+    """LatentMDGenModel._stacked_adaln (every adaLN linear as one GEMM on the HIP training path)
+    returns each module's own SiLU + Linear output."""
+    d, cfg = load_golden("small_sim_T8")
+    m, _ = build_model(cfg)
+    with torch.no_grad():
+        for p in m.parameters():
+            p.add_(0.01 * torch.randn_like(p))
+        c0 = torch.randn(3, m.args.embed_dim)
+        ipa, blocks, fin = m._stacked_adaln(c0)
+        for out, layer in zip(ipa, m.ipa_layers if m.args.prepend_ipa else []):
+            torch.testing.assert_close(out, layer.adaLN_modulation(c0), rtol=1e-5, atol=1e-6)
+        for out, layer in zip(blocks, m.layers):
+            torch.testing.assert_close(out, layer.adaLN_modulation(c0), rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(fin, m.emb_to_latent.adaLN_modulation(c0), rtol=1e-5, atol=1e-6)
+        assert len(blocks) == len(m.layers)
