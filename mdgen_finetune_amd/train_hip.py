@@ -36,6 +36,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 
 import torch
 
@@ -95,6 +96,17 @@ class LayerHelper:
         self.rope = not a.no_rope
         self.set_dtype(dtype)
         self._tables = {}
+
+    def __getstate__(self):
+        """Picklable (the model and its IPA layers keep a reference): the ctypes library and
+        the device tables are rebuilt on demand."""
+        st = dict(self.__dict__)
+        st["lib"], st["_tables"] = None, {}
+        return st
+
+    def __setstate__(self, st):
+        self.__dict__.update(st)
+        self.lib = _lib.load() if os.path.exists(_lib.LIB_PATH) else None
 
     def set_dtype(self, dtype):
         if dtype not in ("bf16", "f32"):
