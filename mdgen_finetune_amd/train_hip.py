@@ -101,7 +101,7 @@ class LayerHelper:
         """Picklable (the model and its IPA layers keep a reference): the ctypes library and
         the device tables are rebuilt on demand."""
         st = dict(self.__dict__)
-        st["lib"], st["_tables"] = None, {}
+        st["lib"], st["_tables"], st["_planes"] = None, {}, {}
         return st
 
     def __setstate__(self, st):
@@ -125,6 +125,17 @@ class LayerHelper:
             t = torch.cat([freqs.cos().reshape(-1), freqs.sin().reshape(-1)]).to(inv_freq.device)
             self._tables[key] = t
         return t
+
+    def planes(self, key, shape, device):
+        """(buffer, fresh): the layer's persistent padded q|k|v planes for this shape (fresh = just
+        allocated: its pad columns still need mdg_layer_fwd_train's init_planes pass)."""
+        cache = self.__dict__.setdefault("_planes", {})
+        key = key + (self.dtype_name, str(device))
+        buf = cache.get(key)
+        if buf is None:
+            buf = cache[key] = torch.empty(*shape, device=device, dtype=self.ct)
+            return buf, True
+        return buf, False
 
     def dims(self, B, T, L):
         return _lib.MdgDims(B=B, T=T, L=L, C=self.C, H=self.H, D=self.D, F=self.F, latent=self.model.latent_dim,
@@ -218,10 +229,16 @@ class _HipLayerFn(torch.autograd.Function):
         _lib.check(lib.mdg_mask_bias(B, T, L, mask.data_ptr(), kb_t.data_ptr(), kb_s.data_ptr(), s), "mdg_mask_bias")
         e = lambda *shape, dt=ct: torch.empty(*shape, device=dev, dtype=dt)  # noqa: E731
         r = lambda cols: _rows(N, cols, ct, dev)  # noqa: E731  (operands of the weight gradients)
+        # the padded attention planes persist per layer and shape: their pad columns (0, and 1.0 in
+        # k / v column D) are written once (init_planes) instead of a memset + set_vpad pass per
+        # step; the q|k|v GEMM rewrites every other column each forward
+        planes_t, fresh_t = hl.planes(("t", params[0].data_ptr(), B, T, L), (3, B * L, H, T, _lib.MDG_DP), dev)
+        planes_s, fresh_s = (hl.planes(("s", params[0].data_ptr(), B, T, L), (3, B * T, H, L, _lib.MDG_DP), dev)
+                             if long_l else (e(N, 3 * C), False))
         sv = {"xn": [r(C) for _ in range(3)], "stats": [e(N, 2, dt=torch.float32) for _ in range(3)],
-              "qkv_s": e(3, B * T, H, L, _lib.MDG_DP) if long_l else e(N, 3 * C),
+              "qkv_s": planes_s,
               "lse_s": e(B * T, H, L, dt=torch.float32) if long_l else None,
-              "qkv_t": e(3, B * L, H, T, _lib.MDG_DP), "lse_t": e(B * L, H, T, dt=torch.float32),
+              "qkv_t": planes_t, "lse_t": e(B * L, H, T, dt=torch.float32),
               "o": [r(C), r(C)], "y": [e(N, C) for _ in range(3)],
               "h1": e(N, C, dt=torch.float32), "h2": e(N, C, dt=torch.float32), "u": e(N, F), "act": r(F)}
         cs = _lib.MdgLayerSaved()
@@ -231,7 +248,7 @@ class _HipLayerFn(torch.autograd.Function):
         cs.qkv_t, cs.lse_t = sv["qkv_t"].data_ptr(), sv["lse_t"].data_ptr()
         cs.o[0], cs.o[1] = sv["o"][0].data_ptr(), sv["o"][1].data_ptr()
         cs.h1, cs.h2, cs.u, cs.act = sv["h1"].data_ptr(), sv["h2"].data_ptr(), sv["u"].data_ptr(), sv["act"].data_ptr()
-        cs.init_planes = 1
+        cs.init_planes = int(fresh_t or fresh_s)
         h_out = torch.empty_like(h)
         _lib.check(lib.mdg_layer_fwd_train(ctypes.byref(dims), ctypes.byref(lw), _lib.ptr(rope_l), _lib.ptr(rope_t),
                                            mods.data_ptr(), mask.data_ptr(), kb_t.data_ptr(), kb_s.data_ptr(),
