@@ -352,14 +352,30 @@ __global__ __launch_bounds__(256) void attn_bwd_prep_kernel(int B, int T, int L,
   const CT* drow = dout + n * C + head * D;
   CT* prow = dop + (((size_t)seq * H + head) * T + t) * kDP;
   float dl = 0.f;
-  for (int d0 = 0; d0 < kDP; d0 += 4) {
-    float4 dv = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (d0 < D) {
-      const float4 ov = ld4f<CT>(orow + d0);
-      dv = ld4f<CT>(drow + d0);
-      dl += dv.x * ov.x + dv.y * ov.y + dv.z * ov.z + dv.w * ov.w;
+  if (D % 8 == 0) {  // 16-B (bf16) pieces: half the memory instructions of the 4-wide loop below
+#pragma unroll
+    for (int d0 = 0; d0 < kDP; d0 += 8) {
+      typename V8<CT>::T dv = zero8<CT>();
+      if (d0 < D) {
+        const typename V8<CT>::T ov = ld8<CT>(orow + d0);
+        dv = ld8<CT>(drow + d0);
+#pragma unroll
+        for (int j = 0; j < 8; j += 4)
+          dl += (float)dv[j] * (float)ov[j] + (float)dv[j + 1] * (float)ov[j + 1] + (float)dv[j + 2] * (float)ov[j + 2] +
+                (float)dv[j + 3] * (float)ov[j + 3];
+      }
+      st8<CT>(prow + d0, dv);
     }
-    st4<CT>(prow + d0, dv.x, dv.y, dv.z, dv.w);
+  } else {
+    for (int d0 = 0; d0 < kDP; d0 += 4) {
+      float4 dv = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (d0 < D) {
+        const float4 ov = ld4f<CT>(orow + d0);
+        dv = ld4f<CT>(drow + d0);
+        dl += dv.x * ov.x + dv.y * ov.y + dv.z * ov.z + dv.w * ov.w;
+      }
+      st4<CT>(prow + d0, dv.x, dv.y, dv.z, dv.w);
+    }
   }
   delta[((size_t)seq * H + head) * T + t] = dl;
 }
