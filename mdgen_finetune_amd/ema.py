@@ -22,8 +22,9 @@ class ExponentialMovingAverage:
 
     @torch.no_grad()
     def update(self, model: torch.nn.Module) -> None:
-        """stored -= (stored - v) * w per floating tensor, as three multi-tensor launches (the
-        same two roundings as the per-tensor form, which cost 3 launches per tensor)."""
+        """stored -= (stored - v) * w per floating tensor (ema.py's update), as ONE multi-tensor
+        lerp pass: stored + w (v - stored) is the same update (within an ulp; the per-tensor form
+        cost 3 launches per tensor, a three-pass foreach form 2.7x the bytes of this one)."""
         w = 1.0 - self.decay
         fs, fv = [], []
         for k, v in model.state_dict().items():
@@ -34,9 +35,7 @@ class ExponentialMovingAverage:
             else:
                 stored.copy_(v)
         if fs:
-            d = torch._foreach_sub(fs, fv)
-            torch._foreach_mul_(d, w)
-            torch._foreach_sub_(fs, d)
+            torch._foreach_lerp_(fs, fv, w)
 
     def load_state_dict(self, state_dict) -> None:
         for k, v in state_dict["params"].items():
