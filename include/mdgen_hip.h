@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define MDG_ABI_VERSION 16
+#define MDG_ABI_VERSION 17
 #define MDG_MAX_LAYERS 16
 #define MDG_DP 32      /* padded head dim of the attention operand buffers for head_dim <= 31 */
 #define MDG_DP_WIDE 64 /* ... and for 32 <= head_dim <= 63 (column head_dim of the padded k / v rows
@@ -232,10 +232,12 @@ int mdg_attn_temporal_packed(int32_t dtype, int32_t B, int32_t T, int32_t L, int
                              const void* qkv_t, const float* kbias, const float* kvb, void* out,
                              void* stream);
 /* The same, also writing lse [B*L][H][T] = log2 of each query row's softmax normaliser in the
-   planes' score units (the training backward recomputes P from it). */
+   planes' score units (the training backward recomputes P from it), and (bf16, optional) out_lo
+   CT [N][C] = O - bf16(O), the rounding residual of out, so the backward's delta = dO . O is
+   accurate where the bias key dominates a row (null = skip). */
 int mdg_attn_temporal_lse(int32_t dtype, int32_t B, int32_t T, int32_t L, int32_t H, int32_t D,
-                          const void* qkv_t, const float* kbias, const float* kvb, void* out, float* lse,
-                          void* stream);
+                          const void* qkv_t, const float* kbias, const float* kvb, void* out, void* out_lo,
+                          float* lse, void* stream);
 
 /* Batch preparation (NewMDGenWrapper.prep_batch, wrapper.py:283-365 with get_offsets,
    utils.py:7-14, and rot_to_quat, rigid_utils.py:191-210), per token (b, t, l):
@@ -368,6 +370,9 @@ typedef struct {
   void* qkv_t;       /* CT [3][B*L][H][T][32] temporal q|k|v planes (k, v pad column D = 1) */
   float* lse_t;      /* [B*L][H][T] */
   void* o[2];        /* CT [N][C] attention outputs: spatial, temporal */
+  void* o_lo[2];     /* bf16 only (else null): CT [N][C] rounding residuals O - bf16(O) of the
+                        attentions that run on the temporal kernel (temporal; spatial for L >= 16),
+                        null = skip (the backward then takes delta from o alone) */
   void* y[3];        /* CT [N][C] pre-gate projection outputs: spatial out_proj, temporal
                         out_proj, fc2 */
   float* h1;         /* fp32 [N][C] residual after the spatial sublayer */
@@ -410,14 +415,16 @@ int32_t mdg_attn_spatial_bwd_parts(int32_t n_frames, int32_t L, int32_t D);
 /* Scratch of mdg_attn_temporal_bwd: dO planes CT [B*L][H][T][32] then delta fp32 [B*L][H][T]. */
 size_t mdg_attn_temporal_bwd_scratch(int32_t dtype, int32_t B, int32_t T, int32_t L, int32_t H);
 /* Temporal (and L >= 16 spatial) attention backward: from the forward's planes (qkv_t), lse,
-   output o (CT [N][C]) and its gradient dout (CT [N][C]), writes dq | dk | dv of the linear
+   output o (CT [N][C]; o_lo its residual from mdg_attn_temporal_lse or null) and its gradient
+   dout (CT [N][C]), writes dq | dk | dv of the linear
    projections (RoPE and the q scale undone: qscale = D^-1/2) into dqkv (CT, token-major rows of
    ld_dqkv >= 3C, packed column order); kscale = ln 2 for planes in log2 units (the forward's
    q carries log2 e).  bias_k / bias_v gradients (w.r.t. the rotated kvb rows) are written as
    per-slot partials bpart [H][parts][2][32].  generic = 1 selects the scalar kernels (the
    fp32 path always uses them). */
 int mdg_attn_temporal_bwd(int32_t dtype, int32_t B, int32_t T, int32_t L, int32_t H, int32_t D, const void* qkv_t,
-                          const float* kbias, const float* kvb, const void* o, const void* dout, const float* lse,
+                          const float* kbias, const float* kvb, const void* o, const void* o_lo, const void* dout,
+                          const float* lse,
                           const float* rope, int32_t rope_rows, void* scratch, void* dqkv, int32_t ld_dqkv,
                           float* bpart, float qscale, float kscale, int32_t generic, void* stream);
 /* Spatial attention backward (L < 16): q|k|v [N][3C] as saved by the forward, dout CT [N][C];

@@ -75,7 +75,7 @@ class MdgGemmDesc(ctypes.Structure):
 
 class MdgLayerSaved(ctypes.Structure):
     _fields_ = [("xn", _vp * 3), ("stats", _vp * 3), ("qkv_s", _vp), ("lse_s", _vp), ("qkv_t", _vp),
-                ("lse_t", _vp), ("o", _vp * 2), ("y", _vp * 3), ("h1", _vp), ("h2", _vp), ("u", _vp), ("act", _vp),
+                ("lse_t", _vp), ("o", _vp * 2), ("o_lo", _vp * 2), ("y", _vp * 3), ("h1", _vp), ("h2", _vp), ("u", _vp), ("act", _vp),
                 ("init_planes", _i32)]
 
 
@@ -140,7 +140,7 @@ SIGNATURES = [
     ("mdg_attn_spatial", _i32, [_i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
     ("mdg_attn_temporal", _i32, [_i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
     ("mdg_attn_temporal_packed", _i32, [_i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
-    ("mdg_attn_temporal_lse", _i32, [_i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
+    ("mdg_attn_temporal_lse", _i32, [_i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     ("mdg_prep_latents", _i32, [_i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     ("mdg_latents_to_atom14", _i32, [_i32, _i32, _i32, _i32, _i32, _i32] + [_vp] * 12),
     ("mdg_cond_workspace_bytes", ctypes.c_size_t, [ctypes.POINTER(MdgCondDims)]),
@@ -155,7 +155,7 @@ SIGNATURES = [
     ("mdg_attn_temporal_bwd_parts", _i32, [_i32, _i32, _i32, _i32]),
     ("mdg_attn_spatial_bwd_parts", _i32, [_i32, _i32, _i32]),
     ("mdg_attn_temporal_bwd_scratch", ctypes.c_size_t, [_i32, _i32, _i32, _i32, _i32]),
-    ("mdg_attn_temporal_bwd", _i32, [_i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32,
+    ("mdg_attn_temporal_bwd", _i32, [_i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32,
                                      _vp, _vp, _i32, _vp, _f32, _f32, _i32, _vp]),
     ("mdg_attn_spatial_bwd", _i32, [_i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _f32,
                                     _vp]),
@@ -167,7 +167,7 @@ SIGNATURES = [
     ("mdg_train_unpack_layer", _i32, [ctypes.POINTER(MdgTrainUnpack), _vp]),
 ]
 
-ABI_VERSION = 16
+ABI_VERSION = 17
 _LIB = None
 
 

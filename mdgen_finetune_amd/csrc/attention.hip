@@ -400,7 +400,7 @@ __device__ __forceinline__ void ta_setup(const bf16_t* Qg, const float* kvh, int
 
 // O = O^T / row sum (O^T row D), stored as O[token][head*D + d]
 __device__ __forceinline__ void ta_store(const f32x16& o, bf16_t* out, int q, int T, int L, int H, int D, int seq,
-                                         int head, int h, float mt, float* lse) {
+                                         int head, int h, float mt, float* lse, bf16_t* out_lo) {
   const int hD = (D >> 2) & 1, regD = (D & 3) + 4 * (D >> 3);
   float mine = 0.f;
 #pragma unroll
@@ -421,6 +421,25 @@ __device__ __forceinline__ void ta_store(const f32x16& o, bf16_t* out, int q, in
       if (d0 < D)
         st4<bf16_t>(orow + d0, o[4 * g4] * inv, o[4 * g4 + 1] * inv, o[4 * g4 + 2] * inv, o[4 * g4 + 3] * inv);
     }
+    // training: the bf16 rounding residual of O (O = out + out_lo to ~2^-17), so the backward's
+    // delta = dO . O matches the fp32 P it recomputes even where the bias key dominates a row
+    // (a fully padded sequence: P = [1, 0, ...], true dS = 0)
+    if (out_lo) {
+      bf16_t* lrow = out_lo + ((size_t)(b * T + q) * L + l) * C + head * D;
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d0 = 8 * g4 + 4 * h;
+        if (d0 < D) {
+          float v[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float x = o[4 * g4 + e] * inv;
+            v[e] = x - (float)(bf16_t)x;
+          }
+          st4<bf16_t>(lrow + d0, v[0], v[1], v[2], v[3]);
+        }
+      }
+    }
   }
 }
 
@@ -430,7 +449,8 @@ __global__ __launch_bounds__(kTW * 64, 4) void attn_temporal_bf16_kernel(const b
                                                                     const float* __restrict__ kbias,
                                                                     const float* __restrict__ kvb,
                                                                     bf16_t* __restrict__ out, int T, int L,
-                                                                    int H, int D, int BL, float* __restrict__ lse) {
+                                                                    int H, int D, int BL, float* __restrict__ lse,
+                                                                    bf16_t* __restrict__ out_lo) {
   constexpr int DP = MDG_DP, KC = kTKC, NTH = kTW * 64;
   constexpr bool PACKED = PD > 0;
   constexpr int RS = PACKED ? PD : DP;  // plane row stride (a compile-time constant either way)
@@ -552,7 +572,7 @@ __global__ __launch_bounds__(kTW * 64, 4) void attn_temporal_bf16_kernel(const b
       __syncthreads();
     }
     if (grow || !s_bad) {  // block-uniform
-      ta_store(o, out, q, T, L, H, D, seq, head, h, mt, lse);
+      ta_store(o, out, q, T, L, H, D, seq, head, h, mt, lse, out_lo);
       return;
     }
   }
@@ -720,8 +740,9 @@ __global__ __launch_bounds__(256) void attn_spatial_quad_kernel(const CT* __rest
 
 hipError_t attn_temporal_launch(int dtype, int B, int T, int L, int H, int D, const void* qkv_t,
                                 const float* kbias, const float* kvb, void* out, hipStream_t s, float* lse,
-                                bool packed) {
+                                bool packed, void* out_lo) {
   if (packed && (dtype != MDG_BF16 || D % 8 || D >= MDG_DP)) return hipErrorInvalidValue;
+  if (out_lo && (dtype != MDG_BF16 || D >= MDG_DP)) return hipErrorInvalidValue;  // bf16 MFMA kernel only
   if (D >= MDG_DP) {  // wide heads (32..63): the generic 16x16 MFMA kernel on 64-column rows
     dim3 grid((T + 127) / 128, H, B * L);
     if (dtype == MDG_BF16)
@@ -742,14 +763,14 @@ hipError_t attn_temporal_launch(int dtype, int B, int T, int L, int H, int D, co
       dim3 grid((unsigned)((T + 127) / 128 * H * B * L));
 #define MDG_TA4(PD_)                                                                                     \
   hipLaunchKernelGGL((attn_temporal_bf16_kernel<4, 64, PD_>), grid, dim3(256), 0, s, (const bf16_t*)qkv_t, kbias, \
-                     kvb, (bf16_t*)out, T, L, H, D, B * L, lse)
+                     kvb, (bf16_t*)out, T, L, H, D, B * L, lse, (bf16_t*)out_lo)
       if (!packed) MDG_TA4(0); else if (D == 24) MDG_TA4(24); else if (D == 16) MDG_TA4(16); else MDG_TA4(8);
 #undef MDG_TA4
     } else {
       dim3 grid((unsigned)((T + 255) / 256 * H * B * L));
 #define MDG_TA8(PD_)                                                                                      \
   hipLaunchKernelGGL((attn_temporal_bf16_kernel<8, 128, PD_>), grid, dim3(512), 0, s, (const bf16_t*)qkv_t, kbias, \
-                     kvb, (bf16_t*)out, T, L, H, D, B * L, lse)
+                     kvb, (bf16_t*)out, T, L, H, D, B * L, lse, (bf16_t*)out_lo)
       if (!packed) MDG_TA8(0); else if (D == 24) MDG_TA8(24); else if (D == 16) MDG_TA8(16); else MDG_TA8(8);
 #undef MDG_TA8
     }

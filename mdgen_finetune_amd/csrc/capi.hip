@@ -40,7 +40,7 @@ bool rowln_qkv_supported(const mdg_gemm_desc& r, const mdg_gemm_desc& q);
 hipError_t rowln_qkv_launch(const mdg_gemm_desc& r, const mdg_gemm_desc& q, hipStream_t s);
 hipError_t attn_temporal_launch(int dtype, int B, int T, int L, int H, int D, const void* qkv_t,
                                 const float* kbias, const float* kvb, void* out, hipStream_t s,
-                                float* lse = nullptr, bool packed = false);
+                                float* lse = nullptr, bool packed = false, void* out_lo = nullptr);
 hipError_t attn_spatial_launch(int dtype, int nf, int L, int H, int D, const void* qkv,
                                const float* kvb, const float* mask, void* out, hipStream_t s);
 hipError_t embed_launch(int N, int T, int L, int C, int K, const float* x, const float* W,
@@ -69,7 +69,8 @@ hipError_t ln_gate_bwd_launch(int dtype, int M, int C, int TL, const void* dxn, 
                               float* dh_out, const void* y, int gate_off, void* dy, float* part, hipStream_t s);
 int attn_bwd_parts(int dtype, int B, int T, int L);
 hipError_t attn_temporal_bwd_launch(int dtype, int B, int T, int L, int H, int D, const void* qkv_t,
-                                    const float* kbias, const float* kvb, const void* o, const void* dout,
+                                    const float* kbias, const float* kvb, const void* o, const void* o_lo,
+                                    const void* dout,
                                     const float* lse, const float* rope, int rope_rows, void* dop, float* delta,
                                     void* dqkv, int ldq, float* bpart, float qscale, float kscale, int generic,
                                     hipStream_t s);
@@ -113,6 +114,9 @@ int fail(int code, const char* fmt, ...) {
   return code;
 }
 
+#ifdef MDG_DIAGNOSTICS
+// Diagnostic builds only (make DIAG=1; tools/lane_snap.py, tools/lane_hist.py): the product
+// library has none of this state, so its calls stay reentrant (include/mdgen_hip.h).
 // Diagnostic (MDG_DEBUG_COHERENCE, tools/lane_hist.py): inside a denoise step every checked
 // launch is followed by a small kernel on the same stream.  =1: each of its waves performs an
 // agent-scope release + acquire (L2 write-back + invalidate on the XCD it runs on, L1 invalidate
@@ -166,11 +170,15 @@ int debug_coherence() {
   return v;
 }
 
+#endif  // MDG_DIAGNOSTICS
+
 int hip_check(hipError_t e, const char* what) {
   if (e == hipSuccess) {
+#ifdef MDG_DIAGNOSTICS
     if (g_dbg_in_step && debug_coherence())
       hipLaunchKernelGGL(coherence_kernel, dim3(1024), dim3(64), 0, g_dbg_stream, debug_coherence() == 1 ? 1 : 0);
     if (g_dbg_in_step && g_snap.dst) debug_snapshot(what);
+#endif
     return MDG_OK;
   }
   return fail((int)e, "%s: %s", what, hipGetErrorString(e));
@@ -433,15 +441,17 @@ int mdg_attn_temporal_packed(int32_t dtype, int32_t B, int32_t T, int32_t L, int
 }
 
 int mdg_attn_temporal_lse(int32_t dtype, int32_t B, int32_t T, int32_t L, int32_t H, int32_t D,
-                          const void* qkv_t, const float* kbias, const float* kvb, void* out, float* lse,
-                          void* stream) {
+                          const void* qkv_t, const float* kbias, const float* kvb, void* out, void* out_lo,
+                          float* lse, void* stream) {
   if (dtype != MDG_F32 && dtype != MDG_BF16) return fail(MDG_E_DTYPE, "dtype %d", dtype);
   if (!qkv_t || !kbias || !kvb || !out || !lse) return fail(MDG_E_ARG, "attn_temporal_lse: null pointer");
+  if (out_lo && dtype != MDG_BF16) return fail(MDG_E_ARG, "attn_temporal_lse: out_lo is for bf16 (f32 O is exact)");
   if (B <= 0 || T <= 0 || L <= 0 || H <= 0 || D <= 0 || D % 4 || D >= MDG_DP)
     return fail(MDG_E_SHAPE, "attn_temporal_lse: B=%d T=%d L=%d H=%d D=%d (training kernels: head_dim < %d)", B, T,
                 L, H, D, MDG_DP);
   if (H > 65535 || B * L > 65535) return fail(MDG_E_SHAPE, "attn_temporal_lse: grid too large");
-  return hip_check(mdg::attn_temporal_launch(dtype, B, T, L, H, D, qkv_t, kbias, kvb, out, (hipStream_t)stream, lse),
+  return hip_check(mdg::attn_temporal_launch(dtype, B, T, L, H, D, qkv_t, kbias, kvb, out, (hipStream_t)stream, lse,
+                                             false, out_lo),
                    "attn_temporal_lse");
 }
 
@@ -715,6 +725,7 @@ static int denoise_range(const mdg_model* m, const mdg_step_io* io, const float*
   return mdg_gemm(&g, stream);  // bf16: the one-pass final_euler_kernel
 }
 
+#ifdef MDG_DIAGNOSTICS
 static int denoise_range_dbg(const mdg_model* m, const mdg_step_io* io, const float* mask, void* ws, int first,
                              int last, void* stream) {
   g_dbg_stream = (hipStream_t)stream;
@@ -731,6 +742,13 @@ static int denoise_range_dbg(const mdg_model* m, const mdg_step_io* io, const fl
   g_dbg_in_step = false;
   return e;
 }
+
+#else
+static int denoise_range_dbg(const mdg_model* m, const mdg_step_io* io, const float* mask, void* ws, int first,
+                             int last, void* stream) {
+  return denoise_range(m, io, mask, ws, first, last, stream);
+}
+#endif
 
 int mdg_denoise_step(const mdg_model* m, const mdg_step_io* io, const float* mask, void* ws, void* stream) {
   if (!m) return fail(MDG_E_ARG, "denoise_step: null model/io");
@@ -869,7 +887,7 @@ int mdg_layer_fwd_train(const mdg_dims* d, const mdg_layer_weights* w, const flo
   if (long_l) {
     q.qkv_layout = MDG_QKV_TEMPORAL; q.qkv_out = sv->qkv_s; q.qscale = qs * log2e; q.T = L; q.L = 1;
     if (int e = mdg_gemm(&q, stream)) return e;
-    if (int e = mdg_attn_temporal_lse(d->dtype, B * T, L, 1, H, D, sv->qkv_s, kbias_s, w->kvb[0], sv->o[0], sv->lse_s,
+    if (int e = mdg_attn_temporal_lse(d->dtype, B * T, L, 1, H, D, sv->qkv_s, kbias_s, w->kvb[0], sv->o[0], sv->o_lo[0], sv->lse_s,
                                       stream))
       return e;
     q.T = T; q.L = L;
@@ -888,7 +906,8 @@ int mdg_layer_fwd_train(const mdg_dims* d, const mdg_layer_weights* w, const flo
   q.epi = MDG_EPI_QKV; q.A = sv->xn[1]; q.W = w->wqkv[1]; q.bias = w->bqkv[1];
   q.qkv_layout = MDG_QKV_TEMPORAL; q.qkv_out = sv->qkv_t; q.qscale = qs * log2e; q.rope = rope_t; q.rope_rows = T + 1;
   if (int e = mdg_gemm(&q, stream)) return e;
-  if (int e = mdg_attn_temporal_lse(d->dtype, B, T, L, H, D, sv->qkv_t, kbias_t, w->kvb[1], sv->o[1], sv->lse_t, stream))
+  if (int e = mdg_attn_temporal_lse(d->dtype, B, T, L, H, D, sv->qkv_t, kbias_t, w->kvb[1], sv->o[1], sv->o_lo[1], sv->lse_t,
+                                    stream))
     return e;
   r.A = sv->o[1]; r.W = w->wo[1]; r.bias = w->bo[1]; r.resid_in = sv->h1; r.resid = sv->h2; r.gate_off = 5 * C;
   r.aux = sv->y[1];
@@ -940,7 +959,8 @@ size_t mdg_attn_temporal_bwd_scratch(int32_t dtype, int32_t B, int32_t T, int32_
 }
 
 int mdg_attn_temporal_bwd(int32_t dtype, int32_t B, int32_t T, int32_t L, int32_t H, int32_t D, const void* qkv_t,
-                          const float* kbias, const float* kvb, const void* o, const void* dout, const float* lse,
+                          const float* kbias, const float* kvb, const void* o, const void* o_lo, const void* dout,
+                          const float* lse,
                           const float* rope, int32_t rope_rows, void* scratch, void* dqkv, int32_t ld_dqkv,
                           float* bpart, float qscale, float kscale, int32_t generic, void* stream) {
   if (dtype != MDG_F32 && dtype != MDG_BF16) return fail(MDG_E_DTYPE, "dtype %d", dtype);
@@ -954,7 +974,7 @@ int mdg_attn_temporal_bwd(int32_t dtype, int32_t B, int32_t T, int32_t L, int32_
   const size_t rows = (size_t)B * L * H * T;
   void* dop = scratch;
   float* delta = (float*)((char*)scratch + align256(rows * MDG_DP * ct_size(dtype)));
-  return hip_check(mdg::attn_temporal_bwd_launch(dtype, B, T, L, H, D, qkv_t, kbias, kvb, o, dout, lse, rope,
+  return hip_check(mdg::attn_temporal_bwd_launch(dtype, B, T, L, H, D, qkv_t, kbias, kvb, o, o_lo, dout, lse, rope,
                                                  rope_rows, dop, delta, dqkv, ld_dqkv, bpart, qscale, kscale,
                                                  generic || dtype == MDG_F32, (hipStream_t)stream),
                    "attn_temporal_bwd");
@@ -1282,6 +1302,7 @@ int mdg_wgrad(int32_t dtype, int32_t N, int32_t M, int32_t K, const void* dy, in
 
 }  // extern "C"
 
+#ifdef MDG_DIAGNOSTICS
 // ---- diagnostics (not part of the ABI in include/mdgen_hip.h; tools/lane_snap.py)
 extern "C" int mdg_debug_snapshots(void* dst, size_t cap) {
   g_snap.dst = (char*)dst;
@@ -1301,3 +1322,4 @@ extern "C" int mdg_debug_snapshot_info(int i, size_t* off, void** ws, char* labe
   snprintf(label, n, "%s", g_snap.label[i].c_str());
   return 0;
 }
+#endif  // MDG_DIAGNOSTICS

@@ -159,3 +159,14 @@ static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
 
 // row stride of the padded attention operands (planes, bias_kv rows) for head dim D
 __host__ __device__ constexpr int dp_of(int D) { return MDG_HEAD_STRIDE(D); }
+
+// One dword from / to an address that is only 4-B aligned (rows of 3-, 7-, 9-, 14- or 21-float
+// records).  A relaxed workgroup-scope atomic is a plain global_load_dword / global_store_dword,
+// but the load-store vectoriser never merges it, so no dwordx2/x3/x4 access is formed at an
+// alignment below its size ("Concurrent-lane divergence").
+__device__ __forceinline__ float ld1(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void st1(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}

@@ -61,7 +61,7 @@ __global__ void ipa_init_kernel(int R, int B, int L, int C, int mstride, const i
     const float* q = rel7 + ((size_t)b * L + l) * 7;
     float acc = 0.f;
 #pragma unroll
-    for (int k = 0; k < 7; ++k) acc = fmaf(w[c * 7 + k], q[k], acc);
+    for (int k = 0; k < 7; ++k) acc = fmaf(ld1(w + c * 7 + k), ld1(q + k), acc);
     v = acc + bias[c];
   }
   if (aa_emb) v += aa_emb[aatype[(size_t)b * L + l] * C + c];
@@ -114,8 +114,8 @@ __global__ __launch_bounds__(64) void ipa_attn_kernel(int R, int B, int L, int H
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
 #pragma unroll
-      for (int c = 0; c < 3; ++c) Ri[a][c] = rot_b[(size_t)ii * 9 + a * 3 + c];
-      ti[a] = tr_b[(size_t)ii * 3 + a];
+      for (int c = 0; c < 3; ++c) Ri[a][c] = ld1(rot_b + (size_t)ii * 9 + a * 3 + c);
+      ti[a] = ld1(tr_b + (size_t)ii * 3 + a);
     }
 #pragma unroll
     for (int p = 0; p < PQ; ++p) {
@@ -143,8 +143,8 @@ __global__ __launch_bounds__(64) void ipa_attn_kernel(int R, int B, int L, int H
 #pragma unroll
         for (int a = 0; a < 3; ++a) {
 #pragma unroll
-          for (int c = 0; c < 3; ++c) Rj[a][c] = rot_b[(size_t)j * 9 + a * 3 + c];
-          tj[a] = tr_b[(size_t)j * 3 + a];
+          for (int c = 0; c < 3; ++c) Rj[a][c] = ld1(rot_b + (size_t)j * 9 + a * 3 + c);
+          tj[a] = ld1(tr_b + (size_t)j * 3 + a);
         }
 #pragma unroll
         for (int p = 0; p < PQ + PV; ++p) {

@@ -28,8 +28,8 @@ __device__ __forceinline__ Rig load_rig(const float* __restrict__ rots, const fl
 #pragma unroll
   for (int a = 0; a < 3; ++a) {
 #pragma unroll
-    for (int b = 0; b < 3; ++b) g.r[a][b] = rots[i * 9 + a * 3 + b];
-    g.t[a] = trans[i * 3 + a];
+    for (int b = 0; b < 3; ++b) g.r[a][b] = ld1(rots + i * 9 + a * 3 + b);
+    g.t[a] = ld1(trans + i * 3 + a);
   }
   return g;
 }
@@ -104,8 +104,8 @@ __global__ void prep_latents_kernel(int B, int T, int L, int lat, int tps, int n
   float* lrow = latents + n * lat;
   float* xrow = x_cond ? x_cond + n * lat : nullptr;
   auto put = [&](int i, float v) {
-    lrow[i] = v;
-    if (xrow) xrow[i] = cond ? v : 0.f;
+    st1(lrow + i, v);
+    if (xrow) st1(xrow + i, cond ? v : 0.f);
   };
   const Rig x = load_rig(rots, trans, n);
   const int nref = tps ? 2 : 1;
@@ -126,7 +126,7 @@ __global__ void prep_latents_kernel(int B, int T, int L, int lat, int tps, int n
     for (int i = 0; i < 3; ++i) put(7 * k + 4 + i, o.t[i]);
   }
 #pragma unroll
-  for (int i = 0; i < 14; ++i) put(7 * nref + i, torsions ? torsions[n * 14 + i] : 0.f);
+  for (int i = 0; i < 14; ++i) put(7 * nref + i, torsions ? ld1(torsions + n * 14 + i) : 0.f);
   if (cond_mask) cond_mask[n] = cond ? 1 : 0;
 }
 
@@ -165,7 +165,8 @@ __global__ void latents_to_atom14_kernel(int B, int T, int L, int lat, int tors_
   const int b = (int)(n / ((size_t)T * L));
   const float* x = samples + n * lat;
   // Rigid.from_tensor_7(offsets, normalize_quats=True) (rigid_utils.py:155-189 quat -> rot)
-  float qa = x[0], qb = x[1], qc = x[2], qd = x[3];
+  float qa = ld1(x), qb = ld1(x + 1), qc = ld1(x + 2), qd = ld1(x + 3);
+  const float x4 = ld1(x + 4), x5 = ld1(x + 5), x6 = ld1(x + 6);
   const float qn = sqrtf(qa * qa + qb * qb + qc * qc + qd * qd);
   qa /= qn; qb /= qn; qc /= qn; qd /= qn;
   const float rr[3][3] = {
@@ -178,19 +179,19 @@ __global__ void latents_to_atom14_kernel(int B, int T, int L, int lat, int tors_
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
 #pragma unroll
-    for (int j = 0; j < 3; ++j) r0[i][j] = ref_rots[bl * 9 + i * 3 + j];
-    t0[i] = ref_trans[bl * 3 + i];
+    for (int j = 0; j < 3; ++j) r0[i][j] = ld1(ref_rots + bl * 9 + i * 3 + j);
+    t0[i] = ld1(ref_trans + bl * 3 + i);
   }
   float R[3][3], Tt[3];
   mat3_mul(r0, rr, R);
 #pragma unroll
-  for (int i = 0; i < 3; ++i) Tt[i] = r0[i][0] * x[4] + r0[i][1] * x[5] + r0[i][2] * x[6] + t0[i];
+  for (int i = 0; i < 3; ++i) Tt[i] = r0[i][0] * x4 + r0[i][1] * x5 + r0[i][2] * x6 + t0[i];
   if (out_rots) {
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
 #pragma unroll
-      for (int j = 0; j < 3; ++j) out_rots[n * 9 + i * 3 + j] = R[i][j];
-      out_trans[n * 3 + i] = Tt[i];
+      for (int j = 0; j < 3; ++j) st1(out_rots + n * 9 + i * 3 + j, R[i][j]);
+      st1(out_trans + n * 3 + i, Tt[i]);
     }
   }
   int aa = (int)aatype[n];
@@ -201,8 +202,8 @@ __global__ void latents_to_atom14_kernel(int B, int T, int L, int lat, int tors_
   for (int g = 0; g < 8; ++g) {
     float sa = 0.f, ca = 1.f;  // backbone group: identity rotation (bb_rot = (0, 1))
     if (g > 0) {
-      sa = x[tors_off + 2 * (g - 1)];
-      ca = x[tors_off + 2 * (g - 1) + 1];
+      sa = ld1(x + tors_off + 2 * (g - 1));
+      ca = ld1(x + tors_off + 2 * (g - 1) + 1);
       if (renorm) {
         const float nn = sqrtf(sa * sa + ca * ca);
         sa /= nn;
@@ -239,6 +240,7 @@ __global__ void latents_to_atom14_kernel(int B, int T, int L, int lat, int tors_
     const int g = group_idx[aa * 14 + a];
     const float m = atom_mask[aa * 14 + a];
     const float* p = lit + ((size_t)aa * 14 + a) * 3;
+    const float p0 = ld1(p), p1 = ld1(p + 1), p2 = ld1(p + 2);
     float lr[3][3], lt[3];
     // select the group frame without dynamic register indexing
 #pragma unroll
@@ -260,9 +262,9 @@ __global__ void latents_to_atom14_kernel(int B, int T, int L, int lat, int tors_
     // local = group frame . lit ; global = frame . local
     float loc[3];
 #pragma unroll
-    for (int i = 0; i < 3; ++i) loc[i] = lr[i][0] * p[0] + lr[i][1] * p[1] + lr[i][2] * p[2] + lt[i];
+    for (int i = 0; i < 3; ++i) loc[i] = lr[i][0] * p0 + lr[i][1] * p1 + lr[i][2] * p2 + lt[i];
 #pragma unroll
-    for (int i = 0; i < 3; ++i) out[a * 3 + i] = (R[i][0] * loc[0] + R[i][1] * loc[1] + R[i][2] * loc[2] + Tt[i]) * m;
+    for (int i = 0; i < 3; ++i) st1(out + a * 3 + i, (R[i][0] * loc[0] + R[i][1] * loc[1] + R[i][2] * loc[2] + Tt[i]) * m);
   }
 }
 
@@ -297,9 +299,9 @@ __global__ void tps_rel7_kernel(int BL, const float* __restrict__ rots, const fl
     const float sg = q[0] < 0.f ? -1.f : 1.f;
     float* row = out + ((size_t)k * BL + n) * 7;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) row[i] = q[i] * sg;
+    for (int i = 0; i < 4; ++i) st1(row + i, q[i] * sg);
 #pragma unroll
-    for (int i = 0; i < 3; ++i) row[4 + i] = o.t[i];
+    for (int i = 0; i < 3; ++i) st1(row + 4 + i, o.t[i]);
   }
 }
 

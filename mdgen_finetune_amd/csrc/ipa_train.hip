@@ -126,8 +126,11 @@ __global__ __launch_bounds__(64) void ipa_core_fwd_kernel(int L, int H, const fl
     orow[h * CH + d] = acc;
   }
   // points: global sum - t_i, then R_i^T, norm
-  const float* R = rots + tok * 9;
-  const float* t = trans + tok * 3;
+  float R[9], t[3];
+#pragma unroll
+  for (int e = 0; e < 9; ++e) R[e] = ld1(rots + tok * 9 + e);
+#pragma unroll
+  for (int e = 0; e < 3; ++e) t[e] = ld1(trans + tok * 3 + e);
   for (int p = 0; p < PV; ++p) {
     float g[3];
 #pragma unroll
@@ -191,8 +194,11 @@ __global__ __launch_bounds__(64) void ipa_core_bwd_kernel(int L, int H, const fl
     ipa_row_softmax<CH, PQ>(qr, qpr, S.s.M[i], L, S.s.K, S.s.KP, S.s.M, wc, hwh, Prow);
     const int W = H * CH + 4 * H * PV;
     const float* grow = dout + tok * W;
-    const float* R = rots + tok * 9;
-    const float* t = trans + tok * 3;
+    float R[9], t[3];
+#pragma unroll
+    for (int e = 0; e < 9; ++e) R[e] = ld1(rots + tok * 9 + e);
+#pragma unroll
+    for (int e = 0; e < 3; ++e) t[e] = ld1(trans + tok * 3 + e);
     // d o_i -> LDS; d(point outputs) -> d og_i = R_i (d ol + dn ol / n)
     for (int d = 0; d < CH; ++d) S.DO[i * CH + d] = grow[h * CH + d];
     for (int p = 0; p < PV; ++p) {

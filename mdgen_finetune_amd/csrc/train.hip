@@ -339,6 +339,7 @@ __device__ __forceinline__ void rope_inv(float& a, float& b, const float* rope, 
 // [seq][head][T][32] (pad columns 0).  n = (b*T + t)*L + l, seq = b*L + l.
 template <typename CT>
 __global__ __launch_bounds__(256) void attn_bwd_prep_kernel(int B, int T, int L, int H, int D, const CT* __restrict__ o,
+                                                            const CT* __restrict__ o_lo,
                                                             const CT* __restrict__ dout, CT* __restrict__ dop,
                                                             float* __restrict__ delta) {
   const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;
@@ -363,6 +364,11 @@ __global__ __launch_bounds__(256) void attn_bwd_prep_kernel(int B, int T, int L,
         for (int j = 0; j < 8; j += 4)
           dl += (float)dv[j] * (float)ov[j] + (float)dv[j + 1] * (float)ov[j + 1] + (float)dv[j + 2] * (float)ov[j + 2] +
                 (float)dv[j + 3] * (float)ov[j + 3];
+        if (o_lo) {
+          const typename V8<CT>::T lv = ld8<CT>(o_lo + n * C + head * D + d0);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) dl += (float)dv[j] * (float)lv[j];
+        }
       }
       st8<CT>(prow + d0, dv);
     }
@@ -373,6 +379,10 @@ __global__ __launch_bounds__(256) void attn_bwd_prep_kernel(int B, int T, int L,
         const float4 ov = ld4f<CT>(orow + d0);
         dv = ld4f<CT>(drow + d0);
         dl += dv.x * ov.x + dv.y * ov.y + dv.z * ov.z + dv.w * ov.w;
+        if (o_lo) {
+          const float4 lv = ld4f<CT>(o_lo + n * C + head * D + d0);
+          dl += dv.x * lv.x + dv.y * lv.y + dv.z * lv.z + dv.w * lv.w;
+        }
       }
       st4<CT>(prow + d0, dv.x, dv.y, dv.z, dv.w);
     }
@@ -869,7 +879,8 @@ int attn_bwd_parts(int dtype, int B, int T, int L) {  // bias-gradient partial s
 }
 
 hipError_t attn_temporal_bwd_launch(int dtype, int B, int T, int L, int H, int D, const void* qkv_t,
-                                    const float* kbias, const float* kvb, const void* o, const void* dout,
+                                    const float* kbias, const float* kvb, const void* o, const void* o_lo,
+                                    const void* dout,
                                     const float* lse, const float* rope, int rope_rows, void* dop, float* delta,
                                     void* dqkv, int ldq, float* bpart, float qscale, float kscale, int generic,
                                     hipStream_t s) {
@@ -878,10 +889,10 @@ hipError_t attn_temporal_bwd_launch(int dtype, int B, int T, int L, int H, int D
   dim3 pgrid((unsigned)((nth + 255) / 256));
   if (dtype == MDG_BF16) {
     hipLaunchKernelGGL(attn_bwd_prep_kernel<bf16_t>, pgrid, dim3(256), 0, s, B, T, L, H, D, (const bf16_t*)o,
-                       (const bf16_t*)dout, (bf16_t*)dop, delta);
+                       (const bf16_t*)o_lo, (const bf16_t*)dout, (bf16_t*)dop, delta);
   } else {
     hipLaunchKernelGGL(attn_bwd_prep_kernel<float>, pgrid, dim3(256), 0, s, B, T, L, H, D, (const float*)o,
-                       (const float*)dout, (float*)dop, delta);
+                       (const float*)o_lo, (const float*)dout, (float*)dop, delta);
   }
   if (hipError_t e = hipGetLastError()) return e;
   if (dtype == MDG_BF16 && !generic) {

@@ -168,6 +168,9 @@ class LatentMDGenModel(nn.Module):
         self.backend = "hip"
         self.train_backend = "hip"
         self._engine = None
+        # [2, B, L, 7] device tensor of relative_tensor7(start, end) / (end, start) that a
+        # captured training step fills on the host before each replay (train.GraphedStep)
+        self._rel7_feed = None
 
     # ------------------------------------------------------------------ init (latent_model.py:134-177)
     def initialize_weights(self):
@@ -232,8 +235,12 @@ class LatentMDGenModel(nn.Module):
                 x = layer(x, c, mask_b, rots, trans, mods=None if ada is None else ada[k])
             return x
         erots, etrans = frames_to_tensors(end_frames, mask_b.device)
-        x_f = self.latent_to_emb_f(relative_tensor7(rots, trans, erots, etrans))
-        x_r = self.latent_to_emb_r(relative_tensor7(erots, etrans, rots, trans))
+        if self._rel7_feed is not None:  # staged by the graphed training step (host eigh outside the graph)
+            rel_f, rel_r = self._rel7_feed[0], self._rel7_feed[1]
+        else:
+            rel_f, rel_r = relative_tensor7(rots, trans, erots, etrans), relative_tensor7(erots, etrans, rots, trans)
+        x_f = self.latent_to_emb_f(rel_f)
+        x_r = self.latent_to_emb_r(rel_r)
         if use_aa:
             x_f = x_f + self.aatype_to_emb(aatype)
             x_r = x_r + self.aatype_to_emb(aatype)

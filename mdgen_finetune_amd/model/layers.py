@@ -35,7 +35,9 @@ class _TokenLinear(torch.autograd.Function):
         dx = (g2 @ w.to(g2.dtype)).reshape(x.shape) if ctx.needs_input_grad[0] else None
         n, S = g2.shape[0], 16
         if n % S == 0 and n >= 64 * S:
-            dw = torch.bmm(g2.reshape(S, n // S, -1).transpose(1, 2), x2.to(g2.dtype).reshape(S, n // S, -1)).sum(0)
+            # fp32 partials (under bf16-mixed autocast g is bf16: bf16 partials would round each
+            # chunk's sum before the sum over chunks)
+            dw = torch.bmm(g2.float().reshape(S, n // S, -1).transpose(1, 2), x2.float().reshape(S, n // S, -1)).sum(0)
         else:
             dw = g2.t() @ x2.to(g2.dtype)
         db = g2.sum(0) if ctx.has_bias else None

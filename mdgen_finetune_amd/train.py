@@ -294,7 +294,36 @@ class GraphedStep:
         self.params = [p for p in tr.wrapper.model.parameters() if p.requires_grad]
         self.split = tr.world > 1
         model = tr.wrapper.model
+        # TPS: the relative frames come from a host eigh (relative_tensor7), which a capture
+        # cannot contain; they are computed here per step and read from a static buffer
+        self.rel7 = None
+        if getattr(model, "tps", False):
+            B, L = self.static["trans"].shape[0], self.static["trans"].shape[2]
+            self.rel7 = torch.empty(2, B, L, 7, device=dev)
+            self._stage_rel7(self.static)
+            model._rel7_feed = self.rel7
+        try:
+            self._build(tr, model, dev, warmup)
+        finally:
+            model._rel7_feed = None
+
+    def _stage_rel7(self, batch):
+        from .model.latent_model import relative_tensor7
+
+        rots, trans = batch["rots"].float(), batch["trans"].float()
+        r0, t0, r1, t1 = rots[:, 0], trans[:, 0], rots[:, -1], trans[:, -1]
+        self.rel7.copy_(torch.stack([relative_tensor7(r0, t0, r1, t1), relative_tensor7(r1, t1, r0, t0)]),
+                        non_blocking=False)
+
+    def _build(self, tr, model, dev, warmup):
+        # warm-up trains nothing: snapshot everything it updates and put it back afterwards.
+        # Optimizer state that exists before warm-up (a --ckpt resume) is restored as loaded;
+        # state warm-up itself creates (a fresh run) is zeroed, i.e. "no step taken yet".
         snap = [p.detach().clone() for p in model.parameters()]
+        opt_snap = {id(p): {k: (v.detach().clone() if torch.is_tensor(v) else v) for k, v in st.items()}
+                    for p, st in tr.optimizer.state.items()}
+        ema = tr.wrapper.ema
+        ema_snap = {k: v.detach().clone() for k, v in ema.params.items()} if ema is not None else None
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
@@ -302,16 +331,21 @@ class GraphedStep:
                 tr._eager_step([self.static], log=False, update=False)
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
-        with torch.no_grad():  # warm-up trains nothing: restore weights, optimizer state, EMA
+        with torch.no_grad():
             for p, v in zip(model.parameters(), snap):
                 p.copy_(v)
-            for st in tr.optimizer.state.values():
-                for v in st.values():
-                    if torch.is_tensor(v):
+            for p, st in tr.optimizer.state.items():
+                old = opt_snap.get(id(p))
+                for k, v in st.items():
+                    if not torch.is_tensor(v):
+                        continue
+                    if old is not None and torch.is_tensor(old.get(k)):
+                        v.copy_(old[k])  # in place: the capture below reads these very tensors
+                    else:
                         v.zero_()
-            if tr.wrapper.ema is not None:
-                for k, v in model.state_dict().items():
-                    tr.wrapper.ema.params[k].copy_(v)
+            if ema is not None:
+                for k, v in ema_snap.items():
+                    ema.params[k].copy_(v)
         tr.optimizer.zero_grad(set_to_none=True)
         n = sum(p.numel() for p in self.params)
         self.flat = torch.empty(n, device=dev) if self.split else None
@@ -354,6 +388,8 @@ class GraphedStep:
         for k, v in batch.items():
             if torch.is_tensor(v):
                 self.static[k].copy_(v, non_blocking=True)
+        if self.rel7 is not None:
+            self._stage_rel7(batch)
         self.g1.replay()
         if self.split:
             self.tr.allreduce_grads(self.flat)

@@ -37,12 +37,18 @@ from __future__ import annotations
 import ctypes
 import math
 import os
+import weakref
 
 import torch
 
 from . import _lib
 
 _LN2 = math.log(2.0)
+_PLANE_CACHE_MAX = 64  # plane cache entries (layer x tag) before stale ones are dropped
+
+
+class _PlaneLease:
+    """Held by a training call's autograd context while its planes are in use."""
 
 
 def pad_tokens(n):
@@ -126,16 +132,31 @@ class LayerHelper:
             self._tables[key] = t
         return t
 
-    def planes(self, key, shape, device):
-        """(buffer, fresh): the layer's persistent padded q|k|v planes for this shape (fresh = just
-        allocated: its pad columns still need mdg_layer_fwd_train's init_planes pass)."""
+    def planes(self, key, shape, device, owner):
+        """(buffer, fresh): persistent padded q|k|v planes of one layer (key = (tag, layer id,
+        B, T, L)); fresh = just allocated, so its pad columns still need mdg_layer_fwd_train's
+        init_planes pass.  The planes are also saved activations of the call's backward, so a
+        buffer is lent to one forward at a time: ``owner`` (an object the autograd context
+        holds until its backward has run) marks the slot in use, and a second forward of the
+        same layer and shape before that backward (TPS runs every IPA layer twice per step,
+        latent_model.py:240-243) gets a slot of its own.  Only the latest shape of each layer
+        is kept (a new shape drops the old slots; buffers still lent stay alive through their
+        contexts)."""
         cache = self.__dict__.setdefault("_planes", {})
-        key = key + (self.dtype_name, str(device))
-        buf = cache.get(key)
-        if buf is None:
-            buf = cache[key] = torch.empty(*shape, device=device, dtype=self.ct)
-            return buf, True
-        return buf, False
+        tag, shape_key = key[:2] + (self.dtype_name, str(device)), key[2:]
+        ent = cache.get(tag)
+        if ent is None or ent[0] != shape_key:
+            ent = cache[tag] = (shape_key, [])
+            if len(cache) > _PLANE_CACHE_MAX:  # stale layer ids (re-allocated parameters)
+                for k in [k for k, (_, slots) in cache.items() if k != tag and all(r() is None for _, r in slots)]:
+                    del cache[k]
+        for slot in ent[1]:
+            if slot[1]() is None:
+                slot[1] = weakref.ref(owner)
+                return slot[0], False
+        buf = torch.empty(*shape, device=device, dtype=self.ct)
+        ent[1].append([buf, weakref.ref(owner)])
+        return buf, True
 
     def dims(self, B, T, L):
         return _lib.MdgDims(B=B, T=T, L=L, C=self.C, H=self.H, D=self.D, F=self.F, latent=self.model.latent_dim,
@@ -232,14 +253,18 @@ class _HipLayerFn(torch.autograd.Function):
         # the padded attention planes persist per layer and shape: their pad columns (0, and 1.0 in
         # k / v column D) are written once (init_planes) instead of a memset + set_vpad pass per
         # step; the q|k|v GEMM rewrites every other column each forward
-        planes_t, fresh_t = hl.planes(("t", params[0].data_ptr(), B, T, L), (3, B * L, H, T, _lib.MDG_DP), dev)
-        planes_s, fresh_s = (hl.planes(("s", params[0].data_ptr(), B, T, L), (3, B * T, H, L, _lib.MDG_DP), dev)
-                             if long_l else (e(N, 3 * C), False))
+        lease = _PlaneLease()
+        planes_t, fresh_t = hl.planes(("t", params[0].data_ptr(), B, T, L), (3, B * L, H, T, _lib.MDG_DP), dev, lease)
+        planes_s, fresh_s = (hl.planes(("s", params[0].data_ptr(), B, T, L), (3, B * T, H, L, _lib.MDG_DP), dev,
+                                       lease) if long_l else (e(N, 3 * C), False))
         sv = {"xn": [r(C) for _ in range(3)], "stats": [e(N, 2, dt=torch.float32) for _ in range(3)],
               "qkv_s": planes_s,
               "lse_s": e(B * T, H, L, dt=torch.float32) if long_l else None,
               "qkv_t": planes_t, "lse_t": e(B * L, H, T, dt=torch.float32),
               "o": [r(C), r(C)], "y": [e(N, C) for _ in range(3)],
+              # bf16: O - bf16(O) of the attentions on the temporal kernel (the backward's delta)
+              "o_lo": [e(N, C) if (ct == torch.bfloat16 and long_l) else None,
+                       e(N, C) if ct == torch.bfloat16 else None],
               "h1": e(N, C, dt=torch.float32), "h2": e(N, C, dt=torch.float32), "u": e(N, F), "act": r(F)}
         cs = _lib.MdgLayerSaved()
         for i in range(3):
@@ -247,6 +272,7 @@ class _HipLayerFn(torch.autograd.Function):
         cs.qkv_s, cs.lse_s = sv["qkv_s"].data_ptr(), _lib.ptr(sv["lse_s"])
         cs.qkv_t, cs.lse_t = sv["qkv_t"].data_ptr(), sv["lse_t"].data_ptr()
         cs.o[0], cs.o[1] = sv["o"][0].data_ptr(), sv["o"][1].data_ptr()
+        cs.o_lo[0], cs.o_lo[1] = _lib.ptr(sv["o_lo"][0]), _lib.ptr(sv["o_lo"][1])
         cs.h1, cs.h2, cs.u, cs.act = sv["h1"].data_ptr(), sv["h2"].data_ptr(), sv["u"].data_ptr(), sv["act"].data_ptr()
         cs.init_planes = int(fresh_t or fresh_s)
         h_out = torch.empty_like(h)
@@ -254,7 +280,7 @@ class _HipLayerFn(torch.autograd.Function):
                                            mods.data_ptr(), mask.data_ptr(), kb_t.data_ptr(), kb_s.data_ptr(),
                                            h.data_ptr(), h_out.data_ptr(), ctypes.byref(cs), s),
                    "mdg_layer_fwd_train")
-        ctx.hl, ctx.sv, ctx.P = hl, sv, P
+        ctx.hl, ctx.sv, ctx.P, ctx.lease = hl, sv, P, lease
         ctx.shape = (B, T, L)
         ctx.kb = (kb_t, kb_s)
         ctx.mask = mask
@@ -315,7 +341,7 @@ class _HipLayerFn(torch.autograd.Function):
         dy_t = r(C)
         part_t = lngate(dxn3, sv["h2"], sv["stats"][2], 6 * C, 7 * C, dh3, dh2, sv["y"][1], 5 * C, dy_t)
 
-        def attention(i, dy, o, xn, qkv, lse):
+        def attention(i, dy, o, o_lo, xn, qkv, lse):
             """out_proj + attention backward of attention i (0 spatial, 1 temporal); returns dxn."""
             grads[f"wo{i}"], _ = wg(dy, o)
             do = dx_gemm(dy, P[f"wo_t{i}"], C, C)
@@ -329,7 +355,8 @@ class _HipLayerFn(torch.autograd.Function):
                 scratch = torch.empty(lib.mdg_attn_temporal_bwd_scratch(dt, Bq, Tq, Lq, H), device=dev,
                                       dtype=torch.uint8)
                 _lib.check(lib.mdg_attn_temporal_bwd(dt, Bq, Tq, Lq, H, D, qkv.data_ptr(), kb.data_ptr(),
-                                                     P[f"kvb{i}"].data_ptr(), o.data_ptr(), do.data_ptr(),
+                                                     P[f"kvb{i}"].data_ptr(), o.data_ptr(), _lib.ptr(o_lo),
+                                                     do.data_ptr(),
                                                      lse.data_ptr(), _lib.ptr(rope), rows, scratch.data_ptr(),
                                                      dqkv.data_ptr(), 3 * C, bpart.data_ptr(), qscale, _LN2, 0, s),
                            "mdg_attn_temporal_bwd")
@@ -346,11 +373,11 @@ class _HipLayerFn(torch.autograd.Function):
             grads[f"wqkv{i}"], grads[f"bqkv{i}"] = wg(dqkv, xn, True)
             return dx_gemm(dqkv, P[f"wqkv_t{i}"], 3 * C, C)
 
-        dxn2 = attention(1, dy_t, sv["o"][1], sv["xn"][1], sv["qkv_t"], sv["lse_t"])
+        dxn2 = attention(1, dy_t, sv["o"][1], sv["o_lo"][1], sv["xn"][1], sv["qkv_t"], sv["lse_t"])
         dh1 = e(N, C, dtp=torch.float32)
         dy_s = r(C)
         part_s = lngate(dxn2, sv["h1"], sv["stats"][1], 3 * C, 4 * C, dh2, dh1, sv["y"][0], 2 * C, dy_s)
-        dxn1 = attention(0, dy_s, sv["o"][0], sv["xn"][0], sv["qkv_s"], sv["lse_s"])
+        dxn1 = attention(0, dy_s, sv["o"][0], sv["o_lo"][0], sv["xn"][0], sv["qkv_s"], sv["lse_s"])
         dh0 = e(N, C, dtp=torch.float32)
         part_0 = lngate(dxn1, h.reshape(N, C), sv["stats"][0], 0, C, dh1, dh0, None, 0, None)
 
@@ -379,5 +406,5 @@ class _HipLayerFn(torch.autograd.Function):
             out += [g["gq", i], g["gbq", i], g["gk", i], g["gbk", i], g["gv", i], g["gbv", i], grads[f"wo{i}"],
                     grads[f"bo{i}"], g["gbias_k", i], g["gbias_v", i]]
         out += [grads["w1"], grads["b1"], grads["w2"], grads["b2"]]
-        del ctx.sv, ctx.P
+        del ctx.sv, ctx.P, ctx.lease  # the planes go back to the layer's pool
         return (dh0.reshape(B, T, L, C), dmods, None, None, None, *out)

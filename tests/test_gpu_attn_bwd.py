@@ -1,0 +1,164 @@
+"""mdg_attn_temporal_bwd (csrc/train.hip) against fp32 torch autograd of the same attention, at
+the sizes config 3 trains: T = 129, 257 and 1000 frames (2, 3 and 8 chunks of 128 keys /
+queries, with tails), head_dim 24 (C = 384, 16 heads), the bias_k / bias_v virtual key, RoPE
+(fair-esm, bias key at position T) and key padding.  Reference op: the temporal
+MultiheadAttention under loss.backward() (reference src/mdgen/model/mha.py:255-397, the
+backward of 359-389; latent_model.py:482-486).
+
+The operands are built in the kernel's own basis (q / k columns pair-interleaved per head, so
+RoPE rotates neighbouring columns): q' = rope(q_lin * D^-1/2), k' = rope(k_lin), planes
+[BL][H][T][32] with q' * log2(e) in the q plane and 1.0 in pad column D of the k / v planes,
+lse the per-row log2-sum-exp2.  The reference differentiates
+    o = softmax([q'.bk, q'.k' + kbias]) [bv; v]
+with respect to q_lin, k_lin, v, bk, bv (fp64 on the device).  Bounds: f32 (scalar kernels)
+||d|| / ||ref|| <= 1e-5; bf16 (MFMA kernels: P and dS rounded to bf16 as MFMA operands)
+<= BF16_TOL, ~2x the worst observed (logged to MDG_PARITY_LOG).  n_pad = -1: one sequence has
+every key padded (a padded residue's temporal attention: P = [1, 0, ...], exact dS = 0), which
+the bf16 path gets right only through o_lo (delta = dO . (o + o_lo))."""
+import json
+import math
+import os
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+BF16_TOL = 2e-2
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    from mdgen_finetune_amd import _lib
+
+    _lib.load()
+
+
+def _rope_tab(rows, D):
+    inv = 1.0 / (10000 ** (torch.arange(0, D, 2).float() / D))
+    f = torch.einsum("i,j->ij", torch.arange(rows).float(), inv)
+    return f.cos(), f.sin()
+
+
+def _rope(x, cos, sin):
+    """x [..., T, D] in the pair-interleaved basis; rotation of pair i at row position t."""
+    a, b = x[..., 0::2], x[..., 1::2]
+    out = torch.empty_like(x)
+    out[..., 0::2] = a * cos - b * sin
+    out[..., 1::2] = b * cos + a * sin
+    return out
+
+
+def _case(T, BL, H, D, n_pad_keys, seed, dev="cuda"):
+    g = torch.Generator().manual_seed(seed)
+    r = lambda *s: torch.randn(*s, generator=g, dtype=torch.float64)  # noqa: E731
+    q_lin, k_lin, v = r(BL, H, T, D), r(BL, H, T, D), r(BL, H, T, D)
+    bk_lin, bv = r(H, D), r(H, D)
+    dout = r(BL, H, T, D)
+    kbias = torch.zeros(BL, T, dtype=torch.float64)
+    if n_pad_keys < 0:  # sequence 1 entirely padded (a padded residue): only the bias key is valid
+        kbias[0, T - 3:] = -math.inf
+        kbias[1, :] = -math.inf
+    elif n_pad_keys:  # pad the tail frames of sequence 0 and a scattered set of sequence 1
+        kbias[0, T - n_pad_keys:] = -math.inf
+        if BL > 1:
+            kbias[1, torch.randperm(T, generator=g)[:n_pad_keys]] = -math.inf
+    return {k: v.to(dev) for k, v in dict(q_lin=q_lin, k_lin=k_lin, v=v, bk_lin=bk_lin, bv=bv, dout=dout,
+                                         kbias=kbias).items()}
+
+
+def _forward(c, D, T, cos, sin, qscale):
+    """o (natural units) from differentiable inputs; bias key rotated at position T."""
+    qn = _rope(c["q_lin"] * qscale, cos[:T], sin[:T])
+    kr = _rope(c["k_lin"], cos[:T], sin[:T])
+    bk = _rope(c["bk_lin"][:, None, :], cos[T:T + 1], sin[T:T + 1])[:, 0]  # [H, D]
+    s = torch.einsum("shtd,shud->shtu", qn, kr) + c["kbias"][:, None, None, :]
+    sb = torch.einsum("shtd,hd->sht", qn, bk)[..., None]
+    p = torch.softmax(torch.cat([sb, s], -1), -1)
+    o = p[..., :1] * c["bv"][None, :, None, :] + torch.einsum("shtu,shud->shtd", p[..., 1:], c["v"])
+    return o, qn, kr, bk, torch.cat([sb, s], -1)
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "f32"])
+@pytest.mark.parametrize("T,n_pad", [(129, 0), (257, 5), (1000, 17), (300, -1)])
+def test_temporal_attention_backward_multi_chunk(dtype, T, n_pad):
+    from mdgen_finetune_amd import _lib
+
+    lib = _lib.load()
+    dev = "cuda"
+    B, L, H, D = 1, 2, 16, 24
+    BL, C, DP = B * L, H * D, _lib.MDG_DP
+    ct = torch.bfloat16 if dtype == "bf16" else torch.float32
+    mdt = _lib.MDG_BF16 if dtype == "bf16" else _lib.MDG_F32
+    qscale, log2e = D ** -0.5, 1.0 / math.log(2.0)
+    c = _case(T, BL, H, D, n_pad, seed=T + n_pad)
+    cos, sin = (x.double().to(dev) for x in _rope_tab(T + 1, D))
+    for k in ("q_lin", "k_lin", "v", "bk_lin", "bv"):
+        c[k].requires_grad_(True)
+    o, qn, kr, bk, s_all = _forward(c, D, T, cos, sin, qscale)
+    (o * c["dout"]).sum().backward()
+
+    # kernel operands (rounded to CT where the kernel reads CT)
+    with torch.no_grad():
+        planes = torch.zeros(3, BL, H, T, DP, device=dev, dtype=ct)
+        planes[0, ..., :D] = (qn * log2e).to(ct)
+        planes[1, ..., :D] = kr.to(ct)
+        planes[2, ..., :D] = c["v"].to(ct)
+        planes[1, ..., D] = 1.0
+        planes[2, ..., D] = 1.0
+        qp, kp, vp = (planes[i, ..., :D].double() for i in range(3))
+        # lse / o from the operands the kernel sees (log2 units)
+        s2 = torch.einsum("shtd,shud->shtu", qp, kp) + c["kbias"][:, None, None, :]
+        sb2 = torch.einsum("shtd,hd->sht", qp, bk.detach())[..., None]
+        s2 = torch.cat([sb2, s2], -1)
+        lse = torch.logsumexp(s2 * math.log(2.0), -1) * log2e
+        p2 = torch.exp2(s2 - lse[..., None])
+        o_k = p2[..., :1] * c["bv"].detach()[None, :, None, :] + torch.einsum("shtu,shud->shtd", p2[..., 1:], vp)
+
+        def tok_major(x):  # [BL][H][T][D] -> [N][C], n = (b*T + t)*L + l, seq = b*L + l
+            return x.reshape(B, L, H, T, D).permute(0, 3, 1, 2, 4).reshape(B * T * L, C)
+
+        o_t = tok_major(o_k).to(ct).contiguous()
+        lo_t = (tok_major(o_k) - o_t.double()).to(ct).contiguous() if dtype == "bf16" else None
+        do_t = tok_major(c["dout"]).to(ct).contiguous()
+        kvb = torch.zeros(H, 2, DP, device=dev)
+        kvb[:, 0, :D] = bk.detach().float()
+        kvb[:, 1, :D] = c["bv"].detach().float()
+        kb = c["kbias"].float().contiguous()
+        lse_f = lse.float().contiguous()
+        rope = torch.cat([cos.float().reshape(-1), sin.float().reshape(-1)]).contiguous()
+        parts = lib.mdg_attn_temporal_bwd_parts(mdt, B, T, L)
+        bpart = torch.zeros(H, parts, 2, DP, device=dev)
+        scratch = torch.empty(lib.mdg_attn_temporal_bwd_scratch(mdt, B, T, L, H), device=dev, dtype=torch.uint8)
+        dqkv = torch.full((B * T * L, 3 * C), float("nan"), device=dev, dtype=ct)
+        _lib.check(lib.mdg_attn_temporal_bwd(mdt, B, T, L, H, D, planes.data_ptr(), kb.data_ptr(), kvb.data_ptr(),
+                                             o_t.data_ptr(), _lib.ptr(lo_t), do_t.data_ptr(), lse_f.data_ptr(),
+                                             rope.data_ptr(), T + 1,
+                                             scratch.data_ptr(), dqkv.data_ptr(), 3 * C, bpart.data_ptr(), qscale,
+                                             math.log(2.0), 0, _lib.stream_handle()), "mdg_attn_temporal_bwd")
+        torch.cuda.synchronize()
+        got = dqkv.double()
+        gb = bpart.double().sum(1)
+    refs = {"dq": tok_major(c["q_lin"].grad), "dk": tok_major(c["k_lin"].grad), "dv": tok_major(c["v"].grad),
+            "dbk": _rope_inv_bias(c, cos, sin, T), "dbv": c["bv"].grad}
+    gots = {"dq": got[:, :C], "dk": got[:, C:2 * C], "dv": got[:, 2 * C:], "dbk": gb[:, 0, :D], "dbv": gb[:, 1, :D]}
+    # f32, fully padded sequence: the bias-key gradient's exact value there is 0, so what remains is
+    # the fp32 rounding of O summed over its queries (observed 2e-5 of the whole dbk)
+    tol = BF16_TOL if dtype == "bf16" else (5e-5 if n_pad < 0 else 1e-5)
+    errs = {k: float((gots[k] - refs[k]).norm() / refs[k].norm()) for k in refs}
+    path = os.environ.get("MDG_PARITY_LOG")
+    if path:
+        with open(path, "a") as f:
+            f.write(json.dumps({"test": "attn_temporal_bwd", "dtype": dtype, "T": T, "n_pad": n_pad, **errs}) + "\n")
+    assert torch.isfinite(got).all(), "unwritten or non-finite dq|dk|dv"
+    for k, e in errs.items():
+        assert e <= tol, (k, e, errs)
+
+
+def _rope_inv_bias(c, cos, sin, T):
+    """d loss / d (rotated bias_k) from autograd's d / d bk_lin: the kernel reports the gradient
+    w.r.t. the rotated row (mdg_train_unpack_layer undoes the rotation)."""
+    g = c["bk_lin"].grad  # = R^T dbk_rot  ->  dbk_rot = R g
+    return _rope(g[:, None, :], cos[T:T + 1], sin[T:T + 1])[:, 0]

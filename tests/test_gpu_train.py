@@ -85,7 +85,7 @@ def _model_loss(m, d, device):
 
 
 # grad tolerance per train path: ||g - g_ref|| / ||g_ref|| per parameter (and for the loss)
-TRAIN_TOL = {"torch": (1e-5, 1e-4), "hip-f32": (1e-5, 1e-4), "hip-bf16": (1e-3, 2.5e-2)}
+TRAIN_TOL = {"torch": (1e-5, 1e-4), "hip-f32": (1e-5, 1e-4), "hip-bf16": (1e-3, 2e-2)}  # bf16 worst 9.1e-3
 
 
 def _log_train(rec):
@@ -173,7 +173,7 @@ def test_hip_layer_backward_matches_eager_autograd(dtype, T, L, n_pad):
     # HIP Function (mods from the same adaLN module)
     out = hip_layer_forward(hl, layer, h, layer.adaLN_modulation(c), mask)
     gots = torch.autograd.grad(out, [h, c] + list(layer.parameters()), gout)
-    tol = 1e-4 if dtype == "f32" else 4.5e-2
+    tol = 1e-4 if dtype == "f32" else 2.6e-2
     fwd = float((out - out_ref).norm() / out_ref.norm())
     names = ["h", "c"] + [n for n, _ in layer.named_parameters()]
     worst = (fwd, "forward")
@@ -184,6 +184,54 @@ def test_hip_layer_backward_matches_eager_autograd(dtype, T, L, n_pad):
         worst = max(worst, (rel, n))
     _log_train({"test": "layer_bwd", "dtype": dtype, "T": T, "L": L, "n_pad": n_pad, "fwd_rel": fwd,
                 "worst_rel": worst[0], "worst": worst[1]})
+    assert worst[0] <= tol, worst
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("T,n_pad", [(129, 1), (257, 0), (1000, 1)])
+def test_hip_layer_backward_default_dims_multi_chunk(dtype, T, n_pad):
+    """The layer backward at config 3's dims (C = 384, 16 heads, head_dim 24) and lengths whose
+    temporal attention backward runs 2, 3 and 8 chunks of 128 keys / queries with tails
+    (T = 129, 257, 1000), one trajectory, against eager autograd of the same module.  Also
+    pads frames at the end of the trajectory for one residue (temporal key padding across the
+    last chunk) besides the padded residue.  Bounds as the layer test above."""
+    import argparse
+
+    from mdgen_finetune_amd import synthetic
+    from mdgen_finetune_amd.model.latent_model import LatentMDGenLayer
+    from mdgen_finetune_amd.train_hip import LayerHelper, hip_layer_forward
+
+    torch.manual_seed(T)
+    C, H, B, L = 384, 16, 1, 4
+    layer = LatentMDGenLayer(C, 4 * C, H, use_rotary_embeddings=True).cuda()
+    synthetic.fill_module_(layer, 5)
+    args = argparse.Namespace(embed_dim=C, mha_heads=H, no_rope=False, num_layers=1)
+    hl = LayerHelper(argparse.Namespace(args=args, latent_dim=21), dtype)
+    h = torch.randn(B, T, L, C, device="cuda", requires_grad=True)
+    c = torch.randn(B, C, device="cuda", requires_grad=True)
+    mask = torch.ones(B, T, L, device="cuda")
+    if n_pad:
+        mask[:, :, L - n_pad:] = 0
+    mask[:, T - 7:, 0] = 0  # residue 0 missing in the last 7 frames: padded keys in the tail chunk
+    gout = torch.randn(B, T, L, C, device="cuda")
+    out_ref = layer(h, c[:, None], mask)
+    refs = torch.autograd.grad(out_ref, [h, c] + list(layer.parameters()), gout)
+    out = hip_layer_forward(hl, layer, h, layer.adaLN_modulation(c), mask)
+    gots = torch.autograd.grad(out, [h, c] + list(layer.parameters()), gout)
+    tol = 1e-4 if dtype == "f32" else 2.6e-2
+    fwd = float((out - out_ref).norm() / out_ref.norm())
+    names = ["h", "c"] + [n for n, _ in layer.named_parameters()]
+    worst, errs = (fwd, "forward"), {}
+    for n, a, b in zip(names, gots, refs):
+        if b is None or float(b.norm()) == 0:
+            continue
+        assert torch.isfinite(a).all(), n
+        rel = float((a.float() - b).norm() / b.norm())
+        errs[n] = rel
+        worst = max(worst, (rel, n))
+    _log_train({"test": "layer_bwd_default_dims", "dtype": dtype, "T": T, "L": L, "n_pad": n_pad, "fwd_rel": fwd,
+                "worst_rel": worst[0], "worst": worst[1],
+                "attn_t": max(v for k, v in errs.items() if k.startswith("mha_t"))})
     assert worst[0] <= tol, worst
 
 
@@ -202,17 +250,19 @@ def _default_dims_case(B=2, T=64, L=4, seed=31):
 
 
 @pytest.mark.parametrize("dtype", ["f32", "bf16"])
-def test_default_dims_training_grads_match_oracle(dtype):
-    """The HIP training path at the dims config 3 trains (C=384, H=16, D=24, 5 layers, T=64):
+@pytest.mark.parametrize("B,T", [(2, 64), (1, 320)])
+def test_default_dims_training_grads_match_oracle(dtype, B, T):
+    """The HIP training path at the dims config 3 trains (C=384, H=16, D=24, 5 layers; T = 64,
+    and T = 320, whose temporal attention backward runs 3 chunks with a tail):
     the GVP loss and EVERY parameter gradient against the oracle under autograd (CPU fp32).
     Bounds: f32 loss rel 1e-5, grads 1e-4; bf16 loss 1e-2, grads BF16_DEFAULT_GRAD (~2x the
-    worst observed, profiles/r03_parity_train.jsonl)."""
+    worst observed, profiles/r04_parity_train.jsonl)."""
     from mdgen_finetune_amd.rigid_utils import Rigid, Rotation
     from mdgen_finetune_amd.transport import create_transport
     from mdgen_finetune_amd.transport.transport import mean_flat
     from oracle import mdgen_oracle as O
 
-    inp, cfg = _default_dims_case()
+    inp, cfg = _default_dims_case(B=B, T=T)
     f = lambda k: torch.from_numpy(np.ascontiguousarray(inp[k]))  # noqa: E731
     c = O.Cfg(crop=4)
     P = O.seeded_params(c, cfg["weights_seed"])
@@ -224,7 +274,7 @@ def test_default_dims_training_grads_match_oracle(dtype):
     loss_ref, _ = O.gvp_training_loss(P, c, f("x"), f("x0"), f("t_loss"), f("loss_mask"), **kw_cpu)
     loss_ref.mean().backward()
 
-    m, _ = build_model(cfg, "cuda", T=64)
+    m, _ = build_model(cfg, "cuda", T=T)
     m.train()
     m.hip_dtype = dtype
     g = lambda k: f(k).cuda()  # noqa: E731
@@ -247,7 +297,7 @@ def test_default_dims_training_grads_match_oracle(dtype):
         rel = float((gg.detach().float().cpu() - p.grad).norm()) / float(p.grad.norm())
         worst = max(worst, (rel, k))
         checked += 1
-    _log_train({"test": "default_dims_grads", "dtype": dtype, "loss_rel": lrel, "worst_grad_rel": worst[0],
+    _log_train({"test": "default_dims_grads", "dtype": dtype, "B": B, "T": T, "loss_rel": lrel, "worst_grad_rel": worst[0],
                 "worst_param": worst[1], "checked": checked})
     loss_tol, grad_tol = (1e-5, 1e-4) if dtype == "f32" else (1e-2, BF16_DEFAULT_GRAD)
     assert lrel <= loss_tol, lrel
@@ -255,7 +305,7 @@ def test_default_dims_training_grads_match_oracle(dtype):
     assert checked > 250
 
 
-BF16_DEFAULT_GRAD = 3.5e-2  # 2x the worst observed (1.63e-2, layers.4.mha_t.attn.k_proj.bias)
+BF16_DEFAULT_GRAD = 2e-2  # ~2x the worst observed (8.3e-3 at T=320, 7.7e-3 at T=64: r04_parity_train.jsonl)
 
 
 def _fixed_noise(tr, B, shape, seed=5):
@@ -385,3 +435,117 @@ def test_grad_checkpointing_on_hip_layers_same_grads():
         grads.append(torch.cat([p.grad.flatten() for p in m.parameters() if p.grad is not None]))
     assert grads[0].shape == grads[1].shape
     assert torch.equal(grads[0], grads[1]), float((grads[0] - grads[1]).abs().max())
+
+
+def _trainer_state(tr):
+    params = torch.cat([p.detach().flatten() for p in tr.wrapper.model.parameters()])
+    ema = torch.cat([v.flatten() for v in tr.wrapper.ema.params.values() if v.is_floating_point()])
+    moments = torch.cat([st[k].detach().flatten().float() for st in tr.optimizer.state.values()
+                         for k in ("exp_avg", "exp_avg_sq", "step") if k in st])
+    return params, ema, moments
+
+
+def test_graphed_resume_keeps_optimizer_state_and_ema(tmp_path):
+    """--ckpt resume into the graphed step (train_graph 1, the ROCm default): GraphedStep's warm-up
+    must hand the capture the LOADED Adam moments / step count and EMA, not zeros.
+    Train 2 graphed steps, save; resume twice (graphed and eager) and take one step on the same
+    batch and noise: parameters, Adam state and EMA agree."""
+    import os
+
+    from mdgen_finetune_amd.checkpoint import load_checkpoint
+    from mdgen_finetune_amd.train import Trainer
+
+    base = ["--lr", "1e-3", "--embed_dim", "64", "--mha_heads", "4", "--ema", "--ema_decay", "0.9"]
+    a = _args(base + ["--train_graph", "1", "--max_steps", "2", "--epochs", "1"], tmp_path)
+    tr = Trainer(a, device=torch.device("cuda"))
+    tr.fit()
+    ck_path = os.path.join(tmp_path, sorted(os.listdir(tmp_path))[-1])
+    ck = load_checkpoint(ck_path)
+    saved_steps = [float(s["step"]) for s in ck["optimizer_states"][0]["state"].values()]
+    assert saved_steps and all(s == 2.0 for s in saved_steps)
+    res = {}
+    for mode in (1, 0):
+        a2 = _args(base + ["--train_graph", str(mode), "--ckpt", ck_path], tmp_path)
+        tr2 = Trainer(a2, device=torch.device("cuda"))
+        b = _batch(a2, B=2, seed=3)
+        _fixed_noise(tr2, 2, (2, a2.num_frames, a2.crop, 21))
+        tr2.step([b], log=False)
+        res[mode] = _trainer_state(tr2)
+        steps = {float(st["step"]) for st in tr2.optimizer.state.values()}
+        assert steps == {3.0}, (mode, steps)
+    for i, what in enumerate(("params", "ema", "adam")):
+        d = float((res[0][i] - res[1][i]).abs().max())
+        assert d <= 1e-6 * max(1.0, float(res[0][i].abs().max())), (what, d)
+
+
+def test_tps_graphed_step_equals_eager_step():
+    """TPS fine-tuning (--tps_condition) in the graphed step: the relative frames (a host eigh)
+    are staged outside the capture (GraphedStep._stage_rel7); the replayed step equals the eager
+    step (the capture used to fail on the .cpu() inside relative_tensor7)."""
+    from mdgen_finetune_amd.train import Trainer
+
+    res = {}
+    for mode in (0, 1):
+        a = _args(["--lr", "1e-3", "--embed_dim", "64", "--mha_heads", "4", "--tps_condition", "--train_graph",
+                   str(mode)])
+        a.sim_condition = False
+        tr = Trainer(a, device=torch.device("cuda"))
+        assert tr.graph_mode == bool(mode) and tr.wrapper.model.tps
+        b = _batch(a, B=2)
+        _fixed_noise(tr, 2, (2, a.num_frames, a.crop, 28))
+        loss = float(tr.step([b], log=False)[0])  # (the graphed step's loss is a static buffer)
+        if mode:  # a second batch re-stages its own frames
+            tr.step([_batch(a, B=2, seed=9)], log=False)
+            tr2 = Trainer(a, device=torch.device("cuda"))
+            tr2.graph_mode = False
+            _fixed_noise(tr2, 2, (2, a.num_frames, a.crop, 28))
+            tr2.step([b], log=False)
+            tr2.step([_batch(a, B=2, seed=9)], log=False)
+            p2 = torch.cat([p.detach().flatten() for p in tr2.wrapper.model.parameters()])
+        res[mode] = (loss, torch.cat([p.detach().flatten() for p in tr.wrapper.model.parameters()]))
+    assert abs(res[0][0] - res[1][0]) <= 1e-5 * abs(res[0][0])
+    p1 = res[1][1]
+    assert float((p1 - p2).abs().max()) <= 1e-6, float((p1 - p2).abs().max())
+
+
+@pytest.mark.parametrize("L", [16, 20])
+def test_tps_ipa_long_crop_grads_match_eager(L):
+    """TPS with the IPA prepend at crops L >= 16: run_ipa calls every IPA layer twice per step
+    (x_r, x_f; latent_model.py:240-243) on the HIP layer Function, whose L >= 16 spatial planes are
+    saved activations; the two calls must not share them.  Every parameter gradient of
+    the HIP f32 path against eager autograd on the same device, rel <= 1e-4."""
+    from mdgen_finetune_amd.transport.transport import mean_flat
+    from mdgen_finetune_amd.wrapper import NewMDGenWrapper
+
+    a = _args(["--embed_dim", "64", "--mha_heads", "4", "--tps_condition", "--crop", str(L), "--num_frames", "4"])
+    a.sim_condition = False
+    torch.manual_seed(0)
+    w = NewMDGenWrapper(a).cuda()
+    m = w.model
+    from mdgen_finetune_amd import synthetic
+
+    synthetic.fill_module_(m, 11)  # non-zero IPA linear_out / adaLN so every path carries gradient
+    m.train()
+    m.hip_dtype = "f32"
+    b = {k: (v.cuda() if torch.is_tensor(v) else v) for k, v in _batch(a, B=2, seed=4).items()}
+    prep = w.prep_batch(b)
+    gen = torch.Generator().manual_seed(2)
+    x0 = torch.randn(prep["latents"].shape, generator=gen).cuda()
+    t = (0.1 + 0.8 * torch.rand(2, generator=gen)).cuda()
+    grads = {}
+    for backend in ("hip", "torch"):
+        m.train_backend = backend
+        m.zero_grad(set_to_none=True)
+        tt, xt, ut = w.transport.path_sampler.plan(t, x0, prep["latents"])
+        v = m(xt, tt, **prep["model_kwargs"])
+        mean_flat((v - ut) ** 2, prep["loss_mask"]).mean().backward()
+        grads[backend] = {n: p.grad.detach().clone() for n, p in m.named_parameters() if p.grad is not None}
+    worst = (0.0, None)
+    for n, gr in grads["torch"].items():
+        if float(gr.norm()) < 1e-10:
+            continue
+        assert n in grads["hip"], n
+        worst = max(worst, (float((grads["hip"][n] - gr).norm() / gr.norm()), n))
+    _log_train({"test": "tps_ipa_long_crop", "L": L, "worst_grad_rel": worst[0], "worst_param": worst[1]})
+    assert worst[0] <= 1e-4, worst
+    assert any(n.startswith("ipa_layers.") and "mha_l" in n for n in grads["hip"])

@@ -10,6 +10,6 @@ if [ -n "${FIRST:-}" ]; then
   echo "first rc=$rc"; grep -E "PASSED|FAILED|ERROR|Error|assert" gpurun_out/pytest_first.log | head -30
   [ $rc -ne 0 ] && exit $rc
 fi
-timeout -k 10 900 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1; rc=$?
+timeout -k 10 900 python -u -m pytest tests -m gpu -q --maxfail=8 --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1; rc=$?
 echo "suite rc=$rc"; tail -8 gpurun_out/pytest_gpu.log
 exit $rc
