@@ -69,10 +69,23 @@ def parse():
                     help="BASELINE config 3 evidence line: the GVP training step (forward + loss + backward + "
                          "clip + Adam + EMA, the HIP block stack, graphed) at B trajectories x T frames per GPU "
                          "(use --batch 8); ranks average gradients over RCCL")
+    ap.add_argument("--train-rccl1", action="store_true",
+                    help="with --train at one GPU: a world-1 RCCL group with the gradient reduction forced on, "
+                         "so the step's graph carries its per-bucket all-reduces (rehearsal of the N-GPU step)")
     ap.add_argument("--tps", action="store_true",
                     help="TPS / interpolation model (BASELINE config 4: --tps_condition, latent 28, start + end "
                          "frames conditioned; use with --frames 100); an evidence line, not the headline")
     return ap.parse_args()
+
+
+def _free_port():
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
 
 
 def make_model(T, L, seed=0, tps=False):
@@ -471,7 +484,12 @@ def train_main(a, world, rank, dev, share):
                              str(T), "--crop", str(L), "--batch_size", str(B), "--synthetic_size", str(B * world),
                              "--hip_dtype", a.dtype, "--seed", "137"])
     torch.set_float32_matmul_precision("medium")  # train.py:13
+    rehearse = a.train_rccl1 and world == 1
+    if rehearse:  # a world-1 RCCL group with the reduction forced on: the in-graph bucket all-reduces run
+        torch.distributed.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % _free_port(), rank=0,
+                                             world_size=1, device_id=dev)
     tr = Trainer(args, rank, world, dev)
+    tr.force_allreduce = rehearse
     batch = {k: (v.to(dev) if torch.is_tensor(v) else v) for k, v in next(iter(tr.loader)).items()}
     for _ in range(max(1, a.warmup)):
         loss, _ = tr.step([batch], log=False)
@@ -504,7 +522,11 @@ def train_main(a, world, rank, dev, share):
                                   f"B={B} trajectories x T={T} frames x L={L} per GPU",
                       "model": "LatentMDGenModel default (5 layers, C=384, 16 heads, IPA prepend, abs pos emb)",
                       "global_batch": B * world, "seq_len": T, "crop": L,
-                      "parallelism": f"dp{world}" + (" (flat RCCL all-reduce between graphs)" if world > 1 else ""),
+                      "parallelism": f"dp{world}" + (
+                          (" (per-bucket RCCL all-reduces captured in the step's graph, overlapped with backward)"
+                           if tr._graphed is not None and tr._graphed.overlap else
+                           " (flat all-reduce between two graphs)") if (world > 1 or rehearse) else ""),
+                      "allreduce_rehearsal_world1": bool(rehearse),
                       "hipgraph": bool(tr.graph_mode)},
            "step_roofline": {"flops_per_step": flops, "flops_basis": "3 x forward FLOPs of the block stack + "
                                                                      "embedding / FinalLayer (step_model), B per GPU",
@@ -515,6 +537,12 @@ def train_main(a, world, rank, dev, share):
     if share:
         out["shared_gpu"] = True
         out["ranks_sharing_gpu"] = world
+    if rehearse:
+        red = tr._graphed.reducer
+        out["allreduce_buckets"] = {"n": len(red.buckets), "bytes": [int(sl.numel() * 4) for sl in red.slices],
+                                    "launched_after_grads": [n for _, n in red.launch_log],
+                                    "grads_total": sum(len(b) for b in red.buckets)}
+        torch.distributed.destroy_process_group()
     print(json.dumps(out), flush=True)
 
 

@@ -1,0 +1,128 @@
+"""Bucketed gradient all-reduce overlapped with backward, usable inside a hipGraph capture.
+
+The reference averages gradients with Lightning's DDP (``/root/reference/src/train.py:46-60``):
+bucketed all-reduces that NCCL runs while backward is still producing the earlier layers'
+gradients.  DDP's reducer cannot be captured (it synchronises with the host between
+iterations), and the graphed optimizer step (train.GraphedStep) is what removes the eager
+step's host-launch bound, so this class does DDP's job inside the capture:
+
+* the parameters are laid out in a flat fp32 buffer in the order backward COMPLETES their
+  gradients (recorded once from post-accumulate-grad hooks during warm-up), cut into buckets
+  of ``cap_bytes``, so each bucket is one contiguous slice that becomes final at one moment;
+* a post-accumulate-grad hook counts a bucket's parameters down; when the last one lands, the
+  bucket's gradients are packed into its slice (one ``cat`` on the producing stream), an event
+  forks a side stream, and the slice's all-reduce (RCCL over xGMI) + 1/world scale run there
+  while backward continues on the main stream;
+* ``finish()`` joins the side stream (graph-capture legal: event record / wait) and points
+  every ``p.grad`` at its slice, so clip / Adam / EMA read the averaged values in place.
+
+Inside a capture the collectives become graph nodes on the side stream's branch, interleaved
+with the backward kernels (the replay keeps the overlap).  On CPU (gloo) the same object runs
+eagerly with ``async_op`` all-reduces, which is how the world-2 CPU tests exercise it.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+
+def record_grad_order(params):
+    """Register hooks that log the order in which backward completes each parameter's
+    gradient; returns (order list of indices, remove())."""
+    order, handles = [], []
+    for i, p in enumerate(params):
+        handles.append(p.register_post_accumulate_grad_hook(lambda _p, i=i: order.append(i)))
+
+    def remove():
+        for h in handles:
+            h.remove()
+
+    return order, remove
+
+
+class BucketedAllReduce:
+    def __init__(self, params, order, cap_bytes, world, group=None):
+        self.params = list(params)
+        self.world, self.group = world, group
+        dev = self.params[0].device
+        # parameters that backward never reached keep grad None (the optimizer skips them)
+        seen = list(dict.fromkeys(order))
+        self.buckets, cur, size = [], [], 0
+        for i in seen:
+            nb = self.params[i].numel() * 4
+            if cur and size + nb > cap_bytes:
+                self.buckets.append(cur)
+                cur, size = [], 0
+            cur.append(i)
+            size += nb
+        if cur:
+            self.buckets.append(cur)
+        n = sum(self.params[i].numel() for b in self.buckets for i in b)
+        self.flat = torch.zeros(n, device=dev, dtype=torch.float32)
+        self.slices, self.views, self.bucket_of, off = [], {}, {}, 0
+        for bi, b in enumerate(self.buckets):
+            start = off
+            for i in b:
+                p = self.params[i]
+                self.views[i] = self.flat[off:off + p.numel()].view_as(p)
+                self.bucket_of[i] = bi
+                off += p.numel()
+            self.slices.append(self.flat[start:off])
+        self.cuda = dev.type == "cuda"
+        self.side = torch.cuda.Stream(device=dev) if self.cuda else None
+        self._handles = []
+        self.launch_log = []  # (bucket, number of hooks fired so far) per launch: the overlap record
+
+    # ---------------------------------------------------------------- per step
+    def attach(self):
+        """Arm the hooks for one backward pass."""
+        self.detach()
+        self._pending = [len(b) for b in self.buckets]
+        self._works, self._fired = [], 0
+        self.launch_log = []
+        for bi, b in enumerate(self.buckets):
+            for i in b:
+                self._handles.append(self.params[i].register_post_accumulate_grad_hook(
+                    lambda _p, i=i: self._ready(i)))
+
+    def detach(self):
+        for h in self._handles:
+            h.remove()
+        self._handles = []
+
+    def _ready(self, i):
+        self._fired += 1
+        bi = self.bucket_of[i]
+        self._pending[bi] -= 1
+        if self._pending[bi] == 0:
+            self._launch(bi)
+
+    def _launch(self, bi):
+        self.launch_log.append((bi, self._fired))
+        sl = self.slices[bi]
+        torch.cat([self.params[i].grad.reshape(-1) for i in self.buckets[bi]], out=sl)
+        if self.cuda:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(sl.device))
+            self.side.wait_event(ev)
+            with torch.cuda.stream(self.side):
+                dist.all_reduce(sl, group=self.group)
+                sl.div_(self.world)
+        else:
+            self._works.append((dist.all_reduce(sl, group=self.group, async_op=True), sl))
+
+    def finish(self):
+        """Join the reductions and point every gradient at its averaged slice."""
+        if any(self._pending):
+            missing = [bi for bi, n in enumerate(self._pending) if n]
+            raise RuntimeError(f"gradient buckets {missing} never completed: backward skipped parameters "
+                               "that produced gradients in warm-up")
+        if self.cuda:
+            torch.cuda.current_stream(self.flat.device).wait_stream(self.side)
+        else:
+            for w, sl in self._works:
+                w.wait()
+                sl.div_(self.world)
+        for i, v in self.views.items():
+            self.params[i].grad = v
+        self.detach()

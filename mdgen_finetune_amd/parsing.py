@@ -55,7 +55,7 @@ _EXTRA = [
     ("synthetic_size", _I, 64, "number of synthetic trajectories"),
     ("max_steps", _I, None, "stop after this many optimizer steps"),
     ("seed", _I, 137, "base RNG seed (rank r uses seed + r for its noise draws)"),
-    ("bucket_cap_mb", _F, 32.0, "DDP gradient bucket size (all-reduce overlaps backward per bucket)"),
+    ("bucket_cap_mb", _F, 32.0, "gradient bucket size of the all-reduce overlapped with backward (DDP and the graphed step)"),
     ("model_dir", _S, None, "checkpoint directory (default workdir/<run_name>, the reference's MODEL_DIR)"),
     ("train_backend", _S, "hip", "'hip': on a ROCm device every block's forward + backward runs in "
                                  "libmdgen_hip.so (train_hip.py); 'torch': eager autograd"),
@@ -64,6 +64,9 @@ _EXTRA = [
     ("train_graph", _I, 1, "1: on a ROCm device the optimizer step replays hipGraphs (forward + loss + "
                            "backward [+ RCCL gradient all-reduce between two graphs] + clip + Adam + EMA); "
                            "0: eager step (also used for grad accumulation > 1 and 16-mixed)"),
+    ("allreduce_overlap", _I, 1, "graphed step with world > 1 over RCCL: 1 = per-bucket all-reduces captured "
+                                 "in the graph on a side stream, each issued as backward completes its bucket "
+                                 "(--bucket_cap_mb); 0 = one flat all-reduce between two graphs"),
 ]
 
 _REQUIRED = ("train_split", "val_split", "data_dir")

@@ -35,6 +35,7 @@ from torch.nn.parallel import DistributedDataParallel as DDP
 
 from .checkpoint import load_checkpoint, model_state_dict, save_checkpoint
 from .data import SyntheticMDDataset, collate
+from .grad_buckets import BucketedAllReduce, record_grad_order
 from .parsing import parse_train_args
 from .wrapper import NewMDGenWrapper
 
@@ -279,9 +280,17 @@ class GraphedStep:
     stream (autograd buffers, optimizer / EMA state, RoPE tables; the parameters, optimizer
     state and EMA are restored afterwards, so warm-up trains nothing), one capture records
       world 1: prep_batch -> GVP loss -> backward -> grad clip -> Adam (capturable) -> EMA
-    and each step is: copy the batch into the static buffers, replay.  With world > 1 the step
-    is two graphs around an eager RCCL all-reduce of the flat gradient buffer (graph 1 ends by
-    packing the gradients into it; graph 2's clip / Adam read them through views of it):
+    and each step is: copy the batch into the static buffers, replay.  With world > 1 over RCCL
+    (``--allreduce_overlap 1``, the default) the gradient all-reduce is captured too: the
+    parameters' gradients are bucketed in the order backward completes them, and each bucket's
+    RCCL all-reduce runs on a side-stream branch of the same graph as soon as its last gradient
+    lands, overlapped with the rest of backward (grad_buckets.BucketedAllReduce, DDP's schedule
+    inside the capture):
+      prep_batch -> loss -> backward  -> join -> clip -> Adam -> EMA
+                              \_ bucket k: cat -> all_reduce / world (side stream) _/
+    Otherwise (gloo, which cannot be captured, or ``--allreduce_overlap 0``) the step is two
+    graphs around an eager all-reduce of the flat gradient buffer (graph 1 ends by packing the
+    gradients into it; graph 2's clip / Adam read them through views of it):
       graph 1: prep_batch -> loss -> backward -> cat(grads) | all_reduce(flat) / world |
       graph 2: clip -> Adam -> EMA.
     The (t, x0) draws come from the CUDA generator's graph-safe philox offsets, so every replay
@@ -292,7 +301,12 @@ class GraphedStep:
         dev = tr.device
         self.static = {k: (v.to(dev).clone() if torch.is_tensor(v) else v) for k, v in batch.items()}
         self.params = [p for p in tr.wrapper.model.parameters() if p.requires_grad]
-        self.split = tr.world > 1
+        # force_allreduce: run the reduction machinery at world 1 (a world-1 RCCL group: the GPU
+        # tests' capture check on a one-GPU box)
+        self.split = tr.world > 1 or bool(getattr(tr, "force_allreduce", False))
+        self.overlap = bool(self.split and int(getattr(tr.args, "allreduce_overlap", 1)) and dist.is_initialized()
+                            and dist.get_backend() == "nccl")
+        self.reducer = None
         model = tr.wrapper.model
         # TPS: the relative frames come from a host eigh (relative_tensor7), which a capture
         # cannot contain; they are computed here per step and read from a static buffer
@@ -326,9 +340,17 @@ class GraphedStep:
         ema_snap = {k: v.detach().clone() for k, v in ema.params.items()} if ema is not None else None
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
+        order, unhook = record_grad_order(self.params)  # the order backward completes gradients
         with torch.cuda.stream(side):
-            for _ in range(warmup):
+            for w in range(warmup):
                 tr._eager_step([self.static], log=False, update=False)
+                if w == 0:
+                    unhook()
+        unhook()
+        if self.overlap:
+            self.reducer = BucketedAllReduce(self.params, order, int(tr.args.bucket_cap_mb * 2 ** 20), tr.world)
+            with torch.cuda.stream(side):  # the communicator exists before the capture
+                dist.all_reduce(torch.zeros(1, device=dev))
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
         with torch.no_grad():
@@ -348,16 +370,21 @@ class GraphedStep:
                     ema.params[k].copy_(v)
         tr.optimizer.zero_grad(set_to_none=True)
         n = sum(p.numel() for p in self.params)
-        self.flat = torch.empty(n, device=dev) if self.split else None
+        self.flat = self.reducer.flat if self.overlap else (torch.empty(n, device=dev) if self.split else None)
         self.g1 = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.g1):
+            if self.overlap:
+                self.reducer.attach()
             self.loss, self.losses, self.t = self._fwd_bwd()
-            if self.split:
+            if self.overlap:  # one graph: the bucket all-reduces are branches of it
+                self.reducer.finish()
+                self.gnorm = self._update()
+            elif self.split:
                 self.grads_g1 = [p.grad for p in self.params]  # graph-1 memory, kept referenced
                 torch.cat([g.reshape(-1) for g in self.grads_g1], out=self.flat)
             else:
                 self.gnorm = self._update()
-        if self.split:
+        if self.split and not self.overlap:
             off = 0
             for p in self.params:  # graph 2 reads the averaged gradients in place
                 p.grad = self.flat[off:off + p.numel()].view_as(p)
@@ -391,7 +418,7 @@ class GraphedStep:
         if self.rel7 is not None:
             self._stage_rel7(batch)
         self.g1.replay()
-        if self.split:
+        if self.split and not self.overlap:
             self.tr.allreduce_grads(self.flat)
             self.g2.replay()
         model = self.tr.wrapper.model  # the replayed Adam bumps no version counters: tell the engine

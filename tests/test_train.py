@@ -207,6 +207,76 @@ def test_ddp_world2_gloo_allreduce_matches_local_mean():
         assert first_bucket < last_grad, (first_bucket, last_grad)
 
 
+def _bucket_worker(rank, world, port, out):
+    """grad_buckets.BucketedAllReduce (the graphed step's in-capture all-reduce) run eagerly over
+    gloo: the order recorded from one backward, the buckets launched from the hooks."""
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from mdgen_finetune_amd.grad_buckets import BucketedAllReduce, record_grad_order
+    from mdgen_finetune_amd.train import Trainer, setup_distributed
+
+    r, w, dev = setup_distributed()
+    a = _args(["--grad_clip", "0"])
+    tr = Trainer(a, r, w, dev)
+    m = tr.wrapper.model
+    params = [p for p in m.parameters() if p.requires_grad]
+    b = _batch(a, B=2, seed=100 + rank)
+    g = torch.Generator().manual_seed(7 + rank)
+    x0, t = torch.randn(2, 8, 4, 21, generator=g), torch.rand(2, generator=g)
+    tr.wrapper.transport.sample = lambda x1: (t, x0, x1)
+
+    def backward():
+        m.zero_grad(set_to_none=True)
+        tr.wrapper.general_step(b, model=m).backward()
+
+    order, unhook = record_grad_order(params)
+    backward()
+    unhook()
+    local = [p.grad.clone() if p.grad is not None else None for p in params]
+    red = BucketedAllReduce(params, order, cap_bytes=40 * 1024, world=w)
+    red.attach()
+    backward()
+    red.finish()
+    err, scale = 0.0, 0.0
+    for p, lg in zip(params, local):
+        if lg is None:
+            assert p.grad is None
+            continue
+        ref = lg.clone()
+        dist.all_reduce(ref)
+        ref /= w
+        err = max(err, float((p.grad - ref).abs().max()))
+        scale = max(scale, float(ref.abs().max()))
+    # a second step through the same reducer (hooks re-armed) gives the same averages
+    g1 = red.flat.clone()
+    red.attach()
+    backward()
+    red.finish()
+    out[rank] = (err, scale, len(red.buckets), red.launch_log, len(order), float((red.flat - g1).abs().max()),
+                 sum(p.numel() for p, lg in zip(params, local) if lg is not None) == red.flat.numel())
+    dist.destroy_process_group()
+
+
+def test_bucketed_allreduce_world2_gloo_overlaps_and_averages():
+    """The graphed step's bucketed all-reduce (grad_buckets.py), world 2 over gloo: every
+    gradient equals the ranks' mean, the buckets follow backward's completion order, and the
+    first bucket is reduced before backward has produced the last gradient (overlap)."""
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_bucket_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    for r in range(2):
+        err, scale, nb, log, n_grads, drift, covers = out[r]
+        assert err <= 1e-6 * max(1.0, scale), (r, err, scale)
+        assert nb >= 3, nb
+        assert [bi for bi, _ in log] == list(range(nb)), log  # launched in layout order
+        assert log[0][1] < n_grads, (log, n_grads)  # before the last gradient landed
+        assert drift == 0.0
+        assert covers
+
+
 def _bench_worker(rank, world, port, out):
     import torch.distributed as dist
 

@@ -1,0 +1,52 @@
+"""Summarise a rocprofv3 kernel trace of `bench.py --train --train-rccl1` (the graphed training
+step with its per-bucket RCCL all-reduces captured in the graph): for every collective kernel of
+the last replayed steps, when it started within the step, how long it ran, which library kernels
+ran concurrently with it (overlap with backward) and how many kernels of the step started after
+it.  Usage: python tools/rccl_overlap_trace.py <kernel_trace.csv> <buckets per step> [out.md]"""
+import csv
+import sys
+
+
+def main():
+    path, nb = sys.argv[1], int(sys.argv[2])
+    out = sys.argv[3] if len(sys.argv) > 3 else None
+    rows = []
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
+    rows.sort()
+    is_coll = [("nccl" in n.lower() or "rccl" in n.lower()) for _, _, n in rows]
+    coll = [i for i, c in enumerate(is_coll) if c]
+    if len(coll) < nb:
+        print(f"only {len(coll)} collective kernels in the trace", file=sys.stderr)
+        sys.exit(1)
+    nsteps = len(coll) // nb
+    lines = [f"# In-graph RCCL bucket all-reduces ({path.split('/')[-1]})", "",
+             f"{len(rows)} kernels, {len(coll)} collective kernels, {nb} buckets per step, {nsteps} steps traced.", ""]
+    for s in range(max(0, nsteps - 2), nsteps):
+        idx = coll[s * nb:(s + 1) * nb]
+        # the step's window: from the kernel after the previous step's last collective (or the
+        # trace start) to the step's last collective's end plus the optimizer tail
+        lo = coll[s * nb - 1] + 1 if s > 0 else 0
+        hi = coll[(s + 1) * nb] if s + 1 < nsteps else len(rows)
+        t0 = rows[lo][0]
+        lines += [f"## step {s} ({hi - lo} kernels, {(rows[hi - 1][1] - t0) / 1e3:.1f} us)", "",
+                  "| bucket | start (us into step) | duration (us) | concurrent kernels | step kernels started after it | concurrent examples |",
+                  "|---|---|---|---|---|---|"]
+        for b, i in enumerate(idx):
+            st, en, name = rows[i]
+            conc = [rows[j][2] for j in range(lo, hi) if not is_coll[j] and rows[j][0] < en and rows[j][1] > st]
+            after = sum(1 for j in range(i + 1, hi) if not is_coll[j])
+            ex = sorted(set(n.split("(")[0][:40] for n in conc))[:3]
+            lines.append(f"| {b} | {(st - t0) / 1e3:.1f} | {(en - st) / 1e3:.1f} | {len(conc)} | {after} | "
+                         f"{', '.join(ex)} |")
+        lines.append("")
+    txt = "\n".join(lines)
+    print(txt)
+    if out:
+        with open(out, "w") as f:
+            f.write(txt + "\n")
+
+
+if __name__ == "__main__":
+    main()
