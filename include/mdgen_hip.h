@@ -412,7 +412,8 @@ int mdg_ln_gate_bwd(int32_t dtype, int32_t M, int32_t C, int32_t rows_per_b, con
 /* Bias-key gradient partial slots per head of the attention backward kernels below. */
 int32_t mdg_attn_temporal_bwd_parts(int32_t dtype, int32_t B, int32_t T, int32_t L);
 int32_t mdg_attn_spatial_bwd_parts(int32_t n_frames, int32_t L, int32_t D);
-/* Scratch of mdg_attn_temporal_bwd: dO planes CT [B*L][H][T][32] then delta fp32 [B*L][H][T]. */
+/* Scratch of mdg_attn_temporal_bwd: dO planes CT [B*L][H][T][32], delta fp32 [B*L][H][T], and
+   for bf16 with T > 256 the fused kernel's fp32 dQ accumulator [B*L][H][T][32]. */
 size_t mdg_attn_temporal_bwd_scratch(int32_t dtype, int32_t B, int32_t T, int32_t L, int32_t H);
 /* Temporal (and L >= 16 spatial) attention backward: from the forward's planes (qkv_t), lse,
    output o (CT [N][C]; o_lo its residual from mdg_attn_temporal_lse or null) and its gradient
@@ -420,8 +421,9 @@ size_t mdg_attn_temporal_bwd_scratch(int32_t dtype, int32_t B, int32_t T, int32_
    projections (RoPE and the q scale undone: qscale = D^-1/2) into dqkv (CT, token-major rows of
    ld_dqkv >= 3C, packed column order); kscale = ln 2 for planes in log2 units (the forward's
    q carries log2 e).  bias_k / bias_v gradients (w.r.t. the rotated kvb rows) are written as
-   per-slot partials bpart [H][parts][2][32].  generic = 1 selects the scalar kernels (the
-   fp32 path always uses them). */
+   per-slot partials bpart [H][parts][2][32].  generic: 0 = the fused single-pass MFMA kernel
+   (bf16 default: P / dP once per pair, one block per (sequence, head), deterministic), 2 = the
+   two-pass MFMA kernels (dQ; dK / dV), 1 = the scalar kernels (the fp32 path always uses them). */
 int mdg_attn_temporal_bwd(int32_t dtype, int32_t B, int32_t T, int32_t L, int32_t H, int32_t D, const void* qkv_t,
                           const float* kbias, const float* kvb, const void* o, const void* o_lo, const void* dout,
                           const float* lse,
@@ -441,7 +443,8 @@ int mdg_attn_spatial_bwd(int32_t dtype, int32_t n_frames, int32_t L, int32_t H, 
    dy CT [N][ldy] (columns 0..M-1), x CT [N][ldx] (columns 0..K-1); the reduction is split over
    token chunks whose fp32 partials (in ws) are summed in chunk order: deterministic.  bf16 needs
    N % 32 == 0 (pad the token rows with zeros); M, K, ldy, ldx multiples of 8; 16-B aligned
-   operands.  ws: mdg_wgrad_workspace_bytes(dtype, N, M, K, need_dw, need_db) bytes. */
+   operands and dw, lddw a multiple of 4.  bf16 with both outputs: the column sums ride in the
+   dW blocks and one launch reduces both.  ws: mdg_wgrad_workspace_bytes(dtype, N, M, K, need_dw, need_db) bytes. */
 size_t mdg_wgrad_workspace_bytes(int32_t dtype, int32_t N, int32_t M, int32_t K, int32_t need_dw, int32_t need_db);
 int mdg_wgrad(int32_t dtype, int32_t N, int32_t M, int32_t K, const void* dy, int32_t ldy, const void* x, int32_t ldx,
               float* dw, int32_t lddw, float* db, void* ws, size_t ws_bytes, void* stream);

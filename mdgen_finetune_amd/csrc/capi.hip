@@ -73,7 +73,7 @@ hipError_t attn_temporal_bwd_launch(int dtype, int B, int T, int L, int H, int D
                                     const void* dout,
                                     const float* lse, const float* rope, int rope_rows, void* dop, float* delta,
                                     void* dqkv, int ldq, float* bpart, float qscale, float kscale, int generic,
-                                    hipStream_t s);
+                                    float* dqacc, hipStream_t s);
 int attn_spatial_bwd_parts(int nf, int L, int D);
 hipError_t attn_spatial_bwd_launch(int dtype, int nf, int L, int H, int D, const void* qkv, const float* kvb,
                                    const float* mask, const void* dout, const float* rope, int rope_rows, void* dqkv,
@@ -955,7 +955,9 @@ int32_t mdg_attn_spatial_bwd_parts(int32_t n_frames, int32_t L, int32_t D) {
 
 size_t mdg_attn_temporal_bwd_scratch(int32_t dtype, int32_t B, int32_t T, int32_t L, int32_t H) {
   const size_t rows = (size_t)B * L * H * T;
-  return align256(rows * MDG_DP * ct_size(dtype)) + align256(rows * sizeof(float));
+  // + the fused bf16 kernel's fp32 dQ accumulator when the keys take more than one 256-key pass
+  const size_t acc = (dtype == MDG_BF16 && T > 256) ? align256(rows * MDG_DP * sizeof(float)) : 0;
+  return align256(rows * MDG_DP * ct_size(dtype)) + align256(rows * sizeof(float)) + acc;
 }
 
 int mdg_attn_temporal_bwd(int32_t dtype, int32_t B, int32_t T, int32_t L, int32_t H, int32_t D, const void* qkv_t,
@@ -974,9 +976,11 @@ int mdg_attn_temporal_bwd(int32_t dtype, int32_t B, int32_t T, int32_t L, int32_
   const size_t rows = (size_t)B * L * H * T;
   void* dop = scratch;
   float* delta = (float*)((char*)scratch + align256(rows * MDG_DP * ct_size(dtype)));
+  float* dqacc = (float*)((char*)delta + align256(rows * sizeof(float)));
+  if (generic < 0 || generic > 2) return fail(MDG_E_ARG, "attn_temporal_bwd: generic=%d (0, 1, 2)", generic);
   return hip_check(mdg::attn_temporal_bwd_launch(dtype, B, T, L, H, D, qkv_t, kbias, kvb, o, o_lo, dout, lse, rope,
                                                  rope_rows, dop, delta, dqkv, ld_dqkv, bpart, qscale, kscale,
-                                                 generic || dtype == MDG_F32, (hipStream_t)stream),
+                                                 dtype == MDG_F32 ? 1 : generic, dqacc, (hipStream_t)stream),
                    "attn_temporal_bwd");
 }
 
@@ -1293,7 +1297,8 @@ int mdg_wgrad(int32_t dtype, int32_t N, int32_t M, int32_t K, const void* dy, in
     return fail(MDG_E_SHAPE, "wgrad: N=%d M=%d K=%d ldy=%d ldx=%d lddw=%d (M, K, ld multiples of 8)", N, M, K, ldy, ldx,
                 lddw);
   if (dtype == MDG_BF16 && N % 32) return fail(MDG_E_SHAPE, "wgrad bf16: N=%d not a multiple of 32 (pad with zero rows)", N);
-  if (!aligned16(dy) || (dw && !aligned16(x))) return fail(MDG_E_SHAPE, "wgrad: operands must be 16-B aligned");
+  if (!aligned16(dy) || (dw && (!aligned16(x) || !aligned16(dw) || lddw % 4)))
+    return fail(MDG_E_SHAPE, "wgrad: operands and dw must be 16-B aligned, lddw a multiple of 4");
   const size_t need = mdg::wgrad_ws_bytes(dtype, N, M, K, dw != nullptr, db != nullptr);
   if (!ws || ws_bytes < need) return fail(MDG_E_ARG, "wgrad: workspace %zu < %zu bytes", ws_bytes, need);
   return hip_check(mdg::wgrad_launch(dtype, N, M, K, dy, ldy, x, ldx, dw, lddw, db, (float*)ws, (hipStream_t)stream),

@@ -873,6 +873,272 @@ __global__ __launch_bounds__(kBW * 64) void attn_bwd_dkdv_bf16_kernel(
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Fused single-pass backward: one block per (sequence, head), 8 waves x 32 keys = a 256-key
+// block, the key blocks of the sequence in turn (T > 256: several passes).  Per 64-query chunk
+// (Q / dO images double-buffered through registers, as the dK/dV kernel stages them):
+//   phase A (per wave, its 32 keys x 64 queries, v_mfma_f32_32x32x16_bf16):
+//     S = Q K^T, dP = dO V^T, P = exp2(S + kbias - lse), dS = P (dP - delta),
+//     dV^T += dO^T P, dK^T += Q^T dS  (the accumulator-as-operand map of the dK/dV kernel),
+//     and dS^T (bf16) into a block-wide [256 keys][64 queries] LDS image;
+//   barrier;
+//   phase B (per wave, a 16-dim x 16-query tile of dQ^T over the block's 256 keys,
+//     v_mfma_f32_16x16x32_bf16): dQ^T += K^T dS^T, both operands read TRANSPOSED out of their
+//     images with ds_read_b64_tr_b16 (K^T from a [256 keys][32] copy of the block's K rows).
+// P and dP are computed once per (query, key) pair (the two-pass kernels compute them twice),
+// and no float atomics are used: dQ of a query sums the key blocks in order through an fp32
+// [seq][head][T][32] buffer that only this block touches (stored in the first pass, read-add-
+// stored in the middle ones); the LAST pass adds the bias key's term (dS_b bk), applies the q
+// scale and the inverse RoPE and writes bf16 dQ straight into the token-major gradient, and
+// accumulates the bias_k / bias_v gradient (sum over queries of dS_b q, P_b dO) per block.
+// Deterministic run to run.  LDS 65 KiB: two blocks per CU.
+constexpr int kFQC = 64;  // queries per chunk
+
+// dS^T image [256][64] bf16, 128-B rows: 8-B slot s of row r at s ^ f(r), f a bit permutation
+// of r's low 4 bits that makes both the 16-row ds_write_b64 groups and the tr reads (rows
+// k0 + 8g + {0..3}, 4 slots each) bank-conflict free.
+__device__ __forceinline__ int fds_off(int row, int col) {
+  const int f = (((row >> 3) & 1) << 3) | (((row >> 1) & 1) << 2) | (((row >> 2) & 1) << 1) | (row & 1);
+  return row * kFQC + ((((col >> 2) ^ f)) << 2) + (col & 3);
+}
+// K image [256][32] bf16, 64-B rows: slot s of row r at s ^ (((r >> 3) & 1) << 2)
+__device__ __forceinline__ int fk_off(int row, int col) {
+  return row * kDP + ((((col >> 2) ^ (((row >> 3) & 1) << 2))) << 2) + (col & 3);
+}
+
+// 16x16x32 operand read transposed out of a row-major image whose rows are the k axis:
+// lane l (group g = l >> 4, i = l & 15) receives X[k0 + 8g + j][c0 + i], j = 0..7.
+template <bool KIMG>
+__device__ __forceinline__ bf16x8 ftr16(const bf16_t* img, int k0, int c0, int lane) {
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int r0 = k0 + 8 * g + q, c = c0 + 4 * p;
+  const int o0 = KIMG ? fk_off(r0, c) : fds_off(r0, c);
+  const int o1 = KIMG ? fk_off(r0 + 4, c) : fds_off(r0 + 4, c);
+  const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(img + o0));
+  const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(img + o1));
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    r[j] = lo[j];
+    r[4 + j] = hi[j];
+  }
+  return r;
+}
+
+__global__ __launch_bounds__(kBW * 64, 2) void attn_bwd_fused_bf16_kernel(
+    const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dop, const float* __restrict__ lse,
+    const float* __restrict__ delta, const float* __restrict__ kbias, const float* __restrict__ kvb,
+    const float* __restrict__ rope, int rope_rows, bf16_t* __restrict__ dqkv, int ldq, float* __restrict__ dqacc,
+    float* __restrict__ bpart, int T, int L, int H, int D, int BL, float qscale, float kscale) {
+  constexpr int NTH = kBW * 64, KB = kBW * 32;
+  static_assert(2 * kFQC * kDP / 8 == NTH, "one 16-B piece of Q or dO per thread per chunk");
+  __shared__ __attribute__((aligned(16))) bf16_t Qs[2][kFQC * kDP];
+  __shared__ __attribute__((aligned(16))) bf16_t Ds[2][kFQC * kDP];
+  __shared__ __attribute__((aligned(16))) float ls[2][kFQC];
+  __shared__ __attribute__((aligned(16))) float dls[2][kFQC];
+  __shared__ __attribute__((aligned(16))) bf16_t dsT[KB * kFQC];
+  __shared__ __attribute__((aligned(16))) bf16_t Kim[KB * kDP];
+  __shared__ float dsbs[kFQC], pbs[kFQC];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
+  const int wg = xcd_remap(H * BL);
+  const int head = wg % H, seq = wg / H, sh = seq * H + head;
+  const size_t plane = (size_t)BL * H * T * kDP;
+  const bf16_t* Qg = qkv + (size_t)sh * T * kDP;
+  const bf16_t* Kg = Qg + plane;
+  const bf16_t* Vg = Qg + 2 * plane;
+  const bf16_t* dOg = dop + (size_t)sh * T * kDP;
+  const float* lg = lse + (size_t)sh * T;
+  const float* dg = delta + (size_t)sh * T;
+  const float* kbg = kbias + (size_t)seq * T;
+  const float* bk = kvb + head * 2 * kDP;
+  const float* bv = bk + kDP;
+  float* acc_g = dqacc + (size_t)sh * T * kDP;
+  const int nkb = (T + KB - 1) / KB, nch = (T + kFQC - 1) / kFQC;
+  const int b = seq / L, l = seq % L, half = D >> 1, C = H * D;
+  // staging roles: image (Q / dO), row, 16-B piece; lse / delta by threads 0..127
+  const int simg = tid >> 8, srow = (tid >> 2) & (kFQC - 1), spc = tid & 3;
+  const bf16_t* sg = simg ? dOg : Qg;
+  u32x4 sreg;
+  float lreg = 0.f;
+  auto gload = [&](int c) {
+    const int qq = c * kFQC + srow;
+    sreg = u32x4{0u, 0u, 0u, 0u};
+    if (qq < T) sreg = *reinterpret_cast<const u32x4*>(sg + (size_t)qq * kDP + spc * 8);
+    if (tid < 2 * kFQC) {
+      const int q2 = c * kFQC + (tid & (kFQC - 1));
+      lreg = tid < kFQC ? (q2 < T ? lg[q2] : INFINITY) : (q2 < T ? dg[q2] : 0.f);
+    }
+  };
+  auto lstore = [&](int buf) {
+    *reinterpret_cast<u32x4*>(&(simg ? Ds : Qs)[buf][img_off(srow, spc * 8)]) = sreg;
+    if (tid < kFQC) ls[buf][tid] = lreg;
+    else if (tid < 2 * kFQC) dls[buf][tid - kFQC] = lreg;
+  };
+  // phase-B tile of this wave: dims 16 bd .. +15, queries 16 bq .. +15 of the chunk; the lane
+  // holds dims dB .. dB+3 of query column (lane & 15)
+  const int bq = wave >> 1, bd = wave & 1, dB = 16 * bd + 4 * (lane >> 4);
+  // bias-gradient roles (last pass): dim bgd, gk (0) / gv (1), queries 8 bqs .. +7 of a chunk
+  const int bgd = tid & 31, bgw = (tid >> 5) & 1, bqs = tid >> 6;
+  float bacc = 0.f;
+
+  for (int kb = 0; kb < nkb; ++kb) {
+    const bool last = kb == nkb - 1;
+    const int key = kb * KB + wave * 32 + r;
+    const bool live = key < T;
+    bf16x8 kf[2], vf[2];
+    plane_frag(Kg, key, live, h, kf);
+    plane_frag(Vg, key, live, h, vf);
+    const float kbl = live ? kbg[key] : -INFINITY;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+      *reinterpret_cast<bf16x8*>(&Kim[fk_off(wave * 32 + r, 16 * s2 + 8 * h)]) = kf[s2];
+    f32x16 dk, dv;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dk[i] = dv[i] = 0.f;
+    gload(0);
+    lstore(0);
+    __syncthreads();
+    for (int c = 0; c < nch; ++c) {
+      const int cur = c & 1;
+      if (c + 1 < nch) gload(c + 1);
+      const int qB = c * kFQC + 16 * bq + (lane & 15);
+      const bool qlive = qB < T && dB < D;
+      float4 prev = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (kb > 0 && qlive) prev = *reinterpret_cast<const float4*>(acc_g + (size_t)qB * kDP + dB);
+      if (last && tid < kFQC) {  // the bias key's P_b, dS_b per query of the chunk
+        const int q = c * kFQC + tid;
+        float sb = 0.f, dpb = 0.f;
+#pragma unroll
+        for (int d0 = 0; d0 < kDP; d0 += 8) {
+          const bf16x8 qv = *reinterpret_cast<const bf16x8*>(&Qs[cur][img_off(tid, d0)]);
+          const bf16x8 dv8 = *reinterpret_cast<const bf16x8*>(&Ds[cur][img_off(tid, d0)]);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            sb += (float)qv[j] * bk[d0 + j];
+            dpb += (float)dv8[j] * (d0 + j < D ? bv[d0 + j] : 0.f);
+          }
+        }
+        const float pb = q < T ? __builtin_amdgcn_exp2f(sb - ls[cur][tid]) : 0.f;
+        dsbs[tid] = pb * (dpb - dls[cur][tid]);
+        pbs[tid] = pb;
+      }
+      // phase A
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) {
+        const int base = qt * 32;
+        f32x16 sacc, pacc;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sacc[i] = pacc[i] = 0.f;
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(img_row(Qs[cur], base + r, s2, h), kf[s2], sacc, 0, 0, 0);
+          pacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(img_row(Ds[cur], base + r, s2, h), vf[s2], pacc, 0, 0, 0);
+        }
+        float pr[16], dsr[16];
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const float4 l4 = *reinterpret_cast<const float4*>(&ls[cur][base + 8 * g4 + 4 * h]);
+          const float4 d4 = *reinterpret_cast<const float4*>(&dls[cur][base + 8 * g4 + 4 * h]);
+          const float lv[4] = {l4.x, l4.y, l4.z, l4.w}, dv4[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int i = 4 * g4 + e;
+            const float p = __builtin_amdgcn_exp2f(sacc[i] + kbl - lv[e]);
+            pr[i] = p;
+            dsr[i] = p * (pacc[i] - dv4[e]);
+          }
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          bf16x8 pf, dsf;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            pf[j] = (bf16_t)pr[8 * s2 + j];
+            dsf[j] = (bf16_t)dsr[8 * s2 + j];
+          }
+          dv = __builtin_amdgcn_mfma_f32_32x32x16_bf16(img_tr(Ds[cur], base, s2, lane), pf, dv, 0, 0, 0);
+          dk = __builtin_amdgcn_mfma_f32_32x32x16_bf16(img_tr(Qs[cur], base, s2, lane), dsf, dk, 0, 0, 0);
+          // dS^T rows = this wave's keys, columns = queries base + 16 s2 + 8 (j >> 2) + 4h + (j & 3)
+          bf16x4 lo, hi;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            lo[j] = dsf[j];
+            hi[j] = dsf[4 + j];
+          }
+          *reinterpret_cast<bf16x4*>(&dsT[fds_off(wave * 32 + r, base + 16 * s2 + 4 * h)]) = lo;
+          *reinterpret_cast<bf16x4*>(&dsT[fds_off(wave * 32 + r, base + 16 * s2 + 8 + 4 * h)]) = hi;
+        }
+      }
+      if (c + 1 < nch) lstore(cur ^ 1);
+      __syncthreads();
+      // phase B: dQ^T (dims dB.., query qB) += K^T dS^T over the block's 256 keys
+      f32x4 acc = {prev.x, prev.y, prev.z, prev.w};
+#pragma unroll
+      for (int ks = 0; ks < KB / 32; ++ks)
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ftr16<true>(Kim, 32 * ks, 16 * bd, lane),
+                                                      ftr16<false>(dsT, 32 * ks, 16 * bq, lane), acc, 0, 0, 0);
+      if (!last) {
+        if (qlive) *reinterpret_cast<float4*>(acc_g + (size_t)qB * kDP + dB) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+      } else {
+        if (qlive) {
+          const float dsb = dsbs[qB - c * kFQC];
+          float a0 = (acc[0] + dsb * bk[dB]) * qscale, a1 = (acc[1] + dsb * bk[dB + 1]) * qscale;
+          float a2 = (acc[2] + dsb * bk[dB + 2]) * qscale, a3 = (acc[3] + dsb * bk[dB + 3]) * qscale;
+          if (rope) {
+            rope_inv(a0, a1, rope, rope_rows, half, qB, dB >> 1);
+            rope_inv(a2, a3, rope, rope_rows, half, qB, (dB >> 1) + 1);
+          }
+          const size_t tok = ((size_t)b * T + qB) * L + l;
+          st4<bf16_t>(dqkv + tok * ldq + head * D + dB, a0, a1, a2, a3);
+        }
+        // bias_k / bias_v gradients: this thread's dim over 8 queries of the chunk
+        const bf16_t* X = bgw ? Ds[cur] : Qs[cur];
+        const float* coef = bgw ? pbs : dsbs;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int qq = 8 * bqs + j;
+          bacc += coef[qq] * (float)X[img_off(qq, bgd)];
+        }
+      }
+      __syncthreads();
+    }
+    // dK / dV of this key block (the dK/dV kernel's epilogue)
+    if (live) {
+      const size_t tok = ((size_t)b * T + key) * L + l;
+      bf16_t* ok = dqkv + tok * ldq + C + head * D;
+      bf16_t* ov = dqkv + tok * ldq + 2 * C + head * D;
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d0 = 8 * g4 + 4 * h;
+        if (d0 < D) {
+          float a0 = dk[4 * g4] * kscale, a1 = dk[4 * g4 + 1] * kscale;
+          float a2 = dk[4 * g4 + 2] * kscale, a3 = dk[4 * g4 + 3] * kscale;
+          if (rope) {
+            rope_inv(a0, a1, rope, rope_rows, half, key, d0 >> 1);
+            rope_inv(a2, a3, rope, rope_rows, half, key, (d0 >> 1) + 1);
+          }
+          st4<bf16_t>(ok + d0, a0, a1, a2, a3);
+          st4<bf16_t>(ov + d0, dv[4 * g4], dv[4 * g4 + 1], dv[4 * g4 + 2], dv[4 * g4 + 3]);
+        }
+      }
+    }
+  }
+  // bias partials: the 8 query groups of each (dim, gk / gv) summed in order; the sequence's
+  // first slot of the two-pass kernels' layout gets the block total, its other slots zero
+  float* red = reinterpret_cast<float*>(dsT);
+  red[tid] = bacc;
+  __syncthreads();
+  const int nqb = (T + kBW * 32 - 1) / (kBW * 32), nps = nqb * kBW;
+  float* dst = bpart + ((size_t)head * BL * nps + (size_t)seq * nps) * 2 * kDP;
+  if (tid < 2 * kDP) {
+    float s = 0.f;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) s += red[64 * g + tid];
+    dst[tid] = (tid < kDP) ? s * kscale : s;
+  }
+  for (int e = 2 * kDP + tid; e < nps * 2 * kDP; e += NTH) dst[e] = 0.f;
+}
+
 int attn_bwd_parts(int dtype, int B, int T, int L) {  // bias-gradient partial slots per head
   if (dtype == MDG_BF16) return B * L * ((T + kBW * 32 - 1) / (kBW * 32)) * kBW;
   return B * L * ((T + 255) / 256);
@@ -883,7 +1149,7 @@ hipError_t attn_temporal_bwd_launch(int dtype, int B, int T, int L, int H, int D
                                     const void* dout,
                                     const float* lse, const float* rope, int rope_rows, void* dop, float* delta,
                                     void* dqkv, int ldq, float* bpart, float qscale, float kscale, int generic,
-                                    hipStream_t s) {
+                                    float* dqacc, hipStream_t s) {
   const int BL = B * L;
   const size_t nth = (size_t)B * T * L * H;
   dim3 pgrid((unsigned)((nth + 255) / 256));
@@ -895,7 +1161,13 @@ hipError_t attn_temporal_bwd_launch(int dtype, int B, int T, int L, int H, int D
                        (const float*)o_lo, (const float*)dout, (float*)dop, delta);
   }
   if (hipError_t e = hipGetLastError()) return e;
-  if (dtype == MDG_BF16 && !generic) {
+  if (dtype == MDG_BF16 && generic == 0) {  // fused single pass
+    hipLaunchKernelGGL(attn_bwd_fused_bf16_kernel, dim3(H * BL), dim3(kBW * 64), 0, s, (const bf16_t*)qkv_t,
+                       (const bf16_t*)dop, lse, delta, kbias, kvb, rope, rope_rows, (bf16_t*)dqkv, ldq, dqacc, bpart, T,
+                       L, H, D, BL, qscale, kscale);
+    return hipGetLastError();
+  }
+  if (dtype == MDG_BF16 && generic == 2) {  // the two-pass MFMA kernels (dQ; dK / dV)
     const int nblk = (T + kBW * 32 - 1) / (kBW * 32) * H * BL;
     hipLaunchKernelGGL(attn_bwd_dq_bf16_kernel, dim3(nblk), dim3(kBW * 64), 0, s, (const bf16_t*)qkv_t,
                        (const bf16_t*)dop, lse, delta, kbias, kvb, rope, rope_rows, (bf16_t*)dqkv, ldq, bpart, T, L,

@@ -34,7 +34,8 @@ __device__ __forceinline__ int wg_off(int r, int c) { return r * kWgTile + (((c 
 struct WgArgs {
   const void* dy;
   const void* x;
-  float* part;  // [S][M][K] fp32 (S == 1 with direct = true: dW itself)
+  float* part;   // [S][M][K] fp32 (S == 1 with direct = true: dW itself)
+  float* cpart;  // [S][M] fp32 column sums of dY per split (the bias gradient; null: none)
   int N, M, K, ldy, ldx, ldp, chunk;
 };
 
@@ -105,6 +106,11 @@ __global__ __launch_bounds__(kWgThreads, 2) void wgrad_bf16_kernel(const WgArgs 
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[t][u][i] = 0.f;
 
+  // bias gradient: the blocks of the first K tile also sum their dY fragments over the tokens
+  // (waves wk == 0 hold every feature of the M tile once): 8 tokens per lane and k-step, the
+  // two lane halves combined at the end.  No separate column-sum pass over dY.
+  const bool csum = a.cpart != nullptr && blockIdx.y == 0 && wk == 0;
+  float cs[2] = {0.f, 0.f};
   for (int s0 = 0; s0 < kWgStages - 1; ++s0)
     if (s0 < nsteps) issue(s0);
   for (int s = 0; s < nsteps; ++s) {
@@ -128,6 +134,23 @@ __global__ __launch_bounds__(kWgThreads, 2) void wgrad_bf16_kernel(const WgArgs 
       for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int u = 0; u < 2; ++u) acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[t], bfr[u], acc[t][u], 0, 0, 0);
+      if (csum) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          float v = 0.f;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v += (float)af[t][j];
+          cs[t] += v;
+        }
+      }
+    }
+  }
+  if (csum) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const float v = cs[t] + __shfl_xor(cs[t], 32, 64);
+      const int m = m0 + 64 * wm + 32 * t + lane;
+      if (lane < 32 && m < a.M) a.cpart[(size_t)z * a.M + m] = v;
     }
   }
   // D[m][k]: k = lane & 31, m = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
@@ -220,6 +243,31 @@ __global__ __launch_bounds__(256) void colsum_kernel(const CT* __restrict__ dy, 
   }
 }
 
+// dW[m][k] (ld ldo) = sum over z in order of part[z][m][k] (ld K, 4 columns per thread), and in
+// the same launch db[m] = sum over z of cpart[z][m] (the threads past dW's quads)
+__global__ __launch_bounds__(256) void split_sum_wb_kernel(const float* __restrict__ part, int S, int M, int K,
+                                                           float* __restrict__ out, int ldo,
+                                                           const float* __restrict__ cpart, float* __restrict__ db) {
+  const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long nq = (long long)M * (K >> 2);
+  if (e < nq) {
+    const int m = (int)(e / (K >> 2)), k = 4 * (int)(e % (K >> 2));
+    const size_t zs = (size_t)M * K;
+    const float* p = part + (size_t)m * K + k;
+    float4 s = *reinterpret_cast<const float4*>(p);
+    for (int z = 1; z < S; ++z) {
+      const float4 v = *reinterpret_cast<const float4*>(p + z * zs);
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    *reinterpret_cast<float4*>(out + (size_t)m * ldo + k) = s;
+  } else if (db && e - nq < M) {
+    const int m = (int)(e - nq);
+    float s = cpart[m];
+    for (int z = 1; z < S; ++z) s += cpart[(size_t)z * M + m];
+    db[m] = s;
+  }
+}
+
 // out[m][k] (ld ldo) = sum over z in order of part[z][m][k] (ld ldp)
 __global__ __launch_bounds__(256) void split_sum_kernel(const float* __restrict__ part, int S, int M, int K, int ldp,
                                                         float* __restrict__ out, int ldo) {
@@ -253,6 +301,12 @@ WgPlan wgrad_plan(int dtype, int N, int M, int K, bool need_w, bool need_b) {
   p.chunk = ((nq + S - 1) / S) * quantum;
   p.S = (N + p.chunk - 1) / p.chunk;
   p.part_elems = need_w ? (size_t)p.S * M * K : 0;
+  if (need_b && need_w && dtype == MDG_BF16) {  // column sums fused into the wgrad blocks
+    p.cs_chunk = p.chunk;
+    p.cs_S = p.S;
+    p.cs_elems = (size_t)p.S * M;
+    return p;
+  }
   const int cblocks = (M + 511) / 512;
   int cs = need_b ? max(1, min(256 / cblocks, N / 64)) : 0;
   p.cs_chunk = need_b ? (N + cs - 1) / cs : 0;
@@ -264,12 +318,15 @@ WgPlan wgrad_plan(int dtype, int N, int M, int K, bool need_w, bool need_b) {
 hipError_t wgrad_launch(int dtype, int N, int M, int K, const void* dy, int ldy, const void* x, int ldx, float* dw,
                         int lddw, float* db, float* ws, hipStream_t s) {
   const WgPlan p = wgrad_plan(dtype, N, M, K, dw != nullptr, db != nullptr);
+  const bool fused_b = db && dw && dtype == MDG_BF16;
   if (dw) {
     WgArgs a;
     a.dy = dy; a.x = x; a.N = N; a.M = M; a.K = K; a.ldy = ldy; a.ldx = ldx; a.chunk = p.chunk;
     const bool direct = p.S == 1;
     a.part = direct ? dw : ws;
     a.ldp = direct ? lddw : K;
+    float* cp = ws + (p.S > 1 ? p.part_elems : 0);
+    a.cpart = fused_b ? (direct ? db : cp) : nullptr;
     if (dtype == MDG_BF16) {
       static bool attr = false;
       if (!attr) {
@@ -284,12 +341,19 @@ hipError_t wgrad_launch(int dtype, int N, int M, int K, const void* dy, int ldy,
       hipLaunchKernelGGL(wgrad_f32_kernel, dim3((M + 63) / 64, (K + 63) / 64, p.S), dim3(256), 0, s, a);
     }
     if (hipError_t e = hipGetLastError()) return e;
+    if (!direct && fused_b) {
+      const long long n = (long long)M * (K / 4) + M;
+      hipLaunchKernelGGL(split_sum_wb_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, (const float*)ws, p.S,
+                         M, K, dw, lddw, (const float*)cp, db);
+      return hipGetLastError();
+    }
     if (!direct) {
-      const long long n = (long long)M * K;
-      hipLaunchKernelGGL(split_sum_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, (const float*)ws, p.S, M,
-                         K, K, dw, lddw);
+      const long long n = (long long)M * (K / 4);
+      hipLaunchKernelGGL(split_sum_wb_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, (const float*)ws, p.S,
+                         M, K, dw, lddw, nullptr, nullptr);
       if (hipError_t e = hipGetLastError()) return e;
     }
+    if (fused_b) return hipSuccess;  // direct: the kernel wrote db itself
   }
   if (db) {
     float* cp = ws + (p.S > 1 ? p.part_elems : 0);

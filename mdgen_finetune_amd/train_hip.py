@@ -44,6 +44,9 @@ import torch
 from . import _lib
 
 _LN2 = math.log(2.0)
+# temporal attention backward: the fused single-pass kernel (default) or the two-pass MFMA kernels
+# (MDG_ATTN_BWD=2pass, for A/B measurements); see mdg_attn_temporal_bwd's `generic`
+_ATTN_BWD_VARIANT = {"fused": 0, "2pass": 2}[os.environ.get("MDG_ATTN_BWD", "fused")]
 _PLANE_CACHE_MAX = 64  # plane cache entries (layer x tag) before stale ones are dropped
 
 
@@ -358,7 +361,8 @@ class _HipLayerFn(torch.autograd.Function):
                                                      P[f"kvb{i}"].data_ptr(), o.data_ptr(), _lib.ptr(o_lo),
                                                      do.data_ptr(),
                                                      lse.data_ptr(), _lib.ptr(rope), rows, scratch.data_ptr(),
-                                                     dqkv.data_ptr(), 3 * C, bpart.data_ptr(), qscale, _LN2, 0, s),
+                                                     dqkv.data_ptr(), 3 * C, bpart.data_ptr(), qscale, _LN2,
+                                                     _ATTN_BWD_VARIANT, s),
                            "mdg_attn_temporal_bwd")
             else:
                 parts = lib.mdg_attn_spatial_bwd_parts(B * T, L, D)

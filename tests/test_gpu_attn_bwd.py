@@ -81,9 +81,14 @@ def _forward(c, D, T, cos, sin, qscale):
     return o, qn, kr, bk, torch.cat([sb, s], -1)
 
 
-@pytest.mark.parametrize("dtype", ["bf16", "f32"])
-@pytest.mark.parametrize("T,n_pad", [(129, 0), (257, 5), (1000, 17), (300, -1)])
+@pytest.mark.parametrize("dtype", ["bf16", "bf16-2pass", "f32"])
+@pytest.mark.parametrize("T,n_pad", [(129, 0), (257, 5), (1000, 17), (300, -1), (40, 3), (513, 0)])
 def test_temporal_attention_backward_multi_chunk(dtype, T, n_pad):
+    """bf16: the fused single-pass kernel (generic 0: one block per (sequence, head), 256-key
+    passes, 64-query chunks: T = 257 / 300 / 513 / 1000 take 2-4 passes with ragged tails);
+    bf16-2pass: the two-pass MFMA kernels (generic 2); f32: the scalar kernels."""
+    generic = 2 if dtype == "bf16-2pass" else 0
+    dtype = dtype.split("-")[0]
     from mdgen_finetune_amd import _lib
 
     lib = _lib.load()
@@ -137,7 +142,7 @@ def test_temporal_attention_backward_multi_chunk(dtype, T, n_pad):
                                              o_t.data_ptr(), _lib.ptr(lo_t), do_t.data_ptr(), lse_f.data_ptr(),
                                              rope.data_ptr(), T + 1,
                                              scratch.data_ptr(), dqkv.data_ptr(), 3 * C, bpart.data_ptr(), qscale,
-                                             math.log(2.0), 0, _lib.stream_handle()), "mdg_attn_temporal_bwd")
+                                             math.log(2.0), generic, _lib.stream_handle()), "mdg_attn_temporal_bwd")
         torch.cuda.synchronize()
         got = dqkv.double()
         gb = bpart.double().sum(1)
@@ -151,7 +156,8 @@ def test_temporal_attention_backward_multi_chunk(dtype, T, n_pad):
     path = os.environ.get("MDG_PARITY_LOG")
     if path:
         with open(path, "a") as f:
-            f.write(json.dumps({"test": "attn_temporal_bwd", "dtype": dtype, "T": T, "n_pad": n_pad, **errs}) + "\n")
+            f.write(json.dumps({"test": "attn_temporal_bwd", "dtype": dtype, "generic": generic, "T": T, "n_pad": n_pad,
+                                **errs}) + "\n")
     assert torch.isfinite(got).all(), "unwritten or non-finite dq|dk|dv"
     for k, e in errs.items():
         assert e <= tol, (k, e, errs)

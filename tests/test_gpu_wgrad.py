@@ -57,7 +57,9 @@ def test_wgrad_strided_operands_and_bias_only():
     dw, db = wgrad(lib, _lib.MDG_BF16, dy, x, need_b=True)
     assert _rel(dw.double(), dy.double().t() @ x.double()) <= 1e-5
     _, db2 = wgrad(lib, _lib.MDG_BF16, dy, None, need_b=True)
-    assert torch.equal(db, db2)
+    # db rides in the dW blocks when both are asked for, else the column-sum pass: two orders
+    assert _rel(db.double(), db2.double()) <= 1e-6
+    assert _rel(db2.double(), dy.double().sum(0)) <= 1e-5
 
 
 def test_wgrad_rejects_unpadded_bf16_rows():

@@ -22,5 +22,5 @@ with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
     for _ in range(2):
         tr.step([batch])
     torch.cuda.synchronize()
-print(prof.key_averages().table(sort_by="cuda_time_total", row_limit=30, max_name_column_width=60))
+print(prof.key_averages().table(sort_by="self_cuda_time_total", row_limit=60, max_name_column_width=70))
 print(prof.key_averages().table(sort_by="cpu_time_total", row_limit=25, max_name_column_width=60))
