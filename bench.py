@@ -562,6 +562,9 @@ def dopri5_main(a, world, rank, dev, share):
     sampler = Sampler(create_transport(m.args, "GVP", "velocity"))
     fn = sampler.sample_ode()  # dopri5 (parsing.py:102)
     model = functools.partial(m.forward_inference, **kw)
+    from mdgen_finetune_amd.engine import get_engine
+
+    fn.lanes = get_engine(m)._nlanes(B)
     with torch.no_grad():
         for _ in range(max(1, a.warmup)):
             ys = fn(zs, model)
@@ -595,7 +598,22 @@ def dopri5_main(a, world, rank, dev, share):
            "nfe_per_window": nfe, "accepted_steps": [s.accepted for s in stats],
            "rejected_steps": [s.rejected for s in stats],
            "ms_per_evaluation": round(sec / nfe * 1e3, 3),
-           "forward_frames_per_s": round(world * B * T * nfe * a.steps / el, 1)}  # comparable to the Euler line
+           "forward_frames_per_s": round(world * B * T * nfe * a.steps / el, 1),  # comparable to the Euler line
+           "lanes": getattr(fn, "lanes", None)}
+    # the whole window against the MFMA roof: nfe forwards of B trajectories (the conditioning and
+    # the solver's vector arithmetic included in the time, excluded from the FLOPs)
+    sm = step_model(B, T, L, dtype=a.dtype)
+    tf = sm["flops"] * nfe / sec / 1e12
+    out["step_roofline"] = {"unit_of_work": "one dopri5 evaluation = one forward of B trajectories",
+                            "flops_per_evaluation": sm["flops"], "achieved_tflops": round(tf, 1),
+                            "peak_tflops": PEAK_TFLOPS[a.dtype], "mfma_frac": round(tf / PEAK_TFLOPS[a.dtype], 4)}
+    if not a.no_cpu_baseline and world == 1:
+        cpu = cpu_baseline(T, L, a.cpu_seconds)
+        # the oracle's forward rate on the host, priced at this window's measured evaluation count
+        per_eval = T / cpu["value"]  # seconds per B=1 forward (+ Euler update) on the host
+        cpu = dict(cpu, value=round(T / (per_eval * nfe), 2),
+                   sample=cpu["sample"] + f"; dopri5 window = {nfe:.0f} such forwards (this run's NFE)")
+        out["cpu_baseline"] = cpu
     print(json.dumps(out), flush=True)
 
 

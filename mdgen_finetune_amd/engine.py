@@ -480,51 +480,99 @@ class HipEngine:
         return gs.states.clone()
 
     # ------------------------------------------------------------------ adaptive solvers
+    _VF_LANE = 64  # workspace keys of the velocity field's own states (base / mask bias hoisted)
+
     @torch.no_grad()
     def velocity_field(self, x_like, mask=None, start_frames=None, end_frames=None, x_cond=None, x_cond_mask=None,
                        aatype=None, use_graph=True):
         """f(t, y) -> v = model(y, ones(B)·t, **kw) for an adaptive solver (dopri5): t is a
-        device scalar, y a [B,T,L,latent] device tensor.  Everything but (t, y) is staged once;
-        each evaluation is ONE hipGraph replay of [conditioning at t (t-embedding, adaLN, IPA
-        prepend), base embedding, mask bias, mdg_denoise_step] reading t and y from static
-        buffers, so no host sync happens inside an evaluation."""
+        device scalar, y a [B,T,L,latent] device tensor.
+
+        The Euler window's machinery, per evaluation instead of per window:
+          * everything t-independent is computed ONCE here: the base embedding (cond_to_emb +
+            mask_to_emb + pos_embed + biases) and the key-padding biases live in the field's own
+            workspaces (keys _VF_LANE + k, never touched by the Euler sampler or forward);
+          * ``f.precondition(ts)`` runs the t-dependent conditioning (t-embedding, every adaLN
+            row, the IPA prepend) for ALL stage times of an adaptive step in one
+            mdg_precompute_cond call (S rows of t, like the Euler window's 49), and
+            ``f.stage(i, y)`` is evaluation i on those rows — the graphed dopri5 step
+            (integrators.odeint_dopri5_graphed) conditions its 5 new stages at once;
+          * B >= 8 runs as 2 lanes (parallel graph branches on 2 streams, the Euler window's
+            lane split, bit-identical per trajectory to one chain at these shapes).
+        f itself (one evaluation: precondition([t]) + stage 0) is one hipGraph replay per call,
+        with no host sync inside."""
         B, T, L, mask, rots, trans, erots, etrans, aa = self._inputs(x_like, mask, start_frames, end_frames, aatype)
-        st = self._state(B, T, L)
         self._prepare_tps(rots, trans, erots, etrans)
         dev = self.model.device
+        nl = self._nlanes(B)
+        st = self._state(B, T, L, lane=self._VF_LANE)
+        Bl = B // nl
+        lanes = [st] if nl == 1 else [self._state(Bl, T, L, lane=self._VF_LANE + 1 + k) for k in range(nl)]
+        if len(self._lane_streams) < nl:
+            self._lane_streams += [torch.cuda.Stream() for _ in range(nl - len(self._lane_streams))]
         vs = _ShapeState()
         vs.x = torch.empty(B, T, L, self.lat, device=dev)
         vs.v = torch.empty_like(vs.x)
-        vs.t = torch.zeros(1, B, device=dev)
+        vs.t = torch.zeros(1, device=dev)
         vs.mask = mask.clone()
-        vs.graph = None
         for name, val in (("rots", rots), ("trans", trans), ("erots", erots), ("etrans", etrans), ("aatype", aa)):
             self._copy_opt(vs, name, val)
         self._copy_opt(vs, "rel7", self._rel7)
-        vs.has_cond = x_cond is not None
-        if vs.has_cond:
-            self._copy_opt(vs, "x_cond", x_cond.float())
-            self._copy_opt(vs, "x_cond_mask", x_cond_mask.to(torch.int64))
         vs.graph = None
+        vs.ios = []
+        # hoisted, t-independent: base embedding and key-padding biases (per lane workspace)
+        s = _lib.stream_handle()
+        self._base(st, x_cond, x_cond_mask)
+        for k, ls in enumerate(lanes):
+            mk = vs.mask[k * Bl:(k + 1) * Bl]
+            _lib.check(self.lib.mdg_prepare_mask(ctypes.byref(ls.dims), mk.data_ptr(), ls.ws.data_ptr(), s),
+                       "mdg_prepare_mask")
+        rows = Bl * T * L
+
+        def precondition(ts):
+            """Conditioning rows for the stage times ts [S] (device fp32; capturable)."""
+            S = ts.shape[0]
+            t_sb = ts.to(torch.float32).reshape(S, 1).expand(S, B).contiguous()
+            self._rel7 = vs.rel7
+            vs.cond = self.conditioning(t_sb, vs.mask, vs.rots, vs.trans, getattr(vs, "erots", None),
+                                        getattr(vs, "etrans", None), getattr(vs, "aatype", None), nl)
+
+        def stage(i, y):
+            """v for stage i of the last precondition() at y (capturable); returns a new tensor."""
+            vs.x.copy_(y)
+            mods, mods_f, ipa = vs.cond
+            main = torch.cuda.current_stream()
+            if nl == 1:
+                io = self._step_io(st, vs.x.data_ptr(), None, vs.v.data_ptr(),
+                                   None if ipa is None else ipa[i].data_ptr(), mods[i].data_ptr(),
+                                   mods_f[i].data_ptr(), 0.0, alone=True)
+                vs.ios.append(io)
+                _lib.check(self.lib.mdg_denoise_step(ctypes.byref(st.model_struct), ctypes.byref(io),
+                                                     vs.mask.data_ptr(), st.ws.data_ptr(), _lib.stream_handle()),
+                           "mdg_denoise_step")
+            else:
+                for k, ls in enumerate(lanes):
+                    strm = self._lane_streams[k]
+                    strm.wait_stream(main)
+                    io = self._step_io(ls, vs.x[k * Bl].data_ptr(), None, vs.v[k * Bl].data_ptr(),
+                                       None if ipa is None else ipa[i, k * Bl].data_ptr(), mods[k][i].data_ptr(),
+                                       mods_f[i, k * Bl].data_ptr(), 0.0, base=st.base.data_ptr() + k * rows * self.C * 4)
+                    vs.ios.append(io)
+                    _lib.check(self.lib.mdg_denoise_step(ctypes.byref(ls.model_struct), ctypes.byref(io),
+                                                         vs.mask[k * Bl].data_ptr(), ls.ws.data_ptr(),
+                                                         strm.cuda_stream), "mdg_denoise_step(lane)")
+                for k in range(nl):
+                    main.wait_stream(self._lane_streams[k])
+            del vs.ios[:-nl]  # the launches copied their arguments; keep only the latest structs
+            return vs.v.clone()
 
         def program():
-            s = _lib.stream_handle()
-            self._rel7 = vs.rel7
-            mods, mods_f, ipa = self.conditioning(vs.t, vs.mask, vs.rots, vs.trans, getattr(vs, "erots", None),
-                                                  getattr(vs, "etrans", None), getattr(vs, "aatype", None))
-            vs.cond = (mods, mods_f, ipa)
-            self._base(st, vs.x_cond if vs.has_cond else None, vs.x_cond_mask if vs.has_cond else None)
-            _lib.check(self.lib.mdg_prepare_mask(ctypes.byref(st.dims), vs.mask.data_ptr(), st.ws.data_ptr(), s),
-                       "mdg_prepare_mask")
-            vs.io = self._step_io(st, vs.x.data_ptr(), None, vs.v.data_ptr(),
-                                  None if ipa is None else ipa[0].data_ptr(), mods[0].data_ptr(),
-                                  mods_f[0].data_ptr(), 0.0, alone=True)
-            _lib.check(self.lib.mdg_denoise_step(ctypes.byref(st.model_struct), ctypes.byref(vs.io),
-                                                 vs.mask.data_ptr(), st.ws.data_ptr(), s), "mdg_denoise_step")
+            precondition(vs.t)
+            stage(0, vs.x)
 
         def f(t, y):
             vs.x.copy_(y)
-            vs.t.copy_(torch.as_tensor(t, device=dev).float().reshape(1, 1).expand(1, B))
+            vs.t.copy_(torch.as_tensor(t, device=dev).float().reshape(1))
             if vs.graph is not None:
                 vs.graph.replay()
             else:
@@ -538,15 +586,17 @@ class HipEngine:
             return vs.v.clone()
 
         def f_capturable(t, y):
-            """The same evaluation as device work only (no replay, no host read of t): for a
-            caller that captures several evaluations into its own graph (the graphed dopri5)."""
+            """The same evaluation as device work only (no replay, no host read of t)."""
             vs.x.copy_(y)
-            vs.t.copy_(t.to(torch.float32).reshape(1, 1).expand(1, B))
+            vs.t.copy_(t.to(torch.float32).reshape(1))
             program()
             return vs.v.clone()
 
+        f_capturable.precondition = precondition
+        f_capturable.stage = stage
         f.state = vs
         f.capturable = f_capturable
+        f.lanes = nl
         return f
 
     def _copy_opt(self, gs, name, val):

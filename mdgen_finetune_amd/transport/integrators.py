@@ -232,19 +232,27 @@ def odeint_dopri5_graphed(func, y0, t, rtol=1e-3, atol=1e-6, max_num_steps=2 ** 
          "coeffs": [y0.clone() for _ in range(5)], "acc": torch.zeros((), dtype=torch.int64, device=dev),
          "tries": torch.zeros((), dtype=torch.int64, device=dev)}
 
+    # a field that conditions several times at once (HipEngine.velocity_field: t-embedding, adaLN
+    # rows and IPA prepend for all 5 stage times in one call) gets the step's stage times up front
+    pre = getattr(func, "precondition", None)
+
     def step():
         y, fy, t_hi, dt = S["y"], S["fy"], S["t_hi"], S["dt"]
         t1 = t_hi + dt
         dt_y = dt.to(dty)
         ks = [fy]
-        for a_i, b_i in zip(_ALPHA, beta):
-            yi = _combine(y, ks, b_i, dt_y)
+        tts = []
+        for a_i in _ALPHA:
             if a_i == 1.0:
                 tt = t1.to(dty)
-                tt = torch.nextafter(tt, tt - 1)
+                tts.append(torch.nextafter(tt, tt - 1))
             else:
-                tt = (t_hi + a_i * dt).to(dty)
-            ks.append(func(tt, yi))
+                tts.append((t_hi + a_i * dt).to(dty))
+        if pre is not None:
+            pre(torch.stack(tts))
+        for i, b_i in enumerate(beta):
+            yi = _combine(y, ks, b_i, dt_y)
+            ks.append(func.stage(i, yi) if pre is not None else func(tts[i], yi))
         y1 = yi
         err = _combine(None, ks, c_err, dt_y)
         tol = atol + rtol * torch.max(y.abs(), y1.abs())
