@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define MDG_ABI_VERSION 17
+#define MDG_ABI_VERSION 18
 #define MDG_MAX_LAYERS 16
 #define MDG_DP 32      /* padded head dim of the attention operand buffers for head_dim <= 31 */
 #define MDG_DP_WIDE 64 /* ... and for 32 <= head_dim <= 63 (column head_dim of the padded k / v rows
@@ -448,6 +448,34 @@ int mdg_attn_spatial_bwd(int32_t dtype, int32_t n_frames, int32_t L, int32_t H, 
 size_t mdg_wgrad_workspace_bytes(int32_t dtype, int32_t N, int32_t M, int32_t K, int32_t need_dw, int32_t need_db);
 int mdg_wgrad(int32_t dtype, int32_t N, int32_t M, int32_t K, const void* dy, int32_t ldy, const void* x, int32_t ldx,
               float* dw, int32_t lddw, float* db, void* ws, size_t ws_bytes, void* stream);
+
+/* Training backward of the token embedding (latent_model.py:242-255 under loss.backward()),
+   from the residual gradient dh [N][C] fp32 (N = B*T*L tokens, n = (b*T + t)*L + l):
+     dw1 [C][K1]    = sum_n dh[n] x1[n]^T         latent_to_emb.weight (x1 [N][K1], the noised latents)
+     dw2 [C][K2]    = sum_n dh[n] x2[n]^T         cond_to_emb.weight (x2 [N][K2] = x_cond; null: skip)
+     db  [C]        = sum_n dh[n]                 each embedding bias (null: skip)
+     demb [E][C]    = sum_{n: idx[n] = e} dh[n]   mask_to_emb.weight (idx null: skip)
+     dipa [B][L][C] = sum_t dh[b, t, l]           the IPA prepend broadcast over frames (null: skip)
+   fp32; per-chunk partials in ws summed in chunk order (deterministic).  K1, K2 <= 32, E <= 4,
+   L <= 8, C % 128 == 0.  ws: mdg_embed_bwd_workspace_bytes(B, T, L, C, K1, K2, E). */
+size_t mdg_embed_bwd_workspace_bytes(int32_t B, int32_t T, int32_t L, int32_t C, int32_t K1, int32_t K2, int32_t E);
+int mdg_embed_bwd(int32_t B, int32_t T, int32_t L, int32_t C, int32_t K1, const float* x1, int32_t K2, const float* x2,
+                  const int64_t* idx, int32_t E, const float* dh, float* dw1, float* dw2, float* db, float* demb,
+                  float* dipa, void* ws, size_t ws_bytes, void* stream);
+
+/* Training FinalLayer (layers.py:58-75), fp32, C = 384, latent 21 or 28.  Row n belongs to
+   trajectory b = n / rows_per_b; mods [B][2C] = (shift | scale) of its adaLN:
+     fwd: xn = LN(h[n]) (1 + scale) + shift (no-affine LN, eps 1e-6); v[n] = xn w^T + bias
+          (w [latent][C], the nn.Linear weight); stats [N][2] = (mean, rstd) for the backward.
+     bwd: from dv [N][latent]: dh [N][C] (written), and reduced in block order (deterministic)
+          dw [latent][C], dbias [latent] (null: skip), dmods [B][2C] (d shift | d scale).
+   ws: mdg_final_bwd_workspace_bytes(N, rows_per_b, latent). */
+int mdg_final_fwd_train(int32_t N, int32_t rows_per_b, int32_t C, int32_t latent, const float* h, const float* mods,
+                        const float* w, const float* bias, float* v, float* stats, void* stream);
+size_t mdg_final_bwd_workspace_bytes(int32_t N, int32_t rows_per_b, int32_t latent);
+int mdg_final_bwd_train(int32_t N, int32_t rows_per_b, int32_t C, int32_t latent, const float* h, const float* stats,
+                        const float* mods, const float* w, const float* dv, float* dh, float* dw, float* dbias,
+                        float* dmods, void* ws, size_t ws_bytes, void* stream);
 
 /* Invariant point attention core of the IPA prepend under autograd (reference
    src/mdgen/model/ipa.py:92-255, c_z = 0; latent_model.py:179-214), fp32, L <= 32, c = 32,

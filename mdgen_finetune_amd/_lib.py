@@ -165,9 +165,14 @@ SIGNATURES = [
     ("mdg_ipa_core_bwd", _i32, [_i32] * 6 + [_vp] * 8 + [_f32] + [_vp] * 7),
     ("mdg_train_pack_layer", _i32, [ctypes.POINTER(MdgTrainPack), _vp]),
     ("mdg_train_unpack_layer", _i32, [ctypes.POINTER(MdgTrainUnpack), _vp]),
+    ("mdg_embed_bwd_workspace_bytes", ctypes.c_size_t, [_i32] * 7),
+    ("mdg_embed_bwd", _i32, [_i32] * 5 + [_vp, _i32, _vp, _vp, _i32] + [_vp] * 6 + [_vp, ctypes.c_size_t, _vp]),
+    ("mdg_final_fwd_train", _i32, [_i32] * 4 + [_vp] * 7),
+    ("mdg_final_bwd_workspace_bytes", ctypes.c_size_t, [_i32] * 3),
+    ("mdg_final_bwd_train", _i32, [_i32] * 4 + [_vp] * 9 + [_vp, ctypes.c_size_t, _vp]),
 ]
 
-ABI_VERSION = 17
+ABI_VERSION = 18
 _LIB = None
 
 

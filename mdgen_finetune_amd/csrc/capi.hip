@@ -93,6 +93,17 @@ hipError_t ipa_attn_launch(int R, int B, int L, int H, int c, int pq, int pv, co
                            float* out, int ldc, hipStream_t s);
 hipError_t tps_rel7_launch(int B, int L, const float* rots, const float* trans, const float* erots,
                            const float* etrans, float* out, hipStream_t s);
+// train_glue.hip
+size_t embed_bwd_ws_bytes(int B, int T, int L, int C, int K1, int K2, int E);
+hipError_t embed_bwd_launch(int B, int T, int L, int C, int K1, const float* x1, int K2, const float* x2,
+                            const int64_t* idx, int E, const float* dh, float* dw1, float* dw2, float* db, float* demb,
+                            float* dipa, float* ws, hipStream_t s);
+hipError_t final_fwd_train_launch(int N, int rows_per_b, int lat, const float* h, const float* mods, const float* w,
+                                  const float* bias, float* v, float* stats, hipStream_t s);
+size_t final_bwd_ws_bytes(int N, int rows_per_b, int lat);
+hipError_t final_bwd_train_launch(int N, int rows_per_b, int lat, const float* h, const float* stats, const float* mods,
+                                  const float* w, const float* dv, float* dh, float* dw, float* dbias, float* dmods,
+                                  float* ws, hipStream_t s);
 // wgrad.hip
 size_t wgrad_ws_bytes(int dtype, int N, int M, int K, bool need_w, bool need_b);
 hipError_t wgrad_launch(int dtype, int N, int M, int K, const void* dy, int ldy, const void* x, int ldx, float* dw,
@@ -1282,6 +1293,56 @@ int mdg_precompute_cond(const mdg_cond_model* m, const mdg_cond_io* io, void* ws
   if (d.tps)  // x_r + x_f (latent_model.py:211)
     if (int e = hip_check(mdg::add_inplace_launch((size_t)M * C, io->ipa, F(c.x2), s), "ipa add")) return e;
   return MDG_OK;
+}
+
+size_t mdg_embed_bwd_workspace_bytes(int32_t B, int32_t T, int32_t L, int32_t C, int32_t K1, int32_t K2, int32_t E) {
+  if (B <= 0 || T <= 0 || L <= 0 || C <= 0 || K1 <= 0 || K2 < 0 || E < 0) return 0;
+  return mdg::embed_bwd_ws_bytes(B, T, L, C, K1, K2, E);
+}
+
+int mdg_embed_bwd(int32_t B, int32_t T, int32_t L, int32_t C, int32_t K1, const float* x1, int32_t K2, const float* x2,
+                  const int64_t* idx, int32_t E, const float* dh, float* dw1, float* dw2, float* db, float* demb,
+                  float* dipa, void* ws, size_t ws_bytes, void* stream) {
+  if (!x1 || !dh || !ws) return fail(MDG_E_ARG, "embed_bwd: null x1 / dh / ws");
+  if (B <= 0 || T <= 0 || L <= 0 || L > 8 || C <= 0 || C % 128 || K1 <= 0 || K1 > 32 || (x2 && (K2 <= 0 || K2 > 32)) ||
+      (idx && (E <= 0 || E > 4)))
+    return fail(MDG_E_SHAPE, "embed_bwd: B=%d T=%d L=%d C=%d K1=%d K2=%d E=%d (L <= 8, C %% 128, K <= 32, E <= 4)", B, T,
+                L, C, K1, K2, E);
+  const size_t need = mdg::embed_bwd_ws_bytes(B, T, L, C, K1, x2 ? K2 : 0, idx ? E : 0);
+  if (ws_bytes < need) return fail(MDG_E_ARG, "embed_bwd: workspace %zu < %zu bytes", ws_bytes, need);
+  return hip_check(mdg::embed_bwd_launch(B, T, L, C, K1, x1, x2 ? K2 : 0, x2, idx, idx ? E : 0, dh, dw1, dw2, db, demb,
+                                         dipa, (float*)ws, (hipStream_t)stream),
+                   "embed_bwd");
+}
+
+int mdg_final_fwd_train(int32_t N, int32_t rows_per_b, int32_t C, int32_t latent, const float* h, const float* mods,
+                        const float* w, const float* bias, float* v, float* stats, void* stream) {
+  if (!h || !mods || !w || !v || !stats) return fail(MDG_E_ARG, "final_fwd_train: null pointer");
+  if (C != 384 || (latent != 21 && latent != 28) || N <= 0 || rows_per_b <= 0 || N % rows_per_b)
+    return fail(MDG_E_SHAPE, "final_fwd_train: N=%d rows_per_b=%d C=%d latent=%d (C = 384, latent 21 / 28)", N,
+                rows_per_b, C, latent);
+  return hip_check(mdg::final_fwd_train_launch(N, rows_per_b, latent, h, mods, w, bias, v, stats, (hipStream_t)stream),
+                   "final_fwd_train");
+}
+
+size_t mdg_final_bwd_workspace_bytes(int32_t N, int32_t rows_per_b, int32_t latent) {
+  if (N <= 0 || rows_per_b <= 0 || latent <= 0) return 0;
+  return mdg::final_bwd_ws_bytes(N, rows_per_b, latent);
+}
+
+int mdg_final_bwd_train(int32_t N, int32_t rows_per_b, int32_t C, int32_t latent, const float* h, const float* stats,
+                        const float* mods, const float* w, const float* dv, float* dh, float* dw, float* dbias,
+                        float* dmods, void* ws, size_t ws_bytes, void* stream) {
+  if (!h || !stats || !mods || !w || !dv || !dh || !dw || !dmods || !ws)
+    return fail(MDG_E_ARG, "final_bwd_train: null pointer");
+  if (C != 384 || (latent != 21 && latent != 28) || N <= 0 || rows_per_b <= 0 || N % rows_per_b)
+    return fail(MDG_E_SHAPE, "final_bwd_train: N=%d rows_per_b=%d C=%d latent=%d (C = 384, latent 21 / 28)", N,
+                rows_per_b, C, latent);
+  const size_t need = mdg::final_bwd_ws_bytes(N, rows_per_b, latent);
+  if (ws_bytes < need) return fail(MDG_E_ARG, "final_bwd_train: workspace %zu < %zu bytes", ws_bytes, need);
+  return hip_check(mdg::final_bwd_train_launch(N, rows_per_b, latent, h, stats, mods, w, dv, dh, dw, dbias, dmods,
+                                               (float*)ws, (hipStream_t)stream),
+                   "final_bwd_train");
 }
 
 size_t mdg_wgrad_workspace_bytes(int32_t dtype, int32_t N, int32_t M, int32_t K, int32_t need_dw, int32_t need_db) {

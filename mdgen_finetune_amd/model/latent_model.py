@@ -288,26 +288,35 @@ class LatentMDGenModel(nn.Module):
         """Eager PyTorch forward (latent_model.py:216-269) — the training path."""
         if mask.dim() == 2:
             mask = mask.repeat(x.shape[0], 1, 1)
-        h = token_linear(self.latent_to_emb, x)
-        if self.args.abs_pos_emb:
-            h = h + self.pos_embed
-        if getattr(self.args, "abs_time_emb", False):
-            h = h + self.time_embed[:, :, None]
-        if x_cond is not None:
-            emb = (_SmallTableEmbedding.apply(self.mask_to_emb.weight, x_cond_mask) if torch.is_grad_enabled()
-                   else self.mask_to_emb(x_cond_mask))
-            h = h + token_linear(self.cond_to_emb, x_cond) + emb
+        hip_layers = self._use_hip_layers(x)
+        from ..train_hip import glue_supported
+        # the embedding and the FinalLayer on the glue kernels (train_hip.hip_embed / hip_final)
+        glue = hip_layers and glue_supported(self, x.shape[2])
+        if not glue:
+            h = token_linear(self.latent_to_emb, x)
+            if self.args.abs_pos_emb:
+                h = h + self.pos_embed
+            if getattr(self.args, "abs_time_emb", False):
+                h = h + self.time_embed[:, :, None]
+            if x_cond is not None:
+                emb = (_SmallTableEmbedding.apply(self.mask_to_emb.weight, x_cond_mask) if torch.is_grad_enabled()
+                       else self.mask_to_emb(x_cond_mask))
+                h = h + token_linear(self.cond_to_emb, x_cond) + emb
         c = self.embed_time(t)[:, None]
-        hip_layers = self._use_hip_layers(h)
         ckpt = bool(getattr(self.args, "grad_checkpointing", False)) and self.training
         # the HIP training path: every adaLN linear of the model as one stacked GEMM
         ada = self._stacked_adaln(c[:, 0]) if hip_layers else None
+        ipa = None
         if self.args.prepend_ipa:
-            h = h + self.run_ipa(c[:, 0], mask[:, 0], start_frames, end_frames, aatype,
-                                 ada=None if ada is None else ada[0])[:, None]
+            ipa = self.run_ipa(c[:, 0], mask[:, 0], start_frames, end_frames, aatype,
+                               ada=None if ada is None else ada[0])
         if hip_layers:
-            from ..train_hip import hip_layer_forward
+            from ..train_hip import hip_embed, hip_final, hip_layer_forward
             hl = self._train_helper()
+        if glue:
+            h = hip_embed(hl, self, x, x_cond, x_cond_mask, ipa)
+        elif ipa is not None:
+            h = h + ipa[:, None]
         for k, layer in enumerate(self.layers):
             if hip_layers and ckpt:  # --grad_checkpointing: the HIP Function re-runs in backward
                 # (reentrant form: the first forward runs without autograd, so the Function's
@@ -320,6 +329,8 @@ class LatentMDGenModel(nn.Module):
                 h = torch.utils.checkpoint.checkpoint(layer, h, c, mask, use_reentrant=False)
             else:
                 h = layer(h, c, mask)
+        if glue:
+            return hip_final(hl, self.emb_to_latent, h, ada[2])
         return self.emb_to_latent(h, c, mods=None if ada is None else ada[2][:, None])
 
     def _stacked_adaln(self, c0):

@@ -412,3 +412,138 @@ class _HipLayerFn(torch.autograd.Function):
         out += [grads["w1"], grads["b1"], grads["w2"], grads["b2"]]
         del ctx.sv, ctx.P, ctx.lease  # the planes go back to the layer's pool
         return (dh0.reshape(B, T, L, C), dmods, None, None, None, *out)
+
+
+# ------------------------------------------------------------------------------------------
+# The step's glue around the block stack on library kernels (csrc/train_glue.hip): the token
+# embedding (latent_model.py:242-255, forward by mdg_embed, backward by mdg_embed_bwd) and the
+# FinalLayer (layers.py:58-75, mdg_final_fwd_train / mdg_final_bwd_train), fp32 like the
+# reference's parameters.  Each replaces ~20 eager kernels over the [N][C] fp32 residual.
+
+def glue_supported(model, L):
+    """The glue kernels' shapes: C = 384 (the FinalLayer kernels' row layout), L <= 8, latent 21 / 28;
+    MDG_TRAIN_GLUE=0 keeps the eager embedding / FinalLayer (A/B)."""
+    if os.environ.get("MDG_TRAIN_GLUE", "1") == "0":
+        return False
+    return model.args.embed_dim == 384 and L <= 8 and model.latent_dim in (21, 28)
+
+
+class _HipEmbedFn(torch.autograd.Function):
+    """h = latent_to_emb(x) + pos_embed + cond_to_emb(x_cond) + mask_to_emb[x_cond_mask]
+    + ipa[b, l] (the IPA prepend broadcast over frames).  x / x_cond / the mask carry no
+    gradient (the noised latents and the conditioning); ipa, both linears and the mask table do."""
+
+    @staticmethod
+    def forward(ctx, x, xc, idx, ipa, w1, b1, w2, b2, memb, pos, hl):
+        lib, s = hl.lib, _lib.stream_handle()
+        B, T, L, K1 = x.shape
+        C, N = w1.shape[0], B * T * L
+        x = x.detach().float().contiguous()
+        dev = x.device
+        out = torch.empty(N, C, device=dev)
+        ipa_c = ipa.detach().float().contiguous() if ipa is not None else None
+        pos_c = pos.detach().float().contiguous() if pos is not None else None
+        w1t = w1.detach().t().contiguous()
+        if xc is not None:
+            xc = xc.detach().float().contiguous()
+            idx = idx.to(torch.int64).contiguous()
+            base = torch.empty(N, C, device=dev)
+            bsum = (b1.detach() + b2.detach()).contiguous()
+            _lib.check(lib.mdg_embed(N, T, L, C, xc.shape[-1], xc.data_ptr(), w2.detach().t().contiguous().data_ptr(),
+                                     bsum.data_ptr(), None, _lib.ptr(pos_c), memb.detach().contiguous().data_ptr(),
+                                     idx.data_ptr(), None, base.data_ptr(), s), "mdg_embed(cond)")
+            _lib.check(lib.mdg_embed(N, T, L, C, K1, x.data_ptr(), w1t.data_ptr(), None, base.data_ptr(), None, None,
+                                     None, _lib.ptr(ipa_c), out.data_ptr(), s), "mdg_embed(latent)")
+        else:
+            _lib.check(lib.mdg_embed(N, T, L, C, K1, x.data_ptr(), w1t.data_ptr(), b1.detach().contiguous().data_ptr(),
+                                     None, _lib.ptr(pos_c), None, None, _lib.ptr(ipa_c), out.data_ptr(), s),
+                       "mdg_embed(latent)")
+        ctx.save_for_backward(x, xc, idx)
+        ctx.hl, ctx.shape, ctx.E = hl, (B, T, L, C), memb.shape[0]
+        ctx.has_ipa, ctx.has_cond = ipa is not None, xc is not None
+        return out.view(B, T, L, C)
+
+    @staticmethod
+    def backward(ctx, dh):
+        x, xc, idx = ctx.saved_tensors
+        hl = ctx.hl
+        lib = hl.lib
+        B, T, L, C = ctx.shape
+        dev = dh.device
+        dh = dh.float().contiguous()
+        K1 = x.shape[-1]
+        K2 = xc.shape[-1] if xc is not None else 0
+        E = ctx.E if ctx.has_cond else 0
+        dw1 = torch.empty(C, K1, device=dev)
+        db = torch.empty(C, device=dev)
+        dw2 = torch.empty(C, K2, device=dev) if ctx.has_cond else None
+        demb = torch.empty(E, C, device=dev) if ctx.has_cond else None
+        dipa = torch.empty(B, L, C, device=dev) if ctx.has_ipa else None
+        wsb = lib.mdg_embed_bwd_workspace_bytes(B, T, L, C, K1, K2, E)
+        ws = torch.empty(wsb, device=dev, dtype=torch.uint8)
+        _lib.check(lib.mdg_embed_bwd(B, T, L, C, K1, x.data_ptr(), K2, _lib.ptr(xc), _lib.ptr(idx), E, dh.data_ptr(),
+                                     dw1.data_ptr(), _lib.ptr(dw2), db.data_ptr(), _lib.ptr(demb), _lib.ptr(dipa),
+                                     ws.data_ptr(), wsb, _lib.stream_handle()), "mdg_embed_bwd")
+        return (None, None, None, dipa, dw1, db, dw2, db if ctx.has_cond else None, demb, None, None)
+
+
+def hip_embed(hl, model, x, x_cond, x_cond_mask, ipa):
+    """The model's token embedding + IPA prepend on the glue kernels (latent_model.py:242-255);
+    x [B,T,L,lat], ipa [B,L,C] or None."""
+    m = model
+    pos = m.pos_embed[0] if m.args.abs_pos_emb else None
+    if x_cond is not None:
+        h = _HipEmbedFn.apply(x, x_cond, x_cond_mask, ipa, m.latent_to_emb.weight, m.latent_to_emb.bias,
+                              m.cond_to_emb.weight, m.cond_to_emb.bias, m.mask_to_emb.weight, pos, hl)
+    else:
+        h = _HipEmbedFn.apply(x, None, None, ipa, m.latent_to_emb.weight, m.latent_to_emb.bias, None, None,
+                              m.mask_to_emb.weight, pos, hl)
+    if getattr(m.args, "abs_time_emb", False):
+        h = h + m.time_embed[:, :, None]
+    return h
+
+
+class _HipFinalFn(torch.autograd.Function):
+    """FinalLayer: LN(h) * (1 + scale) + shift -> Linear(C, latent), mods [B, 2C] = shift | scale."""
+
+    @staticmethod
+    def forward(ctx, h, mods, w, b, hl):
+        lib = hl.lib
+        B, T, L, C = h.shape
+        N, lat = B * T * L, w.shape[0]
+        h = h.detach().float().contiguous()
+        mods = mods.detach().float().contiguous()
+        w = w.detach().float().contiguous()
+        v = torch.empty(N, lat, device=h.device)
+        stats = torch.empty(N, 2, device=h.device)
+        _lib.check(lib.mdg_final_fwd_train(N, T * L, C, lat, h.data_ptr(), mods.data_ptr(), w.data_ptr(),
+                                           b.detach().contiguous().data_ptr(), v.data_ptr(), stats.data_ptr(),
+                                           _lib.stream_handle()), "mdg_final_fwd_train")
+        ctx.save_for_backward(h, stats, mods, w)
+        ctx.hl = hl
+        return v.view(B, T, L, lat)
+
+    @staticmethod
+    def backward(ctx, dv):
+        h, stats, mods, w = ctx.saved_tensors
+        lib = ctx.hl.lib
+        B, T, L, C = h.shape
+        N, lat = B * T * L, w.shape[0]
+        dev = h.device
+        dv = dv.float().contiguous()
+        dh = torch.empty_like(h)
+        dw = torch.empty(lat, C, device=dev)
+        db = torch.empty(lat, device=dev)
+        dmods = torch.empty(B, 2 * C, device=dev)
+        wsb = lib.mdg_final_bwd_workspace_bytes(N, T * L, lat)
+        ws = torch.empty(wsb, device=dev, dtype=torch.uint8)
+        _lib.check(lib.mdg_final_bwd_train(N, T * L, C, lat, h.data_ptr(), stats.data_ptr(), mods.data_ptr(),
+                                           w.data_ptr(), dv.data_ptr(), dh.data_ptr(), dw.data_ptr(), db.data_ptr(),
+                                           dmods.data_ptr(), ws.data_ptr(), wsb, _lib.stream_handle()),
+                   "mdg_final_bwd_train")
+        return dh, dmods, dw, db, None
+
+
+def hip_final(hl, final_layer, h, mods):
+    """FinalLayer (layers.py:58-75) on the glue kernels; mods [B, 2C] (the stacked adaLN rows)."""
+    return _HipFinalFn.apply(h, mods, final_layer.linear.weight, final_layer.linear.bias, hl)

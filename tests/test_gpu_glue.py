@@ -1,0 +1,93 @@
+"""The training step's glue kernels (csrc/train_glue.hip, train_hip.hip_embed / hip_final)
+against eager fp32 autograd of the same ops: the token embedding + IPA prepend broadcast
+(latent_model.py:242-255) and the FinalLayer (layers.py:58-75), forward values and every
+gradient, at the training step's shape (C = 384, L = 4, latent 21) and the TPS latent (28),
+with frame counts that leave ragged chunks.  Tolerance: fp32 reduction order only,
+||d|| / ||ref|| <= 2e-6 (forward) and 1e-5 (gradients)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    from mdgen_finetune_amd import _lib
+
+    _lib.load()
+
+
+def _rel(a, b):
+    return float((a.double() - b.double()).norm() / b.double().norm().clamp_min(1e-30))
+
+
+class _Hl:
+    def __init__(self):
+        from mdgen_finetune_amd import _lib
+
+        self.lib = _lib.load()
+
+
+@pytest.mark.parametrize("B,T,lat,cond,ipa", [(2, 70, 21, True, True), (3, 33, 28, True, True), (1, 32, 21, False, True),
+                                             (2, 5, 21, True, False)])
+def test_embed_forward_and_backward_match_eager(B, T, lat, cond, ipa):
+    from mdgen_finetune_amd.train_hip import _HipEmbedFn
+
+    torch.manual_seed(B * 100 + T)
+    L, C, dev = 4, 384, "cuda"
+    x = torch.randn(B, T, L, lat, device=dev)
+    xc = torch.randn(B, T, L, lat, device=dev) if cond else None
+    idx = torch.randint(0, 2, (B, T, L), device=dev) if cond else None
+    p = {k: torch.randn(*s, device=dev, requires_grad=True) * 0.3 for k, s in
+         dict(w1=(C, lat), b1=(C,), w2=(C, lat), b2=(C,), memb=(2, C), ipa=(B, L, C)).items()}
+    for v in p.values():
+        v.retain_grad()
+    pos = torch.randn(L, C, device=dev)
+    g = torch.randn(B, T, L, C, device=dev)
+    ipa_t = p["ipa"] if ipa else None
+    h = _HipEmbedFn.apply(x, xc, idx, ipa_t, p["w1"], p["b1"], p["w2"] if cond else None, p["b2"] if cond else None,
+                          p["memb"], pos, _Hl())
+    (h * g).sum().backward()
+    got = {k: v.grad.clone() for k, v in p.items() if v.grad is not None}
+    for v in p.values():
+        v.grad = None
+    ref = x @ p["w1"].t() + p["b1"] + pos
+    if cond:
+        ref = ref + (xc @ p["w2"].t() + p["b2"] + p["memb"][idx])
+    if ipa:
+        ref = ref + p["ipa"][:, None]
+    (ref * g).sum().backward()
+    assert _rel(h, ref) <= 2e-6, _rel(h, ref)
+    for k, v in p.items():
+        if v.grad is None:
+            assert k not in got or (not cond and k in ("w2", "b2")) or (not ipa and k == "ipa"), k
+            continue
+        assert k in got, k
+        assert _rel(got[k], v.grad) <= 1e-5, (k, _rel(got[k], v.grad))
+
+
+@pytest.mark.parametrize("B,T,lat", [(2, 70, 21), (3, 33, 28), (1, 1000, 21)])
+def test_final_layer_forward_and_backward_match_eager(B, T, lat):
+    from mdgen_finetune_amd.train_hip import _HipFinalFn
+
+    torch.manual_seed(T + lat)
+    L, C, dev = 4, 384, "cuda"
+    h = (torch.randn(B, T, L, C, device=dev) * 2 + 0.5).requires_grad_(True)
+    mods = (torch.randn(B, 2 * C, device=dev) * 0.2).requires_grad_(True)
+    w = (torch.randn(lat, C, device=dev) * 0.05).requires_grad_(True)
+    b = (torch.randn(lat, device=dev) * 0.1).requires_grad_(True)
+    dv = torch.randn(B, T, L, lat, device=dev)
+    v = _HipFinalFn.apply(h, mods, w, b, _Hl())
+    (v * dv).sum().backward()
+    got = [t.grad.clone() for t in (h, mods, w, b)]
+    for t in (h, mods, w, b):
+        t.grad = None
+    shift, scale = mods.chunk(2, -1)
+    xn = torch.nn.functional.layer_norm(h, (C,), eps=1e-6) * (1 + scale[:, None, None]) + shift[:, None, None]
+    ref = xn @ w.t() + b
+    (ref * dv).sum().backward()
+    assert _rel(v, ref) <= 2e-6, _rel(v, ref)
+    for name, a, t in zip(("h", "mods", "w", "b"), got, (h, mods, w, b)):
+        assert _rel(a, t.grad) <= 1e-5, (name, _rel(a, t.grad))

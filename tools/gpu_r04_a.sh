@@ -5,7 +5,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 bash tools/gpu_steps.sh \
-  "kern_tests|300|python -u -m pytest -x -v --timeout 200 --timeout-method thread -p no:cacheprovider tests/test_gpu_attn_bwd.py tests/test_gpu_wgrad.py tests/test_gpu_parity.py -k \"bwd or wgrad or dopri5\"" \
+  "kern_tests|300|python -u -m pytest -x -v --timeout 200 --timeout-method thread -p no:cacheprovider tests/test_gpu_attn_bwd.py tests/test_gpu_wgrad.py tests/test_gpu_glue.py tests/test_gpu_parity.py -k \"bwd or wgrad or dopri5 or embed or final_layer\"" \
   "attn_bwd_bench|120|python tools/attn_bwd_bench.py > gpurun_out/attn_bwd_bench.json" \
   "rccl_test|300|python -u -m pytest -x -v --timeout 200 --timeout-method thread -p no:cacheprovider tests/test_gpu_train.py -k rccl" \
   "smoke|300|python -c 'import __graft_entry__ as g; g.smoke()'" \
