@@ -939,6 +939,7 @@ __global__ __launch_bounds__(kBW * 64, 2) void attn_bwd_fused_bf16_kernel(
   __shared__ __attribute__((aligned(16))) bf16_t dsT[KB * kFQC];
   __shared__ __attribute__((aligned(16))) bf16_t Kim[KB * kDP];
   __shared__ float dsbs[kFQC], pbs[kFQC];
+  __shared__ float bkv[2 * kDP];  // bias_k | bias_v row of this head (loop-invariant: LDS, not VGPRs)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
   const int wg = xcd_remap(H * BL);
   const int head = wg % H, seq = wg / H, sh = seq * H + head;
@@ -950,8 +951,9 @@ __global__ __launch_bounds__(kBW * 64, 2) void attn_bwd_fused_bf16_kernel(
   const float* lg = lse + (size_t)sh * T;
   const float* dg = delta + (size_t)sh * T;
   const float* kbg = kbias + (size_t)seq * T;
-  const float* bk = kvb + head * 2 * kDP;
-  const float* bv = bk + kDP;
+  if (tid < 2 * kDP) bkv[tid] = kvb[head * 2 * kDP + tid];  // visible after the first barrier
+  const float* bk = bkv;
+  const float* bv = bkv + kDP;
   float* acc_g = dqacc + (size_t)sh * T * kDP;
   const int nkb = (T + KB - 1) / KB, nch = (T + kFQC - 1) / kFQC;
   const int b = seq / L, l = seq % L, half = D >> 1, C = H * D;
@@ -981,8 +983,10 @@ __global__ __launch_bounds__(kBW * 64, 2) void attn_bwd_fused_bf16_kernel(
   const int bgd = tid & 31, bgw = (tid >> 5) & 1, bqs = tid >> 6;
   float bacc = 0.f;
 
-  for (int kb = 0; kb < nkb; ++kb) {
-    const bool last = kb == nkb - 1;
+  // one 256-key pass; LAST (the final pass: dQ finalised, bias gradients) as a compile-time
+  // flag so the other passes carry none of its registers
+  auto key_pass = [&](const int kb, auto last_tag) {
+    constexpr bool last = decltype(last_tag)::value;
     const int key = kb * KB + wave * 32 + r;
     const bool live = key < T;
     bf16x8 kf[2], vf[2];
@@ -1122,7 +1126,9 @@ __global__ __launch_bounds__(kBW * 64, 2) void attn_bwd_fused_bf16_kernel(
         }
       }
     }
-  }
+  };
+  for (int kb = 0; kb + 1 < nkb; ++kb) key_pass(kb, std::false_type{});
+  key_pass(nkb - 1, std::true_type{});
   // bias partials: the 8 query groups of each (dim, gk / gv) summed in order; the sequence's
   // first slot of the two-pass kernels' layout gets the block total, its other slots zero
   float* red = reinterpret_cast<float*>(dsT);

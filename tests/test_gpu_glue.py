@@ -40,10 +40,8 @@ def test_embed_forward_and_backward_match_eager(B, T, lat, cond, ipa):
     x = torch.randn(B, T, L, lat, device=dev)
     xc = torch.randn(B, T, L, lat, device=dev) if cond else None
     idx = torch.randint(0, 2, (B, T, L), device=dev) if cond else None
-    p = {k: torch.randn(*s, device=dev, requires_grad=True) * 0.3 for k, s in
+    p = {k: (torch.randn(*s, device=dev) * 0.3).requires_grad_(True) for k, s in
          dict(w1=(C, lat), b1=(C,), w2=(C, lat), b2=(C,), memb=(2, C), ipa=(B, L, C)).items()}
-    for v in p.values():
-        v.retain_grad()
     pos = torch.randn(L, C, device=dev)
     g = torch.randn(B, T, L, C, device=dev)
     ipa_t = p["ipa"] if ipa else None
