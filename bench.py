@@ -542,8 +542,15 @@ def train_main(a, world, rank, dev, share):
         out["allreduce_buckets"] = {"n": len(red.buckets), "bytes": [int(sl.numel() * 4) for sl in red.slices],
                                     "launched_after_grads": [n for _, n in red.launch_log],
                                     "grads_total": sum(len(b) for b in red.buckets)}
-        torch.distributed.destroy_process_group()
     print(json.dumps(out), flush=True)
+    if rehearse:  # the graph holding the captured collectives goes before the communicator
+        tr._graphed = None
+        del tr
+        import gc
+
+        gc.collect()
+        torch.cuda.synchronize()
+        torch.distributed.destroy_process_group()
 
 
 def dopri5_main(a, world, rank, dev, share):

@@ -468,6 +468,13 @@ def main(argv=None):
         print(json.dumps({"done": True, "steps": tr.global_step, "wall_s": round(time.time() - t0, 2)}), flush=True)
     if world > 1:
         dist.barrier()
+        # the captured step's graph holds RCCL collectives: release it before the communicator
+        tr._graphed = None
+        import gc
+
+        gc.collect()
+        if device.type == "cuda":
+            torch.cuda.synchronize()
         dist.destroy_process_group()
 
 

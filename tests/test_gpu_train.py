@@ -551,6 +551,42 @@ def test_tps_ipa_long_crop_grads_match_eager(L):
     assert any(n.startswith("ipa_layers.") and "mha_l" in n for n in grads["hip"])
 
 
+def _rccl_world1_worker(rank, port, out):
+    """The body of test_graphed_step_rccl_bucket_allreduce_in_capture_world1 in a child process:
+    the RCCL communicator and the graphs that captured its collectives die with the child
+    (os._exit after the results are handed over) instead of being torn down in the test runner."""
+    import os
+
+    import torch.distributed as dist
+
+    from mdgen_finetune_amd.train import Trainer
+
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    res = {}
+    info = {}
+    for mode in ("plain", "rccl"):
+        a = _args(["--lr", "1e-3", "--embed_dim", "192", "--mha_heads", "8", "--ema", "--train_graph", "1",
+                   "--bucket_cap_mb", "0.5"])
+        tr = Trainer(a, device=torch.device("cuda"))
+        tr.force_allreduce = mode == "rccl"
+        b = _batch(a, B=2)
+        _fixed_noise(tr, 2, (2, a.num_frames, a.crop, 21))
+        losses = [float(tr.step([b], log=False)[0]) for _ in range(2)]
+        g = tr._graphed
+        if mode == "rccl":
+            red = g.reducer
+            info = {"overlap": bool(g.overlap), "has_g2": hasattr(g, "g2"), "buckets": len(red.buckets),
+                    "log": list(red.launch_log), "grads": sum(len(bk) for bk in red.buckets),
+                    "views": all(p.grad is None or p.grad.data_ptr() == red.views[i].data_ptr()
+                                 for i, p in enumerate(g.params) if i in red.views)}
+        st = _trainer_state(tr)
+        res[mode] = (losses, [t.cpu() for t in st])
+        torch.cuda.synchronize()
+    out["res"], out["info"] = res, info
+    os._exit(0)
+
+
 def test_graphed_step_rccl_bucket_allreduce_in_capture_world1():
     """The graphed step's gradient all-reduce captured INSIDE the graph (grad_buckets.py): a world-1
     RCCL group (a one-GPU box cannot hold two RCCL ranks) with the reduction forced on.  The step
@@ -560,40 +596,23 @@ def test_graphed_step_rccl_bucket_allreduce_in_capture_world1():
     the last gradient lands.  (Timeline of the captured collectives: tools/rccl_overlap_trace.py.)"""
     import socket
 
-    import torch.distributed as dist
-
-    from mdgen_finetune_amd.train import Trainer
+    import torch.multiprocessing as mp
 
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
-    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
-                            device_id=torch.device("cuda", 0))
-    try:
-        res = {}
-        for mode in ("plain", "rccl"):
-            a = _args(["--lr", "1e-3", "--embed_dim", "192", "--mha_heads", "8", "--ema", "--train_graph", "1",
-                       "--bucket_cap_mb", "0.5"])
-            tr = Trainer(a, device=torch.device("cuda"))
-            tr.force_allreduce = mode == "rccl"
-            b = _batch(a, B=2)
-            _fixed_noise(tr, 2, (2, a.num_frames, a.crop, 21))
-            losses = [float(tr.step([b], log=False)[0]) for _ in range(2)]
-            g = tr._graphed
-            if mode == "rccl":
-                assert g.overlap and not hasattr(g, "g2")
-                red = g.reducer
-                assert len(red.buckets) >= 3, len(red.buckets)
-                assert [bi for bi, _ in red.launch_log] == list(range(len(red.buckets)))
-                assert red.launch_log[0][1] < sum(len(bk) for bk in red.buckets)
-                assert all(p.grad is None or p.grad.data_ptr() == red.views[i].data_ptr()
-                           for i, p in enumerate(g.params) if i in red.views)
-            res[mode] = (losses, _trainer_state(tr))
-        (l0, s0), (l1, s1) = res["plain"], res["rccl"]
-        assert l0 == l1, (l0, l1)
-        for i, what in enumerate(("params", "ema", "adam")):
-            d = float((s0[i] - s1[i]).abs().max())
-            assert d <= 1e-6 * max(1.0, float(s0[i].abs().max())), (what, d)
-    finally:
-        dist.destroy_process_group()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_rccl_world1_worker, args=(port, out), nprocs=1, join=True)
+    info = out["info"]
+    assert info["overlap"] and not info["has_g2"], info
+    assert info["buckets"] >= 3, info
+    assert [bi for bi, _ in info["log"]] == list(range(info["buckets"])), info
+    assert info["log"][0][1] < info["grads"], info
+    assert info["views"]
+    (l0, s0), (l1, s1) = out["res"]["plain"], out["res"]["rccl"]
+    assert l0 == l1, (l0, l1)
+    for i, what in enumerate(("params", "ema", "adam")):
+        d = float((s0[i] - s1[i]).abs().max())
+        assert d <= 1e-6 * max(1.0, float(s0[i].abs().max())), (what, d)
