@@ -34,8 +34,9 @@
 extern "C" {
 #endif
 
-#define MDG_ABI_VERSION 18
+#define MDG_ABI_VERSION 19
 #define MDG_MAX_LAYERS 16
+#define MDG_SEG_MAX 16 /* segments of one mdg_seg_linear */
 #define MDG_DP 32      /* padded head dim of the attention operand buffers for head_dim <= 31 */
 #define MDG_DP_WIDE 64 /* ... and for 32 <= head_dim <= 63 (column head_dim of the padded k / v rows
                           carries the softmax offset / row sum, so it must exist) */
@@ -449,6 +450,38 @@ size_t mdg_wgrad_workspace_bytes(int32_t dtype, int32_t N, int32_t M, int32_t K,
 int mdg_wgrad(int32_t dtype, int32_t N, int32_t M, int32_t K, const void* dy, int32_t ldy, const void* x, int32_t ldx,
               float* dw, int32_t lddw, float* db, void* ws, size_t ws_bytes, void* stream);
 
+/* Few-row fp32 linears of the training step's conditioning (the TimestepEmbedder MLP,
+   layers.py:17-55; every adaLN_modulation Linear of the model, latent_model.py:341-493 and
+   layers.py:58-75; the IPA projections and linear_out, ipa.py:92-250), forward and backward,
+   for nseg nn.Linear layers that share one input x [M][K] (ld ldx): segment i has n[i] output
+   features, weight w[i] [n[i]][K] (nn.Linear layout), bias b[i] [n[i]] (null: none).
+   in_act MDG_ACT_NONE: x' = x; MDG_ACT_SILU: x' = SiLU(x) (the adaLN / t-MLP nn.SiLU in front).
+     fwd: y[i][m][j] = resid[i][m][j] (if non-null, ld ldr[i]) + b[i][j] + sum_k x'[m][k] w[i][j][k]
+          (y ld ldy[i]; exact fp32 FMAs in ascending k).
+     bwd: from dy[i] [M][lddy[i]]: dw[i] [n[i]][K] = dy^T x', db[i] = column sums of dy (either
+          null: skip), and dx [M][lddx] = (sum_i dy[i] w[i]) * SiLU'(x) for SILU (null: skip),
+          the weight-row reduction split into chunks of 256 rows whose partials (in ws) are
+          summed in chunk order (deterministic).  ws: mdg_seg_linear_bwd_workspace_bytes. */
+typedef struct {
+  int32_t nseg;
+  int32_t n[MDG_SEG_MAX];
+  const float* w[MDG_SEG_MAX];
+  const float* b[MDG_SEG_MAX];
+  float* y[MDG_SEG_MAX];
+  int32_t ldy[MDG_SEG_MAX];
+  const float* resid[MDG_SEG_MAX];
+  int32_t ldr[MDG_SEG_MAX];
+  const float* dy[MDG_SEG_MAX];
+  int32_t lddy[MDG_SEG_MAX];
+  float* dw[MDG_SEG_MAX];
+  float* db[MDG_SEG_MAX];
+} mdg_seg_linear;
+int mdg_seg_linear_fwd(int32_t M, int32_t K, const float* x, int32_t ldx, int32_t in_act, const mdg_seg_linear* s,
+                       void* stream);
+size_t mdg_seg_linear_bwd_workspace_bytes(int32_t M, int32_t K, const mdg_seg_linear* s);
+int mdg_seg_linear_bwd(int32_t M, int32_t K, const float* x, int32_t ldx, int32_t in_act, const mdg_seg_linear* s,
+                       float* dx, int32_t lddx, void* ws, size_t ws_bytes, void* stream);
+
 /* Training backward of the token embedding (latent_model.py:242-255 under loss.backward()),
    from the residual gradient dh [N][C] fp32 (N = B*T*L tokens, n = (b*T + t)*L + l):
      dw1 [C][K1]    = sum_n dh[n] x1[n]^T         latent_to_emb.weight (x1 [N][K1], the noised latents)
@@ -480,20 +513,27 @@ int mdg_final_bwd_train(int32_t N, int32_t rows_per_b, int32_t C, int32_t latent
 /* Invariant point attention core of the IPA prepend under autograd (reference
    src/mdgen/model/ipa.py:92-255, c_z = 0; latent_model.py:179-214), fp32, L <= 32, c = 32,
    8 query/key points and 8 value points (the reference's defaults; other shapes: MDG_E_SHAPE).
-   Operands per token b*L + i, head h:  q [..][H][c], kv [..][H][2c] (k | v), qp [..][H][Pq][3]
-   and kvp [..][H][Pq + Pv][3] (points already in the global frame), mask [B][L], rots
-   [B][L][3][3], trans [B][L][3], hw [H] = softplus(head_weights) * sqrt(1 / (3 Pq 9/2)),
-   wc = sqrt(1 / (3c)).
+   Operands per token b*L + i, head h:  q [..][H][c], kv [..][H][2c] (k | v), mask [B][L], rots
+   [B][L][3][3], trans [B][L][3], wc = sqrt(1 / (3c)); the points and head weights by `flags`:
+     0: qp [..][H][Pq][3] and kvp [..][H][Pq + Pv][3] already in the global frame, hw [H] =
+        softplus(head_weights) * sqrt(1 / (3 Pq 9/2));
+     MDG_IPA_LOCAL_POINTS: qp [..][3][H*Pq] and kvp [..][3][H*(Pq + Pv)], the raw linear_q_points /
+        linear_kv_points rows (x | y | z blocks, point h*P + p: ipa.py:121-140), in the residue's
+        local frame; the kernel applies R p + t (rigid_utils.py:64-86) and the backward returns
+        d raw = R^T d global in the same layout;
+     MDG_IPA_RAW_HW: hw [H] is the raw head_weights parameter (softplus taken in the kernel),
+        and dhw_part is the gradient w.r.t. it.
    fwd: out [B*L][H*c + 4*H*Pv] = [o | ol_x | ol_y | ol_z | |ol|], the linear_out input.
-   bwd: from dout (same layout): dq, dkv, dqp, dkvp (same layouts as the operands) and
-   dhw_part [B][H] (sum over B = d hw). */
+   bwd: from dout (same layout): dq, dkv, dqp, dkvp (the operands' layouts) and dhw_part [B][H]
+   (sum over B = d hw). */
+enum { MDG_IPA_LOCAL_POINTS = 1, MDG_IPA_RAW_HW = 2 };
 int mdg_ipa_core_fwd(int32_t B, int32_t L, int32_t H, int32_t c, int32_t Pq, int32_t Pv, const float* q,
                      const float* kv, const float* qp, const float* kvp, const float* mask, const float* rots,
-                     const float* trans, const float* hw, float wc, float* out, void* stream);
+                     const float* trans, const float* hw, float wc, float* out, int32_t flags, void* stream);
 int mdg_ipa_core_bwd(int32_t B, int32_t L, int32_t H, int32_t c, int32_t Pq, int32_t Pv, const float* q,
                      const float* kv, const float* qp, const float* kvp, const float* mask, const float* rots,
                      const float* trans, const float* hw, float wc, const float* dout, float* dq, float* dkv,
-                     float* dqp, float* dkvp, float* dhw_part, void* stream);
+                     float* dqp, float* dkvp, float* dhw_part, int32_t flags, void* stream);
 
 /* Per-step weight packing / gradient unpacking of one training layer (train_hip._HipLayerFn;
    latent_model.py:456-493 parameters, mha.py:245-247 projections, fair-esm RoPE of bias_k at

@@ -22,6 +22,8 @@ MDG_ACT_NONE, MDG_ACT_GELU, MDG_ACT_SILU, MDG_ACT_DGELU = 0, 1, 2, 3
 MDG_QKV_SPATIAL, MDG_QKV_TEMPORAL, MDG_QKV_TEMPORAL_PACKED = 0, 1, 2
 MDG_PREP_TPS, MDG_PREP_NO_OFFSETS, MDG_PREP_COND_FIRST, MDG_PREP_COND_LAST = 1, 2, 4, 8
 MDG_MAX_LAYERS = 16
+MDG_SEG_MAX = 16
+MDG_IPA_LOCAL_POINTS, MDG_IPA_RAW_HW = 1, 2
 MDG_DP = 32
 MDG_DP_WIDE = 64
 
@@ -117,6 +119,13 @@ class MdgTrainUnpack(ctypes.Structure):
         ("dmods", _vp), ("gbo", _vp * 2), ("gb2", _vp)]
 
 
+class MdgSegLinear(ctypes.Structure):
+    _fields_ = [("nseg", _i32), ("n", _i32 * MDG_SEG_MAX), ("w", _vp * MDG_SEG_MAX), ("b", _vp * MDG_SEG_MAX),
+                ("y", _vp * MDG_SEG_MAX), ("ldy", _i32 * MDG_SEG_MAX), ("resid", _vp * MDG_SEG_MAX),
+                ("ldr", _i32 * MDG_SEG_MAX), ("dy", _vp * MDG_SEG_MAX), ("lddy", _i32 * MDG_SEG_MAX),
+                ("dw", _vp * MDG_SEG_MAX), ("db", _vp * MDG_SEG_MAX)]
+
+
 # (name, restype, argtypes) of every exported entry point — the test suite checks that the
 # built library exports exactly these and that include/mdgen_hip.h declares them.
 SIGNATURES = [
@@ -161,8 +170,8 @@ SIGNATURES = [
                                     _vp]),
     ("mdg_wgrad_workspace_bytes", ctypes.c_size_t, [_i32, _i32, _i32, _i32, _i32, _i32]),
     ("mdg_wgrad", _i32, [_i32, _i32, _i32, _i32, _vp, _i32, _vp, _i32, _vp, _i32, _vp, _vp, ctypes.c_size_t, _vp]),
-    ("mdg_ipa_core_fwd", _i32, [_i32] * 6 + [_vp] * 8 + [_f32, _vp, _vp]),
-    ("mdg_ipa_core_bwd", _i32, [_i32] * 6 + [_vp] * 8 + [_f32] + [_vp] * 7),
+    ("mdg_ipa_core_fwd", _i32, [_i32] * 6 + [_vp] * 8 + [_f32, _vp, _i32, _vp]),
+    ("mdg_ipa_core_bwd", _i32, [_i32] * 6 + [_vp] * 8 + [_f32] + [_vp] * 6 + [_i32, _vp]),
     ("mdg_train_pack_layer", _i32, [ctypes.POINTER(MdgTrainPack), _vp]),
     ("mdg_train_unpack_layer", _i32, [ctypes.POINTER(MdgTrainUnpack), _vp]),
     ("mdg_embed_bwd_workspace_bytes", ctypes.c_size_t, [_i32] * 7),
@@ -170,9 +179,13 @@ SIGNATURES = [
     ("mdg_final_fwd_train", _i32, [_i32] * 4 + [_vp] * 7),
     ("mdg_final_bwd_workspace_bytes", ctypes.c_size_t, [_i32] * 3),
     ("mdg_final_bwd_train", _i32, [_i32] * 4 + [_vp] * 9 + [_vp, ctypes.c_size_t, _vp]),
+    ("mdg_seg_linear_fwd", _i32, [_i32, _i32, _vp, _i32, _i32, ctypes.POINTER(MdgSegLinear), _vp]),
+    ("mdg_seg_linear_bwd_workspace_bytes", ctypes.c_size_t, [_i32, _i32, ctypes.POINTER(MdgSegLinear)]),
+    ("mdg_seg_linear_bwd", _i32, [_i32, _i32, _vp, _i32, _i32, ctypes.POINTER(MdgSegLinear), _vp, _i32, _vp,
+                                  ctypes.c_size_t, _vp]),
 ]
 
-ABI_VERSION = 18
+ABI_VERSION = 19
 _LIB = None
 
 

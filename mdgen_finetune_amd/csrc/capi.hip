@@ -27,11 +27,11 @@ hipError_t train_unpack_launch(const mdg_train_unpack& u, hipStream_t s);
 bool ipa_core_supported(int L, int c, int Pq, int Pv);
 hipError_t ipa_core_fwd_launch(int B, int L, int H, const float* q, const float* kv, const float* qp, const float* kvp,
                                const float* mask, const float* rots, const float* trans, const float* hw, float wc,
-                               float* out, hipStream_t s);
+                               float* out, int flags, hipStream_t s);
 hipError_t ipa_core_bwd_launch(int B, int L, int H, const float* q, const float* kv, const float* qp, const float* kvp,
                                const float* mask, const float* rots, const float* trans, const float* hw, float wc,
                                const float* dout, float* dq, float* dkv, float* dqp, float* dkvp, float* dhw_part,
-                               hipStream_t s);
+                               int flags, hipStream_t s);
 bool rowln_splitk_supported(const mdg_gemm_desc& r, int S);
 hipError_t rowln_splitk_launch(const mdg_gemm_desc& r, hipStream_t s, float* part, int S);
 bool final_euler_supported(const mdg_gemm_desc& p);
@@ -108,6 +108,12 @@ hipError_t final_bwd_train_launch(int N, int rows_per_b, int lat, const float* h
 size_t wgrad_ws_bytes(int dtype, int N, int M, int K, bool need_w, bool need_b);
 hipError_t wgrad_launch(int dtype, int N, int M, int K, const void* dy, int ldy, const void* x, int ldx, float* dw,
                         int lddw, float* db, float* ws, hipStream_t s);
+// linear_small.hip
+int seg_total(const mdg_seg_linear* s);
+size_t seg_linear_ws_bytes(int M, int K, int total);
+hipError_t seg_linear_fwd_launch(int M, int K, const float* x, int ldx, int act, const mdg_seg_linear* s, hipStream_t st);
+hipError_t seg_linear_bwd_launch(int M, int K, const float* x, int ldx, int act, const mdg_seg_linear* s, float* dx,
+                                 int lddx, float* ws, hipStream_t st);
 }  // namespace mdg
 
 namespace {
@@ -1010,12 +1016,13 @@ int mdg_attn_spatial_bwd(int32_t dtype, int32_t n_frames, int32_t L, int32_t H, 
 
 int mdg_ipa_core_fwd(int32_t B, int32_t L, int32_t H, int32_t c, int32_t Pq, int32_t Pv, const float* q,
                      const float* kv, const float* qp, const float* kvp, const float* mask, const float* rots,
-                     const float* trans, const float* hw, float wc, float* out, void* stream) {
+                     const float* trans, const float* hw, float wc, float* out, int32_t flags, void* stream) {
   if (!q || !kv || !qp || !kvp || !mask || !rots || !trans || !hw || !out) return fail(MDG_E_ARG, "ipa_core_fwd: null");
   if (B <= 0 || H <= 0 || !mdg::ipa_core_supported(L, c, Pq, Pv))
     return fail(MDG_E_SHAPE, "ipa_core_fwd: B=%d L=%d H=%d c=%d Pq=%d Pv=%d (L <= 32, c = 32, 8 + 8 points)", B, L, H,
                 c, Pq, Pv);
-  return hip_check(mdg::ipa_core_fwd_launch(B, L, H, q, kv, qp, kvp, mask, rots, trans, hw, wc, out,
+  if (flags & ~(MDG_IPA_LOCAL_POINTS | MDG_IPA_RAW_HW)) return fail(MDG_E_ARG, "ipa_core_fwd: flags %d", flags);
+  return hip_check(mdg::ipa_core_fwd_launch(B, L, H, q, kv, qp, kvp, mask, rots, trans, hw, wc, out, flags,
                                             (hipStream_t)stream),
                    "ipa_core_fwd");
 }
@@ -1023,15 +1030,16 @@ int mdg_ipa_core_fwd(int32_t B, int32_t L, int32_t H, int32_t c, int32_t Pq, int
 int mdg_ipa_core_bwd(int32_t B, int32_t L, int32_t H, int32_t c, int32_t Pq, int32_t Pv, const float* q,
                      const float* kv, const float* qp, const float* kvp, const float* mask, const float* rots,
                      const float* trans, const float* hw, float wc, const float* dout, float* dq, float* dkv,
-                     float* dqp, float* dkvp, float* dhw_part, void* stream) {
+                     float* dqp, float* dkvp, float* dhw_part, int32_t flags, void* stream) {
   if (!q || !kv || !qp || !kvp || !mask || !rots || !trans || !hw || !dout || !dq || !dkv || !dqp || !dkvp ||
       !dhw_part)
     return fail(MDG_E_ARG, "ipa_core_bwd: null");
   if (B <= 0 || H <= 0 || !mdg::ipa_core_supported(L, c, Pq, Pv))
     return fail(MDG_E_SHAPE, "ipa_core_bwd: B=%d L=%d H=%d c=%d Pq=%d Pv=%d (L <= 32, c = 32, 8 + 8 points)", B, L, H,
                 c, Pq, Pv);
+  if (flags & ~(MDG_IPA_LOCAL_POINTS | MDG_IPA_RAW_HW)) return fail(MDG_E_ARG, "ipa_core_bwd: flags %d", flags);
   return hip_check(mdg::ipa_core_bwd_launch(B, L, H, q, kv, qp, kvp, mask, rots, trans, hw, wc, dout, dq, dkv, dqp,
-                                            dkvp, dhw_part, (hipStream_t)stream),
+                                            dkvp, dhw_part, flags, (hipStream_t)stream),
                    "ipa_core_bwd");
 }
 
@@ -1364,6 +1372,45 @@ int mdg_wgrad(int32_t dtype, int32_t N, int32_t M, int32_t K, const void* dy, in
   if (!ws || ws_bytes < need) return fail(MDG_E_ARG, "wgrad: workspace %zu < %zu bytes", ws_bytes, need);
   return hip_check(mdg::wgrad_launch(dtype, N, M, K, dy, ldy, x, ldx, dw, lddw, db, (float*)ws, (hipStream_t)stream),
                    "wgrad");
+}
+
+size_t mdg_seg_linear_bwd_workspace_bytes(int32_t M, int32_t K, const mdg_seg_linear* s) {
+  const int tot = mdg::seg_total(s);
+  if (M <= 0 || K <= 0 || tot <= 0) return 0;
+  return mdg::seg_linear_ws_bytes(M, K, tot);
+}
+
+static int seg_check(const char* what, int32_t M, int32_t K, const float* x, int32_t ldx, int32_t in_act,
+                     const mdg_seg_linear* s) {
+  if (!x || !s) return fail(MDG_E_ARG, "%s: null x / segments", what);
+  if (in_act != MDG_ACT_NONE && in_act != MDG_ACT_SILU) return fail(MDG_E_ARG, "%s: in_act %d", what, in_act);
+  if (mdg::seg_total(s) <= 0)
+    return fail(MDG_E_SHAPE, "%s: nseg %d (1..%d, every n > 0)", what, s->nseg, MDG_SEG_MAX);
+  if (M <= 0 || K <= 0 || ldx < K) return fail(MDG_E_SHAPE, "%s: M=%d K=%d ldx=%d", what, M, K, ldx);
+  for (int i = 0; i < s->nseg; ++i)
+    if (!s->w[i]) return fail(MDG_E_ARG, "%s: null weight of segment %d", what, i);
+  return MDG_OK;
+}
+
+int mdg_seg_linear_fwd(int32_t M, int32_t K, const float* x, int32_t ldx, int32_t in_act, const mdg_seg_linear* s,
+                       void* stream) {
+  if (int e = seg_check("seg_linear_fwd", M, K, x, ldx, in_act, s)) return e;
+  for (int i = 0; i < s->nseg; ++i)
+    if (!s->y[i] || s->ldy[i] < s->n[i] || (s->resid[i] && s->ldr[i] < s->n[i]))
+      return fail(MDG_E_ARG, "seg_linear_fwd: segment %d output null or ld < n", i);
+  return hip_check(mdg::seg_linear_fwd_launch(M, K, x, ldx, in_act, s, (hipStream_t)stream), "seg_linear_fwd");
+}
+
+int mdg_seg_linear_bwd(int32_t M, int32_t K, const float* x, int32_t ldx, int32_t in_act, const mdg_seg_linear* s,
+                       float* dx, int32_t lddx, void* ws, size_t ws_bytes, void* stream) {
+  if (int e = seg_check("seg_linear_bwd", M, K, x, ldx, in_act, s)) return e;
+  for (int i = 0; i < s->nseg; ++i)
+    if (!s->dy[i] || s->lddy[i] < s->n[i]) return fail(MDG_E_ARG, "seg_linear_bwd: segment %d dy null or ld < n", i);
+  if (dx && lddx < K) return fail(MDG_E_SHAPE, "seg_linear_bwd: lddx %d < K %d", lddx, K);
+  const size_t need = dx ? mdg::seg_linear_ws_bytes(M, K, mdg::seg_total(s)) : 0;
+  if (need && (!ws || ws_bytes < need)) return fail(MDG_E_ARG, "seg_linear_bwd: workspace %zu < %zu bytes", ws_bytes, need);
+  return hip_check(mdg::seg_linear_bwd_launch(M, K, x, ldx, in_act, s, dx, lddx, (float*)ws, (hipStream_t)stream),
+                   "seg_linear_bwd");
 }
 
 }  // extern "C"

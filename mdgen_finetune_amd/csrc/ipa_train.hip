@@ -27,6 +27,20 @@ namespace {
 constexpr int kIpaMaxL = 32;  // the tetrapeptide crop and small proteins; longer crops take the eager path
 constexpr float kIpaInf = 1e5f, kIpaEps = 1e-8f;
 
+// flags (mdg_ipa_core_fwd / _bwd): MDG_IPA_LOCAL_POINTS = the points arrive as the raw
+// linear_q_points / linear_kv_points rows [x block | y block | z block] of n = H * P points
+// (point h * P + p; ipa.py:121-140's split + stack) in the residue's local frame, and the kernel
+// applies R x + t (rigid_utils.py:64-86) itself -- the backward returns d raw = R^T d global;
+// MDG_IPA_RAW_HW = hw is the raw head_weights parameter, softplus(w) * sqrt(1 / (3 Pq 9/2))
+// taken in the kernel (ipa.py:178-183), d hw is returned w.r.t. the raw parameter.
+__device__ __forceinline__ void frame_point(const float* raw, int n, int pidx, const float* R, const float* t,
+                                            float (&g)[3]) {
+  const float p0 = raw[pidx], p1 = raw[n + pidx], p2 = raw[2 * n + pidx];
+#pragma unroll
+  for (int x = 0; x < 3; ++x) g[x] = (__fmul_rn(R[x * 3], p0) + __fmul_rn(R[x * 3 + 1], p1)) + __fmul_rn(R[x * 3 + 2], p2) + t[x];
+}
+__device__ __forceinline__ float softplus_f(float w) { return w > 20.f ? w : log1pf(expf(w)); }
+
 template <int CH, int PQ, int PV>
 struct IpaShape {
   static constexpr int KV = 2 * CH;          // k | v per head
@@ -72,18 +86,37 @@ template <int CH, int PQ, int PV>
 struct IpaSmem {
   float K[kIpaMaxL * CH], V[kIpaMaxL * CH], KP[kIpaMaxL * PQ * 3], VP[kIpaMaxL * PV * 3], M[kIpaMaxL];
   float P[kIpaMaxL * (kIpaMaxL + 1)];
+  float R[kIpaMaxL * 9], Tt[kIpaMaxL * 3];  // the sample's frames (MDG_IPA_LOCAL_POINTS)
 };
 
-// stage the block's keys (k, v, key points, value points, mask) of sample b, head h
+// stage the block's keys (k, v, key points, value points, mask) of sample b, head h (and, for
+// local points, the sample's frames first)
 template <int CH, int PQ, int PV>
 __device__ __forceinline__ void ipa_stage_keys(IpaSmem<CH, PQ, PV>& S, int b, int h, int L, int H, const float* kv,
-                                               const float* kvp, const float* mask) {
+                                               const float* kvp, const float* mask, const float* rots,
+                                               const float* trans, int flags) {
   using SH = IpaShape<CH, PQ, PV>;
   for (int e = threadIdx.x; e < L * CH; e += blockDim.x) {
     const int j = e / CH, d = e % CH;
     const float* row = kv + (((size_t)b * L + j) * H + h) * SH::KV;
     S.K[e] = row[d];
     S.V[e] = row[CH + d];
+  }
+  for (int j = threadIdx.x; j < L; j += blockDim.x) S.M[j] = mask[(size_t)b * L + j];
+  if (flags & MDG_IPA_LOCAL_POINTS) {
+    for (int e = threadIdx.x; e < L * 9; e += blockDim.x) S.R[e] = ld1(rots + (size_t)b * L * 9 + e);
+    for (int e = threadIdx.x; e < L * 3; e += blockDim.x) S.Tt[e] = ld1(trans + (size_t)b * L * 3 + e);
+    __syncthreads();
+    constexpr int NP = PQ + PV;
+    for (int e = threadIdx.x; e < L * NP; e += blockDim.x) {
+      const int j = e / NP, p = e % NP;
+      float g[3];
+      frame_point(kvp + ((size_t)b * L + j) * H * NP * 3, H * NP, h * NP + p, S.R + j * 9, S.Tt + j * 3, g);
+      float* dst = p < PQ ? S.KP + j * PQ * 3 + 3 * p : S.VP + j * PV * 3 + 3 * (p - PQ);
+#pragma unroll
+      for (int x = 0; x < 3; ++x) dst[x] = g[x];
+    }
+    return;
   }
   for (int e = threadIdx.x; e < L * PQ * 3; e += blockDim.x) {
     const int j = e / (PQ * 3), r = e % (PQ * 3);
@@ -93,7 +126,10 @@ __device__ __forceinline__ void ipa_stage_keys(IpaSmem<CH, PQ, PV>& S, int b, in
     const int j = e / (PV * 3), r = e % (PV * 3);
     S.VP[e] = kvp[(((size_t)b * L + j) * H + h) * SH::PKV + PQ * 3 + r];
   }
-  for (int j = threadIdx.x; j < L; j += blockDim.x) S.M[j] = mask[(size_t)b * L + j];
+}
+
+__device__ __forceinline__ float ipa_hw(const float* hw, int h, int flags, float pq) {
+  return (flags & MDG_IPA_RAW_HW) ? softplus_f(hw[h]) * sqrtf(1.0f / (3.0f * (pq * 9.0f / 2.0f))) : hw[h];
 }
 
 template <int CH, int PQ, int PV>
@@ -103,20 +139,30 @@ __global__ __launch_bounds__(64) void ipa_core_fwd_kernel(int L, int H, const fl
                                                           const float* __restrict__ rots,
                                                           const float* __restrict__ trans,
                                                           const float* __restrict__ hw, float wc,
-                                                          float* __restrict__ out) {
+                                                          float* __restrict__ out, int flags) {
   __shared__ IpaSmem<CH, PQ, PV> S;
   const int b = blockIdx.x / H, h = blockIdx.x % H, i = threadIdx.x;
-  ipa_stage_keys<CH, PQ, PV>(S, b, h, L, H, kv, kvp, mask);
+  ipa_stage_keys<CH, PQ, PV>(S, b, h, L, H, kv, kvp, mask, rots, trans, flags);
   __syncthreads();
   if (i >= L) return;
   const size_t tok = (size_t)b * L + i;
   float qr[CH], qpr[PQ * 3];
 #pragma unroll
   for (int d = 0; d < CH; ++d) qr[d] = q[(tok * H + h) * CH + d];
+  if (flags & MDG_IPA_LOCAL_POINTS) {
 #pragma unroll
-  for (int r = 0; r < PQ * 3; ++r) qpr[r] = qpts[(tok * H + h) * PQ * 3 + r];
+    for (int p = 0; p < PQ; ++p) {
+      float g[3];
+      frame_point(qpts + tok * H * PQ * 3, H * PQ, h * PQ + p, S.R + i * 9, S.Tt + i * 3, g);
+#pragma unroll
+      for (int x = 0; x < 3; ++x) qpr[3 * p + x] = g[x];
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < PQ * 3; ++r) qpr[r] = qpts[(tok * H + h) * PQ * 3 + r];
+  }
   float* Prow = S.P + i * (kIpaMaxL + 1);
-  ipa_row_softmax<CH, PQ>(qr, qpr, S.M[i], L, S.K, S.KP, S.M, wc, hw[h], Prow);
+  ipa_row_softmax<CH, PQ>(qr, qpr, S.M[i], L, S.K, S.KP, S.M, wc, ipa_hw(hw, h, flags, (float)PQ), Prow);
   const int W = H * CH + 4 * H * PV;
   float* orow = out + tok * W;
   // o_i
@@ -167,21 +213,33 @@ __global__ __launch_bounds__(64) void ipa_core_bwd_kernel(int L, int H, const fl
                                                           const float* __restrict__ hw, float wc,
                                                           const float* __restrict__ dout, float* __restrict__ dq,
                                                           float* __restrict__ dkv, float* __restrict__ dqp,
-                                                          float* __restrict__ dkvp, float* __restrict__ dhw_part) {
+                                                          float* __restrict__ dkvp, float* __restrict__ dhw_part,
+                                                          int flags) {
   using SH = IpaShape<CH, PQ, PV>;
   __shared__ IpaBwdSmem<CH, PQ, PV> S;
   const int b = blockIdx.x / H, h = blockIdx.x % H, i = threadIdx.x;
-  ipa_stage_keys<CH, PQ, PV>(S.s, b, h, L, H, kv, kvp, mask);
+  const bool local = flags & MDG_IPA_LOCAL_POINTS;
+  ipa_stage_keys<CH, PQ, PV>(S.s, b, h, L, H, kv, kvp, mask, rots, trans, flags);
   for (int e = threadIdx.x; e < L * CH; e += blockDim.x) {
     const int j = e / CH, d = e % CH;
     S.Q[e] = q[(((size_t)b * L + j) * H + h) * CH + d];
   }
-  for (int e = threadIdx.x; e < L * PQ * 3; e += blockDim.x) {
-    const int j = e / (PQ * 3), r = e % (PQ * 3);
-    S.QP[e] = qpts[(((size_t)b * L + j) * H + h) * PQ * 3 + r];
+  if (local) {
+    for (int e = threadIdx.x; e < L * PQ; e += blockDim.x) {
+      const int j = e / PQ, p = e % PQ;
+      float g[3];
+      frame_point(qpts + ((size_t)b * L + j) * H * PQ * 3, H * PQ, h * PQ + p, S.s.R + j * 9, S.s.Tt + j * 3, g);
+#pragma unroll
+      for (int x = 0; x < 3; ++x) S.QP[j * PQ * 3 + 3 * p + x] = g[x];
+    }
+  } else {
+    for (int e = threadIdx.x; e < L * PQ * 3; e += blockDim.x) {
+      const int j = e / (PQ * 3), r = e % (PQ * 3);
+      S.QP[e] = qpts[(((size_t)b * L + j) * H + h) * PQ * 3 + r];
+    }
   }
   __syncthreads();
-  const float hwh = hw[h];
+  const float hwh = ipa_hw(hw, h, flags, (float)PQ);
   float dhw = 0.f;
   if (i < L) {
     const size_t tok = (size_t)b * L + i;
@@ -257,9 +315,20 @@ __global__ __launch_bounds__(64) void ipa_core_bwd_kernel(int L, int H, const fl
     float* dqr = dq + (tok * H + h) * CH;
 #pragma unroll
     for (int d = 0; d < CH; ++d) dqr[d] = wc * gq[d];
-    float* dqpr = dqp + (tok * H + h) * PQ * 3;
+    if (local) {  // d raw = R_i^T d global, into the raw [x | y | z] blocks
+      float* dr = dqp + tok * H * PQ * 3;
+      const float* R = S.s.R + i * 9;
 #pragma unroll
-    for (int r = 0; r < PQ * 3; ++r) dqpr[r] = -hwh * gqp[r];
+      for (int p = 0; p < PQ; ++p)
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+          dr[c * H * PQ + h * PQ + p] =
+              -hwh * (R[0 * 3 + c] * gqp[3 * p] + R[1 * 3 + c] * gqp[3 * p + 1] + R[2 * 3 + c] * gqp[3 * p + 2]);
+    } else {
+      float* dqpr = dqp + (tok * H + h) * PQ * 3;
+#pragma unroll
+      for (int r = 0; r < PQ * 3; ++r) dqpr[r] = -hwh * gqp[r];
+    }
   }
   // d hw_h of this sample: -1/2 sum_ij dl_ij d2_ij
   S.red[threadIdx.x] = dhw;
@@ -267,7 +336,10 @@ __global__ __launch_bounds__(64) void ipa_core_bwd_kernel(int L, int H, const fl
   if (threadIdx.x == 0) {
     float s = 0.f;
     for (int k = 0; k < L; ++k) s += S.red[k];
-    dhw_part[(size_t)b * H + h] = -0.5f * s;
+    float d = -0.5f * s;
+    if (flags & MDG_IPA_RAW_HW)  // d softplus(w) c / dw = c sigmoid(w)
+      d *= sqrtf(1.0f / (3.0f * ((float)PQ * 9.0f / 2.0f))) / (1.0f + expf(-hw[h]));
+    dhw_part[(size_t)b * H + h] = d;
   }
   // key side: lane j
   const int j = threadIdx.x;
@@ -298,6 +370,20 @@ __global__ __launch_bounds__(64) void ipa_core_bwd_kernel(int L, int H, const fl
     dkvr[d] = wc * gk[d];
     dkvr[CH + d] = gv[d];
   }
+  if (local) {
+    constexpr int NP = PQ + PV;
+    float* dr = dkvp + tok * H * NP * 3;
+    const float* R = S.s.R + j * 9;
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      const float sc = p < PQ ? hwh : 1.0f;
+      const float* gg = p < PQ ? gkp + 3 * p : gvp + 3 * (p - PQ);
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+        dr[c * H * NP + h * NP + p] = sc * (R[0 * 3 + c] * gg[0] + R[1 * 3 + c] * gg[1] + R[2 * 3 + c] * gg[2]);
+    }
+    return;
+  }
   float* dkvpr = dkvp + (tok * H + h) * SH::PKV;
 #pragma unroll
   for (int r = 0; r < PQ * 3; ++r) dkvpr[r] = hwh * gkp[r];
@@ -311,18 +397,18 @@ bool ipa_core_supported(int L, int c, int Pq, int Pv) { return L >= 1 && L <= kI
 
 hipError_t ipa_core_fwd_launch(int B, int L, int H, const float* q, const float* kv, const float* qp, const float* kvp,
                                const float* mask, const float* rots, const float* trans, const float* hw, float wc,
-                               float* out, hipStream_t s) {
+                               float* out, int flags, hipStream_t s) {
   hipLaunchKernelGGL((ipa_core_fwd_kernel<32, 8, 8>), dim3(B * H), dim3(64), 0, s, L, H, q, kv, qp, kvp, mask, rots,
-                     trans, hw, wc, out);
+                     trans, hw, wc, out, flags);
   return hipGetLastError();
 }
 
 hipError_t ipa_core_bwd_launch(int B, int L, int H, const float* q, const float* kv, const float* qp, const float* kvp,
                                const float* mask, const float* rots, const float* trans, const float* hw, float wc,
                                const float* dout, float* dq, float* dkv, float* dqp, float* dkvp, float* dhw_part,
-                               hipStream_t s) {
+                               int flags, hipStream_t s) {
   hipLaunchKernelGGL((ipa_core_bwd_kernel<32, 8, 8>), dim3(B * H), dim3(64), 0, s, L, H, q, kv, qp, kvp, mask, rots,
-                     trans, hw, wc, dout, dq, dkv, dqp, dkvp, dhw_part);
+                     trans, hw, wc, dout, dq, dkv, dqp, dkvp, dhw_part, flags);
   return hipGetLastError();
 }
 

@@ -207,8 +207,26 @@ class LatentMDGenModel(nn.Module):
 
     # ------------------------------------------------------------------ x-independent pieces
     def embed_time(self, t):
-        """c = TEmb(t * time_multiplier)  [B, C]  (latent_model.py:252)."""
+        """c = TEmb(t * time_multiplier)  [B, C]  (latent_model.py:252).  Differentiable calls on
+        the HIP training path run the MLP on the segmented library linears."""
+        if self._hip_glue(t):
+            from ..train_hip import seg_linear
+            from .layers import timestep_embedding
+
+            te = self.t_embedder
+            e = timestep_embedding(t * self.args.time_multiplier, te.frequency_embedding_size, freqs=te.freqs)
+            h = seg_linear(e, [te.mlp[0]])[0]
+            return seg_linear(h, [te.mlp[2]], act="silu")[0]
         return self.t_embedder(t * self.args.time_multiplier)
+
+    def _hip_glue(self, x):
+        """The conditioning's few-row linears on mdg_seg_linear: differentiable CUDA calls with
+        the HIP training backend (MDG_TRAIN_SEG=0 keeps them eager)."""
+        if self.backend != "hip" or getattr(self, "train_backend", "hip") != "hip":
+            return False
+        from ..train_hip import seg_supported
+
+        return seg_supported(x)
 
     def run_ipa(self, c, mask_b, start_frames, end_frames, aatype, ada=None):
         """latent_model.py:179-214 (sim / TPS branches); c [B, C], mask_b [B, L]; ada: the IPA
@@ -342,8 +360,13 @@ class LatentMDGenModel(nn.Module):
         mods = [l.adaLN_modulation for l in ipa] + [l.adaLN_modulation for l in self.layers] + \
             [self.emb_to_latent.adaLN_modulation]
         lin = [m[-1] for m in mods]
-        y = F.linear(F.silu(c0), torch.cat([l.weight for l in lin]), torch.cat([l.bias for l in lin]))
-        parts = torch.split(y, [l.out_features for l in lin], -1)
+        if self._hip_glue(c0) and len(lin) <= 16:  # one library launch, no concatenated weights
+            from ..train_hip import seg_linear
+
+            parts = seg_linear(c0, lin, act="silu")
+        else:
+            y = F.linear(F.silu(c0), torch.cat([l.weight for l in lin]), torch.cat([l.bias for l in lin]))
+            parts = torch.split(y, [l.out_features for l in lin], -1)
         return list(parts[:len(ipa)]), list(parts[len(ipa):len(ipa) + len(self.layers)]), parts[-1]
 
     def _use_hip_layers(self, h):

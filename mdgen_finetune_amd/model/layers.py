@@ -212,22 +212,25 @@ class AttentionWithRoPE(nn.Module):
 class _IpaCoreFn(torch.autograd.Function):
     """The IPA attention core (logits, softmax, value / point aggregation, inverse frame, point
     norms: ipa.py:149-250) as one HIP kernel each way (csrc/ipa_train.hip, mdg_ipa_core_fwd /
-    _bwd); the projections around it stay autograd ops.  Returns the linear_out input
-    [B, L, H*c + 4*H*Pv]."""
+    _bwd).  flags 0: points in the global frame and hw = softplus(head_weights) * c;
+    MDG_IPA_LOCAL_POINTS | MDG_IPA_RAW_HW: the raw point projections and the raw head_weights
+    (the frame application and the softplus run in the kernels, ipa.py:121-140, 178-183).
+    Returns the linear_out input [B, L, H*c + 4*H*Pv]."""
 
     @staticmethod
-    def forward(ctx, q, kv, qp, kvp, mask, rots, trans, hw, wc):
+    def forward(ctx, q, kv, qp, kvp, mask, rots, trans, hw, wc, flags=0):
         from .. import _lib
 
         lib = _lib.load()
         B, L, H, c = q.shape
-        Pq, Pv = qp.shape[3], kvp.shape[3] - qp.shape[3]
+        Pq = (qp.shape[-1] // (3 * H)) if flags & _lib.MDG_IPA_LOCAL_POINTS else qp.shape[3]
+        Pv = ((kvp.shape[-1] // (3 * H)) if flags & _lib.MDG_IPA_LOCAL_POINTS else kvp.shape[3]) - Pq
         ops = [t.detach().float().contiguous() for t in (q, kv, qp, kvp, mask, rots, trans, hw)]
         out = torch.empty(B, L, H * c + 4 * H * Pv, device=q.device)
-        _lib.check(lib.mdg_ipa_core_fwd(B, L, H, c, Pq, Pv, *[t.data_ptr() for t in ops], wc, out.data_ptr(),
+        _lib.check(lib.mdg_ipa_core_fwd(B, L, H, c, Pq, Pv, *[t.data_ptr() for t in ops], wc, out.data_ptr(), flags,
                                         _lib.stream_handle()), "mdg_ipa_core_fwd")
         ctx.save_for_backward(*ops)
-        ctx.wc = wc
+        ctx.wc, ctx.flags, ctx.P = wc, flags, (Pq, Pv)
         return out
 
     @staticmethod
@@ -238,14 +241,15 @@ class _IpaCoreFn(torch.autograd.Function):
         ops = ctx.saved_tensors
         q, kv, qp, kvp = ops[:4]
         B, L, H, c = q.shape
-        Pq, Pv = qp.shape[3], kvp.shape[3] - qp.shape[3]
+        Pq, Pv = ctx.P
         dq, dkv, dqp, dkvp = (torch.empty_like(t) for t in (q, kv, qp, kvp))
         dhw = torch.empty(B, H, device=q.device)
         _lib.check(lib.mdg_ipa_core_bwd(B, L, H, c, Pq, Pv, *[t.data_ptr() for t in ops], ctx.wc,
                                         dout.float().contiguous().data_ptr(), dq.data_ptr(), dkv.data_ptr(),
-                                        dqp.data_ptr(), dkvp.data_ptr(), dhw.data_ptr(), _lib.stream_handle()),
+                                        dqp.data_ptr(), dkvp.data_ptr(), dhw.data_ptr(), ctx.flags,
+                                        _lib.stream_handle()),
                    "mdg_ipa_core_bwd")
-        return dq, dkv, dqp, dkvp, None, None, None, dhw.sum(0), None
+        return dq, dkv, dqp, dkvp, None, None, None, dhw.sum(0), None, None
 
 
 class InvariantPointAttention(nn.Module):
@@ -271,6 +275,21 @@ class InvariantPointAttention(nn.Module):
     def forward(self, s, rots, trans, mask):
         B, L, _ = s.shape
         H, c, Pq, Pv = self.no_heads, self.c_hidden, self.no_qk_points, self.no_v_points
+        hip = self.hip_core and s.is_cuda and L <= 32 and c == 32 and Pq == 8 and Pv == 8
+        if hip:
+            from ..train_hip import seg_linear, seg_supported
+
+            if seg_supported(s):
+                # the four projections as one library launch; the frame application of the points
+                # and the head-weight softplus inside the core kernels
+                from .. import _lib
+
+                q, kv, qp, kvp = seg_linear(s, [self.linear_q, self.linear_kv, self.linear_q_points,
+                                                self.linear_kv_points])
+                o = _IpaCoreFn.apply(q.reshape(B, L, H, c), kv.reshape(B, L, H, 2 * c), qp, kvp, mask, rots, trans,
+                                     self.head_weights, math.sqrt(1.0 / (3 * c)),
+                                     _lib.MDG_IPA_LOCAL_POINTS | _lib.MDG_IPA_RAW_HW)
+                return seg_linear(o, [self.linear_out])[0]
         q = self.linear_q(s).reshape(B, L, H, c)
         kv = self.linear_kv(s).reshape(B, L, H, 2 * c)
         k, v = kv[..., :c], kv[..., c:]
@@ -278,15 +297,15 @@ class InvariantPointAttention(nn.Module):
         # Frame applications as one broadcast product + a 3-term sum each (r x: sum_j r_ij x_j;
         # the per-component form of rigid_utils.py:64-86 costs ~17 kernels forward and ~40
         # backward per application, and the training step runs 4 per IPA layer)
-        def points(lin, n):
-            pts = lin(s).reshape(B, L, 3, n).transpose(-1, -2)  # stack(split(raw, n), -1)
+        def points(raw, n):
+            pts = raw.reshape(B, L, 3, n).transpose(-1, -2)  # stack(split(raw, n), -1)
             rp = (rots[:, :, None] * pts[..., None, :]).sum(-1)
             return rp + trans[:, :, None]
 
-        q_pts = points(self.linear_q_points, H * Pq).reshape(B, L, H, Pq, 3)
-        kv_pts = points(self.linear_kv_points, H * (Pq + Pv)).reshape(B, L, H, Pq + Pv, 3)
+        q_pts = points(self.linear_q_points(s), H * Pq).reshape(B, L, H, Pq, 3)
+        kv_pts = points(self.linear_kv_points(s), H * (Pq + Pv)).reshape(B, L, H, Pq + Pv, 3)
         hw = F.softplus(self.head_weights) * math.sqrt(1.0 / (3 * (Pq * 9.0 / 2)))
-        if self.hip_core and s.is_cuda and L <= 32 and c == 32 and Pq == 8 and Pv == 8:
+        if hip:
             return self.linear_out(_IpaCoreFn.apply(q, kv, q_pts, kv_pts, mask, rots, trans, hw,
                                                     math.sqrt(1.0 / (3 * c))))
         k_pts, v_pts = kv_pts[..., :Pq, :], kv_pts[..., Pq:, :]

@@ -547,3 +547,80 @@ class _HipFinalFn(torch.autograd.Function):
 def hip_final(hl, final_layer, h, mods):
     """FinalLayer (layers.py:58-75) on the glue kernels; mods [B, 2C] (the stacked adaLN rows)."""
     return _HipFinalFn.apply(h, mods, final_layer.linear.weight, final_layer.linear.bias, hl)
+
+
+# ------------------------------------------------------------------------------------------
+# Few-row linears of the conditioning (t-MLP, every adaLN linear, the IPA projections and
+# linear_out) on mdg_seg_linear_fwd / _bwd (csrc/linear_small.hip): nseg nn.Linear layers that
+# share one input, one launch forward and two backward, no weight concatenation or output split.
+
+_ACT = {"none": _lib.MDG_ACT_NONE, "silu": _lib.MDG_ACT_SILU}
+
+
+class _SegLinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, act, nseg, resid, *wb):
+        lib = _lib.load()
+        K = x.shape[-1]
+        lead = x.shape[:-1]
+        x2 = x.detach().reshape(-1, K).float().contiguous()
+        M = x2.shape[0]
+        ws, bs = wb[:nseg], wb[nseg:]
+        sl = _lib.MdgSegLinear(nseg=nseg)
+        outs = []
+        for i, (w, b) in enumerate(zip(ws, bs)):
+            n = w.shape[0]
+            y = torch.empty(M, n, device=x.device)
+            sl.n[i], sl.w[i], sl.b[i], sl.y[i], sl.ldy[i] = n, _src(w.detach()), _lib.ptr(b), y.data_ptr(), n
+            outs.append(y)
+        if resid is not None:
+            r = resid.detach().reshape(M, -1).float().contiguous()
+            sl.resid[0], sl.ldr[0] = r.data_ptr(), r.shape[1]
+        _lib.check(lib.mdg_seg_linear_fwd(M, K, x2.data_ptr(), K, _ACT[act], ctypes.byref(sl), _lib.stream_handle()),
+                   "mdg_seg_linear_fwd")
+        ctx.save_for_backward(x2, *ws)
+        ctx.act, ctx.nseg, ctx.lead, ctx.has_bias = act, nseg, lead, [b is not None for b in bs]
+        ctx.has_resid = resid is not None
+        return tuple(y.view(*lead, y.shape[1]) for y in outs)
+
+    @staticmethod
+    def backward(ctx, *dys):
+        lib = _lib.load()
+        x2, *ws = ctx.saved_tensors
+        M, K = x2.shape
+        nseg = ctx.nseg
+        sl = _lib.MdgSegLinear(nseg=nseg)
+        keep, dws, dbs = [], [], []
+        for i, (w, dy) in enumerate(zip(ws, dys)):
+            n = w.shape[0]
+            dy2 = dy.reshape(M, n).float().contiguous()
+            keep.append(dy2)
+            dw = torch.empty(n, K, device=x2.device) if ctx.needs_input_grad[4 + i] else None
+            db = torch.empty(n, device=x2.device) if ctx.has_bias[i] and ctx.needs_input_grad[4 + nseg + i] else None
+            sl.n[i], sl.w[i], sl.dy[i], sl.lddy[i] = n, w.data_ptr(), dy2.data_ptr(), n
+            sl.dw[i], sl.db[i] = _lib.ptr(dw), _lib.ptr(db)
+            dws.append(dw)
+            dbs.append(db)
+        dx = torch.empty(M, K, device=x2.device) if ctx.needs_input_grad[0] else None
+        wsb = lib.mdg_seg_linear_bwd_workspace_bytes(M, K, ctypes.byref(sl)) if dx is not None else 0
+        wsp = torch.empty(max(wsb, 1), device=x2.device, dtype=torch.uint8)
+        _lib.check(lib.mdg_seg_linear_bwd(M, K, x2.data_ptr(), K, _ACT[ctx.act], ctypes.byref(sl), _lib.ptr(dx), K,
+                                          wsp.data_ptr(), wsb, _lib.stream_handle()), "mdg_seg_linear_bwd")
+        dresid = dys[0] if ctx.has_resid else None
+        dxo = dx.view(*ctx.lead, K) if dx is not None else None
+        return (dxo, None, None, dresid, *dws, *dbs)
+
+
+def seg_linear(x, linears, act="none", resid=None):
+    """[lin(act(x)) for lin in linears] (+ resid on the single output) through the segmented
+    library linear; x fp32 [..., K], every lin an nn.Linear(K, n_i)."""
+    if resid is not None and len(linears) != 1:
+        raise ValueError("seg_linear: resid needs exactly one segment")
+    ws = [l.weight for l in linears]
+    bs = [l.bias for l in linears]
+    return _SegLinearFn.apply(x, act, len(linears), resid, *ws, *bs)
+
+
+def seg_supported(x):
+    """The segmented linears serve differentiable CUDA fp32 calls (MDG_TRAIN_SEG=0: eager, A/B)."""
+    return x.is_cuda and torch.is_grad_enabled() and os.environ.get("MDG_TRAIN_SEG", "1") != "0"

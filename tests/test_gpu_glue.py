@@ -89,3 +89,45 @@ def test_final_layer_forward_and_backward_match_eager(B, T, lat):
     assert _rel(v, ref) <= 2e-6, _rel(v, ref)
     for name, a, t in zip(("h", "mods", "w", "b"), got, (h, mods, w, b)):
         assert _rel(a, t.grad) <= 1e-5, (name, _rel(a, t.grad))
+
+
+@pytest.mark.parametrize("lead,K,ns,act,resid", [
+    ((8,), 384, [2304] * 5 + [3456] * 5 + [768], "silu", False),  # every adaLN linear of the model
+    ((8, 4), 384, [128, 256, 96, 192], "none", False),            # the IPA projections (B*L tokens)
+    ((8, 4), 256, [384], "none", True),                           # linear_out + the IPA residual
+    ((8,), 256, [384], "none", False),                            # t-MLP first linear
+    ((37,), 100, [5, 70, 130], "silu", False),                    # ragged everything
+])
+def test_seg_linear_forward_and_backward_match_fp64(lead, K, ns, act, resid):
+    """mdg_seg_linear_fwd / _bwd (csrc/linear_small.hip) against float64 autograd of
+    [lin(act(x)) (+ resid)]: outputs, dx, every weight and bias gradient.  fp32 FMA chains vs
+    fp64: ||d|| / ||ref|| <= 2e-6."""
+    from mdgen_finetune_amd.train_hip import seg_linear
+
+    torch.manual_seed(K + len(ns))
+    dev = "cuda"
+    lins = [torch.nn.Linear(K, n).to(dev) for n in ns]
+    for l in lins:
+        torch.nn.init.normal_(l.bias, std=0.1)
+    x = torch.randn(*lead, K, device=dev, requires_grad=True)
+    r = torch.randn(*lead, ns[0], device=dev, requires_grad=True) if resid else None
+    outs = seg_linear(x, lins, act=act, resid=r)
+    gs = [torch.randn_like(o) for o in outs]
+    sum((o * g).sum() for o, g in zip(outs, gs)).backward()
+    got = [x.grad.clone()] + [t.grad.clone() for l in lins for t in (l.weight, l.bias)]
+    if resid:
+        got.append(r.grad.clone())
+    xd = x.detach().double().requires_grad_(True)
+    wd = [(l.weight.detach().double().requires_grad_(True), l.bias.detach().double().requires_grad_(True)) for l in lins]
+    rd = r.detach().double().requires_grad_(True) if resid else None
+    xa = torch.nn.functional.silu(xd) if act == "silu" else xd
+    refs = [xa @ w.t() + b for w, b in wd]
+    if resid:
+        refs[0] = rd + refs[0]
+    sum((o * g.double()).sum() for o, g in zip(refs, gs)).backward()
+    for o, ref in zip(outs, refs):
+        assert o.shape == ref.shape
+        assert _rel(o, ref) <= 2e-6, _rel(o, ref)
+    want = [xd.grad] + [t.grad for pair in wd for t in pair] + ([rd.grad] if resid else [])
+    for i, (a, b) in enumerate(zip(got, want)):
+        assert _rel(a, b) <= 2e-6, (i, _rel(a, b))

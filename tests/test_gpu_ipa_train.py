@@ -26,8 +26,12 @@ def _frames(B, L, gen):
     return R, 5.0 * torch.randn(B, L, 3, generator=gen)
 
 
+@pytest.mark.parametrize("seg", ["1", "0"])
 @pytest.mark.parametrize("B,L,n_pad", [(8, 4, 0), (3, 6, 2), (2, 20, 3), (2, 32, 0)])
-def test_ipa_core_matches_eager_autograd(B, L, n_pad):
+def test_ipa_core_matches_eager_autograd(B, L, n_pad, seg, monkeypatch):
+    """seg "1": the projections on mdg_seg_linear and the frames / softplus inside the core
+    (MDG_IPA_LOCAL_POINTS | MDG_IPA_RAW_HW); "0": eager projections and global-frame points."""
+    monkeypatch.setenv("MDG_TRAIN_SEG", seg)
     gen = torch.Generator().manual_seed(100 + L)
     C = 384
     ipa = InvariantPointAttention(C, 0, 32, 4, 8, 8)

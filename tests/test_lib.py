@@ -60,6 +60,8 @@ int main(void){
  printf("%zu %zu %zu %zu %zu %zu %zu\n", sizeof(mdg_train_pack), offsetof(mdg_train_pack, rope_rows),
         offsetof(mdg_train_pack, w1_t), sizeof(mdg_train_unpack), offsetof(mdg_train_unpack, part),
         offsetof(mdg_train_unpack, gb2), offsetof(mdg_step_io, chain_alone));
+ printf("%zu %zu %zu %zu\n", sizeof(mdg_seg_linear), offsetof(mdg_seg_linear, w), offsetof(mdg_seg_linear, resid),
+        offsetof(mdg_seg_linear, db));
  printf("%zu %zu %zu %zu %zu %zu %zu\n", offsetof(mdg_step_io, dt), offsetof(mdg_step_io, h),
         offsetof(mdg_gemm_desc, qscale), offsetof(mdg_gemm_desc, rope_rows), offsetof(mdg_gemm_desc, aux),
         offsetof(mdg_gemm_desc, ldaux), offsetof(mdg_layer_saved, init_planes));
@@ -74,7 +76,10 @@ int main(void){
     sizes = [int(v) for v in out[:6]]
     cond = [int(v) for v in out[6:13]]
     train = [int(v) for v in out[13:20]]
-    offs = [int(v) for v in out[20:]]
+    seg = [int(v) for v in out[20:24]]
+    offs = [int(v) for v in out[24:]]
+    S = _lib.MdgSegLinear
+    assert seg == [ctypes.sizeof(S), S.w.offset, S.resid.offset, S.db.offset]
     assert train == [ctypes.sizeof(_lib.MdgTrainPack), _lib.MdgTrainPack.rope_rows.offset, _lib.MdgTrainPack.w1_t.offset,
                      ctypes.sizeof(_lib.MdgTrainUnpack), _lib.MdgTrainUnpack.part.offset,
                      _lib.MdgTrainUnpack.gb2.offset, _lib.MdgStepIO.chain_alone.offset]
