@@ -179,7 +179,7 @@ def hip_layer_forward(hl, layer, h, mods, mask):
     """h [B,T,L,C] fp32, mods [B, 9C] (adaLN output), mask [B,T,L] -> layer(h) through the
     HIP training Function."""
     inv_freq = layer.mha_l.attn.rot_emb.inv_freq if hl.rope else None
-    return _HipLayerFn.apply(h, mods, mask, hl, inv_freq, *_layer_params(layer))
+    return _HipLayerFn.apply(h, mods, mask, hl, inv_freq, False, *_layer_params(layer))
 
 
 def hip_ipa_layer_tail(hl, layer, x1, mods6, mask_b):
@@ -187,8 +187,9 @@ def hip_ipa_layer_tail(hl, layer, x1, mods6, mask_b):
     then + g_m MLP(mod(LN .)), on the HIP training Function as a T = 1 block whose temporal
     sublayer has gate 0: adaLN rows [sh_l, sc_l, g_l, 0, 0, 0, sh_m, sc_m, g_m].  With g_t = 0
     the temporal branch adds exactly 0 forward and passes exactly 0 gradient back (dy_t = dh * 0),
-    so this is the IPA layer's arithmetic; its stand-in weights (mha_l's again) receive zero
-    gradients.  x1 [B, L, C], mods6 [B, 6C], mask_b [B, L]."""
+    so this is the IPA layer's arithmetic; its stand-in weights (mha_l's again) would receive zero
+    gradients, so the Function returns None for them (``tail``: no gradient accumulation of the
+    shared parameters).  x1 [B, L, C], mods6 [B, 6C], mask_b [B, L]."""
     C = hl.C
     inv_freq = layer.mha_l.attn.rot_emb.inv_freq if hl.rope else None
     mods9 = torch.cat([mods6[:, :3 * C], mods6.new_zeros(mods6.shape[0], 3 * C), mods6[:, 3 * C:]], -1)
@@ -196,13 +197,13 @@ def hip_ipa_layer_tail(hl, layer, x1, mods6, mask_b):
     att = [mha.q_proj.weight, mha.q_proj.bias, mha.k_proj.weight, mha.k_proj.bias, mha.v_proj.weight, mha.v_proj.bias,
            mha.out_proj.weight, mha.out_proj.bias, mha.bias_k, mha.bias_v]
     params = att + att + [layer.fc1.weight, layer.fc1.bias, layer.fc2.weight, layer.fc2.bias]
-    out = _HipLayerFn.apply(x1[:, None], mods9, mask_b[:, None], hl, inv_freq, *params)
+    out = _HipLayerFn.apply(x1[:, None], mods9, mask_b[:, None], hl, inv_freq, True, *params)
     return out[:, 0]
 
 
 class _HipLayerFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, h, mods, mask, hl, inv_freq, *params):
+    def forward(ctx, h, mods, mask, hl, inv_freq, tail, *params):
         lib = hl.lib
         B, T, L, C = h.shape
         H, D, F, ct = hl.H, hl.D, hl.F, hl.ct
@@ -284,7 +285,7 @@ class _HipLayerFn(torch.autograd.Function):
                                            h.data_ptr(), h_out.data_ptr(), ctypes.byref(cs), s),
                    "mdg_layer_fwd_train")
         ctx.hl, ctx.sv, ctx.P, ctx.lease = hl, sv, P, lease
-        ctx.shape = (B, T, L)
+        ctx.shape, ctx.tail = (B, T, L), tail
         ctx.kb = (kb_t, kb_s)
         ctx.mask = mask
         ctx.rope = (rope_l, rope_t)
@@ -410,8 +411,10 @@ class _HipLayerFn(torch.autograd.Function):
             out += [g["gq", i], g["gbq", i], g["gk", i], g["gbk", i], g["gv", i], g["gbv", i], grads[f"wo{i}"],
                     grads[f"bo{i}"], g["gbias_k", i], g["gbias_v", i]]
         out += [grads["w1"], grads["b1"], grads["w2"], grads["b2"]]
+        if ctx.tail:  # the zero-gate temporal stand-ins: exactly zero, nothing to accumulate
+            out[10:20] = [None] * 10
         del ctx.sv, ctx.P, ctx.lease  # the planes go back to the layer's pool
-        return (dh0.reshape(B, T, L, C), dmods, None, None, None, *out)
+        return (dh0.reshape(B, T, L, C), dmods, None, None, None, None, *out)
 
 
 # ------------------------------------------------------------------------------------------
