@@ -2653,8 +2653,29 @@ __device__ __forceinline__ void quad_pv6(float* o, const float* v, float p0, flo
 #if MDG_DIAG_SPA == 9
 __device__ unsigned g_spa_diag[4 + 32 * 128];  // [0] = mismatching lanes, then 32-word records
 #endif
-template <int S>  // ring depth (K-steps)
-__global__ __launch_bounds__(kSpaThreads) void gemm_qkv_attn_spatial_kernel(const mdg_gemm_desc p) {
+// MFMA epilogue (MF = true, the default; MDG_SPA_MFMA=0 keeps the lane-per-(frame, head)
+// VALU epilogue above for A/B): wave w of band i holds the q|k|v of ITS 16 tokens = 4 whole
+// frames in registers (C layout: lane (column lr, group lg) = tokens 4lg..4lg+3), so each wave
+// runs its frames' attention alone:
+//   1. + bias, q * qscale, RoPE (partner column = the quad neighbour, one DPP move), bf16 ->
+//      a wave-private [144 features][16 tokens] LDS image, one 8-B store per fragment;
+//   2. per head: S^T = K . Q^T and the bias-key scores sb = bk . Q^T as two 16x16x32 MFMAs
+//      (operands by ds_read_b64_tr_b16 from the image, dims 24..31 zeroed), so lane (q, g)
+//      holds q's scores against the 4 residues of frame g -- a complete softmax row where
+//      g == q / 4 (the block-diagonal frame), nothing to reduce across lanes;
+//   3. softmax in those lanes (bias key + the unmasked residues, fp32), the unnormalised P as
+//      the B operand of O^T = V^T . P^T (two 16x16x16 MFMAs, V^T by plain 8-B reads of the
+//      image), then (O + pb bv) / sum, pb and 1 / sum fetched from the row's lane by one
+//      ds_bpermute each, 8-B bf16 stores.
+// q, k, v are rounded to bf16 before the attention (as on the unfused route's planes).
+constexpr int kSpaImg = kSpaBN * 16;                             // bf16 elements of one wave's image
+constexpr int kSpaRtab = 4 * kSpaImg * 2;                        // byte offset of the RoPE table
+static_assert(kSpaRtab + 12 * 2 * 4 * 4 <= kSpaStage * 2, "images + RoPE table fit the 2-stage ring");
+typedef __attribute__((ext_vector_type(4))) short spa_s4;
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4_t;
+
+template <int S, bool MF>  // ring depth (K-steps); MF: the MFMA epilogue
+__global__ __launch_bounds__(kSpaThreads, MF ? 4 : 1) void gemm_qkv_attn_spatial_kernel(const mdg_gemm_desc p) {
 #if MDG_DIAG_ORDER
   if (threadIdx.x == 0) {
     OrderSlot& o = order_slot(p.A);
@@ -2755,6 +2776,125 @@ __global__ __launch_bounds__(kSpaThreads) void gemm_qkv_attn_spatial_kernel(cons
   }
 #undef MDG_SPA_LOAD
 
+  if constexpr (MF) {
+    // ---------------------------------------------------------------- MFMA epilogue
+    const int gi = lane & 15;
+    float* rtab = reinterpret_cast<float*>(smem + kSpaRtab);  // [12 pairs][cos | sin][4 residues]
+    bf16_t* img = lds + wave * kSpaImg;                        // [144 features][16 tokens], wave-private
+    __syncthreads();                                           // every wave is done reading the ring
+    if (p.rope && tid < 12 * 2 * 4) {
+      const int pr = tid >> 3, cs = (tid >> 2) & 1, r = tid & 3;
+      rtab[tid] = p.rope[(size_t)(cs * p.rope_rows + r) * (D / 2) + pr];
+    }
+    __syncthreads();
+    const bf16x8 z8 = {};
+#pragma unroll
+    for (int band = 0; band < 2; ++band) {
+      // 1. bias, q scale, RoPE at position l = token % 4 (the lane's 4 rows are residues 0..3)
+#pragma unroll
+      for (int j = 0; j < NF; ++j) {
+        const float bc = p.bias ? p.bias[wrow(j * 16 + lr)] : 0.f;
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = (acc[band][j][r] + bc) * (j < 3 ? p.qscale : 1.0f);
+        if (j < 6 && p.rope) {
+          const int d = (16 * (j % 3) + lr) % D, pr = d >> 1;
+          const f32x4 cs = *reinterpret_cast<const f32x4*>(rtab + pr * 8);
+          const f32x4 sn = *reinterpret_cast<const f32x4*>(rtab + pr * 8 + 4);
+          const float sg = (d & 1) ? 1.0f : -1.0f;  // even dim: x c - y s; odd: x c + y s
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float y = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v[r]), 0xB1, 0xF, 0xF, true));
+            v[r] = fmaf(y, sg * sn[r], v[r] * cs[r]);
+          }
+        }
+        bf16x4 o4;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o4[r] = (bf16_t)v[r];
+        *reinterpret_cast<bf16x4*>(img + (16 * j + lr) * 16 + 4 * lg) = o4;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      // key validity of this lane's 4 keys (frame lg's residues)
+      const int tb = m0 + band * 64 + 16 * wave;  // the wave's first token
+      f32x4 km = {1.f, 1.f, 1.f, 1.f};
+      if (p.key_mask && tb + 4 * lg < M) km = *reinterpret_cast<const f32x4*>(p.key_mask + tb + 4 * lg);
+      const bool own = lg == (lr >> 2);
+      const int src = lr + 16 * (lr >> 2);  // the lane holding token lr's softmax row
+      const int m = tb + lr;
+#pragma unroll
+      for (int hh = 0; hh < HP; ++hh) {
+        // 2. operands (EXEC full for the transposing reads; lg == 3 = dims 24..31 zeroed after)
+        auto tr8 = [&](int fbase) {
+          const bf16_t* a0 = img + (fbase + 8 * lg + (gi >> 2)) * 16 + 4 * (gi & 3);
+          const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)a0);
+          const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4_t*)(a0 + 4 * 16));
+          bf16x8 r8;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            r8[e] = lo[e];
+            r8[4 + e] = hi[e];
+          }
+          return lg < 3 ? r8 : z8;
+        };
+        const bf16x8 qf = tr8(hh * D), kf = tr8(HD + hh * D);
+        const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+        // the bias key (fair-esm RoPE at position L, kvb) as the A operand of sb = bk . Q^T, and
+        // the bias value of this lane's output dims
+        const float* kb = p.kvb + (size_t)(pair * HP + hh) * 2 * MDG_DP;
+        bf16x8 bkf;
+        {
+          const f32x4 b0 = *reinterpret_cast<const f32x4*>(kb + 8 * lg), b1 = *reinterpret_cast<const f32x4*>(kb + 8 * lg + 4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            bkf[e] = (bf16_t)(lg < 3 ? b0[e] : 0.f);
+            bkf[4 + e] = (bf16_t)(lg < 3 ? b1[e] : 0.f);
+          }
+        }
+        const f32x4 st = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf, z4, 0, 0, 0);    // S[q][4lg + r]
+        const f32x4 sbt = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bkf, qf, z4, 0, 0, 0);  // sb[q]
+        // 3. softmax over the bias key + the frame's unmasked residues (mha.py:359-389)
+        const float sb = sbt[0];
+        float mx = sb;
+        bool val[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          val[r] = own && km[r] != 0.f;
+          if (val[r]) mx = fmaxf(mx, st[r]);
+        }
+        const float pb = expf(sb - mx);
+        float pr_[4], sum = pb;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          pr_[r] = val[r] ? expf(st[r] - mx) : 0.f;
+          sum += pr_[r];
+        }
+        const float inv = 1.0f / sum;
+        bf16x4 P;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) P[r] = (bf16_t)pr_[r];
+        const int vrow = 2 * HD + hh * D;
+        const bf16x4 va0 = *reinterpret_cast<const bf16x4*>(img + (vrow + lr) * 16 + 4 * lg);
+        bf16x4 va1 = {};
+        if (lr < D - 16) va1 = *reinterpret_cast<const bf16x4*>(img + (vrow + 16 + lr) * 16 + 4 * lg);
+        const spa_s4 Ps = __builtin_bit_cast(spa_s4, P);
+        const f32x4 o0 = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(spa_s4, va0), Ps, z4, 0, 0, 0);
+        const f32x4 o1 = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(spa_s4, va1), Ps, z4, 0, 0, 0);
+        const float pbq = __shfl(pb, src, 64), invq = __shfl(inv, src, 64);
+        if (m < M) {
+          bf16_t* op = reinterpret_cast<bf16_t*>(p.out) + (size_t)m * p.ldo + (pair * HP + hh) * D;
+          const f32x4 bv0 = *reinterpret_cast<const f32x4*>(kb + MDG_DP + 4 * lg);
+          st4<bf16_t>(op + 4 * lg, (o0[0] + pbq * bv0[0]) * invq, (o0[1] + pbq * bv0[1]) * invq,
+                      (o0[2] + pbq * bv0[2]) * invq, (o0[3] + pbq * bv0[3]) * invq);
+          if (16 + 4 * lg < D) {
+            const f32x4 bv1 = *reinterpret_cast<const f32x4*>(kb + MDG_DP + 16 + 4 * lg);
+            st4<bf16_t>(op + 16 + 4 * lg, (o1[0] + pbq * bv1[0]) * invq, (o1[1] + pbq * bv1[1]) * invq,
+                        (o1[2] + pbq * bv1[2]) * invq, (o1[3] + pbq * bv1[3]) * invq);
+          }
+        }
+      }
+    }
+    return;
+  }
   // ------------------------------------------------------------------ epilogue
   float bcol[NF], scol[NF];
 #pragma unroll
@@ -2947,23 +3087,32 @@ static hipError_t launch_spatial(const mdg_gemm_desc& p0, hipStream_t s) {
     const char* e = getenv("MDG_SPA_XCD");
     return !(e && e[0] == '0');
   }();
+  // MDG_SPA_MFMA=0: the VALU (lane per frame-head) epilogue instead of the MFMA one
+  static const bool mf = [] {
+    const char* e = getenv("MDG_SPA_MFMA");
+    return !(e && e[0] == '0');
+  }();
   mdg_gemm_desc p = p0;
   p.ln_eps = xcd_map ? 0.f : -1.f;
   const int nwg = (p.H / 2) * ((p.M + 127) / 128);
+  if (mf) {
+    hipLaunchKernelGGL((gemm_qkv_attn_spatial_kernel<2, true>), dim3(nwg), dim3(kSpaThreads), spa_smem(2), s, p);
+    return hipGetLastError();
+  }
   switch (spa_stages()) {
-    case 2: hipLaunchKernelGGL((gemm_qkv_attn_spatial_kernel<2>), dim3(nwg), dim3(kSpaThreads), spa_smem(2), s, p); break;
+    case 2: hipLaunchKernelGGL((gemm_qkv_attn_spatial_kernel<2, false>), dim3(nwg), dim3(kSpaThreads), spa_smem(2), s, p); break;
     case 4: {
       static bool attr_set = false;
       if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_qkv_attn_spatial_kernel<4>),
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_qkv_attn_spatial_kernel<4, false>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)spa_smem(4));
         if (e != hipSuccess) return e;
         attr_set = true;
       }
-      hipLaunchKernelGGL((gemm_qkv_attn_spatial_kernel<4>), dim3(nwg), dim3(kSpaThreads), spa_smem(4), s, p);
+      hipLaunchKernelGGL((gemm_qkv_attn_spatial_kernel<4, false>), dim3(nwg), dim3(kSpaThreads), spa_smem(4), s, p);
       break;
     }
-    default: hipLaunchKernelGGL((gemm_qkv_attn_spatial_kernel<3>), dim3(nwg), dim3(kSpaThreads), spa_smem(3), s, p); break;
+    default: hipLaunchKernelGGL((gemm_qkv_attn_spatial_kernel<3, false>), dim3(nwg), dim3(kSpaThreads), spa_smem(3), s, p); break;
   }
   return hipGetLastError();
 }

@@ -168,6 +168,137 @@ __global__ __launch_bounds__(kWgThreads, 2) void wgrad_bf16_kernel(const WgArgs 
     }
 }
 
+// Wide-tile variant (round 4): block tile TM x TK = 64 WMT x 64 WKT, wave tile 32 WMT x 32 WKT
+// (2 x 2 waves), same ring / swizzle / transposing reads.  A 128 x 64 wave tile reads 6 operand
+// fragments per 8 MFMAs instead of 4 per 4 (a quarter fewer LDS bytes per FLOP) and the block
+// stages 24 KiB per 32 tokens for twice the FLOPs of the 128 x 128 tile; taken for the MLP
+// weights (fc1: dW [F][C], fc2: dW [C][F]) whose dims are multiples of 256 on one side.
+template <int WMT, int WKT>
+__global__ __launch_bounds__(kWgThreads, 2) void wgrad_bf16_wide_kernel(const WgArgs a) {
+  constexpr int TM = 64 * WMT, TK = 64 * WKT, IMG_A = kWgBK * TM, SLOT = kWgBK * (TM + TK);
+  constexpr int PW = WMT + WKT;  // 1-KiB LDS-DMA pieces per wave per step
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  bf16_t* ring = reinterpret_cast<bf16_t*>(smem);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int m0 = blockIdx.x * TM, k0 = blockIdx.y * TK, z = blockIdx.z;
+  const int nbeg = z * a.chunk;
+  const int nsteps = (min(a.N, nbeg + a.chunk) - nbeg) / kWgBK;
+  const bf16_t* DY = reinterpret_cast<const bf16_t*>(a.dy);
+  const bf16_t* X = reinterpret_cast<const bf16_t*>(a.x);
+  // piece j of the block (j = PW wave + i): image A (dY, TM wide) for j < TM / 16, then image B
+  // (X, TK wide); in an image of width TW a piece covers 512 / TW token rows, lane -> row
+  // j' (512 / TW) + lane / (TW / 8), physical chunk lane % (TW / 8) holding logical chunk
+  // (lane % (TW / 8)) ^ swz(row)
+  size_t src[PW];
+  int dst[PW];
+  bool isx[PW];
+#pragma unroll
+  for (int i = 0; i < PW; ++i) {
+    const int j = PW * wave + i;
+    const bool bimg = j >= TM / 16;
+    const int TW = bimg ? TK : TM, cpr = TW / 8, jj = bimg ? j - TM / 16 : j;
+    const int r = jj * (64 / cpr) + lane / cpr, cpos = lane % cpr;
+    const int lim = bimg ? a.K : a.M;
+    const int col = min((bimg ? k0 : m0) + 8 * (cpos ^ wg_swz(r)), lim - 8);
+    src[i] = (size_t)(nbeg + r) * (bimg ? a.ldx : a.ldy) + col;
+    dst[i] = (bimg ? IMG_A : 0) + jj * (64 / cpr) * TW;
+    isx[i] = bimg;
+  }
+  auto issue = [&](int st) {
+    bf16_t* sl = ring + (st % kWgStages) * SLOT;
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+      const bf16_t* base = isx[i] ? X : DY;
+      const size_t step = (size_t)st * kWgBK * (isx[i] ? a.ldx : a.ldy);
+      __builtin_amdgcn_global_load_lds((const void*)(base + src[i] + step), (lds_ptr_t)(sl + dst[i]), 16, 0, 0);
+    }
+  };
+  auto frag = [&](const bf16_t* img, int TW, int cbase, int s2) {
+    const int h = lane >> 5, gi = lane & 15;
+    const int col = cbase + 16 * ((lane >> 4) & 1) + 4 * (gi & 3);
+    const int row = 16 * s2 + 4 * h + (gi >> 2);
+    auto off = [&](int rr, int cc) { return rr * TW + (((cc >> 3) ^ wg_swz(rr)) << 3) + (cc & 7); };
+    const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(img + off(row, col)));
+    const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(img + off(row + 8, col)));
+    bf16x8 r8;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      r8[j] = lo[j];
+      r8[4 + j] = hi[j];
+    }
+    return r8;
+  };
+  const int wm = wave >> 1, wk = wave & 1;
+  f32x16 acc[WMT][WKT];
+#pragma unroll
+  for (int t = 0; t < WMT; ++t)
+#pragma unroll
+    for (int u = 0; u < WKT; ++u)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[t][u][i] = 0.f;
+  const bool csum = a.cpart != nullptr && blockIdx.y == 0 && wk == 0;
+  float cs[WMT];
+#pragma unroll
+  for (int t = 0; t < WMT; ++t) cs[t] = 0.f;
+  for (int s0 = 0; s0 < kWgStages - 1; ++s0)
+    if (s0 < nsteps) issue(s0);
+  for (int st = 0; st < nsteps; ++st) {
+    if (st + 1 < nsteps) {
+      if constexpr (PW == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (st + kWgStages - 1 < nsteps) issue(st + kWgStages - 1);
+    const bf16_t* A = ring + (st % kWgStages) * SLOT;
+    const bf16_t* B = A + IMG_A;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      bf16x8 af[WMT], bfr[WKT];
+#pragma unroll
+      for (int t = 0; t < WMT; ++t) af[t] = frag(A, TM, 32 * WMT * wm + 32 * t, s2);
+#pragma unroll
+      for (int u = 0; u < WKT; ++u) bfr[u] = frag(B, TK, 32 * WKT * wk + 32 * u, s2);
+#pragma unroll
+      for (int t = 0; t < WMT; ++t)
+#pragma unroll
+        for (int u = 0; u < WKT; ++u) acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[t], bfr[u], acc[t][u], 0, 0, 0);
+      if (csum) {
+#pragma unroll
+        for (int t = 0; t < WMT; ++t) {
+          float v = 0.f;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v += (float)af[t][j];
+          cs[t] += v;
+        }
+      }
+    }
+  }
+  if (csum) {
+#pragma unroll
+    for (int t = 0; t < WMT; ++t) {
+      const float v = cs[t] + __shfl_xor(cs[t], 32, 64);
+      const int m = m0 + 32 * WMT * wm + 32 * t + lane;
+      if (lane < 32 && m < a.M) a.cpart[(size_t)z * a.M + m] = v;
+    }
+  }
+  float* P = a.part + (size_t)z * a.M * a.ldp;
+#pragma unroll
+  for (int t = 0; t < WMT; ++t)
+#pragma unroll
+    for (int u = 0; u < WKT; ++u) {
+      const int k = k0 + 32 * WKT * wk + 32 * u + (lane & 31);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + 32 * WMT * wm + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (m < a.M && k < a.K) P[(size_t)m * a.ldp + k] = acc[t][u][r];
+      }
+    }
+}
+
 // fp32 parity path: 64 x 64 tile, 16 tokens per LDS step, 4 x 4 outputs per thread.
 __global__ __launch_bounds__(256) void wgrad_f32_kernel(const WgArgs a) {
   __shared__ float As[16][64], Bs[16][64];
@@ -287,16 +418,39 @@ __global__ __launch_bounds__(256) void split_sum_kernel(const float* __restrict_
 struct WgPlan {
   int S, chunk, cs_S, cs_chunk;
   size_t part_elems, cs_elems;
+  int wide;  // bf16 tile: 0 = 128 x 128, 1 = 256 x 128 (WMT 4), 2 = 128 x 256 (WKT 4)
 };
+
+// MDG_WGRAD_WIDE=0: always the 128 x 128 tile (A/B); MDG_WGRAD_BLOCKS: target block count of the
+// token split (default 512 = 2 per CU)
+static int wgrad_wide_enabled() {
+  static const int v = [] {
+    const char* e = getenv("MDG_WGRAD_WIDE");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+static int wgrad_target_blocks() {
+  static const int v = [] {
+    const char* e = getenv("MDG_WGRAD_BLOCKS");
+    const int b = e ? atoi(e) : 512;
+    return b > 0 ? b : 512;
+  }();
+  return v;
+}
 
 WgPlan wgrad_plan(int dtype, int N, int M, int K, bool need_w, bool need_b) {
   WgPlan p{};
-  const int tile = dtype == MDG_BF16 ? kWgTile : 64;
-  const int tiles = ((M + tile - 1) / tile) * ((K + tile - 1) / tile);
+  if (dtype == MDG_BF16 && wgrad_wide_enabled())
+    p.wide = (M % 256 == 0 && K % 128 == 0) ? 1 : (K % 256 == 0 && M % 128 == 0) ? 2 : 0;
+  const int tm = dtype == MDG_BF16 ? (p.wide == 1 ? 256 : kWgTile) : 64;
+  const int tk = dtype == MDG_BF16 ? (p.wide == 2 ? 256 : kWgTile) : 64;
+  const int tiles = ((M + tm - 1) / tm) * ((K + tk - 1) / tk);
   const int quantum = dtype == MDG_BF16 ? kWgBK : 16;
   const int nq = (N + quantum - 1) / quantum;
   // ~2 blocks per CU over the 256 CUs, each split at least 8 K-steps long
-  int S = need_w ? (512 + tiles - 1) / tiles : 1;
+  const int target = wgrad_target_blocks();
+  int S = need_w ? (target + tiles - 1) / tiles : 1;
   S = max(1, min(S, nq / 8));
   p.chunk = ((nq + S - 1) / S) * quantum;
   p.S = (N + p.chunk - 1) / p.chunk;
@@ -327,7 +481,22 @@ hipError_t wgrad_launch(int dtype, int N, int M, int K, const void* dy, int ldy,
     a.ldp = direct ? lddw : K;
     float* cp = ws + (p.S > 1 ? p.part_elems : 0);
     a.cpart = fused_b ? (direct ? db : cp) : nullptr;
-    if (dtype == MDG_BF16) {
+    if (dtype == MDG_BF16 && p.wide) {
+      constexpr int smem = kWgStages * kWgBK * (256 + 128) * 2;
+      static bool attr = false;
+      if (!attr) {
+        for (const void* k : {reinterpret_cast<const void*>(&wgrad_bf16_wide_kernel<4, 2>),
+                              reinterpret_cast<const void*>(&wgrad_bf16_wide_kernel<2, 4>)}) {
+          hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+          if (e != hipSuccess) return e;
+        }
+        attr = true;
+      }
+      if (p.wide == 1)
+        hipLaunchKernelGGL((wgrad_bf16_wide_kernel<4, 2>), dim3(M / 256, K / 128, p.S), dim3(kWgThreads), smem, s, a);
+      else
+        hipLaunchKernelGGL((wgrad_bf16_wide_kernel<2, 4>), dim3(M / 128, K / 256, p.S), dim3(kWgThreads), smem, s, a);
+    } else if (dtype == MDG_BF16) {
       static bool attr = false;
       if (!attr) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_bf16_kernel),

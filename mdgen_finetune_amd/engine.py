@@ -183,6 +183,9 @@ class HipEngine:
         cs = self._states.get(key)
         if cs is not None:
             return cs
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError(f"conditioning state for S={S} B={B} L={L} first requested inside a graph capture "
+                               "(its tables are built on the host): create it before capturing")
         m, dev, cp = self.model, self.model.device, P["cond"]
         a = m.args
         cs = _ShapeState()
@@ -528,6 +531,10 @@ class HipEngine:
             _lib.check(self.lib.mdg_prepare_mask(ctypes.byref(ls.dims), mk.data_ptr(), ls.ws.data_ptr(), s),
                        "mdg_prepare_mask")
         rows = Bl * T * L
+        # conditioning states for one evaluation and for the 6 stage times of a graphed dopri5
+        # step, built here: their RoPE / bias-kv tables are host work that a capture cannot record
+        for S_ in (1, 6):
+            self._cond_state(S_, B, L)
 
         def precondition(ts):
             """Conditioning rows for the stage times ts [S] (device fp32; capturable)."""

@@ -2,7 +2,9 @@
 of every linear layer in the block (the nn.Linear backward of latent_model.py:456-493 under
 loss.backward()), against a plain torch fp32 reference of the same op on the same (bf16-rounded)
 operands.  Tolerance: ||d|| / ||ref|| <= 1e-5 (fp32 accumulation in a different order), and the
-result must be bit-identical across repeated calls (fixed split order, no atomics)."""
+result must be bit-identical across repeated calls (fixed split order, no atomics).  The bf16
+shapes with a side divisible by 256 (fc1 / fc2: 1536 x 384, 384 x 1536) take the wide tiles
+(256 x 128 / 128 x 256, wgrad_bf16_wide_kernel)."""
 import pytest
 import torch
 
@@ -24,7 +26,8 @@ def _rel(a, b):
 
 @pytest.mark.parametrize("dtype", ["bf16", "f32"])
 @pytest.mark.parametrize("N,M,K", [(32000, 1152, 384), (32000, 384, 1536), (544, 192, 64), (96, 200, 72),
-                                   (64, 8, 8), (4000, 1536, 384)])
+                                   (64, 8, 8), (4000, 1536, 384), (32000, 1536, 384), (96, 256, 128),
+                                   (288, 128, 512)])
 def test_wgrad_matches_torch(dtype, N, M, K):
     from mdgen_finetune_amd import _lib
     from mdgen_finetune_amd.train_hip import wgrad

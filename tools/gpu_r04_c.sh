@@ -1,10 +1,13 @@
 #!/bin/bash
 # Round 4: the training step's kernel trace (plain, and with the world-1 RCCL bucket
-# all-reduces captured in the graph), the headline bench line and its kernel trace.
+# all-reduces captured in the graph), the headline bench line and its kernel trace, and kernel
+# traces of the small-M windows (B = 1 one chain; TPS B = 16 x T = 100).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 bash tools/gpu_steps.sh \
-  "trainprof|240|bash tools/gpu_train_prof.sh" \
-  "trainprof_rccl|240|PROF_DIR=gpurun_out/prof_train_rccl BENCH_ARGS=--train-rccl1 bash tools/gpu_train_prof.sh" \
-  "bench|300|python bench.py > gpurun_out/r04_bench.json" \
-  "prof|240|bash tools/gpu_prof.sh"
+  "trainprof|200|bash tools/gpu_train_prof.sh" \
+  "trainprof_rccl|200|PROF_DIR=gpurun_out/prof_train_rccl BENCH_ARGS=--train-rccl1 bash tools/gpu_train_prof.sh" \
+  "bench|240|python bench.py > gpurun_out/r04_bench.json" \
+  "prof|200|bash tools/gpu_prof.sh" \
+  "prof_b1|150|PROF_DIR=gpurun_out/prof_b1 BENCH_ARGS='--batch 1 --lanes 1' bash tools/gpu_prof.sh" \
+  "prof_tps|150|PROF_DIR=gpurun_out/prof_tps BENCH_ARGS='--tps --frames 100 --batch 16' bash tools/gpu_prof.sh"
