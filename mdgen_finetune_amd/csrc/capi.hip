@@ -110,6 +110,7 @@ hipError_t wgrad_launch(int dtype, int N, int M, int K, const void* dy, int ldy,
                         int lddw, float* db, float* ws, hipStream_t s);
 // linear_small.hip
 int seg_total(const mdg_seg_linear* s);
+bool seg_linear_shape_ok(int M, int K);
 size_t seg_linear_ws_bytes(int M, int K, int total);
 hipError_t seg_linear_fwd_launch(int M, int K, const float* x, int ldx, int act, const mdg_seg_linear* s, hipStream_t st);
 hipError_t seg_linear_bwd_launch(int M, int K, const float* x, int ldx, int act, const mdg_seg_linear* s, float* dx,
@@ -1386,7 +1387,11 @@ static int seg_check(const char* what, int32_t M, int32_t K, const float* x, int
   if (in_act != MDG_ACT_NONE && in_act != MDG_ACT_SILU) return fail(MDG_E_ARG, "%s: in_act %d", what, in_act);
   if (mdg::seg_total(s) <= 0)
     return fail(MDG_E_SHAPE, "%s: nseg %d (1..%d, every n > 0)", what, s->nseg, MDG_SEG_MAX);
-  if (M <= 0 || K <= 0 || ldx < K) return fail(MDG_E_SHAPE, "%s: M=%d K=%d ldx=%d", what, M, K, ldx);
+  if (!mdg::seg_linear_shape_ok(M, K) || ldx < K || ldx % 4 || ((uintptr_t)x & 15))
+    return fail(MDG_E_SHAPE, "%s: M=%d K=%d ldx=%d (K %% 4 == 0, K <= 1536, x 16-B aligned, ldx %% 4 == 0)", what, M,
+                K, ldx);
+  for (int i = 0; i < s->nseg; ++i)
+    if ((uintptr_t)s->w[i] & 15) return fail(MDG_E_SHAPE, "%s: weight %d not 16-B aligned", what, i);
   for (int i = 0; i < s->nseg; ++i)
     if (!s->w[i]) return fail(MDG_E_ARG, "%s: null weight of segment %d", what, i);
   return MDG_OK;

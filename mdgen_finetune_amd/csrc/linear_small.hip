@@ -24,10 +24,14 @@
 #include "../../include/mdgen_hip.h"
 #include "common.h"
 
+#include <algorithm>
+
 namespace mdg {
 namespace {
 
-constexpr int kSlR = 32, kSlC = 64, kSlJ = 32, kSlThreads = 256, kSlChunk = 256;  // dX: weight rows per partial
+constexpr int kSlMaxM = 32;   // token rows per block (grid.y covers more)
+constexpr int kSlMaxK = 1536;  // input width (x' rows staged in LDS)
+constexpr int kSlChunk = 256;  // dX: weight rows per partial
 
 struct SegMap {
   int nseg, total;
@@ -47,38 +51,14 @@ __device__ __forceinline__ float dsilu_f(float x) {
   return s * (1.0f + x * (1.0f - s));
 }
 
-// C tile [r0, r0 + 32) x [c0, c0 + 64) += sum_{j in [j0, j1)} A(r, j) B(j, c), accumulated in acc.
-// getA(r, j) / getB(j, c) return 0 outside the operands.  A_JFAST: consecutive threads stage
-// consecutive j of A (A contiguous in j) instead of consecutive r; B_JFAST likewise for B.
-template <bool A_JFAST, bool B_JFAST, typename GA, typename GB>
-__device__ __forceinline__ void sl_tile(float (&acc)[2][4], int r0, int c0, int j0, int j1, GA getA, GB getB,
-                                        float (*As)[kSlJ + 1], float (*Bs)[kSlC + 1]) {
-  const int tid = threadIdx.x, tr = tid >> 4, tc = tid & 15;
-  for (int jb = j0; jb < j1; jb += kSlJ) {
-#pragma unroll
-    for (int u = 0; u < kSlR * kSlJ / kSlThreads; ++u) {
-      const int e = tid + u * kSlThreads;
-      const int r = A_JFAST ? e / kSlJ : e % kSlR, j = A_JFAST ? e % kSlJ : e / kSlR;
-      As[r][j] = jb + j < j1 ? getA(r0 + r, jb + j) : 0.f;
-    }
-#pragma unroll
-    for (int u = 0; u < kSlJ * kSlC / kSlThreads; ++u) {
-      const int e = tid + u * kSlThreads;
-      const int j = B_JFAST ? e % kSlJ : e / kSlC, c = B_JFAST ? e / kSlJ : e % kSlC;
-      Bs[j][c] = jb + j < j1 ? getB(jb + j, c0 + c) : 0.f;
-    }
-    __syncthreads();
-#pragma unroll 8
-    for (int j = 0; j < kSlJ; ++j) {
-      const float a0 = As[tr][j], a1 = As[tr + 16][j];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float b = Bs[j][tc + 16 * q];
-        acc[0][q] = fmaf(a0, b, acc[0][q]);
-        acc[1][q] = fmaf(a1, b, acc[1][q]);
-      }
-    }
-    __syncthreads();
+// x' rows [m0, m0 + mc) of the block -> LDS [mc][K] (SiLU applied), float4 per thread step
+__device__ __forceinline__ void sl_stage_x(float* xs, const float* x, int ldx, int m0, int mc, int K, int act) {
+  const int k4 = K >> 2;
+  for (int e = threadIdx.x; e < mc * k4; e += blockDim.x) {
+    const int m = e / k4, c = (e - m * k4) * 4;
+    float4 v = *reinterpret_cast<const float4*>(x + (size_t)(m0 + m) * ldx + c);
+    if (act == MDG_ACT_SILU) v = make_float4(silu_f(v.x), silu_f(v.y), silu_f(v.z), silu_f(v.w));
+    *reinterpret_cast<float4*>(xs + m * K + c) = v;
   }
 }
 
@@ -94,37 +74,55 @@ struct SlFwdArgs {
   int ldr[MDG_SEG_MAX];
 };
 
-// grid (n tiles of 64, m tiles of 32)
-__global__ __launch_bounds__(kSlThreads) void sl_fwd_kernel(const SlFwdArgs a) {
-  __shared__ float As[kSlR][kSlJ + 1];
-  __shared__ float Bs[kSlJ][kSlC + 1];
-  const int c0 = blockIdx.x * kSlC, r0 = blockIdx.y * kSlR;
-  float acc[2][4] = {};
-  auto getA = [&](int m, int k) -> float {
-    if (m >= a.M) return 0.f;
-    const float v = a.x[(size_t)m * a.ldx + k];
-    return a.act == MDG_ACT_SILU ? silu_f(v) : v;
-  };
-  auto getB = [&](int k, int n) -> float {
-    if (n >= a.sm.total) return 0.f;
-    const int s = seg_of(a.sm, n);
-    return a.w[s][(size_t)(n - a.sm.start[s]) * a.K + k];
-  };
-  sl_tile<true, true>(acc, r0, c0, 0, a.K, getA, getB, As, Bs);
-  const int tr = threadIdx.x >> 4, tc = threadIdx.x & 15;
+// Forward.  Block = 64 weight rows (n) x up to 32 token rows; wave w owns rows n0 + 16w + (lane &
+// 15), lane >> 4 picks a quarter of every 16-wide k chunk: each lane streams float4 pieces of
+// ITS weight row (4 lanes cover 64 contiguous bytes) against the x' rows in LDS (same address
+// within a 16-lane group: broadcast), 32 accumulators; the k quarters are summed by two lane
+// swaps at the end.
+template <int MT>
+__global__ __launch_bounds__(256) void sl_fwd_kernel(const SlFwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float xs[];  // [MT][K]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nl = lane & 15, kq = lane >> 4;
+  const int m0 = blockIdx.y * MT, mc = min(MT, a.M - m0);
+  sl_stage_x(xs, a.x, a.ldx, m0, mc, a.K, a.act);
+  const int n = blockIdx.x * 64 + 16 * wave + nl;
+  const bool live = n < a.sm.total;
+  const int s = live ? seg_of(a.sm, n) : 0, nr = live ? n - a.sm.start[s] : 0;
+  const float* wr = a.w[s] + (size_t)nr * a.K;
+  __syncthreads();
+  float acc[MT];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int n = c0 + tc + 16 * q;
-    if (n >= a.sm.total) continue;
-    const int s = seg_of(a.sm, n), nl = n - a.sm.start[s];
-    const float bias = a.b[s] ? a.b[s][nl] : 0.f;
+  for (int m = 0; m < MT; ++m) acc[m] = 0.f;
+  if (live) {
+    for (int k = 4 * kq; k < a.K; k += 16) {
+      const float4 w4 = *reinterpret_cast<const float4*>(wr + k);
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int m = r0 + tr + 16 * i;
-      if (m >= a.M) continue;
-      float v = acc[i][q] + bias;
-      if (a.resid[s]) v = a.resid[s][(size_t)m * a.ldr[s] + nl] + v;
-      a.y[s][(size_t)m * a.ldy[s] + nl] = v;
+      for (int m = 0; m < MT; ++m) {
+        if (m < mc) {
+          const float4 x4 = *reinterpret_cast<const float4*>(xs + m * a.K + k);
+          acc[m] = fmaf(x4.x, w4.x, acc[m]);
+          acc[m] = fmaf(x4.y, w4.y, acc[m]);
+          acc[m] = fmaf(x4.z, w4.z, acc[m]);
+          acc[m] = fmaf(x4.w, w4.w, acc[m]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    acc[m] += __shfl_xor(acc[m], 16, 64);
+    acc[m] += __shfl_xor(acc[m], 32, 64);
+  }
+  if (!live || kq != 0) return;
+  const float bias = a.b[s] ? a.b[s][nr] : 0.f;
+  float* yr = a.y[s] + nr;
+  const float* rr = a.resid[s] ? a.resid[s] + nr : nullptr;
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    if (m < mc) {
+      float v = acc[m] + bias;
+      if (rr) v = rr[(size_t)(m0 + m) * a.ldr[s]] + v;
+      yr[(size_t)(m0 + m) * a.ldy[s]] = v;
     }
   }
 }
@@ -138,78 +136,136 @@ struct SlBwdArgs {
   int lddy[MDG_SEG_MAX];
   float* dw[MDG_SEG_MAX];
   float* db[MDG_SEG_MAX];
-  int n_dw_blocks;  // blocks [0, n_dw_blocks): dW tiles (n tiles x k tiles); the rest: dX partial tiles
-  int k_tiles, m_tiles, chunks;
+  int n_dw_blocks;  // blocks [0, n_dw_blocks): 64 weight rows of dW / db each; the rest: dX chunks
+  int chunks;
   float* part;  // [chunks][M][K]
 };
 
-__global__ __launch_bounds__(kSlThreads) void sl_bwd_kernel(const SlBwdArgs a) {
-  __shared__ float As[kSlR][kSlJ + 1];
-  __shared__ float Bs[kSlJ][kSlC + 1];
-  const int tr = threadIdx.x >> 4, tc = threadIdx.x & 15;
-  float acc[2][4] = {};
-  auto dy_at = [&](int m, int n) -> float {  // dy of virtual row n at token m (0 outside)
-    if (m >= a.M || n >= a.sm.total) return 0.f;
-    const int s = seg_of(a.sm, n);
-    return a.dy[s][(size_t)m * a.lddy[s] + (n - a.sm.start[s])];
-  };
+// Backward, two block roles in one launch (tokens in chunks of 32):
+//   dW block: 64 weight rows x all K; thread (k4 column group tk = t & 31, row group tn = t >> 5)
+//     owns float4 columns tk + 32 i and rows tn + 8 j; per token m one dy broadcast from LDS
+//     and one x' float4 from LDS per (i, j) product: dW[n][k] = sum_m dy[m][n] x'[m][k], db[n]
+//     = sum_m dy[m][n] (m ascending, exact fp32 FMAs).
+//   dX block: a chunk of kSlChunk weight rows; thread = float4 column group of dx, register
+//     accumulators for every token; per weight row one coalesced float4 of W and the M dy
+//     values from LDS: P[chunk][m][k] = sum_{n in chunk} dy[m][n] W[n][k].
+__global__ __launch_bounds__(256) void sl_bwd_kernel(const SlBwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sm_[];
+  const int t = threadIdx.x;
   if ((int)blockIdx.x < a.n_dw_blocks) {
-    // dW tile: r = n (32 weight rows), c = k (64 input columns), j = m
-    const int nt = blockIdx.x / a.k_tiles, kt = blockIdx.x % a.k_tiles;
-    const int r0 = nt * kSlR, c0 = kt * kSlC;
-    auto getA = [&](int n, int m) { return dy_at(m, n); };
-    auto getB = [&](int m, int k) -> float {
-      if (k >= a.K) return 0.f;
-      const float v = a.x[(size_t)m * a.ldx + k];
-      return a.act == MDG_ACT_SILU ? silu_f(v) : v;
-    };
-    sl_tile<false, false>(acc, r0, c0, 0, a.M, getA, getB, As, Bs);
+    float* xs = sm_;                   // [32][K]: the current token chunk's x'
+    float* dys = sm_ + kSlMaxM * a.K;  // [32][64]
+    const int n0 = blockIdx.x * 64;
+    const int tk = t & 31, tn = t >> 5, k4 = a.K >> 2;
+    for (int i0 = tk; i0 - tk < k4; i0 += 32 * 3) {  // up to 3 float4 column groups per pass
+      float4 acc[3][8];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int n = r0 + tr + 16 * i;
-      if (n >= a.sm.total) continue;
-      const int s = seg_of(a.sm, n), nl = n - a.sm.start[s];
-      if (a.dw[s])
+      for (int i = 0; i < 3; ++i)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int k = c0 + tc + 16 * q;
-          if (k < a.K) a.dw[s][(size_t)nl * a.K + k] = acc[i][q];
+        for (int j = 0; j < 8; ++j) acc[i][j] = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int mb = 0; mb < a.M; mb += kSlMaxM) {  // token chunks, m ascending overall
+        const int mc = min(kSlMaxM, a.M - mb);
+        __syncthreads();
+        sl_stage_x(xs, a.x, a.ldx, mb, mc, a.K, a.act);
+        for (int e = t; e < mc * 64; e += 256) {
+          const int m = e >> 6, c = e & 63, n = n0 + c;
+          float v = 0.f;
+          if (n < a.sm.total) {
+            const int s = seg_of(a.sm, n);
+            v = a.dy[s][(size_t)(mb + m) * a.lddy[s] + (n - a.sm.start[s])];
+          }
+          dys[m * 64 + c] = v;
         }
+        __syncthreads();
+        for (int m = 0; m < mc; ++m) {
+          float4 xv[3];
+#pragma unroll
+          for (int i = 0; i < 3; ++i) {
+            const int c = i0 + 32 * i;
+            xv[i] = c < k4 ? *reinterpret_cast<const float4*>(xs + m * a.K + 4 * c) : make_float4(0.f, 0.f, 0.f, 0.f);
+          }
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float d = dys[m * 64 + tn + 8 * j];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+              acc[i][j].x = fmaf(d, xv[i].x, acc[i][j].x);
+              acc[i][j].y = fmaf(d, xv[i].y, acc[i][j].y);
+              acc[i][j].z = fmaf(d, xv[i].z, acc[i][j].z);
+              acc[i][j].w = fmaf(d, xv[i].w, acc[i][j].w);
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int n = n0 + tn + 8 * j;
+        if (n >= a.sm.total) continue;
+        const int s = seg_of(a.sm, n);
+        if (!a.dw[s]) continue;
+        float* dwr = a.dw[s] + (size_t)(n - a.sm.start[s]) * a.K;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          const int c = i0 + 32 * i;
+          if (c < k4) *reinterpret_cast<float4*>(dwr + 4 * c) = acc[i][j];
+        }
+      }
     }
-    // db[n] = sum_m dy[m][n]: the k-tile-0 blocks, one thread per weight row, m ascending
-    if (kt == 0 && threadIdx.x < kSlR) {
-      const int n = r0 + threadIdx.x;
+    if (t < 64) {  // db, m ascending (dy straight from global memory)
+      const int n = n0 + t;
       if (n < a.sm.total) {
         const int s = seg_of(a.sm, n);
         if (a.db[s]) {
+          const float* col = a.dy[s] + (n - a.sm.start[s]);
           float sum = 0.f;
-          for (int m = 0; m < a.M; ++m) sum += dy_at(m, n);
+          for (int m = 0; m < a.M; ++m) sum += col[(size_t)m * a.lddy[s]];
           a.db[s][n - a.sm.start[s]] = sum;
         }
       }
     }
     return;
   }
-  // dX partial tile: r = m, c = k, j = n over one chunk of kSlChunk weight rows
-  const int t = blockIdx.x - a.n_dw_blocks;
-  const int kt = t % a.k_tiles, mt = (t / a.k_tiles) % a.m_tiles, ch = t / (a.k_tiles * a.m_tiles);
-  const int r0 = mt * kSlR, c0 = kt * kSlC, j0 = ch * kSlChunk, j1 = min(j0 + kSlChunk, a.sm.total);
-  auto getA = [&](int m, int n) { return dy_at(m, n); };
-  auto getB = [&](int n, int k) -> float {
-    if (k >= a.K) return 0.f;
-    const int s = seg_of(a.sm, n);
-    return a.w[s][(size_t)(n - a.sm.start[s]) * a.K + k];
-  };
-  sl_tile<true, false>(acc, r0, c0, j0, j1, getA, getB, As, Bs);
+  // dX partial of one chunk of weight rows, token chunks of 32
+  const int ch = blockIdx.x - a.n_dw_blocks;
+  const int j0 = ch * kSlChunk, j1 = min(j0 + kSlChunk, a.sm.total), nc = j1 - j0;
+  float* dys = sm_;  // [kSlChunk][32]
+  const int k4 = a.K >> 2;
   float* P = a.part + (size_t)ch * a.M * a.K;
+  for (int mb = 0; mb < a.M; mb += kSlMaxM) {
+    const int mc = min(kSlMaxM, a.M - mb);
+    __syncthreads();
+    for (int e = t; e < nc * mc; e += 256) {
+      const int jj = e / mc, m = e - jj * mc, n = j0 + jj;
+      const int s = seg_of(a.sm, n);
+      dys[jj * kSlMaxM + m] = a.dy[s][(size_t)(mb + m) * a.lddy[s] + (n - a.sm.start[s])];
+    }
+    __syncthreads();
+    for (int c = t; c < k4; c += 256) {
+      float4 acc[kSlMaxM];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int m = r0 + tr + 16 * i;
-    if (m >= a.M) continue;
+      for (int m = 0; m < kSlMaxM; ++m) acc[m] = make_float4(0.f, 0.f, 0.f, 0.f);
+      int s = seg_of(a.sm, j0), send = a.sm.start[s + 1];
+      for (int jj = 0; jj < nc; ++jj) {
+        const int n = j0 + jj;
+        while (n >= send && s + 1 < a.sm.nseg) {
+          ++s;
+          send = a.sm.start[s + 1];
+        }
+        const float4 w4 = *reinterpret_cast<const float4*>(a.w[s] + (size_t)(n - a.sm.start[s]) * a.K + 4 * c);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int k = c0 + tc + 16 * q;
-      if (k < a.K) P[(size_t)m * a.K + k] = acc[i][q];
+        for (int m = 0; m < kSlMaxM; ++m) {
+          if (m < mc) {
+            const float d = dys[jj * kSlMaxM + m];
+            acc[m].x = fmaf(d, w4.x, acc[m].x);
+            acc[m].y = fmaf(d, w4.y, acc[m].y);
+            acc[m].z = fmaf(d, w4.z, acc[m].z);
+            acc[m].w = fmaf(d, w4.w, acc[m].w);
+          }
+        }
+      }
+#pragma unroll
+      for (int m = 0; m < kSlMaxM; ++m)
+        if (m < mc) *reinterpret_cast<float4*>(P + (size_t)(mb + m) * a.K + 4 * c) = acc[m];
     }
   }
 }
@@ -255,6 +311,8 @@ size_t seg_linear_ws_bytes(int M, int K, int total) {
   return (size_t)chunks * M * K * sizeof(float);
 }
 
+bool seg_linear_shape_ok(int M, int K) { return M > 0 && K > 0 && K % 4 == 0 && K <= kSlMaxK; }
+
 hipError_t seg_linear_fwd_launch(int M, int K, const float* x, int ldx, int act, const mdg_seg_linear* s,
                                  hipStream_t st) {
   SegMap sm;
@@ -265,8 +323,21 @@ hipError_t seg_linear_fwd_launch(int M, int K, const float* x, int ldx, int act,
     a.w[i] = s->w[i], a.b[i] = s->b[i], a.y[i] = s->y[i], a.ldy[i] = s->ldy[i];
     a.resid[i] = s->resid[i], a.ldr[i] = s->ldr[i];
   }
-  dim3 grid((sm.total + kSlC - 1) / kSlC, (M + kSlR - 1) / kSlR);
-  hipLaunchKernelGGL(sl_fwd_kernel, grid, dim3(kSlThreads), 0, st, a);
+  const unsigned nx = (unsigned)((sm.total + 63) / 64);
+  if (M <= 8) {
+    const size_t smem = (size_t)8 * K * sizeof(float);
+    hipLaunchKernelGGL(sl_fwd_kernel<8>, dim3(nx, 1), dim3(256), smem, st, a);
+  } else {
+    const size_t smem = (size_t)kSlMaxM * K * sizeof(float);
+    static bool attr = false;
+    if (!attr) {
+      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&sl_fwd_kernel<kSlMaxM>),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, kSlMaxM * kSlMaxK * 4);
+      if (e != hipSuccess) return e;
+      attr = true;
+    }
+    hipLaunchKernelGGL(sl_fwd_kernel<kSlMaxM>, dim3(nx, (M + kSlMaxM - 1) / kSlMaxM), dim3(256), smem, st, a);
+  }
   return hipGetLastError();
 }
 
@@ -281,13 +352,20 @@ hipError_t seg_linear_bwd_launch(int M, int K, const float* x, int ldx, int act,
     a.w[i] = s->w[i], a.dy[i] = s->dy[i], a.lddy[i] = s->lddy[i], a.dw[i] = s->dw[i], a.db[i] = s->db[i];
     any_w = any_w || s->dw[i] || s->db[i];
   }
-  a.k_tiles = (K + kSlC - 1) / kSlC;
-  a.m_tiles = (M + kSlR - 1) / kSlR;
   a.chunks = dx ? (sm.total + kSlChunk - 1) / kSlChunk : 0;
-  a.n_dw_blocks = any_w ? ((sm.total + kSlR - 1) / kSlR) * a.k_tiles : 0;
+  a.n_dw_blocks = any_w ? (sm.total + 63) / 64 : 0;
   a.part = ws;
-  const int nblk = a.n_dw_blocks + a.chunks * a.k_tiles * a.m_tiles;
-  if (nblk > 0) hipLaunchKernelGGL(sl_bwd_kernel, dim3(nblk), dim3(kSlThreads), 0, st, a);
+  static bool attr = false;
+  const size_t smax = (size_t)(kSlMaxM * kSlMaxK + kSlMaxM * 64) * 4;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&sl_bwd_kernel),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)smax);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  const size_t smem = std::max((size_t)(kSlMaxM * K + kSlMaxM * 64) * 4, (size_t)kSlChunk * kSlMaxM * 4);
+  const int nblk = a.n_dw_blocks + a.chunks;
+  if (nblk > 0) hipLaunchKernelGGL(sl_bwd_kernel, dim3(nblk), dim3(256), smem, st, a);
   if (dx)
     hipLaunchKernelGGL(sl_dx_reduce_kernel, dim3((M * K + 255) / 256), dim3(256), 0, st, M, K, a.chunks,
                        (const float*)ws, x, ldx, act, dx, lddx);

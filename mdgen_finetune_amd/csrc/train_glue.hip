@@ -82,27 +82,40 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(int B, int T, int L, int
   for (int u = 0; u < kEbEMax; ++u) esum[u] = 0.f;
   const float (*X)[kEbK] = xs[op];
   const float* dcol = dh + n0 * C + c;
-  for (int r = 0; r < ntok; ++r) {
-    const int l = r % L;
-    const float g = dcol[(size_t)r * C];
+  // rows in groups of 8 with their dh (and mask index) loads issued up front: one dependent
+  // HBM round trip per group instead of per row
+  for (int rb = 0; rb < ntok; rb += 8) {
+    float gv[8];
+    int ev[8];
 #pragma unroll
-    for (int k4 = 0; k4 < kEbK; k4 += 4) {
-      if (k4 < K) {
-        const float4 xv = *reinterpret_cast<const float4*>(&X[r][k4]);
-        acc[k4] = fmaf(g, xv.x, acc[k4]);
-        acc[k4 + 1] = fmaf(g, xv.y, acc[k4 + 1]);
-        acc[k4 + 2] = fmaf(g, xv.z, acc[k4 + 2]);
-        acc[k4 + 3] = fmaf(g, xv.w, acc[k4 + 3]);
-      }
+    for (int u = 0; u < 8; ++u) {
+      gv[u] = rb + u < ntok ? dcol[(size_t)(rb + u) * C] : 0.f;
+      ev[u] = (op && idx && rb + u < ntok) ? (int)idx[n0 + rb + u] : -1;
     }
-    if (op == 0) {
-      cs += g;
 #pragma unroll
-      for (int u = 0; u < kEbLMax; ++u) lsum[u] += (u == l) ? g : 0.f;
-    } else if (idx) {
-      const int64_t e = idx[n0 + r];
+    for (int u = 0; u < 8; ++u) {
+      const int r = rb + u;
+      if (r >= ntok) break;
+      const int l = r % L;
+      const float g = gv[u];
 #pragma unroll
-      for (int u = 0; u < kEbEMax; ++u) esum[u] += (u == e) ? g : 0.f;
+      for (int k4 = 0; k4 < kEbK; k4 += 4) {
+        if (k4 < K) {
+          const float4 xv = *reinterpret_cast<const float4*>(&X[r][k4]);
+          acc[k4] = fmaf(g, xv.x, acc[k4]);
+          acc[k4 + 1] = fmaf(g, xv.y, acc[k4 + 1]);
+          acc[k4 + 2] = fmaf(g, xv.z, acc[k4 + 2]);
+          acc[k4 + 3] = fmaf(g, xv.w, acc[k4 + 3]);
+        }
+      }
+      if (op == 0) {
+        cs += g;
+#pragma unroll
+        for (int q = 0; q < kEbLMax; ++q) lsum[q] += (q == l) ? g : 0.f;
+      } else if (idx) {
+#pragma unroll
+        for (int q = 0; q < kEbEMax; ++q) esum[q] += (q == ev[u]) ? g : 0.f;
+      }
     }
   }
   {  // [chunk][k][C]: each store instruction writes 64 consecutive floats
@@ -123,52 +136,76 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(int B, int T, int L, int
   }
 }
 
-// sums the chunk partials in chunk order: dw1 [C][K1], dw2 [C][K2], db [C], demb [E][C],
-// dipa [B][L][C] (over the chunks of trajectory b)
+// Ordered chunk sums, 64 outputs per block: wave q sums chunks [q Z / 4, (q + 1) Z / 4) of its
+// lane's output (4 loads in flight), and lane e of wave 0 adds the four in order -- a fixed
+// association (deterministic), a quarter of the dependent-load chain of one thread per output.
+__device__ __forceinline__ float zsum4(const float* p, size_t zstride, int z0, int z1, float* red) {
+  const int lane = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int Z = z1 - z0, a = z0 + q * Z / 4, b = z0 + (q + 1) * Z / 4;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  int z = a;
+  for (; z + 4 <= b; z += 4) {
+    s0 += p[(size_t)z * zstride];
+    s1 += p[(size_t)(z + 1) * zstride];
+    s2 += p[(size_t)(z + 2) * zstride];
+    s3 += p[(size_t)(z + 3) * zstride];
+  }
+  for (; z < b; ++z) s0 += p[(size_t)z * zstride];
+  red[q * 64 + lane] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  return ((red[lane] + red[64 + lane]) + red[128 + lane]) + red[192 + lane];
+}
+
+// sums the chunk partials: dw1 [C][K1], dw2 [C][K2], db [C], demb [E][C], dipa [B][L][C] (over
+// the chunks of trajectory b); block = 64 outputs x 4 chunk quarters
 __global__ __launch_bounds__(256) void embed_bwd_reduce_kernel(int B, int L, int C, int K1, int K2, int E,
                                                                const float* __restrict__ ws, EbPlan pl,
                                                                float* __restrict__ dw1, float* __restrict__ dw2,
                                                                float* __restrict__ db, float* __restrict__ demb,
                                                                float* __restrict__ dipa) {
-  const long long n1 = (long long)C * K1, n2 = dw2 ? (long long)C * K2 : 0, nb = db ? C : 0,
+  __shared__ float red[256];
+  const long long n1 = dw1 ? (long long)C * K1 : 0, n2 = dw2 ? (long long)C * K2 : 0, nb = db ? C : 0,
                   ne = demb ? (long long)E * C : 0, ni = dipa ? (long long)B * L * C : 0;
-  long long e = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (e < n1) {  // dw1[c][k] from the [chunk][k][C] partials
-    if (!dw1) return;
-    const int c = (int)(e / K1), k = (int)(e % K1);
-    float s = 0.f;
-    for (int z = 0; z < pl.chunks; ++z) s += ws[pl.p1 + ((size_t)z * K1 + k) * C + c];
-    dw1[e] = s;
+  long long e = (long long)blockIdx.x * 64 + (threadIdx.x & 63);
+  const bool wave0 = threadIdx.x < 64;
+  // (block-uniform segment: the segment sizes are multiples of 64 when C is, and every block
+  // starts a fresh segment range because the launch rounds each segment up to 64 outputs)
+  const long long s1 = (n1 + 63) / 64 * 64, s2 = (n2 + 63) / 64 * 64, sb = (nb + 63) / 64 * 64,
+                  se = (ne + 63) / 64 * 64;
+  if (e < s1) {  // dw1[c][k] from the [chunk][k][C] partials; outputs in partial order (c fastest)
+    const bool ok = e < n1;
+    const int k = ok ? (int)(e / C) : 0, c = ok ? (int)(e % C) : 0;
+    const float v = zsum4(ws + pl.p1 + (size_t)k * C + c, (size_t)K1 * C, 0, pl.chunks, red);
+    if (wave0 && ok) dw1[(size_t)c * K1 + k] = v;
     return;
   }
-  e -= n1;
-  if (e < n2) {
-    const int c = (int)(e / K2), k = (int)(e % K2);
-    float s = 0.f;
-    for (int z = 0; z < pl.chunks; ++z) s += ws[pl.p2 + ((size_t)z * K2 + k) * C + c];
-    dw2[e] = s;
+  e -= s1;
+  if (e < s2) {
+    const bool ok = e < n2;
+    const int k = ok ? (int)(e / C) : 0, c = ok ? (int)(e % C) : 0;
+    const float v = zsum4(ws + pl.p2 + (size_t)k * C + c, (size_t)K2 * C, 0, pl.chunks, red);
+    if (wave0 && ok) dw2[(size_t)c * K2 + k] = v;
     return;
   }
-  e -= n2;
-  if (e < nb) {
-    float s = 0.f;
-    for (int z = 0; z < pl.chunks; ++z) s += ws[pl.pb + (size_t)z * C + e];
-    db[e] = s;
+  e -= s2;
+  if (e < sb) {
+    const bool ok = e < nb;
+    const float v = zsum4(ws + pl.pb + (ok ? e : 0), (size_t)C, 0, pl.chunks, red);
+    if (wave0 && ok) db[e] = v;
     return;
   }
-  e -= nb;
-  if (e < ne) {
-    float s = 0.f;
-    for (int z = 0; z < pl.chunks; ++z) s += ws[pl.pe + (size_t)z * E * C + e];
-    demb[e] = s;
+  e -= sb;
+  if (e < se) {
+    const bool ok = e < ne;
+    const float v = zsum4(ws + pl.pe + (ok ? e : 0), (size_t)E * C, 0, pl.chunks, red);
+    if (wave0 && ok) demb[e] = v;
     return;
   }
-  e -= ne;
+  e -= se;
   if (e < ni) {
     const int bb = (int)(e / ((long long)L * C)), rem = (int)(e % ((long long)L * C));
-    float s = 0.f;
-    for (int z = bb * pl.tch; z < (bb + 1) * pl.tch; ++z) s += ws[pl.pi + (size_t)z * L * C + rem];
-    dipa[e] = s;
+    const float v = zsum4(ws + pl.pi + rem, (size_t)L * C, bb * pl.tch, (bb + 1) * pl.tch, red);
+    if (wave0) dipa[e] = v;
   }
 }
 
@@ -302,11 +339,13 @@ __global__ __launch_bounds__(kFThreads) void final_bwd_kernel(int N, int rows_pe
                                                               float* __restrict__ part, FbPlan pl) {
   __shared__ __attribute__((aligned(16))) float ws_[LAT * kFC];
   __shared__ float red[4][kFLat + 2 * kFC];
+  __shared__ float dvs[kFbRows * LAT];  // the block's dv rows (broadcast reads; no per-row global loads)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  for (int i = tid; i < LAT * kFC; i += kFThreads) ws_[i] = w[i];
-  __syncthreads();
   const int b = blockIdx.x / pl.cpb, ch = blockIdx.x % pl.cpb;
   const int r0 = b * rows_per_b + ch * kFbRows, r1 = min(b * rows_per_b + rows_per_b, r0 + kFbRows);
+  for (int i = tid; i < LAT * kFC; i += kFThreads) ws_[i] = w[i];
+  for (int i = tid; i < (r1 - r0) * LAT; i += kFThreads) dvs[i] = dv[(size_t)r0 * LAT + i];
+  __syncthreads();
   float sh[6], sc[6];
   row_ld(mods + (size_t)b * 2 * kFC, lane, sh);
   row_ld(mods + (size_t)b * 2 * kFC + kFC, lane, sc);
@@ -323,7 +362,7 @@ __global__ __launch_bounds__(kFThreads) void final_bwd_kernel(int N, int rows_pe
     for (int e = 0; e < 6; ++e) x[e] = xnext[e];
     if (n + 4 < r1) row_ld(h + (size_t)(n + 4) * kFC, lane, xnext);
     const float2 st = *reinterpret_cast<const float2*>(stats + 2 * (size_t)n);
-    const float* dvr = dv + (size_t)n * LAT;
+    const float* dvr = dvs + (n - r0) * LAT;
     if (lane < LAT) gbl += dvr[lane];
     float d[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -412,23 +451,29 @@ __global__ __launch_bounds__(128) void final_dw_kernel(int N, int rows_per_b, co
 __global__ __launch_bounds__(256) void final_bwd_reduce_kernel(int B, int lat, const float* __restrict__ part,
                                                                FbPlan pl, float* __restrict__ dw,
                                                                float* __restrict__ dbias, float* __restrict__ dmods) {
+  __shared__ float red[256];
   const long long nw = (long long)lat * kFC, nm = (long long)B * 2 * kFC;
-  const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (e < nw) {
-    float s = 0.f;
-    for (int z = 0; z < pl.blocks; ++z) s += part[pl.pw + (size_t)z * nw + e];
-    dw[e] = s;
-  } else if (e < nw + lat) {
-    const int j = (int)(e - nw);
-    float s = 0.f;
-    for (int z = 0; z < pl.blocks; ++z) s += part[pl.pb + (size_t)z * kFLat + j];
-    if (dbias) dbias[j] = s;
-  } else if (e < nw + lat + nm) {
-    const long long i = e - nw - lat;
-    const int bb = (int)(i / (2 * kFC)), c = (int)(i % (2 * kFC));
-    float s = 0.f;
-    for (int z = bb * pl.cpb; z < (bb + 1) * pl.cpb; ++z) s += part[pl.pm + (size_t)z * 2 * kFC + c];
-    dmods[i] = s;
+  const long long sw = (nw + 63) / 64 * 64, sbb = 64;
+  long long e = (long long)blockIdx.x * 64 + (threadIdx.x & 63);
+  const bool wave0 = threadIdx.x < 64;
+  if (e < sw) {
+    const bool ok = e < nw;
+    const float v = zsum4(part + pl.pw + (ok ? e : 0), (size_t)nw, 0, pl.blocks, red);
+    if (wave0 && ok) dw[e] = v;
+    return;
+  }
+  e -= sw;
+  if (e < sbb) {
+    const bool ok = e < lat;
+    const float v = zsum4(part + pl.pb + (ok ? e : 0), (size_t)kFLat, 0, pl.blocks, red);
+    if (wave0 && ok && dbias) dbias[e] = v;
+    return;
+  }
+  e -= sbb;
+  if (e < nm) {
+    const int bb = (int)(e / (2 * kFC)), c = (int)(e % (2 * kFC));
+    const float v = zsum4(part + pl.pm + c, (size_t)2 * kFC, bb * pl.cpb, (bb + 1) * pl.cpb, red);
+    if (wave0) dmods[e] = v;
   }
 }
 
@@ -445,16 +490,18 @@ hipError_t embed_bwd_launch(int B, int T, int L, int C, int K1, const float* x1,
   hipLaunchKernelGGL(embed_bwd_kernel, dim3(pl.chunks, (C + 127) / 128), dim3(256), 0, s, B, T, L, C, K1, x1,
                      x2 ? K2 : 0, x2, idx, E, dh, ws, pl);
   if (hipError_t e = hipGetLastError()) return e;
-  const long long n = (long long)C * K1 + (dw2 && x2 ? (long long)C * K2 : 0) + (db ? C : 0) +
-                      (demb && idx ? (long long)E * C : 0) + (dipa ? (long long)B * L * C : 0);
-  hipLaunchKernelGGL(embed_bwd_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, B, L, C, K1,
+  auto r64 = [](long long v) { return (v + 63) / 64 * 64; };
+  const long long n = r64(dw1 ? (long long)C * K1 : 0) + r64(dw2 && x2 ? (long long)C * K2 : 0) + r64(db ? C : 0) +
+                      r64(demb && idx ? (long long)E * C : 0) + (dipa ? (long long)B * L * C : 0);
+  hipLaunchKernelGGL(embed_bwd_reduce_kernel, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, s, B, L, C, K1,
                      x2 ? K2 : 0, E, ws, pl, dw1, x2 ? dw2 : nullptr, db, idx ? demb : nullptr, dipa);
   return hipGetLastError();
 }
 
 hipError_t final_fwd_train_launch(int N, int rows_per_b, int lat, const float* h, const float* mods, const float* w,
                                   const float* bias, float* v, float* stats, hipStream_t s) {
-  const int grid = min((N + 3) / 4, 2048);
+  // W (LAT x 384 fp32) is staged per block: enough rows per block to amortise it (~16 per wave)
+  const int grid = min((N + 3) / 4, 512);
   if (lat == 21)
     hipLaunchKernelGGL(final_fwd_kernel<21>, dim3(grid), dim3(kFThreads), 0, s, N, rows_per_b, h, mods, w, bias, v, stats);
   else if (lat == 28)
@@ -485,8 +532,8 @@ hipError_t final_bwd_train_launch(int N, int rows_per_b, int lat, const float* h
 #undef MDG_FB
   if (hipError_t e = hipGetLastError()) return e;
   const int B = N / rows_per_b;
-  const long long n = (long long)lat * kFC + lat + (long long)B * 2 * kFC;
-  hipLaunchKernelGGL(final_bwd_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, B, lat, ws, pl, dw,
+  const long long n = ((long long)lat * kFC + 63) / 64 * 64 + 64 + (long long)B * 2 * kFC;
+  hipLaunchKernelGGL(final_bwd_reduce_kernel, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, s, B, lat, ws, pl, dw,
                      dbias, dmods);
   return hipGetLastError();
 }

@@ -421,12 +421,13 @@ struct WgPlan {
   int wide;  // bf16 tile: 0 = 128 x 128, 1 = 256 x 128 (WMT 4), 2 = 128 x 256 (WKT 4)
 };
 
-// MDG_WGRAD_WIDE=0: always the 128 x 128 tile (A/B); MDG_WGRAD_BLOCKS: target block count of the
-// token split (default 512 = 2 per CU)
+// MDG_WGRAD_WIDE=1: the wide tiles for the MLP weights (opt-in: the token split doubles with half
+// the tiles, and the partial round trip eats the per-FLOP gain; 16.48 vs 16.28 ms per training
+// step, same box); MDG_WGRAD_BLOCKS: target block count of the token split (default 512 = 2 per CU)
 static int wgrad_wide_enabled() {
   static const int v = [] {
     const char* e = getenv("MDG_WGRAD_WIDE");
-    return e ? atoi(e) : 1;
+    return e ? atoi(e) : 0;
   }();
   return v;
 }

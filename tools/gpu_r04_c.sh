@@ -10,4 +10,4 @@ bash tools/gpu_steps.sh \
   "bench|240|python bench.py > gpurun_out/r04_bench.json" \
   "prof|200|bash tools/gpu_prof.sh" \
   "prof_b1|150|PROF_DIR=gpurun_out/prof_b1 BENCH_ARGS='--batch 1 --lanes 1' bash tools/gpu_prof.sh" \
-  "prof_tps|150|PROF_DIR=gpurun_out/prof_tps BENCH_ARGS='--tps --frames 100 --batch 16' bash tools/gpu_prof.sh"
+  "dopri5|150|python bench.py --sampler dopri5 --steps 2 --warmup 1 > gpurun_out/r04_bench_dopri5.json"

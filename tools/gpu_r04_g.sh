@@ -1,0 +1,14 @@
+#!/bin/bash
+# Round 4: the rewritten segmented linears and glue kernels (tests, training line, trace), then
+# the wgrad split A/B.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+T="python bench.py --train --batch 8 --no-cpu-baseline --steps 8 --warmup 3"
+bash tools/gpu_steps.sh \
+  "gluetests|300|python -u -m pytest -v --timeout 200 --timeout-method thread -p no:cacheprovider tests/test_gpu_glue.py tests/test_gpu_ipa_train.py tests/test_gpu_train.py -k 'seg or glue or embed or final or ipa or default_dims or gvp or small_loss'" \
+  "train|120|$T > gpurun_out/r04_bench_train.json" \
+  "trainprof|200|bash tools/gpu_train_prof.sh" \
+  "wg_w1_256|100|MDG_WGRAD_WIDE=1 MDG_WGRAD_BLOCKS=256 $T > gpurun_out/wg_w1_256.json" \
+  "wg_w0_256|100|MDG_WGRAD_WIDE=0 MDG_WGRAD_BLOCKS=256 $T > gpurun_out/wg_w0_256.json" \
+  "wg_w0_384|100|MDG_WGRAD_WIDE=0 MDG_WGRAD_BLOCKS=384 $T > gpurun_out/wg_w0_384.json" \
+  "wg_w1_512|100|MDG_WGRAD_WIDE=1 MDG_WGRAD_BLOCKS=512 $T > gpurun_out/wg_w1_512.json"
