@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define MDG_ABI_VERSION 19
+#define MDG_ABI_VERSION 20
 #define MDG_MAX_LAYERS 16
 #define MDG_SEG_MAX 16 /* segments of one mdg_seg_linear */
 #define MDG_DP 32      /* padded head dim of the attention operand buffers for head_dim <= 31 */
@@ -382,6 +382,9 @@ typedef struct {
   void* act;         /* CT [N][F] gelu(u), fc2's input */
   int32_t init_planes; /* nonzero: zero the plane buffers and set their pad columns first
                           (fresh allocations); 0: the pads are already in place */
+  int32_t skip_temporal; /* nonzero: the temporal sublayer is left out (h2 = h1; the IPA layers'
+                            MHA + MLP tail on this block, latent_model.py:341-394, whose temporal
+                            gate is 0): qkv_t / lse_t / o[1] / y[1] / h2 are not written */
 } mdg_layer_saved;
 
 /* Key-padding biases from mask [B,T,L] (0 -> -inf): temporal [B*L][T], spatial [B*T][L]. */
@@ -461,7 +464,8 @@ int mdg_wgrad(int32_t dtype, int32_t N, int32_t M, int32_t K, const void* dy, in
      bwd: from dy[i] [M][lddy[i]]: dw[i] [n[i]][K] = dy^T x', db[i] = column sums of dy (either
           null: skip), and dx [M][lddx] = (sum_i dy[i] w[i]) * SiLU'(x) for SILU (null: skip),
           the weight-row reduction split into chunks of 256 rows whose partials (in ws) are
-          summed in chunk order (deterministic).  ws: mdg_seg_linear_bwd_workspace_bytes. */
+          summed in chunk order (deterministic).  K % 4 == 0, K <= 1024, x and weights 16-B aligned.
+   ws: mdg_seg_linear_bwd_workspace_bytes. */
 typedef struct {
   int32_t nseg;
   int32_t n[MDG_SEG_MAX];

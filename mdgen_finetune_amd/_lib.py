@@ -78,7 +78,7 @@ class MdgGemmDesc(ctypes.Structure):
 class MdgLayerSaved(ctypes.Structure):
     _fields_ = [("xn", _vp * 3), ("stats", _vp * 3), ("qkv_s", _vp), ("lse_s", _vp), ("qkv_t", _vp),
                 ("lse_t", _vp), ("o", _vp * 2), ("o_lo", _vp * 2), ("y", _vp * 3), ("h1", _vp), ("h2", _vp), ("u", _vp), ("act", _vp),
-                ("init_planes", _i32)]
+                ("init_planes", _i32), ("skip_temporal", _i32)]
 
 
 class MdgCondDims(ctypes.Structure):
@@ -185,7 +185,7 @@ SIGNATURES = [
                                   ctypes.c_size_t, _vp]),
 ]
 
-ABI_VERSION = 19
+ABI_VERSION = 20
 _LIB = None
 
 

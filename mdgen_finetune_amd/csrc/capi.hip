@@ -919,27 +919,31 @@ int mdg_layer_fwd_train(const mdg_dims* d, const mdg_layer_weights* w, const flo
   r.resid_in = h_in; r.resid = sv->h1; r.ldr = C; r.gate = mods; r.gate_off = 2 * C; r.aux = sv->y[0]; r.ldaux = C;
   if (int e = mdg_gemm(&r, stream)) return e;
 
-  // ---- temporal sublayer (latent_model.py:474-486)
-  if (int e = ln(sv->h1, 1, 3 * C, 4 * C)) return e;
-  q.epi = MDG_EPI_QKV; q.A = sv->xn[1]; q.W = w->wqkv[1]; q.bias = w->bqkv[1];
-  q.qkv_layout = MDG_QKV_TEMPORAL; q.qkv_out = sv->qkv_t; q.qscale = qs * log2e; q.rope = rope_t; q.rope_rows = T + 1;
-  if (int e = mdg_gemm(&q, stream)) return e;
-  if (int e = mdg_attn_temporal_lse(d->dtype, B, T, L, H, D, sv->qkv_t, kbias_t, w->kvb[1], sv->o[1], sv->o_lo[1], sv->lse_t,
-                                    stream))
-    return e;
-  r.A = sv->o[1]; r.W = w->wo[1]; r.bias = w->bo[1]; r.resid_in = sv->h1; r.resid = sv->h2; r.gate_off = 5 * C;
-  r.aux = sv->y[1];
-  if (int e = mdg_gemm(&r, stream)) return e;
+  // ---- temporal sublayer (latent_model.py:474-486); skipped for the IPA layers' tail (gate 0)
+  const float* h_mlp = sv->h1;
+  if (!sv->skip_temporal) {
+    if (int e = ln(sv->h1, 1, 3 * C, 4 * C)) return e;
+    q.epi = MDG_EPI_QKV; q.A = sv->xn[1]; q.W = w->wqkv[1]; q.bias = w->bqkv[1];
+    q.qkv_layout = MDG_QKV_TEMPORAL; q.qkv_out = sv->qkv_t; q.qscale = qs * log2e; q.rope = rope_t; q.rope_rows = T + 1;
+    if (int e = mdg_gemm(&q, stream)) return e;
+    if (int e = mdg_attn_temporal_lse(d->dtype, B, T, L, H, D, sv->qkv_t, kbias_t, w->kvb[1], sv->o[1], sv->o_lo[1], sv->lse_t,
+                                      stream))
+      return e;
+    r.A = sv->o[1]; r.W = w->wo[1]; r.bias = w->bo[1]; r.resid_in = sv->h1; r.resid = sv->h2; r.gate_off = 5 * C;
+    r.aux = sv->y[1];
+    if (int e = mdg_gemm(&r, stream)) return e;
+    h_mlp = sv->h2;
+  }
 
   // ---- MLP (latent_model.py:488-491)
-  if (int e = ln(sv->h2, 2, 6 * C, 7 * C)) return e;
+  if (int e = ln(h_mlp, 2, 6 * C, 7 * C)) return e;
   mdg_gemm_desc f1 = g;
   f1.epi = MDG_EPI_STORE; f1.act = MDG_ACT_GELU; f1.N = F; f1.K = C; f1.A = sv->xn[2]; f1.lda = C; f1.W = w->w1;
   f1.ldw = C; f1.bias = w->b1; f1.out = sv->act; f1.ldo = F; f1.aux = sv->u; f1.ldaux = F;
   if (int e = mdg_gemm(&f1, stream)) return e;
   mdg_gemm_desc f2 = g;
   f2.epi = MDG_EPI_GATE_RES; f2.N = C; f2.K = F; f2.A = sv->act; f2.lda = F; f2.W = w->w2; f2.ldw = F; f2.bias = w->b2;
-  f2.resid_in = sv->h2; f2.resid = h_out; f2.ldr = C; f2.gate = mods; f2.gate_off = 8 * C; f2.aux = sv->y[2];
+  f2.resid_in = h_mlp; f2.resid = h_out; f2.ldr = C; f2.gate = mods; f2.gate_off = 8 * C; f2.aux = sv->y[2];
   f2.ldaux = C;
   return mdg_gemm(&f2, stream);
 }
@@ -1388,7 +1392,7 @@ static int seg_check(const char* what, int32_t M, int32_t K, const float* x, int
   if (mdg::seg_total(s) <= 0)
     return fail(MDG_E_SHAPE, "%s: nseg %d (1..%d, every n > 0)", what, s->nseg, MDG_SEG_MAX);
   if (!mdg::seg_linear_shape_ok(M, K) || ldx < K || ldx % 4 || ((uintptr_t)x & 15))
-    return fail(MDG_E_SHAPE, "%s: M=%d K=%d ldx=%d (K %% 4 == 0, K <= 1536, x 16-B aligned, ldx %% 4 == 0)", what, M,
+    return fail(MDG_E_SHAPE, "%s: M=%d K=%d ldx=%d (K %% 4 == 0, K <= 1024, x 16-B aligned, ldx %% 4 == 0)", what, M,
                 K, ldx);
   for (int i = 0; i < s->nseg; ++i)
     if ((uintptr_t)s->w[i] & 15) return fail(MDG_E_SHAPE, "%s: weight %d not 16-B aligned", what, i);

@@ -30,7 +30,7 @@ namespace mdg {
 namespace {
 
 constexpr int kSlMaxM = 32;   // token rows per block (grid.y covers more)
-constexpr int kSlMaxK = 1536;  // input width (x' rows staged in LDS)
+constexpr int kSlMaxK = 1024;  // input width (32 x' rows staged in LDS: 128 KiB)
 constexpr int kSlChunk = 256;  // dX: weight rows per partial
 
 struct SegMap {

@@ -279,6 +279,7 @@ class _HipLayerFn(torch.autograd.Function):
         cs.o_lo[0], cs.o_lo[1] = _lib.ptr(sv["o_lo"][0]), _lib.ptr(sv["o_lo"][1])
         cs.h1, cs.h2, cs.u, cs.act = sv["h1"].data_ptr(), sv["h2"].data_ptr(), sv["u"].data_ptr(), sv["act"].data_ptr()
         cs.init_planes = int(fresh_t or fresh_s)
+        cs.skip_temporal = int(bool(tail))  # the IPA layers' tail: gate 0, h2 = h1
         h_out = torch.empty_like(h)
         _lib.check(lib.mdg_layer_fwd_train(ctypes.byref(dims), ctypes.byref(lw), _lib.ptr(rope_l), _lib.ptr(rope_t),
                                            mods.data_ptr(), mask.data_ptr(), kb_t.data_ptr(), kb_s.data_ptr(),
@@ -341,9 +342,6 @@ class _HipLayerFn(torch.autograd.Function):
         du = dx_gemm(dy_m, P["w2_t"], C, F, _lib.MDG_ACT_DGELU, sv["u"])
         grads["w1"], grads["b1"] = wg(du, sv["xn"][2], True)
         dxn3 = dx_gemm(du, P["w1_t"], F, C)
-        dh2 = e(N, C, dtp=torch.float32)
-        dy_t = r(C)
-        part_t = lngate(dxn3, sv["h2"], sv["stats"][2], 6 * C, 7 * C, dh3, dh2, sv["y"][1], 5 * C, dy_t)
 
         def attention(i, dy, o, o_lo, xn, qkv, lse):
             """out_proj + attention backward of attention i (0 spatial, 1 temporal); returns dxn."""
@@ -378,11 +376,25 @@ class _HipLayerFn(torch.autograd.Function):
             grads[f"wqkv{i}"], grads[f"bqkv{i}"] = wg(dqkv, xn, True)
             return dx_gemm(dqkv, P[f"wqkv_t{i}"], 3 * C, C)
 
-        dxn2 = attention(1, dy_t, sv["o"][1], sv["o_lo"][1], sv["xn"][1], sv["qkv_t"], sv["lse_t"])
         dh1 = e(N, C, dtp=torch.float32)
         dy_s = r(C)
-        part_s = lngate(dxn2, sv["h1"], sv["stats"][1], 3 * C, 4 * C, dh2, dh1, sv["y"][0], 2 * C, dy_s)
+        if ctx.tail:
+            # no temporal sublayer (h2 = h1): the MLP's LN backward hands straight to the spatial
+            # gated residual.  Its partials serve both the spatial and the temporal slots of the
+            # unpack: d gate_l (2C), d shift_m / d scale_m (6C, 7C) and the spatial out_proj bias
+            # land where they belong; the temporal slots (3C..5C, the stand-in bias) get copies,
+            # and the caller drops them (zero adaLN columns, None parameter gradients)
+            part_t = part_s = lngate(dxn3, sv["h1"], sv["stats"][2], 6 * C, 7 * C, dh3, dh1, sv["y"][0], 2 * C, dy_s)
+        else:
+            dh2 = e(N, C, dtp=torch.float32)
+            dy_t = r(C)
+            part_t = lngate(dxn3, sv["h2"], sv["stats"][2], 6 * C, 7 * C, dh3, dh2, sv["y"][1], 5 * C, dy_t)
+            dxn2 = attention(1, dy_t, sv["o"][1], sv["o_lo"][1], sv["xn"][1], sv["qkv_t"], sv["lse_t"])
+            part_s = lngate(dxn2, sv["h1"], sv["stats"][1], 3 * C, 4 * C, dh2, dh1, sv["y"][0], 2 * C, dy_s)
         dxn1 = attention(0, dy_s, sv["o"][0], sv["o_lo"][0], sv["xn"][0], sv["qkv_s"], sv["lse_s"])
+        if ctx.tail:  # the unpack's temporal inputs: attention 0's again (outputs dropped)
+            for k in ("wqkv", "bqkv", "kvb", "wo"):
+                grads[f"{k}1"] = grads[f"{k}0"]
         dh0 = e(N, C, dtp=torch.float32)
         part_0 = lngate(dxn1, h.reshape(N, C), sv["stats"][0], 0, C, dh1, dh0, None, 0, None)
 
@@ -625,5 +637,8 @@ def seg_linear(x, linears, act="none", resid=None):
 
 
 def seg_supported(x):
-    """The segmented linears serve differentiable CUDA fp32 calls (MDG_TRAIN_SEG=0: eager, A/B)."""
-    return x.is_cuda and torch.is_grad_enabled() and os.environ.get("MDG_TRAIN_SEG", "1") != "0"
+    """The segmented linears serve differentiable CUDA fp32 calls with K % 4 == 0 and K <= 1024
+    (MDG_TRAIN_SEG=0: eager, A/B)."""
+    K = x.shape[-1]
+    return (x.is_cuda and torch.is_grad_enabled() and K % 4 == 0 and K <= 1024
+            and os.environ.get("MDG_TRAIN_SEG", "1") != "0")

@@ -64,7 +64,7 @@ int main(void){
         offsetof(mdg_seg_linear, db));
  printf("%zu %zu %zu %zu %zu %zu %zu\n", offsetof(mdg_step_io, dt), offsetof(mdg_step_io, h),
         offsetof(mdg_gemm_desc, qscale), offsetof(mdg_gemm_desc, rope_rows), offsetof(mdg_gemm_desc, aux),
-        offsetof(mdg_gemm_desc, ldaux), offsetof(mdg_layer_saved, init_planes));
+        offsetof(mdg_gemm_desc, ldaux), offsetof(mdg_layer_saved, skip_temporal));
  return 0; }
 """
     with tempfile.TemporaryDirectory() as td:
@@ -91,7 +91,7 @@ int main(void){
                                                  _lib.MdgStepIO, _lib.MdgGemmDesc, _lib.MdgLayerSaved)]
     assert offs == [_lib.MdgStepIO.dt.offset, _lib.MdgStepIO.h.offset, _lib.MdgGemmDesc.qscale.offset,
                     _lib.MdgGemmDesc.rope_rows.offset, _lib.MdgGemmDesc.aux.offset, _lib.MdgGemmDesc.ldaux.offset,
-                    _lib.MdgLayerSaved.init_planes.offset]
+                    _lib.MdgLayerSaved.skip_temporal.offset]
 
 
 def test_shape_validation_without_gpu():
