@@ -486,6 +486,24 @@ size_t mdg_seg_linear_bwd_workspace_bytes(int32_t M, int32_t K, const mdg_seg_li
 int mdg_seg_linear_bwd(int32_t M, int32_t K, const float* x, int32_t ldx, int32_t in_act, const mdg_seg_linear* s,
                        float* dx, int32_t lddx, void* ws, size_t ws_bytes, void* stream);
 
+/* The flow-matching plan and loss of Transport.training_losses (transport.py:137-222, velocity
+   model, path.py:81-191), fp32:
+     mdg_gvp_plan: for trajectory b (n_per_b contiguous elements each), t = t[b]; path 0 = GVP
+       (a = sin(t pi / 2), s = cos(t pi / 2), da = pi/2 cos, ds = -pi/2 sin), 1 = Linear (a = t,
+       s = 1 - t, da = 1, ds = -1): xt = a x1 + s x0, ut = da x1 + ds x0 (torch's rounding order).
+     mdg_gvp_loss_fwd: loss[b] = sum (out - ut)^2 m / sum m over the [T][L][K] elements of b
+       (mean_flat, transport.py:12-16), den[b] = sum m; mask element (b, t, l, k) at
+       b s0 + t s1 + l s2 + k s3 (mask_strides: a broadcast view needs no copy); block partials
+       summed in a fixed order.  ws: mdg_gvp_loss_workspace_bytes(B, T*L*K).
+     mdg_gvp_loss_bwd: dout = 2 (out - ut) m gloss[b] / den[b]. */
+int mdg_gvp_plan(int32_t B, int64_t n_per_b, int32_t path, const float* t, const float* x0, const float* x1, float* xt,
+                 float* ut, void* stream);
+size_t mdg_gvp_loss_workspace_bytes(int32_t B, int64_t n_per_b);
+int mdg_gvp_loss_fwd(int32_t B, int32_t T, int32_t L, int32_t K, const float* out, const float* ut, const float* mask,
+                     const int64_t* mask_strides, float* loss, float* den, void* ws, size_t ws_bytes, void* stream);
+int mdg_gvp_loss_bwd(int32_t B, int32_t T, int32_t L, int32_t K, const float* out, const float* ut, const float* mask,
+                     const int64_t* mask_strides, const float* gloss, const float* den, float* dout, void* stream);
+
 /* Training backward of the token embedding (latent_model.py:242-255 under loss.backward()),
    from the residual gradient dh [N][C] fp32 (N = B*T*L tokens, n = (b*T + t)*L + l):
      dw1 [C][K1]    = sum_n dh[n] x1[n]^T         latent_to_emb.weight (x1 [N][K1], the noised latents)

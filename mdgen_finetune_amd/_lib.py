@@ -179,6 +179,10 @@ SIGNATURES = [
     ("mdg_final_fwd_train", _i32, [_i32] * 4 + [_vp] * 7),
     ("mdg_final_bwd_workspace_bytes", ctypes.c_size_t, [_i32] * 3),
     ("mdg_final_bwd_train", _i32, [_i32] * 4 + [_vp] * 9 + [_vp, ctypes.c_size_t, _vp]),
+    ("mdg_gvp_plan", _i32, [_i32, ctypes.c_int64, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
+    ("mdg_gvp_loss_workspace_bytes", ctypes.c_size_t, [_i32, ctypes.c_int64]),
+    ("mdg_gvp_loss_fwd", _i32, [_i32] * 4 + [_vp] * 7 + [ctypes.c_size_t, _vp]),
+    ("mdg_gvp_loss_bwd", _i32, [_i32] * 4 + [_vp] * 8),
     ("mdg_seg_linear_fwd", _i32, [_i32, _i32, _vp, _i32, _i32, ctypes.POINTER(MdgSegLinear), _vp]),
     ("mdg_seg_linear_bwd_workspace_bytes", ctypes.c_size_t, [_i32, _i32, ctypes.POINTER(MdgSegLinear)]),
     ("mdg_seg_linear_bwd", _i32, [_i32, _i32, _vp, _i32, _i32, ctypes.POINTER(MdgSegLinear), _vp, _i32, _vp,

@@ -108,6 +108,14 @@ hipError_t final_bwd_train_launch(int N, int rows_per_b, int lat, const float* h
 size_t wgrad_ws_bytes(int dtype, int N, int M, int K, bool need_w, bool need_b);
 hipError_t wgrad_launch(int dtype, int N, int M, int K, const void* dy, int ldy, const void* x, int ldx, float* dw,
                         int lddw, float* db, float* ws, hipStream_t s);
+// train_glue.hip: the flow-matching plan and loss
+hipError_t gvp_plan_launch(int B, long long npb, int path, const float* t, const float* x0, const float* x1, float* xt,
+                           float* ut, hipStream_t s);
+size_t gvp_loss_ws_bytes(int B, long long npb);
+hipError_t gvp_loss_fwd_launch(int B, int T, int L, int K, const float* out, const float* ut, const float* mask,
+                               const int64_t* ms, float* loss, float* den, float* ws, hipStream_t s);
+hipError_t gvp_loss_bwd_launch(int B, int T, int L, int K, const float* out, const float* ut, const float* mask,
+                               const int64_t* ms, const float* g, const float* den, float* dout, hipStream_t s);
 // linear_small.hip
 int seg_total(const mdg_seg_linear* s);
 bool seg_linear_shape_ok(int M, int K);
@@ -1377,6 +1385,36 @@ int mdg_wgrad(int32_t dtype, int32_t N, int32_t M, int32_t K, const void* dy, in
   if (!ws || ws_bytes < need) return fail(MDG_E_ARG, "wgrad: workspace %zu < %zu bytes", ws_bytes, need);
   return hip_check(mdg::wgrad_launch(dtype, N, M, K, dy, ldy, x, ldx, dw, lddw, db, (float*)ws, (hipStream_t)stream),
                    "wgrad");
+}
+
+int mdg_gvp_plan(int32_t B, int64_t n_per_b, int32_t path, const float* t, const float* x0, const float* x1, float* xt,
+                 float* ut, void* stream) {
+  if (!t || !x0 || !x1 || !xt || !ut) return fail(MDG_E_ARG, "gvp_plan: null pointer");
+  if (B <= 0 || n_per_b <= 0 || (path != 0 && path != 1)) return fail(MDG_E_SHAPE, "gvp_plan: B=%d n=%lld path=%d", B, (long long)n_per_b, path);
+  return hip_check(mdg::gvp_plan_launch(B, n_per_b, path, t, x0, x1, xt, ut, (hipStream_t)stream), "gvp_plan");
+}
+
+size_t mdg_gvp_loss_workspace_bytes(int32_t B, int64_t n_per_b) {
+  if (B <= 0 || n_per_b <= 0) return 0;
+  return mdg::gvp_loss_ws_bytes(B, n_per_b);
+}
+
+int mdg_gvp_loss_fwd(int32_t B, int32_t T, int32_t L, int32_t K, const float* out, const float* ut, const float* mask,
+                     const int64_t* mask_strides, float* loss, float* den, void* ws, size_t ws_bytes, void* stream) {
+  if (!out || !ut || !mask || !mask_strides || !loss || !den || !ws) return fail(MDG_E_ARG, "gvp_loss_fwd: null pointer");
+  if (B <= 0 || T <= 0 || L <= 0 || K <= 0) return fail(MDG_E_SHAPE, "gvp_loss_fwd: B=%d T=%d L=%d K=%d", B, T, L, K);
+  const size_t need = mdg::gvp_loss_ws_bytes(B, (long long)T * L * K);
+  if (ws_bytes < need) return fail(MDG_E_ARG, "gvp_loss_fwd: workspace %zu < %zu bytes", ws_bytes, need);
+  return hip_check(mdg::gvp_loss_fwd_launch(B, T, L, K, out, ut, mask, mask_strides, loss, den, (float*)ws,
+                                            (hipStream_t)stream), "gvp_loss_fwd");
+}
+
+int mdg_gvp_loss_bwd(int32_t B, int32_t T, int32_t L, int32_t K, const float* out, const float* ut, const float* mask,
+                     const int64_t* mask_strides, const float* gloss, const float* den, float* dout, void* stream) {
+  if (!out || !ut || !mask || !mask_strides || !gloss || !den || !dout) return fail(MDG_E_ARG, "gvp_loss_bwd: null pointer");
+  if (B <= 0 || T <= 0 || L <= 0 || K <= 0) return fail(MDG_E_SHAPE, "gvp_loss_bwd: B=%d T=%d L=%d K=%d", B, T, L, K);
+  return hip_check(mdg::gvp_loss_bwd_launch(B, T, L, K, out, ut, mask, mask_strides, gloss, den, dout,
+                                            (hipStream_t)stream), "gvp_loss_bwd");
 }
 
 size_t mdg_seg_linear_bwd_workspace_bytes(int32_t M, int32_t K, const mdg_seg_linear* s) {

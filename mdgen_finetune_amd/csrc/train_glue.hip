@@ -477,6 +477,107 @@ __global__ __launch_bounds__(256) void final_bwd_reduce_kernel(int B, int lat, c
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// The flow-matching plan and loss of Transport.training_losses (transport.py:137-222, velocity
+// model; path.py:81-191): one pass each instead of ~25 small eager kernels per step.
+//   plan (per element of trajectory b, t = t[b]):
+//     GVP:    u = (t * pi) / 2, a = sin u, s = cos u, da = (pi / 2) cos u, ds = (-pi / 2) sin u
+//     Linear: a = t, s = 1 - t, da = 1, ds = -1
+//     xt = a x1 + s x0, ut = da x1 + ds x0  (products rounded, then the sum: torch's order)
+//   loss_b = sum (out - ut)^2 m / sum m over trajectory b's T x L x K elements (mean_flat,
+//   transport.py:12-16; the mask may be a broadcast view: element strides); backward
+//   d out = 2 (out - ut) m g_b / den_b.
+constexpr int kGvpChunk = 8192;  // elements per partial-sum block
+
+__global__ __launch_bounds__(256) void gvp_plan_kernel(long long npb, long long total, int path, const float* __restrict__ t,
+                                                       const float* __restrict__ x0, const float* __restrict__ x1,
+                                                       float* __restrict__ xt, float* __restrict__ ut) {
+#pragma clang fp contract(off)
+  const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= total) return;
+  const float tb = t[e / npb];
+  const float a0 = x0[e], a1 = x1[e];
+  if (path == 0) {  // GVP
+    const float u = (tb * 3.14159265358979323846f) / 2.0f;
+    const float sa = sinf(u), ca = cosf(u);
+    const float da = 1.57079632679489661923f * ca, ds = -1.57079632679489661923f * sa;
+    xt[e] = __fadd_rn(__fmul_rn(sa, a1), __fmul_rn(ca, a0));
+    ut[e] = __fadd_rn(__fmul_rn(da, a1), __fmul_rn(ds, a0));
+  } else {  // Linear
+    xt[e] = __fadd_rn(__fmul_rn(tb, a1), __fmul_rn(1.0f - tb, a0));
+    ut[e] = __fadd_rn(a1, -a0);
+  }
+}
+
+struct GvpDims {
+  int B, T, L, K;
+  long long ms[4];  // mask element strides (b, t, l, k)
+};
+__device__ __forceinline__ float gvp_mask(const float* m, const GvpDims& d, long long e) {
+  const int k = (int)(e % d.K);
+  const long long r = e / d.K;
+  const int l = (int)(r % d.L);
+  const long long r2 = r / d.L;
+  const int tt = (int)(r2 % d.T), b = (int)(r2 / d.T);
+  return m[b * d.ms[0] + tt * d.ms[1] + l * d.ms[2] + k * d.ms[3]];
+}
+
+// partial sums of (num, den) over chunk `blockIdx.x` of trajectory blockIdx.y, block tree order
+__global__ __launch_bounds__(256) void gvp_loss_part_kernel(GvpDims d, const float* __restrict__ out,
+                                                            const float* __restrict__ ut, const float* __restrict__ m,
+                                                            float* __restrict__ part) {
+  __shared__ float rn[256], rd[256];
+  const long long npb = (long long)d.T * d.L * d.K;
+  const int b = blockIdx.y;
+  const long long c0 = (long long)blockIdx.x * kGvpChunk, c1 = min(npb, c0 + kGvpChunk);
+  float sn = 0.f, sd = 0.f;
+  for (long long i = c0 + threadIdx.x; i < c1; i += 256) {
+    const long long e = (long long)b * npb + i;
+    const float df = out[e] - ut[e], mk = gvp_mask(m, d, e);
+    sn += (df * df) * mk;
+    sd += mk;
+  }
+  rn[threadIdx.x] = sn;
+  rd[threadIdx.x] = sd;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) {
+      rn[threadIdx.x] += rn[threadIdx.x + w];
+      rd[threadIdx.x] += rd[threadIdx.x + w];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    part[((size_t)b * gridDim.x + blockIdx.x) * 2] = rn[0];
+    part[((size_t)b * gridDim.x + blockIdx.x) * 2 + 1] = rd[0];
+  }
+}
+
+__global__ void gvp_loss_final_kernel(int B, int nch, const float* __restrict__ part, float* __restrict__ loss,
+                                      float* __restrict__ den) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  float sn = 0.f, sd = 0.f;
+  for (int c = 0; c < nch; ++c) {
+    sn += part[((size_t)b * nch + c) * 2];
+    sd += part[((size_t)b * nch + c) * 2 + 1];
+  }
+  loss[b] = sn / sd;
+  den[b] = sd;
+}
+
+__global__ __launch_bounds__(256) void gvp_loss_bwd_kernel(GvpDims d, long long total, const float* __restrict__ out,
+                                                           const float* __restrict__ ut, const float* __restrict__ m,
+                                                           const float* __restrict__ g, const float* __restrict__ den,
+                                                           float* __restrict__ dout) {
+#pragma clang fp contract(off)
+  const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= total) return;
+  const int b = (int)(e / ((long long)d.T * d.L * d.K));
+  const float gb = g[b] / den[b];
+  dout[e] = (gb * gvp_mask(m, d, e)) * 2.0f * (out[e] - ut[e]);
+}
+
 }  // namespace
 
 size_t embed_bwd_ws_bytes(int B, int T, int L, int C, int K1, int K2, int E) {
@@ -535,6 +636,46 @@ hipError_t final_bwd_train_launch(int N, int rows_per_b, int lat, const float* h
   const long long n = ((long long)lat * kFC + 63) / 64 * 64 + 64 + (long long)B * 2 * kFC;
   hipLaunchKernelGGL(final_bwd_reduce_kernel, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, s, B, lat, ws, pl, dw,
                      dbias, dmods);
+  return hipGetLastError();
+}
+
+hipError_t gvp_plan_launch(int B, long long npb, int path, const float* t, const float* x0, const float* x1, float* xt,
+                           float* ut, hipStream_t s) {
+  const long long total = (long long)B * npb;
+  hipLaunchKernelGGL(gvp_plan_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, npb, total, path, t, x0,
+                     x1, xt, ut);
+  return hipGetLastError();
+}
+
+static GvpDims gvp_dims(int B, int T, int L, int K, const int64_t* ms) {
+  GvpDims d;
+  d.B = B, d.T = T, d.L = L, d.K = K;
+  for (int i = 0; i < 4; ++i) d.ms[i] = ms[i];
+  return d;
+}
+
+size_t gvp_loss_ws_bytes(int B, long long npb) {
+  const long long nch = (npb + kGvpChunk - 1) / kGvpChunk;
+  return (size_t)B * nch * 2 * sizeof(float) + 256;
+}
+
+hipError_t gvp_loss_fwd_launch(int B, int T, int L, int K, const float* out, const float* ut, const float* mask,
+                               const int64_t* ms, float* loss, float* den, float* ws, hipStream_t s) {
+  const GvpDims d = gvp_dims(B, T, L, K, ms);
+  const long long npb = (long long)T * L * K;
+  const int nch = (int)((npb + kGvpChunk - 1) / kGvpChunk);
+  hipLaunchKernelGGL(gvp_loss_part_kernel, dim3(nch, B), dim3(256), 0, s, d, out, ut, mask, ws);
+  if (hipError_t e = hipGetLastError()) return e;
+  hipLaunchKernelGGL(gvp_loss_final_kernel, dim3((B + 63) / 64), dim3(64), 0, s, B, nch, (const float*)ws, loss, den);
+  return hipGetLastError();
+}
+
+hipError_t gvp_loss_bwd_launch(int B, int T, int L, int K, const float* out, const float* ut, const float* mask,
+                               const int64_t* ms, const float* g, const float* den, float* dout, hipStream_t s) {
+  const GvpDims d = gvp_dims(B, T, L, K, ms);
+  const long long total = (long long)B * T * L * K;
+  hipLaunchKernelGGL(gvp_loss_bwd_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, d, total, out, ut,
+                     mask, g, den, dout);
   return hipGetLastError();
 }
 

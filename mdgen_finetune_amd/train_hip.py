@@ -642,3 +642,53 @@ def seg_supported(x):
     K = x.shape[-1]
     return (x.is_cuda and torch.is_grad_enabled() and K % 4 == 0 and K <= 1024
             and os.environ.get("MDG_TRAIN_SEG", "1") != "0")
+
+
+# ------------------------------------------------------------------------------------------
+# The flow-matching plan and loss (transport.py:137-222) as library launches
+# (csrc/train_glue.hip, mdg_gvp_plan / mdg_gvp_loss_fwd / _bwd).
+
+def gvp_plan(t, x0, x1, path):
+    """(xt, ut) of the GVP (path 0) or Linear (1) plan; t [B], x0 / x1 [B, ...] fp32."""
+    lib = _lib.load()
+    x0c, x1c, tc = x0.contiguous(), x1.contiguous(), t.float().contiguous()
+    xt, ut = torch.empty_like(x1c), torch.empty_like(x1c)
+    B = x1c.shape[0]
+    _lib.check(lib.mdg_gvp_plan(B, x1c.numel() // B, path, tc.data_ptr(), x0c.data_ptr(), x1c.data_ptr(),
+                                xt.data_ptr(), ut.data_ptr(), _lib.stream_handle()), "mdg_gvp_plan")
+    return xt, ut
+
+
+class _GvpLossFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, out, ut, mask):
+        lib = _lib.load()
+        B, T, L, K = out.shape
+        o, u = out.detach().contiguous(), ut.detach().contiguous()
+        m = mask.detach().expand(B, T, L, K)
+        ms = (ctypes.c_int64 * 4)(*m.stride())
+        loss = torch.empty(B, device=out.device)
+        den = torch.empty(B, device=out.device)
+        wsb = lib.mdg_gvp_loss_workspace_bytes(B, T * L * K)
+        ws = torch.empty(wsb, device=out.device, dtype=torch.uint8)
+        _lib.check(lib.mdg_gvp_loss_fwd(B, T, L, K, o.data_ptr(), u.data_ptr(), m.data_ptr(), ms, loss.data_ptr(),
+                                        den.data_ptr(), ws.data_ptr(), wsb, _lib.stream_handle()), "mdg_gvp_loss_fwd")
+        ctx.save_for_backward(o, u, m, den)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        lib = _lib.load()
+        o, u, m, den = ctx.saved_tensors
+        B, T, L, K = o.shape
+        ms = (ctypes.c_int64 * 4)(*m.stride())
+        gc = g.float().contiguous()
+        dout = torch.empty_like(o)
+        _lib.check(lib.mdg_gvp_loss_bwd(B, T, L, K, o.data_ptr(), u.data_ptr(), m.data_ptr(), ms, gc.data_ptr(),
+                                        den.data_ptr(), dout.data_ptr(), _lib.stream_handle()), "mdg_gvp_loss_bwd")
+        return dout, None, None
+
+
+def gvp_loss(out, ut, mask):
+    """mean_flat((out - ut) ** 2, mask) per trajectory [B] with its backward on the library."""
+    return _GvpLossFn.apply(out, ut, mask)

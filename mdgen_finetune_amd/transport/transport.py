@@ -112,6 +112,13 @@ class Transport:
         if model_kwargs is None:
             model_kwargs = {}
         t, x0, x1 = self.sample(x1)
+        if _hip_loss_ok(model, x1, mask):  # the plan and the loss as library launches (train_glue.hip)
+            from ..train_hip import gvp_loss, gvp_plan
+
+            xt, ut = gvp_plan(t, x0, x1, 0 if isinstance(self.path_sampler, GVPCPlan) else 1)
+            out = model(xt, t, **model_kwargs)
+            assert out.size() == xt.size()
+            return {"t": t, "pred": out, "loss": gvp_loss(out, ut, mask)}
         t, xt, ut = self.path_sampler.plan(t, x0, x1)
         out = model(xt, t, **model_kwargs)
         assert out.size() == xt.size()
@@ -124,6 +131,21 @@ class Transport:
             return out
 
         return body_fn
+
+
+def _hip_loss_ok(model, x1, mask):
+    """The fused plan / loss serve the HIP training path: a CUDA fp32 batch under autograd, a model
+    whose backend and train_backend are 'hip' (a DDP wrapper's .module counts), a [B,T,L,K]-
+    broadcastable fp32 mask (MDG_TRAIN_GVP=0: eager)."""
+    import os
+
+    m = getattr(model, "module", model)
+    if os.environ.get("MDG_TRAIN_GVP", "1") == "0" or not (x1.is_cuda and torch.is_grad_enabled()):
+        return False
+    if getattr(m, "backend", None) != "hip" or getattr(m, "train_backend", None) != "hip":
+        return False
+    return (x1.dtype == torch.float32 and x1.dim() == 4 and mask is not None and mask.dtype == torch.float32
+            and mask.dim() == 4)
 
 
 def _hip_model_of(model, x):

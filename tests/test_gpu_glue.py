@@ -131,3 +131,32 @@ def test_seg_linear_forward_and_backward_match_fp64(lead, K, ns, act, resid):
     want = [xd.grad] + [t.grad for pair in wd for t in pair] + ([rd.grad] if resid else [])
     for i, (a, b) in enumerate(zip(got, want)):
         assert _rel(a, b) <= 2e-6, (i, _rel(a, b))
+
+
+@pytest.mark.parametrize("path", [0, 1])
+def test_gvp_plan_and_loss_match_eager(path):
+    """mdg_gvp_plan / mdg_gvp_loss_fwd / _bwd (train_glue.hip) against the eager GVP / Linear plan
+    and mean_flat loss of transport.py (the mask a broadcast view over frames, as prep_batch
+    builds it): xt, ut to 1 ulp-level, loss and d out at ||d|| / ||ref|| <= 1e-6."""
+    from mdgen_finetune_amd.train_hip import gvp_loss, gvp_plan
+    from mdgen_finetune_amd.transport.transport import GVPCPlan, ICPlan, mean_flat
+
+    torch.manual_seed(7 + path)
+    B, T, L, K, dev = 3, 50, 4, 21, "cuda"
+    x1 = torch.randn(B, T, L, K, device=dev)
+    x0 = torch.randn_like(x1)
+    t = torch.rand(B, device=dev)
+    _, xt_ref, ut_ref = (GVPCPlan() if path == 0 else ICPlan()).plan(t, x0, x1)
+    xt, ut = gvp_plan(t, x0, x1, path)
+    assert _rel(xt, xt_ref) <= 1e-6 and _rel(ut, ut_ref) <= 1e-6, (_rel(xt, xt_ref), _rel(ut, ut_ref))
+    mask = (torch.rand(B, 1, L, K, device=dev) > 0.3).float().expand(B, T, L, K)
+    out = torch.randn(B, T, L, K, device=dev, requires_grad=True)
+    g = torch.rand(B, device=dev)
+    loss = gvp_loss(out, ut_ref, mask)
+    (loss * g).sum().backward()
+    d_got = out.grad.clone()
+    out.grad = None
+    ref = mean_flat((out - ut_ref) ** 2, mask)
+    (ref * g).sum().backward()
+    assert _rel(loss, ref) <= 1e-6, _rel(loss, ref)
+    assert _rel(d_got, out.grad) <= 1e-6, _rel(d_got, out.grad)
