@@ -140,11 +140,11 @@ def _hip_loss_ok(model, x1, mask):
     import os
 
     m = getattr(model, "module", model)
-    if os.environ.get("MDG_TRAIN_GVP", "1") == "0" or not (x1.is_cuda and torch.is_grad_enabled()):
+    if os.environ.get("MDG_TRAIN_GVP", "1") == "0" or not (x1.is_cuda and th.is_grad_enabled()):
         return False
     if getattr(m, "backend", None) != "hip" or getattr(m, "train_backend", None) != "hip":
         return False
-    return (x1.dtype == torch.float32 and x1.dim() == 4 and mask is not None and mask.dtype == torch.float32
+    return (x1.dtype == th.float32 and x1.dim() == 4 and mask is not None and mask.dtype == th.float32
             and mask.dim() == 4)
 
 
