@@ -31,7 +31,7 @@ namespace {
 
 constexpr int kSlMaxM = 32;   // token rows per block (grid.y covers more)
 constexpr int kSlMaxK = 1024;  // input width (32 x' rows staged in LDS: 128 KiB)
-constexpr int kSlChunk = 256;  // dX: weight rows per partial
+constexpr int kSlChunk = 128;  // dX: weight rows per block (row groups of it give the partials)
 
 struct SegMap {
   int nseg, total;
@@ -157,6 +157,7 @@ __global__ __launch_bounds__(256) void sl_bwd_kernel(const SlBwdArgs a) {
     float* dys = sm_ + kSlMaxM * a.K;  // [32][64]
     const int n0 = blockIdx.x * 64;
     const int tk = t & 31, tn = t >> 5, k4 = a.K >> 2;
+    float dbacc = 0.f;  // thread t < 64: db of weight row n0 + t (first column pass)
     for (int i0 = tk; i0 - tk < k4; i0 += 32 * 3) {  // up to 3 float4 column groups per pass
       float4 acc[3][8];
 #pragma unroll
@@ -177,6 +178,8 @@ __global__ __launch_bounds__(256) void sl_bwd_kernel(const SlBwdArgs a) {
           dys[m * 64 + c] = v;
         }
         __syncthreads();
+        if (i0 == tk && t < 64)
+          for (int m = 0; m < mc; ++m) dbacc += dys[m * 64 + t];
         for (int m = 0; m < mc; ++m) {
           float4 xv[3];
 #pragma unroll
@@ -211,26 +214,29 @@ __global__ __launch_bounds__(256) void sl_bwd_kernel(const SlBwdArgs a) {
         }
       }
     }
-    if (t < 64) {  // db, m ascending (dy straight from global memory)
+    if (t < 64) {  // db, m ascending
       const int n = n0 + t;
       if (n < a.sm.total) {
         const int s = seg_of(a.sm, n);
-        if (a.db[s]) {
-          const float* col = a.dy[s] + (n - a.sm.start[s]);
-          float sum = 0.f;
-          for (int m = 0; m < a.M; ++m) sum += col[(size_t)m * a.lddy[s]];
-          a.db[s][n - a.sm.start[s]] = sum;
-        }
+        if (a.db[s]) a.db[s][n - a.sm.start[s]] = dbacc;
       }
     }
     return;
   }
-  // dX partial of one chunk of weight rows, token chunks of 32
+  // dX partial of one chunk of kSlChunk weight rows, token chunks of 32: thread = (float4 column
+  // group cg, row group rg); row group rg takes rows rg, rg + RG, ... of the chunk, four at a time
+  // with their weight loads issued together (row pointers computed per row, no loop-carried
+  // address), and writes its own partial P[chunk * RG + rg][m][k] (the reduce sums them in order)
   const int ch = blockIdx.x - a.n_dw_blocks;
   const int j0 = ch * kSlChunk, j1 = min(j0 + kSlChunk, a.sm.total), nc = j1 - j0;
   float* dys = sm_;  // [kSlChunk][32]
-  const int k4 = a.K >> 2;
-  float* P = a.part + (size_t)ch * a.M * a.K;
+  const int k4 = a.K >> 2, RG = 256 / k4, cg = t % k4, rg = t / k4;
+  const bool act_t = rg < RG;
+  float* P = a.part + (size_t)(ch * RG + (act_t ? rg : 0)) * a.M * a.K;
+  auto wrow = [&](int jj) {
+    const int n = j0 + jj, s = seg_of(a.sm, n);
+    return reinterpret_cast<const float4*>(a.w[s] + (size_t)(n - a.sm.start[s]) * a.K) + cg;
+  };
   for (int mb = 0; mb < a.M; mb += kSlMaxM) {
     const int mc = min(kSlMaxM, a.M - mb);
     __syncthreads();
@@ -240,45 +246,65 @@ __global__ __launch_bounds__(256) void sl_bwd_kernel(const SlBwdArgs a) {
       dys[jj * kSlMaxM + m] = a.dy[s][(size_t)(mb + m) * a.lddy[s] + (n - a.sm.start[s])];
     }
     __syncthreads();
-    for (int c = t; c < k4; c += 256) {
-      float4 acc[kSlMaxM];
+    if (!act_t) continue;
+    float4 acc[kSlMaxM];
 #pragma unroll
-      for (int m = 0; m < kSlMaxM; ++m) acc[m] = make_float4(0.f, 0.f, 0.f, 0.f);
-      int s = seg_of(a.sm, j0), send = a.sm.start[s + 1];
-      for (int jj = 0; jj < nc; ++jj) {
-        const int n = j0 + jj;
-        while (n >= send && s + 1 < a.sm.nseg) {
-          ++s;
-          send = a.sm.start[s + 1];
-        }
-        const float4 w4 = *reinterpret_cast<const float4*>(a.w[s] + (size_t)(n - a.sm.start[s]) * a.K + 4 * c);
+    for (int m = 0; m < kSlMaxM; ++m) acc[m] = make_float4(0.f, 0.f, 0.f, 0.f);
+    auto use = [&](int jj, const float4 w4) {
 #pragma unroll
-        for (int m = 0; m < kSlMaxM; ++m) {
-          if (m < mc) {
-            const float d = dys[jj * kSlMaxM + m];
-            acc[m].x = fmaf(d, w4.x, acc[m].x);
-            acc[m].y = fmaf(d, w4.y, acc[m].y);
-            acc[m].z = fmaf(d, w4.z, acc[m].z);
-            acc[m].w = fmaf(d, w4.w, acc[m].w);
-          }
+      for (int m = 0; m < kSlMaxM; ++m) {
+        if (m < mc) {
+          const float d = dys[jj * kSlMaxM + m];
+          acc[m].x = fmaf(d, w4.x, acc[m].x);
+          acc[m].y = fmaf(d, w4.y, acc[m].y);
+          acc[m].z = fmaf(d, w4.z, acc[m].z);
+          acc[m].w = fmaf(d, w4.w, acc[m].w);
         }
       }
-#pragma unroll
-      for (int m = 0; m < kSlMaxM; ++m)
-        if (m < mc) *reinterpret_cast<float4*>(P + (size_t)(mb + m) * a.K + 4 * c) = acc[m];
+    };
+    int jj = rg;
+    for (; jj + 3 * RG < nc; jj += 4 * RG) {
+      const float4 w0 = *wrow(jj), w1 = *wrow(jj + RG), w2 = *wrow(jj + 2 * RG), w3 = *wrow(jj + 3 * RG);
+      use(jj, w0);
+      use(jj + RG, w1);
+      use(jj + 2 * RG, w2);
+      use(jj + 3 * RG, w3);
     }
+    for (; jj < nc; jj += RG) use(jj, *wrow(jj));
+#pragma unroll
+    for (int m = 0; m < kSlMaxM; ++m)
+      if (m < mc) *reinterpret_cast<float4*>(P + (size_t)(mb + m) * a.K + 4 * cg) = acc[m];
   }
 }
 
-// dx[m][k] = (sum over chunks, in order) * SiLU'(x) (act SILU) or as is
-__global__ __launch_bounds__(256) void sl_dx_reduce_kernel(int M, int K, int chunks, const float* __restrict__ part,
+// dx[m][k] = (sum over the Z partials, in a fixed order) * SiLU'(x) (act SILU) or as is; 64
+// outputs per block, the four waves take a quarter of the partials each and wave 0 adds the four
+__global__ __launch_bounds__(256) void sl_dx_reduce_kernel(int M, int K, int Z, const float* __restrict__ part,
                                                            const float* __restrict__ x, int ldx, int act,
                                                            float* __restrict__ dx, int lddx) {
-  const int e = blockIdx.x * 256 + threadIdx.x;
-  if (e >= M * K) return;
+  __shared__ float red[256];
+  const int lane = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int e = blockIdx.x * 64 + lane;
+  const bool ok = e < M * K;
+  const size_t zs = (size_t)M * K;
+  const int za = q * Z / 4, zb = (q + 1) * Z / 4;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (ok) {
+    const float* p = part + e;
+    int z = za;
+    for (; z + 4 <= zb; z += 4) {
+      s0 += p[(size_t)z * zs];
+      s1 += p[(size_t)(z + 1) * zs];
+      s2 += p[(size_t)(z + 2) * zs];
+      s3 += p[(size_t)(z + 3) * zs];
+    }
+    for (; z < zb; ++z) s0 += p[(size_t)z * zs];
+  }
+  red[threadIdx.x] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (q != 0 || !ok) return;
+  float s = ((red[lane] + red[64 + lane]) + red[128 + lane]) + red[192 + lane];
   const int m = e / K, k = e - m * K;
-  float s = 0.f;
-  for (int c = 0; c < chunks; ++c) s += part[(size_t)c * M * K + e];
   if (act == MDG_ACT_SILU) s *= dsilu_f(x[(size_t)m * ldx + k]);
   dx[(size_t)m * lddx + k] = s;
 }
@@ -306,9 +332,11 @@ int seg_total(const mdg_seg_linear* s) {
   return seg_map(s, sm) ? sm.total : -1;
 }
 
+static int sl_row_groups(int K) { return 256 / (K >> 2); }
+
 size_t seg_linear_ws_bytes(int M, int K, int total) {
   const int chunks = (total + kSlChunk - 1) / kSlChunk;
-  return (size_t)chunks * M * K * sizeof(float);
+  return (size_t)chunks * sl_row_groups(K) * M * K * sizeof(float);
 }
 
 bool seg_linear_shape_ok(int M, int K) { return M > 0 && K > 0 && K % 4 == 0 && K <= kSlMaxK; }
@@ -367,7 +395,7 @@ hipError_t seg_linear_bwd_launch(int M, int K, const float* x, int ldx, int act,
   const int nblk = a.n_dw_blocks + a.chunks;
   if (nblk > 0) hipLaunchKernelGGL(sl_bwd_kernel, dim3(nblk), dim3(256), smem, st, a);
   if (dx)
-    hipLaunchKernelGGL(sl_dx_reduce_kernel, dim3((M * K + 255) / 256), dim3(256), 0, st, M, K, a.chunks,
+    hipLaunchKernelGGL(sl_dx_reduce_kernel, dim3((M * K + 63) / 64), dim3(256), 0, st, M, K, a.chunks * sl_row_groups(K),
                        (const float*)ws, x, ldx, act, dx, lddx);
   return hipGetLastError();
 }

@@ -13,9 +13,9 @@
 //    mask_to_emb row sums.  The chunk's x rows are staged in LDS (broadcast reads), dh is read
 //    once, coalesced.  Per-chunk partials, then one launch sums them in chunk order
 //    (deterministic).  HBM: one pass over dh (49 MB at B=8, T=1000, L=4).
-//  * final_fwd: one wave per token row: LN statistics as two wave reductions (6 columns per
-//    lane), the modulate, and the 21 output dots from W in LDS, reduced by a halving
-//    transpose-sum (32 shuffles for 32 outputs); writes v and (mean, rstd).
+//  * final_fwd: 32 rows per block: LN statistics as two wave reductions (6 columns per lane)
+//    and the modulate into LDS, then one thread per (row, output group of 3) for the 21 output
+//    dots; writes v and (mean, rstd).
 //  * final_bwd: one wave per row, rows of one trajectory per block: dxn = dv W, the LN +
 //    modulate backward into dh, and per-wave register accumulators of dW (6 columns x 21
 //    outputs per lane), dbias, d shift, d scale; block partials summed in order by a reduce
@@ -82,42 +82,46 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(int B, int T, int L, int
   for (int u = 0; u < kEbEMax; ++u) esum[u] = 0.f;
   const float (*X)[kEbK] = xs[op];
   const float* dcol = dh + n0 * C + c;
-  // rows in groups of 8 with their dh (and mask index) loads issued up front: one dependent
-  // HBM round trip per group instead of per row
-  for (int rb = 0; rb < ntok; rb += 8) {
-    float gv[8];
-    int ev[8];
+  auto row = [&](int r, float g, int e) {
+    const int l = r % L;
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      gv[u] = rb + u < ntok ? dcol[(size_t)(rb + u) * C] : 0.f;
-      ev[u] = (op && idx && rb + u < ntok) ? (int)idx[n0 + rb + u] : -1;
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int r = rb + u;
-      if (r >= ntok) break;
-      const int l = r % L;
-      const float g = gv[u];
-#pragma unroll
-      for (int k4 = 0; k4 < kEbK; k4 += 4) {
-        if (k4 < K) {
-          const float4 xv = *reinterpret_cast<const float4*>(&X[r][k4]);
-          acc[k4] = fmaf(g, xv.x, acc[k4]);
-          acc[k4 + 1] = fmaf(g, xv.y, acc[k4 + 1]);
-          acc[k4 + 2] = fmaf(g, xv.z, acc[k4 + 2]);
-          acc[k4 + 3] = fmaf(g, xv.w, acc[k4 + 3]);
-        }
-      }
-      if (op == 0) {
-        cs += g;
-#pragma unroll
-        for (int q = 0; q < kEbLMax; ++q) lsum[q] += (q == l) ? g : 0.f;
-      } else if (idx) {
-#pragma unroll
-        for (int q = 0; q < kEbEMax; ++q) esum[q] += (q == ev[u]) ? g : 0.f;
+    for (int k4 = 0; k4 < kEbK; k4 += 4) {
+      if (k4 < K) {
+        const float4 xv = *reinterpret_cast<const float4*>(&X[r][k4]);
+        acc[k4] = fmaf(g, xv.x, acc[k4]);
+        acc[k4 + 1] = fmaf(g, xv.y, acc[k4 + 1]);
+        acc[k4 + 2] = fmaf(g, xv.z, acc[k4 + 2]);
+        acc[k4 + 3] = fmaf(g, xv.w, acc[k4 + 3]);
       }
     }
+    if (op == 0) {
+      cs += g;
+#pragma unroll
+      for (int q = 0; q < kEbLMax; ++q) lsum[q] += (q == l) ? g : 0.f;
+    } else if (idx) {
+#pragma unroll
+      for (int q = 0; q < kEbEMax; ++q) esum[q] += (q == e) ? g : 0.f;
+    }
+  };
+  // rows in groups of 4 whose dh (and mask index) loads are issued before any of them is used:
+  // one dependent HBM round trip per group instead of per row
+  int rr = 0;
+  for (; rr + 4 <= ntok; rr += 4) {
+    const float g0 = dcol[(size_t)rr * C], g1 = dcol[(size_t)(rr + 1) * C], g2 = dcol[(size_t)(rr + 2) * C],
+                g3 = dcol[(size_t)(rr + 3) * C];
+    int e0 = -1, e1 = -1, e2 = -1, e3 = -1;
+    if (op && idx) {
+      e0 = (int)idx[n0 + rr];
+      e1 = (int)idx[n0 + rr + 1];
+      e2 = (int)idx[n0 + rr + 2];
+      e3 = (int)idx[n0 + rr + 3];
+    }
+    row(rr, g0, e0);
+    row(rr + 1, g1, e1);
+    row(rr + 2, g2, e2);
+    row(rr + 3, g3, e3);
   }
+  for (; rr < ntok; ++rr) row(rr, dcol[(size_t)rr * C], (op && idx) ? (int)idx[n0 + rr] : -1);
   {  // [chunk][k][C]: each store instruction writes 64 consecutive floats
     float* P = ws + (op ? pl.p2 : pl.p1) + (size_t)chunk * K * C + c;
 #pragma unroll
@@ -258,56 +262,71 @@ __device__ __forceinline__ void ln_row(const float (&x)[6], float& mean, float& 
   rstd = rsqrtf(wave_sum(v) * (1.0f / kFC) + 1e-6f);
 }
 
-// W [LAT][C] staged in LDS and re-read per row as float2 (the compiler would otherwise keep
-// all 6 x LAT values of a lane live in VGPRs and drop the kernel to one wave per SIMD); the
-// next row's h is loaded while the current one computes.
+// 32 rows per block.  Phase 1: wave w LN-modulates rows w, w + 4, ... (their h rows loaded
+// together) into LDS.  Phase 2: thread = (row r, output group g) dots row r with W rows g, g + 8,
+// ... (W read as float4 through the caches, the row from LDS: lanes 32-63 share lanes 0-31's rows).
+constexpr int kFfRows = 32, kFfPad = kFC + 4;
 template <int LAT>
 __global__ __launch_bounds__(kFThreads) void final_fwd_kernel(int N, int rows_per_b, const float* __restrict__ h,
                                                               const float* __restrict__ mods,
                                                               const float* __restrict__ w,
                                                               const float* __restrict__ bias, float* __restrict__ v,
                                                               float* __restrict__ stats) {
-  __shared__ __attribute__((aligned(16))) float ws_[LAT * kFC];
+  __shared__ __attribute__((aligned(16))) float xs[kFfRows * kFfPad];
+  constexpr int RW = kFfRows / 4;  // rows per wave
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  for (int i = tid; i < LAT * kFC; i += kFThreads) ws_[i] = w[i];
-  __syncthreads();
-  const int jo = transpose_sum_index(lane);
-  const float bj = (jo < LAT && bias) ? bias[jo] : 0.f;
-  int n = blockIdx.x * 4 + wave;
-  const int stride = gridDim.x * 4;
-  float xnext[6];
-  if (n < N) row_ld(h + (size_t)n * kFC, lane, xnext);
-  for (; n < N; n += stride) {
-    asm volatile("" ::: "memory");  // W re-read from LDS each row (see above)
-    float x[6], sh[6], sc[6];
+  const int r0 = blockIdx.x * kFfRows;
+  float x[RW][6];
 #pragma unroll
-    for (int e = 0; e < 6; ++e) x[e] = xnext[e];
-    if (n + stride < N) row_ld(h + (size_t)(n + stride) * kFC, lane, xnext);
+  for (int i = 0; i < RW; ++i) {
+    const int n = r0 + wave + 4 * i;
+    if (n < N) row_ld(h + (size_t)n * kFC, lane, x[i]);
+  }
+#pragma unroll
+  for (int i = 0; i < RW; ++i) {
+    const int rr = wave + 4 * i, n = r0 + rr;
+    if (n >= N) break;
     const float* mrow = mods + (size_t)(n / rows_per_b) * 2 * kFC;
+    float sh[6], sc[6];
     row_ld(mrow, lane, sh);
     row_ld(mrow + kFC, lane, sc);
     float mean, rstd;
-    ln_row(x, mean, rstd);
+    ln_row(x[i], mean, rstd);
     float xn[6];
 #pragma unroll
-    for (int e = 0; e < 6; ++e) xn[e] = (x[e] - mean) * rstd * (1.0f + sc[e]) + sh[e];
-    float p[kFLat];
-#pragma unroll
-    for (int j = 0; j < kFLat; ++j) {
-      float s = 0.f;
-      if (j < LAT) {
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-          const float2 wv = *reinterpret_cast<const float2*>(&ws_[j * kFC + 2 * lane + 128 * i]);
-          s = fmaf(xn[2 * i], wv.x, s);
-          s = fmaf(xn[2 * i + 1], wv.y, s);
-        }
-      }
-      p[j] = s;
-    }
-    const float out = transpose_sum32(p, lane) + bj;
-    if (!(lane & 1) && jo < LAT) v[(size_t)n * LAT + jo] = out;
+    for (int e = 0; e < 6; ++e) xn[e] = (x[i][e] - mean) * rstd * (1.0f + sc[e]) + sh[e];
+    row_st(xs + rr * kFfPad, lane, xn);
     if (lane == 0) *reinterpret_cast<float2*>(stats + 2 * (size_t)n) = make_float2(mean, rstd);
+  }
+  __syncthreads();
+  constexpr int NJ = (LAT + 7) / 8;
+  const int r = tid & 31, g = tid >> 5, n = r0 + r;
+  float acc[NJ];
+#pragma unroll
+  for (int jj = 0; jj < NJ; ++jj) acc[jj] = 0.f;
+  const float4* xr = reinterpret_cast<const float4*>(xs + r * kFfPad);
+  const float4* wr = reinterpret_cast<const float4*>(w);
+#pragma unroll 4
+  for (int k4 = 0; k4 < kFC / 4; ++k4) {
+    const float4 xv = xr[k4];
+#pragma unroll
+    for (int jj = 0; jj < NJ; ++jj) {
+      const int j = g + 8 * jj;
+      if (j < LAT) {
+        const float4 wv = wr[j * (kFC / 4) + k4];
+        acc[jj] = fmaf(xv.x, wv.x, acc[jj]);
+        acc[jj] = fmaf(xv.y, wv.y, acc[jj]);
+        acc[jj] = fmaf(xv.z, wv.z, acc[jj]);
+        acc[jj] = fmaf(xv.w, wv.w, acc[jj]);
+      }
+    }
+  }
+  if (n < N) {
+#pragma unroll
+    for (int jj = 0; jj < NJ; ++jj) {
+      const int j = g + 8 * jj;
+      if (j < LAT) v[(size_t)n * LAT + j] = acc[jj] + (bias ? bias[j] : 0.f);
+    }
   }
 }
 
@@ -601,8 +620,7 @@ hipError_t embed_bwd_launch(int B, int T, int L, int C, int K1, const float* x1,
 
 hipError_t final_fwd_train_launch(int N, int rows_per_b, int lat, const float* h, const float* mods, const float* w,
                                   const float* bias, float* v, float* stats, hipStream_t s) {
-  // W (LAT x 384 fp32) is staged per block: enough rows per block to amortise it (~16 per wave)
-  const int grid = min((N + 3) / 4, 512);
+  const int grid = (N + kFfRows - 1) / kFfRows;
   if (lat == 21)
     hipLaunchKernelGGL(final_fwd_kernel<21>, dim3(grid), dim3(kFThreads), 0, s, N, rows_per_b, h, mods, w, bias, v, stats);
   else if (lat == 28)
