@@ -38,11 +38,23 @@ struct SegMap {
   int start[MDG_SEG_MAX + 1];
 };
 
+// Segment of weight row n and per-segment fields picked by it.  The kernel-argument arrays are
+// only ever read at constant indices (scalar loads into SGPRs): the segment count is a sum of
+// compares and a pick is a select chain, where a per-lane dynamic index would turn every lookup
+// into a chain of dependent vector loads from the argument segment.
 __device__ __forceinline__ int seg_of(const SegMap& sm, int n) {
   int s = 0;
-#pragma unroll 1
-  while (s + 1 < sm.nseg && n >= sm.start[s + 1]) ++s;
+#pragma unroll
+  for (int i = 1; i < MDG_SEG_MAX; ++i) s += (i < sm.nseg && n >= sm.start[i]) ? 1 : 0;
   return s;
+}
+template <class T, int N>
+__device__ __forceinline__ T pk(const T (&arr)[N], int s) {
+  T v = arr[0];
+#pragma unroll
+  for (int i = 1; i < MDG_SEG_MAX; ++i)
+    if (s == i) v = arr[i];
+  return v;
 }
 
 __device__ __forceinline__ float silu_f(float x) { return x / (1.0f + expf(-x)); }
@@ -87,8 +99,8 @@ __global__ __launch_bounds__(256) void sl_fwd_kernel(const SlFwdArgs a) {
   sl_stage_x(xs, a.x, a.ldx, m0, mc, a.K, a.act);
   const int n = blockIdx.x * 64 + 16 * wave + nl;
   const bool live = n < a.sm.total;
-  const int s = live ? seg_of(a.sm, n) : 0, nr = live ? n - a.sm.start[s] : 0;
-  const float* wr = a.w[s] + (size_t)nr * a.K;
+  const int s = live ? seg_of(a.sm, n) : 0, nr = live ? n - pk(a.sm.start, s) : 0;
+  const float* wr = pk(a.w, s) + (size_t)nr * a.K;
   __syncthreads();
   float acc[MT];
 #pragma unroll
@@ -114,15 +126,15 @@ __global__ __launch_bounds__(256) void sl_fwd_kernel(const SlFwdArgs a) {
     acc[m] += __shfl_xor(acc[m], 32, 64);
   }
   if (!live || kq != 0) return;
-  const float bias = a.b[s] ? a.b[s][nr] : 0.f;
-  float* yr = a.y[s] + nr;
-  const float* rr = a.resid[s] ? a.resid[s] + nr : nullptr;
+  const float bias = pk(a.b, s) ? pk(a.b, s)[nr] : 0.f;
+  float* yr = pk(a.y, s) + nr;
+  const float* rr = pk(a.resid, s) ? pk(a.resid, s) + nr : nullptr;
 #pragma unroll
   for (int m = 0; m < MT; ++m) {
     if (m < mc) {
       float v = acc[m] + bias;
-      if (rr) v = rr[(size_t)(m0 + m) * a.ldr[s]] + v;
-      yr[(size_t)(m0 + m) * a.ldy[s]] = v;
+      if (rr) v = rr[(size_t)(m0 + m) * pk(a.ldr, s)] + v;
+      yr[(size_t)(m0 + m) * pk(a.ldy, s)] = v;
     }
   }
 }
@@ -137,90 +149,121 @@ struct SlBwdArgs {
   float* dw[MDG_SEG_MAX];
   float* db[MDG_SEG_MAX];
   int n_dw_blocks;  // blocks [0, n_dw_blocks): 64 weight rows of dW / db each; the rest: dX chunks
-  int chunks;
+  int chunks, chunk;  // dX: blocks, weight rows per block (<= kSlChunk)
   float* part;  // [chunks][M][K]
 };
 
 // Backward, two block roles in one launch (tokens in chunks of 32):
-//   dW block: 64 weight rows x all K; thread (k4 column group tk = t & 31, row group tn = t >> 5)
-//     owns float4 columns tk + 32 i and rows tn + 8 j; per token m one dy broadcast from LDS
-//     and one x' float4 from LDS per (i, j) product: dW[n][k] = sum_m dy[m][n] x'[m][k], db[n]
-//     = sum_m dy[m][n] (m ascending, exact fp32 FMAs).
-//   dX block: a chunk of kSlChunk weight rows; thread = float4 column group of dx, register
+//   dW block: 64 weight rows x 32 float4 columns (one column pass of the row block); thread
+//     (column tk = t & 31, row group tn = t >> 5) owns rows tn + 8 j; per token m one dy
+//     broadcast from LDS and one x' float4 from LDS: dW[n][k] = sum_m dy[m][n] x'[m][k], db[n] =
+//     sum_m dy[m][n] (column pass 0; m ascending, exact fp32 FMAs).
+//   dX block: a chunk of weight rows; thread = (float4 column group, row group), register
 //     accumulators for every token; per weight row one coalesced float4 of W and the M dy
-//     values from LDS: P[chunk][m][k] = sum_{n in chunk} dy[m][n] W[n][k].
+//     values from LDS: P[chunk, group][m][k] = sum_{n in the group's rows} dy[m][n] W[n][k].
+// Row pointers come from per-block LDS tables built once (see rrow_ / rdy_).
+template <int MT>  // dX token chunk (8 for M <= 8, else 32)
 __global__ __launch_bounds__(256) void sl_bwd_kernel(const SlBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sm_[];
+  // per-block row tables: segment fields copied at constant indices, then one lookup per row of
+  // the block (W or dW row pointer, dy column pointer and stride, db pointer)
+  __shared__ int st_[MDG_SEG_MAX + 1], ld_[MDG_SEG_MAX];
+  __shared__ const float* sw_[MDG_SEG_MAX];
+  __shared__ const float* sdy_[MDG_SEG_MAX];
+  __shared__ float* sdw_[MDG_SEG_MAX];
+  __shared__ float* sdb_[MDG_SEG_MAX];
+  __shared__ const float* rrow_[kSlChunk];  // dX: W row; dW: dW row (nullptr: no row / no dW)
+  __shared__ const float* rdy_[kSlChunk];   // dy column of the row (nullptr: no row)
+  __shared__ int rld_[kSlChunk];
+  __shared__ float* rdb_[64];
   const int t = threadIdx.x;
-  if ((int)blockIdx.x < a.n_dw_blocks) {
-    float* xs = sm_;                   // [32][K]: the current token chunk's x'
-    float* dys = sm_ + kSlMaxM * a.K;  // [32][64]
-    const int n0 = blockIdx.x * 64;
-    const int tk = t & 31, tn = t >> 5, k4 = a.K >> 2;
-    float dbacc = 0.f;  // thread t < 64: db of weight row n0 + t (first column pass)
-    for (int i0 = tk; i0 - tk < k4; i0 += 32 * 3) {  // up to 3 float4 column groups per pass
-      float4 acc[3][8];
+  const bool dwrole = (int)blockIdx.x < a.n_dw_blocks;
+  if (t == 0) {
 #pragma unroll
-      for (int i = 0; i < 3; ++i)
+    for (int i = 0; i < MDG_SEG_MAX; ++i) {
+      st_[i] = a.sm.start[i];
+      ld_[i] = a.lddy[i];
+      sw_[i] = a.w[i];
+      sdy_[i] = a.dy[i];
+      sdw_[i] = a.dw[i];
+      sdb_[i] = a.db[i];
+    }
+    st_[MDG_SEG_MAX] = a.sm.start[MDG_SEG_MAX];
+  }
+  __syncthreads();
+  {
+    const int base = dwrole ? (int)blockIdx.x / ((a.K / 4 + 31) / 32) * 64 : (blockIdx.x - a.n_dw_blocks) * a.chunk;
+    const int rows = dwrole ? 64 : a.chunk;
+    if (t < rows) {
+      const int n = base + t;
+      const bool live = n < a.sm.total;
+      int sg = 0;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) acc[i][j] = make_float4(0.f, 0.f, 0.f, 0.f);
-      for (int mb = 0; mb < a.M; mb += kSlMaxM) {  // token chunks, m ascending overall
-        const int mc = min(kSlMaxM, a.M - mb);
-        __syncthreads();
-        sl_stage_x(xs, a.x, a.ldx, mb, mc, a.K, a.act);
-        for (int e = t; e < mc * 64; e += 256) {
-          const int m = e >> 6, c = e & 63, n = n0 + c;
-          float v = 0.f;
-          if (n < a.sm.total) {
-            const int s = seg_of(a.sm, n);
-            v = a.dy[s][(size_t)(mb + m) * a.lddy[s] + (n - a.sm.start[s])];
-          }
-          dys[m * 64 + c] = v;
+      for (int i = 1; i < MDG_SEG_MAX; ++i) sg += (i < a.sm.nseg && n >= st_[i]) ? 1 : 0;
+      const int nr = n - st_[sg];
+      rdy_[t] = live ? sdy_[sg] + nr : nullptr;
+      rld_[t] = ld_[sg];
+      if (dwrole) {
+        rrow_[t] = live && sdw_[sg] ? sdw_[sg] + (size_t)nr * a.K : nullptr;
+        rdb_[t] = live && sdb_[sg] ? sdb_[sg] + nr : nullptr;
+      } else {
+        rrow_[t] = live ? sw_[sg] + (size_t)nr * a.K : nullptr;
+      }
+    }
+  }
+  __syncthreads();
+  if (dwrole) {
+    // 64 weight rows x 32 float4 columns (column pass cp of the row block); the token chunk's x'
+    // slice [32][32 float4] and dy tile [32][64] are staged in LDS
+    float4* xs = reinterpret_cast<float4*>(sm_);  // [32][32]
+    float* dys = sm_ + kSlMaxM * 32 * 4;          // [32][64]
+    const int ncp = (a.K / 4 + 31) / 32, cp = blockIdx.x % ncp;
+    const int tk = t & 31, tn = t >> 5, c = cp * 32 + tk;
+    const bool col_ok = c < a.K / 4;
+    float dbacc = 0.f;  // cp == 0, thread t < 64: db of the block's weight row t
+    float4 acc[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int mb = 0; mb < a.M; mb += kSlMaxM) {  // token chunks, m ascending overall
+      const int mc = min(kSlMaxM, a.M - mb);
+      __syncthreads();
+      for (int e = t; e < mc * 32; e += 256) {
+        const int m = e >> 5, cc = cp * 32 + (e & 31);
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (cc < a.K / 4) {
+          v = *reinterpret_cast<const float4*>(a.x + (size_t)(mb + m) * a.ldx + 4 * cc);
+          if (a.act == MDG_ACT_SILU) v = make_float4(silu_f(v.x), silu_f(v.y), silu_f(v.z), silu_f(v.w));
         }
-        __syncthreads();
-        if (i0 == tk && t < 64)
-          for (int m = 0; m < mc; ++m) dbacc += dys[m * 64 + t];
-        for (int m = 0; m < mc; ++m) {
-          float4 xv[3];
+        xs[e] = v;
+      }
+      for (int e = t; e < mc * 64; e += 256) {
+        const int m = e >> 6, cc = e & 63;
+        const float* col = rdy_[cc];
+        dys[m * 64 + cc] = col ? col[(size_t)(mb + m) * rld_[cc]] : 0.f;
+      }
+      __syncthreads();
+      if (cp == 0 && t < 64)
+        for (int m = 0; m < mc; ++m) dbacc += dys[m * 64 + t];
+      for (int m = 0; m < mc; ++m) {
+        const float4 xv = xs[m * 32 + tk];
 #pragma unroll
-          for (int i = 0; i < 3; ++i) {
-            const int c = i0 + 32 * i;
-            xv[i] = c < k4 ? *reinterpret_cast<const float4*>(xs + m * a.K + 4 * c) : make_float4(0.f, 0.f, 0.f, 0.f);
-          }
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const float d = dys[m * 64 + tn + 8 * j];
-#pragma unroll
-            for (int i = 0; i < 3; ++i) {
-              acc[i][j].x = fmaf(d, xv[i].x, acc[i][j].x);
-              acc[i][j].y = fmaf(d, xv[i].y, acc[i][j].y);
-              acc[i][j].z = fmaf(d, xv[i].z, acc[i][j].z);
-              acc[i][j].w = fmaf(d, xv[i].w, acc[i][j].w);
-            }
-          }
+        for (int j = 0; j < 8; ++j) {
+          const float d = dys[m * 64 + tn + 8 * j];
+          acc[j].x = fmaf(d, xv.x, acc[j].x);
+          acc[j].y = fmaf(d, xv.y, acc[j].y);
+          acc[j].z = fmaf(d, xv.z, acc[j].z);
+          acc[j].w = fmaf(d, xv.w, acc[j].w);
         }
       }
+    }
+    if (col_ok) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const int n = n0 + tn + 8 * j;
-        if (n >= a.sm.total) continue;
-        const int s = seg_of(a.sm, n);
-        if (!a.dw[s]) continue;
-        float* dwr = a.dw[s] + (size_t)(n - a.sm.start[s]) * a.K;
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-          const int c = i0 + 32 * i;
-          if (c < k4) *reinterpret_cast<float4*>(dwr + 4 * c) = acc[i][j];
-        }
+        float* dwr = const_cast<float*>(rrow_[tn + 8 * j]);
+        if (dwr) *reinterpret_cast<float4*>(dwr + 4 * c) = acc[j];
       }
     }
-    if (t < 64) {  // db, m ascending
-      const int n = n0 + t;
-      if (n < a.sm.total) {
-        const int s = seg_of(a.sm, n);
-        if (a.db[s]) a.db[s][n - a.sm.start[s]] = dbacc;
-      }
-    }
+    if (cp == 0 && t < 64 && rdb_[t]) *rdb_[t] = dbacc;  // db, m ascending
     return;
   }
   // dX partial of one chunk of kSlChunk weight rows, token chunks of 32: thread = (float4 column
@@ -228,33 +271,29 @@ __global__ __launch_bounds__(256) void sl_bwd_kernel(const SlBwdArgs a) {
   // with their weight loads issued together (row pointers computed per row, no loop-carried
   // address), and writes its own partial P[chunk * RG + rg][m][k] (the reduce sums them in order)
   const int ch = blockIdx.x - a.n_dw_blocks;
-  const int j0 = ch * kSlChunk, j1 = min(j0 + kSlChunk, a.sm.total), nc = j1 - j0;
+  const int j0 = ch * a.chunk, nc = min(a.chunk, a.sm.total - j0);
   float* dys = sm_;  // [kSlChunk][32]
   const int k4 = a.K >> 2, RG = 256 / k4, cg = t % k4, rg = t / k4;
   const bool act_t = rg < RG;
   float* P = a.part + (size_t)(ch * RG + (act_t ? rg : 0)) * a.M * a.K;
-  auto wrow = [&](int jj) {
-    const int n = j0 + jj, s = seg_of(a.sm, n);
-    return reinterpret_cast<const float4*>(a.w[s] + (size_t)(n - a.sm.start[s]) * a.K) + cg;
-  };
-  for (int mb = 0; mb < a.M; mb += kSlMaxM) {
-    const int mc = min(kSlMaxM, a.M - mb);
+  auto wrow = [&](int jj) { return reinterpret_cast<const float4*>(rrow_[jj]) + cg; };
+  for (int mb = 0; mb < a.M; mb += MT) {
+    const int mc = min(MT, a.M - mb);
     __syncthreads();
     for (int e = t; e < nc * mc; e += 256) {
-      const int jj = e / mc, m = e - jj * mc, n = j0 + jj;
-      const int s = seg_of(a.sm, n);
-      dys[jj * kSlMaxM + m] = a.dy[s][(size_t)(mb + m) * a.lddy[s] + (n - a.sm.start[s])];
+      const int jj = e / mc, m = e - jj * mc;
+      dys[jj * MT + m] = rdy_[jj][(size_t)(mb + m) * rld_[jj]];
     }
     __syncthreads();
     if (!act_t) continue;
-    float4 acc[kSlMaxM];
+    float4 acc[MT];
 #pragma unroll
-    for (int m = 0; m < kSlMaxM; ++m) acc[m] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int m = 0; m < MT; ++m) acc[m] = make_float4(0.f, 0.f, 0.f, 0.f);
     auto use = [&](int jj, const float4 w4) {
 #pragma unroll
-      for (int m = 0; m < kSlMaxM; ++m) {
+      for (int m = 0; m < MT; ++m) {
         if (m < mc) {
-          const float d = dys[jj * kSlMaxM + m];
+          const float d = dys[jj * MT + m];
           acc[m].x = fmaf(d, w4.x, acc[m].x);
           acc[m].y = fmaf(d, w4.y, acc[m].y);
           acc[m].z = fmaf(d, w4.z, acc[m].z);
@@ -272,7 +311,7 @@ __global__ __launch_bounds__(256) void sl_bwd_kernel(const SlBwdArgs a) {
     }
     for (; jj < nc; jj += RG) use(jj, *wrow(jj));
 #pragma unroll
-    for (int m = 0; m < kSlMaxM; ++m)
+    for (int m = 0; m < MT; ++m)
       if (m < mc) *reinterpret_cast<float4*>(P + (size_t)(mb + m) * a.K + 4 * cg) = acc[m];
   }
 }
@@ -333,9 +372,11 @@ int seg_total(const mdg_seg_linear* s) {
 }
 
 static int sl_row_groups(int K) { return 256 / (K >> 2); }
+// dX rows per block: kSlChunk when that still gives >= 128 blocks, else 32 (few-row linears)
+static int sl_chunk(int total) { return total >= 128 * kSlChunk ? kSlChunk : 32; }
 
 size_t seg_linear_ws_bytes(int M, int K, int total) {
-  const int chunks = (total + kSlChunk - 1) / kSlChunk;
+  const int chunks = (total + sl_chunk(total) - 1) / sl_chunk(total);
   return (size_t)chunks * sl_row_groups(K) * M * K * sizeof(float);
 }
 
@@ -380,20 +421,18 @@ hipError_t seg_linear_bwd_launch(int M, int K, const float* x, int ldx, int act,
     a.w[i] = s->w[i], a.dy[i] = s->dy[i], a.lddy[i] = s->lddy[i], a.dw[i] = s->dw[i], a.db[i] = s->db[i];
     any_w = any_w || s->dw[i] || s->db[i];
   }
-  a.chunks = dx ? (sm.total + kSlChunk - 1) / kSlChunk : 0;
-  a.n_dw_blocks = any_w ? (sm.total + 63) / 64 : 0;
+  a.chunk = sl_chunk(sm.total);
+  a.chunks = dx ? (sm.total + a.chunk - 1) / a.chunk : 0;
+  a.n_dw_blocks = any_w ? (sm.total + 63) / 64 * ((K / 4 + 31) / 32) : 0;
   a.part = ws;
-  static bool attr = false;
-  const size_t smax = (size_t)(kSlMaxM * kSlMaxK + kSlMaxM * 64) * 4;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&sl_bwd_kernel),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)smax);
-    if (e != hipSuccess) return e;
-    attr = true;
-  }
-  const size_t smem = std::max((size_t)(kSlMaxM * K + kSlMaxM * 64) * 4, (size_t)kSlChunk * kSlMaxM * 4);
+  const size_t smem = std::max((size_t)(kSlMaxM * 32 * 4 + kSlMaxM * 64) * 4, (size_t)kSlChunk * kSlMaxM * 4);
   const int nblk = a.n_dw_blocks + a.chunks;
-  if (nblk > 0) hipLaunchKernelGGL(sl_bwd_kernel, dim3(nblk), dim3(256), smem, st, a);
+  if (nblk > 0) {
+    if (M <= 8)
+      hipLaunchKernelGGL(sl_bwd_kernel<8>, dim3(nblk), dim3(256), smem, st, a);
+    else
+      hipLaunchKernelGGL(sl_bwd_kernel<kSlMaxM>, dim3(nblk), dim3(256), smem, st, a);
+  }
   if (dx)
     hipLaunchKernelGGL(sl_dx_reduce_kernel, dim3((M * K + 63) / 64), dim3(256), 0, st, M, K, a.chunks * sl_row_groups(K),
                        (const float*)ws, x, ldx, act, dx, lddx);
