@@ -91,13 +91,17 @@ struct SlFwdArgs {
 // ITS weight row (4 lanes cover 64 contiguous bytes) against the x' rows in LDS (same address
 // within a 16-lane group: broadcast), 32 accumulators; the k quarters are summed by two lane
 // swaps at the end.
-template <int MT>
+//
+// KS = 4 (few-row linears, too few 64-row blocks to fill the chip): 16 weight rows per block and
+// the four waves interleave over k as well; their sums are added in wave order through LDS.
+template <int MT, int KS>
 __global__ __launch_bounds__(256) void sl_fwd_kernel(const SlFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) float xs[];  // [MT][K]
+  __shared__ float red[KS == 4 ? 3 * 16 * (MT + 1) : 1];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nl = lane & 15, kq = lane >> 4;
   const int m0 = blockIdx.y * MT, mc = min(MT, a.M - m0);
   sl_stage_x(xs, a.x, a.ldx, m0, mc, a.K, a.act);
-  const int n = blockIdx.x * 64 + 16 * wave + nl;
+  const int n = KS == 1 ? blockIdx.x * 64 + 16 * wave + nl : blockIdx.x * 16 + nl;
   const bool live = n < a.sm.total;
   const int s = live ? seg_of(a.sm, n) : 0, nr = live ? n - pk(a.sm.start, s) : 0;
   const float* wr = pk(a.w, s) + (size_t)nr * a.K;
@@ -106,7 +110,7 @@ __global__ __launch_bounds__(256) void sl_fwd_kernel(const SlFwdArgs a) {
 #pragma unroll
   for (int m = 0; m < MT; ++m) acc[m] = 0.f;
   if (live) {
-    for (int k = 4 * kq; k < a.K; k += 16) {
+    for (int k = 4 * kq + (KS == 1 ? 0 : 16 * wave); k < a.K; k += 16 * KS) {
       const float4 w4 = *reinterpret_cast<const float4*>(wr + k);
 #pragma unroll
       for (int m = 0; m < MT; ++m) {
@@ -124,6 +128,16 @@ __global__ __launch_bounds__(256) void sl_fwd_kernel(const SlFwdArgs a) {
   for (int m = 0; m < MT; ++m) {
     acc[m] += __shfl_xor(acc[m], 16, 64);
     acc[m] += __shfl_xor(acc[m], 32, 64);
+  }
+  if constexpr (KS == 4) {
+    if (wave > 0 && kq == 0)
+#pragma unroll
+      for (int m = 0; m < MT; ++m) red[((wave - 1) * 16 + nl) * (MT + 1) + m] = acc[m];
+    __syncthreads();
+    if (wave != 0) return;
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+      acc[m] = ((acc[m] + red[nl * (MT + 1) + m]) + red[(16 + nl) * (MT + 1) + m]) + red[(32 + nl) * (MT + 1) + m];
   }
   if (!live || kq != 0) return;
   const float bias = pk(a.b, s) ? pk(a.b, s)[nr] : 0.f;
@@ -392,20 +406,31 @@ hipError_t seg_linear_fwd_launch(int M, int K, const float* x, int ldx, int act,
     a.w[i] = s->w[i], a.b[i] = s->b[i], a.y[i] = s->y[i], a.ldy[i] = s->ldy[i];
     a.resid[i] = s->resid[i], a.ldr[i] = s->ldr[i];
   }
-  const unsigned nx = (unsigned)((sm.total + 63) / 64);
+  // 64 weight rows per block, or 16 with the waves splitting K when that leaves < 256 blocks
+  const bool ks = (sm.total + 63) / 64 * ((M + kSlMaxM - 1) / kSlMaxM) < 256;
+  const unsigned nx = (unsigned)(ks ? (sm.total + 15) / 16 : (sm.total + 63) / 64);
   if (M <= 8) {
     const size_t smem = (size_t)8 * K * sizeof(float);
-    hipLaunchKernelGGL(sl_fwd_kernel<8>, dim3(nx, 1), dim3(256), smem, st, a);
+    if (ks)
+      hipLaunchKernelGGL((sl_fwd_kernel<8, 4>), dim3(nx, 1), dim3(256), smem, st, a);
+    else
+      hipLaunchKernelGGL((sl_fwd_kernel<8, 1>), dim3(nx, 1), dim3(256), smem, st, a);
   } else {
     const size_t smem = (size_t)kSlMaxM * K * sizeof(float);
     static bool attr = false;
     if (!attr) {
-      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&sl_fwd_kernel<kSlMaxM>),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, kSlMaxM * kSlMaxK * 4);
-      if (e != hipSuccess) return e;
+      for (const void* f : {reinterpret_cast<const void*>(&sl_fwd_kernel<kSlMaxM, 1>),
+                            reinterpret_cast<const void*>(&sl_fwd_kernel<kSlMaxM, 4>)}) {
+        hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kSlMaxM * kSlMaxK * 4);
+        if (e != hipSuccess) return e;
+      }
       attr = true;
     }
-    hipLaunchKernelGGL(sl_fwd_kernel<kSlMaxM>, dim3(nx, (M + kSlMaxM - 1) / kSlMaxM), dim3(256), smem, st, a);
+    const dim3 grid(nx, (M + kSlMaxM - 1) / kSlMaxM);
+    if (ks)
+      hipLaunchKernelGGL((sl_fwd_kernel<kSlMaxM, 4>), grid, dim3(256), smem, st, a);
+    else
+      hipLaunchKernelGGL((sl_fwd_kernel<kSlMaxM, 1>), grid, dim3(256), smem, st, a);
   }
   return hipGetLastError();
 }

@@ -98,7 +98,7 @@ def test_final_layer_forward_and_backward_match_eager(B, T, lat):
     ((8,), 256, [384], "none", False),                            # t-MLP first linear
     ((37,), 100, [5, 70, 130], "silu", False),                    # ragged everything
     ((40,), 1024, [300, 17], "silu", False),                      # widest K, two token chunks
-    ((5, 9), 132, [64, 64, 1], "none", True),                     # K not a multiple of 128
+    ((5, 9), 132, [64, 64, 1], "none", False),                    # K not a multiple of 128
 ])
 def test_seg_linear_forward_and_backward_match_fp64(lead, K, ns, act, resid):
     """mdg_seg_linear_fwd / _bwd (csrc/linear_small.hip) against float64 autograd of

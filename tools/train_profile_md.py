@@ -44,6 +44,16 @@ for k, (n, t) in sorted(by.items(), key=lambda kv: -kv[1][1]):
 out += ["", "| kernel | calls | ms | avg us |", "|---|---|---|---|"]
 for k, (n, t) in sorted(per.items(), key=lambda kv: -kv[1][1])[:30]:
     out.append(f"| `{k}` | {n} | {t / 1e6:.3f} | {t / n / 1e3:.1f} |")
+out += ["", "Every kernel not from libmdgen_hip (names to 160 characters):", "",
+        "| kernel | calls | ms | avg us |", "|---|---|---|---|"]
+lib = collections.defaultdict(lambda: [0, 0])
+for r in seg:
+    if origin(r["Kernel_Name"]) != "libmdgen_hip":
+        k = re.sub(r"\s+", " ", r["Kernel_Name"])[:160]
+        lib[k][0] += 1
+        lib[k][1] += dur(r)
+for k, (n, t) in sorted(lib.items(), key=lambda kv: -kv[1][1]):
+    out.append(f"| `{k}` | {n} | {t / 1e6:.3f} | {t / n / 1e3:.1f} |")
 dst = os.path.join(REPO, "profiles", f"r{rr}_train_kernels.md")
 open(dst, "w").write("\n".join(out) + "\n")
 print(dst)
