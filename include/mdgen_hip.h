@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define MDG_ABI_VERSION 20
+#define MDG_ABI_VERSION 21
 #define MDG_MAX_LAYERS 16
 #define MDG_SEG_MAX 16 /* segments of one mdg_seg_linear */
 #define MDG_DP 32      /* padded head dim of the attention operand buffers for head_dim <= 31 */
@@ -503,6 +503,35 @@ int mdg_gvp_loss_fwd(int32_t B, int32_t T, int32_t L, int32_t K, const float* ou
                      const int64_t* mask_strides, float* loss, float* den, void* ws, size_t ws_bytes, void* stream);
 int mdg_gvp_loss_bwd(int32_t B, int32_t T, int32_t L, int32_t K, const float* out, const float* ut, const float* mask,
                      const int64_t* mask_strides, const float* gloss, const float* den, float* dout, void* stream);
+
+/* The optimizer step of the graphed training step (train.py GraphedStep._update: the reference's
+   Lightning loop runs clip_grad_norm_ (gradient_clip_val, train.py:52) then Adam / AdamW,
+   wrapper.py:167-173), fp32, torch.optim semantics:
+     norm = ||all g||_2 (chunk partials summed in a fixed order), coef = min(1, max_norm /
+     (norm + 1e-6)) (1 when max_norm <= 0), g' = coef g (+ weight_decay p unless decoupled),
+     step += 1, m = b1 m + (1 - b1) g', v = b2 v + (1 - b2) g'^2, p (*= 1 - lr wd when decoupled)
+     -= lr / (1 - b1^step) m / (sqrt(v) / sqrt(1 - b2^step) + eps).
+   g is read, not clipped in place.  One table entry per tensor; the device table image
+   (tensors + chunk map) is built on the host by mdg_adam_table_build and copied by the caller,
+   which may do so after a stream capture that recorded mdg_adam_step (the kernels read the table
+   when they run).  ws: mdg_adam_workspace_bytes(n_chunks).  gnorm (device, may be null) gets norm.
+   Hyper-parameters in double, as torch's Python floats: the bias corrections are formed in double
+   per block, the element update in fp32. */
+typedef struct {
+  float* p;
+  const float* g;
+  float* m;     /* exp_avg */
+  float* v;     /* exp_avg_sq */
+  float* step;  /* the tensor's step count (a 0-d fp32 device tensor, torch's capturable state) */
+  int64_t n;
+} mdg_adam_tensor;
+int32_t mdg_adam_chunks(int32_t n_tensors, const mdg_adam_tensor* tensors);
+size_t mdg_adam_table_bytes(int32_t n_tensors, const mdg_adam_tensor* tensors);
+int mdg_adam_table_build(int32_t n_tensors, const mdg_adam_tensor* tensors, void* table, size_t table_bytes);
+size_t mdg_adam_workspace_bytes(int32_t n_chunks);
+int mdg_adam_step(int32_t n_tensors, int32_t n_chunks, const void* table, double lr, double beta1, double beta2,
+                  double eps, double weight_decay, int32_t decoupled, double max_norm, float* gnorm, void* ws,
+                  size_t ws_bytes, void* stream);
 
 /* Training backward of the token embedding (latent_model.py:242-255 under loss.backward()),
    from the residual gradient dh [N][C] fp32 (N = B*T*L tokens, n = (b*T + t)*L + l):

@@ -126,6 +126,10 @@ class MdgSegLinear(ctypes.Structure):
                 ("dw", _vp * MDG_SEG_MAX), ("db", _vp * MDG_SEG_MAX)]
 
 
+class MdgAdamTensor(ctypes.Structure):
+    _fields_ = [("p", _vp), ("g", _vp), ("m", _vp), ("v", _vp), ("step", _vp), ("n", ctypes.c_int64)]
+
+
 # (name, restype, argtypes) of every exported entry point — the test suite checks that the
 # built library exports exactly these and that include/mdgen_hip.h declares them.
 SIGNATURES = [
@@ -187,9 +191,15 @@ SIGNATURES = [
     ("mdg_seg_linear_bwd_workspace_bytes", ctypes.c_size_t, [_i32, _i32, ctypes.POINTER(MdgSegLinear)]),
     ("mdg_seg_linear_bwd", _i32, [_i32, _i32, _vp, _i32, _i32, ctypes.POINTER(MdgSegLinear), _vp, _i32, _vp,
                                   ctypes.c_size_t, _vp]),
+    ("mdg_adam_chunks", _i32, [_i32, ctypes.POINTER(MdgAdamTensor)]),
+    ("mdg_adam_table_bytes", ctypes.c_size_t, [_i32, ctypes.POINTER(MdgAdamTensor)]),
+    ("mdg_adam_table_build", _i32, [_i32, ctypes.POINTER(MdgAdamTensor), _vp, ctypes.c_size_t]),
+    ("mdg_adam_workspace_bytes", ctypes.c_size_t, [_i32]),
+    ("mdg_adam_step", _i32, [_i32, _i32, _vp] + [ctypes.c_double] * 5 + [_i32, ctypes.c_double, _vp, _vp,
+                                                                          ctypes.c_size_t, _vp]),
 ]
 
-ABI_VERSION = 20
+ABI_VERSION = 21
 _LIB = None
 
 

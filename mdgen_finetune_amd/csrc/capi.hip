@@ -5,6 +5,8 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <cmath>
+
 #include <string>
 #include <vector>
 
@@ -116,6 +118,13 @@ hipError_t gvp_loss_fwd_launch(int B, int T, int L, int K, const float* out, con
                                const int64_t* ms, float* loss, float* den, float* ws, hipStream_t s);
 hipError_t gvp_loss_bwd_launch(int B, int T, int L, int K, const float* out, const float* ut, const float* mask,
                                const int64_t* ms, const float* g, const float* den, float* dout, hipStream_t s);
+// optim.hip
+int adam_chunks(int nt, const mdg_adam_tensor* t);
+size_t adam_table_bytes(int nt, int nc);
+void adam_table_build(int nt, int nc, const mdg_adam_tensor* t, void* table);
+size_t adam_ws_bytes(int nc);
+hipError_t adam_step_launch(int nt, int nc, const void* table, double lr, double b1, double b2, double eps, double wd,
+                            int decoupled, double max_norm, float* gnorm, float* ws, hipStream_t s);
 // linear_small.hip
 int seg_total(const mdg_seg_linear* s);
 bool seg_linear_shape_ok(int M, int K);
@@ -1415,6 +1424,48 @@ int mdg_gvp_loss_bwd(int32_t B, int32_t T, int32_t L, int32_t K, const float* ou
   if (B <= 0 || T <= 0 || L <= 0 || K <= 0) return fail(MDG_E_SHAPE, "gvp_loss_bwd: B=%d T=%d L=%d K=%d", B, T, L, K);
   return hip_check(mdg::gvp_loss_bwd_launch(B, T, L, K, out, ut, mask, mask_strides, gloss, den, dout,
                                             (hipStream_t)stream), "gvp_loss_bwd");
+}
+
+int32_t mdg_adam_chunks(int32_t n_tensors, const mdg_adam_tensor* tensors) {
+  if (n_tensors <= 0 || !tensors) return -1;
+  return mdg::adam_chunks(n_tensors, tensors);
+}
+
+size_t mdg_adam_table_bytes(int32_t n_tensors, const mdg_adam_tensor* tensors) {
+  const int nc = mdg_adam_chunks(n_tensors, tensors);
+  return nc <= 0 ? 0 : mdg::adam_table_bytes(n_tensors, nc);
+}
+
+int mdg_adam_table_build(int32_t n_tensors, const mdg_adam_tensor* tensors, void* table, size_t table_bytes) {
+  if (n_tensors <= 0 || !tensors || !table) return fail(MDG_E_ARG, "adam_table_build: null pointer or no tensors");
+  const int nc = mdg::adam_chunks(n_tensors, tensors);
+  if (nc <= 0) return fail(MDG_E_SHAPE, "adam_table_build: a tensor has no elements");
+  for (int i = 0; i < n_tensors; ++i) {
+    const mdg_adam_tensor& t = tensors[i];
+    if (!t.p || !t.g || !t.m || !t.v || !t.step) return fail(MDG_E_ARG, "adam_table_build: tensor %d: null pointer", i);
+  }
+  const size_t need = mdg::adam_table_bytes(n_tensors, nc);
+  if (table_bytes < need) return fail(MDG_E_ARG, "adam_table_build: table %zu < %zu bytes", table_bytes, need);
+  mdg::adam_table_build(n_tensors, nc, tensors, table);
+  return MDG_OK;
+}
+
+size_t mdg_adam_workspace_bytes(int32_t n_chunks) { return n_chunks <= 0 ? 0 : mdg::adam_ws_bytes(n_chunks); }
+
+int mdg_adam_step(int32_t n_tensors, int32_t n_chunks, const void* table, double lr, double beta1, double beta2,
+                  double eps, double weight_decay, int32_t decoupled, double max_norm, float* gnorm, void* ws,
+                  size_t ws_bytes, void* stream) {
+  if (!table || !ws) return fail(MDG_E_ARG, "adam_step: null pointer");
+  if (n_tensors <= 0 || n_chunks < n_tensors) return fail(MDG_E_SHAPE, "adam_step: %d tensors, %d chunks", n_tensors, n_chunks);
+  if (!(lr >= 0.0) || !(beta1 >= 0.0 && beta1 < 1.0) || !(beta2 >= 0.0 && beta2 < 1.0) || !(eps >= 0.0) ||
+      !(weight_decay >= 0.0) || !std::isfinite(max_norm))
+    return fail(MDG_E_ARG, "adam_step: lr %g betas (%g, %g) eps %g weight_decay %g max_norm %g", lr, beta1, beta2, eps,
+                weight_decay, max_norm);
+  const size_t need = mdg::adam_ws_bytes(n_chunks);
+  if (ws_bytes < need) return fail(MDG_E_ARG, "adam_step: workspace %zu < %zu bytes", ws_bytes, need);
+  return hip_check(mdg::adam_step_launch(n_tensors, n_chunks, table, lr, beta1, beta2, eps, weight_decay, decoupled,
+                                         max_norm, gnorm, (float*)ws, (hipStream_t)stream),
+                   "adam_step");
 }
 
 size_t mdg_seg_linear_bwd_workspace_bytes(int32_t M, int32_t K, const mdg_seg_linear* s) {

@@ -369,6 +369,12 @@ class GraphedStep:
                 for k, v in ema_snap.items():
                     ema.params[k].copy_(v)
         tr.optimizer.zero_grad(set_to_none=True)
+        # clip + Adam on the library's two-pass update (optim_hip.FusedClipAdam) instead of torch's
+        # foreach norm / multiplies / fused Adam launches; MDG_TRAIN_FUSED_OPT=0 keeps torch's (A/B)
+        from .optim_hip import FusedClipAdam
+        self.fused_opt = None
+        if os.environ.get("MDG_TRAIN_FUSED_OPT", "1") != "0" and FusedClipAdam.supported(tr.optimizer):
+            self.fused_opt = FusedClipAdam(tr.optimizer, self.params, tr.args.grad_clip)
         n = sum(p.numel() for p in self.params)
         self.flat = self.reducer.flat if self.overlap else (torch.empty(n, device=dev) if self.split else None)
         self.g1 = torch.cuda.CUDAGraph()
@@ -384,6 +390,8 @@ class GraphedStep:
                 torch.cat([g.reshape(-1) for g in self.grads_g1], out=self.flat)
             else:
                 self.gnorm = self._update()
+        if self.fused_opt is not None and not (self.split and not self.overlap):
+            self.fused_opt.finish_capture()
         if self.split and not self.overlap:
             off = 0
             for p in self.params:  # graph 2 reads the averaged gradients in place
@@ -392,6 +400,8 @@ class GraphedStep:
             self.g2 = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.g2):
                 self.gnorm = self._update()
+            if self.fused_opt is not None:
+                self.fused_opt.finish_capture()
 
     def _fwd_bwd(self):
         tr = self.tr
@@ -406,6 +416,10 @@ class GraphedStep:
 
     def _update(self):
         tr = self.tr
+        if self.fused_opt is not None:
+            gnorm = self.fused_opt.step(capturing=True)
+            tr.wrapper.on_before_zero_grad()
+            return gnorm if tr.args.grad_clip else None
         gnorm = torch.nn.utils.clip_grad_norm_(self.params, tr.args.grad_clip) if tr.args.grad_clip else None
         tr.optimizer.step()
         tr.wrapper.on_before_zero_grad()

@@ -110,3 +110,36 @@ def test_shape_validation_without_gpu():
     vals = [offs[k] for k in _lib.WS_REGIONS]
     assert vals == sorted(vals) and vals[0] == 0 and all(v % 256 == 0 for v in vals)
     assert offs["kbias"] < lib.mdg_workspace_bytes(ctypes.byref(d))
+
+
+def test_adam_table_image_without_gpu():
+    """mdg_adam_table_build (host only): the tensor entries, then chunk -> (tensor, chunk index)
+    for chunks of 16384 elements; tensors without elements and null pointers are refused."""
+    import struct
+
+    from mdgen_finetune_amd import _lib
+
+    lib = _lib.load()
+    sizes = [1, 16384, 16385, 40000]
+    tab = (_lib.MdgAdamTensor * len(sizes))()
+    for i, n in enumerate(sizes):
+        base = 0x1000 * (i + 1)
+        tab[i] = _lib.MdgAdamTensor(base, base + 16, base + 32, base + 48, base + 64, n)
+    nc = lib.mdg_adam_chunks(len(sizes), tab)
+    assert nc == 1 + 1 + 2 + 3
+    nbytes = lib.mdg_adam_table_bytes(len(sizes), tab)
+    assert nbytes == len(sizes) * ctypes.sizeof(_lib.MdgAdamTensor) + 8 * nc
+    buf = (ctypes.c_uint8 * nbytes)()
+    assert lib.mdg_adam_table_build(len(sizes), tab, buf, nbytes) == 0
+    raw = bytes(buf)
+    head = len(sizes) * ctypes.sizeof(_lib.MdgAdamTensor)
+    assert raw[:head] == bytes(tab)
+    ct = struct.unpack(f"<{nc}i", raw[head:head + 4 * nc])
+    ci = struct.unpack(f"<{nc}i", raw[head + 4 * nc:])
+    assert list(ct) == [0, 1, 2, 2, 3, 3, 3] and list(ci) == [0, 0, 0, 1, 0, 1, 2]
+    assert lib.mdg_adam_table_build(len(sizes), tab, buf, nbytes - 1) != 0  # short table
+    tab[1].n = 0
+    assert lib.mdg_adam_chunks(len(sizes), tab) < 0
+    tab[1].n, tab[2].step = 5, None
+    assert lib.mdg_adam_table_build(len(sizes), tab, buf, nbytes) != 0
+    assert b"null" in lib.mdg_last_error_string()
