@@ -112,12 +112,13 @@ __global__ __launch_bounds__(256) void adam_update_kernel(int nt, int nc, const 
   const float step_size = (float)(lr / (1.0 - pow(b1d, st))), bc2s = (float)sqrt(1.0 - pow(b2d, st));
   const float keep = decoupled ? (float)(1.0 - lr * wdd) : 1.0f, l2 = decoupled ? 0.f : (float)wdd;
   const float b1 = (float)b1d, b2 = (float)b2d, eps = (float)epsd;
+  const float omb1 = (float)(1.0 - b1d), omb2 = (float)(1.0 - b2d);  // 1 - beta rounded once, as torch
   auto upd = [&](float& pp, float gg, float& mm, float& vv) {
     float gc = gg * coef;
     if (l2 != 0.f) gc = fmaf(l2, pp, gc);
     pp *= keep;
-    mm = b1 * mm + (1.0f - b1) * gc;
-    vv = b2 * vv + (1.0f - b2) * gc * gc;
+    mm = b1 * mm + omb1 * gc;
+    vv = b2 * vv + omb2 * gc * gc;
     const float denom = sqrtf(vv) / bc2s + eps;
     pp -= step_size * mm / denom;
   };

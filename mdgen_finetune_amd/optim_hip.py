@@ -20,7 +20,11 @@ class FusedClipAdam:
 
     ``step(capturing=True)`` records the launches inside a stream capture; the device table of
     tensor addresses it reads is written by ``finish_capture()`` after the capture ends (the
-    gradients' addresses are the capture's own allocations)."""
+    gradients' addresses are the capture's own allocations).  The table, workspace and norm
+    buffers of a captured step come from ``reserve()``, called BEFORE the capture: memory the
+    capture itself allocated may be reused by the graph's earlier kernels on every replay (the
+    private pool recycles blocks freed within the capture), which would overwrite a table
+    written once from the host."""
 
     def __init__(self, optimizer, params, max_norm):
         if not self.supported(optimizer):
@@ -29,7 +33,28 @@ class FusedClipAdam:
         self.params = list(params)
         self.max_norm = float(max_norm or 0.0)
         self._pending = []
+        self._reserved = None
         self._keep = []  # tables / workspaces of every recorded step, referenced while graphs may replay
+
+    def _sizes(self, ps):
+        lib = _lib.load()
+        tab = (_lib.MdgAdamTensor * len(ps))()
+        for i, p in enumerate(ps):
+            tab[i] = _lib.MdgAdamTensor(1, 1, 1, 1, 1, p.numel())
+        nc = lib.mdg_adam_chunks(len(ps), tab)
+        if nc <= 0:
+            raise ValueError("FusedClipAdam: empty parameter")
+        return lib.mdg_adam_table_bytes(len(ps), tab), lib.mdg_adam_workspace_bytes(nc)
+
+    def _buffers(self, ps):
+        tb, wsb = self._sizes(ps)
+        dev = ps[0].device
+        return (torch.empty(tb, dtype=torch.uint8, device=dev), torch.empty(wsb, dtype=torch.uint8, device=dev),
+                torch.empty((), dtype=torch.float32, device=dev))
+
+    def reserve(self):
+        """Buffers for the next step(capturing=True), sized for every parameter (outside a capture)."""
+        self._reserved = self._buffers([p for p in self.params if p.requires_grad])
 
     @staticmethod
     def supported(optimizer):
@@ -73,13 +98,18 @@ class FusedClipAdam:
         host = (ctypes.c_uint8 * nbytes)()
         _lib.check(lib.mdg_adam_table_build(n, tab, host, nbytes), "mdg_adam_table_build")
         host_t = torch.frombuffer(bytearray(host), dtype=torch.uint8)
-        dev = ps[0].device
-        table = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        if capturing:
+            if self._reserved is None:
+                raise RuntimeError("FusedClipAdam: reserve() the buffers before the capture")
+            table, ws, gnorm = self._reserved
+            self._reserved = None
+        else:
+            table, ws, gnorm = self._buffers(ps)
         wsb = lib.mdg_adam_workspace_bytes(nc)
-        ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
-        gnorm = torch.empty((), dtype=torch.float32, device=dev)
+        if table.numel() < nbytes or ws.numel() < wsb:
+            raise RuntimeError("FusedClipAdam: reserved buffers too small")
         if not capturing:
-            table.copy_(host_t)
+            table[:nbytes].copy_(host_t)
         g = self.opt.param_groups[0]
         b1, b2 = g["betas"]
         decoupled = isinstance(self.opt, torch.optim.AdamW) or bool(g.get("decoupled_weight_decay", False))
@@ -94,6 +124,6 @@ class FusedClipAdam:
     def finish_capture(self):
         """Write the device tables of the launches recorded by step(capturing=True)."""
         for table, host_t in self._pending:
-            table.copy_(host_t)
+            table[:host_t.numel()].copy_(host_t)
         self._pending = []
         torch.cuda.synchronize()

@@ -377,6 +377,8 @@ class GraphedStep:
             self.fused_opt = FusedClipAdam(tr.optimizer, self.params, tr.args.grad_clip)
         n = sum(p.numel() for p in self.params)
         self.flat = self.reducer.flat if self.overlap else (torch.empty(n, device=dev) if self.split else None)
+        if self.fused_opt is not None:
+            self.fused_opt.reserve()  # its tables outside the graph's private pool (optim_hip)
         self.g1 = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.g1):
             if self.overlap:

@@ -93,8 +93,13 @@ def test_fused_clip_adam_graph_replay_matches_eager():
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
     graph = torch.cuda.CUDAGraph()
+    fb.reserve()
     with torch.cuda.stream(s):
         with torch.cuda.graph(graph):
+            # temporaries freed inside the capture: their blocks go back to the graph's pool, and
+            # the replay rewrites them before the optimizer runs (must not hold its table)
+            junk = [torch.full((1 << 16,), 7.0, device="cuda") for _ in range(4)]
+            del junk
             nb = fb.step(capturing=True)
     torch.cuda.current_stream().wait_stream(s)
     fb.finish_capture()
