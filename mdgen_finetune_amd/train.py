@@ -380,7 +380,9 @@ class GraphedStep:
         if self.fused_opt is not None:
             self.fused_opt.reserve()  # its tables outside the graph's private pool (optim_hip)
         self.g1 = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.g1):
+        # thread-local capture: a process group's watchdog thread polls its events during the
+        # capture (global mode would fail that query and abort the process)
+        with torch.cuda.graph(self.g1, capture_error_mode="thread_local"):
             if self.overlap:
                 self.reducer.attach()
             self.loss, self.losses, self.t = self._fwd_bwd()
@@ -400,7 +402,7 @@ class GraphedStep:
                 p.grad = self.flat[off:off + p.numel()].view_as(p)
                 off += p.numel()
             self.g2 = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.g2):
+            with torch.cuda.graph(self.g2, capture_error_mode="thread_local"):
                 self.gnorm = self._update()
             if self.fused_opt is not None:
                 self.fused_opt.finish_capture()

@@ -35,7 +35,8 @@ def main():
             d = (p1.detach() - p2.detach()).abs().flatten()
             i = int(d.argmax())
             s1, s2 = tr.optimizer.state.get(p1, {}), tr2.optimizer.state.get(p2, {})
-            mom = lambda s, k: float(s[k].flatten()[i]) if k in s else float("nan")  # noqa: E731
+            mom = lambda s, k: (float(s[k].flatten()[min(i, s[k].numel() - 1)]) if k in s  # noqa: E731
+                                else float("nan"))
             rows.append((float(d[i]), name, mom(s1, "exp_avg"), mom(s2, "exp_avg"), mom(s1, "exp_avg_sq"),
                          mom(s2, "exp_avg_sq"), mom(s1, "step"), mom(s2, "step")))
         rows.sort(reverse=True)
