@@ -107,19 +107,21 @@ __global__ __launch_bounds__(256) void adam_update_kernel(int nt, int nc, const 
   const long long n = T.n, s0 = (long long)tab.ci[blockIdx.x] * kAdamChunk;
   const int len = (int)min((long long)kAdamChunk, n - s0);
   const float coef = ws[nc];
-  // per block in double, as torch's Python-float bias corrections (adam.py _single_tensor_adam)
+  // the arithmetic of torch's fused Adam (ATen fused_adam_utils.cuh adam_math): bias corrections
+  // in double from the fp32 step, handed over as fp32; the moments formed in double from the
+  // double hyper-parameters and rounded once; denom + eps in double; the parameter update in fp32
   const double st = (double)*T.step;
-  const float step_size = (float)(lr / (1.0 - pow(b1d, st))), bc2s = (float)sqrt(1.0 - pow(b2d, st));
-  const float keep = decoupled ? (float)(1.0 - lr * wdd) : 1.0f, l2 = decoupled ? 0.f : (float)wdd;
-  const float b1 = (float)b1d, b2 = (float)b2d, eps = (float)epsd;
-  const float omb1 = (float)(1.0 - b1d), omb2 = (float)(1.0 - b2d);  // 1 - beta rounded once, as torch
+  const float bc1 = (float)(1.0 - pow(b1d, st)), bc2s = (float)sqrt(1.0 - pow(b2d, st));
+  const float step_size = (float)(lr / (double)bc1);
   auto upd = [&](float& pp, float gg, float& mm, float& vv) {
-    float gc = gg * coef;
-    if (l2 != 0.f) gc = fmaf(l2, pp, gc);
-    pp *= keep;
-    mm = b1 * mm + omb1 * gc;
-    vv = b2 * vv + omb2 * gc * gc;
-    const float denom = sqrtf(vv) / bc2s + eps;
+    float gc = gg * coef;  // clip_grad_norm_'s in-place multiply
+    if (wdd != 0.0) {
+      if (decoupled) pp = (float)((double)pp - lr * wdd * (double)pp);
+      else gc = (float)((double)gc + (double)pp * wdd);
+    }
+    mm = (float)(b1d * (double)mm + (1.0 - b1d) * (double)gc);
+    vv = (float)(b2d * (double)vv + (1.0 - b2d) * (double)gc * (double)gc);
+    const float denom = (float)((double)(sqrtf(vv) / bc2s) + epsd);
     pp -= step_size * mm / denom;
   };
   p += s0, g += s0, m += s0, v += s0;

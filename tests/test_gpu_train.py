@@ -505,7 +505,13 @@ def test_tps_graphed_step_equals_eager_step():
         res[mode] = (loss, torch.cat([p.detach().flatten() for p in tr.wrapper.model.parameters()]))
     assert abs(res[0][0] - res[1][0]) <= 1e-5 * abs(res[0][0])
     p1 = res[1][1]
-    assert float((p1 - p2).abs().max()) <= 1e-6, float((p1 - p2).abs().max())
+    # two optimizer steps: the graphed step updates with the library's clip + Adam
+    # (optim_hip.FusedClipAdam), the eager one with torch's; their clip norms differ in the last
+    # bits, so the second step's gradients differ slightly, and Adam's eps regime (|g| ~ 1e-9,
+    # v ~ 1e-20: update ~ g / (sqrt(v) + eps)) turns that into up to ~1 % of lr on those elements
+    # (tools/diag_tps_graph.py: 8.6e-6 at lr 1e-3, 0 with MDG_TRAIN_FUSED_OPT=0).  A mis-staged
+    # second batch moves O(lr) on most parameters.
+    assert float((p1 - p2).abs().max()) <= 2e-2 * 1e-3, float((p1 - p2).abs().max())
 
 
 @pytest.mark.parametrize("L", [16, 20])
