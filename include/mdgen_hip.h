@@ -413,8 +413,10 @@ int mdg_ln_gate_bwd(int32_t dtype, int32_t M, int32_t C, int32_t rows_per_b, con
                     const float* dh_res, float* dh_out, const void* y, int32_t gate_off, void* dy, float* part,
                     void* stream);
 
-/* Bias-key gradient partial slots per head of the attention backward kernels below. */
-int32_t mdg_attn_temporal_bwd_parts(int32_t dtype, int32_t B, int32_t T, int32_t L);
+/* Bias-key gradient partial slots per head of the attention backward kernels below (every slot
+   is written; generic as passed to mdg_attn_temporal_bwd: the fused bf16 kernel writes one per
+   sequence, ABI 21). */
+int32_t mdg_attn_temporal_bwd_parts(int32_t dtype, int32_t B, int32_t T, int32_t L, int32_t generic);
 int32_t mdg_attn_spatial_bwd_parts(int32_t n_frames, int32_t L, int32_t D);
 /* Scratch of mdg_attn_temporal_bwd: dO planes CT [B*L][H][T][32], delta fp32 [B*L][H][T], and
    for bf16 with T > 256 the fused kernel's fp32 dQ accumulator [B*L][H][T][32]. */
@@ -434,8 +436,8 @@ int mdg_attn_temporal_bwd(int32_t dtype, int32_t B, int32_t T, int32_t L, int32_
                           const float* rope, int32_t rope_rows, void* scratch, void* dqkv, int32_t ld_dqkv,
                           float* bpart, float qscale, float kscale, int32_t generic, void* stream);
 /* Spatial attention backward (L < 16): q|k|v [N][3C] as saved by the forward, dout CT [N][C];
-   dq | dk | dv into dqkv [N][3C]; bias partials bpart [H][parts][2][32] (zero the buffer:
-   columns >= D of a slot may be left unwritten). */
+   dq | dk | dv into dqkv [N][3C]; bias partials bpart [H][parts][2][32] (every slot; columns
+   >= D of a slot may be left unwritten: mdg_train_unpack_layer reads d < D only). */
 int mdg_attn_spatial_bwd(int32_t dtype, int32_t n_frames, int32_t L, int32_t H, int32_t D, const void* qkv,
                          const float* kvb, const float* mask, const void* dout, const float* rope, int32_t rope_rows,
                          void* dqkv, float* bpart, float qscale, void* stream);
@@ -602,7 +604,7 @@ typedef struct {
   void* w1_p; void* w1_t; void* w2_p; void* w2_t;
 } mdg_train_pack;
 /* gwqkv / gbqkv: packed-order fp32 gradients ([3C][C], [3C]); bpart[i]: [H][parts[i]][2][32]
-   bias-key / value partials; part[0..3]: the ln_gate_bwd partials [B][nblk][4][C] of the
+   bias-key / value partials (summed here, one block per head: H <= 128); part[0..3]: the ln_gate_bwd partials [B][nblk][4][C] of the
    layer-input LN, the spatial, temporal and MLP sublayers.  Outputs fp32 in parameter layout;
    dmods [B][9C] in latent_model.py:459-461 chunk order. */
 typedef struct {

@@ -69,7 +69,7 @@ int ln_gate_bwd_blocks(int TL);
 hipError_t ln_gate_bwd_launch(int dtype, int M, int C, int TL, const void* dxn, const float* hln, const float* stats,
                               const float* mods, int mod_stride, int shift_off, int scale_off, const float* dh_res,
                               float* dh_out, const void* y, int gate_off, void* dy, float* part, hipStream_t s);
-int attn_bwd_parts(int dtype, int B, int T, int L);
+int attn_bwd_parts(int dtype, int B, int T, int L, int generic);
 hipError_t attn_temporal_bwd_launch(int dtype, int B, int T, int L, int H, int D, const void* qkv_t,
                                     const float* kbias, const float* kvb, const void* o, const void* o_lo,
                                     const void* dout,
@@ -982,9 +982,9 @@ int mdg_ln_gate_bwd(int32_t dtype, int32_t M, int32_t C, int32_t rows_per_b, con
                    "ln_gate_bwd");
 }
 
-int32_t mdg_attn_temporal_bwd_parts(int32_t dtype, int32_t B, int32_t T, int32_t L) {
+int32_t mdg_attn_temporal_bwd_parts(int32_t dtype, int32_t B, int32_t T, int32_t L, int32_t generic) {
   if (B <= 0 || T <= 0 || L <= 0) return 0;
-  return mdg::attn_bwd_parts(dtype, B, T, L);
+  return mdg::attn_bwd_parts(dtype, B, T, L, generic);
 }
 
 int32_t mdg_attn_spatial_bwd_parts(int32_t n_frames, int32_t L, int32_t D) {
@@ -1083,7 +1083,7 @@ int mdg_train_pack_layer(const mdg_train_pack* p, void* stream) {
 
 int mdg_train_unpack_layer(const mdg_train_unpack* u, void* stream) {
   if (!u) return fail(MDG_E_ARG, "train_unpack: null");
-  if (u->C <= 0 || u->H <= 0 || u->D <= 0 || u->C != u->H * u->D || u->D % 2 || u->D >= MDG_DP || u->B <= 0 ||
+  if (u->C <= 0 || u->H <= 0 || u->H > 128 || u->D <= 0 || u->C != u->H * u->D || u->D % 2 || u->D >= MDG_DP || u->B <= 0 ||
       u->nblk <= 0)
     return fail(MDG_E_SHAPE, "train_unpack: C=%d H=%d D=%d B=%d nblk=%d", u->C, u->H, u->D, u->B, u->nblk);
   for (int i = 0; i < 2; ++i) {

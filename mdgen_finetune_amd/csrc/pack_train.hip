@@ -136,28 +136,42 @@ __global__ __launch_bounds__(256) void unpack_kernel(const mdg_train_unpack u) {
         db[nn] = bv;
       }
     }
-  } else if (job < 4) {  // bias_k / bias_v gradients of attention job - 2 (the caller passes the
-    // partials already summed over their slots: parts = 1 in the training Function)
-    const int i = job - 2, np = u.parts[i];
-    const float* bp = u.bpart[i];  // [H][parts][2][32]
+  } else if (job < 4) {  // bias_k / bias_v gradients of attention job - 2: block h < H sums head
+    // h's [parts][2][32] slots (the 4 waves take every 4th slot, added in wave order), then
+    // applies the rotation's transpose from LDS
+    const int i = job - 2, np = u.parts[i], h = blockIdx.x;
+    if (h >= H) return;
+    __shared__ float red[4][2 * MDG_DP];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const float* bp = u.bpart[i] + (size_t)h * np * 2 * MDG_DP + lane;  // [H][parts][2][32]
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    int q = w;
+    for (; q + 12 < np; q += 16) {
+      a0 += bp[(size_t)q * 2 * MDG_DP];
+      a1 += bp[(size_t)(q + 4) * 2 * MDG_DP];
+      a2 += bp[(size_t)(q + 8) * 2 * MDG_DP];
+      a3 += bp[(size_t)(q + 12) * 2 * MDG_DP];
+    }
+    for (; q < np; q += 4) a0 += bp[(size_t)q * 2 * MDG_DP];
+    red[w][lane] = (a0 + a1) + (a2 + a3);
+    __syncthreads();
+    auto g = [&](int which, int d) {
+      const int e = which * MDG_DP + d;
+      return ((red[0][e] + red[1][e]) + red[2][e]) + red[3][e];
+    };
     const float* tab = u.rope_tab[i];
     const int S = u.rope_pos[i], rows = u.rope_rows[i];
-    auto g = [&](int h, int which, int d) {
-      float s = 0.f;
-      for (int q = 0; q < np; ++q) s += bp[(((size_t)h * np + q) * 2 + which) * MDG_DP + d];
-      return s;
-    };
-    for (int e = t0; e < H * D; e += stride) {
-      const int h = e / D, j = e - h * D;
-      u.gbias_v[i][e] = g(h, 1, j);
+    for (int j = threadIdx.x; j < D; j += blockDim.x) {
+      const int e = h * D + j;
+      u.gbias_v[i][e] = g(1, j);
       if (!u.rope) {
-        u.gbias_k[i][e] = g(h, 0, j);
+        u.gbias_k[i][e] = g(0, j);
         continue;
       }
       // gradient w.r.t. the rotated bias key, natural order; then the transpose of x c + rot(x) s
       const int jp = j < half ? j + half : j - half;
-      const float gr = g(h, 0, j < half ? 2 * j : 2 * (j - half) + 1);
-      const float grp = g(h, 0, jp < half ? 2 * jp : 2 * (jp - half) + 1);
+      const float gr = g(0, j < half ? 2 * j : 2 * (j - half) + 1);
+      const float grp = g(0, jp < half ? 2 * jp : 2 * (jp - half) + 1);
       const float c = tab[S * half + (j % half)], sp = tab[rows * half + S * half + (jp % half)];
       const float z = __fmul_rn(grp, sp);
       u.gbias_k[i][e] = __fadd_rn(__fmul_rn(gr, c), j < half ? z : -z);

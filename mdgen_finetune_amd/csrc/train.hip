@@ -1129,23 +1129,22 @@ __global__ __launch_bounds__(kBW * 64, 2) void attn_bwd_fused_bf16_kernel(
   };
   for (int kb = 0; kb + 1 < nkb; ++kb) key_pass(kb, std::false_type{});
   key_pass(nkb - 1, std::true_type{});
-  // bias partials: the 8 query groups of each (dim, gk / gv) summed in order; the sequence's
-  // first slot of the two-pass kernels' layout gets the block total, its other slots zero
+  // bias partials: the 8 query groups of each (dim, gk / gv) summed in order; one slot per
+  // (head, sequence) (attn_bwd_parts: B*L for this kernel)
   float* red = reinterpret_cast<float*>(dsT);
   red[tid] = bacc;
   __syncthreads();
-  const int nqb = (T + kBW * 32 - 1) / (kBW * 32), nps = nqb * kBW;
-  float* dst = bpart + ((size_t)head * BL * nps + (size_t)seq * nps) * 2 * kDP;
+  float* dst = bpart + ((size_t)head * BL + seq) * 2 * kDP;
   if (tid < 2 * kDP) {
     float s = 0.f;
 #pragma unroll
     for (int g = 0; g < 8; ++g) s += red[64 * g + tid];
     dst[tid] = (tid < kDP) ? s * kscale : s;
   }
-  for (int e = 2 * kDP + tid; e < nps * 2 * kDP; e += NTH) dst[e] = 0.f;
 }
 
-int attn_bwd_parts(int dtype, int B, int T, int L) {  // bias-gradient partial slots per head
+int attn_bwd_parts(int dtype, int B, int T, int L, int generic) {  // bias-gradient partial slots per head
+  if (dtype == MDG_BF16 && generic == 0) return B * L;  // the fused kernel: one per sequence
   if (dtype == MDG_BF16) return B * L * ((T + kBW * 32 - 1) / (kBW * 32)) * kBW;
   return B * L * ((T + 255) / 256);
 }

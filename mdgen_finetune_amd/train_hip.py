@@ -352,8 +352,8 @@ class _HipLayerFn(torch.autograd.Function):
                 Bq, Tq, Lq = (B, T, L) if i == 1 else (B * T, L, 1)
                 rope, rows = (rope_t, T + 1) if i == 1 else (rope_l, L + 1)
                 kb = kb_t if i == 1 else kb_s
-                parts = lib.mdg_attn_temporal_bwd_parts(dt, Bq, Tq, Lq)
-                bpart = torch.zeros(H, parts, 2, _lib.MDG_DP, device=dev)
+                parts = lib.mdg_attn_temporal_bwd_parts(dt, Bq, Tq, Lq, _ATTN_BWD_VARIANT)
+                bpart = torch.empty(H, parts, 2, _lib.MDG_DP, device=dev)  # every slot is written
                 scratch = torch.empty(lib.mdg_attn_temporal_bwd_scratch(dt, Bq, Tq, Lq, H), device=dev,
                                       dtype=torch.uint8)
                 _lib.check(lib.mdg_attn_temporal_bwd(dt, Bq, Tq, Lq, H, D, qkv.data_ptr(), kb.data_ptr(),
@@ -365,14 +365,13 @@ class _HipLayerFn(torch.autograd.Function):
                            "mdg_attn_temporal_bwd")
             else:
                 parts = lib.mdg_attn_spatial_bwd_parts(B * T, L, D)
-                bpart = torch.zeros(H, parts, 2, _lib.MDG_DP, device=dev)
+                bpart = torch.empty(H, parts, 2, _lib.MDG_DP, device=dev)
                 _lib.check(lib.mdg_attn_spatial_bwd(dt, B * T, L, H, D, qkv.data_ptr(), P["kvb0"].data_ptr(),
                                                     ctx.mask.data_ptr(), do.data_ptr(), _lib.ptr(rope_l), L + 1,
                                                     dqkv.data_ptr(), bpart.data_ptr(), qscale, s),
                            "mdg_attn_spatial_bwd")
-            # [H][1][2][32]: the partials summed over their slots by one reduction kernel (the
-            # unpack launch summing 1 024 temporal slots per element serially took 1 ms)
-            grads[f"kvb{i}"] = bpart.sum(1, keepdim=True)
+            # [H][parts][2][32]: the unpack sums the slots (one block per head, 4 waves in order)
+            grads[f"kvb{i}"] = bpart
             grads[f"wqkv{i}"], grads[f"bqkv{i}"] = wg(dqkv, xn, True)
             return dx_gemm(dqkv, P[f"wqkv_t{i}"], 3 * C, C)
 

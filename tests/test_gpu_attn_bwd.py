@@ -134,8 +134,8 @@ def test_temporal_attention_backward_multi_chunk(dtype, T, n_pad):
         kb = c["kbias"].float().contiguous()
         lse_f = lse.float().contiguous()
         rope = torch.cat([cos.float().reshape(-1), sin.float().reshape(-1)]).contiguous()
-        parts = lib.mdg_attn_temporal_bwd_parts(mdt, B, T, L)
-        bpart = torch.zeros(H, parts, 2, DP, device=dev)
+        parts = lib.mdg_attn_temporal_bwd_parts(mdt, B, T, L, generic)
+        bpart = torch.full((H, parts, 2, DP), float("nan"), device=dev)  # every slot is written
         scratch = torch.empty(lib.mdg_attn_temporal_bwd_scratch(mdt, B, T, L, H), device=dev, dtype=torch.uint8)
         dqkv = torch.full((B * T * L, 3 * C), float("nan"), device=dev, dtype=ct)
         _lib.check(lib.mdg_attn_temporal_bwd(mdt, B, T, L, H, D, planes.data_ptr(), kb.data_ptr(), kvb.data_ptr(),
