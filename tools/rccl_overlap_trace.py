@@ -4,6 +4,7 @@ the last replayed steps, when it started within the step, how long it ran, which
 ran concurrently with it (overlap with backward) and how many kernels of the step started after
 it.  Usage: python tools/rccl_overlap_trace.py <kernel_trace.csv> <buckets per step> [out.md]"""
 import csv
+import re
 import sys
 
 
@@ -18,8 +19,10 @@ def main():
     is_coll = [("nccl" in n.lower() or "rccl" in n.lower()) for _, _, n in rows]
     coll = [i for i, c in enumerate(is_coll) if c]
     if len(coll) < nb:
-        print(f"only {len(coll)} collective kernels in the trace", file=sys.stderr)
-        sys.exit(1)
+        # world 1: RCCL elides a one-rank all-reduce (no collective kernel); the bucket's packing
+        # `cat`, issued by the same hook on the same branch right before the collective, marks when
+        # each bucket left backward
+        return world1(path, rows, nb, out)
     nsteps = len(coll) // nb
     lines = [f"# In-graph RCCL bucket all-reduces ({path.split('/')[-1]})", "",
              f"{len(rows)} kernels, {len(coll)} collective kernels, {nb} buckets per step, {nsteps} steps traced.", ""]
@@ -41,6 +44,33 @@ def main():
             lines.append(f"| {b} | {(st - t0) / 1e3:.1f} | {(en - st) / 1e3:.1f} | {len(conc)} | {after} | "
                          f"{', '.join(ex)} |")
         lines.append("")
+    txt = "\n".join(lines)
+    print(txt)
+    if out:
+        with open(out, "w") as f:
+            f.write(txt + "\n")
+
+
+def world1(path, rows, nb, out):
+    marks = [i for i, (_, _, n) in enumerate(rows) if "prep_latents" in n]
+    lo, hi = marks[-2], marks[-1]  # the last complete replayed step
+    t0, t1 = rows[lo][0], rows[hi - 1][1]
+    bwd0 = min((i for i in range(lo, hi) if "wgrad" in rows[i][2]), default=lo)  # backward's first dW
+    cats = [i for i in range(bwd0, hi) if "CatArrayBatchedCopy" in rows[i][2]]
+    bwd_end = max((rows[i][1] for i in range(lo, hi) if "adam" not in rows[i][2]
+                   and ("bwd" in rows[i][2] or "wgrad" in rows[i][2])), default=t1)
+    lines = [f"# In-graph bucket all-reduces, world-1 rehearsal ({path.split('/')[-1]})", "",
+             "A one-rank RCCL all-reduce launches no collective kernel, so this trace cannot show the "
+             "collectives themselves; each bucket's packing `cat` (same post-accumulate hook, same side "
+             "branch, immediately before the bucket's all-reduce) marks when the bucket left backward.",
+             f"Last complete step: {hi - lo} kernels, {(t1 - t0) / 1e3:.1f} us; backward's last kernel "
+             f"ends {(bwd_end - t0) / 1e3:.1f} us into the step; {nb} buckets expected.", "",
+             "| packing kernel | start (us into step) | duration (us) | step kernels started after it |",
+             "|---|---|---|---|"]
+    for i in cats:
+        st, en, name = rows[i]
+        short = re.search(r"CatArrayBatchedCopy\w*", name).group(0)
+        lines.append(f"| `{short}` | {(st - t0) / 1e3:.1f} | {(en - st) / 1e3:.1f} | {hi - i - 1} |")
     txt = "\n".join(lines)
     print(txt)
     if out:
