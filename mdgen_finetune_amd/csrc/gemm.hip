@@ -688,7 +688,11 @@ __device__ __forceinline__ void epi_tile8(const mdg_gemm_desc& p, const float* _
   }
 }
 
-template <int EPI, int BK, bool WIDE = false>  // WIDE: the 16-B-store epilogue (epi_tile8)
+// NS: operand ring depth.  2 (default for BK 64): wait for everything, then prefetch one step
+// ahead.  3 / 4 (BK 32, the training step's large-M GEMMs, MDG_B4_STAGES): stages issued NS - 1
+// steps ahead and a COUNTED vmcnt per step (the next stages' loads stay in flight across the
+// barrier), as the 256x128 kernel below; LDS NS x 16 KiB.
+template <int EPI, int BK, bool WIDE = false, int NS = 2>  // WIDE: the 16-B-store epilogue (epi_tile8)
 __global__ __launch_bounds__(kB4Threads) void gemm_bf16_b4_kernel(const mdg_gemm_desc p) {
   constexpr int BM = kB4Tile, BN = kB4Tile, TILE = BM * BK, LDS_ST = BN + 4;
   constexpr int CPR = BK / 8;      // 16-B chunks per tile row
@@ -740,14 +744,36 @@ __global__ __launch_bounds__(kB4Threads) void gemm_bf16_b4_kernel(const mdg_gemm
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  MDG_B4_LOAD(0, 0);
   const int nk = K / BK;
   const int swz = swz_of(lr);  // every fragment row this lane reads is lr mod 16
+  MDG_B4_LOAD(0, 0);
+  if constexpr (NS > 2) {
+#pragma unroll
+    for (int s0 = 1; s0 < NS - 1; ++s0)
+      if (s0 < nk) MDG_B4_LOAD(s0, s0 * BK);
+  }
+  int cur = 0;
   for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (kt + 1 < nk) MDG_B4_LOAD(cur ^ 1, (kt + 1) * BK);
+    if constexpr (NS == 2) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (kt + 1 < nk) MDG_B4_LOAD(cur ^ 1, (kt + 1) * BK);
+    } else {
+      // stage kt landed for this wave: the loads of the (at most NS - 2) later stages already
+      // issued stay outstanding (2 NLD per stage); then every wave's loads + every wave done
+      // reading stage kt - 1 (lgkmcnt: its ds_reads retired), whose slot is refilled below
+      const int ahead = min(NS - 2, nk - 1 - kt);
+      if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * NLD) : "memory");
+      else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NLD) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (kt + NS - 1 < nk) {
+        const int nb = (cur + NS - 1) % NS;
+        MDG_B4_LOAD(nb, (kt + NS - 1) * BK);
+      }
+    }
     const bf16_t* As = lds + cur * 2 * TILE;
     const bf16_t* Bs = As + TILE;
 #pragma unroll
@@ -763,6 +789,7 @@ __global__ __launch_bounds__(kB4Threads) void gemm_bf16_b4_kernel(const mdg_gemm
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
     }
+    cur = (NS == 2) ? (cur ^ 1) : (cur + 1 == NS ? 0 : cur + 1);
   }
 #undef MDG_B4_LOAD
 
@@ -792,23 +819,48 @@ __global__ __launch_bounds__(kB4Threads) void gemm_bf16_b4_kernel(const mdg_gemm
   }
 }
 
-template <int BK>
+template <int BK, int NS = 2>
 __host__ __device__ constexpr size_t b4_smem() {
-  return BK == 64 ? (size_t)kB4Tile * (kB4Tile + 4) * 4 : (size_t)(kB4Tile / 2) * (kB4Tile + 4) * 4;
+  // max(the operand ring, the fp32 epilogue image: the whole tile (BK 64) or a 64-row band)
+  return BK == 64 ? (size_t)kB4Tile * (kB4Tile + 4) * 4
+                  : (NS * 2 * kB4Tile * BK * 2 > (kB4Tile / 2) * (kB4Tile + 4) * 4
+                         ? (size_t)NS * 2 * kB4Tile * BK * 2
+                         : (size_t)(kB4Tile / 2) * (kB4Tile + 4) * 4);
 }
 
-template <int EPI, int BK, bool WIDE>
+template <int EPI, int BK, bool WIDE, int NS>
 static hipError_t launch_b4_v(const mdg_gemm_desc& p, hipStream_t s) {
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_bf16_b4_kernel<EPI, BK, WIDE>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)b4_smem<BK>());
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_bf16_b4_kernel<EPI, BK, WIDE, NS>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)b4_smem<BK, NS>());
     if (e != hipSuccess) return e;
     attr_set = true;
   }
   const int nwg = (p.N / kB4Tile) * ((p.M + kB4Tile - 1) / kB4Tile);
-  hipLaunchKernelGGL((gemm_bf16_b4_kernel<EPI, BK, WIDE>), dim3(nwg), dim3(kB4Threads), b4_smem<BK>(), s, p);
+  constexpr size_t smem = b4_smem<BK, NS>();
+  hipLaunchKernelGGL((gemm_bf16_b4_kernel<EPI, BK, WIDE, NS>), dim3(nwg), dim3(kB4Threads), smem, s, p);
   return hipGetLastError();
+}
+
+// operand ring depth of the K-step-32 kernel (MDG_B4_STAGES=2|3|4)
+static int b4_stages() {
+  static const int v = [] {
+    const char* e = getenv("MDG_B4_STAGES");
+    const int n = e ? atoi(e) : 2;
+    return (n == 3 || n == 4) ? n : 2;
+  }();
+  return v;
+}
+
+template <int EPI, int BK, bool WIDE>
+static hipError_t launch_b4_ns(const mdg_gemm_desc& p, hipStream_t s) {
+  if constexpr (BK == 32) {
+    const int ns = b4_stages();
+    if (ns == 3) return launch_b4_v<EPI, BK, WIDE, 3>(p, s);
+    if (ns == 4) return launch_b4_v<EPI, BK, WIDE, 4>(p, s);
+  }
+  return launch_b4_v<EPI, BK, WIDE, 2>(p, s);
 }
 
 // the 16-B-store epilogue where its alignment holds (MDG_WIDE_EPI=0: the 8-B one, A/B knob)
@@ -822,8 +874,8 @@ static hipError_t launch_b4(const mdg_gemm_desc& p, hipStream_t s) {
   if constexpr (EPI == MDG_EPI_STORE) wide = p.ldo % 8 == 0 && (!p.aux || p.ldaux % 8 == 0);
   if constexpr (EPI == MDG_EPI_QKV) wide = p.D % 8 == 0;
   if constexpr (EPI == MDG_EPI_STORE || EPI == MDG_EPI_QKV)
-    if (wide && knob) return launch_b4_v<EPI, BK, true>(p, s);
-  return launch_b4_v<EPI, BK, false>(p, s);
+    if (wide && knob) return launch_b4_ns<EPI, BK, true>(p, s);
+  return launch_b4_ns<EPI, BK, false>(p, s);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -3244,7 +3296,7 @@ GemmPlan gemm_plan(const mdg_gemm_desc& p) {
       g.bm = kB4Tile;
     } else {
       g.cfg = kCfgB4K32;  // 128x128, K-step 32, four blocks per CU
-      g.smem = b4_smem<32>();
+      g.smem = b4_stages() == 4 ? b4_smem<32, 4>() : b4_stages() == 3 ? b4_smem<32, 3>() : b4_smem<32>();
       g.bm = kB4Tile;
     }
     g.bn = 128;

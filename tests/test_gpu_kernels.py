@@ -49,7 +49,8 @@ def _ln_mod(a, mods, rows_per, sh_off, sc_off, C, eps=1e-6):
 
 
 @pytest.mark.parametrize("dt", ["f32", "bf16"])
-@pytest.mark.parametrize("M,N,K,act", [(200, 384, 384, 0), (64, 1536, 384, 1), (130, 192, 1536, 2), (7, 64, 64, 0)])
+@pytest.mark.parametrize("M,N,K,act", [(200, 384, 384, 0), (64, 1536, 384, 1), (130, 192, 1536, 2), (7, 64, 64, 0),
+                                        (300, 128, 64, 0), (257, 256, 128, 1), (520, 384, 1536, 0)])
 def test_gemm_plain_store(lib, dt, M, N, K, act):
     from mdgen_finetune_amd import _lib
 
