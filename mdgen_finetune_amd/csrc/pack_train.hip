@@ -121,7 +121,39 @@ __global__ __launch_bounds__(256) void unpack_kernel(const mdg_train_unpack u) {
   const int job = blockIdx.y;
   const int stride = gridDim.x * blockDim.x;
   const int t0 = blockIdx.x * blockDim.x + threadIdx.x;
-  if (job < 2) {  // q|k|v weight + bias gradients of attention `job`, natural row order
+  const bool vec = job < 2 && C % 4 == 0 &&
+                   ((reinterpret_cast<uintptr_t>(u.gwqkv[job & 1]) | reinterpret_cast<uintptr_t>(u.gq[job & 1]) |
+                     reinterpret_cast<uintptr_t>(u.gk[job & 1]) | reinterpret_cast<uintptr_t>(u.gv[job & 1])) & 15) == 0;
+  if (vec) {  // q|k|v weight + bias gradients of attention `job`, natural row order:
+    // float4 pieces, four per thread loaded before any is stored (the loads of a scalar loop
+    // could not pass its stores: 13 dependent round trips per thread)
+    const int i = job, C4 = C / 4, total = 3 * C * C4;
+    constexpr int U = 4;
+    for (int e0 = t0; e0 < total; e0 += U * stride) {
+      float4 v[U];
+      int nn_[U], blk_[U], k4_[U], r_[U];
+#pragma unroll
+      for (int j = 0; j < U; ++j) {
+        const int e = min(e0 + j * stride, total - 1);
+        const int n = e / C4, k4 = e - n * C4;
+        const int blk = n / C, nn = n - blk * C;
+        const int r = blk * C + (blk < 2 && u.rope ? packed_of_nat(nn, D) : nn);
+        v[j] = *reinterpret_cast<const float4*>(u.gwqkv[i] + (size_t)r * C + 4 * k4);
+        nn_[j] = nn, blk_[j] = blk, k4_[j] = k4, r_[j] = r;
+      }
+#pragma unroll
+      for (int j = 0; j < U; ++j) {
+        if (e0 + j * stride >= total) break;
+        const int blk = blk_[j], nn = nn_[j];
+        float* dst = blk == 0 ? u.gq[i] : blk == 1 ? u.gk[i] : u.gv[i];
+        *reinterpret_cast<float4*>(dst + (size_t)nn * C + 4 * k4_[j]) = v[j];
+        if (k4_[j] == 0) {
+          float* db = blk == 0 ? u.gbq[i] : blk == 1 ? u.gbk[i] : u.gbv[i];
+          db[nn] = u.gbqkv[i][r_[j]];
+        }
+      }
+    }
+  } else if (job < 2) {  // (C % 4 != 0 or unaligned) one element per step
     const int i = job;
     for (int e = t0; e < 3 * C * C; e += stride) {
       const int n = e / C, k = e - n * C;  // natural row n of [q; k; v]

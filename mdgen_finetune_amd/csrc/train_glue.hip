@@ -58,17 +58,20 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(int B, int T, int L, int
                                                         const int64_t* __restrict__ idx, int E,
                                                         const float* __restrict__ dh, float* __restrict__ ws,
                                                         EbPlan pl) {
-  // the chunk's x1 and x2 rows, zero-padded to kEbK columns (64 KiB: two blocks per CU)
-  __shared__ __attribute__((aligned(16))) float xs[2][kEbFrames * kEbLMax][kEbK];
+  // the chunk's x1 and x2 rows, zero-padded to kEbK columns: [2][kEbFrames L][kEbK] (dynamic:
+  // 32 KiB at L = 4, four blocks per CU)
+  extern __shared__ __attribute__((aligned(16))) float xs_[];
   const int chunk = blockIdx.x, b = chunk / pl.tch, tc = chunk % pl.tch;
   const int t0 = tc * kEbFrames, nf = min(kEbFrames, T - t0), ntok = nf * L;
+  float (*xs0)[kEbK] = reinterpret_cast<float (*)[kEbK]>(xs_);
+  float (*xs1)[kEbK] = reinterpret_cast<float (*)[kEbK]>(xs_ + (size_t)kEbFrames * L * kEbK);
   const size_t n0 = ((size_t)b * T + t0) * L;
   const int tid = threadIdx.x, op = tid >> 7, c = blockIdx.y * 128 + (tid & 127);
   const int K = op ? K2 : K1;
   for (int i = tid; i < ntok * kEbK; i += 256) {
     const int r = i / kEbK, k = i % kEbK;
-    xs[0][r][k] = k < K1 ? x1[(n0 + r) * K1 + k] : 0.f;
-    xs[1][r][k] = (x2 && k < K2) ? x2[(n0 + r) * K2 + k] : 0.f;
+    xs0[r][k] = k < K1 ? x1[(n0 + r) * K1 + k] : 0.f;
+    xs1[r][k] = (x2 && k < K2) ? x2[(n0 + r) * K2 + k] : 0.f;
   }
   __syncthreads();
   if (c >= C || (op && !x2)) return;
@@ -80,7 +83,7 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(int B, int T, int L, int
   for (int u = 0; u < kEbLMax; ++u) lsum[u] = 0.f;
 #pragma unroll
   for (int u = 0; u < kEbEMax; ++u) esum[u] = 0.f;
-  const float (*X)[kEbK] = xs[op];
+  const float (*X)[kEbK] = op ? xs1 : xs0;
   const float* dcol = dh + n0 * C + c;
   auto row = [&](int r, float g, int e) {
     const int l = r % L;
@@ -103,23 +106,20 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(int B, int T, int L, int
       for (int q = 0; q < kEbEMax; ++q) esum[q] += (q == e) ? g : 0.f;
     }
   };
-  // rows in groups of 4 whose dh (and mask index) loads are issued before any of them is used:
+  // rows in groups of 8 whose dh (and mask index) loads are issued before any of them is used:
   // one dependent HBM round trip per group instead of per row
+  constexpr int G = 8;
   int rr = 0;
-  for (; rr + 4 <= ntok; rr += 4) {
-    const float g0 = dcol[(size_t)rr * C], g1 = dcol[(size_t)(rr + 1) * C], g2 = dcol[(size_t)(rr + 2) * C],
-                g3 = dcol[(size_t)(rr + 3) * C];
-    int e0 = -1, e1 = -1, e2 = -1, e3 = -1;
-    if (op && idx) {
-      e0 = (int)idx[n0 + rr];
-      e1 = (int)idx[n0 + rr + 1];
-      e2 = (int)idx[n0 + rr + 2];
-      e3 = (int)idx[n0 + rr + 3];
+  for (; rr + G <= ntok; rr += G) {
+    float g[G];
+    int e[G];
+#pragma unroll
+    for (int j = 0; j < G; ++j) {
+      g[j] = dcol[(size_t)(rr + j) * C];
+      e[j] = (op && idx) ? (int)idx[n0 + rr + j] : -1;
     }
-    row(rr, g0, e0);
-    row(rr + 1, g1, e1);
-    row(rr + 2, g2, e2);
-    row(rr + 3, g3, e3);
+#pragma unroll
+    for (int j = 0; j < G; ++j) row(rr + j, g[j], e[j]);
   }
   for (; rr < ntok; ++rr) row(rr, dcol[(size_t)rr * C], (op && idx) ? (int)idx[n0 + rr] : -1);
   {  // [chunk][k][C]: each store instruction writes 64 consecutive floats
@@ -607,7 +607,8 @@ hipError_t embed_bwd_launch(int B, int T, int L, int C, int K1, const float* x1,
                             const int64_t* idx, int E, const float* dh, float* dw1, float* dw2, float* db, float* demb,
                             float* dipa, float* ws, hipStream_t s) {
   const EbPlan pl = eb_plan(B, T, L, C, K1, x2 ? K2 : 0, E);
-  hipLaunchKernelGGL(embed_bwd_kernel, dim3(pl.chunks, (C + 127) / 128), dim3(256), 0, s, B, T, L, C, K1, x1,
+  const size_t smem = (size_t)2 * kEbFrames * L * kEbK * sizeof(float);
+  hipLaunchKernelGGL(embed_bwd_kernel, dim3(pl.chunks, (C + 127) / 128), dim3(256), smem, s, B, T, L, C, K1, x1,
                      x2 ? K2 : 0, x2, idx, E, dh, ws, pl);
   if (hipError_t e = hipGetLastError()) return e;
   auto r64 = [](long long v) { return (v + 63) / 64 * 64; };
