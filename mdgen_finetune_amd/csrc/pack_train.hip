@@ -176,16 +176,22 @@ __global__ __launch_bounds__(256) void unpack_kernel(const mdg_train_unpack u) {
     __shared__ float red[4][2 * MDG_DP];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const float* bp = u.bpart[i] + (size_t)h * np * 2 * MDG_DP + lane;  // [H][parts][2][32]
-    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    // 16 slots in flight per lane (the spatial backward leaves 500 per head at B = 8, T = 1000)
+    constexpr int NA = 16;
+    float a[NA];
+#pragma unroll
+    for (int j = 0; j < NA; ++j) a[j] = 0.f;
     int q = w;
-    for (; q + 12 < np; q += 16) {
-      a0 += bp[(size_t)q * 2 * MDG_DP];
-      a1 += bp[(size_t)(q + 4) * 2 * MDG_DP];
-      a2 += bp[(size_t)(q + 8) * 2 * MDG_DP];
-      a3 += bp[(size_t)(q + 12) * 2 * MDG_DP];
+    for (; q + 4 * (NA - 1) < np; q += 4 * NA) {
+#pragma unroll
+      for (int j = 0; j < NA; ++j) a[j] += bp[(size_t)(q + 4 * j) * 2 * MDG_DP];
     }
-    for (; q < np; q += 4) a0 += bp[(size_t)q * 2 * MDG_DP];
-    red[w][lane] = (a0 + a1) + (a2 + a3);
+    for (; q < np; q += 4) a[0] += bp[(size_t)q * 2 * MDG_DP];
+#pragma unroll
+    for (int st = NA / 2; st >= 1; st >>= 1)
+#pragma unroll
+      for (int j = 0; j < st; ++j) a[j] += a[j + st];
+    red[w][lane] = a[0];
     __syncthreads();
     auto g = [&](int which, int d) {
       const int e = which * MDG_DP + d;
