@@ -224,6 +224,7 @@ __global__ __launch_bounds__(256) void unpack_kernel(const mdg_train_unpack u) {
       const int b = e0 / (9 * C), ck = e0 - b * 9 * C, c9 = ck / C, k = ck - c9 * C;
       const float* pp = u.part[src[c9]];
       float s = 0.f;
+#pragma unroll 4
       for (int q = g; q < nb; q += 8) s += pp[(((size_t)b * nb + q) * 4 + row[c9]) * C + k];
       s += __shfl_xor(s, 1, 64);
       s += __shfl_xor(s, 2, 64);
@@ -256,7 +257,8 @@ hipError_t train_pack_launch(const mdg_train_pack& p, hipStream_t s) {
 }
 
 hipError_t train_unpack_launch(const mdg_train_unpack& u, hipStream_t s) {
-  hipLaunchKernelGGL(unpack_kernel, dim3(128, 6), dim3(256), 0, s, u);
+  // 512 x 6: the adaLN / bias row-block sums (jobs 4, 5) get 4 x the lanes of the old 128-wide grid
+  hipLaunchKernelGGL(unpack_kernel, dim3(512, 6), dim3(256), 0, s, u);
   return hipGetLastError();
 }
 
