@@ -65,7 +65,9 @@ __global__ __launch_bounds__(256) void pack_kernel(const mdg_train_pack p) {
 #pragma clang fp contract(off)
   __shared__ float tile[32][33];
   const int C = p.C, D = p.D, F = p.F, H = p.H, half = D / 2;
-  const int job = blockIdx.y;
+  // the bias-key slot sums (jobs 2, 3: the longest dependent chains) take the first grid rows,
+  // so they are dispatched first
+  const int job = (blockIdx.y + 2) % 6;
   const int stride = gridDim.x * blockDim.x;
   const int t0 = blockIdx.x * blockDim.x + threadIdx.x;
   if (job < 2) {  // q|k|v weight of attention `job`
@@ -118,7 +120,9 @@ __global__ __launch_bounds__(256) void pack_kernel(const mdg_train_pack p) {
 __global__ __launch_bounds__(256) void unpack_kernel(const mdg_train_unpack u) {
 #pragma clang fp contract(off)
   const int C = u.C, D = u.D, H = u.H, B = u.B, nb = u.nblk, half = D / 2;
-  const int job = blockIdx.y;
+  // the bias-key slot sums (jobs 2, 3: the longest dependent chains) take the first grid rows,
+  // so they are dispatched first
+  const int job = (blockIdx.y + 2) % 6;
   const int stride = gridDim.x * blockDim.x;
   const int t0 = blockIdx.x * blockDim.x + threadIdx.x;
   const bool vec = job < 2 && C % 4 == 0 &&
@@ -257,8 +261,7 @@ hipError_t train_pack_launch(const mdg_train_pack& p, hipStream_t s) {
 }
 
 hipError_t train_unpack_launch(const mdg_train_unpack& u, hipStream_t s) {
-  // 512 x 6: the adaLN / bias row-block sums (jobs 4, 5) get 4 x the lanes of the old 128-wide grid
-  hipLaunchKernelGGL(unpack_kernel, dim3(512, 6), dim3(256), 0, s, u);
+  hipLaunchKernelGGL(unpack_kernel, dim3(128, 6), dim3(256), 0, s, u);
   return hipGetLastError();
 }
 
