@@ -65,9 +65,7 @@ __global__ __launch_bounds__(256) void pack_kernel(const mdg_train_pack p) {
 #pragma clang fp contract(off)
   __shared__ float tile[32][33];
   const int C = p.C, D = p.D, F = p.F, H = p.H, half = D / 2;
-  // the bias-key slot sums (jobs 2, 3: the longest dependent chains) take the first grid rows,
-  // so they are dispatched first
-  const int job = (blockIdx.y + 2) % 6;
+  const int job = blockIdx.y;
   const int stride = gridDim.x * blockDim.x;
   const int t0 = blockIdx.x * blockDim.x + threadIdx.x;
   if (job < 2) {  // q|k|v weight of attention `job`
@@ -120,9 +118,7 @@ __global__ __launch_bounds__(256) void pack_kernel(const mdg_train_pack p) {
 __global__ __launch_bounds__(256) void unpack_kernel(const mdg_train_unpack u) {
 #pragma clang fp contract(off)
   const int C = u.C, D = u.D, H = u.H, B = u.B, nb = u.nblk, half = D / 2;
-  // the bias-key slot sums (jobs 2, 3: the longest dependent chains) take the first grid rows,
-  // so they are dispatched first
-  const int job = (blockIdx.y + 2) % 6;
+  const int job = blockIdx.y;
   const int stride = gridDim.x * blockDim.x;
   const int t0 = blockIdx.x * blockDim.x + threadIdx.x;
   const bool vec = job < 2 && C % 4 == 0 &&
