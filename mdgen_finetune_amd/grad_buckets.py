@@ -10,7 +10,8 @@ step's host-launch bound, so this class does DDP's job inside the capture:
   gradients (recorded once from post-accumulate-grad hooks during warm-up), cut into buckets
   of ``cap_bytes``, so each bucket is one contiguous slice that becomes final at one moment;
 * a post-accumulate-grad hook counts a bucket's parameters down; when the last one lands, the
-  bucket's gradients are packed into its slice (one ``cat`` on the producing stream), an event
+  bucket's gradients are packed into its slice (one foreach copy on the producing stream; every
+  gradient 16-B aligned in the buffer), an event
   forks a side stream, and the slice's all-reduce (RCCL over xGMI) + 1/world scale run there
   while backward continues on the main stream;
 * ``finish()`` joins the side stream (graph-capture legal: event record / wait) and points
@@ -57,7 +58,10 @@ class BucketedAllReduce:
             size += nb
         if cur:
             self.buckets.append(cur)
-        n = sum(self.params[i].numel() for b in self.buckets for i in b)
+        # every gradient starts on a 16-B boundary (the library optimizer's float4 path); the pad
+        # elements stay zero and are reduced along with the bucket
+        pad4 = lambda v: (v + 3) // 4 * 4  # noqa: E731
+        n = sum(pad4(self.params[i].numel()) for b in self.buckets for i in b)
         self.flat = torch.zeros(n, device=dev, dtype=torch.float32)
         self.slices, self.views, self.bucket_of, off = [], {}, {}, 0
         for bi, b in enumerate(self.buckets):
@@ -66,7 +70,7 @@ class BucketedAllReduce:
                 p = self.params[i]
                 self.views[i] = self.flat[off:off + p.numel()].view_as(p)
                 self.bucket_of[i] = bi
-                off += p.numel()
+                off += pad4(p.numel())
             self.slices.append(self.flat[start:off])
         self.cuda = dev.type == "cuda"
         self.side = torch.cuda.Stream(device=dev) if self.cuda else None
@@ -100,14 +104,16 @@ class BucketedAllReduce:
     def _launch(self, bi):
         self.launch_log.append((bi, self._fired))
         sl = self.slices[bi]
-        torch.cat([self.params[i].grad.reshape(-1) for i in self.buckets[bi]], out=sl)
+        b = self.buckets[bi]
+        torch._foreach_copy_([self.views[i] for i in b], [self.params[i].grad for i in b])
         if self.cuda:
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(sl.device))
             self.side.wait_event(ev)
             with torch.cuda.stream(self.side):
                 dist.all_reduce(sl, group=self.group)
-                sl.div_(self.world)
+                if self.world > 1:
+                    sl.div_(self.world)
         else:
             self._works.append((dist.all_reduce(sl, group=self.group, async_op=True), sl))
 
@@ -122,7 +128,8 @@ class BucketedAllReduce:
         else:
             for w, sl in self._works:
                 w.wait()
-                sl.div_(self.world)
+                if self.world > 1:
+                    sl.div_(self.world)
         for i, v in self.views.items():
             self.params[i].grad = v
         self.detach()

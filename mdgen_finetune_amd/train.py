@@ -272,7 +272,7 @@ class Trainer:
 
 
 class GraphedStep:
-    """The optimizer step as hipGraph replays (Trainer.graph_mode).
+    r"""The optimizer step as hipGraph replays (Trainer.graph_mode).
 
     The eager step launches ~2 300 kernels from the host (the IPA / t-MLP / loss autograd, the
     per-layer weight packing, the HIP layer kernels): 33 ms of CPU against ~25 ms of GPU work per

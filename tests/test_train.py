@@ -256,7 +256,8 @@ def _bucket_worker(rank, world, port, out):
     backward()
     red.finish()
     out[rank] = (err, scale, len(red.buckets), red.launch_log, len(order), float((red.flat - g1).abs().max()),
-                 sum(p.numel() for p, lg in zip(params, local) if lg is not None) == red.flat.numel())
+                 sum((p.numel() + 3) // 4 * 4 for p, lg in zip(params, local) if lg is not None) == red.flat.numel()
+                 and all((v.data_ptr() - red.flat.data_ptr()) % 16 == 0 for v in red.views.values()))
     dist.destroy_process_group()
 
 
