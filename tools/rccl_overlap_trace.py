@@ -56,20 +56,22 @@ def world1(path, rows, nb, out):
     lo, hi = marks[-2], marks[-1]  # the last complete replayed step
     t0, t1 = rows[lo][0], rows[hi - 1][1]
     bwd0 = min((i for i in range(lo, hi) if "wgrad" in rows[i][2]), default=lo)  # backward's first dW
-    cats = [i for i in range(bwd0, hi) if "CatArrayBatchedCopy" in rows[i][2]]
+    pack = lambda n: "CatArrayBatchedCopy" in n or "TensorListMetadata<2>" in n  # noqa: E731  (cat / foreach copy)
+    cats = [i for i in range(bwd0, hi) if pack(rows[i][2])]
     bwd_end = max((rows[i][1] for i in range(lo, hi) if "adam" not in rows[i][2]
                    and ("bwd" in rows[i][2] or "wgrad" in rows[i][2])), default=t1)
     lines = [f"# In-graph bucket all-reduces, world-1 rehearsal ({path.split('/')[-1]})", "",
              "A one-rank RCCL all-reduce launches no collective kernel, so this trace cannot show the "
-             "collectives themselves; each bucket's packing `cat` (same post-accumulate hook, same side "
-             "branch, immediately before the bucket's all-reduce) marks when the bucket left backward.",
+             "collectives themselves; each bucket's packing copy (a foreach copy into the bucket's slice: one or "
+             "more multi-tensor launches, issued by the same post-accumulate hook right before the bucket's "
+             "all-reduce) marks when the bucket left backward.",
              f"Last complete step: {hi - lo} kernels, {(t1 - t0) / 1e3:.1f} us; backward's last kernel "
              f"ends {(bwd_end - t0) / 1e3:.1f} us into the step; {nb} buckets expected.", "",
              "| packing kernel | start (us into step) | duration (us) | step kernels started after it |",
              "|---|---|---|---|"]
     for i in cats:
         st, en, name = rows[i]
-        short = re.search(r"CatArrayBatchedCopy\w*", name).group(0)
+        short = re.search(r"CatArrayBatchedCopy\w*|multi_tensor_apply_kernel", name).group(0)
         lines.append(f"| `{short}` | {(st - t0) / 1e3:.1f} | {(en - st) / 1e3:.1f} | {hi - i - 1} |")
     txt = "\n".join(lines)
     print(txt)
