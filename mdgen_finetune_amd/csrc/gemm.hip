@@ -596,6 +596,15 @@ __device__ __forceinline__ void epi_tile8(const mdg_gemm_desc& p, const float* _
     *reinterpret_cast<bf16x8*>(dst) = o;
   };
   if constexpr (EPI == MDG_EPI_STORE) {
+    // DGELU: every row's pre-activation piece is loaded up front (one HBM round trip per band
+    // instead of one per U-row batch)
+    bf16x8 ax[RPT];
+    if (p.act == MDG_ACT_DGELU) {
+#pragma unroll
+      for (int i = 0; i < RPT; ++i)
+        ax[i] = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const bf16_t*>(p.aux) +
+                                                 (size_t)min(m0 + r0 + RS * i, M - 1) * p.ldaux + n);
+    }
 #pragma unroll
     for (int u0 = 0; u0 < RPT; u0 += U) {
       float v[U][8];
@@ -608,10 +617,8 @@ __device__ __forceinline__ void epi_tile8(const mdg_gemm_desc& p, const float* _
 #pragma unroll
           for (int j = 0; j < 8; ++j) v[u][j] = gelu_fast(v[u][j]);
         } else if (p.act == MDG_ACT_DGELU) {
-          const bf16x8 a = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const bf16_t*>(p.aux) +
-                                                            (size_t)min(m, M - 1) * p.ldaux + n);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) v[u][j] *= gelu_grad_fast((float)a[j]);
+          for (int j = 0; j < 8; ++j) v[u][j] *= gelu_grad_fast((float)ax[u0 + u][j]);
         } else if (p.act == MDG_ACT_SILU) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) v[u][j] = silu(v[u][j]);
@@ -3280,8 +3287,9 @@ GemmPlan gemm_plan(const mdg_gemm_desc& p) {
     g.bn = p.N;
     return g;
   } else if (bf && p.N % kB4Tile == 0 && p.K % 64 == 0 && p.lda % 8 == 0 && p.ldw % 8 == 0) {
-    // MDG_GEMM_TILE=256 / 64 select the 256x128 3-stage kernel / the 128x128 K-step-64 kernel
-    // (tuning knob); default: 128x128 with K-step 32 at four blocks per CU
+    // MDG_GEMM_TILE=256 / 64 / 32 select the 256x128 3-stage kernel / the 128x128 K-step-64 /
+    // K-step-32 kernel (tuning knob); default: K-step 64, or K-step 32 at four blocks per CU when
+    // an aux operand rides along (the GELU pre-activation store / DGELU read)
     static const int forced = [] {
       const char* e = getenv("MDG_GEMM_TILE");
       return e ? atoi(e) : 0;
@@ -3290,8 +3298,11 @@ GemmPlan gemm_plan(const mdg_gemm_desc& p) {
       g.cfg = kCfgB8;  // 256x128, 3-stage glds ring
       g.smem = kB8Smem;
       g.bm = kB8M;
-    } else if (forced == 64) {
-      g.cfg = kCfgB4;  // 128x128, K-step 64, two blocks per CU
+    } else if (forced == 64 || (forced == 0 && !p.aux)) {
+      // 128x128, K-step 64, two blocks per CU: the default without an aux operand (the
+      // training step's input-gradient GEMMs: 45 vs 56 us at N 384, K 1536; the same K order,
+      // bit-identical to K-step 32); MDG_GEMM_TILE=32 keeps K-step 32 everywhere
+      g.cfg = kCfgB4;
       g.smem = b4_smem<64>();
       g.bm = kB4Tile;
     } else {
