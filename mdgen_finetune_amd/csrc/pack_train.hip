@@ -238,6 +238,7 @@ __global__ __launch_bounds__(256) void unpack_kernel(const mdg_train_unpack u) {
       const float* pp = u.part[w + 1];
       float s = 0.f;
       for (int b = 0; b < B; ++b)
+#pragma unroll 4
         for (int q = g; q < nb; q += 8) s += pp[(((size_t)b * nb + q) * 4 + 3) * C + k];
       s += __shfl_xor(s, 1, 64);
       s += __shfl_xor(s, 2, 64);

@@ -386,6 +386,7 @@ __global__ __launch_bounds__(256) void split_sum_wb_kernel(const float* __restri
     const size_t zs = (size_t)M * K;
     const float* p = part + (size_t)m * K + k;
     float4 s = *reinterpret_cast<const float4*>(p);
+#pragma unroll 8  // (the loads of 8 splits in flight; the adds keep z order)
     for (int z = 1; z < S; ++z) {
       const float4 v = *reinterpret_cast<const float4*>(p + z * zs);
       s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
@@ -394,6 +395,7 @@ __global__ __launch_bounds__(256) void split_sum_wb_kernel(const float* __restri
   } else if (db && e - nq < M) {
     const int m = (int)(e - nq);
     float s = cpart[m];
+#pragma unroll 8
     for (int z = 1; z < S; ++z) s += cpart[(size_t)z * M + m];
     db[m] = s;
   }
@@ -408,6 +410,7 @@ __global__ __launch_bounds__(256) void split_sum_kernel(const float* __restrict_
   const size_t zs = (size_t)M * ldp;
   const float* p = part + (size_t)m * ldp + k;
   float s = p[0];
+#pragma unroll 8
   for (int z = 1; z < S; ++z) s += p[z * zs];
   out[(size_t)m * ldo + k] = s;
 }
