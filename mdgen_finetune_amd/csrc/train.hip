@@ -390,6 +390,57 @@ __global__ __launch_bounds__(256) void attn_bwd_prep_kernel(int B, int T, int L,
   delta[((size_t)seq * H + head) * T + t] = dl;
 }
 
+// Tiled form of attn_bwd_prep_kernel for bf16, D % 8 == 0 and 256 % H == 0: block = one sequence
+// (b, l) x TT = 256 / H consecutive frames x every head; thread (frame tl, head) computes delta
+// exactly as above (the same loads, the same summation order: bit-identical), but its dO row goes
+// through LDS so the plane writes leave as contiguous TT x 64-B runs per head (the one-thread-per-
+// row form scattered every 16-B store over H planes: 64 write transactions per wave instruction).
+__global__ __launch_bounds__(256) void attn_bwd_prep_tiled_kernel(int B, int T, int L, int H, int D,
+                                                                  const bf16_t* __restrict__ o,
+                                                                  const bf16_t* __restrict__ o_lo,
+                                                                  const bf16_t* __restrict__ dout,
+                                                                  bf16_t* __restrict__ dop, float* __restrict__ delta) {
+  __shared__ __attribute__((aligned(16))) bf16_t tile[256 * kDP];  // [head][tl][kDP]
+  const int TT = 256 / H, seq = blockIdx.y, b = seq / L, l = seq - b * L;
+  const int t0 = blockIdx.x * TT, head = threadIdx.x % H, tl = threadIdx.x / H, t = t0 + tl;
+  const int C = H * D;
+  if (t < T) {
+    const size_t n = ((size_t)b * T + t) * L + l;
+    const bf16_t* orow = o + n * C + head * D;
+    const bf16_t* drow = dout + n * C + head * D;
+    bf16_t* trow = tile + ((size_t)head * TT + tl) * kDP;
+    float dl = 0.f;
+#pragma unroll
+    for (int d0 = 0; d0 < kDP; d0 += 8) {
+      bf16x8 dv = zero8<bf16_t>();
+      if (d0 < D) {
+        const bf16x8 ov = ld8<bf16_t>(orow + d0);
+        dv = ld8<bf16_t>(drow + d0);
+#pragma unroll
+        for (int j = 0; j < 8; j += 4)
+          dl += (float)dv[j] * (float)ov[j] + (float)dv[j + 1] * (float)ov[j + 1] + (float)dv[j + 2] * (float)ov[j + 2] +
+                (float)dv[j + 3] * (float)ov[j + 3];
+        if (o_lo) {
+          const bf16x8 lv = ld8<bf16_t>(o_lo + n * C + head * D + d0);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) dl += (float)dv[j] * (float)lv[j];
+        }
+      }
+      *reinterpret_cast<bf16x8*>(trow + d0) = dv;
+    }
+    delta[((size_t)seq * H + head) * T + t] = dl;
+  }
+  __syncthreads();
+  // head h's rows t0 .. t0 + nt - 1 are one contiguous run of nt x kDP elements in its plane
+  const int nt = min(TT, T - t0), pieces = nt * (kDP / 8);
+  for (int e = threadIdx.x; e < H * (TT * kDP / 8); e += 256) {
+    const int h = e / (TT * kDP / 8), q = e - h * (TT * kDP / 8);
+    if (q < pieces)
+      *reinterpret_cast<bf16x8*>(dop + (((size_t)seq * H + h) * T + t0) * kDP + 8 * q) =
+          *reinterpret_cast<const bf16x8*>(tile + (size_t)h * TT * kDP + 8 * q);
+  }
+}
+
 // Scalar reference / fp32 path: dq pass (one thread per (seq, head, query)) including the bias
 // key and its parameter gradients (block partials over the block's 256 queries).
 template <typename CT>
@@ -1158,7 +1209,11 @@ hipError_t attn_temporal_bwd_launch(int dtype, int B, int T, int L, int H, int D
   const int BL = B * L;
   const size_t nth = (size_t)B * T * L * H;
   dim3 pgrid((unsigned)((nth + 255) / 256));
-  if (dtype == MDG_BF16) {
+  if (dtype == MDG_BF16 && D % 8 == 0 && H <= 256 && 256 % H == 0) {
+    const int TT = 256 / H;
+    hipLaunchKernelGGL(attn_bwd_prep_tiled_kernel, dim3((T + TT - 1) / TT, BL), dim3(256), 0, s, B, T, L, H, D,
+                       (const bf16_t*)o, (const bf16_t*)o_lo, (const bf16_t*)dout, (bf16_t*)dop, delta);
+  } else if (dtype == MDG_BF16) {
     hipLaunchKernelGGL(attn_bwd_prep_kernel<bf16_t>, pgrid, dim3(256), 0, s, B, T, L, H, D, (const bf16_t*)o,
                        (const bf16_t*)o_lo, (const bf16_t*)dout, (bf16_t*)dop, delta);
   } else {
