@@ -111,6 +111,7 @@ class LayerHelper:
         the device tables are rebuilt on demand."""
         st = dict(self.__dict__)
         st["lib"], st["_tables"], st["_planes"] = None, {}, {}
+        st["_kb"] = {}
         return st
 
     def __setstate__(self, st):
@@ -134,6 +135,32 @@ class LayerHelper:
             t = torch.cat([freqs.cos().reshape(-1), freqs.sin().reshape(-1)]).to(inv_freq.device)
             self._tables[key] = t
         return t
+
+    def mask_bias(self, mask, B, T, L, s):
+        """(kb_t [B*L][T], kb_s [B*T][L]): the key-padding biases of the block stack's mask
+        (mdg_mask_bias), computed once per mask and shared by every layer of the pass.  The
+        entry holds the mask itself, so an equal (address, version, shape, strides) key is the
+        same, unchanged data; inside a capture the first layer's launch is recorded and
+        recomputes them on every replay, which the later layers read."""
+        # (views share their base's version counter; the held reference keeps the storage, so
+        # the address cannot be reused by another tensor while the entry lives)
+        # (an entry made outside a stream capture is never used inside one and vice versa: a
+        # captured pass must record its own launch, which every replay then repeats)
+        key = (mask.data_ptr(), mask._version, tuple(mask.shape), tuple(mask.stride()), str(mask.device),
+               mask.is_cuda and torch.cuda.is_current_stream_capturing())
+        cache = self.__dict__.setdefault("_kb", {})
+        ent = cache.get(key)
+        if ent is not None:
+            return ent[1], ent[2]
+        dev = mask.device
+        kb_t = torch.empty(B * L, T, device=dev)
+        kb_s = torch.empty(B * T, L, device=dev)
+        _lib.check(self.lib.mdg_mask_bias(B, T, L, mask.data_ptr(), kb_t.data_ptr(), kb_s.data_ptr(), s),
+                   "mdg_mask_bias")
+        if len(cache) >= 2:  # the IPA layers' and the blocks' masks
+            cache.pop(next(iter(cache)))
+        cache[key] = (mask, kb_t, kb_s)
+        return kb_t, kb_s
 
     def planes(self, key, shape, device, owner):
         """(buffer, fresh): persistent padded q|k|v planes of one layer (key = (tag, layer id,
@@ -249,9 +276,7 @@ class _HipLayerFn(torch.autograd.Function):
         lw.w1, lw.b1, lw.w2, lw.b2 = P["w1"].data_ptr(), P["b1"].data_ptr(), P["w2"].data_ptr(), P["b2"].data_ptr()
         dims = hl.dims(B, T, L)
         long_l = L >= 16
-        kb_t = torch.empty(B * L, T, device=dev)
-        kb_s = torch.empty(B * T, L, device=dev)
-        _lib.check(lib.mdg_mask_bias(B, T, L, mask.data_ptr(), kb_t.data_ptr(), kb_s.data_ptr(), s), "mdg_mask_bias")
+        kb_t, kb_s = hl.mask_bias(mask, B, T, L, s)
         e = lambda *shape, dt=ct: torch.empty(*shape, device=dev, dtype=dt)  # noqa: E731
         r = lambda cols: _rows(N, cols, ct, dev)  # noqa: E731  (operands of the weight gradients)
         # the padded attention planes persist per layer and shape: their pad columns (0, and 1.0 in
