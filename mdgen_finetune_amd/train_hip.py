@@ -136,7 +136,7 @@ class LayerHelper:
             self._tables[key] = t
         return t
 
-    def mask_bias(self, mask, B, T, L, s):
+    def mask_bias(self, mask, B, T, L, s, src=None):
         """(kb_t [B*L][T], kb_s [B*T][L]): the key-padding biases of the block stack's mask
         (mdg_mask_bias), computed once per mask and shared by every layer of the pass.  The
         entry holds the mask itself, so an equal (address, version, shape, strides) key is the
@@ -155,7 +155,8 @@ class LayerHelper:
         dev = mask.device
         kb_t = torch.empty(B * L, T, device=dev)
         kb_s = torch.empty(B * T, L, device=dev)
-        _lib.check(self.lib.mdg_mask_bias(B, T, L, mask.data_ptr(), kb_t.data_ptr(), kb_s.data_ptr(), s),
+        src = mask if src is None else src  # (the contiguous fp32 form of the keyed mask)
+        _lib.check(self.lib.mdg_mask_bias(B, T, L, src.data_ptr(), kb_t.data_ptr(), kb_s.data_ptr(), s),
                    "mdg_mask_bias")
         if len(cache) >= 2:  # the IPA layers' and the blocks' masks
             cache.pop(next(iter(cache)))
@@ -238,6 +239,7 @@ class _HipLayerFn(torch.autograd.Function):
         s = _lib.stream_handle()
         h = h.contiguous().float()
         mods = mods.contiguous().float()
+        mask_key = mask  # the caller's tensor: the same object for every layer of a pass
         mask = mask.contiguous().float()
         # the layer's operands in the kernels' layouts (q / k rows pair-interleaved, CT casts, the
         # transposes the backward's input-gradient GEMMs read, RoPE-rotated bias key): one launch
@@ -276,7 +278,7 @@ class _HipLayerFn(torch.autograd.Function):
         lw.w1, lw.b1, lw.w2, lw.b2 = P["w1"].data_ptr(), P["b1"].data_ptr(), P["w2"].data_ptr(), P["b2"].data_ptr()
         dims = hl.dims(B, T, L)
         long_l = L >= 16
-        kb_t, kb_s = hl.mask_bias(mask, B, T, L, s)
+        kb_t, kb_s = hl.mask_bias(mask_key, B, T, L, s, src=mask)
         e = lambda *shape, dt=ct: torch.empty(*shape, device=dev, dtype=dt)  # noqa: E731
         r = lambda cols: _rows(N, cols, ct, dev)  # noqa: E731  (operands of the weight gradients)
         # the padded attention planes persist per layer and shape: their pad columns (0, and 1.0 in
