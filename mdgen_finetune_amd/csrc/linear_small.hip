@@ -66,6 +66,7 @@ __device__ __forceinline__ float dsilu_f(float x) {
 // x' rows [m0, m0 + mc) of the block -> LDS [mc][K] (SiLU applied), float4 per thread step
 __device__ __forceinline__ void sl_stage_x(float* xs, const float* x, int ldx, int m0, int mc, int K, int act) {
   const int k4 = K >> 2;
+  #pragma unroll 4  // (four global loads in flight before their LDS stores)
   for (int e = threadIdx.x; e < mc * k4; e += blockDim.x) {
     const int m = e / k4, c = (e - m * k4) * 4;
     float4 v = *reinterpret_cast<const float4*>(x + (size_t)(m0 + m) * ldx + c);
@@ -241,6 +242,7 @@ __global__ __launch_bounds__(256) void sl_bwd_kernel(const SlBwdArgs a) {
     for (int mb = 0; mb < a.M; mb += kSlMaxM) {  // token chunks, m ascending overall
       const int mc = min(kSlMaxM, a.M - mb);
       __syncthreads();
+      #pragma unroll 4  // (four global loads in flight before their LDS stores)
       for (int e = t; e < mc * 32; e += 256) {
         const int m = e >> 5, cc = cp * 32 + (e & 31);
         float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -250,6 +252,7 @@ __global__ __launch_bounds__(256) void sl_bwd_kernel(const SlBwdArgs a) {
         }
         xs[e] = v;
       }
+      #pragma unroll 4  // (four global loads in flight before their LDS stores)
       for (int e = t; e < mc * 64; e += 256) {
         const int m = e >> 6, cc = e & 63;
         const float* col = rdy_[cc];
@@ -294,6 +297,7 @@ __global__ __launch_bounds__(256) void sl_bwd_kernel(const SlBwdArgs a) {
   for (int mb = 0; mb < a.M; mb += MT) {
     const int mc = min(MT, a.M - mb);
     __syncthreads();
+    #pragma unroll 4  // (four global loads in flight before their LDS stores)
     for (int e = t; e < nc * mc; e += 256) {
       const int jj = e / mc, m = e - jj * mc;
       dys[jj * MT + m] = rdy_[jj][(size_t)(mb + m) * rld_[jj]];

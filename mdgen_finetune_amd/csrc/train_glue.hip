@@ -68,6 +68,7 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(int B, int T, int L, int
   const size_t n0 = ((size_t)b * T + t0) * L;
   const int tid = threadIdx.x, op = tid >> 7, c = blockIdx.y * 128 + (tid & 127);
   const int K = op ? K2 : K1;
+#pragma unroll 4  // (global loads in flight before their LDS stores)
   for (int i = tid; i < ntok * kEbK; i += 256) {
     const int r = i / kEbK, k = i % kEbK;
     xs0[r][k] = k < K1 ? x1[(n0 + r) * K1 + k] : 0.f;
@@ -362,7 +363,9 @@ __global__ __launch_bounds__(kFThreads) void final_bwd_kernel(int N, int rows_pe
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int b = blockIdx.x / pl.cpb, ch = blockIdx.x % pl.cpb;
   const int r0 = b * rows_per_b + ch * kFbRows, r1 = min(b * rows_per_b + rows_per_b, r0 + kFbRows);
+#pragma unroll 8
   for (int i = tid; i < LAT * kFC; i += kFThreads) ws_[i] = w[i];
+#pragma unroll 4
   for (int i = tid; i < (r1 - r0) * LAT; i += kFThreads) dvs[i] = dv[(size_t)r0 * LAT + i];
   __syncthreads();
   float sh[6], sc[6];
