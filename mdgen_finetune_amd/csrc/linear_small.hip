@@ -106,13 +106,19 @@ __global__ __launch_bounds__(256) void sl_fwd_kernel(const SlFwdArgs a) {
   const bool live = n < a.sm.total;
   const int s = live ? seg_of(a.sm, n) : 0, nr = live ? n - pk(a.sm.start, s) : 0;
   const float* wr = pk(a.w, s) + (size_t)nr * a.K;
+  // the first weight piece is requested before the x' staging barrier, and each next one while
+  // the current one is used (one exposed load latency per row instead of one per k step)
+  const int kstep = 16 * KS, k0 = 4 * kq + (KS == 1 ? 0 : 16 * wave);
+  float4 wn = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (live && k0 < a.K) wn = *reinterpret_cast<const float4*>(wr + k0);
   __syncthreads();
   float acc[MT];
 #pragma unroll
   for (int m = 0; m < MT; ++m) acc[m] = 0.f;
   if (live) {
-    for (int k = 4 * kq + (KS == 1 ? 0 : 16 * wave); k < a.K; k += 16 * KS) {
-      const float4 w4 = *reinterpret_cast<const float4*>(wr + k);
+    for (int k = k0; k < a.K; k += kstep) {
+      const float4 w4 = wn;
+      if (k + kstep < a.K) wn = *reinterpret_cast<const float4*>(wr + k + kstep);
 #pragma unroll
       for (int m = 0; m < MT; ++m) {
         if (m < mc) {
