@@ -13,9 +13,9 @@
 //    mask_to_emb row sums.  The chunk's x rows are staged in LDS (broadcast reads), dh is read
 //    once, coalesced.  Per-chunk partials, then one launch sums them in chunk order
 //    (deterministic).  HBM: one pass over dh (49 MB at B=8, T=1000, L=4).
-//  * final_fwd: 32 rows per block: LN statistics as two wave reductions (6 columns per lane)
-//    and the modulate into LDS, then one thread per (row, output group of 3) for the 21 output
-//    dots; writes v and (mean, rstd).
+//  * final_fwd: 64 rows per block, W in LDS: LN statistics as two wave reductions (6 columns
+//    per lane) and the modulate into LDS, then one thread per (row, output group) for the 21
+//    output dots (W reads are LDS broadcasts); writes v and (mean, rstd).
 //  * final_bwd: one wave per row, rows of one trajectory per block: dxn = dv W, the LN +
 //    modulate backward into dh, and per-wave register accumulators of dW (6 columns x 21
 //    outputs per lane), dbias, d shift, d scale; block partials summed in order by a reduce
@@ -263,56 +263,66 @@ __device__ __forceinline__ void ln_row(const float (&x)[6], float& mean, float& 
   rstd = rsqrtf(wave_sum(v) * (1.0f / kFC) + 1e-6f);
 }
 
-// 32 rows per block.  Phase 1: wave w LN-modulates rows w, w + 4, ... (their h rows loaded
-// together) into LDS.  Phase 2: thread = (row r, output group g) dots row r with W rows g, g + 8,
-// ... (W read as float4 through the caches, the row from LDS: lanes 32-63 share lanes 0-31's rows).
-constexpr int kFfRows = 32, kFfPad = kFC + 4;
+// 64 rows per block, W [LAT][C] staged in LDS once per block.  Phase 1: wave w LN-modulates
+// rows w, w + 4, ... (eight h rows loaded together per pass) into LDS.  Phase 2: thread = (row r,
+// output group g = wave) dots row r with W rows g, g + 4, ...: the W reads are wave-uniform LDS
+// broadcasts (W read per thread from L2 cost 87 us a step at 32 rows per block).
+constexpr int kFfRows = 64, kFfPad = kFC + 4;
+template <int LAT>
+constexpr size_t ff_smem() { return ((size_t)kFfRows * kFfPad + (size_t)LAT * kFC) * sizeof(float); }
 template <int LAT>
 __global__ __launch_bounds__(kFThreads) void final_fwd_kernel(int N, int rows_per_b, const float* __restrict__ h,
                                                               const float* __restrict__ mods,
                                                               const float* __restrict__ w,
                                                               const float* __restrict__ bias, float* __restrict__ v,
                                                               float* __restrict__ stats) {
-  __shared__ __attribute__((aligned(16))) float xs[kFfRows * kFfPad];
-  constexpr int RW = kFfRows / 4;  // rows per wave
+  extern __shared__ __attribute__((aligned(16))) float ff_[];
+  float* xs = ff_;                      // [kFfRows][kFfPad]
+  float* wsm = ff_ + kFfRows * kFfPad;  // [LAT][kFC]
+  constexpr int RW = 8;                 // rows per wave per pass
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r0 = blockIdx.x * kFfRows;
-  float x[RW][6];
+#pragma unroll 4
+  for (int i = tid; i < LAT * kFC / 4; i += kFThreads)
+    reinterpret_cast<float4*>(wsm)[i] = reinterpret_cast<const float4*>(w)[i];
+  for (int pass = 0; pass < kFfRows / (4 * RW); ++pass) {
+    float x[RW][6];
 #pragma unroll
-  for (int i = 0; i < RW; ++i) {
-    const int n = r0 + wave + 4 * i;
-    if (n < N) row_ld(h + (size_t)n * kFC, lane, x[i]);
-  }
+    for (int i = 0; i < RW; ++i) {
+      const int n = r0 + pass * 4 * RW + wave + 4 * i;
+      if (n < N) row_ld(h + (size_t)n * kFC, lane, x[i]);
+    }
 #pragma unroll
-  for (int i = 0; i < RW; ++i) {
-    const int rr = wave + 4 * i, n = r0 + rr;
-    if (n >= N) break;
-    const float* mrow = mods + (size_t)(n / rows_per_b) * 2 * kFC;
-    float sh[6], sc[6];
-    row_ld(mrow, lane, sh);
-    row_ld(mrow + kFC, lane, sc);
-    float mean, rstd;
-    ln_row(x[i], mean, rstd);
-    float xn[6];
+    for (int i = 0; i < RW; ++i) {
+      const int rr = pass * 4 * RW + wave + 4 * i, n = r0 + rr;
+      if (n >= N) break;
+      const float* mrow = mods + (size_t)(n / rows_per_b) * 2 * kFC;
+      float sh[6], sc[6];
+      row_ld(mrow, lane, sh);
+      row_ld(mrow + kFC, lane, sc);
+      float mean, rstd;
+      ln_row(x[i], mean, rstd);
+      float xn[6];
 #pragma unroll
-    for (int e = 0; e < 6; ++e) xn[e] = (x[i][e] - mean) * rstd * (1.0f + sc[e]) + sh[e];
-    row_st(xs + rr * kFfPad, lane, xn);
-    if (lane == 0) *reinterpret_cast<float2*>(stats + 2 * (size_t)n) = make_float2(mean, rstd);
+      for (int e = 0; e < 6; ++e) xn[e] = (x[i][e] - mean) * rstd * (1.0f + sc[e]) + sh[e];
+      row_st(xs + rr * kFfPad, lane, xn);
+      if (lane == 0) *reinterpret_cast<float2*>(stats + 2 * (size_t)n) = make_float2(mean, rstd);
+    }
   }
   __syncthreads();
-  constexpr int NJ = (LAT + 7) / 8;
-  const int r = tid & 31, g = tid >> 5, n = r0 + r;
+  constexpr int NJ = (LAT + 3) / 4;
+  const int r = tid & 63, g = wave, n = r0 + r;
   float acc[NJ];
 #pragma unroll
   for (int jj = 0; jj < NJ; ++jj) acc[jj] = 0.f;
   const float4* xr = reinterpret_cast<const float4*>(xs + r * kFfPad);
-  const float4* wr = reinterpret_cast<const float4*>(w);
+  const float4* wr = reinterpret_cast<const float4*>(wsm);
 #pragma unroll 4
   for (int k4 = 0; k4 < kFC / 4; ++k4) {
     const float4 xv = xr[k4];
 #pragma unroll
     for (int jj = 0; jj < NJ; ++jj) {
-      const int j = g + 8 * jj;
+      const int j = g + 4 * jj;
       if (j < LAT) {
         const float4 wv = wr[j * (kFC / 4) + k4];
         acc[jj] = fmaf(xv.x, wv.x, acc[jj]);
@@ -325,7 +335,7 @@ __global__ __launch_bounds__(kFThreads) void final_fwd_kernel(int N, int rows_pe
   if (n < N) {
 #pragma unroll
     for (int jj = 0; jj < NJ; ++jj) {
-      const int j = g + 8 * jj;
+      const int j = g + 4 * jj;
       if (j < LAT) v[(size_t)n * LAT + j] = acc[jj] + (bias ? bias[j] : 0.f);
     }
   }
@@ -625,10 +635,22 @@ hipError_t embed_bwd_launch(int B, int T, int L, int C, int K1, const float* x1,
 hipError_t final_fwd_train_launch(int N, int rows_per_b, int lat, const float* h, const float* mods, const float* w,
                                   const float* bias, float* v, float* stats, hipStream_t s) {
   const int grid = (N + kFfRows - 1) / kFfRows;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&final_fwd_kernel<21>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)ff_smem<21>());
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute(reinterpret_cast<const void*>(&final_fwd_kernel<28>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)ff_smem<28>());
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
   if (lat == 21)
-    hipLaunchKernelGGL(final_fwd_kernel<21>, dim3(grid), dim3(kFThreads), 0, s, N, rows_per_b, h, mods, w, bias, v, stats);
+    hipLaunchKernelGGL(final_fwd_kernel<21>, dim3(grid), dim3(kFThreads), ff_smem<21>(), s, N, rows_per_b, h, mods, w,
+                       bias, v, stats);
   else if (lat == 28)
-    hipLaunchKernelGGL(final_fwd_kernel<28>, dim3(grid), dim3(kFThreads), 0, s, N, rows_per_b, h, mods, w, bias, v, stats);
+    hipLaunchKernelGGL(final_fwd_kernel<28>, dim3(grid), dim3(kFThreads), ff_smem<28>(), s, N, rows_per_b, h, mods, w,
+                       bias, v, stats);
   else
     return hipErrorInvalidValue;
   return hipGetLastError();
