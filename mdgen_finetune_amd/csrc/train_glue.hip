@@ -285,6 +285,12 @@ __global__ __launch_bounds__(kFThreads) void final_fwd_kernel(int N, int rows_pe
 #pragma unroll 4
   for (int i = tid; i < LAT * kFC / 4; i += kFThreads)
     reinterpret_cast<float4*>(wsm)[i] = reinterpret_cast<const float4*>(w)[i];
+  // the modulation rows of the block's first trajectory, reloaded only where the rows cross into
+  // the next one (rows_per_b = T L >> 64: at most once per block)
+  int cur_b = min(r0, N - 1) / rows_per_b;
+  float sh[6], sc[6];
+  row_ld(mods + (size_t)cur_b * 2 * kFC, lane, sh);
+  row_ld(mods + (size_t)cur_b * 2 * kFC + kFC, lane, sc);
   for (int pass = 0; pass < kFfRows / (4 * RW); ++pass) {
     float x[RW][6];
 #pragma unroll
@@ -296,10 +302,12 @@ __global__ __launch_bounds__(kFThreads) void final_fwd_kernel(int N, int rows_pe
     for (int i = 0; i < RW; ++i) {
       const int rr = pass * 4 * RW + wave + 4 * i, n = r0 + rr;
       if (n >= N) break;
-      const float* mrow = mods + (size_t)(n / rows_per_b) * 2 * kFC;
-      float sh[6], sc[6];
-      row_ld(mrow, lane, sh);
-      row_ld(mrow + kFC, lane, sc);
+      const int bb = n / rows_per_b;
+      if (bb != cur_b) {  // (wave-uniform)
+        cur_b = bb;
+        row_ld(mods + (size_t)bb * 2 * kFC, lane, sh);
+        row_ld(mods + (size_t)bb * 2 * kFC + kFC, lane, sc);
+      }
       float mean, rstd;
       ln_row(x[i], mean, rstd);
       float xn[6];
