@@ -130,13 +130,17 @@ def time_kernel(fn, iters=20):
 
 
 def _traffic(kernel, B, T, L, dtype):
-    """HBM bytes per launch from the committed PMC pass (profiles/traffic_r03.json, FETCH_SIZE x2
-    + WRITE_SIZE per the gfx950 correction of MI355X_MICROARCH.md §HBM), or None."""
-    prof = os.path.join(REPO, "profiles", "traffic_r03.json")  # this round's PMC passes
-    try:
-        return json.load(open(prof))[kernel].get(f"B{B}_T{T}_L{L}_{dtype}")
-    except Exception:
-        return None
+    """HBM bytes per launch from the committed PMC passes (profiles/traffic_r04.json, this round's
+    tools/roof_pmc.sh; shapes it lacks, e.g. ATLAS, from traffic_r03.json of the same kernels):
+    FETCH_SIZE x2 + WRITE_SIZE per the gfx950 correction of MI355X_MICROARCH.md §HBM, or None."""
+    for rr in ("04", "03"):
+        try:
+            v = json.load(open(os.path.join(REPO, "profiles", f"traffic_r{rr}.json")))[kernel].get(f"B{B}_T{T}_L{L}_{dtype}")
+        except Exception:
+            v = None
+        if v is not None:
+            return v
+    return None
 
 
 def roofline(eng, st, dtype, B, T, L):
