@@ -37,6 +37,7 @@ import time
 import torch
 
 REPO = os.path.dirname(os.path.abspath(__file__))
+ROUND = "05"  # the round whose profiles/ files (summary, PMC traffic) this bench line cites
 sys.path.insert(0, REPO)
 
 PEAK_TFLOPS = {"bf16": 2500.0, "f32": 157.3}   # MI355X dense MFMA (MI355X_MICROARCH.md:42-43)
@@ -130,10 +131,10 @@ def time_kernel(fn, iters=20):
 
 
 def _traffic(kernel, B, T, L, dtype):
-    """HBM bytes per launch from the committed PMC passes (profiles/traffic_r04.json, this round's
-    tools/roof_pmc.sh; shapes it lacks, e.g. ATLAS, from traffic_r03.json of the same kernels):
-    FETCH_SIZE x2 + WRITE_SIZE per the gfx950 correction of MI355X_MICROARCH.md §HBM, or None."""
-    for rr in ("04", "03"):
+    """HBM bytes per launch from the committed PMC passes (profiles/traffic_r{ROUND}.json, this
+    round's tools/roof_pmc.sh; shapes or kernels it lacks from the earlier rounds' files of the same
+    kernels): FETCH_SIZE x2 + WRITE_SIZE per the gfx950 correction of MI355X_MICROARCH.md §HBM, or None."""
+    for rr in (ROUND, "04", "03"):
         try:
             v = json.load(open(os.path.join(REPO, "profiles", f"traffic_r{rr}.json")))[kernel].get(f"B{B}_T{T}_L{L}_{dtype}")
         except Exception:
@@ -265,7 +266,7 @@ def roofline(eng, st, dtype, B, T, L):
                      "hbm_frac": round(hbm_ach / PEAK_HBM_GBS, 4), "shape": f"B={B} T={T} L={L}",
                      "timing": "standalone: 50 back-to-back launches outside the graph, one lane's shape, the "
                                "step's workspace activations and layer-0 weights, zero adaLN rows; in the graph two "
-                               "lanes share the chip and each launch takes longer (profiles/r02_summary.md)"}
+                               f"lanes share the chip and each launch takes longer (in-graph averages: profiles/r{ROUND}_summary.md)"}
     return out
 
 

@@ -523,13 +523,26 @@ class HipEngine:
         self._copy_opt(vs, "rel7", self._rel7)
         vs.graph = None
         vs.ios = []
-        # hoisted, t-independent: base embedding and key-padding biases (per lane workspace)
-        s = _lib.stream_handle()
-        self._base(st, x_cond, x_cond_mask)
-        for k, ls in enumerate(lanes):
-            mk = vs.mask[k * Bl:(k + 1) * Bl]
-            _lib.check(self.lib.mdg_prepare_mask(ctypes.byref(ls.dims), mk.data_ptr(), ls.ws.data_ptr(), s),
-                       "mdg_prepare_mask")
+        # hoisted, t-independent: base embedding and key-padding biases, in the shape's shared
+        # velocity-field workspace.  A later field of the same shape overwrites them, so the
+        # workspace records its owner and ensure() re-hoists this field's before it runs again
+        # (the older field used to read the newer field's conditioning).
+        vs.x_cond = None if x_cond is None else x_cond.float().clone()
+        vs.x_cond_mask = None if x_cond_mask is None else x_cond_mask.clone()
+        vs.token = object()
+
+        def ensure():
+            if getattr(st, "vf_owner", None) is vs.token:
+                return
+            s = _lib.stream_handle()
+            self._base(st, vs.x_cond, vs.x_cond_mask)
+            for k, ls in enumerate(lanes):
+                mk = vs.mask[k * Bl:(k + 1) * Bl]
+                _lib.check(self.lib.mdg_prepare_mask(ctypes.byref(ls.dims), mk.data_ptr(), ls.ws.data_ptr(), s),
+                           "mdg_prepare_mask")
+            st.vf_owner = vs.token
+
+        ensure()
         rows = Bl * T * L
         # conditioning states for one evaluation and for the 6 stage times of a graphed dopri5
         # step, built here: their RoPE / bias-kv tables are host work that a capture cannot record
@@ -578,6 +591,7 @@ class HipEngine:
             stage(0, vs.x)
 
         def f(t, y):
+            ensure()
             vs.x.copy_(y)
             vs.t.copy_(torch.as_tensor(t, device=dev).float().reshape(1))
             if vs.graph is not None:
@@ -601,6 +615,8 @@ class HipEngine:
 
         f_capturable.precondition = precondition
         f_capturable.stage = stage
+        f_capturable.ensure = ensure  # eager: call before each replay of a graph that captured it
+        f.ensure = ensure
         f.state = vs
         f.capturable = f_capturable
         f.lanes = nl

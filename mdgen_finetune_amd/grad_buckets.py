@@ -17,6 +17,14 @@ step's host-launch bound, so this class does DDP's job inside the capture:
 * ``finish()`` joins the side stream (graph-capture legal: event record / wait) and points
   every ``p.grad`` at its slice, so clip / Adam / EMA read the averaged values in place.
 
+Rank agreement (DDP's rules, which this class must keep because the collectives are matched by
+sequence): every rank builds its layout from RANK 0's recorded order (broadcast at construction)
+and checks by an all-gather that all ranks hold the same parameter set, bucket sizes and the same
+set of gradients reached by backward; and buckets are reduced strictly in layout order — a bucket
+that completes early waits for its predecessors — so the collectives' sequence is the same on
+every rank whatever order the local hooks fire in.  A hook that fires twice in one backward
+(a reentrant re-run) is an error, not a silent early launch.
+
 Inside a capture the collectives become graph nodes on the side stream's branch, interleaved
 with the backward kernels (the replay keeps the overlap).  On CPU (gloo) the same object runs
 eagerly with ``async_op`` all-reduces, which is how the world-2 CPU tests exercise it.
@@ -41,13 +49,47 @@ def record_grad_order(params):
     return order, remove
 
 
+def agree_order(params, order, world, group=None):
+    """Rank 0's completion order, broadcast to every rank, after checking that all ranks hold the
+    same parameter shapes and reached the same set of gradients (raises RuntimeError otherwise).
+    On world 1 (or without an initialised group) the local order is returned unchanged."""
+    seen = list(dict.fromkeys(order))
+    if world <= 1 or not dist.is_initialized():
+        return seen
+    dev = params[0].device if dist.get_backend(group) == "nccl" else torch.device("cpu")
+    n = len(params)
+    # per-rank signature: parameter count, total elements, a shape checksum, the reached set
+    reached = torch.zeros(n, dtype=torch.int64)
+    reached[seen] = 1
+    numels = torch.tensor([p.numel() for p in params], dtype=torch.int64)
+    sig = torch.cat([torch.tensor([n, int(numels.sum()), int((numels * torch.arange(1, n + 1)).sum())]), reached])
+    sig = sig.to(dev)
+    allsig = [torch.empty_like(sig) for _ in range(world)]
+    dist.all_gather(allsig, sig, group=group)
+    for r, other in enumerate(allsig):
+        if not torch.equal(other, sig):
+            o = other.cpu()
+            if not torch.equal(o[:3], sig.cpu()[:3]):
+                raise RuntimeError(f"gradient buckets: rank {r} holds different parameters (count / sizes "
+                                   f"{o[:3].tolist()} vs {sig.cpu()[:3].tolist()})")
+            diff = (o[3:] != sig.cpu()[3:]).nonzero().flatten().tolist()
+            raise RuntimeError(f"gradient buckets: rank {r} reached a different set of gradients in backward "
+                               f"(parameters {diff[:8]}{'...' if len(diff) > 8 else ''} differ)")
+    buf = torch.full((n,), -1, dtype=torch.int64)
+    buf[:len(seen)] = torch.tensor(seen, dtype=torch.int64)
+    buf = buf.to(dev)
+    dist.broadcast(buf, 0, group=group)
+    return [int(i) for i in buf.cpu().tolist() if i >= 0]
+
+
 class BucketedAllReduce:
     def __init__(self, params, order, cap_bytes, world, group=None):
         self.params = list(params)
         self.world, self.group = world, group
         dev = self.params[0].device
-        # parameters that backward never reached keep grad None (the optimizer skips them)
-        seen = list(dict.fromkeys(order))
+        # parameters that backward never reached keep grad None (the optimizer skips them).
+        # Layout from rank 0's order on every rank (DDP syncs its rebuilt buckets the same way)
+        seen = agree_order(self.params, order, world, group)
         self.buckets, cur, size = [], [], 0
         for i in seen:
             nb = self.params[i].numel() * 4
@@ -83,6 +125,7 @@ class BucketedAllReduce:
         self.detach()
         self._pending = [len(b) for b in self.buckets]
         self._works, self._fired = [], 0
+        self._done, self._next = set(), 0  # fired parameter indices; next bucket to reduce
         self.launch_log = []
         for bi, b in enumerate(self.buckets):
             for i in b:
@@ -95,11 +138,18 @@ class BucketedAllReduce:
         self._handles = []
 
     def _ready(self, i):
+        if i in self._done:
+            raise RuntimeError(f"gradient buckets: parameter {i}'s gradient hook fired twice in one backward "
+                               "(a reentrant re-run would reduce the bucket before its final gradients)")
+        if i not in self.bucket_of:
+            raise RuntimeError(f"gradient buckets: parameter {i} produced a gradient that warm-up never saw")
+        self._done.add(i)
         self._fired += 1
-        bi = self.bucket_of[i]
-        self._pending[bi] -= 1
-        if self._pending[bi] == 0:
-            self._launch(bi)
+        self._pending[self.bucket_of[i]] -= 1
+        # reduce in layout order: the collectives' sequence must be the same on every rank
+        while self._next < len(self.buckets) and self._pending[self._next] == 0:
+            self._launch(self._next)
+            self._next += 1
 
     def _launch(self, bi):
         self.launch_log.append((bi, self._fired))

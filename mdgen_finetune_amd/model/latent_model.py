@@ -21,6 +21,8 @@ identical at T == 1).
 """
 from __future__ import annotations
 
+import warnings
+
 import numpy as np
 import torch
 import torch.nn.functional as F
@@ -377,9 +379,19 @@ class LatentMDGenModel(nn.Module):
             return False
         if not torch.is_grad_enabled():
             return False
+        why = None
         if self.args.embed_dim // self.args.mha_heads >= 32:  # the training kernels take head_dim < 32
+            why = f"head_dim {self.args.embed_dim // self.args.mha_heads} >= 32"
+        elif self.training and float(getattr(self.args, "dropout", 0.0) or 0.0) > 0.0:
+            why = f"--dropout {self.args.dropout} (attention-probability dropout, mha.py:383)"
+        if why is not None:
+            if getattr(self, "_hip_refusal", None) != why:  # logged once per reason, never silent
+                self._hip_refusal = why
+                warnings.warn(f"LatentMDGenModel: the HIP training kernels do not take {why}; the block "
+                              "stack runs eager PyTorch autograd on the device (slower, same arithmetic)",
+                              RuntimeWarning, stacklevel=3)
             return False
-        return not (self.training and float(getattr(self.args, "dropout", 0.0) or 0.0) > 0.0)
+        return True
 
     def _train_helper(self):
         from ..train_hip import LayerHelper

@@ -116,9 +116,10 @@ class FusedClipAdam:
         _lib.check(lib.mdg_adam_step(n, nc, table.data_ptr(), float(g["lr"]), float(b1), float(b2), float(g["eps"]),
                                      float(g["weight_decay"]), int(decoupled), self.max_norm, gnorm.data_ptr(),
                                      ws.data_ptr(), wsb, _lib.stream_handle()), "mdg_adam_step")
-        if capturing:
+        if capturing:  # a graph replays these buffers: keep them for the optimizer's lifetime
             self._pending.append((table, host_t))
-        self._keep.append((table, ws, gnorm, host_t))
+            self._keep.append((table, ws, gnorm, host_t))
+        # eager: the caching allocator recycles table / ws only after this stream's launch
         return gnorm
 
     def finish_capture(self):

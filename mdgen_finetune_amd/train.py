@@ -34,7 +34,7 @@ import torch.distributed as dist
 from torch.nn.parallel import DistributedDataParallel as DDP
 
 from .checkpoint import load_checkpoint, model_state_dict, save_checkpoint
-from .data import SyntheticMDDataset, collate
+from .data import MDGenDataset, SyntheticMDDataset, collate
 from .grad_buckets import BucketedAllReduce, record_grad_order
 from .parsing import parse_train_args
 from .wrapper import NewMDGenWrapper
@@ -109,16 +109,32 @@ class Trainer:
                              bucket_cap_mb=args.bucket_cap_mb, gradient_as_bucket_view=True, static_graph=True)
         self.optimizer = self.wrapper.configure_optimizers(capturable=self.graph_mode)
         self.epoch, self.global_step, self.skip_batches = 0, 0, 0
+        self.valset = None
         if dataset is None:
-            if not args.synthetic:
-                raise NotImplementedError("only --synthetic data is available offline (the reference's "
-                                          "MDGenDataset needs the gs://mdgen-public trajectories)")
-            dataset = SyntheticMDDataset(args.num_frames, args.crop, size=args.synthetic_size, seed=args.seed)
+            if args.synthetic:
+                dataset = SyntheticMDDataset(args.num_frames, args.crop, size=args.synthetic_size, seed=args.seed)
+            else:  # train.py:25-30: the reference's .npy trajectories (window draws per rank)
+                dataset = MDGenDataset(args, split=args.train_split,
+                                       rng=np.random.default_rng([args.seed, rank]))
+                if not args.no_validate:
+                    self.valset = dataset if args.overfit else MDGenDataset(
+                        args, split=args.val_split, repeat=args.val_repeat,
+                        rng=np.random.default_rng([args.seed, rank, 1]))
         self.dataset = dataset
         self.sampler = torch.utils.data.DistributedSampler(dataset, num_replicas=world, rank=rank, shuffle=True,
                                                            seed=args.seed, drop_last=True)
+        # item loading is host work (memmap reads, geometry): worker processes overlap it with the
+        # step (train.py:32-43); a worker's window draws continue the rank's generator
+        nw = 0 if args.synthetic else int(getattr(args, "num_workers", 0) or 0)
         self.loader = torch.utils.data.DataLoader(dataset, batch_size=args.batch_size, sampler=self.sampler,
-                                                  num_workers=0, collate_fn=collate, drop_last=True)
+                                                  num_workers=nw, collate_fn=collate, drop_last=True,
+                                                  worker_init_fn=_worker_init if nw else None,
+                                                  persistent_workers=bool(nw))
+        self.val_loader = None
+        if self.valset is not None:
+            vs = torch.utils.data.DistributedSampler(self.valset, num_replicas=world, rank=rank, shuffle=False)
+            self.val_loader = torch.utils.data.DataLoader(self.valset, batch_size=args.batch_size, sampler=vs,
+                                                          num_workers=0, collate_fn=collate)
         if args.ckpt:
             self.resume(args.ckpt)
 
@@ -243,6 +259,25 @@ class Trainer:
                 del w._log[k]
         return mean
 
+    @torch.no_grad()
+    def validate(self):
+        """wrapper.py:88-109: the GVP loss on the validation split (EMA weights when --ema), logged
+        under ``val_`` and gathered over ranks at the end."""
+        a, w = self.args, self.wrapper
+        if w.ema is not None:
+            w.load_ema_weights()
+        w.eval()
+        try:
+            for bi, batch in enumerate(self.val_loader):
+                if a.val_batches is not None and bi >= a.val_batches:
+                    break
+                w.general_step(self._to_device(batch), "val", model=w.model)
+        finally:
+            if w.ema is not None:
+                w.restore_cached_weights()
+            w.train()
+        return self.print_log("val")
+
     def fit(self):
         a = self.args
         acc = max(1, a.accumulate_grad)
@@ -266,6 +301,8 @@ class Trainer:
                     self.save(epoch_complete=False, batches_done=bi + 1)
                     return
             self.print_log("train")
+            if self.val_loader is not None and (self.epoch + 1) % max(1, a.val_epoch_freq) == 0:
+                self.validate()
             if (self.epoch + 1) % a.ckpt_freq == 0:
                 self.save()
             self.epoch += 1
@@ -464,6 +501,14 @@ def resolve_precision(precision, device):
     if dt == torch.float16 and device.type != "cuda":
         raise NotImplementedError("--precision 16-mixed needs a GPU (fp16 autocast + GradScaler)")
     return dt
+
+
+def _worker_init(worker_id):
+    """A DataLoader worker's dataset copy draws from its own stream of the rank's generator."""
+    info = torch.utils.data.get_worker_info()
+    ds = info.dataset
+    if hasattr(ds, "rng"):
+        ds.rng = np.random.default_rng([int(ds.rng.integers(2 ** 31)), worker_id])
 
 
 class _null:

@@ -690,8 +690,11 @@ class _GvpLossFn(torch.autograd.Function):
     def forward(ctx, out, ut, mask):
         lib = _lib.load()
         B, T, L, K = out.shape
-        o, u = out.detach().contiguous(), ut.detach().contiguous()
-        m = mask.detach().expand(B, T, L, K)
+        # the kernels read fp32: a half-precision prediction (the eager FinalLayer under bf16 /
+        # fp16 autocast) is promoted here, as the reference's (out - ut) with an fp32 ut promotes
+        ctx.out_dtype = out.dtype
+        o, u = out.detach().float().contiguous(), ut.detach().float().contiguous()
+        m = mask.detach().float().expand(B, T, L, K)
         ms = (ctypes.c_int64 * 4)(*m.stride())
         loss = torch.empty(B, device=out.device)
         den = torch.empty(B, device=out.device)
@@ -712,7 +715,7 @@ class _GvpLossFn(torch.autograd.Function):
         dout = torch.empty_like(o)
         _lib.check(lib.mdg_gvp_loss_bwd(B, T, L, K, o.data_ptr(), u.data_ptr(), m.data_ptr(), ms, gc.data_ptr(),
                                         den.data_ptr(), dout.data_ptr(), _lib.stream_handle()), "mdg_gvp_loss_bwd")
-        return dout, None, None
+        return dout.to(ctx.out_dtype), None, None
 
 
 def gvp_loss(out, ut, mask):

@@ -235,6 +235,7 @@ def odeint_dopri5_graphed(func, y0, t, rtol=1e-3, atol=1e-6, max_num_steps=2 ** 
     # a field that conditions several times at once (HipEngine.velocity_field: t-embedding, adaLN
     # rows and IPA prepend for all 5 stage times in one call) gets the step's stage times up front
     pre = getattr(func, "precondition", None)
+    ensure = getattr(func, "ensure", None)  # the field's hoisted state back in place (engine)
 
     def step():
         y, fy, t_hi, dt = S["y"], S["fy"], S["t_hi"], S["dt"]
@@ -294,6 +295,8 @@ def odeint_dopri5_graphed(func, y0, t, rtol=1e-3, atol=1e-6, max_num_steps=2 ** 
                 raise AssertionError(f"max_num_steps exceeded ({n_steps}>={max_num_steps})")
             if not t_hi_v + dt_v > t_hi_v:
                 raise AssertionError(f"underflow in dt {dt_v}")
+            if ensure is not None:
+                ensure()
             g.replay()
             n_steps += 1
         x = ((t[i] - S["t_lo"]) / (S["t_hi"] - S["t_lo"])).to(dty)

@@ -558,10 +558,10 @@ def test_tps_ipa_long_crop_grads_match_eager(L):
 
 
 def _rccl_world1_worker(rank, port, out):
-    """The body of test_graphed_step_rccl_bucket_allreduce_in_capture_world1 in a child process:
-    the RCCL communicator and the graphs that captured its collectives die with the child
-    (os._exit after the results are handed over) instead of being torn down in the test runner."""
-    import os
+    """The body of test_graphed_step_rccl_bucket_allreduce_in_capture_world1 in a child process,
+    ending with the production teardown of train.main: the graphs holding captured collectives
+    released, the device drained, destroy_process_group, a normal return (no os._exit)."""
+    import gc
 
     import torch.distributed as dist
 
@@ -589,8 +589,14 @@ def _rccl_world1_worker(rank, port, out):
         st = _trainer_state(tr)
         res[mode] = (losses, [t.cpu() for t in st])
         torch.cuda.synchronize()
+        g = red = None
+        tr._graphed = None  # train.main's order: the graph before the communicator
+        tr = None
     out["res"], out["info"] = res, info
-    os._exit(0)
+    gc.collect()
+    torch.cuda.synchronize()
+    dist.destroy_process_group()
+    out["teardown"] = "ok"
 
 
 def test_graphed_step_rccl_bucket_allreduce_in_capture_world1():
@@ -612,6 +618,7 @@ def test_graphed_step_rccl_bucket_allreduce_in_capture_world1():
     out = mgr.dict()
     mp.spawn(_rccl_world1_worker, args=(port, out), nprocs=1, join=True)
     info = out["info"]
+    assert out.get("teardown") == "ok"
     assert info["overlap"] and not info["has_g2"], info
     assert info["buckets"] >= 3, info
     assert [bi for bi, _ in info["log"]] == list(range(info["buckets"])), info

@@ -278,6 +278,79 @@ def test_bucketed_allreduce_world2_gloo_overlaps_and_averages():
         assert covers
 
 
+def _bucket_order_worker(rank, world, port, out):
+    """Rank agreement of grad_buckets.BucketedAllReduce: rank 1 records a PERMUTED completion order
+    and fires its hooks in yet another order; the layout must still be rank 0's, the buckets must
+    be reduced in layout order on both ranks, and every parameter averaged with itself.  Then a
+    rank that reached a different gradient set, and a hook firing twice, must raise."""
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(1)
+    from mdgen_finetune_amd.grad_buckets import BucketedAllReduce
+
+    sizes = [300, 17, 1024, 5, 640, 96, 2048, 33, 512, 7]
+    params = [torch.nn.Parameter(torch.zeros(n)) for n in sizes]
+    order0 = list(range(len(sizes)))
+    perm = [7, 2, 9, 0, 4, 1, 8, 3, 6, 5]
+    red = BucketedAllReduce(params, order0 if rank == 0 else perm, cap_bytes=4 * 1100, world=world)
+    layouts = [None] * world
+    dist.all_gather_object(layouts, red.buckets)
+    red.attach()
+    gen = torch.Generator().manual_seed(40 + rank)
+    local = [torch.randn(n, generator=gen) for n in sizes]
+    fire = order0 if rank == 0 else list(reversed(perm))  # rank 1 completes in another order still
+    for i in fire:
+        params[i].grad = local[i].clone()
+        red._ready(i)
+    red.finish()
+    err = 0.0
+    for p, lg in zip(params, local):
+        ref = lg.clone()
+        dist.all_reduce(ref)
+        ref /= world
+        err = max(err, float((p.grad - ref).abs().max()))
+    res = dict(layouts=layouts, log=[bi for bi, _ in red.launch_log], nb=len(red.buckets), err=err)
+    # a hook that fires twice in one backward
+    red.attach()
+    params[0].grad = local[0].clone()
+    red._ready(0)
+    try:
+        red._ready(0)
+        res["dup"] = "no error"
+    except RuntimeError as e:
+        res["dup"] = str(e)
+    # drain the collectives rank 0's single fire may have launched (same sequence on both ranks)
+    for i in order0[1:]:
+        params[i].grad = local[i].clone()
+        red._ready(i)
+    red.finish()
+    # a rank whose backward reached a different set of gradients
+    try:
+        BucketedAllReduce(params, order0 if rank == 0 else order0[:-1], cap_bytes=4 * 1100, world=world)
+        res["mismatch"] = "no error"
+    except RuntimeError as e:
+        res["mismatch"] = str(e)
+    out[rank] = res
+    dist.destroy_process_group()
+
+
+def test_bucket_layout_agreed_across_ranks_world2_gloo():
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_bucket_order_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    r0, r1 = out[0], out[1]
+    assert r0["layouts"][0] == r0["layouts"][1] == r1["layouts"][0]
+    assert [i for b in r0["layouts"][0] for i in b] == list(range(10))  # rank 0's order
+    for r in (r0, r1):
+        assert r["nb"] >= 3
+        assert r["log"] == list(range(r["nb"])), r["log"]
+        assert r["err"] <= 1e-6, r["err"]
+        assert "fired twice" in r["dup"], r["dup"]
+        assert "different set of gradients" in r["mismatch"], r["mismatch"]
+
+
 def _bench_worker(rank, world, port, out):
     import torch.distributed as dist
 

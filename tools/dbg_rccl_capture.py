@@ -26,7 +26,7 @@ side = torch.cuda.Stream()
 g = torch.cuda.CUDAGraph()
 y = torch.ones(1024, device=dev)
 torch.cuda.synchronize()
-with torch.cuda.graph(g):
+with torch.cuda.graph(g, capture_error_mode=os.environ.get('CAPMODE', 'thread_local')):
     z = y * 2
     ev = torch.cuda.Event()
     ev.record(torch.cuda.current_stream())
