@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define MDG_ABI_VERSION 21
+#define MDG_ABI_VERSION 22
 #define MDG_MAX_LAYERS 16
 #define MDG_SEG_MAX 16 /* segments of one mdg_seg_linear */
 #define MDG_DP 32      /* padded head dim of the attention operand buffers for head_dim <= 31 */
@@ -147,8 +147,12 @@ typedef struct {
      resid_in  GATE_RES reads the residual from resid_in [M][ldr] and writes resid (out of place);
      aux       STORE with act GELU: also stores CT(pre-activation) to aux [M][ldaux] (saved for
                the backward); STORE with act DGELU: out = acc * gelu'(aux) (aux = the forward's
-               pre-activation, read); GATE_RES: also stores CT(acc + bias), the pre-gate value. */
+               pre-activation, read); GATE_RES: also stores CT(acc + bias), the pre-gate value.
+     ln_stats  GATE_RES + LayerNorm (xn_out set): also stores each row's (mean, rstd) as fp32
+               [M][2] (ABI 22; bf16, N 384, with resid_in and aux: the training forward's row-LN
+               route, one launch instead of the GEMM + mdg_ln_mod pass). */
   const float* resid_in; void* aux; int32_t ldaux;
+  float* ln_stats;
 } mdg_gemm_desc;
 
 int mdg_abi_version(void);

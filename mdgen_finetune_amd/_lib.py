@@ -72,6 +72,7 @@ class MdgGemmDesc(ctypes.Structure):
         ("xn_out", _vp), ("xn_mods", _vp), ("xn_mod_stride", _i32), ("xn_shift_off", _i32), ("xn_scale_off", _i32),
         ("kvb", _vp), ("key_mask", _vp),
         ("resid_in", _vp), ("aux", _vp), ("ldaux", _i32),
+        ("ln_stats", _vp),
     ]
 
 
@@ -199,7 +200,7 @@ SIGNATURES = [
                                                                           ctypes.c_size_t, _vp]),
 ]
 
-ABI_VERSION = 21
+ABI_VERSION = 22
 _LIB = None
 
 

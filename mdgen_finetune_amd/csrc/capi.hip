@@ -880,6 +880,17 @@ static int init_planes(const mdg_dims* d, void* planes, int B, int T, int L, hip
   return hip_check(mdg::set_vpad_launch(d->dtype, (char*)planes + rows * MDG_DP * cs, 2 * rows, d->D, s), "set_vpad");
 }
 
+// the row-LN route of the training forward (gemm.hip kCfgRowTrain); MDG_TRAIN_ROWLN=0: the GEMM +
+// mdg_ln_mod pair (A/B)
+static constexpr int kCfgRowTrainId = 105;
+static bool train_rowln_on() {
+  static const bool v = [] {
+    const char* e = getenv("MDG_TRAIN_ROWLN");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
 int mdg_layer_fwd_train(const mdg_dims* d, const mdg_layer_weights* w, const float* rope_l, const float* rope_t,
                         const float* mods, const float* mask, const float* kbias_t, const float* kbias_s,
                         const float* h_in, float* h_out, const mdg_layer_saved* sv, void* stream) {
@@ -934,12 +945,35 @@ int mdg_layer_fwd_train(const mdg_dims* d, const mdg_layer_weights* w, const flo
   mdg_gemm_desc r = g;
   r.epi = MDG_EPI_GATE_RES; r.N = C; r.K = C; r.A = sv->o[0]; r.lda = C; r.W = w->wo[0]; r.ldw = C; r.bias = w->bo[0];
   r.resid_in = h_in; r.resid = sv->h1; r.ldr = C; r.gate = mods; r.gate_off = 2 * C; r.aux = sv->y[0]; r.ldaux = C;
-  if (int e = mdg_gemm(&r, stream)) return e;
+  // the out_proj and the NEXT sublayer's LayerNorm + modulate as one row-LN launch (its xn, the
+  // LN row statistics and the pre-gate value saved), where the bf16 row-LN GEMM takes the shape;
+  // otherwise the GEMM then mdg_ln_mod.  Returns 1 when the LN was fused.
+  auto out_proj_ln = [&](mdg_gemm_desc& rr, int next, int shift_off, int scale_off, bool& fused) -> int {
+    fused = false;
+    if (train_rowln_on()) {
+      mdg_gemm_desc f = rr;
+      f.xn_out = sv->xn[next]; f.xn_mods = mods; f.xn_mod_stride = ms; f.xn_shift_off = shift_off;
+      f.xn_scale_off = scale_off; f.ln_eps = 1e-6f; f.ln_stats = sv->stats[next];
+      if (mdg::gemm_plan(f).cfg == kCfgRowTrainId) {
+        fused = true;
+        return mdg_gemm(&f, stream);
+      }
+    }
+    return mdg_gemm(&rr, stream);
+  };
+  bool fused_ln = false;
+  if (sv->skip_temporal) {
+    if (int e = out_proj_ln(r, 2, 6 * C, 7 * C, fused_ln)) return e;
+  } else {
+    if (int e = out_proj_ln(r, 1, 3 * C, 4 * C, fused_ln)) return e;
+  }
 
   // ---- temporal sublayer (latent_model.py:474-486); skipped for the IPA layers' tail (gate 0)
   const float* h_mlp = sv->h1;
+  bool mlp_ln_done = sv->skip_temporal && fused_ln;
   if (!sv->skip_temporal) {
-    if (int e = ln(sv->h1, 1, 3 * C, 4 * C)) return e;
+    if (!fused_ln)
+      if (int e = ln(sv->h1, 1, 3 * C, 4 * C)) return e;
     q.epi = MDG_EPI_QKV; q.A = sv->xn[1]; q.W = w->wqkv[1]; q.bias = w->bqkv[1];
     q.qkv_layout = MDG_QKV_TEMPORAL; q.qkv_out = sv->qkv_t; q.qscale = qs * log2e; q.rope = rope_t; q.rope_rows = T + 1;
     if (int e = mdg_gemm(&q, stream)) return e;
@@ -948,12 +982,13 @@ int mdg_layer_fwd_train(const mdg_dims* d, const mdg_layer_weights* w, const flo
       return e;
     r.A = sv->o[1]; r.W = w->wo[1]; r.bias = w->bo[1]; r.resid_in = sv->h1; r.resid = sv->h2; r.gate_off = 5 * C;
     r.aux = sv->y[1];
-    if (int e = mdg_gemm(&r, stream)) return e;
+    if (int e = out_proj_ln(r, 2, 6 * C, 7 * C, mlp_ln_done)) return e;
     h_mlp = sv->h2;
   }
 
   // ---- MLP (latent_model.py:488-491)
-  if (int e = ln(h_mlp, 2, 6 * C, 7 * C)) return e;
+  if (!mlp_ln_done)
+    if (int e = ln(h_mlp, 2, 6 * C, 7 * C)) return e;
   mdg_gemm_desc f1 = g;
   f1.epi = MDG_EPI_STORE; f1.act = MDG_ACT_GELU; f1.N = F; f1.K = C; f1.A = sv->xn[2]; f1.lda = C; f1.W = w->w1;
   f1.ldw = C; f1.bias = w->b1; f1.out = sv->act; f1.ldo = F; f1.aux = sv->u; f1.ldaux = F;

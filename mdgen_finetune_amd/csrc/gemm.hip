@@ -1052,14 +1052,17 @@ struct RowsFrames {
   }
 };
 
-template <int NCOL, typename RM>
+// TRAIN: the residual is read from resid_in (the training forward keeps the sublayer input for
+// the backward), the pre-gate value and the LN row statistics are stored (rowln_fast_epilogue_impl)
+template <int NCOL, typename RM, bool TRAIN = false>
 __device__ __forceinline__ void rowln_load_band(const mdg_gemm_desc& p, RM rows, int u, float4 (&h4)[2][NCOL / 128]) {
   constexpr int NE = NCOL / 128;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, half = lane >> 5, hl = lane & 31;
+  const float* src = TRAIN ? p.resid_in : p.resid;
 #pragma unroll
   for (int pr = 0; pr < 2; ++pr) {
     const int m = min(rows(u * 32 + wave * 4 + 2 * pr + half), p.M - 1);
-    const float* hr = p.resid + (size_t)m * p.ldr + 4 * hl;
+    const float* hr = src + (size_t)m * p.ldr + 4 * hl;
 #pragma unroll
     for (int e = 0; e < NE; ++e) h4[pr][e] = *reinterpret_cast<const float4*>(hr + 128 * e);
   }
@@ -1074,7 +1077,7 @@ __device__ __forceinline__ void rowln_load_band(const mdg_gemm_desc& p, RM rows,
 // bands 0-2 at once (at band 0's call; band 3 at its own) and free their registers early.
 // LATE_H: h4 is not loaded yet; band 0's residual rows are read right after band 0's staging (a
 // caller whose accumulators fill the registers until then).
-template <int NCOL, int NREG = 1, bool LATE_H = false, typename StageBand, typename RM = RowsLinear>
+template <int NCOL, int NREG = 1, bool LATE_H = false, typename StageBand, typename RM = RowsLinear, bool TRAIN = false>
 __device__ __forceinline__ void rowln_fast_epilogue_impl(const mdg_gemm_desc& p, StageBand stage_band,
                                                          float4 (&h4)[2][NCOL / 128], unsigned char* smem, RM rows,
                                                          int b_lo, float inv_rpm, bf16_t* xlds = nullptr) {
@@ -1088,7 +1091,7 @@ __device__ __forceinline__ void rowln_fast_epilogue_impl(const mdg_gemm_desc& p,
   const int b_hi = fdiv(min(rows(BM - 1), M - 1), p.rows_per_mod, inv_rpm);
   float* stage = reinterpret_cast<float*>(smem);
   const float invN = 1.0f / (float)NCOL;
-  auto load_unit4 = [&](int u, float4 (&hb)[2][NE]) { rowln_load_band<NCOL>(p, rows, u, hb); };
+  auto load_unit4 = [&](int u, float4 (&hb)[2][NE]) { rowln_load_band<NCOL, RM, TRAIN>(p, rows, u, hb); };
   float* emods = stage + NREG * 32 * LDS_ST;  // [2][3][NCOL]: gate | xn scale | xn shift
   // the caller's smem holds (32 * LDS_ST + 6 * NCOL) floats: the band stage + the adaLN rows
   static_assert(LDS_ST % 4 == 0, "16-B aligned stage rows");
@@ -1114,7 +1117,7 @@ __device__ __forceinline__ void rowln_fast_epilogue_impl(const mdg_gemm_desc& p,
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // previous band's stage reads (and the adaLN rows) are done
     stage_band(band, stage);
-    if (LATE_H && band == 0) rowln_load_band<NCOL>(p, rows, 0, h4);
+    if (LATE_H && band == 0) rowln_load_band<NCOL, RM, TRAIN>(p, rows, 0, h4);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     const float* bstage = stage + (band % NREG) * 32 * LDS_ST;
     __builtin_amdgcn_s_barrier();
@@ -1129,10 +1132,14 @@ __device__ __forceinline__ void rowln_fast_epilogue_impl(const mdg_gemm_desc& p,
       const float* srow = bstage + (wave * 4 + 2 * pr + half) * LDS_ST + 4 * hl;
       const float* gr = emods + eb[pr] * 3 * NCOL + 4 * hl;
       float sacc = 0.f;
+      const int mrow = rows(band * 32 + wave * 4 + 2 * pr + half);
 #pragma unroll
       for (int e = 0; e < NE; ++e) {
         const float4 v = *reinterpret_cast<const float4*>(srow + 128 * e);
         const float4 g = *reinterpret_cast<const float4*>(gr + 128 * e);
+        if (TRAIN && mrow < M)  // the pre-gate out_proj / fc2 output, saved for the gate's backward
+          st4<bf16_t>(reinterpret_cast<bf16_t*>(p.aux) + (size_t)mrow * p.ldaux + 4 * hl + 128 * e, v.x + b4[e].x,
+                      v.y + b4[e].y, v.z + b4[e].z, v.w + b4[e].w);
         float4& h = h4[pr][e];
         h.x += g.x * (v.x + b4[e].x);
         h.y += g.y * (v.y + b4[e].y);
@@ -1174,6 +1181,8 @@ __device__ __forceinline__ void rowln_fast_epilogue_impl(const mdg_gemm_desc& p,
       for (int pr = 0; pr < 2; ++pr) {
         const int rl = band * 32 + wave * 4 + 2 * pr + half, m = rows(rl);
         const float rs = 1.0f / sqrtf(ss[pr] * invN + p.ln_eps);
+        if (TRAIN && hl == 0 && m < M)  // (mean, rstd) for the LN backward (ln_mod's stats layout)
+          *reinterpret_cast<float2*>(p.ln_stats + 2 * (size_t)m) = make_float2(sum[pr], rs);
         const float* mr = emods + eb[pr] * 3 * NCOL + 4 * hl;
 #pragma unroll
         for (int e = 0; e < NE; ++e) {
@@ -1201,7 +1210,7 @@ __device__ __forceinline__ void rowln_fast_epilogue_impl(const mdg_gemm_desc& p,
 
 // The 8-wave (2 x 4) accumulator layout of the row-LN GEMM / fused MLP / fused out_proj + qkv:
 // wave (wm, wn) holds rows wm * 64 + 16 i + 4 lg + r, columns wn * NCOL / 4 + 16 j + lr.
-template <int NCOL, typename RM = RowsLinear>
+template <int NCOL, typename RM = RowsLinear, bool TRAIN = false>
 __device__ __forceinline__ void rowln_fast_epilogue(const mdg_gemm_desc& p, f32x4 (&acc)[4][NCOL / 64],
                                                     float4 (&h4)[2][NCOL / 128], unsigned char* smem, RM rows,
                                                     int b_lo, float inv_rpm, bf16_t* xlds = nullptr) {
@@ -1221,12 +1230,15 @@ __device__ __forceinline__ void rowln_fast_epilogue(const mdg_gemm_desc& p, f32x
       }
     }
   };
-  rowln_fast_epilogue_impl<NCOL>(p, stage_band, h4, smem, rows, b_lo, inv_rpm, xlds);
+  rowln_fast_epilogue_impl<NCOL, 1, false, decltype(stage_band), RM, TRAIN>(p, stage_band, h4, smem, rows, b_lo, inv_rpm,
+                                                                            xlds);
 }
 
 // PART: split-K form for small M — block (tile, y) runs K-steps [y nk, (y + 1) nk) and writes its
 // fp32 partial tile to (float*)p.aux + y * M * NCOL; mlp_split_reduce_kernel finishes the rows
-template <int NCOL, int BM, bool PART = false>
+// TRAIN (BM 128, every tile on the fast epilogue: rows_per_mod >= 128): the training forward's
+// out_proj / fc2 — residual read from resid_in, out of place; pre-gate value to aux; LN stats
+template <int NCOL, int BM, bool PART = false, bool TRAIN = false>
 __global__ __launch_bounds__(kRowThreads, BM == 64 ? 4 : 1) void gemm_rowln_kernel(const mdg_gemm_desc p) {
   constexpr int kRowStages = RowCfg<BM>::STAGES, WMW = RowCfg<BM>::WMW, WNW = 8 / WMW;
   constexpr int BK = 32, WTN = NCOL / WNW, NT = WTN / 16, ATILE = BM * BK, STAGE = (BM + NCOL) * BK;
@@ -1308,7 +1320,7 @@ __global__ __launch_bounds__(kRowThreads, BM == 64 ? 4 : 1) void gemm_rowln_kern
   float4 h4[2][NE];
   float2 hv[RG][NE], gv[NE];
   if (!PART) {
-    if (fast) rowln_load_band<NCOL>(p, RowsLinear{m0}, 0, h4);
+    if (fast) rowln_load_band<NCOL, RowsLinear, TRAIN>(p, RowsLinear{m0}, 0, h4);
     else if (BM == 64) load_unit(0, hv, gv);
   }
 
@@ -1385,10 +1397,11 @@ __global__ __launch_bounds__(kRowThreads, BM == 64 ? 4 : 1) void gemm_rowln_kern
   if constexpr (BM == 128) {
     static_assert((32 * LDS_ST + 6 * NCOL) * 4 <= kRowStages * STAGE * 2, "adaLN rows fit the ring");
     if (fast) {
-      rowln_fast_epilogue<NCOL>(p, acc, h4, smem, RowsLinear{m0}, b_lo, inv_rpm);
+      rowln_fast_epilogue<NCOL, RowsLinear, TRAIN>(p, acc, h4, smem, RowsLinear{m0}, b_lo, inv_rpm);
       return;
     }
   }
+  if constexpr (TRAIN) return;  // (unreachable: the host takes this route only when every tile is fast)
   if (BM == 128) load_unit(0, hv, gv);  // the rare tile over > 2 entries: no prefetch under the K loop
   __syncthreads();  // all waves are done with the ring
 #pragma unroll 1
@@ -1524,6 +1537,19 @@ static hipError_t launch_rowln(const mdg_gemm_desc& p, hipStream_t s) {
   }
   hipLaunchKernelGGL((gemm_rowln_kernel<NCOL, BM>), dim3((p.M + BM - 1) / BM), dim3(kRowThreads),
                      (rowln_smem<NCOL, BM>()), s, p);
+  return hipGetLastError();
+}
+
+static hipError_t launch_rowln_train(const mdg_gemm_desc& p, hipStream_t s) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_rowln_kernel<384, 128, false, true>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)rowln_smem<384, 128>());
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((gemm_rowln_kernel<384, 128, false, true>), dim3((p.M + 127) / 128), dim3(kRowThreads),
+                     (rowln_smem<384, 128>()), s, p);
   return hipGetLastError();
 }
 
@@ -3200,7 +3226,7 @@ static bool stage_fits() {
   return stage <= room;
 }
 
-constexpr int kCfgB4 = 100, kCfgB8 = 101, kCfgB4K32 = 102, kCfgRow = 103, kCfgSpa = 104;
+constexpr int kCfgB4 = 100, kCfgB8 = 101, kCfgB4K32 = 102, kCfgRow = 103, kCfgSpa = 104, kCfgRowTrain = 105;
 
 struct GemmPlan {
   int cfg;  // index into the config table below; -1 = unsupported
@@ -3274,7 +3300,16 @@ GemmPlan gemm_plan(const mdg_gemm_desc& p) {
     g.bn = kSpaBN;
     return g;
   }
-  const bool ext = p.resid_in || p.aux;  // training extensions: epi4 / epi_tile kernels only
+  const bool ext = p.resid_in || p.aux || p.ln_stats;  // training extensions: epi4 / epi_tile kernels only
+  if (bf && p.epi == MDG_EPI_GATE_RES && p.xn_out && p.resid_in && p.aux && p.ln_stats && p.N == 384 &&
+      p.K % 64 == 0 && p.lda % 8 == 0 && p.ldw % 8 == 0 && p.ldaux % 4 == 0 && p.rows_per_mod >= 128 &&
+      rowln_bm(p.M) == 128) {
+    g.cfg = kCfgRowTrain;  // the training forward's out_proj / fc2 + the next LN (row-LN GEMM)
+    g.smem = rowln_smem<384, 128>();
+    g.bm = 128;
+    g.bn = 384;
+    return g;
+  }
   if (bf && ln) cfg = (p.N % 128 == 0) ? (big ? 0 : 2) : (p.N % 32 == 0 ? (big ? 1 : 3) : -1);
   else if (bf && !ext && p.epi == MDG_EPI_GATE_RES && p.xn_out && p.K % 64 == 0 && p.lda % 8 == 0 && p.ldw % 8 == 0 &&
            (p.N == 128 || p.N == 256 || p.N == 384 || p.N == 512)) {
@@ -3331,6 +3366,7 @@ GemmPlan gemm_plan(const mdg_gemm_desc& p) {
 
 hipError_t gemm_launch(const mdg_gemm_desc& p, const GemmPlan& g, hipStream_t s) {
   if (g.cfg == kCfgSpa) return launch_spatial(p, s);
+  if (g.cfg == kCfgRowTrain) return launch_rowln_train(p, s);
   if (g.cfg == kCfgRow) {
     if (g.bm == 64) {
       switch (p.N) {

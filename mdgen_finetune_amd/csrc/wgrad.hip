@@ -37,11 +37,27 @@ struct WgArgs {
   float* part;   // [S][M][K] fp32 (S == 1 with direct = true: dW itself)
   float* cpart;  // [S][M] fp32 column sums of dY per split (the bias gradient; null: none)
   int N, M, K, ldy, ldx, ldp, chunk;
+  int gx, gy, gz;  // M tiles, K tiles, token splits (the bf16 kernels' 1-D grid is gx * gy * gz)
 };
 
 typedef __attribute__((ext_vector_type(16))) float f32x16;
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+// Block -> (M tile, K tile, token split) with every tile of one token split on the SAME XCD:
+// the 1-D grid is dispatched round-robin over the 8 XCDs, so the remap hands each XCD a
+// contiguous range of (split, tile) indices, split-major.  The blocks of a split stream the
+// same token rows of dY and X at about the same time, and that XCD's L2 serves the re-reads
+// (the 3-D grid spread a split's tiles over all 8 L2s: 4x the algorithmic HBM bytes).
+__device__ __forceinline__ void wg_tile_of(int gx, int gy, int gz, int& mt, int& kt, int& z) {
+  const int nwg = gx * gy * gz;
+  const int xcd = blockIdx.x & 7, loc = blockIdx.x >> 3, q = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + loc;
+  z = wg / (gx * gy);
+  const int t = wg - z * gx * gy;
+  kt = t / gx;
+  mt = t - kt * gx;
+}
 
 __device__ __forceinline__ void wg_vm_wait(int n) {
   if (n >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
@@ -65,11 +81,14 @@ __device__ __forceinline__ bf16x8 wg_frag(const bf16_t* img, int cbase, int s2, 
   return r;
 }
 
+template <int NS>  // operand ring depth (3: the default; MDG_WGRAD_STAGES=4 / 5 for A/B)
 __global__ __launch_bounds__(kWgThreads, 2) void wgrad_bf16_kernel(const WgArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   bf16_t* ring = reinterpret_cast<bf16_t*>(smem);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int m0 = blockIdx.x * kWgTile, k0 = blockIdx.y * kWgTile, z = blockIdx.z;
+  int mt, kt, z;
+  wg_tile_of(a.gx, a.gy, a.gz, mt, kt, z);
+  const int m0 = mt * kWgTile, k0 = kt * kWgTile;
   const int nbeg = z * a.chunk;
   const int nsteps = (min(a.N, nbeg + a.chunk) - nbeg) / kWgBK;
   const bf16_t* DY = reinterpret_cast<const bf16_t*>(a.dy);
@@ -89,7 +108,7 @@ __global__ __launch_bounds__(kWgThreads, 2) void wgrad_bf16_kernel(const WgArgs 
     dst[j] = img * kWgImg + rb * kWgTile;
   }
   auto issue = [&](int s) {
-    bf16_t* sl = ring + (s % kWgStages) * kWgSlot;
+    bf16_t* sl = ring + (s % NS) * kWgSlot;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const bf16_t* base = (j >> 1) ? X : DY;
@@ -109,19 +128,24 @@ __global__ __launch_bounds__(kWgThreads, 2) void wgrad_bf16_kernel(const WgArgs 
   // bias gradient: the blocks of the first K tile also sum their dY fragments over the tokens
   // (waves wk == 0 hold every feature of the M tile once): 8 tokens per lane and k-step, the
   // two lane halves combined at the end.  No separate column-sum pass over dY.
-  const bool csum = a.cpart != nullptr && blockIdx.y == 0 && wk == 0;
+  const bool csum = a.cpart != nullptr && kt == 0 && wk == 0;
   float cs[2] = {0.f, 0.f};
-  for (int s0 = 0; s0 < kWgStages - 1; ++s0)
+  for (int s0 = 0; s0 < NS - 1; ++s0)
     if (s0 < nsteps) issue(s0);
   for (int s = 0; s < nsteps; ++s) {
-    // step s landed (step s+1's pieces stay in flight); every wave's reads of step s-1 are
-    // retired (lgkmcnt) before the barrier, so the slot can be refilled with step s+2
-    wg_vm_wait(s + 1 < nsteps ? 4 : 0);
+    // step s landed (the NS - 2 later steps' pieces stay in flight, 4 per step); every wave's
+    // reads of step s-1 are retired (lgkmcnt) before the barrier, so the slot can be refilled
+    // with step s + NS - 1
+    const int ahead = min(NS - 2, nsteps - 1 - s);
+    if (ahead >= 3) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else if (ahead == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (s + kWgStages - 1 < nsteps) issue(s + kWgStages - 1);
-    const bf16_t* A = ring + (s % kWgStages) * kWgSlot;
+    if (s + NS - 1 < nsteps) issue(s + NS - 1);
+    const bf16_t* A = ring + (s % NS) * kWgSlot;
     const bf16_t* B = A + kWgImg;
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
@@ -180,7 +204,9 @@ __global__ __launch_bounds__(kWgThreads, 2) void wgrad_bf16_wide_kernel(const Wg
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   bf16_t* ring = reinterpret_cast<bf16_t*>(smem);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int m0 = blockIdx.x * TM, k0 = blockIdx.y * TK, z = blockIdx.z;
+  int mt, kt, z;
+  wg_tile_of(a.gx, a.gy, a.gz, mt, kt, z);
+  const int m0 = mt * TM, k0 = kt * TK;
   const int nbeg = z * a.chunk;
   const int nsteps = (min(a.N, nbeg + a.chunk) - nbeg) / kWgBK;
   const bf16_t* DY = reinterpret_cast<const bf16_t*>(a.dy);
@@ -236,7 +262,7 @@ __global__ __launch_bounds__(kWgThreads, 2) void wgrad_bf16_wide_kernel(const Wg
     for (int u = 0; u < WKT; ++u)
 #pragma unroll
       for (int i = 0; i < 16; ++i) acc[t][u][i] = 0.f;
-  const bool csum = a.cpart != nullptr && blockIdx.y == 0 && wk == 0;
+  const bool csum = a.cpart != nullptr && kt == 0 && wk == 0;
   float cs[WMT];
 #pragma unroll
   for (int t = 0; t < WMT; ++t) cs[t] = 0.f;
@@ -434,6 +460,14 @@ static int wgrad_wide_enabled() {
   }();
   return v;
 }
+static int wgrad_stages() {
+  static const int v = [] {
+    const char* e = getenv("MDG_WGRAD_STAGES");
+    const int n = e ? atoi(e) : 3;
+    return (n == 4 || n == 5) ? n : 3;
+  }();
+  return v;
+}
 static int wgrad_target_blocks() {
   static const int v = [] {
     const char* e = getenv("MDG_WGRAD_BLOCKS");
@@ -452,9 +486,12 @@ WgPlan wgrad_plan(int dtype, int N, int M, int K, bool need_w, bool need_b) {
   const int tiles = ((M + tm - 1) / tm) * ((K + tk - 1) / tk);
   const int quantum = dtype == MDG_BF16 ? kWgBK : 16;
   const int nq = (N + quantum - 1) / quantum;
-  // ~2 blocks per CU over the 256 CUs, each split at least 8 K-steps long
+  // ~2 blocks per CU over the 256 CUs, each split at least 8 K-steps long.  The block count
+  // stays AT MOST the target (two resident blocks per CU): rounding the split count up put the
+  // last few blocks in a second round, which then took as long as the first (w2: 540 blocks,
+  // 78 us; at 504 blocks the grid is one round)
   const int target = wgrad_target_blocks();
-  int S = need_w ? (target + tiles - 1) / tiles : 1;
+  int S = need_w ? max(1, target / tiles) : 1;
   S = max(1, min(S, nq / 8));
   p.chunk = ((nq + S - 1) / S) * quantum;
   p.S = (N + p.chunk - 1) / p.chunk;
@@ -496,20 +533,34 @@ hipError_t wgrad_launch(int dtype, int N, int M, int K, const void* dy, int ldy,
         }
         attr = true;
       }
+      a.gx = p.wide == 1 ? M / 256 : M / 128;
+      a.gy = p.wide == 1 ? K / 128 : K / 256;
+      a.gz = p.S;
+      const dim3 grid((unsigned)(a.gx * a.gy * a.gz));
       if (p.wide == 1)
-        hipLaunchKernelGGL((wgrad_bf16_wide_kernel<4, 2>), dim3(M / 256, K / 128, p.S), dim3(kWgThreads), smem, s, a);
+        hipLaunchKernelGGL((wgrad_bf16_wide_kernel<4, 2>), grid, dim3(kWgThreads), smem, s, a);
       else
-        hipLaunchKernelGGL((wgrad_bf16_wide_kernel<2, 4>), dim3(M / 128, K / 256, p.S), dim3(kWgThreads), smem, s, a);
+        hipLaunchKernelGGL((wgrad_bf16_wide_kernel<2, 4>), grid, dim3(kWgThreads), smem, s, a);
     } else if (dtype == MDG_BF16) {
       static bool attr = false;
       if (!attr) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_bf16_kernel),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, kWgStages * kWgSlot * 2);
-        if (e != hipSuccess) return e;
+        const void* ks[3] = {reinterpret_cast<const void*>(&wgrad_bf16_kernel<3>),
+                             reinterpret_cast<const void*>(&wgrad_bf16_kernel<4>),
+                             reinterpret_cast<const void*>(&wgrad_bf16_kernel<5>)};
+        for (int i = 0; i < 3; ++i) {
+          hipError_t e = hipFuncSetAttribute(ks[i], hipFuncAttributeMaxDynamicSharedMemorySize, (3 + i) * kWgSlot * 2);
+          if (e != hipSuccess) return e;
+        }
         attr = true;
       }
-      hipLaunchKernelGGL(wgrad_bf16_kernel, dim3((M + 127) / 128, (K + 127) / 128, p.S), dim3(kWgThreads),
-                         kWgStages * kWgSlot * 2, s, a);
+      a.gx = (M + 127) / 128;
+      a.gy = (K + 127) / 128;
+      a.gz = p.S;
+      const dim3 grid((unsigned)(a.gx * a.gy * a.gz));
+      const int ns = wgrad_stages();
+      if (ns == 5) hipLaunchKernelGGL(wgrad_bf16_kernel<5>, grid, dim3(kWgThreads), 5 * kWgSlot * 2, s, a);
+      else if (ns == 4) hipLaunchKernelGGL(wgrad_bf16_kernel<4>, grid, dim3(kWgThreads), 4 * kWgSlot * 2, s, a);
+      else hipLaunchKernelGGL(wgrad_bf16_kernel<3>, grid, dim3(kWgThreads), 3 * kWgSlot * 2, s, a);
     } else {
       hipLaunchKernelGGL(wgrad_f32_kernel, dim3((M + 63) / 64, (K + 63) / 64, p.S), dim3(256), 0, s, a);
     }
