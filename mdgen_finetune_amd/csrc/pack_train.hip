@@ -216,33 +216,43 @@ __global__ __launch_bounds__(256) void unpack_kernel(const mdg_train_unpack u) {
     }
   } else if (job == 4) {  // adaLN gradient [B][9C]
     // chunk -> (part tensor, row): shift_l, scale_l | gate_l | shift_t, scale_t | gate_t | shift_m,
-    // scale_m | gate_m  (latent_model.py:459-461).  8 lanes per element split the row blocks
-    // (a serial sum over them per element was latency-bound), combined by shuffles in lane order.
+    // scale_m | gate_m  (latent_model.py:459-461).  One thread per element, its nb row-block
+    // partials loaded 8 at a time into 8 independent sums (every load of a thread in flight
+    // together; consecutive threads read consecutive columns), combined in a fixed tree.
     const int src[9] = {0, 0, 1, 1, 1, 2, 2, 2, 3}, row[9] = {0, 1, 2, 0, 1, 2, 0, 1, 2};
-    const int g = t0 & 7;
-    for (int e0 = t0 >> 3; e0 < B * 9 * C; e0 += stride >> 3) {
+    for (int e0 = t0; e0 < B * 9 * C; e0 += stride) {
       const int b = e0 / (9 * C), ck = e0 - b * 9 * C, c9 = ck / C, k = ck - c9 * C;
-      const float* pp = u.part[src[c9]];
-      float s = 0.f;
-#pragma unroll 4
-      for (int q = g; q < nb; q += 8) s += pp[(((size_t)b * nb + q) * 4 + row[c9]) * C + k];
-      s += __shfl_xor(s, 1, 64);
-      s += __shfl_xor(s, 2, 64);
-      s += __shfl_xor(s, 4, 64);
-      if (g == 0) u.dmods[e0] = s;
+      const float* pp = u.part[src[c9]] + ((size_t)b * nb * 4 + row[c9]) * C + k;  // slot q at + q 4C
+      float a[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a[j] = 0.f;
+      int q = 0;
+#pragma unroll 2
+      for (; q + 8 <= nb; q += 8)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) a[j] += pp[(size_t)(q + j) * 4 * C];
+      for (; q < nb; ++q) a[0] += pp[(size_t)q * 4 * C];
+      u.dmods[e0] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
     }
   } else {  // out_proj (spatial, temporal) and fc2 bias gradients: row 3 of part_s / part_t / part_m
-    const int g = t0 & 7;
-    for (int e0 = t0 >> 3; e0 < 3 * C; e0 += stride >> 3) {
+    // 32 lanes per element over its B x nb partials (16 each at B = 8, T = 1000), 8 loads in
+    // flight per lane, then a shuffle tree (a serial sum per 8 lanes was the launch's long pole)
+    const int g = t0 & 31, n = B * nb;
+    for (int e0 = t0 >> 5; e0 < 3 * C; e0 += stride >> 5) {
       const int w = e0 / C, k = e0 - w * C;
-      const float* pp = u.part[w + 1];
-      float s = 0.f;
-      for (int b = 0; b < B; ++b)
-#pragma unroll 4
-        for (int q = g; q < nb; q += 8) s += pp[(((size_t)b * nb + q) * 4 + 3) * C + k];
-      s += __shfl_xor(s, 1, 64);
-      s += __shfl_xor(s, 2, 64);
-      s += __shfl_xor(s, 4, 64);
+      const float* pp = u.part[w + 1] + 3 * C + k;  // (b, q) slot i = b nb + q at + i 4C
+      float a[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a[j] = 0.f;
+      int i = g;
+#pragma unroll 2
+      for (; i + 32 * 7 < n; i += 32 * 8)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) a[j] += pp[(size_t)(i + 32 * j) * 4 * C];
+      for (; i < n; i += 32) a[0] += pp[(size_t)i * 4 * C];
+      float s = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+#pragma unroll
+      for (int o = 1; o < 32; o <<= 1) s += __shfl_xor(s, o, 64);
       if (g == 0) (w == 0 ? u.gbo[0] : w == 1 ? u.gbo[1] : u.gb2)[k] = s;
     }
   }
@@ -258,7 +268,7 @@ hipError_t train_pack_launch(const mdg_train_pack& p, hipStream_t s) {
 }
 
 hipError_t train_unpack_launch(const mdg_train_unpack& u, hipStream_t s) {
-  hipLaunchKernelGGL(unpack_kernel, dim3(128, 6), dim3(256), 0, s, u);
+  hipLaunchKernelGGL(unpack_kernel, dim3(144, 6), dim3(256), 0, s, u);
   return hipGetLastError();
 }
 

@@ -1005,7 +1005,10 @@ __global__ __launch_bounds__(kBW * 64, 2) void attn_bwd_fused_bf16_kernel(
   if (tid < 2 * kDP) bkv[tid] = kvb[head * 2 * kDP + tid];  // visible after the first barrier
   const float* bk = bkv;
   const float* bv = bkv + kDP;
-  float* acc_g = dqacc + (size_t)sh * T * kDP;
+  // the fp32 dQ accumulator rows hold only the D live dims (stride DS = D rounded to 4: 24 at the
+  // default head dim, three quarters of the padded plane's bytes per pass)
+  const int DS = (D + 3) & ~3;
+  float* acc_g = dqacc + (size_t)sh * T * DS;
   const int nkb = (T + KB - 1) / KB, nch = (T + kFQC - 1) / kFQC;
   const int b = seq / L, l = seq % L, half = D >> 1, C = H * D;
   // staging roles: image (Q / dO), row, 16-B piece; lse / delta by threads 0..127
@@ -1059,7 +1062,7 @@ __global__ __launch_bounds__(kBW * 64, 2) void attn_bwd_fused_bf16_kernel(
       const int qB = c * kFQC + 16 * bq + (lane & 15);
       const bool qlive = qB < T && dB < D;
       float4 prev = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (kb > 0 && qlive) prev = *reinterpret_cast<const float4*>(acc_g + (size_t)qB * kDP + dB);
+      if (kb > 0 && qlive) prev = *reinterpret_cast<const float4*>(acc_g + (size_t)qB * DS + dB);
       if (last && tid < kFQC) {  // the bias key's P_b, dS_b per query of the chunk
         const int q = c * kFQC + tid;
         float sb = 0.f, dpb = 0.f;
@@ -1133,7 +1136,7 @@ __global__ __launch_bounds__(kBW * 64, 2) void attn_bwd_fused_bf16_kernel(
         acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ftr16<true>(Kim, 32 * ks, 16 * bd, lane),
                                                       ftr16<false>(dsT, 32 * ks, 16 * bq, lane), acc, 0, 0, 0);
       if (!last) {
-        if (qlive) *reinterpret_cast<float4*>(acc_g + (size_t)qB * kDP + dB) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+        if (qlive) *reinterpret_cast<float4*>(acc_g + (size_t)qB * DS + dB) = make_float4(acc[0], acc[1], acc[2], acc[3]);
       } else {
         if (qlive) {
           const float dsb = dsbs[qB - c * kFQC];
