@@ -70,6 +70,8 @@ def parse():
                     help="BASELINE config 3 evidence line: the GVP training step (forward + loss + backward + "
                          "clip + Adam + EMA, the HIP block stack, graphed) at B trajectories x T frames per GPU "
                          "(use --batch 8); ranks average gradients over RCCL")
+    ap.add_argument("--no-cond-gather", action="store_true",
+                    help="--train-rccl1: bucket every gradient (no replicated conditioning, cond_dist.py)")
     ap.add_argument("--train-rccl1", action="store_true",
                     help="with --train at one GPU: a world-1 RCCL group with the gradient reduction forced on, "
                          "so the step's graph carries its per-bucket all-reduces (rehearsal of the N-GPU step)")
@@ -495,6 +497,8 @@ def train_main(a, world, rank, dev, share):
                                              world_size=1, device_id=dev)
     tr = Trainer(args, rank, world, dev)
     tr.force_allreduce = rehearse
+    if rehearse and not a.no_cond_gather:  # the replicated conditioning's all-gathers at world 1 too
+        tr.setup_cond_gather()
     batch = {k: (v.to(dev) if torch.is_tensor(v) else v) for k, v in next(iter(tr.loader)).items()}
     for _ in range(max(1, a.warmup)):
         loss, _ = tr.step([batch], log=False)
@@ -544,6 +548,8 @@ def train_main(a, world, rank, dev, share):
         out["ranks_sharing_gpu"] = world
     if rehearse:
         red = tr._graphed.reducer
+        out["replicated_conditioning_params"] = sum(p.numel() for p in tr.wrapper.model.parameters()
+                                                    if id(p) in tr.replicated)
         out["allreduce_buckets"] = {"n": len(red.buckets), "bytes": [int(sl.numel() * 4) for sl in red.slices],
                                     "launched_after_grads": [n for _, n in red.launch_log],
                                     "grads_total": sum(len(b) for b in red.buckets)}

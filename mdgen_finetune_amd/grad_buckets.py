@@ -31,8 +31,12 @@ eagerly with ``async_op`` all-reduces, which is how the world-2 CPU tests exerci
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.distributed as dist
+
+_MARK = os.environ.get("MDG_BUCKET_MARK") == "1"
 
 
 def record_grad_order(params):
@@ -83,7 +87,11 @@ def agree_order(params, order, world, group=None):
 
 
 class BucketedAllReduce:
-    def __init__(self, params, order, cap_bytes, world, group=None):
+    """tail_bytes: the LAST bucket (the gradients backward completes last, which nothing overlaps)
+    is cut further into pieces of at most this size (default cap / 4), so all but its final piece
+    leave while backward is still running."""
+
+    def __init__(self, params, order, cap_bytes, world, group=None, tail_bytes=None):
         self.params = list(params)
         self.world, self.group = world, group
         dev = self.params[0].device
@@ -100,6 +108,17 @@ class BucketedAllReduce:
             size += nb
         if cur:
             self.buckets.append(cur)
+        tail = cap_bytes // 4 if tail_bytes is None else tail_bytes
+        if self.buckets and tail > 0:
+            last, pieces, cur, size = self.buckets.pop(), [], [], 0
+            for i in last:
+                nb = self.params[i].numel() * 4
+                if cur and size + nb > tail:
+                    pieces.append(cur)
+                    cur, size = [], 0
+                cur.append(i)
+                size += nb
+            self.buckets += pieces + [cur]
         # every gradient starts on a 16-B boundary (the library optimizer's float4 path); the pad
         # elements stay zero and are reduced along with the bucket
         pad4 = lambda v: (v + 3) // 4 * 4  # noqa: E731
@@ -161,6 +180,8 @@ class BucketedAllReduce:
             ev.record(torch.cuda.current_stream(sl.device))
             self.side.wait_event(ev)
             with torch.cuda.stream(self.side):
+                if _MARK:  # profiling: a one-kernel marker per bucket in the trace (tools/rccl_overlap_trace.py)
+                    torch.cuda._sleep(1)
                 dist.all_reduce(sl, group=self.group)
                 if self.world > 1:
                     sl.div_(self.world)

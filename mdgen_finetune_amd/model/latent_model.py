@@ -118,9 +118,12 @@ class LatentMDGenLayer(nn.Module):
         self.fc2 = nn.Linear(ffn_embed_dim, embed_dim)
         self.final_layer_norm = nn.LayerNorm(embed_dim, elementwise_affine=False, eps=1e-6)
 
-    def forward(self, x, t, mask):
+    def forward(self, x, t, mask, mods=None):
+        """mods: this layer's adaLN output [B, 9C] computed elsewhere (the stacked adaLN GEMM of
+        the training path); None: adaLN_modulation(t) here, as the reference."""
         B, T, L, C = x.shape
-        (sh_l, sc_l, g_l, sh_t, sc_t, g_t, sh_m, sc_m, g_m) = self.adaLN_modulation(t).chunk(9, dim=-1)
+        m9 = self.adaLN_modulation(t) if mods is None else mods.reshape(B, 1, 9 * C)
+        (sh_l, sc_l, g_l, sh_t, sc_t, g_t, sh_m, sc_m, g_m) = m9.chunk(9, dim=-1)
         h = modulate(self.mha_layer_norm(x), sh_l, sc_l)
         h = self.mha_l(h.reshape(B * T, L, C), mask.reshape(B * T, L)).reshape(B, T, L, C)
         x = x + g_l.unsqueeze(1) * h
@@ -322,14 +325,20 @@ class LatentMDGenModel(nn.Module):
                 emb = (_SmallTableEmbedding.apply(self.mask_to_emb.weight, x_cond_mask) if torch.is_grad_enabled()
                        else self.mask_to_emb(x_cond_mask))
                 h = h + token_linear(self.cond_to_emb, x_cond) + emb
-        c = self.embed_time(t)[:, None]
         ckpt = bool(getattr(self.args, "grad_checkpointing", False)) and self.training
-        # the HIP training path: every adaLN linear of the model as one stacked GEMM
-        ada = self._stacked_adaln(c[:, 0]) if hip_layers else None
-        ipa = None
-        if self.args.prepend_ipa:
-            ipa = self.run_ipa(c[:, 0], mask[:, 0], start_frames, end_frames, aatype,
-                               ada=None if ada is None else ada[0])
+        cg = getattr(self, "_cond_gather", None)
+        if cg is not None and torch.is_grad_enabled() and not self.tps:
+            # data-parallel training: the conditioning on the ranks' global batch, local rows kept
+            # (cond_dist.CondGather: its parameters' gradients come out rank-averaged)
+            c, ada, ipa = self._replicated_conditioning(cg, t, mask, start_frames, aatype)
+        else:
+            c = self.embed_time(t)[:, None]
+            # the HIP training path: every adaLN linear of the model as one stacked GEMM
+            ada = self._stacked_adaln(c[:, 0]) if hip_layers else None
+            ipa = None
+            if self.args.prepend_ipa:
+                ipa = self.run_ipa(c[:, 0], mask[:, 0], start_frames, end_frames, aatype,
+                                   ada=None if ada is None else ada[0])
         if hip_layers:
             from ..train_hip import hip_embed, hip_final, hip_layer_forward
             hl = self._train_helper()
@@ -346,12 +355,41 @@ class LatentMDGenModel(nn.Module):
             elif hip_layers:  # block forward + backward in libmdgen_hip.so (train_hip.py)
                 h = hip_layer_forward(hl, layer, h, ada[1][k], mask)
             elif getattr(self.args, "grad_checkpointing", False) and self.training:
-                h = torch.utils.checkpoint.checkpoint(layer, h, c, mask, use_reentrant=False)
+                h = torch.utils.checkpoint.checkpoint(layer, h, c, mask, None if ada is None else ada[1][k],
+                                                      use_reentrant=False)
             else:
-                h = layer(h, c, mask)
+                h = layer(h, c, mask, mods=None if ada is None else ada[1][k])
         if glue:
             return hip_final(hl, self.emb_to_latent, h, ada[2])
         return self.emb_to_latent(h, c, mods=None if ada is None else ada[2][:, None])
+
+    def _replicated_conditioning(self, cg, t, mask, start_frames, aatype):
+        """(c [B,1,C], (IPA mods, block mods, final mods), ipa [B,L,C]) of this rank's samples,
+        computed on the all-gathered batch of every rank (cond_dist.py)."""
+        B, L = mask.shape[0], mask.shape[2]
+        C = self.args.embed_dim
+        rots, trans = frames_to_tensors(start_frames, mask.device)
+        if rots is None:
+            rots = torch.eye(3, device=mask.device).expand(B, L, 3, 3)
+            trans = torch.zeros(B, L, 3, device=mask.device)
+        t_g, mask_g, rots_g, trans_g, aa_g = cg.gather_inputs(t, mask[:, 0], rots, trans, aatype)
+        W = t_g.shape[0]
+        c_g = self.embed_time(t_g)
+        ada_g = self._stacked_adaln(c_g)
+        pieces = [c_g] + list(ada_g[1]) + [ada_g[2]]
+        if self.args.prepend_ipa:
+            fr = torch.zeros(W, L, 4, 4, device=mask.device)
+            fr[..., :3, :3] = rots_g
+            fr[..., :3, 3] = trans_g
+            fr[..., 3, 3] = 1.0
+            ipa_g = self.run_ipa(c_g, mask_g, fr, None, aa_g, ada=ada_g[0])
+            pieces.append(ipa_g.reshape(W, L * C))
+        loc = torch.split(cg.local(torch.cat(pieces, -1)), [p.shape[-1] for p in pieces], -1)
+        nl = len(self.layers)
+        c = loc[0][:, None]
+        ada = (None, list(loc[1:1 + nl]), loc[1 + nl])
+        ipa = loc[2 + nl].reshape(B, L, C) if self.args.prepend_ipa else None
+        return c, ada, ipa
 
     def _stacked_adaln(self, c0):
         """Every adaLN linear (IPA layers 6C, blocks 9C, FinalLayer 2C: latent_model.py:341-493,

@@ -64,6 +64,10 @@ _EXTRA = [
     ("train_graph", _I, 1, "1: on a ROCm device the optimizer step replays hipGraphs (forward + loss + "
                            "backward [+ RCCL gradient all-reduce between two graphs] + clip + Adam + EMA); "
                            "0: eager step (also used for grad accumulation > 1 and 16-mixed)"),
+    ("cond_allgather", _I, 1, "data-parallel training (world > 1): 1 = the conditioning (t-MLP, adaLN, IPA "
+                              "prepend) runs on the all-gathered batch of every rank and its parameters' "
+                              "gradients come out rank-averaged, so they leave the gradient all-reduce "
+                              "(cond_dist.py); 0 = every gradient all-reduced"),
     ("allreduce_overlap", _I, 1, "graphed step with world > 1 over RCCL: 1 = per-bucket all-reduces captured "
                                  "in the graph on a side stream, each issued as backward completes its bucket "
                                  "(--bucket_cap_mb); 0 = one flat all-reduce between two graphs"),

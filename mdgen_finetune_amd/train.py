@@ -104,6 +104,11 @@ class Trainer:
                                and m.backend == "hip" and self.scaler is None and max(1, args.accumulate_grad) == 1)
         self._graphed = None
         self.model = self.wrapper.model
+        # the conditioning on the ranks' global batch (cond_dist.py): its collectives must be capturable
+        # in graph mode (RCCL; gloo's graphed path keeps every gradient in the flat all-reduce)
+        self.replicated = set()
+        if world > 1 and int(getattr(args, "cond_allgather", 1)):
+            self.setup_cond_gather()
         if world > 1 and not self.graph_mode:
             self.model = DDP(self.wrapper.model, device_ids=[self.device.index] if self.device.type == "cuda" else None,
                              bucket_cap_mb=args.bucket_cap_mb, gradient_as_bucket_view=True, static_graph=True)
@@ -137,6 +142,22 @@ class Trainer:
                                                           num_workers=0, collate_fn=collate)
         if args.ckpt:
             self.resume(args.ckpt)
+
+    def setup_cond_gather(self):
+        """Run the conditioning on the ranks' global batch (cond_dist.py) and take its parameters
+        out of the gradient all-reduce.  Graph mode needs capturable collectives (RCCL); TPS
+        keeps the all-reduce.  (Also called at world 1 for the RCCL capture rehearsal.)"""
+        m = self.wrapper.model
+        if m.tps or (self.graph_mode and not (dist.is_initialized() and dist.get_backend() == "nccl")):
+            return False
+        from .cond_dist import CondGather, replicated_params
+
+        m._cond_gather = CondGather(self.world, self.rank)
+        names = replicated_params(m)
+        self.replicated = {id(p) for n, p in m.named_parameters() if n in names}
+        if not self.graph_mode and self.world > 1:  # DDP leaves them alone (they arrive averaged)
+            DDP._set_params_and_buffers_to_ignore_for_model(m, names)
+        return True
 
     # ------------------------------------------------------------------ checkpoint
     def resume(self, path):
@@ -187,7 +208,8 @@ class Trainer:
         all-reduce of the flat fp32 buffer (RCCL over xGMI; gloo on CPU)."""
         if self.world == 1:
             return
-        params = [p for p in self.wrapper.model.parameters() if p.requires_grad]
+        # (parameters averaged by the replicated conditioning stay out of the all-reduce)
+        params = [p for p in self.wrapper.model.parameters() if p.requires_grad and id(p) not in self.replicated]
         own = flat is None
         if own:
             flat = torch.cat([(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1) for p in params])
@@ -385,6 +407,8 @@ class GraphedStep:
                     unhook()
         unhook()
         if self.overlap:
+            # parameters the replicated conditioning averages already (cond_dist.py) are not bucketed
+            order = [i for i in order if id(self.params[i]) not in tr.replicated]
             self.reducer = BucketedAllReduce(self.params, order, int(tr.args.bucket_cap_mb * 2 ** 20), tr.world)
             with torch.cuda.stream(side):  # the communicator exists before the capture
                 dist.all_reduce(torch.zeros(1, device=dev))

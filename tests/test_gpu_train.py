@@ -571,21 +571,27 @@ def _rccl_world1_worker(rank, port, out):
                             device_id=torch.device("cuda", 0))
     res = {}
     info = {}
-    for mode in ("plain", "rccl"):
+    from mdgen_finetune_amd import synthetic
+
+    for mode in ("plain", "rccl", "rccl_cg"):
         a = _args(["--lr", "1e-3", "--embed_dim", "192", "--mha_heads", "8", "--ema", "--train_graph", "1",
                    "--bucket_cap_mb", "0.5"])
         tr = Trainer(a, device=torch.device("cuda"))
-        tr.force_allreduce = mode == "rccl"
+        synthetic.fill_module_(tr.wrapper.model, 23)  # gradients reach every parameter
+        tr.force_allreduce = mode != "plain"
+        if mode == "rccl_cg":  # + the replicated conditioning's all-gathers (cond_dist.py) in the capture
+            assert tr.setup_cond_gather()
         b = _batch(a, B=2)
         _fixed_noise(tr, 2, (2, a.num_frames, a.crop, 21))
         losses = [float(tr.step([b], log=False)[0]) for _ in range(2)]
         g = tr._graphed
-        if mode == "rccl":
+        if mode != "plain":
             red = g.reducer
-            info = {"overlap": bool(g.overlap), "has_g2": hasattr(g, "g2"), "buckets": len(red.buckets),
-                    "log": list(red.launch_log), "grads": sum(len(bk) for bk in red.buckets),
-                    "views": all(p.grad is None or p.grad.data_ptr() == red.views[i].data_ptr()
-                                 for i, p in enumerate(g.params) if i in red.views)}
+            info[mode] = {"overlap": bool(g.overlap), "has_g2": hasattr(g, "g2"), "buckets": len(red.buckets),
+                          "log": list(red.launch_log), "grads": sum(len(bk) for bk in red.buckets),
+                          "replicated": len(tr.replicated),
+                          "views": all(p.grad is None or p.grad.data_ptr() == red.views[i].data_ptr()
+                                       for i, p in enumerate(g.params) if i in red.views)}
         st = _trainer_state(tr)
         res[mode] = (losses, [t.cpu() for t in st])
         torch.cuda.synchronize()
@@ -617,15 +623,21 @@ def test_graphed_step_rccl_bucket_allreduce_in_capture_world1():
     mgr = mp.Manager()
     out = mgr.dict()
     mp.spawn(_rccl_world1_worker, args=(port, out), nprocs=1, join=True)
-    info = out["info"]
     assert out.get("teardown") == "ok"
-    assert info["overlap"] and not info["has_g2"], info
-    assert info["buckets"] >= 3, info
-    assert [bi for bi, _ in info["log"]] == list(range(info["buckets"])), info
-    assert info["log"][0][1] < info["grads"], info
-    assert info["views"]
-    (l0, s0), (l1, s1) = out["res"]["plain"], out["res"]["rccl"]
-    assert l0 == l1, (l0, l1)
-    for i, what in enumerate(("params", "ema", "adam")):
-        d = float((s0[i] - s1[i]).abs().max())
-        assert d <= 1e-6 * max(1.0, float(s0[i].abs().max())), (what, d)
+    for mode in ("rccl", "rccl_cg"):
+        info = out["info"][mode]
+        assert info["overlap"] and not info["has_g2"], info
+        assert info["buckets"] >= 3, info
+        assert [bi for bi, _ in info["log"]] == list(range(info["buckets"])), info
+        assert info["log"][0][1] < info["grads"], info
+        assert info["views"]
+    # the replicated conditioning's parameters leave the buckets
+    assert out["info"]["rccl_cg"]["replicated"] > 20
+    assert out["info"]["rccl_cg"]["grads"] + out["info"]["rccl_cg"]["replicated"] == out["info"]["rccl"]["grads"]
+    (l0, s0) = out["res"]["plain"]
+    for mode in ("rccl", "rccl_cg"):
+        l1, s1 = out["res"][mode]
+        assert l0 == l1, (mode, l0, l1)
+        for i, what in enumerate(("params", "ema", "adam")):
+            d = float((s0[i] - s1[i]).abs().max())
+            assert d <= 1e-6 * max(1.0, float(s0[i].abs().max())), (mode, what, d)

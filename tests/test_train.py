@@ -137,10 +137,13 @@ def _ddp_worker(rank, world, port, out):
     torch.set_num_threads(1)
     from mdgen_finetune_amd.train import Trainer, setup_distributed
 
+    from mdgen_finetune_amd import synthetic
+
     r, w, dev = setup_distributed()
     dist._DEFAULT_FIRST_BUCKET_BYTES = 50 * 1024  # DDP's first bucket would hold this whole small model
-    a = _args(["--grad_clip", "0", "--bucket_cap_mb", "0.05"])
+    a = _args(["--grad_clip", "0", "--bucket_cap_mb", "0.05", "--cond_allgather", "0"])
     tr = Trainer(a, r, w, dev)
+    synthetic.fill_module_(tr.wrapper.model, 21)  # non-zero gradients everywhere (zero-init layers pass none)
     b = _batch(a, B=2, seed=100 + rank)
     # local gradient without communication, from the same (t, x0) draw
     g = torch.Generator().manual_seed(7 + rank)
@@ -218,10 +221,13 @@ def _bucket_worker(rank, world, port, out):
     from mdgen_finetune_amd.grad_buckets import BucketedAllReduce, record_grad_order
     from mdgen_finetune_amd.train import Trainer, setup_distributed
 
+    from mdgen_finetune_amd import synthetic
+
     r, w, dev = setup_distributed()
-    a = _args(["--grad_clip", "0"])
+    a = _args(["--grad_clip", "0", "--cond_allgather", "0"])
     tr = Trainer(a, r, w, dev)
     m = tr.wrapper.model
+    synthetic.fill_module_(m, 21)  # non-zero gradients everywhere
     params = [p for p in m.parameters() if p.requires_grad]
     b = _batch(a, B=2, seed=100 + rank)
     g = torch.Generator().manual_seed(7 + rank)
@@ -349,6 +355,75 @@ def test_bucket_layout_agreed_across_ranks_world2_gloo():
         assert r["err"] <= 1e-6, r["err"]
         assert "fired twice" in r["dup"], r["dup"]
         assert "different set of gradients" in r["mismatch"], r["mismatch"]
+
+
+def _cond_gather_worker(rank, world, port, out):
+    """Replicated conditioning (cond_dist.py) under DDP, world 2 over gloo: every parameter's
+    averaged gradient — the conditioning's from the all-gathered batch, the rest from DDP's
+    all-reduce — equals the single-process gradient of the mean loss over both ranks' batches."""
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from mdgen_finetune_amd.data import collate
+    from mdgen_finetune_amd.train import Trainer, setup_distributed
+
+    from mdgen_finetune_amd import synthetic
+
+    r, w, dev = setup_distributed()
+    dist._DEFAULT_FIRST_BUCKET_BYTES = 50 * 1024
+    a = _args(["--grad_clip", "0", "--bucket_cap_mb", "0.05"])
+    tr = Trainer(a, r, w, dev)
+    m = tr.wrapper.model
+    # non-zero weights everywhere (a fresh model's zero-init adaLN / final layers pass no gradient
+    # to anything upstream); DDP broadcast the old values at wrap time, so fill on every rank alike
+    synthetic.fill_module_(m, 21)
+    assert m._cond_gather is not None and len(tr.replicated) > 0
+    batches = [_batch(a, B=2, seed=100 + k) for k in range(w)]
+    noise = []
+    for k in range(w):
+        g = torch.Generator().manual_seed(7 + k)
+        noise.append((torch.rand(2, generator=g), torch.randn(2, 8, 4, 21, generator=g)))
+    t, x0 = noise[rank]
+    tr.wrapper.transport.sample = lambda x1: (t, x0, x1)
+    for _ in range(3):  # DDP buckets from its third iteration (static graph); measure the last
+        tr.optimizer.zero_grad(set_to_none=True)
+        tr.wrapper.general_step(batches[rank], model=tr.model).backward()
+    got = {n: p.grad.detach().clone() for n, p in m.named_parameters() if p.grad is not None}
+    # single-process reference: a fresh trainer (same seed = same weights), no gather, both batches
+    a1 = _args(["--grad_clip", "0"])
+    ref = Trainer(a1)
+    rm = ref.wrapper.model
+    synthetic.fill_module_(rm, 21)
+    tt = torch.cat([n_[0] for n_ in noise])
+    xx = torch.cat([n_[1] for n_ in noise])
+    ref.wrapper.transport.sample = lambda x1: (tt, xx, x1)
+    big = collate([{k: v[i] if torch.is_tensor(v) else v[i] for k, v in b.items()} for b in batches for i in range(2)])
+    ref.wrapper.general_step(big, model=rm).backward()
+    want = {n: p.grad for n, p in rm.named_parameters() if p.grad is not None}
+    rep = {n for n, p in m.named_parameters() if id(p) in tr.replicated}
+    worst, worst_rep = 0.0, 0.0
+    nonzero = sum(1 for n in rep if n in want and float(want[n].abs().max()) > 0)
+    assert nonzero > 20, nonzero
+    for n, g in want.items():
+        e = float((got[n] - g).abs().max()) / max(1e-12, float(g.abs().max()))
+        worst = max(worst, e)
+        if n in rep:
+            worst_rep = max(worst_rep, e)
+    out[rank] = (worst, worst_rep, len(rep), len(want), sorted(set(want) - set(got)))
+    dist.destroy_process_group()
+
+
+def test_replicated_conditioning_world2_gloo_equals_big_batch():
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_cond_gather_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    for r in range(2):
+        worst, worst_rep, n_rep, n_all, missing = out[r]
+        assert not missing, missing
+        assert n_rep > 20 and n_all > n_rep
+        assert worst <= 1e-4, (r, worst, worst_rep)
 
 
 def _bench_worker(rank, world, port, out):

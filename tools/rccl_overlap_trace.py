@@ -2,7 +2,8 @@
 step with its per-bucket RCCL all-reduces captured in the graph): for every collective kernel of
 the last replayed steps, when it started within the step, how long it ran, which library kernels
 ran concurrently with it (overlap with backward) and how many kernels of the step started after
-it.  Usage: python tools/rccl_overlap_trace.py <kernel_trace.csv> <buckets per step> [out.md]"""
+it.  Usage: python tools/rccl_overlap_trace.py <kernel_trace.csv> <buckets per step> [out.md]
+[bucket bytes, comma-separated: a world-1 trace with MDG_BUCKET_MARK=1 markers]"""
 import csv
 import re
 import sys
@@ -18,6 +19,8 @@ def main():
     rows.sort()
     is_coll = [("nccl" in n.lower() or "rccl" in n.lower()) for _, _, n in rows]
     coll = [i for i, c in enumerate(is_coll) if c]
+    if len(sys.argv) > 4:  # bucket sizes (bytes, comma-separated): the marked world-1 trace
+        return world1_marked(path, rows, nb, out, [int(x) for x in sys.argv[4].split(",")])
     if len(coll) < nb:
         # world 1: RCCL elides a one-rank all-reduce (no collective kernel); the bucket's packing
         # `cat`, issued by the same hook on the same branch right before the collective, marks when
@@ -44,6 +47,36 @@ def main():
             lines.append(f"| {b} | {(st - t0) / 1e3:.1f} | {(en - st) / 1e3:.1f} | {len(conc)} | {after} | "
                          f"{', '.join(ex)} |")
         lines.append("")
+    txt = "\n".join(lines)
+    print(txt)
+    if out:
+        with open(out, "w") as f:
+            f.write(txt + "\n")
+
+
+def world1_marked(path, rows, nb, out, sizes):
+    """MDG_BUCKET_MARK=1 trace: one spin marker kernel per bucket, issued on the side branch right
+    before the bucket's all-reduce; with the bucket sizes (bench JSON) this gives the bytes that
+    leave backward in its last 0.5 ms (the part of the exchange nothing overlaps)."""
+    marks = [i for i, (_, _, n) in enumerate(rows) if "prep_latents" in n]
+    lo, hi = marks[-2], marks[-1]
+    t0 = rows[lo][0]
+    spins = [i for i in range(lo, hi) if "spin" in rows[i][2].lower()]
+    bwd_end = max((rows[i][1] for i in range(lo, hi) if ("bwd" in rows[i][2] or "wgrad" in rows[i][2]
+                                                         or "unpack" in rows[i][2])), default=rows[hi - 1][1])
+    lines = [f"# In-graph bucket all-reduces, world-1 rehearsal with bucket markers ({path.split('/')[-1]})", "",
+             f"Last complete step {(rows[hi - 1][1] - t0) / 1e3:.1f} us; backward's last kernel ends "
+             f"{(bwd_end - t0) / 1e3:.1f} us into it; {len(spins)} bucket markers ({nb} buckets).", "",
+             "| bucket | MB | leaves backward at (us into step) | backward left after it (us) |", "|---|---|---|---|"]
+    tail = 0.0
+    for b, i in enumerate(spins):
+        st = rows[i][0]
+        left = (bwd_end - st) / 1e3
+        mb = sizes[b] / 1e6 if b < len(sizes) else float("nan")
+        if left <= 500.0:
+            tail += mb
+        lines.append(f"| {b} | {mb:.2f} | {(st - t0) / 1e3:.1f} | {left:.1f} |")
+    lines += ["", f"**{tail:.2f} MB leave backward in its last 0.5 ms** (of {sum(sizes) / 1e6:.1f} MB bucketed)."]
     txt = "\n".join(lines)
     print(txt)
     if out:
