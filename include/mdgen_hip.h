@@ -389,6 +389,15 @@ typedef struct {
   int32_t skip_temporal; /* nonzero: the temporal sublayer is left out (h2 = h1; the IPA layers'
                             MHA + MLP tail on this block, latent_model.py:341-394, whose temporal
                             gate is 0): qkv_t / lse_t / o[1] / y[1] / h2 are not written */
+  /* Layer-to-layer LayerNorm hand-off (ABI 22): */
+  int32_t xn0_given;     /* nonzero: xn[0] / stats[0] already hold LN_s(h_in) (the previous layer's
+                            fc2 produced them); the first LayerNorm pass is skipped */
+  void* xn_next;         /* non-null: also write the NEXT layer's LN_s(h_out) modulated by mods_next
+                            (shift at 0, scale at C of its [B][9C] rows) to xn_next (CT [N][C]) and its
+                            row statistics to stats_next ([N][2]) — fused into fc2's row-LN epilogue
+                            where the bf16 row-LN GEMM takes the shape */
+  float* stats_next;
+  const float* mods_next;
 } mdg_layer_saved;
 
 /* Key-padding biases from mask [B,T,L] (0 -> -inf): temporal [B*L][T], spatial [B*T][L]. */

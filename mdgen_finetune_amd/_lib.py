@@ -79,7 +79,8 @@ class MdgGemmDesc(ctypes.Structure):
 class MdgLayerSaved(ctypes.Structure):
     _fields_ = [("xn", _vp * 3), ("stats", _vp * 3), ("qkv_s", _vp), ("lse_s", _vp), ("qkv_t", _vp),
                 ("lse_t", _vp), ("o", _vp * 2), ("o_lo", _vp * 2), ("y", _vp * 3), ("h1", _vp), ("h2", _vp), ("u", _vp), ("act", _vp),
-                ("init_planes", _i32), ("skip_temporal", _i32)]
+                ("init_planes", _i32), ("skip_temporal", _i32),
+                ("xn0_given", _i32), ("xn_next", _vp), ("stats_next", _vp), ("mods_next", _vp)]
 
 
 class MdgCondDims(ctypes.Structure):

@@ -926,7 +926,8 @@ int mdg_layer_fwd_train(const mdg_dims* d, const mdg_layer_weights* w, const flo
   g.H = H; g.D = D; g.T = T; g.L = L;
 
   // ---- spatial sublayer (latent_model.py:466-472)
-  if (int e = ln(h_in, 0, 0, C)) return e;
+  if (!sv->xn0_given)
+    if (int e = ln(h_in, 0, 0, C)) return e;
   mdg_gemm_desc q = g;
   q.epi = MDG_EPI_QKV; q.N = 3 * C; q.K = C; q.A = sv->xn[0]; q.lda = C; q.W = w->wqkv[0]; q.ldw = C;
   q.bias = w->bqkv[0]; q.rope = rope_l; q.rope_rows = L + 1;
@@ -997,7 +998,18 @@ int mdg_layer_fwd_train(const mdg_dims* d, const mdg_layer_weights* w, const flo
   f2.epi = MDG_EPI_GATE_RES; f2.N = C; f2.K = F; f2.A = sv->act; f2.lda = F; f2.W = w->w2; f2.ldw = F; f2.bias = w->b2;
   f2.resid_in = h_mlp; f2.resid = h_out; f2.ldr = C; f2.gate = mods; f2.gate_off = 8 * C; f2.aux = sv->y[2];
   f2.ldaux = C;
-  return mdg_gemm(&f2, stream);
+  if (!sv->xn_next) return mdg_gemm(&f2, stream);
+  if (!sv->stats_next || !sv->mods_next) return fail(MDG_E_ARG, "layer_fwd_train: xn_next without stats / mods");
+  // the next layer's first LayerNorm (LN_s with its adaLN rows) in fc2's row-LN epilogue, or after it
+  if (train_rowln_on()) {
+    mdg_gemm_desc f = f2;
+    f.xn_out = sv->xn_next; f.xn_mods = sv->mods_next; f.xn_mod_stride = ms; f.xn_shift_off = 0;
+    f.xn_scale_off = C; f.ln_eps = 1e-6f; f.ln_stats = sv->stats_next;
+    if (mdg::gemm_plan(f).cfg == kCfgRowTrainId) return mdg_gemm(&f, stream);
+  }
+  if (int e = mdg_gemm(&f2, stream)) return e;
+  return hip_check(mdg::ln_mod_launch(d->dtype, N, C, h_out, sv->mods_next, ms, TL, 0, C, 1e-6f, sv->xn_next, s,
+                                      sv->stats_next), "ln_mod(next)");
 }
 
 int32_t mdg_ln_gate_bwd_blocks(int32_t rows_per_b) { return rows_per_b > 0 ? mdg::ln_gate_bwd_blocks(rows_per_b) : 0; }

@@ -340,8 +340,9 @@ class LatentMDGenModel(nn.Module):
                 ipa = self.run_ipa(c[:, 0], mask[:, 0], start_frames, end_frames, aatype,
                                    ada=None if ada is None else ada[0])
         if hip_layers:
-            from ..train_hip import hip_embed, hip_final, hip_layer_forward
+            from ..train_hip import hip_embed, hip_final, hip_layer_forward, hip_layer_forward_chain
             hl = self._train_helper()
+        pre = None
         if glue:
             h = hip_embed(hl, self, x, x_cond, x_cond_mask, ipa)
         elif ipa is not None:
@@ -352,8 +353,10 @@ class LatentMDGenModel(nn.Module):
                 # saved activations of every layer but the one being differentiated are freed)
                 h = torch.utils.checkpoint.checkpoint(hip_layer_forward, hl, layer, h, ada[1][k], mask,
                                                       use_reentrant=True)
-            elif hip_layers:  # block forward + backward in libmdgen_hip.so (train_hip.py)
-                h = hip_layer_forward(hl, layer, h, ada[1][k], mask)
+            elif hip_layers:  # block forward + backward in libmdgen_hip.so (train_hip.py); each layer's
+                # fc2 also writes the next layer's first LayerNorm (the hand-off, no separate pass)
+                nxt = ada[1][k + 1] if k + 1 < len(self.layers) else None
+                h, pre = hip_layer_forward_chain(hl, layer, h, ada[1][k], mask, next_mods=nxt, pre=pre)
             elif getattr(self.args, "grad_checkpointing", False) and self.training:
                 h = torch.utils.checkpoint.checkpoint(layer, h, c, mask, None if ada is None else ada[1][k],
                                                       use_reentrant=False)

@@ -207,7 +207,20 @@ def hip_layer_forward(hl, layer, h, mods, mask):
     """h [B,T,L,C] fp32, mods [B, 9C] (adaLN output), mask [B,T,L] -> layer(h) through the
     HIP training Function."""
     inv_freq = layer.mha_l.attn.rot_emb.inv_freq if hl.rope else None
-    return _HipLayerFn.apply(h, mods, mask, hl, inv_freq, False, *_layer_params(layer))
+    return _HipLayerFn.apply(h, mods, mask, hl, inv_freq, False, None, *_layer_params(layer))
+
+
+def hip_layer_forward_chain(hl, layer, h, mods, mask, next_mods=None, pre=None):
+    """hip_layer_forward with the layer-to-layer LayerNorm hand-off: the layer's fc2 also writes
+    the NEXT layer's first LayerNorm + modulate (next_mods = that layer's adaLN rows [B, 9C]) and
+    its row statistics, which the next call takes as ``pre`` instead of running its own pass
+    (mdg_layer_saved.xn_next / xn0_given).  Returns (h_out, pre for the next layer or None)."""
+    inv_freq = layer.mha_l.attn.rot_emb.inv_freq if hl.rope else None
+    chain = (None if next_mods is None else next_mods.detach(), pre)
+    out = _HipLayerFn.apply(h, mods, mask, hl, inv_freq, False, chain, *_layer_params(layer))
+    if next_mods is None:
+        return out, None
+    return out[0], (out[1], out[2])
 
 
 def hip_ipa_layer_tail(hl, layer, x1, mods6, mask_b):
@@ -225,13 +238,15 @@ def hip_ipa_layer_tail(hl, layer, x1, mods6, mask_b):
     att = [mha.q_proj.weight, mha.q_proj.bias, mha.k_proj.weight, mha.k_proj.bias, mha.v_proj.weight, mha.v_proj.bias,
            mha.out_proj.weight, mha.out_proj.bias, mha.bias_k, mha.bias_v]
     params = att + att + [layer.fc1.weight, layer.fc1.bias, layer.fc2.weight, layer.fc2.bias]
-    out = _HipLayerFn.apply(x1[:, None], mods9, mask_b[:, None], hl, inv_freq, True, *params)
+    out = _HipLayerFn.apply(x1[:, None], mods9, mask_b[:, None], hl, inv_freq, True, None, *params)
     return out[:, 0]
 
 
 class _HipLayerFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, h, mods, mask, hl, inv_freq, tail, *params):
+    def forward(ctx, h, mods, mask, hl, inv_freq, tail, chain, *params):
+        """chain: None, or (next_mods [B, 9C] detached | None, pre (xn0, stats0) | None): the
+        layer-to-layer LayerNorm hand-off of hip_layer_forward_chain."""
         lib = hl.lib
         B, T, L, C = h.shape
         H, D, F, ct = hl.H, hl.D, hl.F, hl.ct
@@ -288,6 +303,7 @@ class _HipLayerFn(torch.autograd.Function):
         planes_t, fresh_t = hl.planes(("t", params[0].data_ptr(), B, T, L), (3, B * L, H, T, _lib.MDG_DP), dev, lease)
         planes_s, fresh_s = (hl.planes(("s", params[0].data_ptr(), B, T, L), (3, B * T, H, L, _lib.MDG_DP), dev,
                                        lease) if long_l else (e(N, 3 * C), False))
+        next_mods, pre = chain if chain is not None else (None, None)
         sv = {"xn": [r(C) for _ in range(3)], "stats": [e(N, 2, dt=torch.float32) for _ in range(3)],
               "qkv_s": planes_s,
               "lse_s": e(B * T, H, L, dt=torch.float32) if long_l else None,
@@ -297,7 +313,16 @@ class _HipLayerFn(torch.autograd.Function):
               "o_lo": [e(N, C) if (ct == torch.bfloat16 and long_l) else None,
                        e(N, C) if ct == torch.bfloat16 else None],
               "h1": e(N, C, dt=torch.float32), "h2": e(N, C, dt=torch.float32), "u": e(N, F), "act": r(F)}
+        if pre is not None:  # LN_s(h) from the previous layer's fc2 epilogue
+            sv["xn"][0], sv["stats"][0] = pre
+        nxt = None
+        if next_mods is not None:
+            nxt = (r(C), e(N, 2, dt=torch.float32))
+            next_mods = next_mods.contiguous().float()
         cs = _lib.MdgLayerSaved()
+        cs.xn0_given = int(pre is not None)
+        if nxt is not None:
+            cs.xn_next, cs.stats_next, cs.mods_next = nxt[0].data_ptr(), nxt[1].data_ptr(), next_mods.data_ptr()
         for i in range(3):
             cs.xn[i], cs.stats[i], cs.y[i] = sv["xn"][i].data_ptr(), sv["stats"][i].data_ptr(), sv["y"][i].data_ptr()
         cs.qkv_s, cs.lse_s = sv["qkv_s"].data_ptr(), _lib.ptr(sv["lse_s"])
@@ -319,10 +344,13 @@ class _HipLayerFn(torch.autograd.Function):
         ctx.rope = (rope_l, rope_t)
         ctx.inv_freq = inv_freq
         ctx.save_for_backward(h, mods)
-        return h_out
+        if nxt is None:
+            return h_out
+        ctx.mark_non_differentiable(nxt[0], nxt[1])
+        return h_out, nxt[0], nxt[1]
 
     @staticmethod
-    def backward(ctx, dh3):
+    def backward(ctx, dh3, *_next_grads):  # (the hand-off outputs are non-differentiable)
         hl, sv, P = ctx.hl, ctx.sv, ctx.P
         lib = hl.lib
         h, mods = ctx.saved_tensors
@@ -452,7 +480,7 @@ class _HipLayerFn(torch.autograd.Function):
         if ctx.tail:  # the zero-gate temporal stand-ins: exactly zero, nothing to accumulate
             out[10:20] = [None] * 10
         del ctx.sv, ctx.P, ctx.lease  # the planes go back to the layer's pool
-        return (dh0.reshape(B, T, L, C), dmods, None, None, None, None, *out)
+        return (dh0.reshape(B, T, L, C), dmods, None, None, None, None, None, *out)
 
 
 # ------------------------------------------------------------------------------------------
