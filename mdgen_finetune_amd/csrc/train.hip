@@ -1014,24 +1014,21 @@ __global__ __launch_bounds__(kBW * 64, 2) void attn_bwd_fused_bf16_kernel(
   // staging roles: image (Q / dO), row, 16-B piece; lse / delta by threads 0..127
   const int simg = tid >> 8, srow = (tid >> 2) & (kFQC - 1), spc = tid & 3;
   const bf16_t* sg = simg ? dOg : Qg;
-  // register staging TWO chunks ahead (sreg: chunk c + 1, stored at the end of chunk c's phase A;
-  // sreg2: chunk c + 2, loaded at the start of chunk c): a chunk's loads get two chunk times to
-  // land instead of one phase A (HBM latency under load outlasted it)
-  u32x4 sreg, sreg2 = u32x4{0u, 0u, 0u, 0u};
-  float lreg = 0.f, lreg2 = 0.f;
-  auto gload = [&](int c, u32x4& sr, float& lr) {
+  u32x4 sreg;
+  float lreg = 0.f;
+  auto gload = [&](int c) {
     const int qq = c * kFQC + srow;
-    sr = u32x4{0u, 0u, 0u, 0u};
-    if (qq < T) sr = *reinterpret_cast<const u32x4*>(sg + (size_t)qq * kDP + spc * 8);
+    sreg = u32x4{0u, 0u, 0u, 0u};
+    if (qq < T) sreg = *reinterpret_cast<const u32x4*>(sg + (size_t)qq * kDP + spc * 8);
     if (tid < 2 * kFQC) {
       const int q2 = c * kFQC + (tid & (kFQC - 1));
-      lr = tid < kFQC ? (q2 < T ? lg[q2] : INFINITY) : (q2 < T ? dg[q2] : 0.f);
+      lreg = tid < kFQC ? (q2 < T ? lg[q2] : INFINITY) : (q2 < T ? dg[q2] : 0.f);
     }
   };
-  auto lstore = [&](int buf, const u32x4& sr, float lr) {
-    *reinterpret_cast<u32x4*>(&(simg ? Ds : Qs)[buf][img_off(srow, spc * 8)]) = sr;
-    if (tid < kFQC) ls[buf][tid] = lr;
-    else if (tid < 2 * kFQC) dls[buf][tid - kFQC] = lr;
+  auto lstore = [&](int buf) {
+    *reinterpret_cast<u32x4*>(&(simg ? Ds : Qs)[buf][img_off(srow, spc * 8)]) = sreg;
+    if (tid < kFQC) ls[buf][tid] = lreg;
+    else if (tid < 2 * kFQC) dls[buf][tid - kFQC] = lreg;
   };
   // phase-B tile of this wave: dims 16 bd .. +15, queries 16 bq .. +15 of the chunk; the lane
   // holds dims dB .. dB+3 of query column (lane & 15)
@@ -1056,13 +1053,12 @@ __global__ __launch_bounds__(kBW * 64, 2) void attn_bwd_fused_bf16_kernel(
     f32x16 dk, dv;
 #pragma unroll
     for (int i = 0; i < 16; ++i) dk[i] = dv[i] = 0.f;
-    gload(0, sreg, lreg);
-    lstore(0, sreg, lreg);
-    if (nch > 1) gload(1, sreg, lreg);
+    gload(0);
+    lstore(0);
     __syncthreads();
     for (int c = 0; c < nch; ++c) {
       const int cur = c & 1;
-      if (c + 2 < nch) gload(c + 2, sreg2, lreg2);
+      if (c + 1 < nch) gload(c + 1);
       const int qB = c * kFQC + 16 * bq + (lane & 15);
       const bool qlive = qB < T && dB < D;
       float4 prev = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1131,9 +1127,7 @@ __global__ __launch_bounds__(kBW * 64, 2) void attn_bwd_fused_bf16_kernel(
           *reinterpret_cast<bf16x4*>(&dsT[fds_off(wave * 32 + r, base + 16 * s2 + 8 + 4 * h)]) = hi;
         }
       }
-      if (c + 1 < nch) lstore(cur ^ 1, sreg, lreg);
-      sreg = sreg2;
-      lreg = lreg2;
+      if (c + 1 < nch) lstore(cur ^ 1);
       __syncthreads();
       // phase B: dQ^T (dims dB.., query qB) += K^T dS^T over the block's 256 keys
       f32x4 acc = {prev.x, prev.y, prev.z, prev.w};
