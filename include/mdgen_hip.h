@@ -220,6 +220,13 @@ int mdg_mlp_fused(const mdg_gemm_desc* fc1, const mdg_gemm_desc* fc2, void* stre
    mdg_gemm(out_proj) then mdg_gemm(qkv).  bf16, C == 384, head_dim % 8 == 0 and <= 48,
    out_proj.rows_per_mod >= 128, no training outputs; MDG_E_SHAPE otherwise. */
 int mdg_rowln_qkv(const mdg_gemm_desc* out_proj, const mdg_gemm_desc* qkv, void* stream);
+/* The temporal attention's out_proj + gated residual + the MLP LayerNorm, then the MLP, as ONE
+   kernel (latent_model.py:486-491; round 5): the descriptors exactly as for mdg_gemm(out_proj)
+   then mdg_mlp_fused(fc1, fc2), with out_proj.xn_out == fc1.A and out_proj.resid == fc2.resid
+   (h and xn are written and read back by the same block).  h and xn equal the three-descriptor
+   form bit for bit.  bf16, C == 384, out_proj.K == 384, >= 64 row tiles of 128 (the one-pass
+   MLP), out_proj.rows_per_mod == fc2.rows_per_mod >= 128; MDG_E_SHAPE otherwise. */
+int mdg_rowln_mlp(const mdg_gemm_desc* out_proj, const mdg_gemm_desc* fc1, const mdg_gemm_desc* fc2, void* stream);
 /* qkv: CT [n_frames*L][3][H][D] (unpadded q | k | v rows of each token) */
 int mdg_attn_spatial(int32_t dtype, int32_t n_frames, int32_t L, int32_t H, int32_t D,
                      const void* qkv, const float* kvb, const float* mask, void* out,

@@ -152,6 +152,8 @@ SIGNATURES = [
     ("mdg_gemm", _i32, [ctypes.POINTER(MdgGemmDesc), _vp]),
     ("mdg_mlp_fused", _i32, [ctypes.POINTER(MdgGemmDesc), ctypes.POINTER(MdgGemmDesc), _vp]),
     ("mdg_rowln_qkv", _i32, [ctypes.POINTER(MdgGemmDesc), ctypes.POINTER(MdgGemmDesc), _vp]),
+    ("mdg_rowln_mlp", _i32, [ctypes.POINTER(MdgGemmDesc), ctypes.POINTER(MdgGemmDesc), ctypes.POINTER(MdgGemmDesc),
+                             _vp]),
     ("mdg_attn_spatial", _i32, [_i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
     ("mdg_attn_temporal", _i32, [_i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),
     ("mdg_attn_temporal_packed", _i32, [_i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp]),

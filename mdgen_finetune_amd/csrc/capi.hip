@@ -22,7 +22,9 @@ struct GemmPlan {
 GemmPlan gemm_plan(const mdg_gemm_desc& p);
 hipError_t gemm_launch(const mdg_gemm_desc& p, const GemmPlan& g, hipStream_t s);
 bool mlp_fused_supported(const mdg_gemm_desc& f1, const mdg_gemm_desc& f2);
-hipError_t mlp_fused_launch(const mdg_gemm_desc& f1, const mdg_gemm_desc& f2, hipStream_t s, float* part);
+hipError_t mlp_fused_launch(const mdg_gemm_desc& f1, const mdg_gemm_desc& f2, hipStream_t s, float* part,
+                            const mdg_gemm_desc* pre = nullptr);
+bool mlp_pre_supported(const mdg_gemm_desc& r, const mdg_gemm_desc& f1, const mdg_gemm_desc& f2);
 int mlp_split_factor(int M, int F);
 hipError_t train_pack_launch(const mdg_train_pack& p, hipStream_t s);
 hipError_t train_unpack_launch(const mdg_train_unpack& u, hipStream_t s);
@@ -266,6 +268,19 @@ bool fused_qkv_on() {
   static const bool on = [] {
     const char* e = getenv("MDG_FUSED_QKV");
     return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+// MDG_MLP_PRE=1: the temporal out_proj row-LN GEMM as the fused MLP's prologue (one launch;
+// gemm.hip mlp_rowln_kernel PRE).  Off by default: bit-identical, but measured neutral (round 5,
+// same box, 2 x 2 alternating runs: 4.698 / 4.698 M frames/s fused vs 4.712 / 4.709 M two launches)
+// -- the step is the sum of the kernels' chip time (two lanes already fill the launch gaps and
+// tails), and the prologue costs what the launch did: its 12 K-steps plus an HBM-bound epilogue.
+bool mlp_pre_on() {
+  static const bool on = [] {
+    const char* e = getenv("MDG_MLP_PRE");
+    return e && e[0] == '1';
   }();
   return on;
 }
@@ -654,11 +669,8 @@ static int layer_fwd_impl(const mdg_dims* d, const mdg_layer_weights* w, const f
   if (fuse) {  // + LN_mlp(h) -> xn
     r.xn_shift_off = 6 * C; r.xn_scale_off = 7 * C;
   }
-  if (int e = rowln_gemm(r)) return e;
 
   // ---- MLP: x += gate_m * fc2(gelu(fc1(mod(LN x))))           (latent_model.py:488-491)
-  if (!fuse)
-    if (int e = ln(6 * C, 7 * C)) return e;
   mdg_gemm_desc f1 = g;
   f1.epi = MDG_EPI_STORE; f1.act = MDG_ACT_GELU;
   f1.N = F; f1.K = C; f1.A = xn; f1.lda = C; f1.W = w->w1; f1.ldw = C; f1.bias = w->b1;
@@ -671,7 +683,13 @@ static int layer_fwd_impl(const mdg_dims* d, const mdg_layer_weights* w, const f
     f2.xn_out = xn; f2.xn_mods = ho.next_mods; f2.xn_mod_stride = ho.next_stride;
     f2.xn_shift_off = ho.next_shift; f2.xn_scale_off = ho.next_scale; f2.ln_eps = 1e-6f;
   }
-  if (fuse && fused_mlp_on() && mdg::mlp_fused_supported(f1, f2))
+  const bool mlp1 = fuse && fused_mlp_on() && mdg::mlp_fused_supported(f1, f2);
+  if (mlp1 && mlp_pre_on() && mdg::mlp_pre_supported(r, f1, f2))  // out_proj + MLP: one launch
+    return hip_check(mdg::mlp_fused_launch(f1, f2, (hipStream_t)stream, nullptr, &r), "out_proj + mlp fused launch");
+  if (int e = rowln_gemm(r)) return e;
+  if (!fuse)
+    if (int e = ln(6 * C, 7 * C)) return e;
+  if (mlp1)
     return hip_check(mdg::mlp_fused_launch(f1, f2, (hipStream_t)stream, (float*)(wsb + lay.mlp_part)),
                      "mlp fused launch");
   if (int e = mdg_gemm(&f1, stream)) return e;
@@ -685,6 +703,15 @@ int mdg_mlp_fused(const mdg_gemm_desc* f1, const mdg_gemm_desc* f2, void* stream
     return fail(MDG_E_SHAPE, "mlp_fused: outside the envelope (bf16, K=N=384, F %% 128, rows_per_mod >= 128) "
                 "M=%d C=%d F=%d", f1->M, f1->K, f1->N);
   return hip_check(mdg::mlp_fused_launch(*f1, *f2, (hipStream_t)stream, nullptr), "mlp fused launch");
+}
+
+int mdg_rowln_mlp(const mdg_gemm_desc* r, const mdg_gemm_desc* f1, const mdg_gemm_desc* f2, void* stream) {
+  if (!r || !f1 || !f2) return fail(MDG_E_ARG, "rowln_mlp: null descriptor");
+  if (!r->A || !r->W || !r->resid || !f1->W || !f2->W || !f2->resid) return fail(MDG_E_ARG, "rowln_mlp: null pointer");
+  if (!mdg::mlp_pre_supported(*r, *f1, *f2))
+    return fail(MDG_E_SHAPE, "rowln_mlp: outside the envelope (bf16, K=N=384, one-pass MLP (>= 64 row tiles), "
+                "out_proj.xn_out == fc1.A, out_proj.resid == fc2.resid, rows_per_mod >= 128) M=%d", r->M);
+  return hip_check(mdg::mlp_fused_launch(*f1, *f2, (hipStream_t)stream, nullptr, r), "rowln_mlp launch");
 }
 
 int mdg_rowln_qkv(const mdg_gemm_desc* r, const mdg_gemm_desc* q, void* stream) {

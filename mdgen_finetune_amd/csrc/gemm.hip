@@ -1569,6 +1569,7 @@ struct MlpArgs {
   mdg_gemm_desc f1, f2;
   float* part;  // split form: [nsplit][M][NCOL] fp32 fc2 partials (no epilogue in the kernel)
   int nsplit;   // hidden chunks are divided over gridDim.y = nsplit blocks per row tile
+  mdg_gemm_desc r;  // PRE form: the temporal out_proj row-LN GEMM run first (r.xn_out = f1.A)
 };
 // timing diagnostics only (tools/diag_mlp_attn.sh builds them into separate libraries): 1 = xn
 // staged for the first hidden chunk only, 2 = GELU replaced by the identity, 3 = nothing staged
@@ -1633,7 +1634,14 @@ __device__ __forceinline__ void vm_wait_upto6(int n) {
   }
 }
 
-template <int NCOL, bool SPLIT>  // SPLIT: chunks [y * cps, (y + 1) * cps) only, fp32 partials out
+// PRE (round 5): the block first runs the temporal attention's out_proj row-LN GEMM on its own
+// 128 rows (latent_model.py:486: h += gate_t * out_proj(o), then LN_mlp + modulate -> xn), the
+// exact K loop and epilogue of gemm_rowln_kernel<384, 128> on this kernel's 3-slot ring (one
+// 32-wide step = 128 o rows + 384 W_o rows = one slot), so h and xn equal the two-launch form bit
+// for bit.  The block's h / xn rows are then read back by the MLP below (ring DMA for xn, the
+// residual load for h): ordered by a work-group barrier with release / acquire at work-group
+// scope (one CU, one L1).  Saves the out_proj launch, its grid tail and the xn HBM round trip.
+template <int NCOL, bool SPLIT, bool PRE = false>  // SPLIT: chunks [y * cps, (y + 1) * cps) only, fp32 partials out
 __global__ __launch_bounds__(kMlpThreads, 1) void mlp_rowln_kernel(const MlpArgs args) {
   static_assert(NCOL == 384, "the ring slot holds 384 W2 rows");
   constexpr int BM = 128, BK = 32, HC = kMlpHC, STAGES = kMlpStages, SLOT = kMlpSlot;
@@ -1661,6 +1669,64 @@ __global__ __launch_bounds__(kMlpThreads, 1) void mlp_rowln_kernel(const MlpArgs
   for (int i = tid; i < F; i += kMlpThreads) b1s[i] = q.bias ? q.bias[i] : 0.f;
   // ring loader: slot row r's 16-B chunk c at c ^ ((-(r >> 2)) & 3); a 16-row piece per glds
   const int cswz = ((lane & 3) ^ ((-(lane >> 4)) & 3)) * 8;
+  if constexpr (PRE) {
+    static_assert(!SPLIT, "the out_proj prologue runs in the one-pass form");
+    const mdg_gemm_desc& r = args.r;
+    constexpr int NK = NCOL / BK;
+    const int chp = (lg ^ ((-(lr >> 2)) & 3)) * 8;  // r.K == NCOL: 12 steps of 32
+    const float inv_rpm_r = 1.0f / (float)r.rows_per_mod;
+    float4 h4p[2][NE];
+    rowln_load_band<NCOL>(r, RowsLinear{m0}, 0, h4p);  // band 0's residual rows, in flight under the K loop
+    // wave w stages slot rows 64 w + 16 i + lane / 4 (i < 4): rows < 128 from o, the rest from W_o
+    const bool ow = wave < 2;
+    const bf16_t* pbase = reinterpret_cast<const bf16_t*>(ow ? r.A : r.W);
+    int poff[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int sr = 64 * wave + 16 * i + (lane >> 2);
+      poff[i] = (ow ? min(m0 + sr, M - 1) * r.lda : (sr - BM) * r.ldw) + cswz;
+    }
+    auto pissue = [&](int s) {
+      bf16_t* sl = ring + (s % STAGES) * SLOT;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        __builtin_amdgcn_global_load_lds((const void*)(pbase + s * BK + poff[i]),
+                                         (lds_ptr_t)(sl + (64 * wave + 16 * i) * BK), 16, 0, 0);
+    };
+    f32x4 acc[4][NT];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    pissue(0);
+    pissue(1);
+    for (int s = 0; s < NK; ++s) {
+      // step s landed (the residual rows with it at s = 0); step s + 1's 4 pieces stay in flight
+      if (s + 1 < NK) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // ring reads retired (see kRingWaitNote)
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (s + 2 < NK) pissue(s + 2);
+      const bf16_t* As = ring + (s % STAGES) * SLOT;
+      const bf16_t* Bs = As + BM * BK;
+      bf16x8 a[4], b[NT];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = *reinterpret_cast<const bf16x8*>(As + (wm * 64 + i * 16 + lr) * BK + chp);
+#pragma unroll
+      for (int j = 0; j < NT; ++j) b[j] = *reinterpret_cast<const bf16x8*>(Bs + (wn * WTN + j * 16 + lr) * BK + chp);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    rowln_fast_epilogue<NCOL>(r, acc, h4p, smem, RowsLinear{m0}, fdiv(m0, r.rows_per_mod, inv_rpm_r), inv_rpm_r);
+    // the block's h and xn rows are stored before any wave reads them back (the ring's xn DMA,
+    // the epilogue's residual load); the stage region is free again for the ring
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
   const bf16_t* X = reinterpret_cast<const bf16_t*>(q.A);
   const bf16_t* W1 = reinterpret_cast<const bf16_t*>(q.W);
   const bf16_t* W2 = reinterpret_cast<const bf16_t*>(p.W);
@@ -1701,6 +1767,7 @@ __global__ __launch_bounds__(kMlpThreads, 1) void mlp_rowln_kernel(const MlpArgs
     }
   };
 
+  const int ch = (lg ^ ((-(lr >> 2)) & 3)) * 8;
   f32x4 acc2[4][NT], acc1[4][2];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -1709,7 +1776,6 @@ __global__ __launch_bounds__(kMlpThreads, 1) void mlp_rowln_kernel(const MlpArgs
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc1[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
-  const int ch = (lg ^ ((-(lr >> 2)) & 3)) * 8;
 #pragma unroll
   for (int s0 = 0; s0 < STAGES - 1; ++s0)
     if (s0 < NS) issue(s0);
@@ -2264,11 +2330,23 @@ static bool mlp_ws_on() {
   return on;
 }
 
-hipError_t mlp_fused_launch(const mdg_gemm_desc& f1, const mdg_gemm_desc& f2, hipStream_t s, float* part) {
+// The out_proj prologue's envelope: r is the fast row-LN path's GEMM (bf16 PLAIN, K = N = 384,
+// rows_per_mod >= 128) whose h and xn outputs are exactly the MLP's residual and fc1 input, on
+// the MLP's rows, and the MLP runs in its one-pass form.
+bool mlp_pre_supported(const mdg_gemm_desc& r, const mdg_gemm_desc& f1, const mdg_gemm_desc& f2) {
+  return mlp_fused_supported(f1, f2) && mlp_split_factor(f1.M, f1.N) == 1 && r.dtype == MDG_BF16 &&
+         r.a_mode == MDG_A_PLAIN && r.epi == MDG_EPI_GATE_RES && r.N == 384 && r.K == 384 && r.M == f1.M &&
+         r.rows_per_mod == f2.rows_per_mod && r.resid == f2.resid && r.ldr == f2.ldr && !r.resid_in && !r.aux &&
+         r.xn_out && r.xn_out == f1.A && f1.lda == 384 && r.xn_mods && r.A && r.W && r.lda % 8 == 0 && r.ldw % 8 == 0;
+}
+
+hipError_t mlp_fused_launch(const mdg_gemm_desc& f1, const mdg_gemm_desc& f2, hipStream_t s, float* part,
+                            const mdg_gemm_desc* pre) {
   static bool attr_set = false;
   if (!attr_set) {
     for (const void* k : {reinterpret_cast<const void*>(&mlp_rowln_kernel<384, false>),
                           reinterpret_cast<const void*>(&mlp_rowln_kernel<384, true>),
+                          reinterpret_cast<const void*>(&mlp_rowln_kernel<384, false, true>),
                           reinterpret_cast<const void*>(&mlp_ws_kernel<384>)}) {
       hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       if (e != hipSuccess) return e;
@@ -2281,6 +2359,12 @@ hipError_t mlp_fused_launch(const mdg_gemm_desc& f1, const mdg_gemm_desc& f2, hi
   a.part = part;
   a.nsplit = part ? mlp_split_factor(f1.M, f1.N) : 1;
   const int tiles = (f1.M + 127) / 128;
+  if (pre) {
+    if (!mlp_pre_supported(*pre, f1, f2)) return hipErrorInvalidValue;
+    a.r = *pre;
+    hipLaunchKernelGGL((mlp_rowln_kernel<384, false, true>), dim3(tiles), dim3(kMlpThreads), mlp_smem(f1.N), s, a);
+    return hipGetLastError();
+  }
   if (a.nsplit > 1) {
     hipLaunchKernelGGL((mlp_rowln_kernel<384, true>), dim3(tiles, a.nsplit), dim3(kMlpThreads), mlp_smem(f1.N), s, a);
     if (hipError_t e = hipGetLastError()) return e;

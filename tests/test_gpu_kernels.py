@@ -172,6 +172,74 @@ def test_mlp_fused_equals_fc1_then_fc2(lib, M, TL, with_ln):
         assert not x_f.any()
 
 
+@pytest.mark.parametrize("M,TL", [(8292, 4146), (16000, 4000), (8320, 200)])
+def test_rowln_mlp_equals_out_proj_then_mlp(lib, M, TL):
+    """mdg_rowln_mlp (the temporal out_proj row-LN GEMM as the fused MLP's prologue, one launch:
+    h and xn written and read back by the same block) against mdg_gemm(out_proj) then
+    mdg_mlp_fused: h and both LayerNorm outputs bit-identical.  Partial last tile, tiles over two
+    trajectories (TL = 200)."""
+    from mdgen_finetune_amd import _lib
+
+    C, F = 384, 1536
+    g = torch.Generator(device="cuda").manual_seed(M + TL + 7)
+    o = torch.randn(M, C, device="cuda", generator=g).to(torch.bfloat16)
+    Wo = (torch.randn(C, C, device="cuda", generator=g) / math.sqrt(C)).to(torch.bfloat16)
+    bo = torch.randn(C, device="cuda", generator=g) * 0.5
+    W1 = (torch.randn(F, C, device="cuda", generator=g) / math.sqrt(C)).to(torch.bfloat16)
+    b1 = torch.randn(F, device="cuda", generator=g) * 0.5
+    W2 = (torch.randn(C, F, device="cuda", generator=g) / math.sqrt(F)).to(torch.bfloat16)
+    b2 = torch.randn(C, device="cuda", generator=g)
+    nb = (M + TL - 1) // TL
+    mods = torch.randn(nb, 9 * C, device="cuda", generator=g) * 0.5
+    nmods = torch.randn(nb, 2 * C, device="cuda", generator=g) * 0.5
+    h0 = torch.randn(M, C, device="cuda", generator=g) * 2
+    outs = []
+    for fused in (False, True):
+        h = h0.clone()
+        xn = torch.zeros(M, C, device="cuda", dtype=torch.bfloat16)
+        xo = torch.zeros(M, C, device="cuda", dtype=torch.bfloat16)
+        r = _desc(dtype=1, a_mode=0, epi=1, M=M, N=C, K=C, A=o.data_ptr(), lda=C, W=Wo.data_ptr(), ldw=C,
+                  bias=bo.data_ptr(), mod_stride=9 * C, rows_per_mod=TL, resid=h.data_ptr(), ldr=C,
+                  gate=mods.data_ptr(), gate_off=5 * C, xn_out=xn.data_ptr(), xn_mods=mods.data_ptr(),
+                  xn_mod_stride=9 * C, xn_shift_off=6 * C, xn_scale_off=7 * C, ln_eps=1e-6)
+        f1 = _desc(dtype=1, a_mode=0, epi=0, act=1, M=M, N=F, K=C, A=xn.data_ptr(), lda=C, W=W1.data_ptr(), ldw=C,
+                   bias=b1.data_ptr(), out=0, ldo=F)
+        f2 = _desc(dtype=1, a_mode=0, epi=1, M=M, N=C, K=F, A=0, lda=F, W=W2.data_ptr(), ldw=F,
+                   bias=b2.data_ptr(), mod_stride=9 * C, rows_per_mod=TL, resid=h.data_ptr(), ldr=C,
+                   gate=mods.data_ptr(), gate_off=8 * C, xn_out=xo.data_ptr(), xn_mods=nmods.data_ptr(),
+                   xn_mod_stride=2 * C, xn_shift_off=0, xn_scale_off=C, ln_eps=1e-6)
+        if fused:
+            _lib.check(lib.mdg_rowln_mlp(ctypes.byref(r), ctypes.byref(f1), ctypes.byref(f2), _s()), "mdg_rowln_mlp")
+        else:
+            _lib.check(lib.mdg_gemm(ctypes.byref(r), _s()), "out_proj")
+            _lib.check(lib.mdg_mlp_fused(ctypes.byref(f1), ctypes.byref(f2), _s()), "mlp")
+        outs.append((h, xn, xo))
+    torch.cuda.synchronize()
+    (h_ref, xn_ref, xo_ref), (h_f, xn_f, xo_f) = outs
+    b = torch.arange(M, device="cuda") // TL
+    h1 = h0 + mods[b, 5 * C:6 * C] * (o.float() @ Wo.float().T + bo)
+    assert xn_ref.any() and xo_ref.any()
+    assert torch.equal(xn_f, xn_ref), (xn_f.float() - xn_ref.float()).abs().max().item()
+    assert torch.equal(h_f, h_ref), (h_f - h_ref).abs().max().item()
+    assert torch.equal(xo_f, xo_ref), (xo_f.float() - xo_ref.float()).abs().max().item()
+    pre = xn_f.float() @ W1.float().T + b1
+    hidden = (pre * 0.5 * (1 + torch.erf(pre / math.sqrt(2)))).to(torch.bfloat16).float()
+    torch.testing.assert_close(h_f, h1 + mods[b, 8 * C:9 * C] * (hidden @ W2.float().T + b2), rtol=5e-3, atol=5e-3)
+
+
+def test_rowln_mlp_rejects_unsupported_shapes(lib):
+    C, F, M = 384, 1536, 8192
+    r = _desc(dtype=1, a_mode=0, epi=1, M=M, N=C, K=C, A=1, lda=C, W=1, ldw=C, resid=2, ldr=C, rows_per_mod=4096,
+              xn_out=3, xn_mods=1)
+    f1 = _desc(dtype=1, a_mode=0, epi=0, act=1, M=M, N=F, K=C, A=3, lda=C, W=1, ldw=C)
+    f2 = _desc(dtype=1, a_mode=0, epi=1, M=M, N=C, K=F, A=1, lda=F, W=1, ldw=F, resid=2, ldr=C, rows_per_mod=4096)
+    r.xn_out = 4  # xn not the MLP's input
+    assert lib.mdg_rowln_mlp(ctypes.byref(r), ctypes.byref(f1), ctypes.byref(f2), _s()) == 1001
+    r.xn_out = 3
+    r.M = f1.M = f2.M = 4000  # < 64 row tiles: the MLP would split
+    assert lib.mdg_rowln_mlp(ctypes.byref(r), ctypes.byref(f1), ctypes.byref(f2), _s()) == 1001
+
+
 def test_mlp_fused_rejects_unsupported_shapes(lib):
     d1 = _desc(dtype=1, a_mode=0, epi=0, act=1, M=256, N=1536, K=256, A=1, lda=256, W=1, ldw=256)
     d2 = _desc(dtype=1, a_mode=0, epi=1, M=256, N=256, K=1536, A=1, lda=1536, W=1, ldw=1536, resid=1, ldr=256,
