@@ -399,7 +399,8 @@ __global__ __launch_bounds__(256) void attn_bwd_prep_tiled_kernel(int B, int T, 
                                                                   const bf16_t* __restrict__ o,
                                                                   const bf16_t* __restrict__ o_lo,
                                                                   const bf16_t* __restrict__ dout,
-                                                                  bf16_t* __restrict__ dop, float* __restrict__ delta) {
+                                                                  bf16_t* __restrict__ dop, float* __restrict__ delta,
+                                                                  const float* __restrict__ lse) {
   __shared__ __attribute__((aligned(16))) bf16_t tile[256 * kDP];  // [head][tl][kDP]
   const int TT = 256 / H, seq = blockIdx.y, b = seq / L, l = seq - b * L;
   const int t0 = blockIdx.x * TT, head = threadIdx.x % H, tl = threadIdx.x / H, t = t0 + tl;
@@ -410,12 +411,23 @@ __global__ __launch_bounds__(256) void attn_bwd_prep_tiled_kernel(int B, int T, 
     const bf16_t* drow = dout + n * C + head * D;
     bf16_t* trow = tile + ((size_t)head * TT + tl) * kDP;
     float dl = 0.f;
+    // the folded backward's dO' = bf16(2^-(lse - hi) dO), hi = bf16(lse) (attn_bwd_fused_bf16_kernel
+    // FOLD); delta' from the rounded dO' itself, so dP' - delta' cancels exactly where dS = 0
+    float cq = 1.f;
+    if (lse) {
+      const float lv = lse[((size_t)seq * H + head) * T + t];
+      cq = __builtin_amdgcn_exp2f((float)(bf16_t)lv - lv);
+    }
 #pragma unroll
     for (int d0 = 0; d0 < kDP; d0 += 8) {
       bf16x8 dv = zero8<bf16_t>();
       if (d0 < D) {
         const bf16x8 ov = ld8<bf16_t>(orow + d0);
         dv = ld8<bf16_t>(drow + d0);
+        if (lse) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) dv[j] = (bf16_t)((float)dv[j] * cq);
+        }
 #pragma unroll
         for (int j = 0; j < 8; j += 4)
           dl += (float)dv[j] * (float)ov[j] + (float)dv[j + 1] * (float)ov[j + 1] + (float)dv[j + 2] * (float)ov[j + 2] +
@@ -976,6 +988,21 @@ __device__ __forceinline__ bf16x8 ftr16(const bf16_t* img, int k0, int c0, int l
   return r;
 }
 
+// FOLD (round 5; D % 8 == 0, D <= 30): the per-pair offsets ride in the S MFMA, as the forward's
+// softmax offset does.  The Q image's pad columns D, D + 1 hold -hi_q = -bf16(lse_q) and 1, the
+// K fragments' hold 1 and the key bias (0, or -30000 for a padded key), so S' = Q K^T + kbias -
+// hi comes out of the MFMA and P' = exp2(S') needs no vector add.  The rest of lse, lo = lse -
+// hi, is folded into the query's dO row by the prep kernel: with c = 2^-lo, dO' = bf16(c dO) and
+// delta' = dO' . (O + O_lo), so dP' = dO' V^T, dS = P' (dP' - delta') and dV = sum P' dO' are the
+// gradients of the upstream gradient dO'/c (dO rounded to bf16 once more), consistent with each
+// other: dS still cancels exactly where it should (a fully padded sequence: P = [1, 0, ...]).
+// Phase A drops two vector ops per score.
+__device__ __forceinline__ unsigned short bf16_bits(float f) {
+  return __builtin_bit_cast(unsigned short, (bf16_t)f);
+}
+__device__ __forceinline__ float bf16_val(unsigned short b) { return __uint_as_float((unsigned)b << 16); }
+
+template <bool FOLD>
 __global__ __launch_bounds__(kBW * 64, 2) void attn_bwd_fused_bf16_kernel(
     const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dop, const float* __restrict__ lse,
     const float* __restrict__ delta, const float* __restrict__ kbias, const float* __restrict__ kvb,
@@ -1015,19 +1042,24 @@ __global__ __launch_bounds__(kBW * 64, 2) void attn_bwd_fused_bf16_kernel(
   const int simg = tid >> 8, srow = (tid >> 2) & (kFQC - 1), spc = tid & 3;
   const bf16_t* sg = simg ? dOg : Qg;
   u32x4 sreg;
-  float lreg = 0.f;
+  float lreg = 0.f, lq = 0.f;
+  const bool sq_live = FOLD && !simg && spc == (D >> 3);  // the Q piece holding pad columns D, D + 1
   auto gload = [&](int c) {
     const int qq = c * kFQC + srow;
     sreg = u32x4{0u, 0u, 0u, 0u};
     if (qq < T) sreg = *reinterpret_cast<const u32x4*>(sg + (size_t)qq * kDP + spc * 8);
+    if (sq_live) lq = (qq < T) ? lg[qq] : 30000.f;
     if (tid < 2 * kFQC) {
       const int q2 = c * kFQC + (tid & (kFQC - 1));
-      lreg = tid < kFQC ? (q2 < T ? lg[q2] : INFINITY) : (q2 < T ? dg[q2] : 0.f);
+      lreg = tid < kFQC ? (q2 < T ? lg[q2] : (FOLD ? 30000.f : INFINITY)) : (q2 < T ? dg[q2] : 0.f);
     }
   };
   auto lstore = [&](int buf) {
-    *reinterpret_cast<u32x4*>(&(simg ? Ds : Qs)[buf][img_off(srow, spc * 8)]) = sreg;
-    if (tid < kFQC) ls[buf][tid] = lreg;
+    u32x4 v = sreg;
+    if (sq_live) v[0] = (unsigned)bf16_bits(-bf16_val(bf16_bits(lq))) | (0x3F80u << 16);  // Q pad: -hi, 1
+    *reinterpret_cast<u32x4*>(&(simg ? Ds : Qs)[buf][img_off(srow, spc * 8)]) = v;
+    // FOLD: ls = hi (the last pass's bias-key P'); dls = delta' as the prep kernel wrote it
+    if (tid < kFQC) ls[buf][tid] = FOLD ? bf16_val(bf16_bits(lreg)) : lreg;
     else if (tid < 2 * kFQC) dls[buf][tid - kFQC] = lreg;
   };
   // phase-B tile of this wave: dims 16 bd .. +15, queries 16 bq .. +15 of the chunk; the lane
@@ -1047,6 +1079,16 @@ __global__ __launch_bounds__(kBW * 64, 2) void attn_bwd_fused_bf16_kernel(
     plane_frag(Kg, key, live, h, kf);
     plane_frag(Vg, key, live, h, vf);
     const float kbl = live ? kbg[key] : -INFINITY;
+    if (FOLD) {  // K pad columns D, D + 1: 1, the key bias
+      const int padS = D >> 4, padH = (D >> 3) & 1;
+      const bf16_t kb16 = (bf16_t)fmaxf(kbl, -30000.f);
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+        if (s2 == padS && h == padH) {
+          kf[s2][0] = (bf16_t)1.0f;
+          kf[s2][1] = kb16;
+        }
+    }
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2)
       *reinterpret_cast<bf16x8*>(&Kim[fk_off(wave * 32 + r, 16 * s2 + 8 * h)]) = kf[s2];
@@ -1072,7 +1114,7 @@ __global__ __launch_bounds__(kBW * 64, 2) void attn_bwd_fused_bf16_kernel(
           const bf16x8 dv8 = *reinterpret_cast<const bf16x8*>(&Ds[cur][img_off(tid, d0)]);
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
-            sb += (float)qv[j] * bk[d0 + j];
+            sb += (FOLD && d0 + j >= D) ? 0.f : (float)qv[j] * bk[d0 + j];  // (FOLD: Q's pad columns hold offsets)
             dpb += (float)dv8[j] * (d0 + j < D ? bv[d0 + j] : 0.f);
           }
         }
@@ -1101,7 +1143,7 @@ __global__ __launch_bounds__(kBW * 64, 2) void attn_bwd_fused_bf16_kernel(
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int i = 4 * g4 + e;
-            const float p = __builtin_amdgcn_exp2f(sacc[i] + kbl - lv[e]);
+            const float p = FOLD ? __builtin_amdgcn_exp2f(sacc[i]) : __builtin_amdgcn_exp2f(sacc[i] + kbl - lv[e]);
             pr[i] = p;
             dsr[i] = p * (pacc[i] - dv4[e]);
           }
@@ -1155,7 +1197,7 @@ __global__ __launch_bounds__(kBW * 64, 2) void attn_bwd_fused_bf16_kernel(
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const int qq = 8 * bqs + j;
-          bacc += coef[qq] * (float)X[img_off(qq, bgd)];
+          bacc += (FOLD && bgd >= D) ? 0.f : coef[qq] * (float)X[img_off(qq, bgd)];
         }
       }
       __syncthreads();
@@ -1197,6 +1239,15 @@ __global__ __launch_bounds__(kBW * 64, 2) void attn_bwd_fused_bf16_kernel(
   }
 }
 
+// MDG_ATTN_BWD_FOLD=0: the fused backward with the offsets as vector ops (A/B knob)
+static bool attn_bwd_fold_on() {
+  static const bool on = [] {
+    const char* e = getenv("MDG_ATTN_BWD_FOLD");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 int attn_bwd_parts(int dtype, int B, int T, int L, int generic) {  // bias-gradient partial slots per head
   if (dtype == MDG_BF16 && generic == 0) return B * L;  // the fused kernel: one per sequence
   if (dtype == MDG_BF16) return B * L * ((T + kBW * 32 - 1) / (kBW * 32)) * kBW;
@@ -1211,11 +1262,15 @@ hipError_t attn_temporal_bwd_launch(int dtype, int B, int T, int L, int H, int D
                                     float* dqacc, hipStream_t s) {
   const int BL = B * L;
   const size_t nth = (size_t)B * T * L * H;
+  // the fused backward with folded offsets (its dO' / delta' come from the tiled prep)
+  const bool fold = dtype == MDG_BF16 && generic == 0 && attn_bwd_fold_on() && D % 8 == 0 && D + 2 <= kDP &&
+                    H <= 256 && 256 % H == 0;
   dim3 pgrid((unsigned)((nth + 255) / 256));
   if (dtype == MDG_BF16 && D % 8 == 0 && H <= 256 && 256 % H == 0) {
     const int TT = 256 / H;
     hipLaunchKernelGGL(attn_bwd_prep_tiled_kernel, dim3((T + TT - 1) / TT, BL), dim3(256), 0, s, B, T, L, H, D,
-                       (const bf16_t*)o, (const bf16_t*)o_lo, (const bf16_t*)dout, (bf16_t*)dop, delta);
+                       (const bf16_t*)o, (const bf16_t*)o_lo, (const bf16_t*)dout, (bf16_t*)dop, delta,
+                       fold ? lse : nullptr);
   } else if (dtype == MDG_BF16) {
     hipLaunchKernelGGL(attn_bwd_prep_kernel<bf16_t>, pgrid, dim3(256), 0, s, B, T, L, H, D, (const bf16_t*)o,
                        (const bf16_t*)o_lo, (const bf16_t*)dout, (bf16_t*)dop, delta);
@@ -1225,9 +1280,14 @@ hipError_t attn_temporal_bwd_launch(int dtype, int B, int T, int L, int H, int D
   }
   if (hipError_t e = hipGetLastError()) return e;
   if (dtype == MDG_BF16 && generic == 0) {  // fused single pass
-    hipLaunchKernelGGL(attn_bwd_fused_bf16_kernel, dim3(H * BL), dim3(kBW * 64), 0, s, (const bf16_t*)qkv_t,
-                       (const bf16_t*)dop, lse, delta, kbias, kvb, rope, rope_rows, (bf16_t*)dqkv, ldq, dqacc, bpart, T,
-                       L, H, D, BL, qscale, kscale);
+    if (fold)
+      hipLaunchKernelGGL(attn_bwd_fused_bf16_kernel<true>, dim3(H * BL), dim3(kBW * 64), 0, s, (const bf16_t*)qkv_t,
+                         (const bf16_t*)dop, lse, delta, kbias, kvb, rope, rope_rows, (bf16_t*)dqkv, ldq, dqacc, bpart,
+                         T, L, H, D, BL, qscale, kscale);
+    else
+      hipLaunchKernelGGL(attn_bwd_fused_bf16_kernel<false>, dim3(H * BL), dim3(kBW * 64), 0, s, (const bf16_t*)qkv_t,
+                         (const bf16_t*)dop, lse, delta, kbias, kvb, rope, rope_rows, (bf16_t*)dqkv, ldq, dqacc, bpart,
+                         T, L, H, D, BL, qscale, kscale);
     return hipGetLastError();
   }
   if (dtype == MDG_BF16 && generic == 2) {  // the two-pass MFMA kernels (dQ; dK / dV)
