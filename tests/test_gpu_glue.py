@@ -162,3 +162,28 @@ def test_gvp_plan_and_loss_match_eager(path):
     (ref * g).sum().backward()
     assert _rel(loss, ref) <= 1e-6, _rel(loss, ref)
     assert _rel(d_got, out.grad) <= 1e-6, _rel(d_got, out.grad)
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_gvp_loss_half_precision_prediction(dt):
+    """A half-precision prediction (the eager FinalLayer under bf16 / fp16 autocast, L > 8, where
+    the HIP FinalLayer is not used) is promoted to fp32 for the kernels, as the reference's
+    (out - ut) with an fp32 ut promotes, and its gradient comes back in the prediction's dtype
+    (the kernels read and wrote fp32 through a half-size buffer)."""
+    from mdgen_finetune_amd.train_hip import gvp_loss
+    from mdgen_finetune_amd.transport.transport import mean_flat
+
+    torch.manual_seed(11)
+    B, T, L, K, dev = 2, 20, 12, 21, "cuda"
+    ut = torch.randn(B, T, L, K, device=dev)
+    mask = (torch.rand(B, 1, L, K, device=dev) > 0.3).float().expand(B, T, L, K)
+    out = torch.randn(B, T, L, K, device=dev).to(dt).requires_grad_(True)
+    loss = gvp_loss(out, ut, mask)
+    loss.sum().backward()
+    assert loss.dtype == torch.float32 and out.grad.dtype == dt
+    d_got = out.grad.float().clone()
+    out.grad = None
+    ref = mean_flat((out - ut) ** 2, mask)
+    ref.sum().backward()
+    assert _rel(loss, ref) <= 1e-6, _rel(loss, ref)
+    assert _rel(d_got, out.grad.float()) <= 1e-2, _rel(d_got, out.grad.float())
