@@ -1002,7 +1002,11 @@ __device__ __forceinline__ unsigned short bf16_bits(float f) {
 }
 __device__ __forceinline__ float bf16_val(unsigned short b) { return __uint_as_float((unsigned)b << 16); }
 
-template <bool FOLD>
+// LACC (round 5): the fp32 dQ accumulator [T][DS] of the block's (sequence, head) lives in LDS
+// (dynamic, T * DS * 4 bytes: 96 000 B at T = 1 000, D = 24, next to the 67 KB of static LDS;
+// the kernel runs one block per CU at its 245-256 VGPRs anyway) instead of global memory: the
+// middle passes' read-add-store round trips (3 x 49 MB per launch at T = 1 000) stay on chip.
+template <bool FOLD, bool LACC = false>
 __global__ __launch_bounds__(kBW * 64, 2) void attn_bwd_fused_bf16_kernel(
     const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dop, const float* __restrict__ lse,
     const float* __restrict__ delta, const float* __restrict__ kbias, const float* __restrict__ kvb,
@@ -1035,7 +1039,8 @@ __global__ __launch_bounds__(kBW * 64, 2) void attn_bwd_fused_bf16_kernel(
   // the fp32 dQ accumulator rows hold only the D live dims (stride DS = D rounded to 4: 24 at the
   // default head dim, three quarters of the padded plane's bytes per pass)
   const int DS = (D + 3) & ~3;
-  float* acc_g = dqacc + (size_t)sh * T * DS;
+  extern __shared__ __attribute__((aligned(16))) float acc_lds[];
+  float* acc_g = LACC ? acc_lds : dqacc + (size_t)sh * T * DS;
   const int nkb = (T + KB - 1) / KB, nch = (T + kFQC - 1) / kFQC;
   const int b = seq / L, l = seq % L, half = D >> 1, C = H * D;
   // staging roles: image (Q / dO), row, 16-B piece; lse / delta by threads 0..127
@@ -1239,6 +1244,25 @@ __global__ __launch_bounds__(kBW * 64, 2) void attn_bwd_fused_bf16_kernel(
   }
 }
 
+// MDG_ATTN_BWD_LACC=0: the fused backward's dQ accumulator in global memory (A/B knob)
+static bool attn_bwd_lacc_on() {
+  static const bool on = [] {
+    const char* e = getenv("MDG_ATTN_BWD_LACC");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+// the LACC kernel's static LDS (its dynamic accumulator comes on top)
+static size_t attn_bwd_static_lds() {
+  static const size_t v = [] {
+    hipFuncAttributes a;
+    if (hipFuncGetAttributes(&a, reinterpret_cast<const void*>(&attn_bwd_fused_bf16_kernel<true, true>)) != hipSuccess)
+      return (size_t)160 * 1024;  // unknown: never take the LDS route
+    return a.sharedSizeBytes;
+  }();
+  return v;
+}
+
 // MDG_ATTN_BWD_FOLD=0: the fused backward with the offsets as vector ops (A/B knob)
 static bool attn_bwd_fold_on() {
   static const bool on = [] {
@@ -1280,7 +1304,20 @@ hipError_t attn_temporal_bwd_launch(int dtype, int B, int T, int L, int H, int D
   }
   if (hipError_t e = hipGetLastError()) return e;
   if (dtype == MDG_BF16 && generic == 0) {  // fused single pass
-    if (fold)
+    const size_t lacc = (size_t)T * ((D + 3) & ~3) * sizeof(float);
+    if (fold && attn_bwd_lacc_on() && T > kBW * 32 && lacc + attn_bwd_static_lds() <= 160 * 1024) {
+      static bool attr_set = false;
+      if (!attr_set) {
+        if (hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_bwd_fused_bf16_kernel<true, true>),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               160 * 1024 - (int)attn_bwd_static_lds()))
+          return e;
+        attr_set = true;
+      }
+      hipLaunchKernelGGL((attn_bwd_fused_bf16_kernel<true, true>), dim3(H * BL), dim3(kBW * 64), lacc, s,
+                         (const bf16_t*)qkv_t, (const bf16_t*)dop, lse, delta, kbias, kvb, rope, rope_rows,
+                         (bf16_t*)dqkv, ldq, dqacc, bpart, T, L, H, D, BL, qscale, kscale);
+    } else if (fold)
       hipLaunchKernelGGL(attn_bwd_fused_bf16_kernel<true>, dim3(H * BL), dim3(kBW * 64), 0, s, (const bf16_t*)qkv_t,
                          (const bf16_t*)dop, lse, delta, kbias, kvb, rope, rope_rows, (bf16_t*)dqkv, ldq, dqacc, bpart,
                          T, L, H, D, BL, qscale, kscale);
