@@ -37,6 +37,8 @@ hipError_t ipa_core_bwd_launch(int B, int L, int H, const float* q, const float*
                                const float* dout, float* dq, float* dkv, float* dqp, float* dkvp, float* dhw_part,
                                int flags, hipStream_t s);
 bool rowln_splitk_supported(const mdg_gemm_desc& r, int S);
+bool rowln_bm32_supported(const mdg_gemm_desc& r);
+hipError_t rowln_bm32_launch(const mdg_gemm_desc& p, hipStream_t s);
 hipError_t rowln_splitk_launch(const mdg_gemm_desc& r, hipStream_t s, float* part, int S);
 bool final_euler_supported(const mdg_gemm_desc& p);
 hipError_t final_euler_launch(const mdg_gemm_desc& p, hipStream_t s);
@@ -267,6 +269,16 @@ bool small_m(long long N) { return (N + 127) / 128 < 64; }
 bool fused_qkv_on() {
   static const bool on = [] {
     const char* e = getenv("MDG_FUSED_QKV");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+// MDG_ROWLN_BM32=0: a lone chain's small-M out_proj row-LN GEMMs split over K (round 3) instead of
+// on 32-row tiles (A/B knob)
+bool rowln_bm32_on() {
+  static const bool on = [] {
+    const char* e = getenv("MDG_ROWLN_BM32");
     return !(e && e[0] == '0');
   }();
   return on;
@@ -583,6 +595,9 @@ static int layer_fwd_impl(const mdg_dims* d, const mdg_layer_weights* w, const f
     int S = 1;
     for (int d2 = 2; d2 <= smax && d2 <= lay.mlp_split; ++d2)
       if (12 % d2 == 0 && ((N + 127) / 128) * d2 <= 320) S = d2;
+    // a lone chain: 32-row tiles (4x the blocks, full K, no partials) before split-K (round 5)
+    if (small_m(N) && ho.alone && rowln_bm32_on() && mdg::rowln_bm32_supported(g))
+      return hip_check(mdg::rowln_bm32_launch(g, s), "rowln 32-row launch");
     if (small_m(N) && mdg::rowln_splitk_supported(g, S))
       return hip_check(mdg::rowln_splitk_launch(g, s, (float*)(wsb + lay.mlp_part), S), "rowln split-K launch");
     return mdg_gemm(&g, stream);

@@ -1026,6 +1026,9 @@ constexpr int kRowThreads = 512;
 template <int BM> struct RowCfg;
 template <> struct RowCfg<128> { static constexpr int WMW = 2, STAGES = 4; };
 template <> struct RowCfg<64> { static constexpr int WMW = 1, STAGES = 2; };
+// 32-row tiles (round 5): a lone chain's out_proj (B = 1 window: 125 tiles instead of 32, no
+// split-K partials or reduction pass); every wave 32 rows x 48 columns
+template <> struct RowCfg<32> { static constexpr int WMW = 1, STAGES = 2; };
 
 template <int NCOL, int BM>
 __host__ __device__ constexpr size_t rowln_smem() {
@@ -1239,8 +1242,9 @@ __device__ __forceinline__ void rowln_fast_epilogue(const mdg_gemm_desc& p, f32x
 // TRAIN (BM 128, every tile on the fast epilogue: rows_per_mod >= 128): the training forward's
 // out_proj / fc2 — residual read from resid_in, out of place; pre-gate value to aux; LN stats
 template <int NCOL, int BM, bool PART = false, bool TRAIN = false>
-__global__ __launch_bounds__(kRowThreads, BM == 64 ? 4 : 1) void gemm_rowln_kernel(const mdg_gemm_desc p) {
+__global__ __launch_bounds__(kRowThreads, BM <= 64 ? 4 : 1) void gemm_rowln_kernel(const mdg_gemm_desc p) {
   constexpr int kRowStages = RowCfg<BM>::STAGES, WMW = RowCfg<BM>::WMW, WNW = 8 / WMW;
+  constexpr int MI = BM >= 64 ? 4 : BM / 16;  // 16-row fragment tiles per wave
   constexpr int BK = 32, WTN = NCOL / WNW, NT = WTN / 16, ATILE = BM * BK, STAGE = (BM + NCOL) * BK;
   constexpr int LDS_ST = NCOL + 4, NE = NCOL / 128;  // float2 column pairs per lane per row
   constexpr int WLD = NCOL / 128;                    // W glds instructions per wave per stage
@@ -1321,12 +1325,12 @@ __global__ __launch_bounds__(kRowThreads, BM == 64 ? 4 : 1) void gemm_rowln_kern
   float2 hv[RG][NE], gv[NE];
   if (!PART) {
     if (fast) rowln_load_band<NCOL, RowsLinear, TRAIN>(p, RowsLinear{m0}, 0, h4);
-    else if (BM == 64) load_unit(0, hv, gv);
+    else if (BM <= 64) load_unit(0, hv, gv);
   }
 
-  f32x4 acc[4][NT];
+  f32x4 acc[MI][NT];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
@@ -1354,20 +1358,20 @@ __global__ __launch_bounds__(kRowThreads, BM == 64 ? 4 : 1) void gemm_rowln_kern
     const bf16_t* As = lds + (kt % kRowStages) * STAGE;
     const bf16_t* Bs = As + ATILE;
     const int ch = (lg ^ swz) * 8;
-    bf16x8 a[4], b[NT];
+    bf16x8 a[MI], b[NT];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) a[i] = *reinterpret_cast<const bf16x8*>(As + (wm * 64 + i * 16 + lr) * BK + ch);
+    for (int i = 0; i < MI; ++i) a[i] = *reinterpret_cast<const bf16x8*>(As + (wm * 64 + i * 16 + lr) * BK + ch);
 #pragma unroll
     for (int j = 0; j < NT; ++j) b[j] = *reinterpret_cast<const bf16x8*>(Bs + (wn * WTN + j * 16 + lr) * BK + ch);
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int j = 0; j < NT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
   }
 #undef MDG_ROW_LOAD
 
   if constexpr (PART) {
-    static_assert(BM == 128, "split-K form: 128-row tiles");
+    static_assert(BM == 128 && MI == 4, "split-K form: 128-row tiles");
     float* pp = reinterpret_cast<float*>(p.aux) + (size_t)blockIdx.y * M * NCOL;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -1408,7 +1412,7 @@ __global__ __launch_bounds__(kRowThreads, BM == 64 ? 4 : 1) void gemm_rowln_kern
   for (int band = 0; band < BM / 32; ++band) {
     if (wm == (band >> 1)) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {  // compile-time acc index; the band selects 2 of the 4
+      for (int i = 0; i < MI; ++i) {  // compile-time acc index; the band selects 2 of the 4
         if ((i >> 1) != (band & 1)) continue;
 #pragma unroll
         for (int j = 0; j < NT; ++j)
@@ -1539,6 +1543,17 @@ static hipError_t launch_rowln(const mdg_gemm_desc& p, hipStream_t s) {
                      (rowln_smem<NCOL, BM>()), s, p);
   return hipGetLastError();
 }
+
+// the 32-row tile form for a lone chain's small-M out_proj (mdg_denoise_step, chain_alone):
+// the fast path's envelope without its tile-height requirement (the general epilogue handles
+// tiles over any number of adaLN entries)
+bool rowln_bm32_supported(const mdg_gemm_desc& r) {
+  return r.dtype == MDG_BF16 && r.a_mode == MDG_A_PLAIN && r.epi == MDG_EPI_GATE_RES && r.N == 384 && r.K % 32 == 0 &&
+         r.K > 0 && r.M > 0 && r.resid && !r.resid_in && !r.aux && r.lda % 8 == 0 && r.ldw % 8 == 0 && r.ldr % 2 == 0 &&
+         (!r.xn_out || r.xn_mods);
+}
+
+hipError_t rowln_bm32_launch(const mdg_gemm_desc& p, hipStream_t s) { return launch_rowln<384, 32>(p, s); }
 
 static hipError_t launch_rowln_train(const mdg_gemm_desc& p, hipStream_t s) {
   static bool attr_set = false;

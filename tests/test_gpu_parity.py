@@ -293,12 +293,14 @@ def test_long_residue_axis_atlas_matches_oracle(T, L, n_pad, dtype):
     _check(v, ref, dtype, valid=inp["mask"][0, 0] > 0)
 
 
-@pytest.mark.parametrize("B,lanes", [(16, 2), (8, 1)])
+@pytest.mark.parametrize("B,lanes", [(16, 2), (8, 1), (1, 1)])
 def test_headline_route_T1000_matches_oracle(B, lanes):
     """The bench's own route (bf16, T=1000, L=4; B=16 as two lanes of 8, and B=8 as one chain):
     the 250-tile launches take the fused MLP (mlp_rowln_kernel) and the fused out_proj + q|k|v
-    (rowln_qkv_kernel).  One Euler step (num_steps=2, dt=1) through the captured window,
-    v = x_1 - x_0 against the oracle forward at t=0 for every trajectory, at the bf16 bounds."""
+    (rowln_qkv_kernel).  B = 1 (the bench's B = 1 window: a lone chain of 32 row tiles) takes the
+    small-M routes instead: the split MLP and the 32-row out_proj tiles.  One Euler step
+    (num_steps=2, dt=1) through the captured window, v = x_1 - x_0 against the oracle forward at
+    t=0 for every trajectory, at the bf16 bounds."""
     from mdgen_finetune_amd.engine import get_engine
     from mdgen_finetune_amd.rigid_utils import Rigid, Rotation
 
@@ -320,8 +322,11 @@ def test_headline_route_T1000_matches_oracle(B, lanes):
     eng = get_engine(m)
     eng.lanes = lanes
     plan = eng.describe_plan(B // lanes, T, 4)
-    assert plan["mlp"].startswith("mlp_fused(fc1+gelu+fc2"), plan
-    assert plan["temporal"].startswith("rowln_qkv"), plan
+    if B == 1:
+        assert plan["mlp"].startswith("mlp_fused(small M"), plan
+    else:
+        assert plan["mlp"].startswith("mlp_fused(fc1+gelu+fc2"), plan
+        assert plan["temporal"].startswith("rowln_qkv"), plan
     g = lambda k: f(k).cuda()  # noqa: E731
     kw = dict(mask=g("mask"), start_frames=Rigid(Rotation(rot_mats=g("rots")), g("trans")), x_cond=g("x_cond"),
               x_cond_mask=g("x_cond_mask"), aatype=g("aatype"))
