@@ -2193,6 +2193,105 @@ __global__ __launch_bounds__(256) void mlp_split_reduce_kernel(const mdg_gemm_de
   }
 }
 
+// The split passes' reduction, round 5: a row per half-wave (4 consecutive columns per lane,
+// 16-B loads: half the memory instructions of the float2 form), the residual / bias / gate rows
+// issued before the partials, the partials unrolled 4 deep.  The partial sum runs in split order
+// as before; the gated residual, the row statistics and the LN arithmetic are the row-LN fast
+// epilogue's (rowln_fast_epilogue_impl), so a small-M step rounds h and xn as the one-pass
+// launches do given the same fc2 / out_proj sums.
+template <int NCOL>
+__global__ __launch_bounds__(256) void split_reduce_rows_kernel(const mdg_gemm_desc p, const float* __restrict__ part,
+                                                                int nsplit) {
+#pragma clang fp contract(off)
+  constexpr int NE = NCOL / 128;
+  const int lane = threadIdx.x & 63, hl = lane & 31;
+  const int m = blockIdx.x * 8 + (threadIdx.x >> 5);  // 8 rows per block, one per half-wave
+  const int M = p.M;
+  const int mm = min(m, M - 1);
+  const size_t b = (size_t)(mm / p.rows_per_mod);
+  float4 h4[NE], b4[NE], g4[NE];
+  float* hr = p.resid + (size_t)mm * p.ldr;
+#pragma unroll
+  for (int e = 0; e < NE; ++e) {
+    const int k = 4 * hl + 128 * e;
+    h4[e] = *reinterpret_cast<const float4*>(hr + k);
+    b4[e] = p.bias ? *reinterpret_cast<const float4*>(p.bias + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+    g4[e] = p.gate ? *reinterpret_cast<const float4*>(p.gate + b * p.mod_stride + p.gate_off + k)
+                   : make_float4(1.f, 1.f, 1.f, 1.f);
+  }
+  float4 v[NE];
+#pragma unroll
+  for (int e = 0; e < NE; ++e) v[e] = make_float4(0.f, 0.f, 0.f, 0.f);
+  const float* pr0 = part + (size_t)mm * NCOL + 4 * hl;
+#pragma unroll 4
+  for (int sp = 0; sp < nsplit; ++sp)
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+      const float4 t = *reinterpret_cast<const float4*>(pr0 + (size_t)sp * M * NCOL + 128 * e);
+      v[e].x += t.x;
+      v[e].y += t.y;
+      v[e].z += t.z;
+      v[e].w += t.w;
+    }
+  float sacc = 0.f;
+#pragma unroll
+  for (int e = 0; e < NE; ++e) {
+    float4& h = h4[e];
+    h.x += g4[e].x * (v[e].x + b4[e].x);
+    h.y += g4[e].y * (v[e].y + b4[e].y);
+    h.z += g4[e].z * (v[e].z + b4[e].z);
+    h.w += g4[e].w * (v[e].w + b4[e].w);
+    sacc += (h.x + h.y) + (h.z + h.w);
+  }
+  if (m < M) {
+#pragma unroll
+    for (int e = 0; e < NE; ++e) *reinterpret_cast<float4*>(hr + 4 * hl + 128 * e) = h4[e];
+  }
+  if (!p.xn_out) return;
+  const float invN = 1.0f / (float)NCOL;
+#pragma unroll
+  for (int o = 16; o >= 1; o >>= 1) sacc += __shfl_xor(sacc, o, 64);
+  const float mean = sacc * invN;
+  float t = 0.f;
+#pragma unroll
+  for (int e = 0; e < NE; ++e) {
+    const float4 h = h4[e];
+    const float a0 = h.x - mean, a1 = h.y - mean, a2 = h.z - mean, a3 = h.w - mean;
+    t += (a0 * a0 + a1 * a1) + (a2 * a2 + a3 * a3);
+  }
+#pragma unroll
+  for (int o = 16; o >= 1; o >>= 1) t += __shfl_xor(t, o, 64);
+  const float rs = 1.0f / sqrtf(t * invN + p.ln_eps);
+  if (m >= M) return;
+  const float* mr = p.xn_mods + b * p.xn_mod_stride;
+#pragma unroll
+  for (int e = 0; e < NE; ++e) {
+    const int k = 4 * hl + 128 * e;
+    const float4 xs = *reinterpret_cast<const float4*>(mr + p.xn_scale_off + k);
+    const float4 xh = *reinterpret_cast<const float4*>(mr + p.xn_shift_off + k);
+    const float4 h = h4[e];
+    st4<bf16_t>(reinterpret_cast<bf16_t*>(p.xn_out) + (size_t)m * NCOL + k, (h.x - mean) * rs * (1.0f + xs.x) + xh.x,
+                (h.y - mean) * rs * (1.0f + xs.y) + xh.y, (h.z - mean) * rs * (1.0f + xs.z) + xh.z,
+                (h.w - mean) * rs * (1.0f + xs.w) + xh.w);
+  }
+}
+
+// the split passes' reduction launch (MDG_SPLIT_REDUCE=0 or a diagnostic ORDER build: the
+// round-3 float2 kernel)
+static hipError_t launch_split_reduce(const mdg_gemm_desc& p, const float* part, int S, hipStream_t s) {
+  static const bool rows4 = [] {
+    const char* e = getenv("MDG_SPLIT_REDUCE");
+    return !(e && e[0] == '0');
+  }();
+  if (rows4 && !MDG_DIAG_ORDER && p.ldr % 4 == 0 && (!p.xn_out || (p.xn_mod_stride % 4 == 0 && p.xn_scale_off % 4 == 0 &&
+                                                                  p.xn_shift_off % 4 == 0)) &&
+      (!p.gate || (p.mod_stride % 4 == 0 && p.gate_off % 4 == 0)))
+    hipLaunchKernelGGL((split_reduce_rows_kernel<384>), dim3((p.M + 7) / 8), dim3(256), 0, s, p, part, S);
+  else
+    hipLaunchKernelGGL((mlp_split_reduce_kernel<384>), dim3((p.M + 3) / 4), dim3(256), 0, s, p, part, S);
+  return hipGetLastError();
+}
+
 // ---------------------------------------------------------------------------------------
 // FinalLayer + Euler update of the bf16 denoise step (layers.py:58-75 then
 // integrators.py:106-113): v = xn . W^T + b, x_out = x_in + dt * v for latent <= 32 columns.
@@ -2383,9 +2482,7 @@ hipError_t mlp_fused_launch(const mdg_gemm_desc& f1, const mdg_gemm_desc& f2, hi
   if (a.nsplit > 1) {
     hipLaunchKernelGGL((mlp_rowln_kernel<384, true>), dim3(tiles, a.nsplit), dim3(kMlpThreads), mlp_smem(f1.N), s, a);
     if (hipError_t e = hipGetLastError()) return e;
-    hipLaunchKernelGGL((mlp_split_reduce_kernel<384>), dim3((f1.M + 3) / 4), dim3(256), 0, s, f2, (const float*)part,
-                       a.nsplit);
-    return hipGetLastError();
+    return launch_split_reduce(f2, (const float*)part, a.nsplit, s);
   }
   if (mlp_ws_on()) {
     hipLaunchKernelGGL((mlp_ws_kernel<384>), dim3(tiles), dim3(kWsThreads), kWsSmem, s, a);
@@ -2418,8 +2515,7 @@ hipError_t rowln_splitk_launch(const mdg_gemm_desc& r, hipStream_t s, float* par
   hipLaunchKernelGGL((gemm_rowln_kernel<384, 128, true>), dim3((r.M + 127) / 128, S), dim3(kRowThreads),
                      (rowln_smem<384, 128>()), s, rp);
   if (hipError_t e = hipGetLastError()) return e;
-  hipLaunchKernelGGL((mlp_split_reduce_kernel<384>), dim3((r.M + 3) / 4), dim3(256), 0, s, r, (const float*)part, S);
-  return hipGetLastError();
+  return launch_split_reduce(r, (const float*)part, S, s);
 }
 
 // ---------------------------------------------------------------------------------------
