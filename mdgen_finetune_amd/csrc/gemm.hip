@@ -1335,11 +1335,39 @@ __global__ __launch_bounds__(kRowThreads, BM <= 64 ? 4 : 1) void gemm_rowln_kern
     for (int j = 0; j < NT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = (PART ? K / (int)gridDim.y : K) / BK, kbeg = PART ? (int)blockIdx.y * nk * BK : 0;
+  // 32-row tiles (a lone chain's small-M launch, W-stream bound: 24 KiB of W per 2 KiB of A per
+  // step): the pieces go global -> VGPRs -> ds_write_b128 into the same LDS image, the next
+  // step's loaded under this step's MFMAs (plain loads fill ~3x faster than LDS-DMA per CU,
+  // tools/ubench/l2lds.hip)
+  constexpr bool VST = BM == 32;
+  u32x4 vr[1 + WLD];
+  auto vload = [&](int k0) {
+    if (has_a) vr[0] = *reinterpret_cast<const u32x4*>(asrc + k0);
 #pragma unroll
-  for (int s0 = 0; s0 < kRowStages - 1; ++s0)
-    if (s0 < nk) MDG_ROW_LOAD(s0, kbeg + s0 * BK);
+    for (int i = 0; i < WLD; ++i) vr[1 + i] = *reinterpret_cast<const u32x4*>(bsrc[i] + k0);
+  };
+  auto vstore = [&](int st) {
+    bf16_t* sa = lds + st * STAGE;
+    if (has_a) *reinterpret_cast<u32x4*>(sa + 16 * wave * BK + 8 * lane) = vr[0];
+#pragma unroll
+    for (int i = 0; i < WLD; ++i) *reinterpret_cast<u32x4*>(sa + ATILE + 16 * (wave * WLD + i) * BK + 8 * lane) = vr[1 + i];
+  };
+  if constexpr (VST) {
+    vload(kbeg);
+    vstore(0);
+  } else {
+#pragma unroll
+    for (int s0 = 0; s0 < kRowStages - 1; ++s0)
+      if (s0 < nk) MDG_ROW_LOAD(s0, kbeg + s0 * BK);
+  }
   const int swz = (-(lr >> 2)) & 3;
   for (int kt = 0; kt < nk; ++kt) {
+    if constexpr (VST) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this stage's writes, the last stage's reads
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (kt + 1 < nk) vload(kbeg + (kt + 1) * BK);
+    } else {
     // stage kt landed: leave the (up to 2) younger stages' loads in flight
     const int younger = min(kRowStages - 2, nk - 1 - kt);
     if (has_a) {
@@ -1355,6 +1383,7 @@ __global__ __launch_bounds__(kRowThreads, BM <= 64 ? 4 : 1) void gemm_rowln_kern
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (kt + kRowStages - 1 < nk) MDG_ROW_LOAD((kt + kRowStages - 1) % kRowStages, kbeg + (kt + kRowStages - 1) * BK);
+    }
     const bf16_t* As = lds + (kt % kRowStages) * STAGE;
     const bf16_t* Bs = As + ATILE;
     const int ch = (lg ^ swz) * 8;
@@ -1367,6 +1396,8 @@ __global__ __launch_bounds__(kRowThreads, BM <= 64 ? 4 : 1) void gemm_rowln_kern
     for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int j = 0; j < NT; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    if constexpr (VST)
+      if (kt + 1 < nk) vstore((kt + 1) % kRowStages);
   }
 #undef MDG_ROW_LOAD
 
@@ -1594,8 +1625,8 @@ struct MlpArgs {
 #endif
 constexpr int kMlpThreads = 512, kMlpHC = 128, kMlpStages = 3, kMlpSlot = 512 * 32;
 
-__host__ __device__ constexpr size_t mlp_smem(int F) {
-  return (size_t)kMlpStages * kMlpSlot * 2 + (size_t)128 * kMlpHC * 2 + (size_t)F * 4;
+__host__ __device__ constexpr size_t mlp_smem(int F, bool vst = false) {
+  return (size_t)(vst ? 2 : kMlpStages) * kMlpSlot * 2 + (size_t)128 * kMlpHC * 2 + (size_t)F * 4;
 }
 
 // LDS accesses the compiler's wait-count pass does not see.  It makes every LDS access that
@@ -1656,10 +1687,16 @@ __device__ __forceinline__ void vm_wait_upto6(int n) {
 // for bit.  The block's h / xn rows are then read back by the MLP below (ring DMA for xn, the
 // residual load for h): ordered by a work-group barrier with release / acquire at work-group
 // scope (one CU, one L1).  Saves the out_proj launch, its grid tail and the xn HBM round trip.
-template <int NCOL, bool SPLIT, bool PRE = false>  // SPLIT: chunks [y * cps, (y + 1) * cps) only, fp32 partials out
+// VST (round 5; the small-M split form): the operand pieces go global -> VGPRs ->
+// ds_write_b128 into the same LDS image instead of global_load_lds, two steps ahead in two
+// register sets, two LDS slots.  A split block streams ~576 KiB of operands for 2 hidden chunks
+// of 128 rows; LDS-DMA fills ~16 B/clk per CU, plain loads ~3x that (tools/ubench/l2lds.hip).
+// (Built for the one-pass form too and measured equal there, round 5 DESIGN §3.)
+template <int NCOL, bool SPLIT, bool PRE = false, bool VST = false>  // SPLIT: chunks [y * cps, (y + 1) * cps) only, fp32 partials out
 __global__ __launch_bounds__(kMlpThreads, 1) void mlp_rowln_kernel(const MlpArgs args) {
   static_assert(NCOL == 384, "the ring slot holds 384 W2 rows");
-  constexpr int BM = 128, BK = 32, HC = kMlpHC, STAGES = kMlpStages, SLOT = kMlpSlot;
+  static_assert(!(PRE && VST), "the out_proj prologue stages by DMA");
+  constexpr int BM = 128, BK = 32, HC = kMlpHC, STAGES = VST ? 2 : kMlpStages, SLOT = kMlpSlot;
   constexpr int WTN = NCOL / 4, NT = WTN / 16, NE = NCOL / 128, LDS_ST = NCOL + 4;
   static_assert((32 * LDS_ST + 6 * NCOL) * 4 <= STAGES * SLOT * 2, "epilogue stage + adaLN rows fit the ring");
   typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -1782,6 +1819,48 @@ __global__ __launch_bounds__(kMlpThreads, 1) void mlp_rowln_kernel(const MlpArgs
     }
   };
 
+  // VST: the same pieces (source address, LDS destination) through 16-B register loads; two
+  // named register sets picked by the step's parity (a uniform branch; no indexed register
+  // array, which the compiler would put in scratch)
+  u32x4 vA[4], vB[4];
+  // K: the step's kind as a compile-time constant (0: fc1 step, 1: fc2 step)
+  auto vload_set = [&](auto K, int s, u32x4(&vr)[4]) __attribute__((always_inline)) {
+    const int j = j0 + s / 10, t = s % 10;
+    if constexpr (!decltype(K)::value) {
+      const bf16_t* base = abase + (size_t)t * 2 * BK + (xw ? (size_t)0 : (size_t)j * HC * q.ldw);
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) vr[2 * h + i] = *reinterpret_cast<const u32x4*>(base + h * BK + aoff[i]);
+    } else {
+      const bf16_t* base = W2 + j * HC + (t - 6) * BK;
+#pragma unroll
+      for (int i = 0; i < 3; ++i) vr[i] = *reinterpret_cast<const u32x4*>(base + boff + i * bstep);
+    }
+  };
+  auto vload = [&](auto P, auto K, int s) __attribute__((always_inline)) {
+    if constexpr (decltype(P)::value) vload_set(K, s, vB);
+    else vload_set(K, s, vA);
+  };
+  auto vcommit_set = [&](auto K, int s, const u32x4(&vr)[4]) __attribute__((always_inline)) {
+    bf16_t* sl = ring + (s % STAGES) * SLOT;
+    if constexpr (!decltype(K)::value) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          *reinterpret_cast<u32x4*>(sl + h * IMG + ((xw ? 0 : BM) + 16 * (2 * (wave & 3) + i)) * BK + 8 * lane) =
+              vr[2 * h + i];
+    } else {
+#pragma unroll
+      for (int i = 0; i < 3; ++i) *reinterpret_cast<u32x4*>(sl + 16 * (3 * wave + i) * BK + 8 * lane) = vr[i];
+    }
+  };
+  auto vcommit = [&](auto P, auto K, int s) __attribute__((always_inline)) {
+    if constexpr (decltype(P)::value) vcommit_set(K, s, vB);
+    else vcommit_set(K, s, vA);
+  };
+
   const int ch = (lg ^ ((-(lr >> 2)) & 3)) * 8;
   f32x4 acc2[4][NT], acc1[4][2];
 #pragma unroll
@@ -1791,12 +1870,25 @@ __global__ __launch_bounds__(kMlpThreads, 1) void mlp_rowln_kernel(const MlpArgs
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc1[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
+  using P0 = std::integral_constant<int, 0>;
+  using P1 = std::integral_constant<int, 1>;
+  if constexpr (VST) {  // steps 0 and 1 are fc1 steps
+    vload(P0{}, P0{}, 0);
+    vcommit(P0{}, P0{}, 0);
+    if (1 < NS) vload(P1{}, P0{}, 1);
+  } else {
 #pragma unroll
-  for (int s0 = 0; s0 < STAGES - 1; ++s0)
-    if (s0 < NS) issue(s0);
-  // step s landed: leave step s+1's pieces in flight; then refill the slot every wave has
-  // finished reading (step s-1's) with step s+2
+    for (int s0 = 0; s0 < STAGES - 1; ++s0)
+      if (s0 < NS) issue(s0);
+  }
+  // DMA: step s landed: leave step s+1's pieces in flight; then refill the slot every wave has
+  // finished reading (step s-1's) with step s+2.  VST: slot s % 2 was written before this
+  // barrier; step s + 2's pieces are loaded here (into the set step s's pieces left), step
+  // s + 1's written after step s's MFMAs (step_end).
   auto step_begin = [&](int s) {
+    if constexpr (VST) {  // (the VST loops call vstep_begin below instead)
+      return ring + (s % STAGES) * SLOT;
+    }
     const int y1 = s + 1 < NS ? ((s + 1) % 10 < 6 ? 4 : 3) : 0;
     vm_wait_upto6(y1);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // ring reads retired (see kRingWaitNote)
@@ -1805,6 +1897,100 @@ __global__ __launch_bounds__(kMlpThreads, 1) void mlp_rowln_kernel(const MlpArgs
     if (s + STAGES - 1 < NS) issue(s + STAGES - 1);
     return ring + (s % STAGES) * SLOT;
   };
+  if constexpr (VST) {
+    // every step of a chunk spelled out with its index as a compile-time constant, so each call
+    // site knows the register set (parity) and the kind of the steps it loads and writes
+    // (step j * 10 + t: t < 6 fc1, else fc2; the chunk's step count, 10, is even)
+    auto vstep_begin = [&](auto P, auto K2, int s) __attribute__((always_inline)) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // slot writes and ring reads retired
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (s + 2 < NS) vload(P, K2, s + 2);  // into the set step s's pieces left
+      return ring + (s % STAGES) * SLOT;
+    };
+    auto step = [&](auto TT, int j) __attribute__((always_inline)) {
+      constexpr int t = decltype(TT)::value;
+      using P = std::integral_constant<int, t & 1>;
+      using Pn = std::integral_constant<int, (t + 1) & 1>;
+      using Kn = std::integral_constant<int, ((t + 1) % 10) >= 6 ? 1 : 0>;  // step s + 1's kind
+      using K2 = std::integral_constant<int, ((t + 2) % 10) >= 6 ? 1 : 0>;  // step s + 2's kind
+      const int s = j * 10 + t;
+      const bf16_t* sl = vstep_begin(P{}, K2{}, s);
+      if constexpr (t < 6) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          bf16x8 a[4], b[2];
+#pragma unroll
+          for (int hi = 0; hi < 4; ++hi)
+            a[hi] = *reinterpret_cast<const bf16x8*>(sl + h * IMG + (BM + wah * 64 + hi * 16 + lr) * BK + ch);
+#pragma unroll
+          for (int ti = 0; ti < 2; ++ti)
+            b[ti] = *reinterpret_cast<const bf16x8*>(sl + h * IMG + (wat * 32 + ti * 16 + lr) * BK + ch);
+#pragma unroll
+          for (int hi = 0; hi < 4; ++hi)
+#pragma unroll
+            for (int ti = 0; ti < 2; ++ti)
+              acc1[hi][ti] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[hi], b[ti], acc1[hi][ti], 0, 0, 0);
+        }
+      } else {
+        constexpr int kb = t - 6;
+        bf16x8 a[4], b[NT];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = wm * 64 + i * 16 + lr;
+          a[i] = *reinterpret_cast<const bf16x8*>(Hs + row * HC + (((kb * 4 + lg) ^ (row & 15)) * 8));
+        }
+#pragma unroll
+        for (int jn = 0; jn < NT; ++jn) b[jn] = *reinterpret_cast<const bf16x8*>(sl + (wn * WTN + jn * 16 + lr) * BK + ch);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int jn = 0; jn < NT; ++jn) acc2[i][jn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[jn], acc2[i][jn], 0, 0, 0);
+      }
+      if (s + 1 < NS) vcommit(Pn{}, Kn{}, s + 1);
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using I3 = std::integral_constant<int, 3>;
+    using I4 = std::integral_constant<int, 4>;
+    using I5 = std::integral_constant<int, 5>;
+    using I6 = std::integral_constant<int, 6>;
+    using I7 = std::integral_constant<int, 7>;
+    using I8 = std::integral_constant<int, 8>;
+    using I9 = std::integral_constant<int, 9>;
+    for (int j = 0; j < NS / 10; ++j) {
+      step(I0{}, j);
+      step(I1{}, j);
+      step(I2{}, j);
+      step(I3{}, j);
+      step(I4{}, j);
+      step(I5{}, j);
+      // the chunk's fc1 is complete: + b1, GELU, bf16 -> Hs; restart acc1
+      const float* b1c = b1s + (j0 + j) * HC;
+      f32x4 b1v[4];
+      {
+        const float* bp = b1c + wah * 64 + lg * 4;
+        lds_ld4x4_raw(bp, bp + 16, bp + 32, bp + 48, b1v[0], b1v[1], b1v[2], b1v[3]);
+      }
+#pragma unroll
+      for (int hi = 0; hi < 4; ++hi)
+#pragma unroll
+        for (int ti = 0; ti < 2; ++ti) {
+          const int hb = wah * 64 + hi * 16 + lg * 4, tok = wat * 32 + ti * 16 + lr;
+          bf16x4 o;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] = (bf16_t)gelu_fast(acc1[hi][ti][r] + b1v[hi][r]);
+          *reinterpret_cast<bf16x4*>(Hs + tok * HC + (((hb >> 3) ^ (tok & 15)) * 8) + (hb & 7)) = o;
+          acc1[hi][ti] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // Hs complete before the next barrier
+      step(I6{}, j);
+      step(I7{}, j);
+      step(I8{}, j);
+      step(I9{}, j);
+    }
+  } else {
   // (the fc1 and fc2 step bodies are separate loops: one loop with a branch per step made the
   // compiler give the accumulators different registers on the two paths)
   for (int j = 0; j < NS / 10; ++j) {
@@ -1860,6 +2046,7 @@ __global__ __launch_bounds__(kMlpThreads, 1) void mlp_rowln_kernel(const MlpArgs
 #pragma unroll
         for (int jn = 0; jn < NT; ++jn) acc2[i][jn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[jn], acc2[i][jn], 0, 0, 0);
     }
+  }
   }
   if constexpr (SPLIT) {
     // this block's fc2 partial sum: 16 consecutive columns (64 B) per 16-lane group and register
@@ -2432,6 +2619,15 @@ int mlp_split_factor(int M, int F) {
   return best;
 }
 
+// MDG_MLP_SPLIT_VST=0: the small-M split MLP stages its operands by LDS-DMA (A/B knob)
+static bool mlp_split_vst_on() {
+  static const bool on = [] {
+    const char* e = getenv("MDG_MLP_SPLIT_VST");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 // MDG_MLP_WS=1 selects the wave-specialised kernel for large M (A/B knob; off by default: it
 // measured 168 vs 130 us at M = 32 000 — each phase's 48 KiB ring slot is issued only one
 // phase (~0.7 us) ahead of its use while an LDS-DMA fill takes ~1.1 us to land, and LDS has no
@@ -2461,6 +2657,7 @@ hipError_t mlp_fused_launch(const mdg_gemm_desc& f1, const mdg_gemm_desc& f2, hi
     for (const void* k : {reinterpret_cast<const void*>(&mlp_rowln_kernel<384, false>),
                           reinterpret_cast<const void*>(&mlp_rowln_kernel<384, true>),
                           reinterpret_cast<const void*>(&mlp_rowln_kernel<384, false, true>),
+                          reinterpret_cast<const void*>(&mlp_rowln_kernel<384, true, false, true>),
                           reinterpret_cast<const void*>(&mlp_ws_kernel<384>)}) {
       hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       if (e != hipSuccess) return e;
@@ -2480,7 +2677,11 @@ hipError_t mlp_fused_launch(const mdg_gemm_desc& f1, const mdg_gemm_desc& f2, hi
     return hipGetLastError();
   }
   if (a.nsplit > 1) {
-    hipLaunchKernelGGL((mlp_rowln_kernel<384, true>), dim3(tiles, a.nsplit), dim3(kMlpThreads), mlp_smem(f1.N), s, a);
+    if (mlp_split_vst_on())
+      hipLaunchKernelGGL((mlp_rowln_kernel<384, true, false, true>), dim3(tiles, a.nsplit), dim3(kMlpThreads),
+                         mlp_smem(f1.N, true), s, a);
+    else
+      hipLaunchKernelGGL((mlp_rowln_kernel<384, true>), dim3(tiles, a.nsplit), dim3(kMlpThreads), mlp_smem(f1.N), s, a);
     if (hipError_t e = hipGetLastError()) return e;
     return launch_split_reduce(f2, (const float*)part, a.nsplit, s);
   }
