@@ -2628,6 +2628,15 @@ static bool mlp_split_vst_on() {
   return on;
 }
 
+// MDG_MLP_VST=1: the one-pass fused MLP with register staging too (A/B knob)
+static bool mlp_vst_on() {
+  static const bool on = [] {
+    const char* e = getenv("MDG_MLP_VST");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
 // MDG_MLP_WS=1 selects the wave-specialised kernel for large M (A/B knob; off by default: it
 // measured 168 vs 130 us at M = 32 000 — each phase's 48 KiB ring slot is issued only one
 // phase (~0.7 us) ahead of its use while an LDS-DMA fill takes ~1.1 us to land, and LDS has no
@@ -2658,6 +2667,7 @@ hipError_t mlp_fused_launch(const mdg_gemm_desc& f1, const mdg_gemm_desc& f2, hi
                           reinterpret_cast<const void*>(&mlp_rowln_kernel<384, true>),
                           reinterpret_cast<const void*>(&mlp_rowln_kernel<384, false, true>),
                           reinterpret_cast<const void*>(&mlp_rowln_kernel<384, true, false, true>),
+                          reinterpret_cast<const void*>(&mlp_rowln_kernel<384, false, false, true>),
                           reinterpret_cast<const void*>(&mlp_ws_kernel<384>)}) {
       hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       if (e != hipSuccess) return e;
@@ -2689,7 +2699,11 @@ hipError_t mlp_fused_launch(const mdg_gemm_desc& f1, const mdg_gemm_desc& f2, hi
     hipLaunchKernelGGL((mlp_ws_kernel<384>), dim3(tiles), dim3(kWsThreads), kWsSmem, s, a);
     return hipGetLastError();
   }
-  hipLaunchKernelGGL((mlp_rowln_kernel<384, false>), dim3(tiles), dim3(kMlpThreads), mlp_smem(f1.N), s, a);
+  if (mlp_vst_on())
+    hipLaunchKernelGGL((mlp_rowln_kernel<384, false, false, true>), dim3(tiles), dim3(kMlpThreads), mlp_smem(f1.N, true),
+                       s, a);
+  else
+    hipLaunchKernelGGL((mlp_rowln_kernel<384, false>), dim3(tiles), dim3(kMlpThreads), mlp_smem(f1.N), s, a);
   return hipGetLastError();
 }
 
