@@ -1691,7 +1691,7 @@ __device__ __forceinline__ void vm_wait_upto6(int n) {
 // ds_write_b128 into the same LDS image instead of global_load_lds, two steps ahead in two
 // register sets, two LDS slots.  A split block streams ~576 KiB of operands for 2 hidden chunks
 // of 128 rows; LDS-DMA fills ~16 B/clk per CU, plain loads ~3x that (tools/ubench/l2lds.hip).
-// (Built for the one-pass form too and measured equal there, round 5 DESIGN §3.)
+// (The one-pass form with VST measured equal, round 5 DESIGN §3, and is not instantiated.)
 template <int NCOL, bool SPLIT, bool PRE = false, bool VST = false>  // SPLIT: chunks [y * cps, (y + 1) * cps) only, fp32 partials out
 __global__ __launch_bounds__(kMlpThreads, 1) void mlp_rowln_kernel(const MlpArgs args) {
   static_assert(NCOL == 384, "the ring slot holds 384 W2 rows");
@@ -2628,15 +2628,6 @@ static bool mlp_split_vst_on() {
   return on;
 }
 
-// MDG_MLP_VST=1: the one-pass fused MLP with register staging too (A/B knob)
-static bool mlp_vst_on() {
-  static const bool on = [] {
-    const char* e = getenv("MDG_MLP_VST");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
-
 // MDG_MLP_WS=1 selects the wave-specialised kernel for large M (A/B knob; off by default: it
 // measured 168 vs 130 us at M = 32 000 — each phase's 48 KiB ring slot is issued only one
 // phase (~0.7 us) ahead of its use while an LDS-DMA fill takes ~1.1 us to land, and LDS has no
@@ -2667,7 +2658,6 @@ hipError_t mlp_fused_launch(const mdg_gemm_desc& f1, const mdg_gemm_desc& f2, hi
                           reinterpret_cast<const void*>(&mlp_rowln_kernel<384, true>),
                           reinterpret_cast<const void*>(&mlp_rowln_kernel<384, false, true>),
                           reinterpret_cast<const void*>(&mlp_rowln_kernel<384, true, false, true>),
-                          reinterpret_cast<const void*>(&mlp_rowln_kernel<384, false, false, true>),
                           reinterpret_cast<const void*>(&mlp_ws_kernel<384>)}) {
       hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       if (e != hipSuccess) return e;
@@ -2699,11 +2689,7 @@ hipError_t mlp_fused_launch(const mdg_gemm_desc& f1, const mdg_gemm_desc& f2, hi
     hipLaunchKernelGGL((mlp_ws_kernel<384>), dim3(tiles), dim3(kWsThreads), kWsSmem, s, a);
     return hipGetLastError();
   }
-  if (mlp_vst_on())
-    hipLaunchKernelGGL((mlp_rowln_kernel<384, false, false, true>), dim3(tiles), dim3(kMlpThreads), mlp_smem(f1.N, true),
-                       s, a);
-  else
-    hipLaunchKernelGGL((mlp_rowln_kernel<384, false>), dim3(tiles), dim3(kMlpThreads), mlp_smem(f1.N), s, a);
+  hipLaunchKernelGGL((mlp_rowln_kernel<384, false>), dim3(tiles), dim3(kMlpThreads), mlp_smem(f1.N), s, a);
   return hipGetLastError();
 }
 
