@@ -194,7 +194,8 @@ def test_hip_layer_backward_default_dims_multi_chunk(dtype, T, n_pad):
     temporal attention backward runs 2, 3 and 8 chunks of 128 keys / queries with tails
     (T = 129, 257, 1000), one trajectory, against eager autograd of the same module.  Also
     pads frames at the end of the trajectory for one residue (temporal key padding across the
-    last chunk) besides the padded residue.  Bounds as the layer test above."""
+    last chunk) besides the padded residue.  Bounds as the layer test above; the f32 path is
+    measured against an fp64 eager run (eager f32's own drift from it is logged beside)."""
     import argparse
 
     from mdgen_finetune_amd import synthetic
@@ -219,20 +220,42 @@ def test_hip_layer_backward_default_dims_multi_chunk(dtype, T, n_pad):
     out = hip_layer_forward(hl, layer, h, layer.adaLN_modulation(c), mask)
     gots = torch.autograd.grad(out, [h, c] + list(layer.parameters()), gout)
     tol = 1e-4 if dtype == "f32" else 2.6e-2
-    fwd = float((out - out_ref).norm() / out_ref.norm())
     names = ["h", "c"] + [n for n, _ in layer.named_parameters()]
-    worst, errs = (fwd, "forward"), {}
-    for n, a, b in zip(names, gots, refs):
+    refs32 = refs
+    if dtype == "f32":
+        # The f32 path is judged against an fp64 eager run of the same layer: bias_k's gradient is
+        # a sum over all T*L queries of dS rows that sum to ~0, so eager f32 itself drifts ~1e-5
+        # from the exact value at T = 1000 and would eat most of a 1e-4 bound.
+        import copy
+
+        l64 = copy.deepcopy(layer).double()
+        h64 = h.detach().double().requires_grad_(True)
+        c64 = c.detach().double().requires_grad_(True)
+        out_ref = l64(h64, c64[:, None], mask.double())
+        refs = torch.autograd.grad(out_ref, [h64, c64] + list(l64.parameters()), gout.double())
+    fwd = float((out.double() - out_ref.double()).norm() / out_ref.double().norm())
+    worst, errs, eager = (fwd, "forward"), {}, {}
+    for n, a, b, b32 in zip(names, gots, refs, refs32):
         if b is None or float(b.norm()) == 0:
             continue
         assert torch.isfinite(a).all(), n
-        rel = float((a.float() - b).norm() / b.norm())
+        b = b.double()
+        rel = float((a.double() - b).norm() / b.norm())
         errs[n] = rel
+        eager[n] = float((b32.double() - b).norm() / b.norm())
         worst = max(worst, (rel, n))
-    _log_train({"test": "layer_bwd_default_dims", "dtype": dtype, "T": T, "L": L, "n_pad": n_pad, "fwd_rel": fwd,
-                "worst_rel": worst[0], "worst": worst[1],
-                "attn_t": max(v for k, v in errs.items() if k.startswith("mha_t"))})
+    rec = {"test": "layer_bwd_default_dims", "dtype": dtype, "T": T, "L": L, "n_pad": n_pad, "fwd_rel": fwd,
+           "worst_rel": worst[0], "worst": worst[1],
+           "attn_t": max(v for k, v in errs.items() if k.startswith("mha_t"))}
+    if dtype == "f32":
+        rec["vs"] = "eager fp64"
+        rec["eager_f32_worst_rel"] = max(eager.values())
+        rec["eager_f32_bias_k_rel"] = eager.get("mha_t.attn.bias_k")
+        rec["hip_bias_k_rel"] = errs.get("mha_t.attn.bias_k")
+    _log_train(rec)
     assert worst[0] <= tol, worst
+    if dtype == "f32":  # and no worse than eager f32's own distance from fp64 (x1.12 measured at T = 1000)
+        assert worst[0] <= max(2.0 * rec["eager_f32_worst_rel"], 1e-5), rec
 
 
 def _default_dims_case(B=2, T=64, L=4, seed=31):
