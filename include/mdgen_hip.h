@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define MDG_ABI_VERSION 22
+#define MDG_ABI_VERSION 23
 #define MDG_MAX_LAYERS 16
 #define MDG_SEG_MAX 16 /* segments of one mdg_seg_linear */
 #define MDG_DP 32      /* padded head dim of the attention operand buffers for head_dim <= 31 */
@@ -316,7 +316,7 @@ typedef struct {
   const float* head_weights; /* raw ipa.head_weights [H] (softplus applied on the device) */
   const float* w_out; const float* b_out; /* linear_out [C][K_pad], K = H*(c + 4*P_v) zero-padded to 64k */
   const float* wqkv; const float* bqkv;   /* mha_l q|k|v [3C][C] / [3C] packed as mdg_layer_weights */
-  const float* kvb;                        /* [H][2][32] as mdg_layer_weights (position L) */
+  const float* kvb;                        /* [H][2][MDG_HEAD_STRIDE(D)] as mdg_layer_weights (position L) */
   const float* wo; const float* bo;        /* out_proj */
   const float* w1; const float* b1; const float* w2; const float* b2; /* fc1 [4C][C], fc2 [C][4C] */
 } mdg_ipa_layer_weights;
@@ -377,9 +377,10 @@ typedef struct {
                         q|k|v and fc1 GEMMs */
   float* stats[3];   /* [N][2] (mean, rstd) of those three LayerNorms */
   void* qkv_s;       /* L < 16: CT [N][3C] spatial q|k|v (q scaled, q / k RoPE-rotated, packed
-                        order); L >= 16: CT [3][B*T][H][L][32] planes (k, v pad column D = 1) */
+                        order); L >= 16: CT [3][B*T][H][L][DP] planes (k, v pad column D = 1;
+                        DP = MDG_HEAD_STRIDE(D) here and below) */
   float* lse_s;      /* L >= 16: [B*T][H][L] log2-sum-exp2 of the spatial softmax rows */
-  void* qkv_t;       /* CT [3][B*L][H][T][32] temporal q|k|v planes (k, v pad column D = 1) */
+  void* qkv_t;       /* CT [3][B*L][H][T][DP] temporal q|k|v planes (k, v pad column D = 1) */
   float* lse_t;      /* [B*L][H][T] */
   void* o[2];        /* CT [N][C] attention outputs: spatial, temporal */
   void* o_lo[2];     /* bf16 only (else null): CT [N][C] rounding residuals O - bf16(O) of the
@@ -438,26 +439,28 @@ int mdg_ln_gate_bwd(int32_t dtype, int32_t M, int32_t C, int32_t rows_per_b, con
    sequence, ABI 21). */
 int32_t mdg_attn_temporal_bwd_parts(int32_t dtype, int32_t B, int32_t T, int32_t L, int32_t generic);
 int32_t mdg_attn_spatial_bwd_parts(int32_t n_frames, int32_t L, int32_t D);
-/* Scratch of mdg_attn_temporal_bwd: dO planes CT [B*L][H][T][32], delta fp32 [B*L][H][T], and
-   for bf16 with T > 256 the fused kernel's fp32 dQ accumulator [B*L][H][T][32]. */
-size_t mdg_attn_temporal_bwd_scratch(int32_t dtype, int32_t B, int32_t T, int32_t L, int32_t H);
+/* Scratch of mdg_attn_temporal_bwd: dO planes CT [B*L][H][T][DP], delta fp32 [B*L][H][T], and
+   for bf16 with T > 256 and head_dim < 32 the fused kernel's fp32 dQ accumulator [B*L][H][T][32].
+   ABI 23: takes head_dim D (the wide heads' 64-column planes); 0 for D outside 1..63. */
+size_t mdg_attn_temporal_bwd_scratch(int32_t dtype, int32_t B, int32_t T, int32_t L, int32_t H, int32_t D);
 /* Temporal (and L >= 16 spatial) attention backward: from the forward's planes (qkv_t), lse,
    output o (CT [N][C]; o_lo its residual from mdg_attn_temporal_lse or null) and its gradient
    dout (CT [N][C]), writes dq | dk | dv of the linear
    projections (RoPE and the q scale undone: qscale = D^-1/2) into dqkv (CT, token-major rows of
    ld_dqkv >= 3C, packed column order); kscale = ln 2 for planes in log2 units (the forward's
    q carries log2 e).  bias_k / bias_v gradients (w.r.t. the rotated kvb rows) are written as
-   per-slot partials bpart [H][parts][2][32].  generic: 0 = the fused single-pass MFMA kernel
+   per-slot partials bpart [H][parts][2][DP].  generic: 0 = the fused single-pass MFMA kernel
    (bf16 default: P / dP once per pair, one block per (sequence, head), deterministic), 2 = the
-   two-pass MFMA kernels (dQ; dK / dV), 1 = the scalar kernels (the fp32 path always uses them). */
+   two-pass MFMA kernels (dQ; dK / dV), 1 = the scalar kernels (the fp32 path always uses them).
+   head_dim 32..63 (ABI 23): bf16 takes generic = 1 only (MDG_E_ARG otherwise). */
 int mdg_attn_temporal_bwd(int32_t dtype, int32_t B, int32_t T, int32_t L, int32_t H, int32_t D, const void* qkv_t,
                           const float* kbias, const float* kvb, const void* o, const void* o_lo, const void* dout,
                           const float* lse,
                           const float* rope, int32_t rope_rows, void* scratch, void* dqkv, int32_t ld_dqkv,
                           float* bpart, float qscale, float kscale, int32_t generic, void* stream);
 /* Spatial attention backward (L < 16): q|k|v [N][3C] as saved by the forward, dout CT [N][C];
-   dq | dk | dv into dqkv [N][3C]; bias partials bpart [H][parts][2][32] (every slot; columns
-   >= D of a slot may be left unwritten: mdg_train_unpack_layer reads d < D only). */
+   dq | dk | dv into dqkv [N][3C]; bias partials bpart [H][parts][2][DP] (every slot; columns
+   >= D of a slot may be left unwritten: mdg_train_unpack_layer reads d < D only); head_dim < 64. */
 int mdg_attn_spatial_bwd(int32_t dtype, int32_t n_frames, int32_t L, int32_t H, int32_t D, const void* qkv,
                          const float* kvb, const float* mask, const void* dout, const float* rope, int32_t rope_rows,
                          void* dqkv, float* bpart, float qscale, void* stream);
@@ -623,7 +626,8 @@ typedef struct {
   void* wqkv[2]; void* wqkv_t[2]; float* bqkv[2]; void* wo_p[2]; void* wo_t[2]; float* kvb[2];
   void* w1_p; void* w1_t; void* w2_p; void* w2_t;
 } mdg_train_pack;
-/* gwqkv / gbqkv: packed-order fp32 gradients ([3C][C], [3C]); bpart[i]: [H][parts[i]][2][32]
+/* kvb[i]: [H][2][MDG_HEAD_STRIDE(D)] (head_dim < 64).
+   gwqkv / gbqkv: packed-order fp32 gradients ([3C][C], [3C]); bpart[i]: [H][parts[i]][2][DP]
    bias-key / value partials (summed here, one block per head: H <= 128); part[0..3]: the ln_gate_bwd partials [B][nblk][4][C] of the
    layer-input LN, the spatial, temporal and MLP sublayers.  Outputs fp32 in parameter layout;
    dmods [B][9C] in latent_model.py:459-461 chunk order. */

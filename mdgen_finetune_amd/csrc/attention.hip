@@ -34,7 +34,8 @@ __global__ __launch_bounds__(256) void attn_temporal_kernel(const CT* __restrict
                                                             const float* __restrict__ kbias,
                                                             const float* __restrict__ kvb,
                                                             CT* __restrict__ out, int T, int L,
-                                                            int H, int D, int BL, float* __restrict__ lse) {
+                                                            int H, int D, int BL, float* __restrict__ lse,
+                                                            CT* __restrict__ out_lo = nullptr) {
   constexpr int KC = 64, LDK = DP + 16;  // DP 32: 96-B LDS rows (bf16), conflict-free b128 + tr reads
   constexpr int KS = DP / 32, DT = DP / 16;
   constexpr int VEC = 16 / sizeof(CT);
@@ -259,9 +260,14 @@ __global__ __launch_bounds__(256) void attn_temporal_kernel(const CT* __restrict
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
         const int d0 = dt * 16 + lg * 4;
-        if (d0 < D)
-          st4<CT>(orow + d0, o[dt][qg][0] * inv, o[dt][qg][1] * inv, o[dt][qg][2] * inv,
-                  o[dt][qg][3] * inv);
+        if (d0 < D) {
+          const float v0 = o[dt][qg][0] * inv, v1 = o[dt][qg][1] * inv, v2 = o[dt][qg][2] * inv,
+                      v3 = o[dt][qg][3] * inv;
+          st4<CT>(orow + d0, v0, v1, v2, v3);
+          if (out_lo)  // training: O - CT(O), the backward's delta = dO . (O + O_lo)
+            st4<CT>(out_lo + (orow - out) + d0, v0 - (float)(CT)v0, v1 - (float)(CT)v1, v2 - (float)(CT)v2,
+                    v3 - (float)(CT)v3);
+        }
       }
     }
   }
@@ -742,12 +748,12 @@ hipError_t attn_temporal_launch(int dtype, int B, int T, int L, int H, int D, co
                                 const float* kbias, const float* kvb, void* out, hipStream_t s, float* lse,
                                 bool packed, void* out_lo) {
   if (packed && (dtype != MDG_BF16 || D % 8 || D >= MDG_DP)) return hipErrorInvalidValue;
-  if (out_lo && (dtype != MDG_BF16 || D >= MDG_DP)) return hipErrorInvalidValue;  // bf16 MFMA kernel only
+  if (out_lo && dtype != MDG_BF16) return hipErrorInvalidValue;  // (f32 O is exact)
   if (D >= MDG_DP) {  // wide heads (32..63): the generic 16x16 MFMA kernel on 64-column rows
     dim3 grid((T + 127) / 128, H, B * L);
     if (dtype == MDG_BF16)
       hipLaunchKernelGGL((attn_temporal_kernel<bf16_t, MDG_DP_WIDE>), grid, dim3(256), 0, s, (const bf16_t*)qkv_t,
-                         kbias, kvb, (bf16_t*)out, T, L, H, D, B * L, lse);
+                         kbias, kvb, (bf16_t*)out, T, L, H, D, B * L, lse, (bf16_t*)out_lo);
     else
       hipLaunchKernelGGL((attn_temporal_kernel<float, MDG_DP_WIDE>), grid, dim3(256), 0, s, (const float*)qkv_t,
                          kbias, kvb, (float*)out, T, L, H, D, B * L, lse);

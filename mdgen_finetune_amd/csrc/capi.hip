@@ -508,9 +508,9 @@ int mdg_attn_temporal_lse(int32_t dtype, int32_t B, int32_t T, int32_t L, int32_
   if (dtype != MDG_F32 && dtype != MDG_BF16) return fail(MDG_E_DTYPE, "dtype %d", dtype);
   if (!qkv_t || !kbias || !kvb || !out || !lse) return fail(MDG_E_ARG, "attn_temporal_lse: null pointer");
   if (out_lo && dtype != MDG_BF16) return fail(MDG_E_ARG, "attn_temporal_lse: out_lo is for bf16 (f32 O is exact)");
-  if (B <= 0 || T <= 0 || L <= 0 || H <= 0 || D <= 0 || D % 4 || D >= MDG_DP)
-    return fail(MDG_E_SHAPE, "attn_temporal_lse: B=%d T=%d L=%d H=%d D=%d (training kernels: head_dim < %d)", B, T,
-                L, H, D, MDG_DP);
+  if (B <= 0 || T <= 0 || L <= 0 || H <= 0 || D <= 0 || D % 4 || D >= MDG_DP_WIDE)
+    return fail(MDG_E_SHAPE, "attn_temporal_lse: B=%d T=%d L=%d H=%d D=%d (head_dim < %d)", B, T, L, H, D,
+                MDG_DP_WIDE);
   if (H > 65535 || B * L > 65535) return fail(MDG_E_SHAPE, "attn_temporal_lse: grid too large");
   return hip_check(mdg::attn_temporal_launch(dtype, B, T, L, H, D, qkv_t, kbias, kvb, out, (hipStream_t)stream, lse,
                                              false, out_lo),
@@ -918,8 +918,9 @@ int mdg_mask_bias(int32_t B, int32_t T, int32_t L, const float* mask, float* kbi
 static int init_planes(const mdg_dims* d, void* planes, int B, int T, int L, hipStream_t s) {
   const size_t cs = ct_size(d->dtype);
   const size_t rows = (size_t)B * L * d->H * T;
-  if (int e = hip_check(hipMemsetAsync(planes, 0, 3 * rows * MDG_DP * cs, s), "planes memset")) return e;
-  return hip_check(mdg::set_vpad_launch(d->dtype, (char*)planes + rows * MDG_DP * cs, 2 * rows, d->D, s), "set_vpad");
+  const size_t dp = dp_of(d->D);
+  if (int e = hip_check(hipMemsetAsync(planes, 0, 3 * rows * dp * cs, s), "planes memset")) return e;
+  return hip_check(mdg::set_vpad_launch(d->dtype, (char*)planes + rows * dp * cs, 2 * rows, d->D, s), "set_vpad");
 }
 
 // the row-LN route of the training forward (gemm.hip kCfgRowTrain); MDG_TRAIN_ROWLN=0: the GEMM +
@@ -937,8 +938,6 @@ int mdg_layer_fwd_train(const mdg_dims* d, const mdg_layer_weights* w, const flo
                         const float* mods, const float* mask, const float* kbias_t, const float* kbias_s,
                         const float* h_in, float* h_out, const mdg_layer_saved* sv, void* stream) {
   if (int e = check_dims(d)) return e;
-  if (d->D >= MDG_DP)
-    return fail(MDG_E_SHAPE, "layer_fwd_train: head_dim %d (the training kernels take head_dim < %d)", d->D, MDG_DP);
   if (!w || !mods || !kbias_t || !h_in || !h_out || !sv || h_in == h_out)
     return fail(MDG_E_ARG, "layer_fwd_train: null pointer or h_in == h_out");
   for (int i = 0; i < 3; ++i)
@@ -1081,11 +1080,12 @@ int32_t mdg_attn_spatial_bwd_parts(int32_t n_frames, int32_t L, int32_t D) {
   return mdg::attn_spatial_bwd_parts(n_frames, L, D);
 }
 
-size_t mdg_attn_temporal_bwd_scratch(int32_t dtype, int32_t B, int32_t T, int32_t L, int32_t H) {
-  const size_t rows = (size_t)B * L * H * T;
+size_t mdg_attn_temporal_bwd_scratch(int32_t dtype, int32_t B, int32_t T, int32_t L, int32_t H, int32_t D) {
+  if (D <= 0 || D >= MDG_DP_WIDE) return 0;
+  const size_t rows = (size_t)B * L * H * T, dp = dp_of(D);
   // + the fused bf16 kernel's fp32 dQ accumulator when the keys take more than one 256-key pass
-  const size_t acc = (dtype == MDG_BF16 && T > 256) ? align256(rows * MDG_DP * sizeof(float)) : 0;
-  return align256(rows * MDG_DP * ct_size(dtype)) + align256(rows * sizeof(float)) + acc;
+  const size_t acc = (dtype == MDG_BF16 && T > 256 && D < MDG_DP) ? align256(rows * MDG_DP * sizeof(float)) : 0;
+  return align256(rows * dp * ct_size(dtype)) + align256(rows * sizeof(float)) + acc;
 }
 
 int mdg_attn_temporal_bwd(int32_t dtype, int32_t B, int32_t T, int32_t L, int32_t H, int32_t D, const void* qkv_t,
@@ -1096,14 +1096,17 @@ int mdg_attn_temporal_bwd(int32_t dtype, int32_t B, int32_t T, int32_t L, int32_
   if (dtype != MDG_F32 && dtype != MDG_BF16) return fail(MDG_E_DTYPE, "dtype %d", dtype);
   if (!qkv_t || !kbias || !kvb || !o || !dout || !lse || !scratch || !dqkv || !bpart)
     return fail(MDG_E_ARG, "attn_temporal_bwd: null pointer");
-  if (B <= 0 || T <= 0 || L <= 0 || H <= 0 || D <= 0 || D % 4 || D >= MDG_DP || ld_dqkv < 3 * H * D ||
+  if (B <= 0 || T <= 0 || L <= 0 || H <= 0 || D <= 0 || D % 4 || D >= MDG_DP_WIDE || ld_dqkv < 3 * H * D ||
       ld_dqkv % 4)
     return fail(MDG_E_SHAPE, "attn_temporal_bwd: B=%d T=%d L=%d H=%d D=%d ld=%d", B, T, L, H, D, ld_dqkv);
+  // wide heads (head_dim 32..63) run the scalar kernels only: the caller sizes bpart for them
+  if (D >= MDG_DP && dtype == MDG_BF16 && generic != 1)
+    return fail(MDG_E_ARG, "attn_temporal_bwd: head_dim %d takes generic = 1 (the scalar kernels)", D);
   if (rope && rope_rows < T) return fail(MDG_E_SHAPE, "attn_temporal_bwd: rope table too short");
   if ((size_t)B * L * H > 65535u * 256u) return fail(MDG_E_SHAPE, "attn_temporal_bwd: grid too large");
   const size_t rows = (size_t)B * L * H * T;
   void* dop = scratch;
-  float* delta = (float*)((char*)scratch + align256(rows * MDG_DP * ct_size(dtype)));
+  float* delta = (float*)((char*)scratch + align256(rows * dp_of(D) * ct_size(dtype)));
   float* dqacc = (float*)((char*)delta + align256(rows * sizeof(float)));
   if (generic < 0 || generic > 2) return fail(MDG_E_ARG, "attn_temporal_bwd: generic=%d (0, 1, 2)", generic);
   return hip_check(mdg::attn_temporal_bwd_launch(dtype, B, T, L, H, D, qkv_t, kbias, kvb, o, o_lo, dout, lse, rope,
@@ -1117,8 +1120,9 @@ int mdg_attn_spatial_bwd(int32_t dtype, int32_t n_frames, int32_t L, int32_t H, 
                          void* dqkv, float* bpart, float qscale, void* stream) {
   if (dtype != MDG_F32 && dtype != MDG_BF16) return fail(MDG_E_DTYPE, "dtype %d", dtype);
   if (!qkv || !kvb || !dout || !dqkv || !bpart) return fail(MDG_E_ARG, "attn_spatial_bwd: null pointer");
-  if (n_frames <= 0 || L <= 0 || L > 16 || H <= 0 || D <= 0 || D % 4 || D >= MDG_DP)
-    return fail(MDG_E_SHAPE, "attn_spatial_bwd: nf=%d L=%d H=%d D=%d (L <= 16)", n_frames, L, H, D);
+  if (n_frames <= 0 || L <= 0 || L > 16 || H <= 0 || D <= 0 || D % 4 || D >= MDG_DP_WIDE)
+    return fail(MDG_E_SHAPE, "attn_spatial_bwd: nf=%d L=%d H=%d D=%d (L <= 16, head_dim < %d)", n_frames, L, H, D,
+                MDG_DP_WIDE);
   if (rope && rope_rows < L) return fail(MDG_E_SHAPE, "attn_spatial_bwd: rope table too short");
   return hip_check(mdg::attn_spatial_bwd_launch(dtype, n_frames, L, H, D, qkv, kvb, mask, dout, rope, rope_rows, dqkv,
                                                 bpart, qscale, (hipStream_t)stream),
@@ -1157,7 +1161,7 @@ int mdg_ipa_core_bwd(int32_t B, int32_t L, int32_t H, int32_t c, int32_t Pq, int
 int mdg_train_pack_layer(const mdg_train_pack* p, void* stream) {
   if (!p) return fail(MDG_E_ARG, "train_pack: null");
   if (p->dtype != MDG_F32 && p->dtype != MDG_BF16) return fail(MDG_E_DTYPE, "train_pack: dtype %d", p->dtype);
-  if (p->C <= 0 || p->H <= 0 || p->D <= 0 || p->C != p->H * p->D || p->D % 2 || p->D >= MDG_DP || p->F <= 0)
+  if (p->C <= 0 || p->H <= 0 || p->D <= 0 || p->C != p->H * p->D || p->D % 2 || p->D >= MDG_DP_WIDE || p->F <= 0)
     return fail(MDG_E_SHAPE, "train_pack: C=%d H=%d D=%d F=%d", p->C, p->H, p->D, p->F);
   for (int i = 0; i < 2; ++i) {
     if (!p->wq[i] || !p->wk[i] || !p->wv[i] || !p->bq[i] || !p->bk[i] || !p->bv[i] || !p->wo[i] || !p->bias_k[i] ||
@@ -1172,7 +1176,7 @@ int mdg_train_pack_layer(const mdg_train_pack* p, void* stream) {
 
 int mdg_train_unpack_layer(const mdg_train_unpack* u, void* stream) {
   if (!u) return fail(MDG_E_ARG, "train_unpack: null");
-  if (u->C <= 0 || u->H <= 0 || u->H > 128 || u->D <= 0 || u->C != u->H * u->D || u->D % 2 || u->D >= MDG_DP || u->B <= 0 ||
+  if (u->C <= 0 || u->H <= 0 || u->H > 128 || u->D <= 0 || u->C != u->H * u->D || u->D % 2 || u->D >= MDG_DP_WIDE || u->B <= 0 ||
       u->nblk <= 0)
     return fail(MDG_E_SHAPE, "train_unpack: C=%d H=%d D=%d B=%d nblk=%d", u->C, u->H, u->D, u->B, u->nblk);
   for (int i = 0; i < 2; ++i) {

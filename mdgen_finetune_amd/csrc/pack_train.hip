@@ -6,7 +6,8 @@
 //
 // pack   (forward):  wqkv[i] = CT [3C][C] rows q | k | v, q and k rows pair-interleaved per head
 //                    (row 2j = dim j, 2j+1 = dim j + D/2) when RoPE is on; its transpose; bqkv[i];
-//                    wo[i], w1, w2 as CT and transposed; kvb[i] = [H][2][32]: bias_k RoPE-rotated at
+//                    wo[i], w1, w2 as CT and transposed; kvb[i] = [H][2][DP] (DP = MDG_HEAD_STRIDE(D):
+//                    32, or 64 for head_dim 32..63): bias_k RoPE-rotated at
 //                    the bias key's position S (fair-esm: x cos + rotate_half(x) sin) in the
 //                    interleaved order, bias_v with 1.0 in pad column D.
 // unpack (backward): the packed-order fp32 q|k|v weight / bias gradients back to q_proj / k_proj /
@@ -94,8 +95,9 @@ __global__ __launch_bounds__(256) void pack_kernel(const mdg_train_pack p) {
     }
     const float* tab = p.rope_tab[i];
     const int S = p.rope_pos[i], rows = p.rope_rows[i];
-    for (int e = t0; e < H * 2 * MDG_DP; e += stride) {
-      const int h = e / (2 * MDG_DP), which = (e / MDG_DP) & 1, d = e % MDG_DP;
+    const int DP = dp_of(D);
+    for (int e = t0; e < H * 2 * DP; e += stride) {
+      const int h = e / (2 * DP), which = (e / DP) & 1, d = e % DP;
       float v = 0.f;
       if (which == 1) {
         v = d < D ? p.bias_v[i][h * D + d] : (d == D ? 1.0f : 0.f);
@@ -169,33 +171,36 @@ __global__ __launch_bounds__(256) void unpack_kernel(const mdg_train_unpack u) {
       }
     }
   } else if (job < 4) {  // bias_k / bias_v gradients of attention job - 2: block h < H sums head
-    // h's [parts][2][32] slots (the 4 waves take every 4th slot, added in wave order), then
-    // applies the rotation's transpose from LDS
-    const int i = job - 2, np = u.parts[i], h = blockIdx.x;
+    // h's [parts][2][DP] slots (the 4 waves take every 4th slot, added in wave order; a lane owns
+    // columns lane, lane + 64 .. of the 2 DP; fp64 sums: the slots nearly cancel), then applies
+    // the rotation's transpose from LDS
+    const int i = job - 2, np = u.parts[i], h = blockIdx.x, DP = dp_of(D);
     if (h >= H) return;
-    __shared__ float red[4][2 * MDG_DP];
+    __shared__ double red[4][2 * MDG_DP_WIDE];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const float* bp = u.bpart[i] + (size_t)h * np * 2 * MDG_DP + lane;  // [H][parts][2][32]
-    // 16 slots in flight per lane (the spatial backward leaves 500 per head at B = 8, T = 1000)
-    constexpr int NA = 16;
-    float a[NA];
+    for (int col = lane; col < 2 * DP; col += 64) {
+      const float* bp = u.bpart[i] + (size_t)h * np * 2 * DP + col;  // [H][parts][2][DP]
+      // 16 slots in flight per lane (the spatial backward leaves 500 per head at B = 8, T = 1000)
+      constexpr int NA = 16;
+      double a[NA];
 #pragma unroll
-    for (int j = 0; j < NA; ++j) a[j] = 0.f;
-    int q = w;
-    for (; q + 4 * (NA - 1) < np; q += 4 * NA) {
+      for (int j = 0; j < NA; ++j) a[j] = 0.0;
+      int q = w;
+      for (; q + 4 * (NA - 1) < np; q += 4 * NA) {
 #pragma unroll
-      for (int j = 0; j < NA; ++j) a[j] += bp[(size_t)(q + 4 * j) * 2 * MDG_DP];
+        for (int j = 0; j < NA; ++j) a[j] += bp[(size_t)(q + 4 * j) * 2 * DP];
+      }
+      for (; q < np; q += 4) a[0] += bp[(size_t)q * 2 * DP];
+#pragma unroll
+      for (int st = NA / 2; st >= 1; st >>= 1)
+#pragma unroll
+        for (int j = 0; j < st; ++j) a[j] += a[j + st];
+      red[w][col] = a[0];
     }
-    for (; q < np; q += 4) a[0] += bp[(size_t)q * 2 * MDG_DP];
-#pragma unroll
-    for (int st = NA / 2; st >= 1; st >>= 1)
-#pragma unroll
-      for (int j = 0; j < st; ++j) a[j] += a[j + st];
-    red[w][lane] = a[0];
     __syncthreads();
     auto g = [&](int which, int d) {
-      const int e = which * MDG_DP + d;
-      return ((red[0][e] + red[1][e]) + red[2][e]) + red[3][e];
+      const int e = which * DP + d;
+      return (float)(((red[0][e] + red[1][e]) + red[2][e]) + red[3][e]);
     };
     const float* tab = u.rope_tab[i];
     const int S = u.rope_pos[i], rows = u.rope_rows[i];

@@ -336,8 +336,8 @@ __device__ __forceinline__ void rope_inv(float& a, float& b, const float* rope, 
 }
 
 // delta[seq][head][t] = sum_d dO[n][head*D + d] * O[n][head*D + d];  dO scattered to planes
-// [seq][head][T][32] (pad columns 0).  n = (b*T + t)*L + l, seq = b*L + l.
-template <typename CT>
+// [seq][head][T][DP] (pad columns 0; DP = MDG_HEAD_STRIDE(D)).  n = (b*T + t)*L + l, seq = b*L + l.
+template <typename CT, int DP>
 __global__ __launch_bounds__(256) void attn_bwd_prep_kernel(int B, int T, int L, int H, int D, const CT* __restrict__ o,
                                                             const CT* __restrict__ o_lo,
                                                             const CT* __restrict__ dout, CT* __restrict__ dop,
@@ -351,11 +351,11 @@ __global__ __launch_bounds__(256) void attn_bwd_prep_kernel(int B, int T, int L,
   const int seq = b * L + l, C = H * D;
   const CT* orow = o + n * C + head * D;
   const CT* drow = dout + n * C + head * D;
-  CT* prow = dop + (((size_t)seq * H + head) * T + t) * kDP;
+  CT* prow = dop + (((size_t)seq * H + head) * T + t) * DP;
   float dl = 0.f;
   if (D % 8 == 0) {  // 16-B (bf16) pieces: half the memory instructions of the 4-wide loop below
 #pragma unroll
-    for (int d0 = 0; d0 < kDP; d0 += 8) {
+    for (int d0 = 0; d0 < DP; d0 += 8) {
       typename V8<CT>::T dv = zero8<CT>();
       if (d0 < D) {
         const typename V8<CT>::T ov = ld8<CT>(orow + d0);
@@ -373,7 +373,7 @@ __global__ __launch_bounds__(256) void attn_bwd_prep_kernel(int B, int T, int L,
       st8<CT>(prow + d0, dv);
     }
   } else {
-    for (int d0 = 0; d0 < kDP; d0 += 4) {
+    for (int d0 = 0; d0 < DP; d0 += 4) {
       float4 dv = make_float4(0.f, 0.f, 0.f, 0.f);
       if (d0 < D) {
         const float4 ov = ld4f<CT>(orow + d0);
@@ -454,65 +454,72 @@ __global__ __launch_bounds__(256) void attn_bwd_prep_tiled_kernel(int B, int T, 
 }
 
 // Scalar reference / fp32 path: dq pass (one thread per (seq, head, query)) including the bias
-// key and its parameter gradients (block partials over the block's 256 queries).
-template <typename CT>
+// key and its parameter gradients (block partials over the block's 256 queries).  DP = the
+// planes' row stride (MDG_HEAD_STRIDE(D)): 32, or 64 for the wide heads (head_dim 32..63; their
+// 129 KiB partial array is within gfx950's 160 KiB of LDS per block).
+template <typename CT, int DP>
 __global__ __launch_bounds__(256) void attn_bwd_dq_generic_kernel(
     const CT* __restrict__ qkv, const CT* __restrict__ dop, const float* __restrict__ lse,
     const float* __restrict__ delta, const float* __restrict__ kbias, const float* __restrict__ kvb,
     const float* __restrict__ rope, int rope_rows, CT* __restrict__ dqkv, int ldq, float* __restrict__ bpart, int T,
     int L, int H, int D, int BL, float qscale, float kscale) {
-  __shared__ float red[256][2 * kDP + 1];
+  __shared__ float red[256][2 * DP + 1];
   const int sh = blockIdx.y, seq = sh / H, head = sh % H;
   const int q = blockIdx.x * 256 + threadIdx.x;
   const bool live = q < T;
-  const size_t plane = (size_t)BL * H * T * kDP;
-  const CT* Qg = qkv + (size_t)sh * T * kDP;
+  const size_t plane = (size_t)BL * H * T * DP;
+  const CT* Qg = qkv + (size_t)sh * T * DP;
   const CT* Kg = Qg + plane;
   const CT* Vg = Qg + 2 * plane;
-  const CT* dOg = dop + (size_t)sh * T * kDP;
-  float qv[kDP], dov[kDP], dq[kDP];
+  const CT* dOg = dop + (size_t)sh * T * DP;
+  float qv[DP], dov[DP], dq[DP];
   const int qq = live ? q : 0;
 #pragma unroll
-  for (int d = 0; d < kDP; ++d) {
-    qv[d] = live && d < D ? (float)Qg[(size_t)qq * kDP + d] : 0.f;
-    dov[d] = live && d < D ? (float)dOg[(size_t)qq * kDP + d] : 0.f;
+  for (int d = 0; d < DP; ++d) {
+    qv[d] = live && d < D ? (float)Qg[(size_t)qq * DP + d] : 0.f;
+    dov[d] = live && d < D ? (float)dOg[(size_t)qq * DP + d] : 0.f;
   }
   const float l2 = live ? lse[(size_t)sh * T + q] : INFINITY;
   const float dl = live ? delta[(size_t)sh * T + q] : 0.f;
-  const float* bk = kvb + head * 2 * kDP;
-  const float* bv = bk + kDP;
+  const float* bk = kvb + head * 2 * DP;
+  const float* bv = bk + DP;
   float sb = 0.f, dpb = 0.f;
 #pragma unroll
-  for (int d = 0; d < kDP; ++d) {
+  for (int d = 0; d < DP; ++d) {
     if (d < D) {
       sb += qv[d] * bk[d];
       dpb += dov[d] * bv[d];
     }
   }
   const float pb = live ? exp2f(sb - l2) : 0.f;
-  const float dsb = pb * (dpb - dl);
+  float dsb = pb * (dpb - dl);
 #pragma unroll
-  for (int d = 0; d < kDP; ++d) {
-    dq[d] = dsb * bk[d];
-    red[threadIdx.x][d] = (d < D) ? dsb * qv[d] * kscale : 0.f;
-    red[threadIdx.x][kDP + d] = (d < D) ? pb * dov[d] : 0.f;
-  }
+  for (int d = 0; d < DP; ++d) dq[d] = dsb * bk[d];
   if (live) {
+    bool anyk = false;
     for (int k = 0; k < T; ++k) {
       const float kb = kbias[(size_t)seq * T + k];
       if (kb == -INFINITY) continue;
+      anyk = true;
       float s = kb, dp = 0.f;
 #pragma unroll
-      for (int d = 0; d < kDP; ++d) {
+      for (int d = 0; d < DP; ++d) {
         if (d < D) {
-          s += qv[d] * (float)Kg[(size_t)k * kDP + d];
-          dp += dov[d] * (float)Vg[(size_t)k * kDP + d];
+          s += qv[d] * (float)Kg[(size_t)k * DP + d];
+          dp += dov[d] * (float)Vg[(size_t)k * DP + d];
         }
       }
       const float ds = exp2f(s - l2) * (dp - dl);
 #pragma unroll
-      for (int d = 0; d < kDP; ++d)
-        if (d < D) dq[d] += ds * (float)Kg[(size_t)k * kDP + d];
+      for (int d = 0; d < DP; ++d)
+        if (d < D) dq[d] += ds * (float)Kg[(size_t)k * DP + d];
+    }
+    if (!anyk) {  // every key padded (a padded residue): P = [1, 0, ...], so dS = 0 exactly — not
+      // the rounding difference of dpb and delta's two summation orders, which summed coherently
+      // over the sequence's T queries (5e-5 of the f32 bias_k gradient at T = 1000)
+      dsb = 0.f;
+#pragma unroll
+      for (int d = 0; d < DP; ++d) dq[d] = 0.f;
     }
     const int b = seq / L, l = seq % L, half = D >> 1;
     const size_t tok = ((size_t)b * T + q) * L + l;
@@ -524,17 +531,24 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_generic_kernel(
       out[d + 1] = (CT)c;
     }
   }
+#pragma unroll
+  for (int d = 0; d < DP; ++d) {
+    red[threadIdx.x][d] = (d < D) ? dsb * qv[d] * kscale : 0.f;
+    red[threadIdx.x][DP + d] = (d < D) ? pb * dov[d] : 0.f;
+  }
   __syncthreads();
-  if (threadIdx.x < 2 * kDP) {
-    float s = 0.f;
+  if (threadIdx.x < 2 * DP) {
+    // the 256 query terms in fp64: they nearly cancel (a row's dS sums to ~0), and an fp32 chain
+    // left the f32 bias_k gradient 5e-5 from fp64 at T = 1000 (eager f32: 7e-6)
+    double s = 0.0;
     for (int i = 0; i < 256; ++i) s += red[i][threadIdx.x];
     const size_t slot = (size_t)seq * gridDim.x + blockIdx.x;
-    bpart[((size_t)head * BL * gridDim.x + slot) * 2 * kDP + threadIdx.x] = s;
+    bpart[((size_t)head * BL * gridDim.x + slot) * 2 * DP + threadIdx.x] = s;
   }
 }
 
 // Scalar reference / fp32 path: dk / dv pass (one thread per (seq, head, key)).
-template <typename CT>
+template <typename CT, int DP>
 __global__ __launch_bounds__(256) void attn_bwd_dkdv_generic_kernel(
     const CT* __restrict__ qkv, const CT* __restrict__ dop, const float* __restrict__ lse,
     const float* __restrict__ delta, const float* __restrict__ kbias, const float* __restrict__ rope, int rope_rows,
@@ -542,36 +556,36 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_generic_kernel(
   const int sh = blockIdx.y, seq = sh / H, head = sh % H;
   const int k = blockIdx.x * 256 + threadIdx.x;
   if (k >= T) return;
-  const size_t plane = (size_t)BL * H * T * kDP;
-  const CT* Qg = qkv + (size_t)sh * T * kDP;
+  const size_t plane = (size_t)BL * H * T * DP;
+  const CT* Qg = qkv + (size_t)sh * T * DP;
   const CT* Kg = Qg + plane;
   const CT* Vg = Qg + 2 * plane;
-  const CT* dOg = dop + (size_t)sh * T * kDP;
+  const CT* dOg = dop + (size_t)sh * T * DP;
   const float kb = kbias[(size_t)seq * T + k];
-  float kv[kDP], vv[kDP], dk[kDP], dv[kDP];
+  float kv[DP], vv[DP], dk[DP], dv[DP];
 #pragma unroll
-  for (int d = 0; d < kDP; ++d) {
-    kv[d] = d < D ? (float)Kg[(size_t)k * kDP + d] : 0.f;
-    vv[d] = d < D ? (float)Vg[(size_t)k * kDP + d] : 0.f;
+  for (int d = 0; d < DP; ++d) {
+    kv[d] = d < D ? (float)Kg[(size_t)k * DP + d] : 0.f;
+    vv[d] = d < D ? (float)Vg[(size_t)k * DP + d] : 0.f;
     dk[d] = dv[d] = 0.f;
   }
   if (kb != -INFINITY) {
     for (int q = 0; q < T; ++q) {
       float s = kb, dp = 0.f;
 #pragma unroll
-      for (int d = 0; d < kDP; ++d) {
+      for (int d = 0; d < DP; ++d) {
         if (d < D) {
-          s += (float)Qg[(size_t)q * kDP + d] * kv[d];
-          dp += (float)dOg[(size_t)q * kDP + d] * vv[d];
+          s += (float)Qg[(size_t)q * DP + d] * kv[d];
+          dp += (float)dOg[(size_t)q * DP + d] * vv[d];
         }
       }
       const float p = exp2f(s - lse[(size_t)sh * T + q]);
       const float ds = p * (dp - delta[(size_t)sh * T + q]);
 #pragma unroll
-      for (int d = 0; d < kDP; ++d) {
+      for (int d = 0; d < DP; ++d) {
         if (d < D) {
-          dk[d] += ds * (float)Qg[(size_t)q * kDP + d];
-          dv[d] += p * (float)dOg[(size_t)q * kDP + d];
+          dk[d] += ds * (float)Qg[(size_t)q * DP + d];
+          dv[d] += p * (float)dOg[(size_t)q * DP + d];
         }
       }
     }
@@ -1273,6 +1287,7 @@ static bool attn_bwd_fold_on() {
 }
 
 int attn_bwd_parts(int dtype, int B, int T, int L, int generic) {  // bias-gradient partial slots per head
+  if (dtype == MDG_BF16 && generic == 1) return B * L * ((T + 255) / 256);
   if (dtype == MDG_BF16 && generic == 0) return B * L;  // the fused kernel: one per sequence
   if (dtype == MDG_BF16) return B * L * ((T + kBW * 32 - 1) / (kBW * 32)) * kBW;
   return B * L * ((T + 255) / 256);
@@ -1286,21 +1301,39 @@ hipError_t attn_temporal_bwd_launch(int dtype, int B, int T, int L, int H, int D
                                     float* dqacc, hipStream_t s) {
   const int BL = B * L;
   const size_t nth = (size_t)B * T * L * H;
+  dim3 pgrid((unsigned)((nth + 255) / 256));
+  dim3 grid((T + 255) / 256, BL * H);
+#define MDG_GEN(CTT, DPP)                                                                                             \
+  hipLaunchKernelGGL((attn_bwd_prep_kernel<CTT, DPP>), pgrid, dim3(256), 0, s, B, T, L, H, D, (const CTT*)o,          \
+                     (const CTT*)o_lo, (const CTT*)dout, (CTT*)dop, delta);                                           \
+  if (hipError_t e = hipGetLastError()) return e;                                                                    \
+  hipLaunchKernelGGL((attn_bwd_dq_generic_kernel<CTT, DPP>), grid, dim3(256), 0, s, (const CTT*)qkv_t,               \
+                     (const CTT*)dop, lse, delta, kbias, kvb, rope, rope_rows, (CTT*)dqkv, ldq, bpart, T, L, H, D, BL, \
+                     qscale, kscale);                                                                                \
+  hipLaunchKernelGGL((attn_bwd_dkdv_generic_kernel<CTT, DPP>), grid, dim3(256), 0, s, (const CTT*)qkv_t,             \
+                     (const CTT*)dop, lse, delta, kbias, rope, rope_rows, (CTT*)dqkv, ldq, T, L, H, D, BL, kscale)
+  // the scalar kernels: f32, generic == 1, and every wide head (head_dim 32..63, 64-column planes;
+  // the MFMA kernels' LDS images are 32 columns wide)
+  if (dtype == MDG_F32 || generic == 1 || D >= kDP) {
+    if (D >= kDP) {
+      if (dtype == MDG_BF16) { MDG_GEN(bf16_t, MDG_DP_WIDE); } else { MDG_GEN(float, MDG_DP_WIDE); }
+    } else {
+      if (dtype == MDG_BF16) { MDG_GEN(bf16_t, kDP); } else { MDG_GEN(float, kDP); }
+    }
+    return hipGetLastError();
+  }
+#undef MDG_GEN
   // the fused backward with folded offsets (its dO' / delta' come from the tiled prep)
   const bool fold = dtype == MDG_BF16 && generic == 0 && attn_bwd_fold_on() && D % 8 == 0 && D + 2 <= kDP &&
                     H <= 256 && 256 % H == 0;
-  dim3 pgrid((unsigned)((nth + 255) / 256));
   if (dtype == MDG_BF16 && D % 8 == 0 && H <= 256 && 256 % H == 0) {
     const int TT = 256 / H;
     hipLaunchKernelGGL(attn_bwd_prep_tiled_kernel, dim3((T + TT - 1) / TT, BL), dim3(256), 0, s, B, T, L, H, D,
                        (const bf16_t*)o, (const bf16_t*)o_lo, (const bf16_t*)dout, (bf16_t*)dop, delta,
                        fold ? lse : nullptr);
-  } else if (dtype == MDG_BF16) {
-    hipLaunchKernelGGL(attn_bwd_prep_kernel<bf16_t>, pgrid, dim3(256), 0, s, B, T, L, H, D, (const bf16_t*)o,
-                       (const bf16_t*)o_lo, (const bf16_t*)dout, (bf16_t*)dop, delta);
   } else {
-    hipLaunchKernelGGL(attn_bwd_prep_kernel<float>, pgrid, dim3(256), 0, s, B, T, L, H, D, (const float*)o,
-                       (const float*)o_lo, (const float*)dout, (float*)dop, delta);
+    hipLaunchKernelGGL((attn_bwd_prep_kernel<bf16_t, kDP>), pgrid, dim3(256), 0, s, B, T, L, H, D, (const bf16_t*)o,
+                       (const bf16_t*)o_lo, (const bf16_t*)dout, (bf16_t*)dop, delta);
   }
   if (hipError_t e = hipGetLastError()) return e;
   if (dtype == MDG_BF16 && generic == 0) {  // fused single pass
@@ -1338,19 +1371,7 @@ hipError_t attn_temporal_bwd_launch(int dtype, int B, int T, int L, int H, int D
                        kscale);
     return hipGetLastError();
   }
-  dim3 grid((T + 255) / 256, BL * H);
-#define MDG_GEN(CTT)                                                                                               \
-  hipLaunchKernelGGL(attn_bwd_dq_generic_kernel<CTT>, grid, dim3(256), 0, s, (const CTT*)qkv_t, (const CTT*)dop,    \
-                     lse, delta, kbias, kvb, rope, rope_rows, (CTT*)dqkv, ldq, bpart, T, L, H, D, BL, qscale, kscale); \
-  hipLaunchKernelGGL(attn_bwd_dkdv_generic_kernel<CTT>, grid, dim3(256), 0, s, (const CTT*)qkv_t, (const CTT*)dop,  \
-                     lse, delta, kbias, rope, rope_rows, (CTT*)dqkv, ldq, T, L, H, D, BL, kscale)
-  if (dtype == MDG_BF16) {
-    MDG_GEN(bf16_t);
-  } else {
-    MDG_GEN(float);
-  }
-#undef MDG_GEN
-  return hipGetLastError();
+  return hipErrorInvalidValue;  // generic outside 0..2 (mdg_attn_temporal_bwd checks it)
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1537,24 +1558,25 @@ __global__ __launch_bounds__(256) void attn_spatial_bwd_quad_kernel(const CT* __
   }
 }
 
-// Any L (< the MFMA route's 16), any D <= 31: one thread per (frame, head).
-template <typename CT>
+// Any L (< the MFMA route's 16), any D <= 63: one thread per (frame, head).  DP = the bias
+// rows' stride (MDG_HEAD_STRIDE(D)).
+template <typename CT, int DP>
 __global__ __launch_bounds__(128) void attn_spatial_bwd_generic_kernel(
     const CT* __restrict__ qkv, const float* __restrict__ kvb, const float* __restrict__ mask,
     const CT* __restrict__ dout, const float* __restrict__ rope, int rope_rows, CT* __restrict__ dqkv,
     float* __restrict__ bpart, int nf, int L, int H, int D, float qscale) {
   constexpr int LM = 16;
-  __shared__ float red[128][2 * kDP + 1];
+  __shared__ float red[128][2 * DP + 1];
   const int head = blockIdx.y;
   const int f = blockIdx.x * 128 + threadIdx.x;
   const bool live = f < nf;
   const int C = H * D;
-  const float* bk = kvb + head * 2 * kDP;
-  const float* bv = bk + kDP;
+  const float* bk = kvb + head * 2 * DP;
+  const float* bv = bk + DP;
   float P[LM][LM + 1], DS[LM][LM + 1];
-  float gbk[kDP], gbv[kDP];
+  float gbk[DP], gbv[DP];
 #pragma unroll
-  for (int d = 0; d < kDP; ++d) gbk[d] = gbv[d] = 0.f;
+  for (int d = 0; d < DP; ++d) gbk[d] = gbv[d] = 0.f;
   if (live) {
     auto at = [&](int tk, int which, int d) -> float {
       return (float)qkv[((size_t)(f * L + tk) * 3 + which) * C + head * D + d];
@@ -1628,46 +1650,49 @@ __global__ __launch_bounds__(128) void attn_spatial_bwd_generic_kernel(
     }
   }
 #pragma unroll
-  for (int d = 0; d < kDP; ++d) {
+  for (int d = 0; d < DP; ++d) {
     red[threadIdx.x][d] = gbk[d];
-    red[threadIdx.x][kDP + d] = gbv[d];
+    red[threadIdx.x][DP + d] = gbv[d];
   }
   __syncthreads();
-  if (threadIdx.x < 2 * kDP) {
-    float s = 0.f;
+  if (threadIdx.x < 2 * DP) {
+    double s = 0.0;  // (fp64: as attn_bwd_dq_generic_kernel)
     for (int i = 0; i < 128; ++i) s += red[i][threadIdx.x];
-    bpart[((size_t)head * gridDim.x + blockIdx.x) * 2 * kDP + threadIdx.x] = s;
+    bpart[((size_t)head * gridDim.x + blockIdx.x) * 2 * DP + threadIdx.x] = s;
   }
 }
 
 int attn_spatial_bwd_parts(int nf, int L, int D) {
-  if (L == 4 && D % 8 == 0) return (nf * 4 + 255) / 256;
+  if (L == 4 && D % 8 == 0 && D < kDP) return (nf * 4 + 255) / 256;
   return (nf + 127) / 128;
 }
 
 hipError_t attn_spatial_bwd_launch(int dtype, int nf, int L, int H, int D, const void* qkv, const float* kvb,
                                    const float* mask, const void* dout, const float* rope, int rope_rows, void* dqkv,
                                    float* bpart, float qscale, hipStream_t s) {
-  if (L == 4 && D % 8 == 0) {
+  if (L == 4 && D % 8 == 0 && D < kDP) {  // (the quad kernel's bias rows are 32 wide)
     dim3 grid((unsigned)((nf * 4 + 255) / 256), H);
 #define MDG_SQ(CTT, DM)                                                                                           \
   hipLaunchKernelGGL((attn_spatial_bwd_quad_kernel<CTT, DM>), grid, dim3(256), 0, s, (const CTT*)qkv, kvb, mask, \
                      (const CTT*)dout, rope, rope_rows, (CTT*)dqkv, bpart, nf, H, D, qscale)
     if (dtype == MDG_BF16) {
-      if (D <= 16) MDG_SQ(bf16_t, 16); else if (D <= 24) MDG_SQ(bf16_t, 24); else MDG_SQ(bf16_t, 32);
+      if (D <= 16) MDG_SQ(bf16_t, 16); else MDG_SQ(bf16_t, 24);
     } else {
-      if (D <= 16) MDG_SQ(float, 16); else if (D <= 24) MDG_SQ(float, 24); else MDG_SQ(float, 32);
+      if (D <= 16) MDG_SQ(float, 16); else MDG_SQ(float, 24);
     }
 #undef MDG_SQ
     return hipGetLastError();
   }
   dim3 grid((unsigned)((nf + 127) / 128), H);
-  if (dtype == MDG_BF16)
-    hipLaunchKernelGGL(attn_spatial_bwd_generic_kernel<bf16_t>, grid, dim3(128), 0, s, (const bf16_t*)qkv, kvb, mask,
-                       (const bf16_t*)dout, rope, rope_rows, (bf16_t*)dqkv, bpart, nf, L, H, D, qscale);
-  else
-    hipLaunchKernelGGL(attn_spatial_bwd_generic_kernel<float>, grid, dim3(128), 0, s, (const float*)qkv, kvb, mask,
-                       (const float*)dout, rope, rope_rows, (float*)dqkv, bpart, nf, L, H, D, qscale);
+#define MDG_SG(CTT, DPP)                                                                                          \
+  hipLaunchKernelGGL((attn_spatial_bwd_generic_kernel<CTT, DPP>), grid, dim3(128), 0, s, (const CTT*)qkv, kvb,    \
+                     mask, (const CTT*)dout, rope, rope_rows, (CTT*)dqkv, bpart, nf, L, H, D, qscale)
+  if (dtype == MDG_BF16) {
+    if (D < kDP) MDG_SG(bf16_t, kDP); else MDG_SG(bf16_t, MDG_DP_WIDE);
+  } else {
+    if (D < kDP) MDG_SG(float, kDP); else MDG_SG(float, MDG_DP_WIDE);
+  }
+#undef MDG_SG
   return hipGetLastError();
 }
 

@@ -414,15 +414,17 @@ class LatentMDGenModel(nn.Module):
 
     def _use_hip_layers(self, h):
         """Differentiable calls on a ROCm device run the block stack through the HIP training
-        Function (train_backend 'hip', the default); dropout > 0 while training and head_dim >= 32
-        are not built there and take eager autograd."""
+        Function (train_backend 'hip', the default); dropout > 0 while training and head_dims the
+        kernels do not take (>= 64, or not a multiple of 4) are not built there and take eager
+        autograd, with a warning.  head_dim 32..63 runs on 64-column attention planes (ABI 23)."""
         if self.backend != "hip" or getattr(self, "train_backend", "hip") != "hip" or not h.is_cuda:
             return False
         if not torch.is_grad_enabled():
             return False
         why = None
-        if self.args.embed_dim // self.args.mha_heads >= 32:  # the training kernels take head_dim < 32
-            why = f"head_dim {self.args.embed_dim // self.args.mha_heads} >= 32"
+        hd = self.args.embed_dim // self.args.mha_heads
+        if hd >= 64 or hd % 4:  # the training kernels' planes: MDG_HEAD_STRIDE(D) <= 64 columns
+            why = f"head_dim {hd} (the kernels take multiples of 4 below 64)"
         elif self.training and float(getattr(self.args, "dropout", 0.0) or 0.0) > 0.0:
             why = f"--dropout {self.args.dropout} (attention-probability dropout, mha.py:383)"
         if why is not None:

@@ -271,7 +271,7 @@ class _HipLayerFn(torch.autograd.Function):
             P[f"wqkv{i}"], P[f"wqkv_t{i}"], P[f"bqkv{i}"] = ee(3 * C, C), ee(C, 3 * C), ee(3 * C, dt=torch.float32)
             P[f"wo{i}"], P[f"wo_t{i}"] = ee(C, C), ee(C, C)
             P[f"bo{i}"] = bo.float().contiguous()
-            P[f"kvb{i}"] = ee(H, 2, _lib.MDG_DP, dt=torch.float32)
+            P[f"kvb{i}"] = ee(H, 2, _lib.head_stride(D), dt=torch.float32)
             S, rows = (L, L + 1) if i == 0 else (T, T + 1)
             tab = hl.table(rows, inv_freq) if hl.rope else None
             tabs.append(tab)
@@ -300,8 +300,9 @@ class _HipLayerFn(torch.autograd.Function):
         # k / v column D) are written once (init_planes) instead of a memset + set_vpad pass per
         # step; the q|k|v GEMM rewrites every other column each forward
         lease = _PlaneLease()
-        planes_t, fresh_t = hl.planes(("t", params[0].data_ptr(), B, T, L), (3, B * L, H, T, _lib.MDG_DP), dev, lease)
-        planes_s, fresh_s = (hl.planes(("s", params[0].data_ptr(), B, T, L), (3, B * T, H, L, _lib.MDG_DP), dev,
+        dp = _lib.head_stride(D)  # 32, or 64 for head_dim 32..63
+        planes_t, fresh_t = hl.planes(("t", params[0].data_ptr(), B, T, L), (3, B * L, H, T, dp), dev, lease)
+        planes_s, fresh_s = (hl.planes(("s", params[0].data_ptr(), B, T, L), (3, B * T, H, L, dp), dev,
                                        lease) if long_l else (e(N, 3 * C), False))
         next_mods, pre = chain if chain is not None else (None, None)
         sv = {"xn": [r(C) for _ in range(3)], "stats": [e(N, 2, dt=torch.float32) for _ in range(3)],
@@ -407,25 +408,27 @@ class _HipLayerFn(torch.autograd.Function):
                 Bq, Tq, Lq = (B, T, L) if i == 1 else (B * T, L, 1)
                 rope, rows = (rope_t, T + 1) if i == 1 else (rope_l, L + 1)
                 kb = kb_t if i == 1 else kb_s
-                parts = lib.mdg_attn_temporal_bwd_parts(dt, Bq, Tq, Lq, _ATTN_BWD_VARIANT)
-                bpart = torch.empty(H, parts, 2, _lib.MDG_DP, device=dev)  # every slot is written
-                scratch = torch.empty(lib.mdg_attn_temporal_bwd_scratch(dt, Bq, Tq, Lq, H), device=dev,
+                # the wide heads (head_dim 32..63) take the scalar kernels (generic 1)
+                variant = _ATTN_BWD_VARIANT if D < _lib.MDG_DP else 1
+                parts = lib.mdg_attn_temporal_bwd_parts(dt, Bq, Tq, Lq, variant)
+                bpart = torch.empty(H, parts, 2, _lib.head_stride(D), device=dev)  # every slot is written
+                scratch = torch.empty(lib.mdg_attn_temporal_bwd_scratch(dt, Bq, Tq, Lq, H, D), device=dev,
                                       dtype=torch.uint8)
                 _lib.check(lib.mdg_attn_temporal_bwd(dt, Bq, Tq, Lq, H, D, qkv.data_ptr(), kb.data_ptr(),
                                                      P[f"kvb{i}"].data_ptr(), o.data_ptr(), _lib.ptr(o_lo),
                                                      do.data_ptr(),
                                                      lse.data_ptr(), _lib.ptr(rope), rows, scratch.data_ptr(),
                                                      dqkv.data_ptr(), 3 * C, bpart.data_ptr(), qscale, _LN2,
-                                                     _ATTN_BWD_VARIANT, s),
+                                                     variant, s),
                            "mdg_attn_temporal_bwd")
             else:
                 parts = lib.mdg_attn_spatial_bwd_parts(B * T, L, D)
-                bpart = torch.empty(H, parts, 2, _lib.MDG_DP, device=dev)
+                bpart = torch.empty(H, parts, 2, _lib.head_stride(D), device=dev)
                 _lib.check(lib.mdg_attn_spatial_bwd(dt, B * T, L, H, D, qkv.data_ptr(), P["kvb0"].data_ptr(),
                                                     ctx.mask.data_ptr(), do.data_ptr(), _lib.ptr(rope_l), L + 1,
                                                     dqkv.data_ptr(), bpart.data_ptr(), qscale, s),
                            "mdg_attn_spatial_bwd")
-            # [H][parts][2][32]: the unpack sums the slots (one block per head, 4 waves in order)
+            # [H][parts][2][DP]: the unpack sums the slots (one block per head, 4 waves in order)
             grads[f"kvb{i}"] = bpart
             grads[f"wqkv{i}"], grads[f"bqkv{i}"] = wg(dqkv, xn, True)
             return dx_gemm(dqkv, P[f"wqkv_t{i}"], 3 * C, C)

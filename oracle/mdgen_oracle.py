@@ -147,7 +147,9 @@ def timestep_embedding(t, dim=256, max_period=10000):
     half = dim // 2
     freqs = torch.exp(-math.log(max_period) * torch.arange(0, half, dtype=torch.float32) / half)
     args = t[:, None].float() * freqs[None]
-    return torch.cat([torch.cos(args), torch.sin(args)], dim=-1)
+    emb = torch.cat([torch.cos(args), torch.sin(args)], dim=-1)
+    # (an fp64 run of the oracle — the tests' exact reference — keeps the fp32 embedding, upcast)
+    return emb.double() if t.dtype == torch.float64 else emb
 
 
 def t_embedder(P, t):
@@ -193,7 +195,7 @@ def mha(P, prefix, x, valid, heads):
     w = q @ k.transpose(-1, -2)                             # [N,H,S,S+1]
     kvalid = torch.cat([valid.bool(), torch.ones(N, 1, dtype=torch.bool)], 1)
     w = w.masked_fill(~kvalid[:, None, None, :], float("-inf"))
-    w = torch.softmax(w, dim=-1, dtype=torch.float32)
+    w = torch.softmax(w, dim=-1, dtype=torch.float64 if w.dtype == torch.float64 else torch.float32)
     o = (w @ v).transpose(1, 2).reshape(N, S, C)
     return linear(P, f"{a}.out_proj", o)
 

@@ -88,13 +88,102 @@ def test_temporal_attention_backward_multi_chunk(dtype, T, n_pad):
     passes, 64-query chunks: T = 257 / 300 / 513 / 1000 take 2-4 passes with ragged tails);
     bf16-2pass: the two-pass MFMA kernels (generic 2); f32: the scalar kernels."""
     generic = 2 if dtype == "bf16-2pass" else 0
-    dtype = dtype.split("-")[0]
+    _run_bwd(dtype.split("-")[0], T, n_pad, generic)
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "f32"])
+@pytest.mark.parametrize("H,D,T,n_pad", [(8, 32, 129, 5), (8, 48, 300, -1), (6, 60, 40, 3)])
+def test_temporal_attention_backward_wide_heads(dtype, H, D, T, n_pad):
+    """head_dim 32..63 (--embed_dim 256 --mha_heads 8 and the like; mha.py:96-102 takes any
+    embed_dim // num_heads): 64-column planes (MDG_HEAD_STRIDE), the scalar kernels (generic 1,
+    the only route for these heads), O's bf16 residual from the wide forward kernel."""
+    _run_bwd(dtype, T, n_pad, 1, H=H, D=D)
+
+
+def test_temporal_attention_backward_wide_heads_refuses_mfma_variants():
+    """The MFMA variants' LDS images are 32 columns wide: a bf16 call with head_dim >= 32 and
+    generic 0 / 2 is refused (its bias slots would not match mdg_attn_temporal_bwd_parts)."""
     from mdgen_finetune_amd import _lib
 
     lib = _lib.load()
     dev = "cuda"
-    B, L, H, D = 1, 2, 16, 24
-    BL, C, DP = B * L, H * D, _lib.MDG_DP
+    B, T, L, H, D = 1, 16, 2, 8, 32
+    z = lambda n, dt=torch.bfloat16: torch.zeros(n, device=dev, dtype=dt)  # noqa: E731
+    rows = B * L * H * T
+    for generic in (0, 2):
+        rc = lib.mdg_attn_temporal_bwd(_lib.MDG_BF16, B, T, L, H, D, z(3 * rows * 64).data_ptr(),
+                                       z(B * L * T, torch.float32).data_ptr(), z(H * 128, torch.float32).data_ptr(),
+                                       z(rows * D).data_ptr(), None, z(rows * D).data_ptr(),
+                                       z(rows, torch.float32).data_ptr(), None, T + 1,
+                                       z(lib.mdg_attn_temporal_bwd_scratch(_lib.MDG_BF16, B, T, L, H, D)).data_ptr(),
+                                       z(B * T * L * 3 * H * D).data_ptr(), 3 * H * D,
+                                       z(H * 64 * 128, torch.float32).data_ptr(), 1.0, 1.0, generic,
+                                       _lib.stream_handle())
+        assert rc != 0 and b"generic" in lib.mdg_last_error_string()
+    assert lib.mdg_attn_temporal_bwd_scratch(_lib.MDG_BF16, B, T, L, H, 64) == 0
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "f32"])
+@pytest.mark.parametrize("D", [24, 48])
+def test_spatial_long_route_backward_shape(dtype, D):
+    """The shape the L >= 16 spatial attention hands these kernels: B*T sequences of L = 16 keys,
+    one residue each (Lq = 1), padded keys."""
+    _run_bwd(dtype, 16, 3, 1 if D >= 32 else 0, H=8, D=D, B=10, L=1)
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "f32"])
+@pytest.mark.parametrize("B,T,L,H,D", [(10, 16, 1, 8, 48), (2, 5, 16, 8, 48), (10, 16, 1, 12, 32), (1, 300, 2, 8, 48),
+                                       (10, 16, 1, 16, 24)])
+def test_temporal_attention_forward_lse(dtype, B, T, L, H, D):
+    """mdg_attn_temporal_lse (the training forward: O, its bf16 residual, the log2-sum-exp2 rows)
+    against fp64 torch on the same CT operands, narrow and wide heads."""
+    from mdgen_finetune_amd import _lib
+
+    lib = _lib.load()
+    dev = "cuda"
+    BL, C, DP = B * L, H * D, _lib.head_stride(D)
+    ct = torch.bfloat16 if dtype == "bf16" else torch.float32
+    mdt = _lib.MDG_BF16 if dtype == "bf16" else _lib.MDG_F32
+    c = _case(T, BL, H, D, 3, seed=7 * T + D)
+    log2e = 1.0 / math.log(2.0)
+    planes = torch.zeros(3, BL, H, T, DP, device=dev, dtype=ct)
+    planes[0, ..., :D] = (c["q_lin"] * D ** -0.5 * log2e).to(ct)
+    planes[1, ..., :D] = c["k_lin"].to(ct)
+    planes[2, ..., :D] = c["v"].to(ct)
+    planes[1, ..., D] = 1.0
+    planes[2, ..., D] = 1.0
+    qp, kp, vp = (planes[i, ..., :D].double() for i in range(3))
+    kvb = torch.zeros(H, 2, DP, device=dev)
+    kvb[:, 0, :D] = c["bk_lin"].float()
+    kvb[:, 1, :D] = c["bv"].float()
+    kvb[:, 1, D] = 1.0  # the bias value row's pad column carries the bias key's share of the row sum
+    s2 = torch.einsum("shtd,shud->shtu", qp, kp) + c["kbias"][:, None, None, :]
+    sb2 = torch.einsum("shtd,hd->sht", qp, kvb[:, 0, :D].double())[..., None]
+    s2 = torch.cat([sb2, s2], -1)
+    lse = torch.logsumexp(s2 * math.log(2.0), -1) * log2e
+    p2 = torch.exp2(s2 - lse[..., None])
+    o = p2[..., :1] * kvb[None, :, 1, None, :D].double() + torch.einsum("shtu,shud->shtd", p2[..., 1:], vp)
+    o_ref = o.reshape(B, L, H, T, D).permute(0, 3, 1, 2, 4).reshape(B * T * L, C)
+    out = torch.full((B * T * L, C), float("nan"), device=dev, dtype=ct)
+    lo = torch.full_like(out, float("nan")) if dtype == "bf16" else None
+    lse_k = torch.full((BL, H, T), float("nan"), device=dev)
+    _lib.check(lib.mdg_attn_temporal_lse(mdt, B, T, L, H, D, planes.data_ptr(), c["kbias"].float().contiguous().data_ptr(),
+                                         kvb.data_ptr(), out.data_ptr(), _lib.ptr(lo), lse_k.data_ptr(),
+                                         _lib.stream_handle()), "mdg_attn_temporal_lse")
+    torch.cuda.synchronize()
+    got = out.double() + (lo.double() if lo is not None else 0)
+    err = float((got - o_ref).norm() / o_ref.norm())
+    lerr = float((lse_k.double() - lse).abs().max())
+    assert err <= (2e-3 if dtype == "bf16" else 1e-5), (err, lerr)
+    assert lerr <= (2e-2 if dtype == "bf16" else 1e-4), (err, lerr)
+
+
+def _run_bwd(dtype, T, n_pad, generic, H=16, D=24, B=1, L=2):
+    from mdgen_finetune_amd import _lib
+
+    lib = _lib.load()
+    dev = "cuda"
+    BL, C, DP = B * L, H * D, _lib.head_stride(D)
     ct = torch.bfloat16 if dtype == "bf16" else torch.float32
     mdt = _lib.MDG_BF16 if dtype == "bf16" else _lib.MDG_F32
     qscale, log2e = D ** -0.5, 1.0 / math.log(2.0)
@@ -136,7 +225,7 @@ def test_temporal_attention_backward_multi_chunk(dtype, T, n_pad):
         rope = torch.cat([cos.float().reshape(-1), sin.float().reshape(-1)]).contiguous()
         parts = lib.mdg_attn_temporal_bwd_parts(mdt, B, T, L, generic)
         bpart = torch.full((H, parts, 2, DP), float("nan"), device=dev)  # every slot is written
-        scratch = torch.empty(lib.mdg_attn_temporal_bwd_scratch(mdt, B, T, L, H), device=dev, dtype=torch.uint8)
+        scratch = torch.empty(lib.mdg_attn_temporal_bwd_scratch(mdt, B, T, L, H, D), device=dev, dtype=torch.uint8)
         dqkv = torch.full((B * T * L, 3 * C), float("nan"), device=dev, dtype=ct)
         _lib.check(lib.mdg_attn_temporal_bwd(mdt, B, T, L, H, D, planes.data_ptr(), kb.data_ptr(), kvb.data_ptr(),
                                              o_t.data_ptr(), _lib.ptr(lo_t), do_t.data_ptr(), lse_f.data_ptr(),
@@ -157,7 +246,7 @@ def test_temporal_attention_backward_multi_chunk(dtype, T, n_pad):
     if path:
         with open(path, "a") as f:
             f.write(json.dumps({"test": "attn_temporal_bwd", "dtype": dtype, "generic": generic, "T": T, "n_pad": n_pad,
-                                **errs}) + "\n")
+                                "H": H, "D": D, **errs}) + "\n")
     assert torch.isfinite(got).all(), "unwritten or non-finite dq|dk|dv"
     for k, e in errs.items():
         assert e <= tol, (k, e, errs)

@@ -3,7 +3,8 @@
 the generic 16x16 MFMA kernel, the spatial L = 4 path the quad kernel (D <= 32) or the generic
 VALU kernel.  The reference accepts any embed_dim // num_heads (mha.py:98-102).  Forward and a
 short Euler solve against the oracle, both operand types, at the tolerances of
-tests/test_gpu_parity.py."""
+tests/test_gpu_parity.py; and the training path's loss and gradients against the oracle's
+autograd (the layer-level checks are tests/test_gpu_train.py::test_hip_layer_backward_wide_heads)."""
 import pytest
 import torch
 
@@ -55,6 +56,24 @@ def test_wide_head_forward_and_euler_match_oracle(flags, T, L, n_pad, dtype):
         fn = Sampler(create_transport(m.args, "GVP", "velocity")).sample_ode(sampling_method="euler", num_steps=4)
         ys = fn(g("x"), functools.partial(m.forward_inference, **kw))
     _check(ys[-1], ys_ref[-1], dtype, solve=True, valid=valid)
+
+
+@pytest.mark.parametrize("dtype,flags,B,T", [
+    ("f32", ["--embed_dim", "256", "--mha_heads", "8"], 2, 24),   # D = 32
+    ("bf16", ["--embed_dim", "256", "--mha_heads", "8"], 2, 24),
+    ("f32", ["--embed_dim", "384", "--mha_heads", "8"], 1, 40),   # D = 48
+    ("bf16", ["--embed_dim", "384", "--mha_heads", "8"], 1, 40),
+])
+def test_wide_head_training_grads_match_oracle(dtype, flags, B, T):
+    """Training at head_dim 32..63 on the HIP kernels (ABI 23; the reference trains any
+    embed_dim // num_heads, mha.py:96-102): the GVP loss and every parameter gradient of the whole
+    model (5 layers, IPA prepend) against the oracle's CPU autograd, bounds as config 3's
+    (tests/test_gpu_train.py::test_default_dims_training_grads_match_oracle); the f32 path
+    against an fp64 oracle run, each gradient within max(1e-4, 2x the fp32 oracle's own error)
+    (the IPA q-projection gradients are ill-conditioned here: fp32 oracle vs fp64 1.5e-3)."""
+    from tests.test_gpu_train import training_grads_vs_oracle
+
+    training_grads_vs_oracle(dtype, B, T, flags=flags, tag="wide_head_grads", ref64=True)
 
 
 def test_wide_head_plan_names_the_generic_route():

@@ -34,7 +34,7 @@ def main():
     # bias-gradient slots: the two-pass kernels need more than the fused one (one per query block and wave)
     parts = max(lib.mdg_attn_temporal_bwd_parts(_lib.MDG_BF16, B, T, L, g) for g in (0, 2))
     bpart = torch.zeros(H, parts, 2, DP, device=dev)
-    scratch = torch.empty(lib.mdg_attn_temporal_bwd_scratch(_lib.MDG_BF16, B, T, L, H), device=dev, dtype=torch.uint8)
+    scratch = torch.empty(lib.mdg_attn_temporal_bwd_scratch(_lib.MDG_BF16, B, T, L, H, D), device=dev, dtype=torch.uint8)
     dqkv = torch.empty(B * T * L, 3 * C, device=dev, dtype=torch.bfloat16)
     s = _lib.stream_handle()
 

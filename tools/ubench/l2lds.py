@@ -44,3 +44,11 @@ for blocks in (8, 32, 64, 128, 256):
     rc2 = lib.l2vgpr_run(buf.data_ptr(), 2 << 20, steps, 0, blocks, sink.data_ptr(), ctypes.byref(ms2))
     print(json.dumps({"blocks": blocks, "lds_dma_B_per_clk_cu": round(by / (ms.value * 1e-3) / CLK / blocks, 1),
                       "vgpr_B_per_clk_cu": round(by / (ms2.value * 1e-3) / CLK / blocks, 1), "rc": [rc, rc2]}), flush=True)
+# co-resident blocks per CU: 256 / 512 / 1024 blocks of 512 threads, 32 KiB of LDS each (depth 2 x 2 pieces)
+for blocks in (256, 512, 1024):
+    steps = 2000
+    ms = ctypes.c_float()
+    rc = lib.l2lds_run(buf.data_ptr(), 2 << 20, steps, 2, 2, blocks, sink.data_ptr(), ctypes.byref(ms))
+    by = blocks * steps * 512 * 16 * 2
+    print(json.dumps({"blocks_total": blocks, "per_cu": blocks // CUS, "rc": rc,
+                      "lds_dma_B_per_clk_cu": round(by / (ms.value * 1e-3) / CLK / CUS, 1)}), flush=True)
