@@ -587,7 +587,8 @@ int mdg_final_bwd_train(int32_t N, int32_t rows_per_b, int32_t C, int32_t latent
                         float* dmods, void* ws, size_t ws_bytes, void* stream);
 
 /* Invariant point attention core of the IPA prepend under autograd (reference
-   src/mdgen/model/ipa.py:92-255, c_z = 0; latent_model.py:179-214), fp32, L <= 32, c = 32,
+   src/mdgen/model/ipa.py:92-255, c_z = 0; latent_model.py:179-214), fp32, L <= 256 (33..256 on
+   the long kernels since round 5: ATLAS crops), c = 32,
    8 query/key points and 8 value points (the reference's defaults; other shapes: MDG_E_SHAPE).
    Operands per token b*L + i, head h:  q [..][H][c], kv [..][H][2c] (k | v), mask [B][L], rots
    [B][L][3][3], trans [B][L][3], wc = sqrt(1 / (3c)); the points and head weights by `flags`:

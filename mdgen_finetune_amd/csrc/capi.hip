@@ -1134,7 +1134,7 @@ int mdg_ipa_core_fwd(int32_t B, int32_t L, int32_t H, int32_t c, int32_t Pq, int
                      const float* trans, const float* hw, float wc, float* out, int32_t flags, void* stream) {
   if (!q || !kv || !qp || !kvp || !mask || !rots || !trans || !hw || !out) return fail(MDG_E_ARG, "ipa_core_fwd: null");
   if (B <= 0 || H <= 0 || !mdg::ipa_core_supported(L, c, Pq, Pv))
-    return fail(MDG_E_SHAPE, "ipa_core_fwd: B=%d L=%d H=%d c=%d Pq=%d Pv=%d (L <= 32, c = 32, 8 + 8 points)", B, L, H,
+    return fail(MDG_E_SHAPE, "ipa_core_fwd: B=%d L=%d H=%d c=%d Pq=%d Pv=%d (L <= 256, c = 32, 8 + 8 points)", B, L, H,
                 c, Pq, Pv);
   if (flags & ~(MDG_IPA_LOCAL_POINTS | MDG_IPA_RAW_HW)) return fail(MDG_E_ARG, "ipa_core_fwd: flags %d", flags);
   return hip_check(mdg::ipa_core_fwd_launch(B, L, H, q, kv, qp, kvp, mask, rots, trans, hw, wc, out, flags,
@@ -1150,7 +1150,7 @@ int mdg_ipa_core_bwd(int32_t B, int32_t L, int32_t H, int32_t c, int32_t Pq, int
       !dhw_part)
     return fail(MDG_E_ARG, "ipa_core_bwd: null");
   if (B <= 0 || H <= 0 || !mdg::ipa_core_supported(L, c, Pq, Pv))
-    return fail(MDG_E_SHAPE, "ipa_core_bwd: B=%d L=%d H=%d c=%d Pq=%d Pv=%d (L <= 32, c = 32, 8 + 8 points)", B, L, H,
+    return fail(MDG_E_SHAPE, "ipa_core_bwd: B=%d L=%d H=%d c=%d Pq=%d Pv=%d (L <= 256, c = 32, 8 + 8 points)", B, L, H,
                 c, Pq, Pv);
   if (flags & ~(MDG_IPA_LOCAL_POINTS | MDG_IPA_RAW_HW)) return fail(MDG_E_ARG, "ipa_core_bwd: flags %d", flags);
   return hip_check(mdg::ipa_core_bwd_launch(B, L, H, q, kv, qp, kvp, mask, rots, trans, hw, wc, dout, dq, dkv, dqp,

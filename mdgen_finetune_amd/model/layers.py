@@ -217,7 +217,7 @@ class AttentionWithRoPE(nn.Module):
 class _IpaCoreFn(torch.autograd.Function):
     """The IPA attention core (logits, softmax, value / point aggregation, inverse frame, point
     norms: ipa.py:149-250) as one HIP kernel each way (csrc/ipa_train.hip, mdg_ipa_core_fwd /
-    _bwd).  flags 0: points in the global frame and hw = softplus(head_weights) * c;
+    _bwd; crops up to 32 residues on one wave per (sample, head), 33..256 on the long kernels).  flags 0: points in the global frame and hw = softplus(head_weights) * c;
     MDG_IPA_LOCAL_POINTS | MDG_IPA_RAW_HW: the raw point projections and the raw head_weights
     (the frame application and the softplus run in the kernels, ipa.py:121-140, 178-183).
     Returns the linear_out input [B, L, H*c + 4*H*Pv]."""
@@ -280,7 +280,7 @@ class InvariantPointAttention(nn.Module):
     def forward(self, s, rots, trans, mask):
         B, L, _ = s.shape
         H, c, Pq, Pv = self.no_heads, self.c_hidden, self.no_qk_points, self.no_v_points
-        hip = self.hip_core and s.is_cuda and L <= 32 and c == 32 and Pq == 8 and Pv == 8
+        hip = self.hip_core and s.is_cuda and L <= 256 and c == 32 and Pq == 8 and Pv == 8
         if hip:
             from ..train_hip import seg_linear, seg_supported
 

@@ -27,10 +27,13 @@ def _frames(B, L, gen):
 
 
 @pytest.mark.parametrize("seg", ["1", "0"])
-@pytest.mark.parametrize("B,L,n_pad", [(8, 4, 0), (3, 6, 2), (2, 20, 3), (2, 32, 0)])
+@pytest.mark.parametrize("B,L,n_pad", [(8, 4, 0), (3, 6, 2), (2, 20, 3), (2, 32, 0), (2, 33, 1), (1, 100, 7),
+                                       (1, 256, 51)])
 def test_ipa_core_matches_eager_autograd(B, L, n_pad, seg, monkeypatch):
     """seg "1": the projections on mdg_seg_linear and the frames / softplus inside the core
-    (MDG_IPA_LOCAL_POINTS | MDG_IPA_RAW_HW); "0": eager projections and global-frame points."""
+    (MDG_IPA_LOCAL_POINTS | MDG_IPA_RAW_HW); "0": eager projections and global-frame points.
+    L <= 32: one wave per (sample, head); L = 33 / 100 / 256 (ATLAS crop, 51 padded residues as
+    in tests/test_gpu_parity.py's ATLAS case): the long kernels."""
     monkeypatch.setenv("MDG_TRAIN_SEG", seg)
     gen = torch.Generator().manual_seed(100 + L)
     C = 384

@@ -590,12 +590,13 @@ def test_tps_graphed_step_equals_eager_step():
     assert float((p1 - p2).abs().max()) <= 2e-2 * 1e-3, float((p1 - p2).abs().max())
 
 
-@pytest.mark.parametrize("L", [16, 20])
+@pytest.mark.parametrize("L", [16, 20, 48])
 def test_tps_ipa_long_crop_grads_match_eager(L):
     """TPS with the IPA prepend at crops L >= 16: run_ipa calls every IPA layer twice per step
     (x_r, x_f; latent_model.py:240-243) on the HIP layer Function, whose L >= 16 spatial planes are
-    saved activations; the two calls must not share them.  Every parameter gradient of
-    the HIP f32 path against eager autograd on the same device, rel <= 1e-4."""
+    saved activations; the two calls must not share them.  L = 48: the IPA core on
+    the long kernels (33..256 residues).  Every parameter gradient of the HIP f32 path against
+    eager autograd on the same device, rel <= 1e-4."""
     from mdgen_finetune_amd.transport.transport import mean_flat
     from mdgen_finetune_amd.wrapper import NewMDGenWrapper
 
