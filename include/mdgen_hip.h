@@ -438,7 +438,7 @@ int mdg_ln_gate_bwd(int32_t dtype, int32_t M, int32_t C, int32_t rows_per_b, con
    is written; generic as passed to mdg_attn_temporal_bwd: the fused bf16 kernel writes one per
    sequence, ABI 21). */
 int32_t mdg_attn_temporal_bwd_parts(int32_t dtype, int32_t B, int32_t T, int32_t L, int32_t generic);
-int32_t mdg_attn_spatial_bwd_parts(int32_t n_frames, int32_t L, int32_t D);
+int32_t mdg_attn_spatial_bwd_parts(int32_t n_frames, int32_t L, int32_t H, int32_t D);  /* (ABI 23: takes H) */
 /* Scratch of mdg_attn_temporal_bwd: dO planes CT [B*L][H][T][DP], delta fp32 [B*L][H][T], and
    for bf16 with T > 256 and head_dim < 32 the fused kernel's fp32 dQ accumulator [B*L][H][T][32].
    ABI 23: takes head_dim D (the wide heads' 64-column planes); 0 for D outside 1..63. */

@@ -170,7 +170,7 @@ SIGNATURES = [
     ("mdg_ln_gate_bwd", _i32, [_i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp, _i32,
                                _vp, _vp, _vp]),
     ("mdg_attn_temporal_bwd_parts", _i32, [_i32, _i32, _i32, _i32, _i32]),
-    ("mdg_attn_spatial_bwd_parts", _i32, [_i32, _i32, _i32]),
+    ("mdg_attn_spatial_bwd_parts", _i32, [_i32, _i32, _i32, _i32]),
     ("mdg_attn_temporal_bwd_scratch", ctypes.c_size_t, [_i32, _i32, _i32, _i32, _i32, _i32]),
     ("mdg_attn_temporal_bwd", _i32, [_i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32,
                                      _vp, _vp, _i32, _vp, _f32, _f32, _i32, _vp]),

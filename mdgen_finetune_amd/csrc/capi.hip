@@ -80,7 +80,7 @@ hipError_t attn_temporal_bwd_launch(int dtype, int B, int T, int L, int H, int D
                                     const float* lse, const float* rope, int rope_rows, void* dop, float* delta,
                                     void* dqkv, int ldq, float* bpart, float qscale, float kscale, int generic,
                                     float* dqacc, hipStream_t s);
-int attn_spatial_bwd_parts(int nf, int L, int D);
+int attn_spatial_bwd_parts(int nf, int L, int H, int D);
 hipError_t attn_spatial_bwd_launch(int dtype, int nf, int L, int H, int D, const void* qkv, const float* kvb,
                                    const float* mask, const void* dout, const float* rope, int rope_rows, void* dqkv,
                                    float* bpart, float qscale, hipStream_t s);
@@ -1075,9 +1075,9 @@ int32_t mdg_attn_temporal_bwd_parts(int32_t dtype, int32_t B, int32_t T, int32_t
   return mdg::attn_bwd_parts(dtype, B, T, L, generic);
 }
 
-int32_t mdg_attn_spatial_bwd_parts(int32_t n_frames, int32_t L, int32_t D) {
-  if (n_frames <= 0 || L <= 0) return 0;
-  return mdg::attn_spatial_bwd_parts(n_frames, L, D);
+int32_t mdg_attn_spatial_bwd_parts(int32_t n_frames, int32_t L, int32_t H, int32_t D) {
+  if (n_frames <= 0 || L <= 0 || H <= 0) return 0;
+  return mdg::attn_spatial_bwd_parts(n_frames, L, H, D);
 }
 
 size_t mdg_attn_temporal_bwd_scratch(int32_t dtype, int32_t B, int32_t T, int32_t L, int32_t H, int32_t D) {

@@ -1391,19 +1391,16 @@ __device__ __forceinline__ float qbi(float x, int i) {
 }
 
 
+// One lane of the L = 4 spatial attention backward: token tok = 4 f + j, head `head` (a quad of
+// lanes = the 4 residues of one (frame, head); the other residues' rows by DPP quad broadcasts):
+// writes dq | dk | dv of its token and returns its bias_k / bias_v partials (pk = dS_b q, pv =
+// P_b dO; zero for a dead lane).
 template <typename CT, int DM>
-__global__ __launch_bounds__(256) void attn_spatial_bwd_quad_kernel(const CT* __restrict__ qkv,
-                                                                    const float* __restrict__ kvb,
-                                                                    const float* __restrict__ mask,
-                                                                    const CT* __restrict__ dout,
-                                                                    const float* __restrict__ rope, int rope_rows,
-                                                                    CT* __restrict__ dqkv, float* __restrict__ bpart,
-                                                                    int nf, int H, int D, float qscale) {
-  __shared__ float red[256][2 * DM + 1];
-  const int head = blockIdx.y;
-  const int idx = blockIdx.x * 256 + threadIdx.x;
-  const bool live = idx < nf * 4;
-  const int j = idx & 3, f = (live ? idx : nf * 4 - 1) >> 2, tok = f * 4 + j;
+__device__ __forceinline__ void spatial_bwd_quad_lane(const CT* __restrict__ qkv, const float* __restrict__ kvb,
+                                                      const float* __restrict__ mask, const CT* __restrict__ dout,
+                                                      const float* __restrict__ rope, int rope_rows,
+                                                      CT* __restrict__ dqkv, int H, int D, float qscale, int head,
+                                                      int tok, int j, bool live, float (&pk)[DM], float (&pv)[DM]) {
   const int C = H * D;
   const CT* base = qkv + (size_t)tok * 3 * C + head * D;
   float q[DM], k[DM], v[DM], g[DM];
@@ -1428,7 +1425,7 @@ __global__ __launch_bounds__(256) void attn_spatial_bwd_quad_kernel(const CT* __
   }
   const float kvalid = (!mask || mask[tok] != 0.f) ? 1.f : 0.f;
   const float* bk = kvb + head * 2 * kDP;
-  const float* bv = bk + kDP;
+  const float* bv = bk + kDP;  // (kvb rows 32 wide: D < 32 on this route)
   float sb = 0.f, dpb = 0.f;
 #pragma unroll
   for (int d = 0; d < DM; ++d) {
@@ -1518,8 +1515,8 @@ __global__ __launch_bounds__(256) void attn_spatial_bwd_quad_kernel(const CT* __
   }
 #pragma unroll
   for (int d = 0; d < DM; ++d) {
-    red[threadIdx.x][d] = live ? dsb * q[d] : 0.f;
-    red[threadIdx.x][DM + d] = live ? pb * g[d] : 0.f;
+    pk[d] = live ? dsb * q[d] : 0.f;
+    pv[d] = live ? pb * g[d] : 0.f;
   }
   {
     float dk[DM];
@@ -1541,6 +1538,28 @@ __global__ __launch_bounds__(256) void attn_spatial_bwd_quad_kernel(const CT* __
       for (int d = 0; d < DM; ++d) dv[d] += pJ[i] * qbi(g[d], i);
     store_row(2, dv, false, 1.0f);
   }
+}
+
+template <typename CT, int DM>
+__global__ __launch_bounds__(256) void attn_spatial_bwd_quad_kernel(const CT* __restrict__ qkv,
+                                                                    const float* __restrict__ kvb,
+                                                                    const float* __restrict__ mask,
+                                                                    const CT* __restrict__ dout,
+                                                                    const float* __restrict__ rope, int rope_rows,
+                                                                    CT* __restrict__ dqkv, float* __restrict__ bpart,
+                                                                    int nf, int H, int D, float qscale) {
+  __shared__ float red[256][2 * DM + 1];
+  const int head = blockIdx.y;
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  const bool live = idx < nf * 4;
+  const int j = idx & 3, f = (live ? idx : nf * 4 - 1) >> 2, tok = f * 4 + j;
+  float pk[DM], pv[DM];
+  spatial_bwd_quad_lane<CT, DM>(qkv, kvb, mask, dout, rope, rope_rows, dqkv, H, D, qscale, head, tok, j, live, pk, pv);
+#pragma unroll
+  for (int d = 0; d < DM; ++d) {
+    red[threadIdx.x][d] = pk[d];
+    red[threadIdx.x][DM + d] = pv[d];
+  }
   // bias_k / bias_v partials of the block: 4 row groups of 64 in parallel, then the 4 sums
   // (a 256-long serial LDS chain per column before)
   __syncthreads();
@@ -1555,6 +1574,67 @@ __global__ __launch_bounds__(256) void attn_spatial_bwd_quad_kernel(const CT* __
     const float s = (red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x]);
     const int which = threadIdx.x / DM, d = threadIdx.x % DM;
     if (d < kDP) bpart[((size_t)head * gridDim.x + blockIdx.x) * 2 * kDP + which * kDP + d] = s;
+  }
+}
+
+// The same lanes ordered as the forward's (attn_spatial_quad_kernel): lane = (f H + h) 4 + j, so a
+// wave reads 16 heads' contiguous pieces of 4 tokens' rows (attn_spatial_bwd_quad_kernel's head-
+// per-block order read each row piece from a different line: 2.6 TB/s).  A grid-stride loop of
+// spq_blocks() blocks keeps every thread on one head (256 % 4H == 0); each iteration's bias
+// partials are summed over the quad by shuffles and added by the quad's lane 0 into the quad's
+// own LDS row (no registers held across iterations), and at the end the block's quads of each
+// head are summed: one slot per block and head.
+static int spq_blocks() {  // MDG_SPQ_BLOCKS: the grid-stride loop's block count (tuning)
+  static const int v = [] {
+    const char* e = getenv("MDG_SPQ_BLOCKS");
+    return e ? atoi(e) : 256;  // one per CU: 11.61 ms step vs 11.66 (512), 11.9 (1024), 12.4 (2048+)
+  }();
+  return v;
+}
+__host__ __device__ constexpr bool spq_heads_ok(int H) { return H > 0 && H <= 64 && 256 % (4 * H) == 0; }
+
+template <typename CT, int DM>
+__global__ __launch_bounds__(256) void attn_spatial_bwd_quadh_kernel(const CT* __restrict__ qkv,
+                                                                     const float* __restrict__ kvb,
+                                                                     const float* __restrict__ mask,
+                                                                     const CT* __restrict__ dout,
+                                                                     const float* __restrict__ rope, int rope_rows,
+                                                                     CT* __restrict__ dqkv, float* __restrict__ bpart,
+                                                                     int nf, int H, int D, float qscale) {
+  __shared__ float red[64][2 * DM + 1];  // [quad][bias_k | bias_v]
+  const int total = nf * H * 4, head = (threadIdx.x >> 2) % H, quad = threadIdx.x >> 2;
+  const bool lead = (threadIdx.x & 3) == 0;
+  if (lead)
+    for (int c = 0; c < 2 * DM; ++c) red[quad][c] = 0.f;
+  for (int base = blockIdx.x * 256; base < total; base += gridDim.x * 256) {  // (block-uniform)
+    const int idx = base + threadIdx.x;
+    const bool live = idx < total;  // (total % 4 == 0: a quad is live or dead as a whole)
+    const int j = idx & 3, fh = (live ? idx : total - 1) >> 2, f = fh / H, tok = f * 4 + j;
+    float pk[DM], pv[DM];
+    spatial_bwd_quad_lane<CT, DM>(qkv, kvb, mask, dout, rope, rope_rows, dqkv, H, D, qscale, head, tok, j, live, pk,
+                                  pv);
+#pragma unroll
+    for (int d = 0; d < DM; ++d) {
+      pk[d] += __shfl_xor(pk[d], 1, 64);
+      pk[d] += __shfl_xor(pk[d], 2, 64);
+      pv[d] += __shfl_xor(pv[d], 1, 64);
+      pv[d] += __shfl_xor(pv[d], 2, 64);
+    }
+    if (lead) {
+#pragma unroll
+      for (int d = 0; d < DM; ++d) {
+        red[quad][d] += pk[d];
+        red[quad][DM + d] += pv[d];
+      }
+    }
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < H * 2 * DM; e += 256) {  // quads h, h + H, ... of the block
+    const int h = e / (2 * DM), c = e % (2 * DM);
+    float sacc = 0.f;
+    for (int qd = h; qd < 64; qd += H) sacc += red[qd][c];
+    const int which = c / DM, d = c % DM;
+    bpart[((size_t)h * gridDim.x + blockIdx.x) * 2 * kDP + which * kDP + d] = sacc;
   }
 }
 
@@ -1662,7 +1742,19 @@ __global__ __launch_bounds__(128) void attn_spatial_bwd_generic_kernel(
   }
 }
 
-int attn_spatial_bwd_parts(int nf, int L, int D) {
+static bool spq_on() {  // MDG_SPATIAL_BWD_QUADH=0: the head-per-block quad kernel (A/B)
+  static const bool v = [] {
+    const char* e = getenv("MDG_SPATIAL_BWD_QUADH");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
+int attn_spatial_bwd_parts(int nf, int L, int H, int D) {
+  if (L == 4 && D % 8 == 0 && D < kDP && spq_on() && spq_heads_ok(H)) {
+    const long long blocks = ((long long)nf * H * 4 + 255) / 256;
+    return (int)(blocks < spq_blocks() ? blocks : spq_blocks());
+  }
   if (L == 4 && D % 8 == 0 && D < kDP) return (nf * 4 + 255) / 256;
   return (nf + 127) / 128;
 }
@@ -1670,6 +1762,19 @@ int attn_spatial_bwd_parts(int nf, int L, int D) {
 hipError_t attn_spatial_bwd_launch(int dtype, int nf, int L, int H, int D, const void* qkv, const float* kvb,
                                    const float* mask, const void* dout, const float* rope, int rope_rows, void* dqkv,
                                    float* bpart, float qscale, hipStream_t s) {
+  if (L == 4 && D % 8 == 0 && D < kDP && spq_on() && spq_heads_ok(H)) {
+    dim3 grid((unsigned)attn_spatial_bwd_parts(nf, L, H, D));
+#define MDG_SQH(CTT, DM)                                                                                            \
+  hipLaunchKernelGGL((attn_spatial_bwd_quadh_kernel<CTT, DM>), grid, dim3(256), 0, s, (const CTT*)qkv, kvb, mask, \
+                     (const CTT*)dout, rope, rope_rows, (CTT*)dqkv, bpart, nf, H, D, qscale)
+    if (dtype == MDG_BF16) {
+      if (D <= 16) MDG_SQH(bf16_t, 16); else MDG_SQH(bf16_t, 24);
+    } else {
+      if (D <= 16) MDG_SQH(float, 16); else MDG_SQH(float, 24);
+    }
+#undef MDG_SQH
+    return hipGetLastError();
+  }
   if (L == 4 && D % 8 == 0 && D < kDP) {  // (the quad kernel's bias rows are 32 wide)
     dim3 grid((unsigned)((nf * 4 + 255) / 256), H);
 #define MDG_SQ(CTT, DM)                                                                                           \

@@ -422,7 +422,7 @@ class _HipLayerFn(torch.autograd.Function):
                                                      variant, s),
                            "mdg_attn_temporal_bwd")
             else:
-                parts = lib.mdg_attn_spatial_bwd_parts(B * T, L, D)
+                parts = lib.mdg_attn_spatial_bwd_parts(B * T, L, H, D)
                 bpart = torch.empty(H, parts, 2, _lib.head_stride(D), device=dev)
                 _lib.check(lib.mdg_attn_spatial_bwd(dt, B * T, L, H, D, qkv.data_ptr(), P["kvb0"].data_ptr(),
                                                     ctx.mask.data_ptr(), do.data_ptr(), _lib.ptr(rope_l), L + 1,
