@@ -8,6 +8,7 @@ only), fair-esm RotaryEmbedding (buffer ``inv_freq``), src/mdgen/model/ipa.py:34
 """
 from __future__ import annotations
 
+import contextlib
 import math
 
 import torch
@@ -190,13 +191,13 @@ class MultiheadAttention(nn.Module):
         if self.rot_emb is not None:
             cos2, sin2 = self.rot_emb.tables2(Sk, x.device)
             q, k = apply_rope(q, cos2, sin2, doubled=True), apply_rope(k, cos2, sin2, doubled=True)
-        # softmax(q k^T masked) v (mha.py:359-389) as one SDPA call on its math backend: the
-        # default ROCm backend is wrong at some shapes (head_dim 48 over 17 keys: 3e-3 rel in fp32
-        # on random operands, 0.12 inside a training layer, against fp64 and the math backend;
-        # tools/dbg/sdpa_check.py), and this eager path is the reference the HIP kernels are
-        # tested against and the fallback that trains what they do not take
+        # softmax(q k^T masked) v (mha.py:359-389) as one SDPA call, on the GPU on its math
+        # backend: the default ROCm backend is wrong at some shapes (head_dim 48 over 17 keys:
+        # 3e-3 rel in fp32 on random operands, 0.12 inside a training layer, against fp64 and the
+        # math backend; tools/dbg/sdpa_check.py), and this eager path is the reference the HIP
+        # kernels are tested against and the fallback that trains what they do not take
         bias = torch.where(kvalid[:, None, None, :], 0.0, float("-inf")).to(q.dtype)
-        with sdpa_kernel(SDPBackend.MATH):
+        with sdpa_kernel(SDPBackend.MATH) if q.is_cuda else contextlib.nullcontext():
             o = F.scaled_dot_product_attention(q, k, v, attn_mask=bias, scale=1.0,
                                                dropout_p=self.dropout if self.training else 0.0)
         o = o.transpose(1, 2).reshape(N, S, C)
