@@ -478,3 +478,31 @@ def test_resume_mid_epoch_continues_same_epoch(tmp_path):
     assert tr2.epoch == 0 and tr2.skip_batches == 1
     tr2.fit()
     assert tr2.global_step == 4  # 1 before the save + the epoch's 3 remaining batches
+
+
+def test_hip_training_gate_by_head_dim_and_dropout():
+    """_use_hip_layers (latent_model.py): head_dim 32..63 takes the HIP training kernels since
+    ABI 23 (--embed_dim 256 --mha_heads 8), head_dim 64 and dropout > 0 are refused with one
+    RuntimeWarning per reason and train eagerly (no GPU needed: the gate reads shapes / flags)."""
+    import types
+    import warnings
+
+    from tests.conftest import build_model
+
+    m, _ = build_model(dict(flags=["--embed_dim", "256", "--mha_heads", "8", "--num_layers", "1"], latent_dim=21, L=4,
+                            T=4, tps=False, weights_seed=1), "cpu", T=4)
+    m.train()
+    dev = types.SimpleNamespace(is_cuda=True)  # stands in for a ROCm tensor
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        assert m._use_hip_layers(dev)  # head_dim 32
+    m.args.mha_heads = 4  # head_dim 64
+    with pytest.warns(RuntimeWarning, match="head_dim 64"):
+        assert not m._use_hip_layers(dev)
+    m.args.mha_heads, m.args.dropout = 8, 0.1
+    with pytest.warns(RuntimeWarning, match="dropout"):
+        assert not m._use_hip_layers(dev)
+    m.eval()  # dropout only matters while training
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")
+        assert m._use_hip_layers(dev)
