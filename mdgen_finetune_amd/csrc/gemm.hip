@@ -1029,6 +1029,9 @@ template <> struct RowCfg<64> { static constexpr int WMW = 1, STAGES = 2; };
 // 32-row tiles (round 5): a lone chain's out_proj (B = 1 window: 125 tiles instead of 32, no
 // split-K partials or reduction pass); every wave 32 rows x 48 columns
 template <> struct RowCfg<32> { static constexpr int WMW = 1, STAGES = 2; };
+// 16-row tiles: a lone chain's out_proj on 250 tiles (B = 1: M = 4 000) instead of 125 on 256 CUs;
+// every wave 16 rows x 48 columns, epilogue bands of 16 rows (2 per wave)
+template <> struct RowCfg<16> { static constexpr int WMW = 1, STAGES = 2; };
 
 template <int NCOL, int BM>
 __host__ __device__ constexpr size_t rowln_smem() {
@@ -1249,7 +1252,9 @@ __global__ __launch_bounds__(kRowThreads, BM <= 64 ? 4 : 1) void gemm_rowln_kern
   constexpr int LDS_ST = NCOL + 4, NE = NCOL / 128;  // float2 column pairs per lane per row
   constexpr int WLD = NCOL / 128;                    // W glds instructions per wave per stage
   constexpr int ALD_WAVES = BM / 16;                 // waves that stage A (one 16-row glds each)
-  constexpr int RG = (BM == 64 && NCOL > 256) ? 2 : 4;  // epilogue rows per wave processed together
+  // epilogue bands of BH rows, RPW per wave; RG of them processed together
+  constexpr int BH = BM >= 32 ? 32 : 16, RPW = BH / 8;
+  constexpr int RG = ((BM == 64 && NCOL > 256) || BM < 32) ? 2 : 4;
   static_assert(NCOL % 128 == 0 && NCOL <= 512 && WTN % 16 == 0, "NCOL");
   static_assert(32 * LDS_ST * 4 <= kRowStages * STAGE * 2, "band stage fits the ring");
   typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -1292,12 +1297,12 @@ __global__ __launch_bounds__(kRowThreads, BM <= 64 ? 4 : 1) void gemm_rowln_kern
   // gate rows are loaded one unit AHEAD of use (unit 0 before the main loop, so its HBM
   // latency hides under the K loop; unit u+1 while unit u computes), so the epilogue pays the
   // residual-read latency once instead of once per band.
-  constexpr int UPB = 4 / RG, NU = (BM / 32) * UPB;
+  constexpr int UPB = RPW / RG, NU = (BM / BH) * UPB;
   const float inv_rpm = 1.0f / (float)p.rows_per_mod;
   // the gate row is per trajectory: one row of it per unit (the unit's first row's entry; a
   // row of another entry, in a unit straddling a trajectory boundary, reloads its own)
   auto load_unit = [&](int u, float2 (&hv)[RG][NE], float2 (&gv)[NE]) {
-    const int mu = min(m0 + (u / UPB) * 32 + wave * 4 + (u % UPB) * RG, M - 1);
+    const int mu = min(m0 + (u / UPB) * BH + wave * RPW + (u % UPB) * RG, M - 1);
     const float* gr = p.gate ? p.gate + (size_t)fdiv(mu, p.rows_per_mod, inv_rpm) * p.mod_stride + p.gate_off : nullptr;
 #pragma unroll
     for (int e = 0; e < NE; ++e)
@@ -1339,7 +1344,7 @@ __global__ __launch_bounds__(kRowThreads, BM <= 64 ? 4 : 1) void gemm_rowln_kern
   // step): the pieces go global -> VGPRs -> ds_write_b128 into the same LDS image, the next
   // step's loaded under this step's MFMAs (plain loads fill ~3x faster than LDS-DMA per CU,
   // tools/ubench/l2lds.hip)
-  constexpr bool VST = BM == 32;
+  constexpr bool VST = BM <= 32;
   u32x4 vr[1 + WLD];
   auto vload = [&](int k0) {
     if (has_a) vr[0] = *reinterpret_cast<const u32x4*>(asrc + k0);
@@ -1440,7 +1445,7 @@ __global__ __launch_bounds__(kRowThreads, BM <= 64 ? 4 : 1) void gemm_rowln_kern
   if (BM == 128) load_unit(0, hv, gv);  // the rare tile over > 2 entries: no prefetch under the K loop
   __syncthreads();  // all waves are done with the ring
 #pragma unroll 1
-  for (int band = 0; band < BM / 32; ++band) {
+  for (int band = 0; band < BM / BH; ++band) {
     if (wm == (band >> 1)) {
 #pragma unroll
       for (int i = 0; i < MI; ++i) {  // compile-time acc index; the band selects 2 of the 4
@@ -1457,11 +1462,11 @@ __global__ __launch_bounds__(kRowThreads, BM <= 64 ? 4 : 1) void gemm_rowln_kern
     // gathered before use and the 4 rows' reductions run interleaved (independent chains)
     // rows of this wave in groups of RG (fewer live registers at BM 64, two blocks per CU)
 #pragma unroll 1
-    for (int g0 = 0; g0 < 4; g0 += RG) {
+    for (int g0 = 0; g0 < RPW; g0 += RG) {
       const int u = band * UPB + g0 / RG;
       float2 hn[RG][NE], gn[NE];
       if (u + 1 < NU) load_unit(u + 1, hn, gn);
-      const int mb0 = min(m0 + band * 32 + wave * 4 + g0, M - 1), mb3 = min(mb0 + RG - 1, M - 1);
+      const int mb0 = min(m0 + band * BH + wave * RPW + g0, M - 1), mb3 = min(mb0 + RG - 1, M - 1);
       const int b0 = fdiv(mb0, p.rows_per_mod, inv_rpm);
       const bool one_b = fdiv(mb3, p.rows_per_mod, inv_rpm) == b0;  // the 4 rows share a batch entry
       float2 xs[NE], xh[NE];
@@ -1477,12 +1482,12 @@ __global__ __launch_bounds__(kRowThreads, BM <= 64 ? 4 : 1) void gemm_rowln_kern
       float sum[RG];
   #pragma unroll
       for (int rr = 0; rr < RG; ++rr) {
-        const float* srow = stage + (wave * 4 + g0 + rr) * LDS_ST;
+        const float* srow = stage + (wave * RPW + g0 + rr) * LDS_ST;
         float2 g2[NE];
   #pragma unroll
         for (int e = 0; e < NE; ++e) g2[e] = gv[e];
         if (!one_b && p.gate) {  // rare: this row belongs to the next trajectory
-          const int br = fdiv(min(m0 + band * 32 + wave * 4 + g0 + rr, M - 1), p.rows_per_mod, inv_rpm);
+          const int br = fdiv(min(m0 + band * BH + wave * RPW + g0 + rr, M - 1), p.rows_per_mod, inv_rpm);
           if (br != b0) {
             const float* gr = p.gate + (size_t)br * p.mod_stride + p.gate_off;
   #pragma unroll
@@ -1498,7 +1503,7 @@ __global__ __launch_bounds__(kRowThreads, BM <= 64 ? 4 : 1) void gemm_rowln_kern
           s += hv[rr][e].x + hv[rr][e].y;
         }
         sum[rr] = s;
-        const int m = m0 + band * 32 + wave * 4 + g0 + rr;
+        const int m = m0 + band * BH + wave * RPW + g0 + rr;
         if (m < M) {
   #pragma unroll
           for (int e = 0; e < NE; ++e) *reinterpret_cast<float2*>(p.resid + (size_t)m * p.ldr + 2 * lane + 128 * e) = hv[rr][e];
@@ -1527,7 +1532,7 @@ __global__ __launch_bounds__(kRowThreads, BM <= 64 ? 4 : 1) void gemm_rowln_kern
           for (int rr = 0; rr < RG; ++rr) ss[rr] += __shfl_xor(ss[rr], o, 64);
   #pragma unroll
         for (int rr = 0; rr < RG; ++rr) {
-          const int m = m0 + band * 32 + wave * 4 + g0 + rr;
+          const int m = m0 + band * BH + wave * RPW + g0 + rr;
           if (m >= M) continue;
           const float rs = 1.0f / sqrtf(ss[rr] * invN + p.ln_eps);
           if (!one_b) {  // rows straddle a batch boundary: this row's own shift / scale
@@ -1584,7 +1589,18 @@ bool rowln_bm32_supported(const mdg_gemm_desc& r) {
          (!r.xn_out || r.xn_mods);
 }
 
-hipError_t rowln_bm32_launch(const mdg_gemm_desc& p, hipStream_t s) { return launch_rowln<384, 32>(p, s); }
+// MDG_ROWLN_BM: the small-M row-LN tile height (16 default: 250 tiles at B = 1, 1.846 / 1.823 vs
+// 1.813 / 1.816 M frames/s with 32, same box; 32 restores the 125-tile form)
+static int rowln_small_bm() {
+  static const int v = [] {
+    const char* e = getenv("MDG_ROWLN_BM");
+    return (e && atoi(e) == 32) ? 32 : 16;
+  }();
+  return v;
+}
+hipError_t rowln_bm32_launch(const mdg_gemm_desc& p, hipStream_t s) {
+  return rowln_small_bm() == 16 ? launch_rowln<384, 16>(p, s) : launch_rowln<384, 32>(p, s);
+}
 
 static hipError_t launch_rowln_train(const mdg_gemm_desc& p, hipStream_t s) {
   static bool attr_set = false;
