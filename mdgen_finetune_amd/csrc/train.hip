@@ -1587,7 +1587,8 @@ __global__ __launch_bounds__(256) void attn_spatial_bwd_quad_kernel(const CT* __
 static int spq_blocks() {  // MDG_SPQ_BLOCKS: the grid-stride loop's block count (tuning)
   static const int v = [] {
     const char* e = getenv("MDG_SPQ_BLOCKS");
-    return e ? atoi(e) : 256;  // one per CU: 11.61 ms step vs 11.66 (512), 11.9 (1024), 12.4 (2048+)
+    const int n = e ? atoi(e) : 256;  // one per CU: 11.61 ms step vs 11.66 (512), 11.9 (1024), 12.4 (2048+)
+    return n > 0 ? n : 256;
   }();
   return v;
 }
