@@ -66,6 +66,9 @@ def parse():
                     help="dopri5: an evidence line for the reference's DEFAULT sampler (parsing.py:102): one "
                          "window = Sampler.sample_ode() (adaptive dopri5, atol 1e-6 / rtol 1e-3, 50 saved points) "
                          "with every adaptive step one hipGraph replay; reports NFE and accepted / rejected steps")
+    ap.add_argument("--model-args", default="",
+                    help="--train only: extra model flags, e.g. '--embed_dim 256 --mha_heads 8' (head_dim 32); "
+                         "the line then carries no step roofline (its FLOP model is the default model's)")
     ap.add_argument("--train", action="store_true",
                     help="BASELINE config 3 evidence line: the GVP training step (forward + loss + backward + "
                          "clip + Adam + EMA, the HIP block stack, graphed) at B trajectories x T frames per GPU "
@@ -489,7 +492,7 @@ def train_main(a, world, rank, dev, share):
     B, T, L = a.batch, a.frames, a.crop
     args = parse_train_args(["--synthetic", "--sim_condition", "--prepend_ipa", "--abs_pos_emb", "--num_frames",
                              str(T), "--crop", str(L), "--batch_size", str(B), "--synthetic_size", str(B * world),
-                             "--hip_dtype", a.dtype, "--seed", "137"])
+                             "--hip_dtype", a.dtype, "--seed", "137"] + a.model_args.split())
     torch.set_float32_matmul_precision("medium")  # train.py:13
     rehearse = a.train_rccl1 and world == 1
     if rehearse:  # a world-1 RCCL group with the reduction forced on: the in-graph bucket all-reduces run
@@ -529,7 +532,8 @@ def train_main(a, world, rank, dev, share):
            "data": "synthetic (seeded weights and tetrapeptide trajectories; no dataset offline)",
            "config": {"workload": f"training step: prep_batch + GVP loss + backward + grad clip + Adam + EMA, "
                                   f"B={B} trajectories x T={T} frames x L={L} per GPU",
-                      "model": "LatentMDGenModel default (5 layers, C=384, 16 heads, IPA prepend, abs pos emb)",
+                      "model": ("LatentMDGenModel default (5 layers, C=384, 16 heads, IPA prepend, abs pos emb)"
+                                if not a.model_args else f"LatentMDGenModel {a.model_args} (IPA prepend, abs pos emb)"),
                       "global_batch": B * world, "seq_len": T, "crop": L,
                       "parallelism": f"dp{world}" + (
                           (" (per-bucket RCCL all-reduces captured in the step's graph, overlapped with backward)"
@@ -543,6 +547,8 @@ def train_main(a, world, rank, dev, share):
                              "mfma_frac": round(tf / PEAK_TFLOPS[a.dtype], 4)},
            "loss": float(loss), "max_mem_gb": round(torch.cuda.max_memory_allocated() / 2 ** 30, 2),
            "cpu_baseline": cpu}
+    if a.model_args:  # (step_model prices the default model only)
+        out["step_roofline"] = None
     if share:
         out["shared_gpu"] = True
         out["ranks_sharing_gpu"] = world

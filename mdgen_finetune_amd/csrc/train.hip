@@ -604,6 +604,211 @@ __global__ __launch_bounds__(256) void attn_bwd_dkdv_generic_kernel(
   }
 }
 
+// Wide heads (head_dim 32..63, 64-column planes): the scalar passes above, restructured so a wave
+// issues few memory instructions per score.  A block = 512 threads = 256 queries (dQ pass) or 256
+// keys (dK / dV pass) x 2 column halves: thread t owns row t >> 1 and columns 32 (t & 1) .. + 31, so
+// its operand rows and accumulators are 32 floats each (the one-thread-per-row form held 4 x 64 and
+// spilled); the two halves' partial dot products meet by one lane swap.  The other side's rows
+// stream through LDS in chunks of 32 (converted to fp32 once, read back as wave-broadcast float4).
+// Same arithmetic as the scalar kernels (fp32, exp2 of log2-unit scores); bias partials per block
+// of 256 queries (the slot count of generic = 1).
+constexpr int kWideRows = 256, kWideChunk = 32, kWideThreads = 2 * kWideRows;
+
+template <typename CT>
+__device__ __forceinline__ void wide_stage_rows(float* dst, const CT* src, int r0, int T, int tid) {
+  // rows r0 .. r0 + 31 of a [T][64] plane -> dst [32][64] fp32 (rows past T: 0)
+  constexpr int DP = MDG_DP_WIDE;
+  for (int e = tid; e < kWideChunk * DP / 4; e += kWideThreads) {
+    const int r = e / (DP / 4), c = 4 * (e % (DP / 4));
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (r0 + r < T) v = ld4f<CT>(src + (size_t)(r0 + r) * DP + c);
+    *reinterpret_cast<float4*>(dst + r * DP + c) = v;
+  }
+}
+
+template <typename CT>
+__global__ __launch_bounds__(kWideThreads) void attn_bwd_dq_wide_kernel(
+    const CT* __restrict__ qkv, const CT* __restrict__ dop, const float* __restrict__ lse,
+    const float* __restrict__ delta, const float* __restrict__ kbias, const float* __restrict__ kvb,
+    const float* __restrict__ rope, int rope_rows, CT* __restrict__ dqkv, int ldq, float* __restrict__ bpart, int T,
+    int L, int H, int D, int BL, float qscale, float kscale) {
+  constexpr int DP = MDG_DP_WIDE, HW = 32;
+  __shared__ __attribute__((aligned(16))) float Ks[kWideChunk * DP], Vs[kWideChunk * DP];
+  __shared__ float kbs[kWideChunk];
+  __shared__ float red[kWideRows][2 * DP + 1];
+  const int tid = threadIdx.x, half = tid & 1, c0 = HW * half;
+  const int sh = blockIdx.y, seq = sh / H, head = sh % H;
+  const int q = blockIdx.x * kWideRows + (tid >> 1);
+  const bool live = q < T;
+  const size_t plane = (size_t)BL * H * T * DP;
+  const CT* Qg = qkv + (size_t)sh * T * DP;
+  const CT* Kg = Qg + plane;
+  const CT* Vg = Qg + 2 * plane;
+  const CT* dOg = dop + (size_t)sh * T * DP;
+  const int qq = live ? q : 0;
+  float qv[HW], dov[HW], dq[HW];
+#pragma unroll
+  for (int j = 0; j < HW; j += 4) {
+    const float4 a = ld4f<CT>(Qg + (size_t)qq * DP + c0 + j), b = ld4f<CT>(dOg + (size_t)qq * DP + c0 + j);
+    const bool in = live && c0 + j < D;  // (D % 4 == 0)
+    qv[j] = in ? a.x : 0.f; qv[j + 1] = in ? a.y : 0.f; qv[j + 2] = in ? a.z : 0.f; qv[j + 3] = in ? a.w : 0.f;
+    dov[j] = in ? b.x : 0.f; dov[j + 1] = in ? b.y : 0.f; dov[j + 2] = in ? b.z : 0.f; dov[j + 3] = in ? b.w : 0.f;
+  }
+  const float l2 = live ? lse[(size_t)sh * T + q] : INFINITY;
+  const float dl = live ? delta[(size_t)sh * T + q] : 0.f;
+  const float* bk = kvb + head * 2 * DP + c0;
+  const float* bv = bk + DP;
+  float sb = 0.f, dpb = 0.f;
+#pragma unroll
+  for (int j = 0; j < HW; ++j) {
+    sb += qv[j] * bk[j];
+    dpb += dov[j] * bv[j];
+  }
+  sb += __shfl_xor(sb, 1, 64);
+  dpb += __shfl_xor(dpb, 1, 64);
+  const float pb = live ? exp2f(sb - l2) : 0.f;
+  float dsb = pb * (dpb - dl);
+#pragma unroll
+  for (int j = 0; j < HW; ++j) dq[j] = 0.f;
+  bool anyk = false;
+  for (int k0 = 0; k0 < T; k0 += kWideChunk) {
+    __syncthreads();  // the previous chunk's reads are done
+    wide_stage_rows<CT>(Ks, Kg, k0, T, tid);
+    wide_stage_rows<CT>(Vs, Vg, k0, T, tid);
+    if (tid < kWideChunk) kbs[tid] = k0 + tid < T ? kbias[(size_t)seq * T + k0 + tid] : -INFINITY;
+    __syncthreads();
+    for (int kk = 0; kk < kWideChunk; ++kk) {
+      const float kb = kbs[kk];
+      if (kb == -INFINITY) continue;  // (block-uniform)
+      anyk = true;
+      const float* kr = Ks + kk * DP + c0;
+      const float* vr = Vs + kk * DP + c0;
+      float sp = 0.f, dpp = 0.f;
+#pragma unroll
+      for (int j = 0; j < HW; j += 4) {
+        const float4 kv4 = *reinterpret_cast<const float4*>(kr + j), vv4 = *reinterpret_cast<const float4*>(vr + j);
+        sp += qv[j] * kv4.x + qv[j + 1] * kv4.y + qv[j + 2] * kv4.z + qv[j + 3] * kv4.w;
+        dpp += dov[j] * vv4.x + dov[j + 1] * vv4.y + dov[j + 2] * vv4.z + dov[j + 3] * vv4.w;
+      }
+      const float sfull = kb + sp + __shfl_xor(sp, 1, 64), dpf = dpp + __shfl_xor(dpp, 1, 64);
+      const float ds = live ? exp2f(sfull - l2) * (dpf - dl) : 0.f;
+#pragma unroll
+      for (int j = 0; j < HW; j += 4) {
+        const float4 kv4 = *reinterpret_cast<const float4*>(kr + j);
+        dq[j] += ds * kv4.x; dq[j + 1] += ds * kv4.y; dq[j + 2] += ds * kv4.z; dq[j + 3] += ds * kv4.w;
+      }
+    }
+  }
+  if (!anyk) dsb = 0.f;  // every key padded: P = [1, 0, ...], dS = 0 exactly (as the scalar kernel)
+  if (live) {
+    const int b = seq / L, l = seq % L, hd = D >> 1;
+    const size_t tok = ((size_t)b * T + q) * L + l;
+    CT* out = dqkv + tok * ldq + head * D;
+    for (int j = 0; j < HW; j += 2) {
+      const int d = c0 + j;
+      if (d >= D) break;
+      float a = (dq[j] + dsb * bk[j]) * qscale, c = (dq[j + 1] + dsb * bk[j + 1]) * qscale;
+      if (rope) rope_inv(a, c, rope, rope_rows, hd, q, d >> 1);
+      out[d] = (CT)a;
+      out[d + 1] = (CT)c;
+    }
+  }
+  const int row = tid >> 1;
+#pragma unroll
+  for (int j = 0; j < HW; ++j) {
+    const bool in = c0 + j < D;
+    red[row][c0 + j] = in ? dsb * qv[j] * kscale : 0.f;
+    red[row][DP + c0 + j] = in ? pb * dov[j] : 0.f;
+  }
+  __syncthreads();
+  if (tid < 2 * DP) {
+    double sacc = 0.0;  // (fp64, as the scalar kernel)
+    for (int i = 0; i < kWideRows; ++i) sacc += red[i][tid];
+    const size_t slot = (size_t)seq * gridDim.x + blockIdx.x;
+    bpart[((size_t)head * BL * gridDim.x + slot) * 2 * DP + tid] = (float)sacc;
+  }
+}
+
+template <typename CT>
+__global__ __launch_bounds__(kWideThreads) void attn_bwd_dkdv_wide_kernel(
+    const CT* __restrict__ qkv, const CT* __restrict__ dop, const float* __restrict__ lse,
+    const float* __restrict__ delta, const float* __restrict__ kbias, const float* __restrict__ rope, int rope_rows,
+    CT* __restrict__ dqkv, int ldq, int T, int L, int H, int D, int BL, float kscale) {
+  constexpr int DP = MDG_DP_WIDE, HW = 32;
+  __shared__ __attribute__((aligned(16))) float Qs[kWideChunk * DP], Ds[kWideChunk * DP];
+  __shared__ float ls[kWideChunk], dls[kWideChunk];
+  const int tid = threadIdx.x, half = tid & 1, c0 = HW * half;
+  const int sh = blockIdx.y, seq = sh / H, head = sh % H;
+  const int k = blockIdx.x * kWideRows + (tid >> 1);
+  const bool live = k < T;
+  const size_t plane = (size_t)BL * H * T * DP;
+  const CT* Qg = qkv + (size_t)sh * T * DP;
+  const CT* Kg = Qg + plane;
+  const CT* Vg = Qg + 2 * plane;
+  const CT* dOg = dop + (size_t)sh * T * DP;
+  const int kk = live ? k : 0;
+  const float kb = live ? kbias[(size_t)seq * T + k] : -INFINITY;
+  float kv[HW], vv[HW], dk[HW], dv[HW];
+#pragma unroll
+  for (int j = 0; j < HW; j += 4) {
+    const float4 a = ld4f<CT>(Kg + (size_t)kk * DP + c0 + j), b = ld4f<CT>(Vg + (size_t)kk * DP + c0 + j);
+    const bool in = c0 + j < D;
+    kv[j] = in ? a.x : 0.f; kv[j + 1] = in ? a.y : 0.f; kv[j + 2] = in ? a.z : 0.f; kv[j + 3] = in ? a.w : 0.f;
+    vv[j] = in ? b.x : 0.f; vv[j + 1] = in ? b.y : 0.f; vv[j + 2] = in ? b.z : 0.f; vv[j + 3] = in ? b.w : 0.f;
+  }
+#pragma unroll
+  for (int j = 0; j < HW; ++j) dk[j] = dv[j] = 0.f;
+  const bool act = kb != -INFINITY;  // (both halves of a key agree)
+  for (int q0 = 0; q0 < T; q0 += kWideChunk) {
+    __syncthreads();
+    wide_stage_rows<CT>(Qs, Qg, q0, T, tid);
+    wide_stage_rows<CT>(Ds, dOg, q0, T, tid);
+    if (tid < kWideChunk) {
+      const bool in = q0 + tid < T;
+      ls[tid] = in ? lse[(size_t)sh * T + q0 + tid] : INFINITY;
+      dls[tid] = in ? delta[(size_t)sh * T + q0 + tid] : 0.f;
+    }
+    __syncthreads();
+    if (!act) continue;
+    const int nq = min(kWideChunk, T - q0);
+    for (int qi = 0; qi < nq; ++qi) {
+      const float* qr = Qs + qi * DP + c0;
+      const float* dr = Ds + qi * DP + c0;
+      float sp = 0.f, dpp = 0.f;
+#pragma unroll
+      for (int j = 0; j < HW; j += 4) {
+        const float4 q4 = *reinterpret_cast<const float4*>(qr + j), d4 = *reinterpret_cast<const float4*>(dr + j);
+        sp += q4.x * kv[j] + q4.y * kv[j + 1] + q4.z * kv[j + 2] + q4.w * kv[j + 3];
+        dpp += d4.x * vv[j] + d4.y * vv[j + 1] + d4.z * vv[j + 2] + d4.w * vv[j + 3];
+      }
+      const float sfull = kb + sp + __shfl_xor(sp, 1, 64), dpf = dpp + __shfl_xor(dpp, 1, 64);
+      const float p = exp2f(sfull - ls[qi]);
+      const float ds = p * (dpf - dls[qi]);
+#pragma unroll
+      for (int j = 0; j < HW; j += 4) {
+        const float4 q4 = *reinterpret_cast<const float4*>(qr + j), d4 = *reinterpret_cast<const float4*>(dr + j);
+        dk[j] += ds * q4.x; dk[j + 1] += ds * q4.y; dk[j + 2] += ds * q4.z; dk[j + 3] += ds * q4.w;
+        dv[j] += p * d4.x; dv[j + 1] += p * d4.y; dv[j + 2] += p * d4.z; dv[j + 3] += p * d4.w;
+      }
+    }
+  }
+  if (!live) return;  // (no barrier below)
+  const int b = seq / L, l = seq % L, hd = D >> 1, C = H * D;
+  const size_t tok = ((size_t)b * T + k) * L + l;
+  CT* ok = dqkv + tok * ldq + C + head * D;
+  CT* ov = dqkv + tok * ldq + 2 * C + head * D;
+  for (int j = 0; j < HW; j += 2) {
+    const int d = c0 + j;
+    if (d >= D) break;
+    float a = dk[j] * kscale, c = dk[j + 1] * kscale;
+    if (rope) rope_inv(a, c, rope, rope_rows, hd, k, d >> 1);
+    ok[d] = (CT)a;
+    ok[d + 1] = (CT)c;
+    ov[d] = (CT)dv[j];
+    ov[d + 1] = (CT)dv[j + 1];
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // bf16 MFMA kernels.  LDS images are [row][32] bf16 (64-B rows) with 16-B chunk c of row r at
 // chunk c ^ ((r >> 3) & 3) (the forward's K image): row reads (ds_read_b128, MFMA A operand
@@ -1286,6 +1491,14 @@ static bool attn_bwd_fold_on() {
   return on;
 }
 
+static bool attn_bwd_wide2_on() {  // MDG_ATTN_BWD_WIDE2=0: the one-thread-per-row scalar kernels at DP 64
+  static const bool v = [] {
+    const char* e = getenv("MDG_ATTN_BWD_WIDE2");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
 int attn_bwd_parts(int dtype, int B, int T, int L, int generic) {  // bias-gradient partial slots per head
   if (dtype == MDG_BF16 && generic == 1) return B * L * ((T + 255) / 256);
   if (dtype == MDG_BF16 && generic == 0) return B * L;  // the fused kernel: one per sequence
@@ -1315,7 +1528,20 @@ hipError_t attn_temporal_bwd_launch(int dtype, int B, int T, int L, int H, int D
   // the scalar kernels: f32, generic == 1, and every wide head (head_dim 32..63, 64-column planes;
   // the MFMA kernels' LDS images are 32 columns wide)
   if (dtype == MDG_F32 || generic == 1 || D >= kDP) {
-    if (D >= kDP) {
+    if (D >= kDP && attn_bwd_wide2_on()) {  // the two-column-half kernels
+      dim3 wgrid((T + kWideRows - 1) / kWideRows, BL * H);
+#define MDG_WIDE(CTT)                                                                                                \
+  hipLaunchKernelGGL((attn_bwd_prep_kernel<CTT, MDG_DP_WIDE>), pgrid, dim3(256), 0, s, B, T, L, H, D, (const CTT*)o, \
+                     (const CTT*)o_lo, (const CTT*)dout, (CTT*)dop, delta);                                          \
+  if (hipError_t e = hipGetLastError()) return e;                                                                   \
+  hipLaunchKernelGGL(attn_bwd_dq_wide_kernel<CTT>, wgrid, dim3(kWideThreads), 0, s, (const CTT*)qkv_t,              \
+                     (const CTT*)dop, lse, delta, kbias, kvb, rope, rope_rows, (CTT*)dqkv, ldq, bpart, T, L, H, D, BL, \
+                     qscale, kscale);                                                                               \
+  hipLaunchKernelGGL(attn_bwd_dkdv_wide_kernel<CTT>, wgrid, dim3(kWideThreads), 0, s, (const CTT*)qkv_t,            \
+                     (const CTT*)dop, lse, delta, kbias, rope, rope_rows, (CTT*)dqkv, ldq, T, L, H, D, BL, kscale)
+      if (dtype == MDG_BF16) { MDG_WIDE(bf16_t); } else { MDG_WIDE(float); }
+#undef MDG_WIDE
+    } else if (D >= kDP) {
       if (dtype == MDG_BF16) { MDG_GEN(bf16_t, MDG_DP_WIDE); } else { MDG_GEN(float, MDG_DP_WIDE); }
     } else {
       if (dtype == MDG_BF16) { MDG_GEN(bf16_t, kDP); } else { MDG_GEN(float, kDP); }
