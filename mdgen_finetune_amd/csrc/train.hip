@@ -1866,29 +1866,35 @@ __global__ __launch_bounds__(256) void attn_spatial_bwd_quadh_kernel(const CT* _
 }
 
 // Any L (< the MFMA route's 16), any D <= 63: one thread per (frame, head).  DP = the bias
-// rows' stride (MDG_HEAD_STRIDE(D)).
-template <typename CT, int DP>
+// rows' stride (MDG_HEAD_STRIDE(D)); LM = the largest L of the instantiation (4: the P / dS
+// tables stay in registers; 16: they spill to scratch).
+template <typename CT, int DP, int LM = 16>
 __global__ __launch_bounds__(128) void attn_spatial_bwd_generic_kernel(
     const CT* __restrict__ qkv, const float* __restrict__ kvb, const float* __restrict__ mask,
     const CT* __restrict__ dout, const float* __restrict__ rope, int rope_rows, CT* __restrict__ dqkv,
     float* __restrict__ bpart, int nf, int L, int H, int D, float qscale) {
-  constexpr int LM = 16;
+  constexpr int UNR = LM <= 4 ? LM : 1;  // (the LM = 16 form keeps its loops rolled)
   __shared__ float red[128][2 * DP + 1];
-  const int head = blockIdx.y;
-  const int f = blockIdx.x * 128 + threadIdx.x;
+  // thread = (frame, head) with the head fastest (the forward's order: a wave reads several
+  // heads' adjacent row pieces of a frame instead of one piece per frame 6 KB apart)
+  const int idx = blockIdx.x * 128 + threadIdx.x, head = idx % H, f = idx / H;
   const bool live = f < nf;
   const int C = H * D;
   const float* bk = kvb + head * 2 * DP;
   const float* bv = bk + DP;
   float P[LM][LM + 1], DS[LM][LM + 1];
-  float gbk[DP], gbv[DP];
-#pragma unroll
-  for (int d = 0; d < DP; ++d) gbk[d] = gbv[d] = 0.f;
+  // the thread's bias_k / bias_v partials accumulate in its own LDS row (register arrays indexed
+  // by the runtime head dim went to scratch)
+  float* gbk = red[threadIdx.x];
+  float* gbv = red[threadIdx.x] + DP;
+  for (int d = 0; d < 2 * DP; ++d) gbk[d] = 0.f;
   if (live) {
     auto at = [&](int tk, int which, int d) -> float {
       return (float)qkv[((size_t)(f * L + tk) * 3 + which) * C + head * D + d];
     };
-    for (int jq = 0; jq < L; ++jq) {
+#pragma unroll UNR
+    for (int jq = 0; jq < LM; ++jq) {
+      if (jq >= L) break;
       const CT* gq = dout + (size_t)(f * L + jq) * C + head * D;
       float sb = 0.f, dpb = 0.f;
       for (int d = 0; d < D; ++d) {
@@ -1896,7 +1902,9 @@ __global__ __launch_bounds__(128) void attn_spatial_bwd_generic_kernel(
         dpb += (float)gq[d] * bv[d];
       }
       float s[LM], dp[LM], m = sb;
-      for (int i = 0; i < L; ++i) {
+#pragma unroll UNR
+      for (int i = 0; i < LM; ++i) {
+        if (i >= L) break;
         float a = 0.f, b = 0.f;
         for (int d = 0; d < D; ++d) {
           a += at(jq, 0, d) * at(i, 1, d);
@@ -1907,18 +1915,24 @@ __global__ __launch_bounds__(128) void attn_spatial_bwd_generic_kernel(
         if (!mask || mask[f * L + i] != 0.f) m = fmaxf(m, a);
       }
       float pb = expf(sb - m), lsum = pb;
-      for (int i = 0; i < L; ++i) {
+#pragma unroll UNR
+      for (int i = 0; i < LM; ++i) {
+        if (i >= L) break;
         P[jq][i] = (!mask || mask[f * L + i] != 0.f) ? expf(s[i] - m) : 0.f;
         lsum += P[jq][i];
       }
       pb /= lsum;
       float dl = pb * dpb;
-      for (int i = 0; i < L; ++i) {
+#pragma unroll UNR
+      for (int i = 0; i < LM; ++i) {
+        if (i >= L) break;
         P[jq][i] /= lsum;
         dl += P[jq][i] * dp[i];
       }
       const float dsb = pb * (dpb - dl);
-      for (int i = 0; i < L; ++i) DS[jq][i] = P[jq][i] * (dp[i] - dl);
+#pragma unroll UNR
+      for (int i = 0; i < LM; ++i)
+        if (i < L) DS[jq][i] = P[jq][i] * (dp[i] - dl);
       for (int d = 0; d < D; ++d) {
         gbk[d] += dsb * at(jq, 0, d);
         gbv[d] += pb * (float)gq[d];
@@ -1926,7 +1940,9 @@ __global__ __launch_bounds__(128) void attn_spatial_bwd_generic_kernel(
       CT* oq = dqkv + (size_t)(f * L + jq) * 3 * C + head * D;
       for (int d = 0; d < D; d += 2) {
         float a = dsb * bk[d], b = dsb * bk[d + 1];
-        for (int i = 0; i < L; ++i) {
+#pragma unroll UNR
+        for (int i = 0; i < LM; ++i) {
+          if (i >= L) break;
           a += DS[jq][i] * at(i, 1, d);
           b += DS[jq][i] * at(i, 1, d + 1);
         }
@@ -1937,11 +1953,15 @@ __global__ __launch_bounds__(128) void attn_spatial_bwd_generic_kernel(
         oq[d + 1] = (CT)b;
       }
     }
-    for (int i = 0; i < L; ++i) {
+#pragma unroll UNR
+    for (int i = 0; i < LM; ++i) {
+      if (i >= L) break;
       CT* ok = dqkv + (size_t)(f * L + i) * 3 * C + C + head * D;
       for (int d = 0; d < D; d += 2) {
         float a = 0.f, b = 0.f, c = 0.f, e = 0.f;
-        for (int jq = 0; jq < L; ++jq) {
+#pragma unroll UNR
+        for (int jq = 0; jq < LM; ++jq) {
+          if (jq >= L) break;
           const CT* gq = dout + (size_t)(f * L + jq) * C + head * D;
           a += DS[jq][i] * at(jq, 0, d);
           b += DS[jq][i] * at(jq, 0, d + 1);
@@ -1956,16 +1976,15 @@ __global__ __launch_bounds__(128) void attn_spatial_bwd_generic_kernel(
       }
     }
   }
-#pragma unroll
-  for (int d = 0; d < DP; ++d) {
-    red[threadIdx.x][d] = gbk[d];
-    red[threadIdx.x][DP + d] = gbv[d];
-  }
   __syncthreads();
-  if (threadIdx.x < 2 * DP) {
-    double s = 0.0;  // (fp64: as attn_bwd_dq_generic_kernel)
-    for (int i = 0; i < 128; ++i) s += red[i][threadIdx.x];
-    bpart[((size_t)head * gridDim.x + blockIdx.x) * 2 * DP + threadIdx.x] = s;
+  // the block's rows of head h are r = r0, r0 + H, ... (r0 = (h - first index) mod H): one slot
+  // per (head, block), fp64 sums in row order
+  const int base = blockIdx.x * 128;
+  for (int e = threadIdx.x; e < H * 2 * DP; e += 128) {
+    const int h = e / (2 * DP), c = e % (2 * DP);
+    double sacc = 0.0;
+    for (int r = ((h - base) % H + H) % H; r < 128; r += H) sacc += red[r][c];
+    bpart[((size_t)h * gridDim.x + blockIdx.x) * 2 * DP + c] = (float)sacc;
   }
 }
 
@@ -1983,7 +2002,7 @@ int attn_spatial_bwd_parts(int nf, int L, int H, int D) {
     return (int)(blocks < spq_blocks() ? blocks : spq_blocks());
   }
   if (L == 4 && D % 8 == 0 && D < kDP) return (nf * 4 + 255) / 256;
-  return (nf + 127) / 128;
+  return (int)(((long long)nf * H + 127) / 128);
 }
 
 hipError_t attn_spatial_bwd_launch(int dtype, int nf, int L, int H, int D, const void* qkv, const float* kvb,
@@ -2015,14 +2034,18 @@ hipError_t attn_spatial_bwd_launch(int dtype, int nf, int L, int H, int D, const
 #undef MDG_SQ
     return hipGetLastError();
   }
-  dim3 grid((unsigned)((nf + 127) / 128), H);
+  dim3 grid((unsigned)attn_spatial_bwd_parts(nf, L, H, D));
 #define MDG_SG(CTT, DPP)                                                                                          \
-  hipLaunchKernelGGL((attn_spatial_bwd_generic_kernel<CTT, DPP>), grid, dim3(128), 0, s, (const CTT*)qkv, kvb,    \
-                     mask, (const CTT*)dout, rope, rope_rows, (CTT*)dqkv, bpart, nf, L, H, D, qscale)
+  if (L <= 4)                                                                                                     \
+    hipLaunchKernelGGL((attn_spatial_bwd_generic_kernel<CTT, DPP, 4>), grid, dim3(128), 0, s, (const CTT*)qkv,    \
+                       kvb, mask, (const CTT*)dout, rope, rope_rows, (CTT*)dqkv, bpart, nf, L, H, D, qscale);     \
+  else                                                                                                            \
+    hipLaunchKernelGGL((attn_spatial_bwd_generic_kernel<CTT, DPP, 16>), grid, dim3(128), 0, s, (const CTT*)qkv,   \
+                       kvb, mask, (const CTT*)dout, rope, rope_rows, (CTT*)dqkv, bpart, nf, L, H, D, qscale)
   if (dtype == MDG_BF16) {
-    if (D < kDP) MDG_SG(bf16_t, kDP); else MDG_SG(bf16_t, MDG_DP_WIDE);
+    if (D < kDP) { MDG_SG(bf16_t, kDP); } else { MDG_SG(bf16_t, MDG_DP_WIDE); }
   } else {
-    if (D < kDP) MDG_SG(float, kDP); else MDG_SG(float, MDG_DP_WIDE);
+    if (D < kDP) { MDG_SG(float, kDP); } else { MDG_SG(float, MDG_DP_WIDE); }
   }
 #undef MDG_SG
   return hipGetLastError();
