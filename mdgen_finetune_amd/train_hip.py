@@ -223,6 +223,28 @@ def hip_layer_forward_chain(hl, layer, h, mods, mask, next_mods=None, pre=None):
     return out[0], (out[1], out[2])
 
 
+class _Mods9(torch.autograd.Function):
+    """[B, 6C] adaLN rows -> [B, 9C] with three zero chunks in the temporal slots (one
+    concatenation against a cached zero block forward, one concatenation of the two kept slices
+    backward: autograd's cat / new_zeros pair took a fill + a copy each way and a fill, two copies
+    and an add back, per IPA layer and step)."""
+    _zeros = {}
+
+    @staticmethod
+    def forward(ctx, mods6, C):
+        key = (mods6.shape[0], C, mods6.dtype, mods6.device)
+        z = _Mods9._zeros.get(key)
+        if z is None:
+            z = _Mods9._zeros[key] = torch.zeros(mods6.shape[0], 3 * C, dtype=mods6.dtype, device=mods6.device)
+        ctx.C = C
+        return torch.cat([mods6[:, :3 * C], z, mods6[:, 3 * C:]], -1)
+
+    @staticmethod
+    def backward(ctx, g):
+        C = ctx.C
+        return torch.cat([g[:, :3 * C], g[:, 6 * C:]], -1), None
+
+
 def hip_ipa_layer_tail(hl, layer, x1, mods6, mask_b):
     """IPALayer (latent_model.py:341-394) after its IPA sublayer: x1 + g_l MHA_L(mod(LN x1)),
     then + g_m MLP(mod(LN .)), on the HIP training Function as a T = 1 block whose temporal
@@ -233,7 +255,7 @@ def hip_ipa_layer_tail(hl, layer, x1, mods6, mask_b):
     shared parameters).  x1 [B, L, C], mods6 [B, 6C], mask_b [B, L]."""
     C = hl.C
     inv_freq = layer.mha_l.attn.rot_emb.inv_freq if hl.rope else None
-    mods9 = torch.cat([mods6[:, :3 * C], mods6.new_zeros(mods6.shape[0], 3 * C), mods6[:, 3 * C:]], -1)
+    mods9 = _Mods9.apply(mods6, C)
     mha = layer.mha_l.attn
     att = [mha.q_proj.weight, mha.q_proj.bias, mha.k_proj.weight, mha.k_proj.bias, mha.v_proj.weight, mha.v_proj.bias,
            mha.out_proj.weight, mha.out_proj.bias, mha.bias_k, mha.bias_v]
@@ -348,6 +370,9 @@ class _HipLayerFn(torch.autograd.Function):
         if nxt is None:
             return h_out
         ctx.mark_non_differentiable(nxt[0], nxt[1])
+        # the hand-off outputs' gradients stay None (materialized they were two zero fills per
+        # layer and step)
+        ctx.set_materialize_grads(False)
         return h_out, nxt[0], nxt[1]
 
     @staticmethod
@@ -361,6 +386,8 @@ class _HipLayerFn(torch.autograd.Function):
         s = _lib.stream_handle()
         rope_l, rope_t = ctx.rope
         kb_t, kb_s = ctx.kb
+        if dh3 is None:  # (set_materialize_grads(False): h_out unused downstream)
+            dh3 = torch.zeros(B, T, L, C, device=h.device)
         dh3 = dh3.contiguous().float().reshape(N, C)
         mods = mods.contiguous()
         nblk = lib.mdg_ln_gate_bwd_blocks(TL)
