@@ -157,11 +157,12 @@ __global__ __launch_bounds__(256) void ln_gate_bwd_kernel(int M, int C, int TL, 
   }
 }
 
-// C = 384 form: half a wave per row (lane: 4 consecutive columns in each of the three 128-wide
-// chunks, so every access is one 16-B f32 / 8-B bf16 vector), two rows per wave, two row pairs
-// in flight per iteration, and the operand presence as template flags: the generic kernel
-// above branches per element on them and issues dword / short loads one wait at a time.
-template <typename CT, bool DXN, bool Y, bool DHW>
+// C = 384 form (named for the default width; C = 128 / 256 / 512 instantiate it too): half a wave
+// per row (lane: 4 consecutive columns in each of the C / 128 chunks of 128, so every access is
+// one 16-B f32 / 8-B bf16 vector), two rows per wave, two row pairs in flight per iteration, and
+// the operand presence as template flags: the generic kernel above branches per element on them
+// and issues dword / short loads one wait at a time (42 vs 28 us per launch at C = 256 / 384).
+template <typename CT, bool DXN, bool Y, bool DHW, int C = 384>
 __global__ __launch_bounds__(256) void ln_gate_bwd384_kernel(int M, int TL, const CT* __restrict__ dxn,
                                                              const float* __restrict__ hln,
                                                              const float* __restrict__ stats,
@@ -169,7 +170,8 @@ __global__ __launch_bounds__(256) void ln_gate_bwd384_kernel(int M, int TL, cons
                                                              int scale_off, const float* dh_res, float* dh_out,
                                                              const CT* __restrict__ y, int gate_off,
                                                              CT* __restrict__ dy, float* __restrict__ part) {
-  constexpr int C = 384, E = 3, R = 2;
+  constexpr int E = C / 128, R = 2;
+  static_assert(C % 128 == 0 && C <= 512, "C");
   __shared__ float red[4][4][C];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, hl = lane & 31, half = lane >> 5;
   const int b = blockIdx.y, jb = blockIdx.x;
@@ -295,15 +297,18 @@ hipError_t ln_gate_bwd_launch(int dtype, int M, int C, int TL, const void* dxn, 
                               float* dh_out, const void* y, int gate_off, void* dy, float* part, hipStream_t s) {
   const int B = M / TL;
   dim3 grid(ln_gate_bwd_blocks(TL), B);
-  if (C == 384 && ((uintptr_t)mods & 15) == 0 && mod_stride % 4 == 0 && scale_off % 4 == 0 && gate_off % 4 == 0) {
+  if ((C == 128 || C == 256 || C == 384 || C == 512) && ((uintptr_t)mods & 15) == 0 && mod_stride % 4 == 0 && scale_off % 4 == 0 && gate_off % 4 == 0) {
     const bool dhw = dxn || dh_out != dh_res;
-#define MDG_LNB384(CTT, X_, Y_, W_)                                                                                hipLaunchKernelGGL((ln_gate_bwd384_kernel<CTT, X_, Y_, W_>), grid, dim3(256), 0, s, M, TL, (const CTT*)dxn, hln,                      stats, mods, mod_stride, scale_off, dh_res, dh_out, (const CTT*)y, gate_off, (CTT*)dy, part)
-#define MDG_LNB384_T(CTT)                                                                      if (dxn && y) MDG_LNB384(CTT, true, true, true);                                             else if (dxn) MDG_LNB384(CTT, true, false, true);                                            else if (y) { if (dhw) MDG_LNB384(CTT, false, true, true); else MDG_LNB384(CTT, false, true, false); }   else { if (dhw) MDG_LNB384(CTT, false, false, true); else MDG_LNB384(CTT, false, false, false); }
-    if (dtype == MDG_BF16) {
-      MDG_LNB384_T(bf16_t)
-    } else {
-      MDG_LNB384_T(float)
-    }
+#define MDG_LNB384(CTT, X_, Y_, W_, NC_)                                                                                hipLaunchKernelGGL((ln_gate_bwd384_kernel<CTT, X_, Y_, W_, NC_>), grid, dim3(256), 0, s, M, TL, (const CTT*)dxn, hln,                      stats, mods, mod_stride, scale_off, dh_res, dh_out, (const CTT*)y, gate_off, (CTT*)dy, part)
+#define MDG_LNB384_T(CTT, NC_)                                                                      if (dxn && y) MDG_LNB384(CTT, true, true, true, NC_);                                             else if (dxn) MDG_LNB384(CTT, true, false, true, NC_);                                            else if (y) { if (dhw) MDG_LNB384(CTT, false, true, true, NC_); else MDG_LNB384(CTT, false, true, false, NC_); }   else { if (dhw) MDG_LNB384(CTT, false, false, true, NC_); else MDG_LNB384(CTT, false, false, false, NC_); }
+#define MDG_LNB384_C(NC_)                                                                                \
+  if (dtype == MDG_BF16) {                                                                               \
+    MDG_LNB384_T(bf16_t, NC_)                                                                            \
+  } else {                                                                                               \
+    MDG_LNB384_T(float, NC_)                                                                             \
+  }
+    if (C == 128) { MDG_LNB384_C(128) } else if (C == 256) { MDG_LNB384_C(256) } else if (C == 384) { MDG_LNB384_C(384) } else { MDG_LNB384_C(512) }
+#undef MDG_LNB384_C
 #undef MDG_LNB384_T
 #undef MDG_LNB384
     return hipGetLastError();
