@@ -452,7 +452,9 @@ struct WgPlan {
 
 // MDG_WGRAD_WIDE=1: the wide tiles for the MLP weights (opt-in: the token split doubles with half
 // the tiles, and the partial round trip eats the per-FLOP gain; 16.48 vs 16.28 ms per training
-// step, same box); MDG_WGRAD_BLOCKS: target block count of the token split (default 512 = 2 per CU)
+// step, same box); MDG_WGRAD_BLOCKS: target block count of the token split (default 768 = 3 per CU:
+// training step 11.30-11.39 ms vs 11.61-11.68 at 512, 11.44-11.49 at 640, 11.82-11.91 at 1 024,
+// 12.0 at 384, same box, round 5)
 static int wgrad_wide_enabled() {
   static const int v = [] {
     const char* e = getenv("MDG_WGRAD_WIDE");
@@ -471,8 +473,8 @@ static int wgrad_stages() {
 static int wgrad_target_blocks() {
   static const int v = [] {
     const char* e = getenv("MDG_WGRAD_BLOCKS");
-    const int b = e ? atoi(e) : 512;
-    return b > 0 ? b : 512;
+    const int b = e ? atoi(e) : 768;
+    return b > 0 ? b : 768;
   }();
   return v;
 }
@@ -486,8 +488,8 @@ WgPlan wgrad_plan(int dtype, int N, int M, int K, bool need_w, bool need_b) {
   const int tiles = ((M + tm - 1) / tm) * ((K + tk - 1) / tk);
   const int quantum = dtype == MDG_BF16 ? kWgBK : 16;
   const int nq = (N + quantum - 1) / quantum;
-  // ~2 blocks per CU over the 256 CUs, each split at least 8 K-steps long.  The block count
-  // stays AT MOST the target (two resident blocks per CU): rounding the split count up put the
+  // ~3 blocks per CU over the 256 CUs, each split at least 8 K-steps long.  The block count
+  // stays AT MOST the target (resident blocks per CU x 256): rounding the split count up put the
   // last few blocks in a second round, which then took as long as the first (w2: 540 blocks,
   // 78 us; at 504 blocks the grid is one round)
   const int target = wgrad_target_blocks();
