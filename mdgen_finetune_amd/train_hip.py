@@ -235,7 +235,12 @@ class _Mods9(torch.autograd.Function):
         key = (mods6.shape[0], C, mods6.dtype, mods6.device)
         z = _Mods9._zeros.get(key)
         if z is None:
-            z = _Mods9._zeros[key] = torch.zeros(mods6.shape[0], 3 * C, dtype=mods6.dtype, device=mods6.device)
+            z = torch.zeros(mods6.shape[0], 3 * C, dtype=mods6.dtype, device=mods6.device)
+            # (a block made inside a stream capture belongs to that graph's pool: not cached; the
+            # cached ones are never evicted — a captured graph may hold their address — and are a
+            # few KiB per (B, C))
+            if not (z.is_cuda and torch.cuda.is_current_stream_capturing()):
+                _Mods9._zeros[key] = z
         ctx.C = C
         return torch.cat([mods6[:, :3 * C], z, mods6[:, 3 * C:]], -1)
 
