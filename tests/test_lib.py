@@ -112,6 +112,28 @@ def test_shape_validation_without_gpu():
     assert offs["kbias"] < lib.mdg_workspace_bytes(ctypes.byref(d))
 
 
+def test_attention_backward_sizes_without_gpu():
+    """ABI 23 host-side sizes: the temporal backward's scratch scales with the head stride (32 ->
+    64 columns at head_dim 32..63) and is 0 outside 1..63; bias-slot counts per variant (the fused
+    kernel one per sequence, the scalar kernels one per 256 queries); the spatial backward's slot
+    count takes H (the L = 4 grid-stride kernel: at most 256 blocks)."""
+    from mdgen_finetune_amd import _lib
+
+    lib = _lib.load()
+    B, T, L, H = 8, 1000, 4, 16
+    narrow = lib.mdg_attn_temporal_bwd_scratch(_lib.MDG_F32, B, T, L, H, 24)
+    wide = lib.mdg_attn_temporal_bwd_scratch(_lib.MDG_F32, B, T, L, H, 48)
+    rows = B * L * H * T
+    assert narrow >= rows * 32 * 4 + rows * 4 and wide >= rows * 64 * 4 + rows * 4 and wide > narrow
+    assert lib.mdg_attn_temporal_bwd_scratch(_lib.MDG_F32, B, T, L, H, 64) == 0
+    assert lib.mdg_attn_temporal_bwd_parts(_lib.MDG_BF16, B, T, L, 0) == B * L
+    assert lib.mdg_attn_temporal_bwd_parts(_lib.MDG_BF16, B, T, L, 1) == B * L * 4
+    assert lib.mdg_attn_temporal_bwd_parts(_lib.MDG_F32, B, T, L, 1) == B * L * 4
+    assert lib.mdg_attn_spatial_bwd_parts(B * T, 4, 16, 24) == 256
+    assert lib.mdg_attn_spatial_bwd_parts(2, 4, 16, 24) == 1
+    assert lib.mdg_attn_spatial_bwd_parts(B * T, 6, 8, 48) == (B * T * 8 + 127) // 128
+
+
 def test_adam_table_image_without_gpu():
     """mdg_adam_table_build (host only): the tensor entries, then chunk -> (tensor, chunk index)
     for chunks of 16384 elements; tensors without elements and null pointers are refused."""
