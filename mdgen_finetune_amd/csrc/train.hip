@@ -407,6 +407,7 @@ __global__ __launch_bounds__(256) void attn_bwd_prep_tiled_kernel(int B, int T, 
                                                                   bf16_t* __restrict__ dop, float* __restrict__ delta,
                                                                   const float* __restrict__ lse) {
   __shared__ __attribute__((aligned(16))) bf16_t tile[256 * kDP];  // [head][tl][kDP]
+  __shared__ float dls[256];                                         // [head][tl]: delta
   const int TT = 256 / H, seq = blockIdx.y, b = seq / L, l = seq - b * L;
   const int t0 = blockIdx.x * TT, head = threadIdx.x % H, tl = threadIdx.x / H, t = t0 + tl;
   const int C = H * D;
@@ -445,11 +446,17 @@ __global__ __launch_bounds__(256) void attn_bwd_prep_tiled_kernel(int B, int T, 
       }
       *reinterpret_cast<bf16x8*>(trow + d0) = dv;
     }
-    delta[((size_t)seq * H + head) * T + t] = dl;
+    dls[head * TT + tl] = dl;
   }
   __syncthreads();
-  // head h's rows t0 .. t0 + nt - 1 are one contiguous run of nt x kDP elements in its plane
+  // head h's rows t0 .. t0 + nt - 1 are one contiguous run of nt x kDP elements in its plane, and
+  // of nt delta values (each thread's own 4-B delta store touched a line of its own; step time
+  // neutral: 11.41 / 11.44 vs 11.43 / 11.44 ms same box, fewer partial-line writes)
   const int nt = min(TT, T - t0), pieces = nt * (kDP / 8);
+  {
+    const int h = threadIdx.x / TT, tt = threadIdx.x - h * TT;
+    if (h < H && tt < nt) delta[((size_t)seq * H + h) * T + t0 + tt] = dls[h * TT + tt];
+  }
   for (int e = threadIdx.x; e < H * (TT * kDP / 8); e += 256) {
     const int h = e / (TT * kDP / 8), q = e - h * (TT * kDP / 8);
     if (q < pieces)
