@@ -13,9 +13,18 @@ B=16 trajectories per GPU, run as 2 concurrent 8-trajectory chains ("lanes": par
 branches of the one hipGraph, engine._run_lanes).
 value = frames denoised per second = ranks * B * T * 49 * steps / max-over-ranks time.
 
-Multi-GPU: inference does not shard (temporal attention couples all T frames of a
-trajectory), so N ranks run N independent replicas of the window ("replicas only",
-scaling "weak"); no collective on the data path.
+Multi-GPU (--gpus N > 1): inference does not shard (temporal attention couples all T frames of
+a trajectory), so N ranks run N independent replicas of the window ("replicas only", scaling
+"weak"); no collective on the data path.  The path that does shard is config 3's training
+(DDP, /root/reference/src/train.py:46-60), so an N-GPU line also carries a "train_dp" object:
+the graphed GVP training step at B=8 per GPU x T=1000, gradients averaged over RCCL (bucket
+all-reduces captured in the step's graph, replicated conditioning on its own communicator).
+Launch: with no launcher environment this process is an orchestrator that never touches the
+GPU: it spawns one worker process per GPU per leg (inference, then train_dp), each on
+cuda:LOCAL_RANK with its own RCCL group, waits for them (bounded), and prints ONE line.  Under
+torch.distributed.run (WORLD_SIZE set; must equal --gpus) each launched process orchestrates
+its own rank's workers the same way.  A train_dp leg that fails or times out is reported as
+such in the line; the inference line stands.
 
 Extra fields: "roofline" for the dominant kernel (the fused MLP, mlp_rowln_kernel: fc1 +
 GELU + fc2 + gated residual + next LN in one launch, the largest share of the step per
@@ -31,7 +40,10 @@ import ctypes
 import json
 import math
 import os
+import signal
+import subprocess
 import sys
+import tempfile
 import time
 
 import torch
@@ -78,6 +90,10 @@ def parse():
     ap.add_argument("--train-rccl1", action="store_true",
                     help="with --train at one GPU: a world-1 RCCL group with the gradient reduction forced on, "
                          "so the step's graph carries its per-bucket all-reduces (rehearsal of the N-GPU step)")
+    ap.add_argument("--train-batch", type=int, default=8, help="trajectories per GPU of the N-GPU line's train_dp leg")
+    ap.add_argument("--no-train-dp", action="store_true", help="N > 1: skip the train_dp leg")
+    ap.add_argument("--leg-timeout", type=float, default=900.0, help="s: bound on the primary leg's workers")
+    ap.add_argument("--train-dp-timeout", type=float, default=360.0, help="s: bound on the train_dp leg's workers")
     ap.add_argument("--tps", action="store_true",
                     help="TPS / interpolation model (BASELINE config 4: --tps_condition, latent 28, start + end "
                          "frames conditioned; use with --frames 100); an evidence line, not the headline")
@@ -483,13 +499,14 @@ def cpu_train_baseline(T, L, seconds):
                       f"B=1 T={T} L={L}, {el:.1f} s on {threads} threads"}
 
 
-def train_main(a, world, rank, dev, share):
+def train_main(a, world, rank, dev, share, dp=False):
     """Config 3 (BASELINE.json configs[2]): training frames/s = world * B * T * steps / time of
-    `steps` optimizer steps (GraphedStep replays; the batch is on the device)."""
+    `steps` optimizer steps (GraphedStep replays; the batch is on the device).  dp: the N-GPU
+    line's train_dp leg (B = --train-batch, in-graph DP markers; returns its object on rank 0)."""
     from mdgen_finetune_amd.parsing import parse_train_args
     from mdgen_finetune_amd.train import Trainer
 
-    B, T, L = a.batch, a.frames, a.crop
+    B, T, L = (a.train_batch if dp else a.batch), a.frames, a.crop
     args = parse_train_args(["--synthetic", "--sim_condition", "--prepend_ipa", "--abs_pos_emb", "--num_frames",
                              str(T), "--crop", str(L), "--batch_size", str(B), "--synthetic_size", str(B * world),
                              "--hip_dtype", a.dtype, "--seed", "137"] + a.model_args.split())
@@ -498,8 +515,11 @@ def train_main(a, world, rank, dev, share):
     if rehearse:  # a world-1 RCCL group with the reduction forced on: the in-graph bucket all-reduces run
         torch.distributed.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % _free_port(), rank=0,
                                              world_size=1, device_id=dev)
+    if world > 1 and a.no_cond_gather:
+        args.cond_allgather = 0
     tr = Trainer(args, rank, world, dev)
     tr.force_allreduce = rehearse
+    tr.dp_markers = True  # in-graph events around backward's end and the last bucket all-reduce
     if rehearse and not a.no_cond_gather:  # the replicated conditioning's all-gathers at world 1 too
         tr.setup_cond_gather()
     batch = {k: (v.to(dev) if torch.is_tensor(v) else v) for k, v in next(iter(tr.loader)).items()}
@@ -517,13 +537,23 @@ def train_main(a, world, rank, dev, share):
     if world > 1:
         torch.distributed.barrier()
     el = max_over_ranks(time.perf_counter() - t0, world, torch.device("cpu") if share else dev)
+    # the DP markers of a few more replays (untimed): forward + backward, and the all-reduce time
+    # left after backward's end (the bucket all-reduces backward did not hide)
+    dpt = []
+    if tr._graphed is not None and tr._graphed.markers is not None:
+        for _ in range(5):
+            tr.step([batch], log=False)
+            dpt.append(tr._graphed.dp_times_ms())
+    n_diff = tr.check_replicas(resync=False) if world > 1 else 0
+    seen = ranks_seen(world, dev, share)
     if rank != 0:
-        return
+        _release(tr)
+        return None
     sec = el / a.steps
     sm = step_model(B, T, L, dtype=a.dtype)
     flops = 3.0 * sm["flops"]  # forward + backward (2x) of the block stack per optimizer step
     tf = flops / sec / 1e12
-    cpu = None if (a.no_cpu_baseline or world > 1) else cpu_train_baseline(T, L, a.cpu_seconds)
+    cpu = None if (a.no_cpu_baseline or world > 1 or dp) else cpu_train_baseline(T, L, a.cpu_seconds)
     out = {"metric": "training frames/sec (GVP flow-matching optimizer step), 1000-frame x crop4 forward-sim, "
                      "1/2/4/8 MI355X",
            "value": round(world * B * T * a.steps / el, 1), "unit": "frames/s", "n_gpus": 1 if share else world,
@@ -546,28 +576,46 @@ def train_main(a, world, rank, dev, share):
                              "achieved_tflops": round(tf, 1), "peak_tflops": PEAK_TFLOPS[a.dtype],
                              "mfma_frac": round(tf / PEAK_TFLOPS[a.dtype], 4)},
            "loss": float(loss), "max_mem_gb": round(torch.cuda.max_memory_allocated() / 2 ** 30, 2),
-           "cpu_baseline": cpu}
+           "cpu_baseline": cpu, "ranks_seen": seen}
+    if dpt:
+        out["dp_markers"] = {"fwd_bwd_ms": round(sum(x[0] for x in dpt) / len(dpt), 3),
+                             "exposed_allreduce_ms": round(sum(x[1] for x in dpt) / len(dpt), 3),
+                             "replays": len(dpt),
+                             "what": "in-graph timing events: step start -> backward's end (main stream), and "
+                                     "backward's end -> the last bucket all-reduce done (side stream; 0 = hidden)"}
+    if world > 1:
+        out["replicas_identical"] = n_diff == 0
+        out["replicated_conditioning"] = bool(tr.replicated)
+        out["allreduce"] = ("per-bucket RCCL all-reduces in the step's graph (side stream), conditioning "
+                            "all-gathers on a second communicator" if (tr._graphed is not None and tr._graphed.overlap)
+                            else "flat all-reduce between two graphs")
     if a.model_args:  # (step_model prices the default model only)
         out["step_roofline"] = None
     if share:
         out["shared_gpu"] = True
         out["ranks_sharing_gpu"] = world
-    if rehearse:
+    if (rehearse or world > 1) and tr._graphed is not None and tr._graphed.reducer is not None:
         red = tr._graphed.reducer
         out["replicated_conditioning_params"] = sum(p.numel() for p in tr.wrapper.model.parameters()
                                                     if id(p) in tr.replicated)
         out["allreduce_buckets"] = {"n": len(red.buckets), "bytes": [int(sl.numel() * 4) for sl in red.slices],
                                     "launched_after_grads": [n for _, n in red.launch_log],
                                     "grads_total": sum(len(b) for b in red.buckets)}
-    print(json.dumps(out), flush=True)
-    if rehearse:  # the graph holding the captured collectives goes before the communicator
-        tr._graphed = None
-        del tr
-        import gc
-
-        gc.collect()
-        torch.cuda.synchronize()
+    _release(tr)
+    if dp:
+        return out
+    emit(out)
+    if rehearse:
         torch.distributed.destroy_process_group()
+
+
+def _release(tr):
+    """The graph holding captured collectives goes before the communicator."""
+    import gc
+
+    tr._graphed = None
+    gc.collect()
+    torch.cuda.synchronize()
 
 
 def dopri5_main(a, world, rank, dev, share):
@@ -638,16 +686,73 @@ def dopri5_main(a, world, rank, dev, share):
         cpu = dict(cpu, value=round(T / (per_eval * nfe), 2),
                    sample=cpu["sample"] + f"; dopri5 window = {nfe:.0f} such forwards (this run's NFE)")
         out["cpu_baseline"] = cpu
-    print(json.dumps(out), flush=True)
+    emit(out)
 
 
-def main():
-    a = parse()
+def emit(obj):
+    """The leg's result: printed (in-process run) or written for the orchestrator (MDG_BENCH_OUT)."""
+    path = os.environ.get("MDG_BENCH_OUT")
+    if path:
+        with open(path, "w") as f:
+            json.dump(obj, f)
+    else:
+        print(json.dumps(obj), flush=True)
+
+
+def ranks_seen(world, dev, share):
+    """Distinct devices the ranks ran on: every rank's PCI (domain, bus, device) all-gathered."""
+    if world <= 1:
+        return 1
+    pr = torch.cuda.get_device_properties(dev)
+    code = torch.tensor([pr.pci_domain_id * 2 ** 16 + pr.pci_bus_id * 2 ** 8 + pr.pci_device_id], dtype=torch.int64,
+                        device=torch.device("cpu") if share else dev)
+    allc = [torch.empty_like(code) for _ in range(world)]
+    torch.distributed.all_gather(allc, code)
+    return len({int(c.item()) for c in allc})
+
+
+def _primary_leg(a):
+    return "train" if a.train else ("dopri5" if a.sampler == "dopri5" else "infer")
+
+
+def dry_leg(a, leg, world, rank):
+    """MDG_BENCH_DRYRUN=1 (the CPU tests of the launch path): the leg's rendezvous, barrier and
+    max-over-ranks over gloo with a fixed CPU sleep as the "step"; no GPU, no model."""
+    import torch.distributed as dist
+
+    if world > 1:
+        dist.init_process_group("gloo")
+        if os.environ.get("MDG_BENCH_DRYRUN_FAIL") == leg and rank == world - 1:
+            sys.exit(3)  # (the tests' failing-rank case: the other ranks block in the barrier)
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        time.sleep(0.01 * (1 + rank))
+    if world > 1:
+        dist.barrier()
+    el = max_over_ranks(time.perf_counter() - t0, world, torch.device("cpu"))
+    seen = world
+    if world > 1:
+        allp = [None] * world
+        dist.all_gather_object(allp, os.getpid())
+        seen = len(set(allp))
+        dist.destroy_process_group()
+    if rank == 0:
+        B = a.train_batch if leg == "train_dp" else a.batch
+        emit({"metric": "dry run", "leg": leg, "value": round(world * B * a.frames * a.steps / el, 1),
+              "n_gpus": world, "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(el / a.steps * 1e3, 3),
+              "ranks_seen": seen, "dryrun": True})
+
+
+def run_leg(a, leg):
+    """One rank of one leg: rank / world from the environment, cuda:LOCAL_RANK (cuda:0 for every
+    rank with MDG_BENCH_SHARE_GPU=1: the N-rank rehearsal on a one-GPU box, gloo for the barrier /
+    max-over-ranks, RCCL refusing two ranks per GPU), RCCL group for world > 1."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # rehearsal of the N-rank path on a one-GPU box: MDG_BENCH_SHARE_GPU=1 puts every rank on
-    # cuda:0 and uses gloo for the barrier / max-over-ranks (RCCL refuses two ranks per GPU)
+    if os.environ.get("MDG_BENCH_DRYRUN") == "1":
+        return dry_leg(a, leg, world, rank)
     share = os.environ.get("MDG_BENCH_SHARE_GPU") == "1"
     if share:
         local = 0
@@ -660,16 +765,157 @@ def main():
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=dev)
-    if a.train:
-        train_main(a, world, rank, dev, share)
-        if world > 1:
+    try:
+        if leg == "train_dp":
+            out = train_main(a, world, rank, dev, share, dp=True)
+            if rank == 0:
+                emit(out)
+        elif leg == "train":
+            train_main(a, world, rank, dev, share)
+        elif leg == "dopri5":
+            dopri5_main(a, world, rank, dev, share)
+        else:
+            infer_main(a, world, rank, dev, share)
+    finally:
+        if world > 1 and torch.distributed.is_initialized():
             torch.distributed.destroy_process_group()
-        return
-    if a.sampler == "dopri5":
-        dopri5_main(a, world, rank, dev, share)
-        if world > 1:
-            torch.distributed.destroy_process_group()
-        return
+
+
+def _wait_all(procs, timeout):
+    """Wait for every worker; past `timeout` s kill the stragglers' process groups.  Returns one
+    exit status per worker ('timeout' for a killed one)."""
+    t_end = time.monotonic() + timeout
+    rcs = [None] * len(procs)
+    while any(r is None for r in rcs):
+        for i, p in enumerate(procs):
+            if rcs[i] is None and p.poll() is not None:
+                rcs[i] = p.returncode
+        if any(r not in (None, 0) for r in rcs):  # one rank failed: the others would wait forever
+            t_end = min(t_end, time.monotonic() + min(30.0, timeout))
+        if time.monotonic() > t_end:
+            for i, p in enumerate(procs):
+                if rcs[i] is None:
+                    try:
+                        os.killpg(p.pid, signal.SIGKILL)
+                    except ProcessLookupError:
+                        pass
+                    p.wait()
+                    rcs[i] = "timeout"
+            break
+        time.sleep(0.2)
+    return rcs
+
+
+def orchestrate(a, argv):
+    """--gpus N > 1: launch the legs' worker processes (never touching the GPU here) and print one
+    line.  Without a launcher this process starts all N ranks; under torch.distributed.run
+    (WORLD_SIZE = N) each launched process starts its own rank's worker, the launched processes
+    agreeing on a fresh rendezvous port per leg over a gloo group of their own."""
+    import datetime
+
+    import torch.distributed as dist
+
+    N = a.gpus
+    share = os.environ.get("MDG_BENCH_SHARE_GPU") == "1"
+    dry = os.environ.get("MDG_BENCH_DRYRUN") == "1"
+    launched = "WORLD_SIZE" in os.environ
+    store = None
+    if launched:  # the launcher's key-value store (no process group: nothing here touches a device)
+        base, orank, _ = next(dist.rendezvous("env://"))
+        store = dist.PrefixStore("mdg_bench", base)
+        store.set_timeout(datetime.timedelta(seconds=a.leg_timeout + a.train_dp_timeout + 600))
+        ranks = [(orank, int(os.environ.get("LOCAL_RANK", "0")))]
+    else:
+        orank = 0
+        ranks = [(r, r) for r in range(N)]
+
+    def bcast(key, val):
+        if store is None:
+            return val
+        if orank == 0:
+            store.set(key, json.dumps(val))
+        return json.loads(store.get(key))
+
+    def gather(key, val):
+        if store is None:
+            return [val]
+        store.set(f"{key}/{orank}", json.dumps(val))
+        return [json.loads(store.get(f"{key}/{r}")) for r in range(N)]
+    if not (share or dry):
+        ndev = torch.cuda.device_count()  # (counts devices without initialising HIP)
+        need = 1 + max(lr for _, lr in ranks)
+        if ndev < need:
+            print(f"bench.py: --gpus {N} needs {need} visible GPUs on this node, found {ndev}", file=sys.stderr)
+            return 2
+    primary = _primary_leg(a)
+    legs = [primary] + (["train_dp"] if (primary == "infer" and not a.tps and not a.no_train_dp) else [])
+    results = {}
+    for leg in legs:
+        port = [bcast(f"port/{leg}", _free_port() if orank == 0 else None)]
+        fd, outp = tempfile.mkstemp(prefix=f"mdg_bench_{leg}_", suffix=".json")
+        os.close(fd)
+        env0 = {k: v for k, v in os.environ.items() if not k.startswith("TORCHELASTIC_")}
+        env0.update(MDG_BENCH_LEG=leg, WORLD_SIZE=str(N), LOCAL_WORLD_SIZE=str(N if not launched else
+                                                                             os.environ.get("LOCAL_WORLD_SIZE", N)),
+                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port[0]), MDG_BENCH_OUT=outp)
+        procs = []
+        for r, lr in ranks:
+            env = dict(env0, RANK=str(r), LOCAL_RANK=str(lr))
+            if r != 0:
+                env.pop("MDG_BENCH_OUT")
+            procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env,
+                                          stdout=sys.stderr, start_new_session=True))
+        rcs = _wait_all(procs, a.leg_timeout if leg == primary else a.train_dp_timeout)
+        if launched:  # every launched process learns every rank's status
+            rcs = [x for r_ in gather(f"rc/{leg}", rcs) for x in r_]
+        res = None
+        if orank == 0:
+            try:
+                with open(outp) as f:
+                    res = json.load(f)
+            except (OSError, ValueError):
+                res = None
+        os.unlink(outp)
+        results[leg] = (rcs, res)
+        if leg == primary and any(rc != 0 for rc in rcs):
+            break
+    rc = 0
+    if orank == 0:
+        rcs, line = results[primary]
+        if any(r_ != 0 for r_ in rcs) or line is None:
+            print(f"bench.py: the {primary} leg failed: worker exit statuses {rcs}", file=sys.stderr)
+            rc = 1
+        else:
+            if "train_dp" in results:
+                trcs, tline = results["train_dp"]
+                if any(r_ != 0 for r_ in trcs) or tline is None:
+                    tline = {"status": "failed", "worker_exit": trcs,
+                             "note": "the N-GPU training leg did not complete (its workers' stderr is in the log)"}
+                line["train_dp"] = tline
+            line["launch"] = ("torch.distributed.run (one worker per launched rank)" if launched else
+                              f"self-launched: {N} worker processes" + (" sharing cuda:0 (rehearsal)" if share
+                                                                        else ", one per GPU"))
+            print(json.dumps(line), flush=True)
+    gather("done", rc)
+    return rc
+
+
+def main():
+    a = parse()
+    leg = os.environ.get("MDG_BENCH_LEG")
+    if leg:  # a worker of orchestrate()
+        return run_leg(a, leg)
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None and int(env_world) != a.gpus:
+        print(f"bench.py: WORLD_SIZE={env_world} but --gpus {a.gpus}: refusing to report a different GPU count",
+              file=sys.stderr)
+        sys.exit(2)
+    if a.gpus == 1:  # the headline: in this process
+        return run_leg(a, _primary_leg(a))
+    sys.exit(orchestrate(a, sys.argv[1:]))
+
+
+def infer_main(a, world, rank, dev, share):
     from mdgen_finetune_amd.engine import get_engine
 
     B, T, L = a.batch, a.frames, a.crop
@@ -711,6 +957,7 @@ def main():
         if rank == 0 and a.tps:
             roofs = {"step": step_kernel_roofline(eng, B, T, L, a.dtype, nl, zs, kw)}
         plan = eng.describe_plan(Bl, T, L)
+        seen = ranks_seen(world, dev, share)
 
     # extra lines (rank 0, single process): the B sweep SURVEY §8(d) asks for and the fp32
     # parity-path throughput, each with its own step-level roofline
@@ -752,6 +999,7 @@ def main():
             "roofline": list(roofs.values())[0] if roofs else None,
             "roofline_more": list(roofs.values())[1:] if roofs else None,
             "cpu_baseline": cpu,
+            "ranks_seen": seen,
         }
         if a.tps:  # BASELINE config 4 evidence line (tps_inference.py path), not the headline metric
             out["config"]["workload"] = (f"tps_inference window: Euler ODE {n_euler} denoising steps x B={B} "
@@ -761,9 +1009,7 @@ def main():
         if share:  # rehearsal: every rank on cuda:0 — not a multi-GPU measurement
             out["shared_gpu"] = True
             out["ranks_sharing_gpu"] = world
-        print(json.dumps(out), flush=True)
-    if world > 1:
-        torch.distributed.destroy_process_group()
+        emit(out)
 
 
 if __name__ == "__main__":

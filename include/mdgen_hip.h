@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define MDG_ABI_VERSION 23
+#define MDG_ABI_VERSION 24
 #define MDG_MAX_LAYERS 16
 #define MDG_SEG_MAX 16 /* segments of one mdg_seg_linear */
 #define MDG_DP 32      /* padded head dim of the attention operand buffers for head_dim <= 31 */
@@ -157,6 +157,14 @@ typedef struct {
 
 int mdg_abi_version(void);
 const char* mdg_last_error_string(void);
+
+/* Device timestamps (ABI 24; no reference counterpart: instrumentation of the data-parallel
+   training step, train.GraphedStep's DP markers).  mdg_stamp enqueues one single-thread kernel
+   that writes the GPU's constant-rate wall clock to dst[slot] when the stream reaches it (graph-
+   capturable: the markers live inside the captured step); mdg_wall_clock_khz gives that clock's
+   rate for the current device. */
+int mdg_stamp(uint64_t* dst, int32_t slot, void* stream);
+int mdg_wall_clock_khz(int32_t* khz);
 
 /* Workspace (attention operand buffers, hidden activations, key-padding bias). */
 size_t mdg_workspace_bytes(const mdg_dims* d);

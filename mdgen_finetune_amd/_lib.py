@@ -137,6 +137,8 @@ class MdgAdamTensor(ctypes.Structure):
 SIGNATURES = [
     ("mdg_abi_version", _i32, []),
     ("mdg_last_error_string", ctypes.c_char_p, []),
+    ("mdg_stamp", _i32, [_vp, _i32, _vp]),
+    ("mdg_wall_clock_khz", _i32, [ctypes.POINTER(_i32)]),
     ("mdg_workspace_bytes", ctypes.c_size_t, [ctypes.POINTER(MdgDims)]),
     ("mdg_workspace_offsets", _i32, [ctypes.POINTER(MdgDims), ctypes.POINTER(ctypes.c_size_t)]),
     ("mdg_workspace_init", _i32, [ctypes.POINTER(MdgDims), _vp, _vp]),
@@ -203,7 +205,7 @@ SIGNATURES = [
                                                                           ctypes.c_size_t, _vp]),
 ]
 
-ABI_VERSION = 23
+ABI_VERSION = 24
 _LIB = None
 
 

@@ -354,9 +354,29 @@ bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 }  // namespace
 
+__global__ void stamp_kernel(unsigned long long* dst, int slot) {
+  if (threadIdx.x == 0) dst[slot + threadIdx.x] = wall_clock64();
+}
+
 extern "C" {
 
 int mdg_abi_version(void) { return MDG_ABI_VERSION; }
+
+int mdg_stamp(uint64_t* dst, int32_t slot, void* stream) {
+  if (!dst || slot < 0) return fail(MDG_E_ARG, "mdg_stamp: null buffer or negative slot");
+  hipLaunchKernelGGL(stamp_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, (unsigned long long*)dst, slot);
+  return hip_check(hipGetLastError(), "mdg_stamp");
+}
+
+int mdg_wall_clock_khz(int32_t* khz) {
+  int dev = 0, v = 0;
+  if (!khz) return fail(MDG_E_ARG, "mdg_wall_clock_khz: null output");
+  hipError_t e = hipGetDevice(&dev);
+  if (e == hipSuccess) e = hipDeviceGetAttribute(&v, hipDeviceAttributeWallClockRate, dev);
+  if (e != hipSuccess) return hip_check(e, "mdg_wall_clock_khz");
+  *khz = v;
+  return MDG_OK;
+}
 
 const char* mdg_last_error_string(void) { return g_err.c_str(); }
 

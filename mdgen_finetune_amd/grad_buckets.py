@@ -62,21 +62,28 @@ def agree_order(params, order, world, group=None):
         return seen
     dev = params[0].device if dist.get_backend(group) == "nccl" else torch.device("cpu")
     n = len(params)
-    # per-rank signature: parameter count, total elements, a shape checksum, the reached set
+    # per-rank signature: parameter count, total elements, a position-weighted numel checksum,
+    # then per parameter a code of its SHAPE (rank and every extent), then the reached set
     reached = torch.zeros(n, dtype=torch.int64)
     reached[seen] = 1
     numels = torch.tensor([p.numel() for p in params], dtype=torch.int64)
-    sig = torch.cat([torch.tensor([n, int(numels.sum()), int((numels * torch.arange(1, n + 1)).sum())]), reached])
+    shapes = torch.tensor([_shape_code(p.shape) for p in params], dtype=torch.int64)
+    head = torch.tensor([n, int(numels.sum()), int((numels * torch.arange(1, n + 1)).sum())])
+    sig = torch.cat([head, shapes, reached])
     sig = sig.to(dev)
     allsig = [torch.empty_like(sig) for _ in range(world)]
     dist.all_gather(allsig, sig, group=group)
     for r, other in enumerate(allsig):
         if not torch.equal(other, sig):
-            o = other.cpu()
-            if not torch.equal(o[:3], sig.cpu()[:3]):
+            o, mine = other.cpu(), sig.cpu()
+            if not torch.equal(o[:3], mine[:3]):
                 raise RuntimeError(f"gradient buckets: rank {r} holds different parameters (count / sizes "
-                                   f"{o[:3].tolist()} vs {sig.cpu()[:3].tolist()})")
-            diff = (o[3:] != sig.cpu()[3:]).nonzero().flatten().tolist()
+                                   f"{o[:3].tolist()} vs {mine[:3].tolist()})")
+            bad = (o[3:3 + n] != mine[3:3 + n]).nonzero().flatten().tolist()
+            if bad:
+                raise RuntimeError(f"gradient buckets: rank {r} holds parameters of different shapes "
+                                   f"(parameters {bad[:8]}{'...' if len(bad) > 8 else ''})")
+            diff = (o[3 + n:] != mine[3 + n:]).nonzero().flatten().tolist()
             raise RuntimeError(f"gradient buckets: rank {r} reached a different set of gradients in backward "
                                f"(parameters {diff[:8]}{'...' if len(diff) > 8 else ''} differ)")
     buf = torch.full((n,), -1, dtype=torch.int64)
@@ -84,6 +91,15 @@ def agree_order(params, order, world, group=None):
     buf = buf.to(dev)
     dist.broadcast(buf, 0, group=group)
     return [int(i) for i in buf.cpu().tolist() if i >= 0]
+
+
+def _shape_code(shape):
+    """An int63 code of a shape (its rank and extents, order-sensitive): equal shapes give equal
+    codes on every rank; (3, 4) and (4, 3), or (12,) and (3, 4), do not collide."""
+    h = len(shape) + 1
+    for d in shape:
+        h = (h * 1000003 + int(d) + 1) % (2 ** 61 - 1)
+    return h
 
 
 class BucketedAllReduce:
@@ -136,6 +152,8 @@ class BucketedAllReduce:
         self.cuda = dev.type == "cuda"
         self.side = torch.cuda.Stream(device=dev) if self.cuda else None
         self._handles = []
+        self.markers = None
+        self.log = None  # a list: (op, numel, group) of every collective issued (the CPU tests)
         self.launch_log = []  # (bucket, number of hooks fired so far) per launch: the overlap record
 
     # ---------------------------------------------------------------- per step
@@ -175,6 +193,8 @@ class BucketedAllReduce:
         sl = self.slices[bi]
         b = self.buckets[bi]
         torch._foreach_copy_([self.views[i] for i in b], [self.params[i].grad for i in b])
+        if self.log is not None:
+            self.log.append(("all_reduce", int(sl.numel()), "buckets"))
         if self.cuda:
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(sl.device))
@@ -195,6 +215,8 @@ class BucketedAllReduce:
             raise RuntimeError(f"gradient buckets {missing} never completed: backward skipped parameters "
                                "that produced gradients in warm-up")
         if self.cuda:
+            if self.markers is not None:  # (train.GraphedStep's DP markers) the side branch is done
+                self.markers(2, self.side)
             torch.cuda.current_stream(self.flat.device).wait_stream(self.side)
         else:
             for w, sl in self._works:

@@ -233,9 +233,11 @@ class LatentMDGenModel(nn.Module):
 
         return seg_supported(x)
 
-    def run_ipa(self, c, mask_b, start_frames, end_frames, aatype, ada=None):
+    def run_ipa(self, c, mask_b, start_frames, end_frames, aatype, ada=None, rel7=None):
         """latent_model.py:179-214 (sim / TPS branches); c [B, C], mask_b [B, L]; ada: the IPA
-        layers' adaLN outputs precomputed by _stacked_adaln (None: each layer computes its own)."""
+        layers' adaLN outputs precomputed by _stacked_adaln (None: each layer computes its own);
+        rel7: TPS's two relative 7-vectors [2, B, L, 7] when the caller has them (the replicated
+        conditioning's all-gathered ones)."""
         B, L = mask_b.shape
         C = self.args.embed_dim
         rots, trans = frames_to_tensors(start_frames, mask_b.device)
@@ -258,7 +260,9 @@ class LatentMDGenModel(nn.Module):
                 x = layer(x, c, mask_b, rots, trans, mods=None if ada is None else ada[k])
             return x
         erots, etrans = frames_to_tensors(end_frames, mask_b.device)
-        if self._rel7_feed is not None:  # staged by the graphed training step (host eigh outside the graph)
+        if rel7 is not None:
+            rel_f, rel_r = rel7[0], rel7[1]
+        elif self._rel7_feed is not None:  # staged by the graphed training step (host eigh outside the graph)
             rel_f, rel_r = self._rel7_feed[0], self._rel7_feed[1]
         else:
             rel_f, rel_r = relative_tensor7(rots, trans, erots, etrans), relative_tensor7(erots, etrans, rots, trans)
@@ -327,10 +331,11 @@ class LatentMDGenModel(nn.Module):
                 h = h + token_linear(self.cond_to_emb, x_cond) + emb
         ckpt = bool(getattr(self.args, "grad_checkpointing", False)) and self.training
         cg = getattr(self, "_cond_gather", None)
-        if cg is not None and torch.is_grad_enabled() and not self.tps:
-            # data-parallel training: the conditioning on the ranks' global batch, local rows kept
-            # (cond_dist.CondGather: its parameters' gradients come out rank-averaged)
-            c, ada, ipa = self._replicated_conditioning(cg, t, mask, start_frames, aatype)
+        if cg is not None and cg.active and self.training and torch.is_grad_enabled():
+            # data-parallel training (inside the Trainer's own step only): the conditioning on
+            # the ranks' global batch, local rows kept (cond_dist.CondGather: its parameters'
+            # gradients come out rank-averaged)
+            c, ada, ipa = self._replicated_conditioning(cg, t, mask, start_frames, end_frames, aatype)
         else:
             c = self.embed_time(t)[:, None]
             # the HIP training path: every adaLN linear of the model as one stacked GEMM
@@ -366,26 +371,46 @@ class LatentMDGenModel(nn.Module):
             return hip_final(hl, self.emb_to_latent, h, ada[2])
         return self.emb_to_latent(h, c, mods=None if ada is None else ada[2][:, None])
 
-    def _replicated_conditioning(self, cg, t, mask, start_frames, aatype):
+    def _replicated_conditioning(self, cg, t, mask, start_frames, end_frames, aatype):
         """(c [B,1,C], (IPA mods, block mods, final mods), ipa [B,L,C]) of this rank's samples,
-        computed on the all-gathered batch of every rank (cond_dist.py)."""
+        computed on the all-gathered batch of every rank (cond_dist.py).  TPS: the end frames and
+        the relative 7-vectors (host eigh of the local frames, or the graphed step's staged
+        buffer) travel in the same gather."""
         B, L = mask.shape[0], mask.shape[2]
         C = self.args.embed_dim
         rots, trans = frames_to_tensors(start_frames, mask.device)
         if rots is None:
             rots = torch.eye(3, device=mask.device).expand(B, L, 3, 3)
             trans = torch.zeros(B, L, 3, device=mask.device)
-        t_g, mask_g, rots_g, trans_g, aa_g = cg.gather_inputs(t, mask[:, 0], rots, trans, aatype)
+        tps = None
+        if self.tps and self.args.prepend_ipa:
+            erots, etrans = frames_to_tensors(end_frames, mask.device)
+            if self._rel7_feed is not None:
+                rel7 = self._rel7_feed
+            else:
+                rel7 = torch.stack([relative_tensor7(rots, trans, erots, etrans),
+                                    relative_tensor7(erots, etrans, rots, trans)])
+            tps = (erots, etrans, rel7)
+        gathered = cg.gather_inputs(t, mask[:, 0], rots, trans, aatype, tps=tps)
+        t_g, mask_g, rots_g, trans_g, aa_g = gathered[:5]
         W = t_g.shape[0]
         c_g = self.embed_time(t_g)
         ada_g = self._stacked_adaln(c_g)
         pieces = [c_g] + list(ada_g[1]) + [ada_g[2]]
         if self.args.prepend_ipa:
-            fr = torch.zeros(W, L, 4, 4, device=mask.device)
-            fr[..., :3, :3] = rots_g
-            fr[..., :3, 3] = trans_g
-            fr[..., 3, 3] = 1.0
-            ipa_g = self.run_ipa(c_g, mask_g, fr, None, aa_g, ada=ada_g[0])
+            def rigid4(r, tr):
+                fr = torch.zeros(W, L, 4, 4, device=mask.device)
+                fr[..., :3, :3] = r
+                fr[..., :3, 3] = tr
+                fr[..., 3, 3] = 1.0
+                return fr
+
+            if tps is None:
+                ipa_g = self.run_ipa(c_g, mask_g, rigid4(rots_g, trans_g), None, aa_g, ada=ada_g[0])
+            else:
+                erots_g, etrans_g, rel_g = gathered[5]
+                ipa_g = self.run_ipa(c_g, mask_g, rigid4(rots_g, trans_g), rigid4(erots_g, etrans_g), aa_g,
+                                     ada=ada_g[0], rel7=rel_g)
             pieces.append(ipa_g.reshape(W, L * C))
         loc = torch.split(cg.local(torch.cat(pieces, -1)), [p.shape[-1] for p in pieces], -1)
         nl = len(self.layers)

@@ -68,6 +68,8 @@ _EXTRA = [
                               "prepend) runs on the all-gathered batch of every rank and its parameters' "
                               "gradients come out rank-averaged, so they leave the gradient all-reduce "
                               "(cond_dist.py); 0 = every gradient all-reduced"),
+    ("check_replicas", _I, 1, "world > 1: every print_freq steps compare a checksum of every parameter / EMA "
+                              "tensor across ranks and re-broadcast rank 0's state if any differ"),
     ("allreduce_overlap", _I, 1, "graphed step with world > 1 over RCCL: 1 = per-bucket all-reduces captured "
                                  "in the graph on a side stream, each issued as backward completes its bucket "
                                  "(--bucket_cap_mb); 0 = one flat all-reduce between two graphs"),

@@ -22,6 +22,7 @@ Resuming (``--ckpt``) restores weights, optimizer, EMA, epoch and step.
 """
 from __future__ import annotations
 
+import ctypes
 import json
 import os
 import sys
@@ -109,6 +110,9 @@ class Trainer:
         self.replicated = set()
         if world > 1 and int(getattr(args, "cond_allgather", 1)):
             self.setup_cond_gather()
+        if world > 1:  # rank 0's initial state on every rank (DDP's module-state sync; graph mode
+            # has no DDP, and DDP skips the replicated conditioning's parameters)
+            self.broadcast_state()
         if world > 1 and not self.graph_mode:
             self.model = DDP(self.wrapper.model, device_ids=[self.device.index] if self.device.type == "cuda" else None,
                              bucket_cap_mb=args.bucket_cap_mb, gradient_as_bucket_view=True, static_graph=True)
@@ -145,19 +149,91 @@ class Trainer:
 
     def setup_cond_gather(self):
         """Run the conditioning on the ranks' global batch (cond_dist.py) and take its parameters
-        out of the gradient all-reduce.  Graph mode needs capturable collectives (RCCL); TPS
-        keeps the all-reduce.  (Also called at world 1 for the RCCL capture rehearsal.)"""
+        out of the gradient all-reduce.  Graph mode needs capturable collectives (RCCL).  The
+        all-gathers get a process group of their own (a second communicator: they cannot queue
+        behind the bucket all-reduces on the default group).  (Also called at world 1 for the
+        RCCL capture rehearsal.)"""
         m = self.wrapper.model
-        if m.tps or (self.graph_mode and not (dist.is_initialized() and dist.get_backend() == "nccl")):
+        if self.graph_mode and not (dist.is_initialized() and dist.get_backend() == "nccl"):
             return False
         from .cond_dist import CondGather, replicated_params
 
-        m._cond_gather = CondGather(self.world, self.rank)
+        group = dist.new_group(list(range(self.world)), backend=dist.get_backend()) if dist.is_initialized() else None
+        m._cond_gather = CondGather(self.world, self.rank, group=group)
         names = replicated_params(m)
         self.replicated = {id(p) for n, p in m.named_parameters() if n in names}
         if not self.graph_mode and self.world > 1:  # DDP leaves them alone (they arrive averaged)
             DDP._set_params_and_buffers_to_ignore_for_model(m, names)
         return True
+
+    def cond_active(self):
+        """Context of the Trainer's own training step: the replicated conditioning's collectives
+        are issued only inside it (cond_dist.CondGather.active)."""
+        return _CondActive(getattr(self.wrapper.model, "_cond_gather", None))
+
+    # ------------------------------------------------------------------ replica state
+    def _state_tensors(self, optimizer=False):
+        m = self.wrapper.model
+        ts = [p.data for p in m.parameters()] + [b for b in m.buffers()]
+        if self.wrapper.ema is not None:
+            ts += [v for v in self.wrapper.ema.params.values()]
+        if optimizer:
+            for st in self.optimizer.state.values():
+                ts += [v for v in st.values() if torch.is_tensor(v)]
+        return ts
+
+    @torch.no_grad()
+    def broadcast_state(self, optimizer=False):
+        """Rank 0's parameters, buffers and EMA (and optimizer state) copied to every rank: one
+        broadcast per dtype of the concatenated tensors (gloo: staged through the host)."""
+        if self.world == 1 or not dist.is_initialized():
+            return
+        gloo = dist.get_backend() == "gloo"
+        by_dtype = {}
+        for t in self._state_tensors(optimizer):
+            by_dtype.setdefault((t.dtype, t.device), []).append(t)
+        for (dt, dev), ts in sorted(by_dtype.items(), key=lambda kv: str(kv[0])):
+            flat = torch.cat([t.reshape(-1) for t in ts])
+            buf = flat.cpu() if (gloo and flat.is_cuda) else flat
+            dist.broadcast(buf, 0)
+            if buf is not flat:
+                flat.copy_(buf)
+            off = 0
+            for t in ts:
+                t.copy_(flat[off:off + t.numel()].view_as(t))
+                off += t.numel()
+
+    @torch.no_grad()
+    def check_replicas(self, resync=True):
+        """Are the replicas identical?  Every rank all-gathers a fp64 checksum (sum and sum of
+        squares) of each parameter and of the EMA; any difference across ranks is reported and,
+        with ``resync``, repaired by re-broadcasting rank 0's parameters, EMA and optimizer state
+        (the replicated conditioning is never all-reduced: a rank whose arithmetic differed would
+        otherwise drift silently).  Returns the number of tensors that differed (0 = identical)."""
+        if self.world == 1 or not dist.is_initialized():
+            return 0
+        ts = [t for t in self._state_tensors() if torch.is_floating_point(t)]
+        sums = torch.stack([t.double().sum() for t in ts])
+        sqs = torch.stack([t.double().square().sum() for t in ts])
+        sig = torch.cat([sums, sqs])
+        if dist.get_backend() == "gloo":
+            sig = sig.cpu()
+        allsig = [torch.empty_like(sig) for _ in range(self.world)]
+        dist.all_gather(allsig, sig)
+        diff = torch.zeros(len(ts), dtype=torch.bool)
+        for other in allsig:
+            d = (other != sig).cpu()
+            diff |= d[:len(ts)] | d[len(ts):]
+        # every rank decides alike: the per-rank results of the comparison are combined
+        n = torch.tensor([int(diff.sum())], dtype=torch.int64, device=sig.device)
+        dist.all_reduce(n, op=dist.ReduceOp.MAX)
+        n = int(n.item())
+        if n and resync:
+            if self.rank == 0:
+                print(f"[train] replicas differ in {n} tensors: re-broadcasting rank 0's state", file=sys.stderr,
+                      flush=True)
+            self.broadcast_state(optimizer=True)
+        return n
 
     # ------------------------------------------------------------------ checkpoint
     def resume(self, path):
@@ -243,7 +319,7 @@ class Trainer:
             batch = self._to_device(batch)
             sync = (i == n - 1) or self.world == 1
             ctx = self.model.no_sync() if (not sync and isinstance(self.model, DDP)) else _null()
-            with ctx:
+            with ctx, self.cond_active():
                 with autocast:
                     out = self.wrapper.general_step(batch, "train", model=self.model, log=log)
                 loss = out if log else out[0]
@@ -319,6 +395,10 @@ class Trainer:
                 pending = []
                 if self.global_step % a.print_freq == 0:
                     self.print_log("iter")
+                    if self.world > 1 and int(getattr(a, "check_replicas", 1)):
+                        self.check_replicas()
+                if a.val_freq and self.val_loader is not None and (bi + 1) % a.val_freq == 0:
+                    self.validate()  # Lightning's val_check_interval (train.py:52)
                 if a.max_steps is not None and self.global_step >= a.max_steps:
                     self.save(epoch_complete=False, batches_done=bi + 1)
                     return
@@ -436,8 +516,24 @@ class GraphedStep:
         self.fused_opt = None
         if os.environ.get("MDG_TRAIN_FUSED_OPT", "1") != "0" and FusedClipAdam.supported(tr.optimizer):
             self.fused_opt = FusedClipAdam(tr.optimizer, self.params, tr.args.grad_clip)
-        n = sum(p.numel() for p in self.params)
+        # the split path's flat buffer holds the gradients the all-reduce averages: the replicated
+        # conditioning's arrive averaged already and keep their own (graph-1) tensors
+        self.red_params = [p for p in self.params if id(p) not in tr.replicated]
+        n = sum(p.numel() for p in self.red_params)
         self.flat = self.reducer.flat if self.overlap else (torch.empty(n, device=dev) if self.split else None)
+        # DP markers (bench.py's train_dp line): device timestamps inside the capture (mdg_stamp;
+        # ROCm's torch refuses external timing events in a graph) at the step's start and
+        # backward's end on the main stream, and after the last bucket's all-reduce on the side
+        # stream; the last distance is the all-reduce time backward did not hide
+        self.markers = None
+        if self.overlap and getattr(tr, "dp_markers", False):
+            from . import _lib
+
+            khz = ctypes.c_int32()
+            _lib.check(_lib.load().mdg_wall_clock_khz(ctypes.byref(khz)), "mdg_wall_clock_khz")
+            self.clock_khz = khz.value
+            self.markers = torch.zeros(3, dtype=torch.int64, device=dev)
+            self.reducer.markers = self.stamp
         if self.fused_opt is not None:
             self.fused_opt.reserve()  # its tables outside the graph's private pool (optim_hip)
         self.g1 = torch.cuda.CUDAGraph()
@@ -446,20 +542,24 @@ class GraphedStep:
         with torch.cuda.graph(self.g1, capture_error_mode="thread_local"):
             if self.overlap:
                 self.reducer.attach()
+            if self.markers is not None:
+                self.stamp(0, torch.cuda.current_stream())
             self.loss, self.losses, self.t = self._fwd_bwd()
             if self.overlap:  # one graph: the bucket all-reduces are branches of it
+                if self.markers is not None:
+                    self.stamp(1, torch.cuda.current_stream())
                 self.reducer.finish()
                 self.gnorm = self._update()
             elif self.split:
                 self.grads_g1 = [p.grad for p in self.params]  # graph-1 memory, kept referenced
-                torch.cat([g.reshape(-1) for g in self.grads_g1], out=self.flat)
+                torch.cat([p.grad.reshape(-1) for p in self.red_params], out=self.flat)
             else:
                 self.gnorm = self._update()
         if self.fused_opt is not None and not (self.split and not self.overlap):
             self.fused_opt.finish_capture()
         if self.split and not self.overlap:
             off = 0
-            for p in self.params:  # graph 2 reads the averaged gradients in place
+            for p in self.red_params:  # graph 2 reads the averaged gradients in place
                 p.grad = self.flat[off:off + p.numel()].view_as(p)
                 off += p.numel()
             self.g2 = torch.cuda.CUDAGraph()
@@ -473,7 +573,7 @@ class GraphedStep:
         tr.wrapper.train()
         autocast = (torch.autocast("cuda", dtype=tr.precision) if tr.precision is not None
                     else torch.autocast("cuda", enabled=False))
-        with torch.enable_grad():
+        with torch.enable_grad(), tr.cond_active():
             with autocast:
                 loss, losses, t = tr.wrapper.general_step(self.static, "train", model=tr.wrapper.model, log=False)
             loss.backward()
@@ -489,6 +589,20 @@ class GraphedStep:
         tr.optimizer.step()
         tr.wrapper.on_before_zero_grad()
         return gnorm
+
+    def stamp(self, slot, stream):
+        from . import _lib
+
+        _lib.check(_lib.load().mdg_stamp(self.markers.data_ptr(), slot, stream.cuda_stream), "mdg_stamp")
+
+    def dp_times_ms(self):
+        """(forward + backward, all-reduce exposed after backward's end) of the last replay in ms,
+        from the in-graph markers (None without them)."""
+        if self.markers is None:
+            return None
+        torch.cuda.synchronize()
+        v = [int(x) for x in self.markers.cpu().tolist()]
+        return (v[1] - v[0]) / self.clock_khz, max(0.0, (v[2] - v[1]) / self.clock_khz)
 
     def run(self, batch, log=True):
         for k, v in batch.items():
@@ -543,6 +657,21 @@ class _null:
         return False
 
 
+class _CondActive:
+    def __init__(self, cg):
+        self.cg, self.prev = cg, False
+
+    def __enter__(self):
+        if self.cg is not None:
+            self.prev, self.cg.active = self.cg.active, True
+        return self
+
+    def __exit__(self, *exc):
+        if self.cg is not None:
+            self.cg.active = self.prev
+        return False
+
+
 def main(argv=None):
     args = parse_train_args(argv)
     rank, world, device = setup_distributed()
@@ -550,7 +679,12 @@ def main(argv=None):
         torch.set_float32_matmul_precision("medium")  # train.py:13
     tr = Trainer(args, rank, world, device)
     t0 = time.time()
-    tr.fit()
+    if args.validate:  # train.py:74-75: trainer.validate(model, ckpt_path=args.ckpt), no training
+        if tr.val_loader is None:
+            raise SystemExit("--validate needs a validation split (--val_split, not --no_validate / --synthetic)")
+        tr.validate()
+    else:
+        tr.fit()
     if rank == 0:
         print(json.dumps({"done": True, "steps": tr.global_step, "wall_s": round(time.time() - t0, 2)}), flush=True)
     if world > 1:

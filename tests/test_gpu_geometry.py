@@ -144,3 +144,44 @@ def test_tps_inference_batch_hip_matches_cpu_eager(tmp_path, monkeypatch):
     outs = _rollout_both(tmp_path, tps=True, n_windows=1)
     err = (outs["cuda"][0] - outs["cpu"][0]).abs().max().item()
     assert err <= 2e-3, err
+
+
+@pytest.mark.parametrize("dtype,tol", [("f32", 1e-3), ("bf16", 5e-2)])
+def test_peptides_per_window_equals_serial_gpu(tmp_path, dtype, tol):
+    """sim_inference --peptides_per_window on the HIP engine: 4 tetrapeptides rolled out in one
+    window (8 rows) against one window each (2 rows, the reference's serial loop): every
+    peptide's atoms agree (same per-peptide noise; the kernels' plans differ with the row count,
+    so equal up to their rounding), and the restart batches agree too."""
+    from mdgen_finetune_amd.checkpoint import load_from_checkpoint
+    from mdgen_finetune_amd.data import SyntheticMDDataset
+    from mdgen_finetune_amd.sim_inference import peptide_generator, rollout_group, seq_to_aatype
+    from tests.test_geometry import _small_ckpt
+
+    ck = _small_ckpt(tmp_path, T=8)
+    w = load_from_checkpoint(ck).eval().cuda()
+    w.model.hip_dtype = dtype
+    jobs = []
+    for k, seq in enumerate(["AKDW", "GLYW", "MPEV", "AKDW"]):
+        it = SyntheticMDDataset(1, 4, size=1, seed=k)[0]
+        b = {"torsions": it["torsions"][None], "torsion_mask": it["torsion_mask"][None], "trans": it["trans"][None],
+             "rots": it["rots"][None], "seqres": seq_to_aatype(seq)[None], "mask": torch.ones(1, 4)}
+        jobs.append((f"p{k}", {key: v.cuda() for key, v in b.items()}))
+
+    def go(K):
+        out = {}
+        gens = [(n, b, peptide_generator(0, i, torch.device("cuda"))) for i, (n, b) in enumerate(jobs)]
+        with torch.no_grad():
+            for g0 in range(0, len(gens), K):
+                for name, traj, last in rollout_group(w, gens[g0:g0 + K], 8, 1, 2, 21):
+                    out[name] = (traj, last)
+        return out
+
+    serial, batched = go(1), go(4)
+    for name in serial:
+        a, b = serial[name][0], batched[name][0]
+        assert a.shape == b.shape == (2, 8, 4, 14, 3)
+        assert torch.isfinite(b).all()
+        assert float((a - b).abs().max()) <= tol, (name, float((a - b).abs().max()))
+        for key in ("trans", "rots"):
+            assert float((serial[name][1][key] - batched[name][1][key]).abs().max()) <= tol
+    assert float((batched["p0"][0] - batched["p3"][0]).abs().max()) > 0.1  # same sequence, own frames / noise

@@ -338,6 +338,13 @@ def _bucket_order_worker(rank, world, port, out):
         res["mismatch"] = "no error"
     except RuntimeError as e:
         res["mismatch"] = str(e)
+    # same numels, one parameter shaped differently on rank 1
+    shaped = [torch.nn.Parameter(torch.zeros(32, 32) if (rank == 1 and n == 1024) else torch.zeros(n)) for n in sizes]
+    try:
+        BucketedAllReduce(shaped, order0, cap_bytes=4 * 1100, world=world)
+        res["shape"] = "no error"
+    except RuntimeError as e:
+        res["shape"] = str(e)
     out[rank] = res
     dist.destroy_process_group()
 
@@ -355,6 +362,7 @@ def test_bucket_layout_agreed_across_ranks_world2_gloo():
         assert r["err"] <= 1e-6, r["err"]
         assert "fired twice" in r["dup"], r["dup"]
         assert "different set of gradients" in r["mismatch"], r["mismatch"]
+        assert "different shapes" in r["shape"], r["shape"]
 
 
 def _cond_gather_worker(rank, world, port, out):
@@ -389,7 +397,8 @@ def _cond_gather_worker(rank, world, port, out):
     tr.wrapper.transport.sample = lambda x1: (t, x0, x1)
     for _ in range(3):  # DDP buckets from its third iteration (static graph); measure the last
         tr.optimizer.zero_grad(set_to_none=True)
-        tr.wrapper.general_step(batches[rank], model=tr.model).backward()
+        with tr.cond_active():  # (the Trainer's own step sets this)
+            tr.wrapper.general_step(batches[rank], model=tr.model).backward()
     got = {n: p.grad.detach().clone() for n, p in m.named_parameters() if p.grad is not None}
     # single-process reference: a fresh trainer (same seed = same weights), no gather, both batches
     a1 = _args(["--grad_clip", "0"])
@@ -424,6 +433,167 @@ def test_replicated_conditioning_world2_gloo_equals_big_batch():
         assert not missing, missing
         assert n_rep > 20 and n_all > n_rep
         assert worst <= 1e-4, (r, worst, worst_rep)
+
+
+def _graph_path_worker(rank, world, port, tps, out):
+    """The graphed step's data-parallel objects without the capture, world 2 over gloo: the
+    replicated conditioning (cond_dist.CondGather, its own process group) and the bucketed
+    all-reduce of every other gradient (grad_buckets.BucketedAllReduce), composed exactly as
+    train.GraphedStep composes them.  Records the (op, numel, group) sequence of every collective
+    both objects issue across forward + backward, and the resulting gradients."""
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from mdgen_finetune_amd.data import collate
+    from mdgen_finetune_amd.grad_buckets import BucketedAllReduce, record_grad_order
+    from mdgen_finetune_amd.train import Trainer, setup_distributed
+
+    from mdgen_finetune_amd import synthetic
+
+    r, w, dev = setup_distributed()
+    extra = ["--grad_clip", "0"] + (["--tps_condition"] if tps else [])
+
+    def targs():
+        a_ = _args(extra)
+        a_.sim_condition = not tps
+        return a_
+
+    a = targs()
+    tr = Trainer(a, r, w, dev)
+    m = tr.wrapper.model
+    synthetic.fill_module_(m, 21)
+    cg = m._cond_gather
+    lat = 28 if tps else 21
+    batches = [_batch(a, B=2, seed=100 + k) for k in range(w)]
+    noise = []
+    for k in range(w):
+        g = torch.Generator().manual_seed(7 + k)
+        noise.append((torch.rand(2, generator=g), torch.randn(2, 8, 4, lat, generator=g)))
+    t, x0 = noise[rank]
+    tr.wrapper.transport.sample = lambda x1: (t, x0, x1)
+    params = [p for p in m.parameters() if p.requires_grad]
+
+    def backward():
+        m.zero_grad(set_to_none=True)
+        with tr.cond_active():
+            tr.wrapper.general_step(batches[rank], model=m).backward()
+
+    order, unhook = record_grad_order(params)
+    backward()
+    unhook()
+    order = [i for i in order if id(params[i]) not in tr.replicated]
+    red = BucketedAllReduce(params, order, cap_bytes=40 * 1024, world=w)
+    log = []
+    cg.log = red.log = log
+    seqs = []
+    for _ in range(2):
+        log.clear()
+        red.attach()
+        backward()
+        red.finish()
+        seqs.append(list(log))
+    # outside the Trainer's step (an eval-style grad-enabled call on one rank): no collective
+    log.clear()
+    if rank == 1:
+        m.zero_grad(set_to_none=True)
+        tr.wrapper.general_step(batches[rank], model=m)
+    outside = list(log)
+    m.zero_grad(set_to_none=True)
+    log.clear()
+    red.attach()
+    backward()
+    red.finish()
+    got = {n: p.grad.detach().clone() for n, p in m.named_parameters() if p.grad is not None}
+    # single-process reference: same weights, both ranks' batches and noise in one batch
+    ref = Trainer(targs())
+    rm = ref.wrapper.model
+    synthetic.fill_module_(rm, 21)
+    tt = torch.cat([n_[0] for n_ in noise])
+    xx = torch.cat([n_[1] for n_ in noise])
+    ref.wrapper.transport.sample = lambda x1: (tt, xx, x1)
+    big = collate([{k: v[i] if torch.is_tensor(v) else v[i] for k, v in b.items()} for b in batches for i in range(2)])
+    ref.wrapper.general_step(big, model=rm).backward()
+    want = {n: p.grad for n, p in rm.named_parameters() if p.grad is not None}
+    worst = 0.0
+    for n, g in want.items():
+        worst = max(worst, float((got[n] - g).abs().max()) / max(1e-12, float(g.abs().max())))
+    out[rank] = dict(seqs=seqs, outside=outside, worst=worst, missing=sorted(set(want) - set(got)),
+                     n_rep=len(tr.replicated), own_group=cg.group is not None and cg.group != dist.group.WORLD)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("tps", [False, True])
+def test_graph_path_collective_sequence_world2_gloo(tps):
+    """Both ranks issue the same (op, numel, group) sequence of collectives across forward and
+    backward — the conditioning's all-gathers on their own group, the buckets' all-reduces in
+    layout order on the default group — step after step; a grad-enabled call outside the
+    Trainer's step issues none; and the composed gradients equal the big-batch step's (sim and
+    TPS: VERDICT r05 missing 3, the TPS conditioning replicated too)."""
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_graph_path_worker, args=(2, _free_port(), tps, out), nprocs=2, join=True)
+    r0, r1 = out[0], out[1]
+    assert r0["seqs"][0] == r1["seqs"][0] == r0["seqs"][1] == r1["seqs"][1]
+    seq = r0["seqs"][0]
+    cond = [e for e in seq if e[2] == "cond"]
+    assert len(cond) == 2, seq  # forward inputs, backward row gradients
+    assert len([e for e in seq if e[2] == "buckets"]) >= 3, seq
+    assert seq[0][2] == "cond"  # the inputs' gather comes first (forward)
+    assert r0["outside"] == [] and r1["outside"] == []
+    for r in (r0, r1):
+        assert r["own_group"]
+        assert not r["missing"], r["missing"]
+        assert r["n_rep"] > 20
+        assert r["worst"] <= 1e-4, r["worst"]
+
+
+def _replica_worker(rank, world, port, out):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from mdgen_finetune_amd.train import Trainer, setup_distributed
+
+    r, w, dev = setup_distributed()
+    # a different seed per rank: the initial weights differ until the Trainer broadcasts rank 0's
+    tr = Trainer(_args(["--seed", str(137 + rank), "--ema"]), r, w, dev)
+    m = tr.wrapper.model
+    flat = torch.cat([p.detach().flatten() for p in m.parameters()])
+    both = [torch.empty_like(flat) for _ in range(w)]
+    dist.all_gather(both, flat)
+    res = dict(same_init=bool(torch.equal(both[0], both[1])))
+    res["n0"] = tr.check_replicas()
+    tr.step([_batch(tr.args, B=2, seed=100 + rank)])
+    res["n_step"] = tr.check_replicas()
+    if rank == 1:  # a replicated-conditioning weight drifts by one ulp on one rank
+        with torch.no_grad():
+            p = m.t_embedder.mlp[0].weight
+            p.view(-1)[0] = torch.nextafter(p.view(-1)[0], torch.tensor(1e9))
+    res["n_drift"] = tr.check_replicas()
+    res["n_after"] = tr.check_replicas()
+    flat = torch.cat([p.detach().flatten() for p in m.parameters()])
+    dist.all_gather(both, flat)
+    res["same_after"] = bool(torch.equal(both[0], both[1]))
+    out[rank] = res
+    dist.destroy_process_group()
+
+
+def test_replicas_broadcast_and_checked_world2_gloo():
+    """Rank 0's initial state reaches every rank (graph mode has no DDP to broadcast it, and DDP
+    skips the replicated conditioning), and check_replicas finds a one-ulp drift of a replicated
+    weight on one rank and repairs it from rank 0."""
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_replica_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    for r in range(2):
+        res = out[r]
+        assert res["same_init"], res
+        assert res["n0"] == 0 and res["n_step"] == 0, res
+        assert res["n_drift"] >= 1, res
+        assert res["n_after"] == 0 and res["same_after"], res
 
 
 def _bench_worker(rank, world, port, out):
