@@ -151,7 +151,7 @@ class SyntheticMDDataset(torch.utils.data.Dataset):
         chain *= 3.8 / np.maximum(np.linalg.norm(rng.standard_normal((1, 3)), axis=-1), 1e-6)
         trans = chain[None] + np.cumsum(rng.standard_normal((T, L, 3)) * 0.1, 0)
         ang = rng.uniform(-np.pi, np.pi, (L, 7)) + np.cumsum(rng.standard_normal((T, L, 7)) * 0.1, 0)
-        torsions = np.stack([np.cos(ang), np.sin(ang)], -1)
+        torsions = np.stack([np.sin(ang), np.cos(ang)], -1)  # (sin, cos): atom37_to_torsions' order
         torsion_mask = np.zeros((L, 7), np.float32)
         torsion_mask[:, :3] = 1.0
         n_chi = rng.integers(0, 5, L)

@@ -18,8 +18,7 @@ def _write_peptide(path, seqres, F, seed):
     L = len(seqres)
     it = SyntheticMDDataset(F, L, size=1, seed=seed)[0]
     aa = torch.tensor([RESTYPES.index(c) for c in seqres])
-    # the dataset's torsions are (cos, sin); the geometry takes (sin, cos)
-    tors = it["torsions"].flip(-1)
+    tors = it["torsions"]  # (sin, cos), as the geometry and MDGenDataset take them
     atom14 = G.frames_torsions_to_atom14(it["rots"], it["trans"], tors, aa[None].expand(F, L))
     np.save(path, atom14.numpy().astype(np.float32))
     return it["rots"], it["trans"], tors
