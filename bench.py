@@ -49,7 +49,7 @@ import time
 import torch
 
 REPO = os.path.dirname(os.path.abspath(__file__))
-ROUND = "05"  # the round whose profiles/ files (summary, PMC traffic) this bench line cites
+ROUND = "06"  # the round whose profiles/ files (summary, PMC traffic) this bench line cites
 sys.path.insert(0, REPO)
 
 PEAK_TFLOPS = {"bf16": 2500.0, "f32": 157.3}   # MI355X dense MFMA (MI355X_MICROARCH.md:42-43)
@@ -155,7 +155,7 @@ def _traffic(kernel, B, T, L, dtype):
     """HBM bytes per launch from the committed PMC passes (profiles/traffic_r{ROUND}.json, this
     round's tools/roof_pmc.sh; shapes or kernels it lacks from the earlier rounds' files of the same
     kernels): FETCH_SIZE x2 + WRITE_SIZE per the gfx950 correction of MI355X_MICROARCH.md §HBM, or None."""
-    for rr in (ROUND, "04", "03"):
+    for rr in (ROUND, "05", "04", "03"):
         try:
             v = json.load(open(os.path.join(REPO, "profiles", f"traffic_r{rr}.json")))[kernel].get(f"B{B}_T{T}_L{L}_{dtype}")
         except Exception:

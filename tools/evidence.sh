@@ -14,6 +14,7 @@
 #   trainpmc  PMC / SQ passes of the training step
 #   rccl1     the training step with a world-1 RCCL group (in-graph bucket all-reduces + cond all-gathers)
 #   share2    bench.py --gpus 2 with both ranks on cuda:0 (the N-GPU launch path rehearsed; gloo)
+#   share2tr  the same under torch.distributed.run (the driver's N-GPU launch form)
 #   dopri5    the reference's default sampler
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -34,6 +35,7 @@ declare -A S=(
   [trainpmc]="r${R}_trainpmc|400|bash tools/train_pmc.sh"
   [rccl1]="r${R}_rccl1|300|python bench.py --train --train-rccl1 --batch 8 --no-cpu-baseline > gpurun_out/r${R}_bench_rccl1.json"
   [share2]="r${R}_share2|400|MDG_BENCH_SHARE_GPU=1 python bench.py --gpus 2 --steps 5 --warmup 2 > gpurun_out/r${R}_share2.json"
+  [share2tr]="r${R}_share2tr|400|MDG_BENCH_SHARE_GPU=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29611 bench.py --gpus 2 --steps 5 --warmup 2 > gpurun_out/r${R}_share2tr.json"
   [dopri5]="r${R}_dopri5|200|python bench.py --sampler dopri5 --steps 2 --warmup 1 > gpurun_out/r${R}_bench_dopri5.json"
 )
 args=()
