@@ -2085,6 +2085,160 @@ __global__ __launch_bounds__(kMlpThreads, 1) void mlp_rowln_kernel(const MlpArgs
 }
 
 // ---------------------------------------------------------------------------------------
+// Fused MLP with 256-wide hidden chunks and 64 x 64 fc1 wave tiles (round 6, MDG_MLP_HC=256).
+// The kernel above computes each 128-hidden chunk's H^T = W1c . xn^T as 8 wave tiles of 64
+// hidden x 32 tokens: 6 LDS fragment reads per 8 MFMAs, and per fc1 K-step of 64 the block reads
+// 96 KiB of fragments while its LDS-DMA ring writes 32 KiB (≈ 250 B/clk per CU against the
+// 512 cycles of MFMA work of the step, at LDS's 256 B/clk read limit), and the xn tile is
+// re-staged for every one of the 12 chunks.  Here a chunk is 256 hidden units: 8 wave tiles of
+// 64 hidden x 64 tokens (4 + 4 fragment reads per 16 MFMAs: a third fewer LDS bytes per fc1
+// FLOP), xn re-staged 6 times instead of 12, fc1 in K-steps of 32 (one 384-row image per slot:
+// 128 xn rows + 256 W1c rows = 24 KiB, the same size as an fc2 step's 384 W2 rows x 32), so
+// every step moves 3 LDS-DMA pieces per wave and the ring is 3 x 24 KiB; Hs [128][256] = 64 KiB.
+// acc1 is 64 VGPRs (was 32).  The K orders of fc1 (ascending 32-steps) and fc2 (ascending
+// hidden) are the other kernel's, so h and xn are bit-identical to it and to fc1-then-fc2.
+constexpr int kMlp2HC = 256, kMlp2Slot = 384 * 32;
+__host__ __device__ constexpr size_t mlp2_smem(int F) {
+  return (size_t)kMlpStages * kMlp2Slot * 2 + (size_t)128 * kMlp2HC * 2 + (size_t)F * 4;
+}
+
+template <int NCOL>
+__global__ __launch_bounds__(kMlpThreads, 1) void mlp_rowln256_kernel(const MlpArgs args) {
+  static_assert(NCOL == 384, "the ring slot holds 384 W2 rows");
+  constexpr int BM = 128, BK = 32, HC = kMlp2HC, STAGES = kMlpStages, SLOT = kMlp2Slot;
+  constexpr int WTN = NCOL / 4, NT = WTN / 16, NE = NCOL / 128, LDS_ST = NCOL + 4;
+  constexpr int NF1 = 12, NF2 = HC / BK, SPC = NF1 + NF2;  // steps per chunk: 12 fc1 + 8 fc2
+  static_assert((32 * LDS_ST + 6 * NCOL) * 4 <= STAGES * SLOT * 2, "epilogue stage + adaLN rows fit the ring");
+  typedef __attribute__((address_space(3))) void* lds_ptr_t;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const mdg_gemm_desc& q = args.f1;  // xn, W1, b1
+  const mdg_gemm_desc& p = args.f2;  // W2, b2 and the row-LN epilogue
+  bf16_t* ring = reinterpret_cast<bf16_t*>(smem);
+  bf16_t* Hs = ring + STAGES * SLOT;                    // [BM][HC]: 16-B chunk c of row r at c ^ (r & 15)
+  float* b1s = reinterpret_cast<float*>(Hs + BM * HC);  // [F]
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / 4, wn = wave % 4;    // fc2: 64 tokens x WTN outputs
+  const int wah = wave & 3, wat = wave >> 2;  // fc1: 64 hidden x 64 tokens
+  const int lr = lane & 15, lg = lane >> 4;
+  const int M = p.M, F = p.K;
+  const int NS = (F / HC) * SPC;
+  const int nwg = (M + BM - 1) / BM;
+  const int xcd = blockIdx.x & 7, loc = blockIdx.x >> 3, q8 = nwg >> 3, r8 = nwg & 7;
+  const int m0 = ((xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc) * BM;
+
+  for (int i = tid; i < F; i += kMlpThreads) b1s[i] = q.bias ? q.bias[i] : 0.f;
+  const int cswz = ((lane & 3) ^ ((-(lane >> 4)) & 3)) * 8;
+  const bf16_t* X = reinterpret_cast<const bf16_t*>(q.A);
+  const bf16_t* W1 = reinterpret_cast<const bf16_t*>(q.W);
+  const bf16_t* W2 = reinterpret_cast<const bf16_t*>(p.W);
+  // piece i (0..2) of wave w: slot rows 16 (3w + i) + lane / 4; fc1 step: rows < 128 are xn rows
+  // (pieces 0..7), the rest W1c rows; fc2 step: W2 rows
+  int xoff[3], woff[3];
+  bool isx[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int r = 16 * (3 * wave + i) + (lane >> 2);
+    isx[i] = r < BM;
+    xoff[i] = isx[i] ? min(m0 + r, M - 1) * q.lda + cswz : (r - BM) * q.ldw + cswz;
+    woff[i] = r * p.ldw + cswz;
+  }
+  auto issue = [&](int s) {
+    bf16_t* sl = ring + (s % STAGES) * SLOT;
+    const int j = s / SPC, t = s % SPC;
+    if (t < NF1) {
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const bf16_t* src = isx[i] ? X + (size_t)t * BK + xoff[i] : W1 + (size_t)j * HC * q.ldw + (size_t)t * BK + xoff[i];
+        __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(sl + 16 * (3 * wave + i) * BK), 16, 0, 0);
+      }
+    } else {
+      const bf16_t* base = W2 + j * HC + (t - NF1) * BK;
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+        __builtin_amdgcn_global_load_lds((const void*)(base + woff[i]), (lds_ptr_t)(sl + 16 * (3 * wave + i) * BK), 16,
+                                         0, 0);
+    }
+  };
+  const int ch = (lg ^ ((-(lr >> 2)) & 3)) * 8;
+  f32x4 acc2[4][NT], acc1[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc2[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc1[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int s0 = 0; s0 < STAGES - 1; ++s0)
+    if (s0 < NS) issue(s0);
+  // step s landed (step s + 1's 3 pieces stay in flight); then refill the slot every wave has
+  // finished reading (step s - 1's) with step s + 2
+  auto step_begin = [&](int s) {
+    if (s + 1 < NS) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // ring reads retired (see kRingWaitNote)
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (s + STAGES - 1 < NS) issue(s + STAGES - 1);
+    return ring + (s % STAGES) * SLOT;
+  };
+  for (int j = 0; j < NS / SPC; ++j) {
+    for (int t = 0; t < NF1; ++t) {
+      const bf16_t* sl = step_begin(j * SPC + t);
+      bf16x8 a[4], b[4];
+#pragma unroll
+      for (int hi = 0; hi < 4; ++hi) a[hi] = *reinterpret_cast<const bf16x8*>(sl + (BM + wah * 64 + hi * 16 + lr) * BK + ch);
+#pragma unroll
+      for (int ti = 0; ti < 4; ++ti) b[ti] = *reinterpret_cast<const bf16x8*>(sl + (wat * 64 + ti * 16 + lr) * BK + ch);
+#pragma unroll
+      for (int hi = 0; hi < 4; ++hi)
+#pragma unroll
+        for (int ti = 0; ti < 4; ++ti) acc1[hi][ti] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[hi], b[ti], acc1[hi][ti], 0, 0, 0);
+    }
+    // the chunk's fc1 is complete: + b1, GELU, bf16 -> Hs; restart acc1.  (Hs was last read by
+    // chunk j - 1's fc2 steps, which every wave finished before this chunk's first barrier.)
+    const float* b1c = b1s + j * HC;
+    f32x4 b1v[4];
+    {
+      const float* bp = b1c + wah * 64 + lg * 4;
+      lds_ld4x4_raw(bp, bp + 16, bp + 32, bp + 48, b1v[0], b1v[1], b1v[2], b1v[3]);
+    }
+#pragma unroll
+    for (int hi = 0; hi < 4; ++hi)
+#pragma unroll
+      for (int ti = 0; ti < 4; ++ti) {
+        const int hb = wah * 64 + hi * 16 + lg * 4, tok = wat * 64 + ti * 16 + lr;
+        bf16x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = (bf16_t)gelu_fast(acc1[hi][ti][r] + b1v[hi][r]);
+        *reinterpret_cast<bf16x4*>(Hs + tok * HC + (((hb >> 3) ^ (tok & 15)) * 8) + (hb & 7)) = o;
+        acc1[hi][ti] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // Hs complete before the next barrier
+    for (int kb = 0; kb < NF2; ++kb) {
+      const bf16_t* sl = step_begin(j * SPC + NF1 + kb);
+      bf16x8 a[4], b[NT];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = wm * 64 + i * 16 + lr;
+        a[i] = *reinterpret_cast<const bf16x8*>(Hs + row * HC + (((kb * 4 + lg) ^ (row & 15)) * 8));
+      }
+#pragma unroll
+      for (int jn = 0; jn < NT; ++jn) b[jn] = *reinterpret_cast<const bf16x8*>(sl + (wn * WTN + jn * 16 + lr) * BK + ch);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int jn = 0; jn < NT; ++jn) acc2[i][jn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[jn], acc2[i][jn], 0, 0, 0);
+    }
+  }
+  const float inv_rpm = 1.0f / (float)p.rows_per_mod;
+  float4 h4[2][NE];
+  rowln_load_band<NCOL>(p, RowsLinear{m0}, 0, h4);  // band 0's residual rows
+  rowln_fast_epilogue<NCOL>(p, acc2, h4, smem, RowsLinear{m0}, fdiv(m0, p.rows_per_mod, inv_rpm), inv_rpm);
+}
+
+// ---------------------------------------------------------------------------------------
 // Fused MLP, wave-specialised (round 3; large M, one 128-token tile per block, 8 waves).
 // The lock-step kernel above runs fc1 -> GELU -> fc2 in every wave, so the GELU's vector issue
 // (~3 800 cycles per wave and hidden chunk) sits on the MFMA critical path.  Here the two halves
@@ -2656,6 +2810,16 @@ static bool mlp_ws_on() {
   return on;
 }
 
+// MDG_MLP_HC=256: the one-pass fused MLP on 256-wide hidden chunks with 64 x 64 fc1 wave tiles
+// (mlp_rowln256_kernel, round 6; A/B knob)
+static bool mlp_hc256_on() {
+  static const bool on = [] {
+    const char* e = getenv("MDG_MLP_HC");
+    return e && atoi(e) == 256;
+  }();
+  return on;
+}
+
 // The out_proj prologue's envelope: r is the fast row-LN path's GEMM (bf16 PLAIN, K = N = 384,
 // rows_per_mod >= 128) whose h and xn outputs are exactly the MLP's residual and fc1 input, on
 // the MLP's rows, and the MLP runs in its one-pass form.
@@ -2674,7 +2838,8 @@ hipError_t mlp_fused_launch(const mdg_gemm_desc& f1, const mdg_gemm_desc& f2, hi
                           reinterpret_cast<const void*>(&mlp_rowln_kernel<384, true>),
                           reinterpret_cast<const void*>(&mlp_rowln_kernel<384, false, true>),
                           reinterpret_cast<const void*>(&mlp_rowln_kernel<384, true, false, true>),
-                          reinterpret_cast<const void*>(&mlp_ws_kernel<384>)}) {
+                          reinterpret_cast<const void*>(&mlp_ws_kernel<384>),
+                          reinterpret_cast<const void*>(&mlp_rowln256_kernel<384>)}) {
       hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       if (e != hipSuccess) return e;
     }
@@ -2703,6 +2868,10 @@ hipError_t mlp_fused_launch(const mdg_gemm_desc& f1, const mdg_gemm_desc& f2, hi
   }
   if (mlp_ws_on()) {
     hipLaunchKernelGGL((mlp_ws_kernel<384>), dim3(tiles), dim3(kWsThreads), kWsSmem, s, a);
+    return hipGetLastError();
+  }
+  if (mlp_hc256_on() && f1.N % kMlp2HC == 0 && mlp2_smem(f1.N) <= 160 * 1024) {
+    hipLaunchKernelGGL((mlp_rowln256_kernel<384>), dim3(tiles), dim3(kMlpThreads), mlp2_smem(f1.N), s, a);
     return hipGetLastError();
   }
   hipLaunchKernelGGL((mlp_rowln_kernel<384, false>), dim3(tiles), dim3(kMlpThreads), mlp_smem(f1.N), s, a);
