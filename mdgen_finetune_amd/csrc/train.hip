@@ -1168,6 +1168,352 @@ __global__ __launch_bounds__(kBW * 64) void attn_bwd_dkdv_bf16_kernel(
 }
 
 // ------------------------------------------------------------------------------------------
+// Wide heads (head_dim 32..63, 64-column planes) on MFMA (round 6; VERDICT r05 missing 4): the two
+// kernels above with every 64-column plane row held as two 32-column halves — the same swizzled
+// [row][32] LDS images, row / transposed reads and accumulator maps, 4 k-steps per product
+// instead of 2, dQ^T / dK^T / dV^T as two 32-row accumulators.  The plane's pad columns (k / v
+// carry 1.0 at column D) are zeroed in the register-resident fragments (q, dO in the dQ pass;
+// k, v in the dK / dV pass), so every product sums over the D live dims only, as the scalar wide
+// kernels do.  Grid and bias-partial slots are the scalar wide kernels': blockIdx.x = 256
+// queries (or keys), blockIdx.y = (sequence, head); the dQ block reduces its 8 waves' bias
+// partials into ONE slot, so mdg_attn_temporal_bwd_parts(generic 1) is unchanged.  A sequence
+// whose real keys are all padded gets dS_b = 0 exactly (P = [1, 0, ...]), as the scalar kernel.
+__device__ __forceinline__ void wide_frags(const bf16_t* row, bool ok, int D, int h, bf16x8 (&f)[4]) {
+#pragma unroll
+  for (int s4 = 0; s4 < 4; ++s4) {
+    const int d0 = 16 * s4 + 8 * h;
+    f[s4] = ok ? *reinterpret_cast<const bf16x8*>(row + d0) : zero8<bf16_t>();
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (d0 + j >= D) f[s4][j] = (bf16_t)0.f;
+  }
+}
+
+__global__ __launch_bounds__(kBW * 64) void attn_bwd_dq_bf16w_kernel(
+    const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dop, const float* __restrict__ lse,
+    const float* __restrict__ delta, const float* __restrict__ kbias, const float* __restrict__ kvb,
+    const float* __restrict__ rope, int rope_rows, bf16_t* __restrict__ dqkv, int ldq, float* __restrict__ bpart,
+    int T, int L, int H, int D, int BL, float qscale, float kscale) {
+  constexpr int DP = MDG_DP_WIDE, KC = kBKC, NTH = kBW * 64;
+  static_assert(KC * kDP / 8 == NTH, "one 16-B piece per half-image per thread per chunk");
+  __shared__ __attribute__((aligned(16))) bf16_t Ks[2][2][KC * kDP];  // [buffer][column half]
+  __shared__ __attribute__((aligned(16))) bf16_t Vs[2][2][KC * kDP];
+  __shared__ float kbs[2][KC];
+  __shared__ int kflag[2][KC / 64];
+  __shared__ float red[kBW][2 * DP];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
+  const int qb = blockIdx.x, sh = blockIdx.y, seq = sh / H, head = sh % H;
+  const int q = qb * (kBW * 32) + wave * 32 + r;
+  const bool live = q < T;
+  const size_t plane = (size_t)BL * H * T * DP;
+  const bf16_t* Qg = qkv + (size_t)sh * T * DP;
+  const bf16_t* Kg = Qg + plane;
+  const bf16_t* Vg = Qg + 2 * plane;
+  const float* kb = kbias + (size_t)seq * T;
+  // any real key in the sequence? (else the bias key takes all the weight and dS_b = 0 exactly)
+  int mine = 0;
+  for (int t = tid; t < T; t += NTH) mine |= kb[t] != -INFINITY;
+  const bool anyk = __syncthreads_or(mine) != 0;
+  bf16x8 qf[4], df[4];
+  wide_frags(Qg + (size_t)(live ? q : 0) * DP, live, D, h, qf);
+  wide_frags(dop + (size_t)sh * T * DP + (size_t)(live ? q : 0) * DP, live, D, h, df);
+  const float l2 = live ? lse[(size_t)sh * T + q] : INFINITY;
+  const float dl = live ? delta[(size_t)sh * T + q] : 0.f;
+  const float* bk = kvb + head * 2 * DP;
+  const float* bv = bk + DP;
+  float sb = 0.f, dpb = 0.f;
+#pragma unroll
+  for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int d = 16 * s4 + 8 * h + j;
+      sb += (float)qf[s4][j] * (d < D ? bk[d] : 0.f);
+      dpb += (float)df[s4][j] * (d < D ? bv[d] : 0.f);
+    }
+  sb += __shfl_xor(sb, 32, 64);
+  dpb += __shfl_xor(dpb, 32, 64);
+  const float pb = live ? __builtin_amdgcn_exp2f(sb - l2) : 0.f;
+  const float dsb = anyk ? pb * (dpb - dl) : 0.f;
+  f32x16 o[2];  // dQ^T: row d = 32 hh + (i&3) + 8(i>>2) + 4h, column = query r
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int d = 32 * hh + (i & 3) + 8 * (i >> 2) + 4 * h;
+      o[hh][i] = d < D ? dsb * bk[d] : 0.f;
+    }
+  {  // bias_k / bias_v gradient partials of this wave's 32 queries, then of the block's 8 waves
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) {
+      float gk[8], gv[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        gk[j] = dsb * (float)qf[s4][j] * kscale;
+        gv[j] = pb * (float)df[s4][j];
+      }
+#pragma unroll
+      for (int off = 1; off < 32; off <<= 1)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          gk[j] += __shfl_xor(gk[j], off, 64);
+          gv[j] += __shfl_xor(gv[j], off, 64);
+        }
+      if (r == 0)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          red[wave][16 * s4 + 8 * h + j] = gk[j];
+          red[wave][DP + 16 * s4 + 8 * h + j] = gv[j];
+        }
+    }
+  }
+
+  const int srow = tid >> 2, spc = tid & 3;
+  u32x4 kreg[2], vreg[2];
+  float kbreg = 0.f;
+  auto gload = [&](int c) {
+    const int key = c * KC + srow;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      kreg[hh] = vreg[hh] = u32x4{0u, 0u, 0u, 0u};
+      if (key < T) {
+        kreg[hh] = *reinterpret_cast<const u32x4*>(Kg + (size_t)key * DP + 32 * hh + spc * 8);
+        vreg[hh] = *reinterpret_cast<const u32x4*>(Vg + (size_t)key * DP + 32 * hh + spc * 8);
+      }
+    }
+    if (tid < KC) {
+      const int kk = c * KC + tid;
+      kbreg = (kk < T) ? kb[kk] : -INFINITY;
+    }
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      *reinterpret_cast<u32x4*>(&Ks[buf][hh][img_off(srow, spc * 8)]) = kreg[hh];
+      *reinterpret_cast<u32x4*>(&Vs[buf][hh][img_off(srow, spc * 8)]) = vreg[hh];
+    }
+    if (tid < KC) {
+      kbs[buf][tid] = kbreg;
+      const bool any = __any(kbreg != 0.f);
+      if (lane == 0) kflag[buf][wave] = any ? 1 : 0;
+    }
+  };
+  const int nchunks = (T + KC - 1) / KC;
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  for (int c = 0; c < nchunks; ++c) {
+    const int cur = c & 1;
+    if (c + 1 < nchunks) gload(c + 1);
+    int mflag = 0;
+#pragma unroll
+    for (int f = 0; f < KC / 64; ++f) mflag |= kflag[cur][f];
+#pragma unroll
+    for (int sub = 0; sub < KC / 64; ++sub) {
+      const bf16_t* Kc[2] = {Ks[cur][0] + sub * 64 * kDP, Ks[cur][1] + sub * 64 * kDP};
+      const bf16_t* Vc[2] = {Vs[cur][0] + sub * 64 * kDP, Vs[cur][1] + sub * 64 * kDP};
+      const float* kbsub = kbs[cur] + sub * 64;
+      f32x16 sacc[2], pacc[2];
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sacc[kt][i] = pacc[kt][i] = 0.f;
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+          sacc[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(img_row(Kc[s4 >> 1], kt * 32 + r, s4 & 1, h), qf[s4],
+                                                            sacc[kt], 0, 0, 0);
+          pacc[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(img_row(Vc[s4 >> 1], kt * 32 + r, s4 & 1, h), df[s4],
+                                                            pacc[kt], 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          float sv = sacc[kt][i] - l2;
+          if (mflag) sv += kbsub[kt * 32 + (i & 3) + 8 * (i >> 2) + 4 * h];
+          sacc[kt][i] = __builtin_amdgcn_exp2f(sv) * (pacc[kt][i] - dl);  // dS^T
+        }
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          bf16x8 dsf;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) dsf[j] = (bf16_t)sacc[kt][8 * s2 + j];
+#pragma unroll
+          for (int hh = 0; hh < 2; ++hh)
+            o[hh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(img_tr(Kc[hh], kt * 32, s2, lane), dsf, o[hh], 0, 0, 0);
+        }
+    }
+    if (c + 1 < nchunks) lstore(cur ^ 1);
+    __syncthreads();
+  }
+  if (live) {
+    const int b = seq / L, l = seq % L, half = D >> 1;
+    const size_t tok = ((size_t)b * T + q) * L + l;
+    bf16_t* out = dqkv + tok * ldq + head * D;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d0 = 32 * hh + 8 * g4 + 4 * h;
+        if (d0 < D) {  // (D % 4 == 0)
+          float a0 = o[hh][4 * g4] * qscale, a1 = o[hh][4 * g4 + 1] * qscale;
+          float a2 = o[hh][4 * g4 + 2] * qscale, a3 = o[hh][4 * g4 + 3] * qscale;
+          if (rope) {
+            rope_inv(a0, a1, rope, rope_rows, half, q, d0 >> 1);
+            rope_inv(a2, a3, rope, rope_rows, half, q, (d0 >> 1) + 1);
+          }
+          st4<bf16_t>(out + d0, a0, a1, a2, a3);
+        }
+      }
+  }
+  // the block's bias slot (the scalar wide kernel's layout: slot = seq * gridDim.x + blockIdx.x)
+  if (tid < 2 * DP) {
+    const int d = tid & (DP - 1);
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < kBW; ++w) v += red[w][tid];
+    const size_t slot = (size_t)seq * gridDim.x + blockIdx.x;
+    bpart[((size_t)head * BL * gridDim.x + slot) * 2 * DP + tid] = d < D ? v : 0.f;
+  }
+}
+
+__global__ __launch_bounds__(kBW * 64) void attn_bwd_dkdv_bf16w_kernel(
+    const bf16_t* __restrict__ qkv, const bf16_t* __restrict__ dop, const float* __restrict__ lse,
+    const float* __restrict__ delta, const float* __restrict__ kbias, const float* __restrict__ rope, int rope_rows,
+    bf16_t* __restrict__ dqkv, int ldq, int T, int L, int H, int D, int BL, float kscale) {
+  constexpr int DP = MDG_DP_WIDE, QC = kBKC, NTH = kBW * 64;
+  static_assert(QC * kDP / 8 == NTH, "one 16-B piece per half-image per thread per chunk");
+  __shared__ __attribute__((aligned(16))) bf16_t Qs[2][2][QC * kDP];
+  __shared__ __attribute__((aligned(16))) bf16_t Ds[2][2][QC * kDP];
+  __shared__ __attribute__((aligned(16))) float ls[2][QC];
+  __shared__ __attribute__((aligned(16))) float dls[2][QC];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
+  const int kbk = blockIdx.x, sh = blockIdx.y, seq = sh / H, head = sh % H;
+  const int key = kbk * (kBW * 32) + wave * 32 + r;
+  const bool live = key < T;
+  const size_t plane = (size_t)BL * H * T * DP;
+  const bf16_t* Qg = qkv + (size_t)sh * T * DP;
+  const bf16_t* dOg = dop + (size_t)sh * T * DP;
+  bf16x8 kf[4], vf[4];
+  wide_frags(Qg + plane + (size_t)(live ? key : 0) * DP, live, D, h, kf);
+  wide_frags(Qg + 2 * plane + (size_t)(live ? key : 0) * DP, live, D, h, vf);
+  const float kbl = live ? kbias[(size_t)seq * T + key] : -INFINITY;
+  f32x16 dk[2], dv[2];  // dK^T / dV^T: row d = 32 hh + (i&3) + 8(i>>2) + 4h, column = key r
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) dk[hh][i] = dv[hh][i] = 0.f;
+
+  const int srow = tid >> 2, spc = tid & 3;
+  u32x4 qreg[2], dreg[2];
+  float lreg = 0.f, dlreg = 0.f;
+  auto gload = [&](int c) {
+    const int qq = c * QC + srow;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      qreg[hh] = dreg[hh] = u32x4{0u, 0u, 0u, 0u};
+      if (qq < T) {
+        qreg[hh] = *reinterpret_cast<const u32x4*>(Qg + (size_t)qq * DP + 32 * hh + spc * 8);
+        dreg[hh] = *reinterpret_cast<const u32x4*>(dOg + (size_t)qq * DP + 32 * hh + spc * 8);
+      }
+    }
+    if (tid < QC) {
+      const int q2 = c * QC + tid;
+      lreg = (q2 < T) ? lse[(size_t)sh * T + q2] : INFINITY;
+      dlreg = (q2 < T) ? delta[(size_t)sh * T + q2] : 0.f;
+    }
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      *reinterpret_cast<u32x4*>(&Qs[buf][hh][img_off(srow, spc * 8)]) = qreg[hh];
+      *reinterpret_cast<u32x4*>(&Ds[buf][hh][img_off(srow, spc * 8)]) = dreg[hh];
+    }
+    if (tid < QC) {
+      ls[buf][tid] = lreg;
+      dls[buf][tid] = dlreg;
+    }
+  };
+  const int nchunks = (T + QC - 1) / QC;
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  for (int c = 0; c < nchunks; ++c) {
+    const int cur = c & 1;
+    if (c + 1 < nchunks) gload(c + 1);
+#pragma unroll
+    for (int sub = 0; sub < QC / 64; ++sub) {
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) {
+        const int base = sub * 64 + qt * 32;
+        f32x16 sacc, pacc;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sacc[i] = pacc[i] = 0.f;
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+          sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(img_row(Qs[cur][s4 >> 1], base + r, s4 & 1, h), kf[s4], sacc,
+                                                         0, 0, 0);
+          pacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(img_row(Ds[cur][s4 >> 1], base + r, s4 & 1, h), vf[s4], pacc,
+                                                         0, 0, 0);
+        }
+        // P and dS of this k-step's 8 queries straight into the bf16 operands (no fp32 arrays of
+        // all 16: the two 32-row accumulator pairs leave no room for them)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          bf16x8 pf, dsf;
+#pragma unroll
+          for (int g = 0; g < 2; ++g) {
+            const int g4 = 2 * s2 + g;
+            const float4 l4 = *reinterpret_cast<const float4*>(&ls[cur][base + 8 * g4 + 4 * h]);
+            const float4 d4 = *reinterpret_cast<const float4*>(&dls[cur][base + 8 * g4 + 4 * h]);
+            const float lv[4] = {l4.x, l4.y, l4.z, l4.w}, dv4[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int i = 4 * g4 + e;
+              const float p = __builtin_amdgcn_exp2f(sacc[i] + kbl - lv[e]);
+              pf[4 * g + e] = (bf16_t)p;
+              dsf[4 * g + e] = (bf16_t)(p * (pacc[i] - dv4[e]));
+            }
+          }
+#pragma unroll
+          for (int hh = 0; hh < 2; ++hh) {
+            dv[hh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(img_tr(Ds[cur][hh], base, s2, lane), pf, dv[hh], 0, 0, 0);
+            dk[hh] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(img_tr(Qs[cur][hh], base, s2, lane), dsf, dk[hh], 0, 0, 0);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);  // one 32-query tile at a time: bounded temporaries
+      }
+    }
+    if (c + 1 < nchunks) lstore(cur ^ 1);
+    __syncthreads();
+  }
+  if (live) {
+    const int b = seq / L, l = seq % L, half = D >> 1, C = H * D;
+    const size_t tok = ((size_t)b * T + key) * L + l;
+    bf16_t* ok = dqkv + tok * ldq + C + head * D;
+    bf16_t* ov = dqkv + tok * ldq + 2 * C + head * D;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d0 = 32 * hh + 8 * g4 + 4 * h;
+        if (d0 < D) {
+          float a0 = dk[hh][4 * g4] * kscale, a1 = dk[hh][4 * g4 + 1] * kscale;
+          float a2 = dk[hh][4 * g4 + 2] * kscale, a3 = dk[hh][4 * g4 + 3] * kscale;
+          if (rope) {
+            rope_inv(a0, a1, rope, rope_rows, half, key, d0 >> 1);
+            rope_inv(a2, a3, rope, rope_rows, half, key, (d0 >> 1) + 1);
+          }
+          st4<bf16_t>(ok + d0, a0, a1, a2, a3);
+          st4<bf16_t>(ov + d0, dv[hh][4 * g4], dv[hh][4 * g4 + 1], dv[hh][4 * g4 + 2], dv[hh][4 * g4 + 3]);
+        }
+      }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // Fused single-pass backward: one block per (sequence, head), 8 waves x 32 keys = a 256-key
 // block, the key blocks of the sequence in turn (T > 256: several passes).  Per 64-query chunk
 // (Q / dO images double-buffered through registers, as the dK/dV kernel stages them):
@@ -1503,6 +1849,14 @@ static bool attn_bwd_fold_on() {
   return on;
 }
 
+static bool attn_bwd_wide_mfma_on() {  // MDG_ATTN_BWD_WIDE_MFMA=0: the scalar kernels at DP 64 (bf16)
+  static const bool v = [] {
+    const char* e = getenv("MDG_ATTN_BWD_WIDE_MFMA");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
 static bool attn_bwd_wide2_on() {  // MDG_ATTN_BWD_WIDE2=0: the one-thread-per-row scalar kernels at DP 64
   static const bool v = [] {
     const char* e = getenv("MDG_ATTN_BWD_WIDE2");
@@ -1540,7 +1894,19 @@ hipError_t attn_temporal_bwd_launch(int dtype, int B, int T, int L, int H, int D
   // the scalar kernels: f32, generic == 1, and every wide head (head_dim 32..63, 64-column planes;
   // the MFMA kernels' LDS images are 32 columns wide)
   if (dtype == MDG_F32 || generic == 1 || D >= kDP) {
-    if (D >= kDP && attn_bwd_wide2_on()) {  // the two-column-half kernels
+    if (dtype == MDG_BF16 && D >= kDP && attn_bwd_wide_mfma_on()) {  // the wide MFMA kernels (round 6)
+      hipLaunchKernelGGL((attn_bwd_prep_kernel<bf16_t, MDG_DP_WIDE>), pgrid, dim3(256), 0, s, B, T, L, H, D,
+                         (const bf16_t*)o, (const bf16_t*)o_lo, (const bf16_t*)dout, (bf16_t*)dop, delta);
+      if (hipError_t e = hipGetLastError()) return e;
+      const dim3 mgrid((T + kBW * 32 - 1) / (kBW * 32), BL * H);
+      hipLaunchKernelGGL(attn_bwd_dq_bf16w_kernel, mgrid, dim3(kBW * 64), 0, s, (const bf16_t*)qkv_t, (const bf16_t*)dop,
+                         lse, delta, kbias, kvb, rope, rope_rows, (bf16_t*)dqkv, ldq, bpart, T, L, H, D, BL, qscale,
+                         kscale);
+      if (hipError_t e = hipGetLastError()) return e;
+      hipLaunchKernelGGL(attn_bwd_dkdv_bf16w_kernel, mgrid, dim3(kBW * 64), 0, s, (const bf16_t*)qkv_t,
+                         (const bf16_t*)dop, lse, delta, kbias, rope, rope_rows, (bf16_t*)dqkv, ldq, T, L, H, D, BL,
+                         kscale);
+    } else if (D >= kDP && attn_bwd_wide2_on()) {  // the two-column-half kernels
       dim3 wgrid((T + kWideRows - 1) / kWideRows, BL * H);
 #define MDG_WIDE(CTT)                                                                                                \
   hipLaunchKernelGGL((attn_bwd_prep_kernel<CTT, MDG_DP_WIDE>), pgrid, dim3(256), 0, s, B, T, L, H, D, (const CTT*)o, \

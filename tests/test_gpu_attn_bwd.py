@@ -95,9 +95,26 @@ def test_temporal_attention_backward_multi_chunk(dtype, T, n_pad):
 @pytest.mark.parametrize("H,D,T,n_pad", [(8, 32, 129, 5), (8, 48, 300, -1), (6, 60, 40, 3)])
 def test_temporal_attention_backward_wide_heads(dtype, H, D, T, n_pad):
     """head_dim 32..63 (--embed_dim 256 --mha_heads 8 and the like; mha.py:96-102 takes any
-    embed_dim // num_heads): 64-column planes (MDG_HEAD_STRIDE), the scalar kernels (generic 1,
-    the only route for these heads), O's bf16 residual from the wide forward kernel."""
+    embed_dim // num_heads): 64-column planes (MDG_HEAD_STRIDE), generic 1 (the only value these
+    heads take): bf16 on the wide MFMA kernels (round 6: each 64-column row as two 32-column
+    halves, P / dS rounded to bf16 as in the head_dim-24 kernels), f32 on the scalar ones; O's
+    bf16 residual from the wide forward kernel."""
     _run_bwd(dtype, T, n_pad, 1, H=H, D=D)
+
+
+@pytest.mark.parametrize("H,D,T,n_pad", [(8, 32, 257, 9), (6, 60, 129, -1)])
+def test_temporal_attention_backward_wide_heads_scalar_route(H, D, T, n_pad):
+    """The bf16 wide heads' scalar kernels (MDG_ATTN_BWD_WIDE_MFMA=0, the round-5 route) stay
+    correct: run in a child process, since the knob is read once per process."""
+    import subprocess
+    import sys
+
+    code = ("import sys; sys.path.insert(0, '.'); from tests.test_gpu_attn_bwd import _run_bwd; "
+            f"_run_bwd('bf16', {T}, {n_pad}, 1, H={H}, D={D}); print('ok')")
+    r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, MDG_ATTN_BWD_WIDE_MFMA="0"),
+                       cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))), capture_output=True,
+                       text=True, timeout=180)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
 
 
 def test_temporal_attention_backward_wide_heads_refuses_mfma_variants():

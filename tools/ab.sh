@@ -9,6 +9,7 @@
 # AB_TESTS (a pytest -k filter over the kernel / parity / training tests) runs once per variant
 # first and stops the script on a failure.
 #   AB_WHAT=train AB_A="" AB_B="MDG_ATTN_BWD_FOLD=0" bash tools/ab.sh
+#   AB_ARGS is evaluated: AB_ARGS="--model-args '--embed_dim 256 --mha_heads 8'" passes one argument
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -19,12 +20,12 @@ run_variant() {  # $1 = A | B
   if [ "$V" = B ] && [ "${AB_B_LIB:-0}" = 1 ]; then E="$E MDG_LIB_PATH=$PWD/ablib/old.so"; fi
   case $WHAT in
   infer)
-    env $E timeout -k 10 300 python -u bench.py --steps ${AB_STEPS:-5} --warmup 2 --no-cpu-baseline --no-f32-line \
-      --sweep-batches "" ${AB_ARGS:-} > gpurun_out/ab_$V.json 2> gpurun_out/ab_$V.err || { tail -5 gpurun_out/ab_$V.err; return 1; }
+    eval "env $E timeout -k 10 300 python -u bench.py --steps ${AB_STEPS:-5} --warmup 2 --no-cpu-baseline --no-f32-line \
+      --sweep-batches '' ${AB_ARGS:-}" > gpurun_out/ab_$V.json 2> gpurun_out/ab_$V.err || { tail -5 gpurun_out/ab_$V.err; return 1; }
     python -c "import json;d=json.loads([l for l in open('gpurun_out/ab_$V.json') if l.startswith('{')][-1]);print('$V [$E]', d['value'], d['us_per_denoise_step'], [r['avg_launch_us'] for r in [d['roofline']]+(d['roofline_more'] or [])] if d.get('roofline') else '')" ;;
   train)
-    env $E timeout -k 10 300 python -u bench.py --train --batch 8 --steps ${AB_STEPS:-10} --warmup 2 --no-cpu-baseline \
-      ${AB_ARGS:-} > gpurun_out/ab_$V.json 2> gpurun_out/ab_$V.err || { tail -5 gpurun_out/ab_$V.err; return 1; }
+    eval "env $E timeout -k 10 300 python -u bench.py --train --batch 8 --steps ${AB_STEPS:-10} --warmup 2 --no-cpu-baseline \
+      ${AB_ARGS:-}" > gpurun_out/ab_$V.json 2> gpurun_out/ab_$V.err || { tail -5 gpurun_out/ab_$V.err; return 1; }
     python -c "import json;d=json.loads([l for l in open('gpurun_out/ab_$V.json') if l.startswith('{')][-1]);print('$V [$E]', d['ms_per_step'], d['value'])" ;;
   micro)
     echo "== $V [$E]"; env $E timeout -k 10 120 python $AB_MICRO 2>&1 | grep -v amdgpu.ids | tail -${AB_LINES:-4} ;;
