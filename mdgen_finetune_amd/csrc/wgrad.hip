@@ -17,6 +17,8 @@
 // 4 waves, each a 64 x 64 quarter (2 x 2 tiles of 32 x 32, 64 accumulator VGPRs).
 //
 // fp32 (the parity path): a plain 64 x 64 LDS-tiled FMA kernel, same split / reduce.
+#include <utility>
+
 #include "common.h"
 
 namespace mdg {
@@ -188,6 +190,148 @@ __global__ __launch_bounds__(kWgThreads, 2) void wgrad_bf16_kernel(const WgArgs 
       for (int r = 0; r < 16; ++r) {
         const int m = m0 + 64 * wm + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
         if (m < a.M && k < a.K) P[(size_t)m * a.ldp + k] = acc[t][u][r];
+      }
+    }
+}
+
+// Register-staged variant (round 6, MDG_WGRAD_VST = NR in 2..4): the same tile, images, swizzle
+// and MFMA sequence, but each step's 4 pieces per wave come global -> VGPRs (global_load_dwordx4
+// from the swizzled source address) -> ds_write_b128 at the piece's lane-linear LDS position (the
+// place LDS-DMA would write them), NR steps ahead in NR register sets, into a 2-slot LDS ring.
+// The DMA stream fills LDS at ≈ 16 B/clk per CU (tools/ubench/l2lds.hip), plain 16-B loads at
+// ≈ 46–63; this kernel moves 16 KiB per 32-token step for 512 MFMA cycles per SIMD (64 B/clk
+// per CU at the full MFMA rate), and its counters show 66 % of wave cycles parked.  Same K order,
+// same results bit for bit.
+template <typename F, int... I>
+__device__ __forceinline__ void wg_unroll(std::integer_sequence<int, I...>, F&& f) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+
+template <int NR>
+__global__ __launch_bounds__(kWgThreads, 2) void wgrad_bf16_vst_kernel(const WgArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  bf16_t* ring = reinterpret_cast<bf16_t*>(smem);  // [2][kWgSlot]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int mt, kt, z;
+  wg_tile_of(a.gx, a.gy, a.gz, mt, kt, z);
+  const int m0 = mt * kWgTile, k0 = kt * kWgTile;
+  const int nbeg = z * a.chunk;
+  const int nsteps = (min(a.N, nbeg + a.chunk) - nbeg) / kWgBK;
+  const bf16_t* DY = reinterpret_cast<const bf16_t*>(a.dy);
+  const bf16_t* X = reinterpret_cast<const bf16_t*>(a.x);
+  const int r_lo = lane >> 4, cpos = lane & 15;
+  size_t src[4];
+  int dst[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int img = j >> 1, rb = 4 * (2 * wave + (j & 1)), r = rb + r_lo;
+    const int lim = img ? a.K : a.M;
+    const int col = min((img ? k0 : m0) + 8 * (cpos ^ wg_swz(r)), lim - 8);
+    src[j] = (size_t)(nbeg + r) * (img ? a.ldx : a.ldy) + col;
+    dst[j] = img * kWgImg + rb * kWgTile + 8 * lane;  // this lane's 16 B of the piece
+  }
+  u32x4 R[NR][4];
+  auto load = [&](int st, u32x4(&rr)[4]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const bf16_t* base = (j >> 1) ? X : DY;
+      const size_t step = (size_t)st * kWgBK * ((j >> 1) ? a.ldx : a.ldy);
+      rr[j] = *reinterpret_cast<const u32x4*>(base + src[j] + step);
+    }
+  };
+  auto commit = [&](int st, const u32x4(&rr)[4]) __attribute__((always_inline)) {
+    bf16_t* sl = ring + (st & 1) * kWgSlot;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) *reinterpret_cast<u32x4*>(sl + dst[j]) = rr[j];
+  };
+  // wait until at most `ahead` later steps' loads (4 per step) are still in flight
+  auto vm_wait_steps = [&](int ahead) __attribute__((always_inline)) {
+    if (ahead >= 3) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else if (ahead == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+  const int wm = wave >> 1, wk = wave & 1;
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[t][u][i] = 0.f;
+  const bool csum = a.cpart != nullptr && kt == 0 && wk == 0;
+  float cs[2] = {0.f, 0.f};
+  // prologue: steps 0 .. NR - 1 in flight; step 0 written to slot 0; step NR into the freed set
+#pragma unroll
+  for (int k = 0; k < NR; ++k)
+    if (k < nsteps) load(k, R[k]);
+  vm_wait_steps(min(NR - 1, nsteps - 1));
+  if (nsteps > 0) commit(0, R[0]);
+  if (NR < nsteps) load(NR, R[0]);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  // step s (slot s & 1 complete): its MFMAs; then step s + 1's registers (set (s + 1) % NR, the
+  // oldest loads in flight) into slot (s + 1) & 1 — last read in step s - 1, before the barrier
+  // that ended it — and step s + 1 + NR's loads into that set; barrier
+  for (int s0 = 0; s0 < nsteps; s0 += NR) {
+    // the NR steps of a round spelled out with u a compile-time constant, so each knows its
+    // register set (an indexed register array would go to scratch)
+    wg_unroll(std::make_integer_sequence<int, NR>{}, [&](auto U) __attribute__((always_inline)) {
+      constexpr int u = decltype(U)::value;
+      const int s = s0 + u;
+      if (s < nsteps) {
+        const bf16_t* A = ring + (s & 1) * kWgSlot;
+        const bf16_t* B = A + kWgImg;
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          bf16x8 af[2], bfr[2];
+#pragma unroll
+          for (int t = 0; t < 2; ++t) af[t] = wg_frag(A, 64 * wm + 32 * t, s2, lane);
+#pragma unroll
+          for (int v = 0; v < 2; ++v) bfr[v] = wg_frag(B, 64 * wk + 32 * v, s2, lane);
+#pragma unroll
+          for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int v = 0; v < 2; ++v) acc[t][v] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[t], bfr[v], acc[t][v], 0, 0, 0);
+          if (csum) {
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+              float vs = 0.f;
+#pragma unroll
+              for (int j = 0; j < 8; ++j) vs += (float)af[t][j];
+              cs[t] += vs;
+            }
+          }
+        }
+        if (s + 1 < nsteps) {
+          constexpr int nxt = (u + 1) % NR;
+          vm_wait_steps(min(NR - 1, nsteps - 2 - s));
+          commit(s + 1, R[nxt]);
+          if (s + 1 + NR < nsteps) load(s + 1 + NR, R[nxt]);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __syncthreads();
+      }
+    });
+  }
+  if (csum) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const float v = cs[t] + __shfl_xor(cs[t], 32, 64);
+      const int m = m0 + 64 * wm + 32 * t + lane;
+      if (lane < 32 && m < a.M) a.cpart[(size_t)z * a.M + m] = v;
+    }
+  }
+  float* P = a.part + (size_t)z * a.M * a.ldp;
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int v = 0; v < 2; ++v) {
+      const int k = k0 + 64 * wk + 32 * v + (lane & 31);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + 64 * wm + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (m < a.M && k < a.K) P[(size_t)m * a.ldp + k] = acc[t][v][r];
       }
     }
 }
@@ -470,6 +614,14 @@ static int wgrad_stages() {
   }();
   return v;
 }
+static int wgrad_vst() {  // MDG_WGRAD_VST = 2..4: the register-staged kernel with that many steps in flight
+  static const int v = [] {
+    const char* e = getenv("MDG_WGRAD_VST");
+    const int n = e ? atoi(e) : 0;
+    return (n >= 2 && n <= 4) ? n : 0;
+  }();
+  return v;
+}
 static int wgrad_target_blocks() {
   static const int v = [] {
     const char* e = getenv("MDG_WGRAD_BLOCKS");
@@ -559,8 +711,11 @@ hipError_t wgrad_launch(int dtype, int N, int M, int K, const void* dy, int ldy,
       a.gy = (K + 127) / 128;
       a.gz = p.S;
       const dim3 grid((unsigned)(a.gx * a.gy * a.gz));
-      const int ns = wgrad_stages();
-      if (ns == 5) hipLaunchKernelGGL(wgrad_bf16_kernel<5>, grid, dim3(kWgThreads), 5 * kWgSlot * 2, s, a);
+      const int ns = wgrad_stages(), vst = wgrad_vst();
+      if (vst == 2) hipLaunchKernelGGL(wgrad_bf16_vst_kernel<2>, grid, dim3(kWgThreads), 2 * kWgSlot * 2, s, a);
+      else if (vst == 3) hipLaunchKernelGGL(wgrad_bf16_vst_kernel<3>, grid, dim3(kWgThreads), 2 * kWgSlot * 2, s, a);
+      else if (vst == 4) hipLaunchKernelGGL(wgrad_bf16_vst_kernel<4>, grid, dim3(kWgThreads), 2 * kWgSlot * 2, s, a);
+      else if (ns == 5) hipLaunchKernelGGL(wgrad_bf16_kernel<5>, grid, dim3(kWgThreads), 5 * kWgSlot * 2, s, a);
       else if (ns == 4) hipLaunchKernelGGL(wgrad_bf16_kernel<4>, grid, dim3(kWgThreads), 4 * kWgSlot * 2, s, a);
       else hipLaunchKernelGGL(wgrad_bf16_kernel<3>, grid, dim3(kWgThreads), 3 * kWgSlot * 2, s, a);
     } else {
