@@ -133,6 +133,29 @@ __device__ __forceinline__ float gelu_fast(float x) {
   return x >= 0.f ? x * (1.0f - 0.5f * q) : x * (0.5f * q);
 }
 
+// gelu_fast on two values with packed fp32 math (v_pk_mul / v_pk_fma / v_pk_add: two lanes'
+// worth of work per instruction; the reciprocal and exp2 stay scalar).  The same IEEE operations
+// in the same order as gelu_fast, so the results are bit-identical to it (1 - 0.5 q: 0.5 q is
+// exact, so the fused and the separate forms round alike).
+typedef __attribute__((ext_vector_type(2))) float f32x2v;
+__device__ __forceinline__ f32x2v gelu_fast2(f32x2v x) {
+#pragma clang fp contract(off)
+  const f32x2v a = __builtin_elementwise_abs(x) * 0.70710678118654752440f;
+  const f32x2v d = __builtin_elementwise_fma(f32x2v{0.3275911f, 0.3275911f}, a, f32x2v{1.0f, 1.0f});
+  const f32x2v t = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  f32x2v q = __builtin_elementwise_fma(f32x2v{1.061405429f, 1.061405429f}, t, f32x2v{-1.453152027f, -1.453152027f});
+  q = __builtin_elementwise_fma(q, t, f32x2v{1.421413741f, 1.421413741f});
+  q = __builtin_elementwise_fma(q, t, f32x2v{-0.284496736f, -0.284496736f});
+  q = __builtin_elementwise_fma(q, t, f32x2v{0.254829592f, 0.254829592f});
+  const f32x2v s = ((-a) * a) * 1.4426950408889634f;
+  const f32x2v e = {__builtin_amdgcn_exp2f(s.x), __builtin_amdgcn_exp2f(s.y)};
+  q = q * (t * e);
+  const f32x2v h = 0.5f * q;
+  const f32x2v p = 1.0f - h;
+  const f32x2v m = {x.x >= 0.f ? p.x : h.x, x.y >= 0.f ? p.y : h.y};
+  return x * m;
+}
+
 // d/dx of the exact-erf GELU: Phi(x) + x phi(x)  (the training backward of layers.py:78-85)
 __device__ __forceinline__ float gelu_grad(float x) {
   return 0.5f * (1.0f + erff(x * 0.70710678118654752440f)) + x * 0.39894228040143267794f * expf(-0.5f * x * x);

@@ -2802,12 +2802,12 @@ static bool mlp_split_vst_on() {
 // measured 168 vs 130 us at M = 32 000 — each phase's 48 KiB ring slot is issued only one
 // phase (~0.7 us) ahead of its use while an LDS-DMA fill takes ~1.1 us to land, and LDS has no
 // room for a third slot beside the double-buffered H)
-static bool mlp_ws_on() {
-  static const bool on = [] {
+static int mlp_ws_mode() {  // MDG_MLP_WS = 1 (round 3's kernel) / 2 (round 6's, mlp_ws2_kernel)
+  static const int v = [] {
     const char* e = getenv("MDG_MLP_WS");
-    return e && e[0] == '1';
+    return e ? atoi(e) : 0;
   }();
-  return on;
+  return v;
 }
 
 // MDG_MLP_HC=256: the one-pass fused MLP on 256-wide hidden chunks with 64 x 64 fc1 wave tiles
@@ -2830,6 +2830,308 @@ bool mlp_pre_supported(const mdg_gemm_desc& r, const mdg_gemm_desc& f1, const md
          r.xn_out && r.xn_out == f1.A && f1.lda == 384 && r.xn_mods && r.A && r.W && r.lda % 8 == 0 && r.ldw % 8 == 0;
 }
 
+// ---------------------------------------------------------------------------------------
+// Fused MLP, wave-specialised, round 6 (MDG_MLP_WS=2; large M, one 128-token tile per block).
+// Waves 0-3 ("P") produce H = GELU(xn W1^T + b1) for 32 tokens each, waves 4-7 ("Q") consume it:
+// acc2 += H W2^T for all 128 tokens x 96 outputs each, then the row-LN epilogue.  Wave w and w + 4
+// share a SIMD, so a P wave's GELU issues beside a Q wave's MFMAs instead of in lock-step with
+// every other wave.  Against the round-3 form (mlp_ws_kernel: 65 spilled VGPRs, a 2-slot ring
+// issued one phase ahead, the whole chunk's GELU in one phase):
+//   * the W2 fragments go straight from L2 to the Q waves' registers (each Q wave reads its own
+//     96 rows of W2 once per tile: no replication), issued one phase ahead; LDS then holds a
+//     3-slot ring of W1 slices only (24 KiB each) beside the double-buffered H (2 x 32 KiB);
+//   * a P wave computes its chunk as two 64-hidden halves over two phases each (6 K-steps of 32
+//     per phase), and runs each half's GELU in the phase after the half completes: half A's in
+//     phase 2 of the same chunk, half B's in phase 0 of the next, so every phase carries at most
+//     half a chunk's GELU; Q's fc2 steps over H(c - 1) read hidden 0-63 in phases 0-1 (written in
+//     phase 2 of chunk c - 1) and 64-127 in phases 2-3 (written in phase 0 of chunk c).
+// Phases: 4 (NCH + 1), one block barrier each.  K orders are the lock-step kernel's (fc1 ascending
+// per hidden unit, fc2 ascending over the hidden units), so h and xn are bit-identical to it.
+// timing diagnostics (separate libraries; results wrong): 2 = GELU replaced by the identity,
+// 3 = the Q waves keep their first W2 fragments, 4 = the W1 ring is filled for the first phases only,
+// | 32 = shader-clock stamps of block 0's waves 0 and 4 (into f1.out; tools/ws2_stamps.py),
+// | 512 = no GELU (nothing written to H), | 1024 = the Q waves only keep the barriers
+#ifndef MDG_DIAG_WS2
+#define MDG_DIAG_WS2 0
+#endif
+#ifndef MDG_WS2_PREFETCH
+#define MDG_WS2_PREFETCH 1
+#endif
+#ifndef MDG_WS2_PACKED
+#define MDG_WS2_PACKED 1
+#endif
+#ifndef MDG_WS2_RELOAD_LATE
+#define MDG_WS2_RELOAD_LATE 1
+#endif
+constexpr bool kWs2ReloadLate = MDG_WS2_RELOAD_LATE;
+constexpr int kWs2Img = 64 * 32, kWs2Slot = 6 * kWs2Img;  // bf16 elements: 6 K-step images of 64 W1 rows
+
+template <int NCOL>
+__global__ __launch_bounds__(kWsThreads, 1) void mlp_ws2_kernel(const MlpArgs args) {
+  static_assert(NCOL == 384, "Q waves own 96 output columns each");
+  constexpr int BM = 128, HC = 128, BK = 32, NQ = 6, LDS_ST = NCOL + 4, NSLOT = 3;
+  typedef __attribute__((address_space(3))) void* lds_ptr_t;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  bf16_t* Hb = reinterpret_cast<bf16_t*>(smem);  // [2][BM][HC]: 16-B chunk c of row r at c ^ (r & 15)
+  bf16_t* ring = Hb + 2 * BM * HC;               // [NSLOT][kWs2Slot]
+  float* b1s = reinterpret_cast<float*>(ring + NSLOT * kWs2Slot);  // [F] (read before the first barrier)
+  const mdg_gemm_desc& q = args.f1;              // xn, W1, b1
+  const mdg_gemm_desc& p = args.f2;              // W2, b2 and the row-LN epilogue
+  // (wave index through readfirstlane: the role branch and the buffer-load scalar offsets are
+  // then known wave-uniform; otherwise every buffer load becomes a waterfall loop)
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), wq = wave & 3;
+  const bool isP = wave < 4;
+  const int lr = lane & 15, lg = lane >> 4;
+  const int M = p.M, F = p.K, NCH = F / HC, NPH = 4 * (NCH + 1);
+  const int nwg = (M + BM - 1) / BM;
+  const int xcd = blockIdx.x & 7, loc = blockIdx.x >> 3, q8 = nwg >> 3, r8 = nwg & 7;
+  const int m0 = ((xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc) * BM;
+  const bf16_t* X = reinterpret_cast<const bf16_t*>(q.A);
+  const bf16_t* W1 = reinterpret_cast<const bf16_t*>(q.W);
+  const bf16_t* W2 = reinterpret_cast<const bf16_t*>(p.W);
+  const int ch = (lg ^ ((-(lr >> 2)) & 3)) * 8;  // fragment rows are lr mod 16
+  const float inv_rpm = 1.0f / (float)p.rows_per_mod;
+  float4 h4[2][NCOL / 128];
+  // DIAG 5: shader-clock stamps of waves 0 (P) and 4 (Q) of block 0 into f1.out (u64 [8][512])
+  int ts_i = 0;
+  auto TS = [&]() __attribute__((always_inline)) {
+    if ((MDG_DIAG_WS2 & 32) && blockIdx.x == 0 && (wave == 0 || wave == 4)) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      if (lane == 0) reinterpret_cast<unsigned long long*>(q.out)[wave * 512 + ts_i] = t;
+      ++ts_i;
+    }
+  };
+  TS();
+  for (int i = tid; i < F; i += kWsThreads) b1s[i] = q.bias ? q.bias[i] : 0.f;
+  if (isP) {
+    // W1 pieces of phase ph (chunk ph / 4, half (ph & 3) >> 1, K range 192 (ph & 1)): piece
+    // id = 6 wq + i -> image k3 = id / 4 (K-step), row block id % 4 (16 of the half's 64 rows)
+    const int prow = lane >> 2, pch = lane & 3;
+    const __amdgpu_buffer_rsrc_t w1rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)W1, 0, F * q.ldw * (int)sizeof(bf16_t), 0x00020000);
+    const int w1lane = (prow * q.ldw + ((pch ^ ((-(prow >> 2)) & 3)) * 8)) * (int)sizeof(bf16_t);
+    auto issue = [&](int ph) {  // buffer loads: the piece offsets are scalar, no address VGPRs
+      if (ph >= 4 * NCH || ((MDG_DIAG_WS2 & 31) == 4 && ph >= NSLOT)) return;
+      bf16_t* sl = ring + (ph % NSLOT) * kWs2Slot;
+      const int base = ((ph >> 2) * HC + 64 * ((ph & 3) >> 1)) * q.ldw + 192 * (ph & 1);
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        const int id = 6 * wq + i;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            w1rs, (lds_ptr_t)(sl + (id >> 2) * kWs2Img + 16 * (id & 3) * BK), 16, w1lane,
+            (base + 32 * (id >> 2) + 16 * (id & 3) * q.ldw) * (int)sizeof(bf16_t), 0, 0);
+      }
+    };
+    // the wave's 32 xn rows as the fc1 B operand: xf[k-step][token tile]
+    bf16x8 xf[12][2];
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni) {
+      const bf16_t* xr = X + (size_t)min(m0 + 32 * wq + 16 * ni + lr, M - 1) * q.lda + 8 * lg;
+#pragma unroll
+      for (int kk = 0; kk < 12; ++kk) xf[kk][ni] = *reinterpret_cast<const bf16x8*>(xr + 32 * kk);
+    }
+    f32x4 acc1[8][2];
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) acc1[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
+    issue(0);
+    issue(1);
+    issue(2);
+    // GELU of hidden block HB (0: units 0-63, 1: 64-127) of chunk c -> H[c & 1]
+    auto gelu_half = [&](auto HB, int c) __attribute__((always_inline)) {
+      constexpr int hb0 = 4 * decltype(HB)::value;
+      if (MDG_DIAG_WS2 & 512) return;
+      bf16_t* Hs = Hb + (c & 1) * BM * HC;
+      f32x4 b1v[4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) b1v[m] = *reinterpret_cast<const f32x4*>(b1s + c * HC + 16 * (hb0 + m) + 4 * lg);
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni) {
+          const int hb = 16 * (hb0 + m) + 4 * lg, tok = 32 * wq + 16 * ni + lr;
+          bf16x4 o;
+#pragma unroll
+          for (int r = 0; r < 4; r += 2) {  // packed pairs (gelu_fast2: bit-identical to gelu_fast)
+            const f32x2v v = f32x2v{acc1[hb0 + m][ni][r], acc1[hb0 + m][ni][r + 1]} + f32x2v{b1v[m][r], b1v[m][r + 1]};
+            const f32x2v g = (MDG_DIAG_WS2 & 31) == 2 ? v
+                             : MDG_WS2_PACKED         ? gelu_fast2(v)
+                                                      : f32x2v{gelu_fast(v.x), gelu_fast(v.y)};
+            o[r] = (bf16_t)g.x;
+            o[r + 1] = (bf16_t)g.y;
+          }
+          *reinterpret_cast<bf16x4*>(Hs + tok * HC + (((hb >> 3) ^ (tok & 15)) * 8) + (hb & 7)) = o;
+          acc1[hb0 + m][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+        __builtin_amdgcn_sched_barrier(0);  // one hidden block at a time: bounded temporaries
+      }
+    };
+    // one P phase: 6 K-steps over the slot's 64 hidden rows (half HB, K half KH), 48 MFMAs
+    // (the next K-step's 4 fragments are read while this one's 8 MFMAs issue: two register sets)
+    auto fc1_phase = [&](auto HB, auto KH, int ph) __attribute__((always_inline)) {
+      constexpr int hb0 = 4 * decltype(HB)::value, kk0 = 6 * decltype(KH)::value;
+      const bf16_t* img = ring + (ph % NSLOT) * kWs2Slot + lr * BK + ch;
+      bf16x8 fa[2][4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) fa[0][m] = *reinterpret_cast<const bf16x8*>(img + 16 * m * BK);
+#pragma unroll
+      for (int k3 = 0; k3 < 6; ++k3) {
+        if (k3 + 1 < 6 && MDG_WS2_PREFETCH) {
+#pragma unroll
+          for (int m = 0; m < 4; ++m)
+            fa[(k3 + 1) & 1][m] = *reinterpret_cast<const bf16x8*>(img + (k3 + 1) * kWs2Img + 16 * m * BK);
+        }
+        if (!MDG_WS2_PREFETCH && k3 > 0) {
+#pragma unroll
+          for (int m = 0; m < 4; ++m) fa[k3 & 1][m] = *reinterpret_cast<const bf16x8*>(img + k3 * kWs2Img + 16 * m * BK);
+        }
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+          for (int ni = 0; ni < 2; ++ni)
+            acc1[hb0 + m][ni] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[k3 & 1][m], xf[kk0 + k3][ni], acc1[hb0 + m][ni], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+    // phase end: this wave's pieces of phase ph + 1 landed (the outstanding ones are phase ph + 1's
+    // and ph + 2's: vmcnt(6) leaves the newer six in flight), LDS ops retired, barrier, then phase
+    // ph + 3's pieces into the slot phase ph used (every wave's reads of it retired before the barrier)
+    auto phase_end = [&](int ph) __attribute__((always_inline)) {
+      if (ph + 2 < 4 * NCH) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      TS();
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      TS();
+      issue(ph + 3);
+    };
+    // (phase 0's pieces landed before the first barrier; 1's and 2's in flight)
+    asm volatile("s_waitcnt vmcnt(12) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    TS();
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    for (int c = 0; c < NCH; ++c) {
+      const int ph = 4 * c;
+      if (c > 0) gelu_half(I1{}, c - 1);  // half B of the previous chunk (its acc rows are free for this chunk's B)
+      TS();
+      fc1_phase(I0{}, I0{}, ph);
+      TS();
+      phase_end(ph);
+      fc1_phase(I0{}, I1{}, ph + 1);
+      TS();
+      phase_end(ph + 1);
+      gelu_half(I0{}, c);  // half A of this chunk
+      TS();
+      fc1_phase(I1{}, I0{}, ph + 2);
+      TS();
+      phase_end(ph + 2);
+      fc1_phase(I1{}, I1{}, ph + 3);
+      TS();
+      phase_end(ph + 3);
+    }
+    gelu_half(I1{}, NCH - 1);
+    for (int ph = 4 * NCH; ph < NPH; ++ph) {  // the Q waves' last chunk
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+    auto no_stage = [&](int, float*) {};
+    TS();
+    rowln_fast_epilogue_impl<NCOL, 3, true>(p, no_stage, h4, smem, RowsLinear{m0}, fdiv(m0, p.rows_per_mod, inv_rpm),
+                                            inv_rpm);
+    TS();
+  } else {
+    f32x4 acc2[8][NQ];
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+      for (int nj = 0; nj < NQ; ++nj) acc2[mi][nj] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // W2 B fragments: output row 96 wq + 16 nj + lr, hidden 8 lg .. + 7 of the K-step
+    // (buffer loads: one lane offset in a VGPR, the K-step / fragment offset in an SGPR, so the six
+    // fragment streams cost no address registers beside the 192 accumulators)
+    const __amdgpu_buffer_rsrc_t w2rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)W2, 0, NCOL * p.ldw * (int)sizeof(bf16_t), 0x00020000);
+    const int w2lane = ((96 * wq + lr) * p.ldw + 8 * lg) * (int)sizeof(bf16_t);
+    auto wfrag = [&](int c, int kb, int nj) __attribute__((always_inline)) {
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(
+          w2rs, w2lane, (c * HC + BK * kb + 16 * nj * p.ldw) * (int)sizeof(bf16_t), 0);
+      return __builtin_bit_cast(bf16x8, v);
+    };
+    bf16x8 bw[NQ];
+#pragma unroll
+    for (int nj = 0; nj < NQ; ++nj) bw[nj] = wfrag(0, 0, nj);
+    // P's first chunk: 4 phases without fc2 work (the barriers only)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    for (int ph = 0; ph < 4; ++ph) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+    TS();
+    for (int c = 1; c <= NCH; ++c) {
+      const bf16_t* Hs = Hb + ((c - 1) & 1) * BM * HC;
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this K-step's W2 fragments
+        TS();
+        const int nc = kb < 3 ? c - 1 : c, nkb = (kb + 1) & 3;
+        const bool more = (kb < 3 || c < NCH) && !(MDG_DIAG_WS2 & 1024);
+        // two halves of 4 token tiles; fragment nj is reloaded for the next K-step right after
+        // its last MFMA of the second half (no second fragment set beside the 192 accumulators)
+#pragma unroll
+        for (int hf = 0; hf < ((MDG_DIAG_WS2 & 1024) ? 0 : 2); ++hf) {
+          bf16x8 a[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int row = 16 * (4 * hf + i) + lr;
+            a[i] = *reinterpret_cast<const bf16x8*>(Hs + row * HC + (((kb * 4 + lg) ^ (row & 15)) * 8));
+          }
+#pragma unroll
+          for (int nj = 0; nj < NQ; ++nj) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+              acc2[4 * hf + i][nj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], bw[nj], acc2[4 * hf + i][nj], 0, 0, 0);
+            if (!kWs2ReloadLate && hf == 1 && more && (MDG_DIAG_WS2 & 31) != 3)
+              bw[nj] = wfrag(nc, nkb, nj);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        if (kWs2ReloadLate && more && (MDG_DIAG_WS2 & 31) != 3) {
+#pragma unroll
+          for (int nj = 0; nj < NQ; ++nj) bw[nj] = wfrag(nc, nkb, nj);
+        }
+        TS();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        TS();
+      }
+    }
+    // band b = accumulator rows 16 mi + 4 lg + r with mi in {2b, 2b+1}; columns 96 wq + 16 nj + lr.
+    // Bands 0-2 go to stage regions 0-2 at band 0 (144 accumulator VGPRs freed before the row
+    // work), band 3 to region 0 once band 0 is done
+    auto stage_band = [&](int band, float* stage) {
+      if (band == 1 || band == 2) return;
+#pragma unroll
+      for (int mi = 0; mi < 8; ++mi) {
+        if (band == 0 ? mi >= 6 : mi < 6) continue;
+        float* rg = stage + ((mi >> 1) % 3) * 32 * LDS_ST;
+#pragma unroll
+        for (int nj = 0; nj < NQ; ++nj)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            rg[((mi & 1) * 16 + lg * 4 + r) * LDS_ST + 96 * wq + 16 * nj + lr] = acc2[mi][nj][r];
+      }
+    };
+    TS();
+    rowln_fast_epilogue_impl<NCOL, 3, true>(p, stage_band, h4, smem, RowsLinear{m0}, fdiv(m0, p.rows_per_mod, inv_rpm),
+                                            inv_rpm);
+    TS();
+  }
+}
+
 hipError_t mlp_fused_launch(const mdg_gemm_desc& f1, const mdg_gemm_desc& f2, hipStream_t s, float* part,
                             const mdg_gemm_desc* pre) {
   static bool attr_set = false;
@@ -2839,7 +3141,8 @@ hipError_t mlp_fused_launch(const mdg_gemm_desc& f1, const mdg_gemm_desc& f2, hi
                           reinterpret_cast<const void*>(&mlp_rowln_kernel<384, false, true>),
                           reinterpret_cast<const void*>(&mlp_rowln_kernel<384, true, false, true>),
                           reinterpret_cast<const void*>(&mlp_ws_kernel<384>),
-                          reinterpret_cast<const void*>(&mlp_rowln256_kernel<384>)}) {
+                          reinterpret_cast<const void*>(&mlp_rowln256_kernel<384>),
+                          reinterpret_cast<const void*>(&mlp_ws2_kernel<384>)}) {
       hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       if (e != hipSuccess) return e;
     }
@@ -2866,7 +3169,11 @@ hipError_t mlp_fused_launch(const mdg_gemm_desc& f1, const mdg_gemm_desc& f2, hi
     if (hipError_t e = hipGetLastError()) return e;
     return launch_split_reduce(f2, (const float*)part, a.nsplit, s);
   }
-  if (mlp_ws_on()) {
+  if (mlp_ws_mode() == 2 && f1.N % 128 == 0) {
+    hipLaunchKernelGGL((mlp_ws2_kernel<384>), dim3(tiles), dim3(kWsThreads), 160 * 1024, s, a);
+    return hipGetLastError();
+  }
+  if (mlp_ws_mode() == 1) {
     hipLaunchKernelGGL((mlp_ws_kernel<384>), dim3(tiles), dim3(kWsThreads), kWsSmem, s, a);
     return hipGetLastError();
   }

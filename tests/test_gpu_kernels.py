@@ -120,12 +120,60 @@ def test_gemm_gate_res_fused_layernorm(lib, N, K, M):
     torch.testing.assert_close(xn.float(), xref, rtol=2e-2, atol=2e-2)
 
 
-@pytest.mark.parametrize("M,TL,with_ln", [(512, 256, True), (4000, 4000, True), (300, 150, True), (1000, 200, False)])
+@pytest.mark.parametrize("M,TL,with_ln", [(512, 256, True), (4000, 4000, True), (300, 150, True), (1000, 200, False),
+                                         (8292, 4146, True)])
 def test_mlp_fused_equals_fc1_then_fc2(lib, M, TL, with_ln):
     """mdg_mlp_fused (fc1 + GELU + fc2 + gated residual + next LN in one kernel, the hidden
     activation on chip) against the same two descriptors through mdg_gemm: h and xn
     bit-identical (same K order, same GELU, same bf16 rounding of the hidden activation), and
-    against torch.  Partial last tiles (M % 128 != 0) and tiles spanning two trajectories."""
+    against torch.  Partial last tiles (M % 128 != 0) and tiles spanning two trajectories;
+    M < 8065 takes the split-hidden route, 8292 the one-pass kernel."""
+    _mlp_fused_vs_unfused(lib, M, TL, with_ln)
+
+
+@pytest.mark.parametrize("knob", ["MDG_MLP_WS=2", "MDG_MLP_WS=1", "MDG_MLP_HC=256"])
+def test_mlp_fused_opt_in_variants(knob):
+    """The opt-in one-pass MLP kernels (wave-specialised rounds 3 and 6, 256-wide hidden chunks)
+    are bit-identical to the unfused pair too: run in a child process (the knobs are read once
+    per process); M = 20000 has a partial last tile and 100 trajectory boundaries, M = 32000 fills
+    the chip (250 tiles)."""
+    import subprocess
+    import sys
+
+    k, v = knob.split("=")
+    code = ("import sys; sys.path.insert(0, '.'); from mdgen_finetune_amd import _lib; "
+            "from tests.test_gpu_kernels import _mlp_fused_vs_unfused; "
+            "_mlp_fused_vs_unfused(_lib.load(), 20000, 200, True); _mlp_fused_vs_unfused(_lib.load(), 8292, 4146, False); "
+            "_mlp_fused_vs_unfused(_lib.load(), 32000, 4000, True); "
+            "print('ok')")
+    r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, **{k: v}),
+                       cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))), capture_output=True,
+                       text=True, timeout=180)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
+
+
+def test_mlp_ws2_window_equals_default():
+    """The round-6 wave-specialised MLP (MDG_MLP_WS=2) in the bench's whole inference window (B = 16,
+    two concurrent lanes, hipGraph, 49 Euler steps: 2 x 250-tile launches per layer): the samples
+    equal the default kernel's bit for bit.  Its first form issued ring slot ph + 2 one phase late
+    and waited on the wrong count, a race that left this window non-finite a few times in ten
+    while the single-launch kernel tests passed."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sums = []
+    for env in ({}, {"MDG_MLP_WS": "2"}):
+        r = subprocess.run([sys.executable, "tools/dbg_ws2.py", "2", "1", "16", "50"], env=dict(os.environ, **env),
+                           cwd=root, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        lines = [ln for ln in r.stdout.splitlines() if ln.startswith("lanes=")]
+        assert len(lines) == 2 and all("finite=True" in ln for ln in lines), r.stdout
+        sums.append([ln.split("sum=")[1] for ln in lines])
+    assert sums[0][0] == sums[0][1] == sums[1][0] == sums[1][1], sums
+
+
+def _mlp_fused_vs_unfused(lib, M, TL, with_ln):
     from mdgen_finetune_amd import _lib
 
     C, F = 384, 1536
