@@ -2798,14 +2798,15 @@ static bool mlp_split_vst_on() {
   return on;
 }
 
-// MDG_MLP_WS=1 selects the wave-specialised kernel for large M (A/B knob; off by default: it
-// measured 168 vs 130 us at M = 32 000 — each phase's 48 KiB ring slot is issued only one
-// phase (~0.7 us) ahead of its use while an LDS-DMA fill takes ~1.1 us to land, and LDS has no
-// room for a third slot beside the double-buffered H)
-static int mlp_ws_mode() {  // MDG_MLP_WS = 1 (round 3's kernel) / 2 (round 6's, mlp_ws2_kernel)
+// The one-pass (large-M) fused MLP kernel, MDG_MLP_WS: 2 (default, round 6) mlp_ws2_kernel;
+// 0 the lock-step mlp_rowln_kernel (round 2; then MDG_MLP_HC=256 selects its 256-wide-chunk
+// form); 1 round 3's wave-specialised kernel (measured 168 vs 130 us at M = 32 000: each phase's
+// 48 KiB ring slot is issued only one phase ahead of an LDS-DMA fill that takes ~1.1 us, and its
+// 65 spilled VGPRs).  All three give bit-identical h and xn.
+static int mlp_ws_mode() {
   static const int v = [] {
     const char* e = getenv("MDG_MLP_WS");
-    return e ? atoi(e) : 0;
+    return e ? atoi(e) : 2;
   }();
   return v;
 }

@@ -131,31 +131,31 @@ def test_mlp_fused_equals_fc1_then_fc2(lib, M, TL, with_ln):
     _mlp_fused_vs_unfused(lib, M, TL, with_ln)
 
 
-@pytest.mark.parametrize("knob", ["MDG_MLP_WS=2", "MDG_MLP_WS=1", "MDG_MLP_HC=256"])
+@pytest.mark.parametrize("knob", ["MDG_MLP_WS=0", "MDG_MLP_WS=1", "MDG_MLP_WS=0 MDG_MLP_HC=256"])
 def test_mlp_fused_opt_in_variants(knob):
-    """The opt-in one-pass MLP kernels (wave-specialised rounds 3 and 6, 256-wide hidden chunks)
-    are bit-identical to the unfused pair too: run in a child process (the knobs are read once
-    per process); M = 20000 has a partial last tile and 100 trajectory boundaries, M = 32000 fills
-    the chip (250 tiles)."""
+    """The other one-pass MLP kernels (lock-step round 2, wave-specialised round 3, 256-wide hidden
+    chunks; the default is round 6's wave-specialised kernel) are bit-identical to the unfused pair
+    too: run in a child process (the knobs are read once per process); M = 20000 has a partial
+    last tile and 100 trajectory boundaries, M = 32000 fills the chip (250 tiles)."""
     import subprocess
     import sys
 
-    k, v = knob.split("=")
+    env = dict(os.environ, **dict(kv.split("=") for kv in knob.split()))
     code = ("import sys; sys.path.insert(0, '.'); from mdgen_finetune_amd import _lib; "
             "from tests.test_gpu_kernels import _mlp_fused_vs_unfused; "
             "_mlp_fused_vs_unfused(_lib.load(), 20000, 200, True); _mlp_fused_vs_unfused(_lib.load(), 8292, 4146, False); "
             "_mlp_fused_vs_unfused(_lib.load(), 32000, 4000, True); "
             "print('ok')")
-    r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, **{k: v}),
+    r = subprocess.run([sys.executable, "-c", code], env=env,
                        cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))), capture_output=True,
                        text=True, timeout=180)
     assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
 
 
-def test_mlp_ws2_window_equals_default():
-    """The round-6 wave-specialised MLP (MDG_MLP_WS=2) in the bench's whole inference window (B = 16,
+def test_mlp_ws2_window_equals_lockstep():
+    """The round-6 wave-specialised MLP (the default) in the bench's whole inference window (B = 16,
     two concurrent lanes, hipGraph, 49 Euler steps: 2 x 250-tile launches per layer): the samples
-    equal the default kernel's bit for bit.  Its first form issued ring slot ph + 2 one phase late
+    equal the lock-step kernel's (MDG_MLP_WS=0) bit for bit, twice over.  Its first form issued ring slot ph + 2 one phase late
     and waited on the wrong count, a race that left this window non-finite a few times in ten
     while the single-launch kernel tests passed."""
     import subprocess
@@ -163,7 +163,7 @@ def test_mlp_ws2_window_equals_default():
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sums = []
-    for env in ({}, {"MDG_MLP_WS": "2"}):
+    for env in ({"MDG_MLP_WS": "0"}, {}):
         r = subprocess.run([sys.executable, "tools/dbg_ws2.py", "2", "1", "16", "50"], env=dict(os.environ, **env),
                            cwd=root, capture_output=True, text=True, timeout=300)
         assert r.returncode == 0, r.stderr[-2000:]
