@@ -26,7 +26,7 @@ torch.distributed.run (WORLD_SIZE set; must equal --gpus) each launched process 
 its own rank's workers the same way.  A train_dp leg that fails or times out is reported as
 such in the line; the inference line stands.
 
-Extra fields: "roofline" for the dominant kernel (the fused MLP, mlp_rowln_kernel: fc1 +
+Extra fields: "roofline" for the dominant kernel (the fused MLP, mlp_ws2_kernel: fc1 +
 GELU + fc2 + gated residual + next LN in one launch, the largest share of the step per
 profiles/; live HIP-event timing on the stream the kernel runs on; with MDG_FUSED_MLP=0 the
 fc2 row-LN GEMM instead), "roofline_more" for the next ones (the out_proj row-LN GEMM, the

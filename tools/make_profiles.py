@@ -39,7 +39,7 @@ if os.path.exists(stats) and default_shape:
         # bench.roofline times each roofline kernel in a loop of 50 launches after the timed
         # windows (plus one warm-up launch): those are the last 50 dispatches of its name; the
         # rest ran inside the hipGraph windows.
-        pats = (("mlp_rowln_kernel", "mlp_fused"), ("rowln_qkv_kernel", "rowln_qkv"), ("gemm_rowln_kernel", "gemm_out_proj_rowln"),
+        pats = (("mlp_rowln_kernel", "mlp_fused"), ("mlp_ws2_kernel", "mlp_fused"), ("rowln_qkv_kernel", "rowln_qkv"), ("gemm_rowln_kernel", "gemm_out_proj_rowln"),
                 ("gemm_bf16_b4_kernel<2", "gemm_qkv_temporal"), ("attn_temporal_bf16", "attn_temporal"))
         per = collections.defaultdict(list)
         for r in csv.DictReader(open(trace)):
@@ -73,7 +73,8 @@ if os.path.exists(stats) and default_shape:
 # each roofline kernel's last 50 dispatches are its bench.roofline timing loop (the row-LN
 # family's: the out_proj one; the fc2 one when the MLP is not fused)
 KMAP = {"gemm_bf16_b4_kernel<2": "gemm_qkv_temporal", "attn_temporal_bf16": "attn_temporal",
-        "gemm_rowln_kernel": "gemm_out_proj_rowln", "mlp_rowln_kernel": "mlp_fused", "rowln_qkv_kernel": "rowln_qkv"}
+        "gemm_rowln_kernel": "gemm_out_proj_rowln", "mlp_rowln_kernel": "mlp_fused", "mlp_ws2_kernel": "mlp_fused",
+        "rowln_qkv_kernel": "rowln_qkv"}
 res = collections.defaultdict(dict)
 for cname, scale in (("FETCH_SIZE", 2 * 1024), ("WRITE_SIZE", 1024)):
     p = os.path.join(pmc_dir, f"{cname}_counter_collection.csv")

@@ -7,7 +7,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 D=${PMC_DIR:-gpurun_out/pmc_train}
 mkdir -p $D
-RX=${PMC_REGEX:-"gemm_bf16_b4|wgrad_bf16|split_sum|attn_bwd_fused|attn_temporal_bf16|mlp_rowln|gemm_rowln"}
+RX=${PMC_REGEX:-"gemm_bf16_b4|wgrad_bf16|split_sum|attn_bwd_fused|attn_temporal_bf16|mlp_rowln|mlp_ws2|gemm_rowln"}
 ARGS="bench.py --train --batch 8 --steps 2 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-}"
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 300 rocprofv3 --pmc $C --kernel-include-regex "$RX" --output-format csv -d $D -o $C -- \
