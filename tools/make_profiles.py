@@ -59,7 +59,7 @@ if os.path.exists(stats) and default_shape:
                   "", "| roofline kernel | rocprof avg of the 50 timed dispatches (us) | bench live avg (us) | in-graph avg, every "
                   "launch of this kernel name (us) | in-graph estimate for this launch (us) |",
                   "|---|---|---|---|---|"]
-        for pat, name in pats:
+        for name in dict.fromkeys(n for _, n in pats):
             v = sorted(per.get(name, []))
             if len(v) < 60:
                 continue
