@@ -2850,7 +2850,8 @@ bool mlp_pre_supported(const mdg_gemm_desc& r, const mdg_gemm_desc& f1, const md
 //     phases 2-3.
 // Phases: 4 (NCH + 1), one block barrier each.  K orders are the lock-step kernel's (fc1 ascending
 // per hidden unit, fc2 ascending over the hidden units) and the GELU is gelu_fast's arithmetic,
-// so h and xn are bit-identical to it.  Measured: 114 vs 128 us at M = 32 000.
+// so h and xn are bit-identical to it.  Measured: 115-117 vs 128-129 us standalone at
+// M = 32 000, 99 vs 107 us on the bench's activations.
 constexpr int kWs2Img = 64 * 32, kWs2Slot = 6 * kWs2Img;  // bf16 elements: 6 K-step images of 64 W1 rows
 
 // GELU of hidden block 16 gm .. + 15 of the chunk held in acc (16 units x 2 token tiles of a P

@@ -46,19 +46,21 @@ if os.path.exists(stats) and default_shape:
             for pat, name in pats:
                 if pat in r["Kernel_Name"]:
                     per[name].append((int(r["Dispatch_Id"]), (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3))
-        bench_live = {}
+        bench_live, work = {}, {}
         bl = os.path.join(REPO, "gpurun_out", "prof", "bench_prof.log")
         if os.path.exists(bl):
             try:
                 d = json.loads([x for x in open(bl).read().splitlines() if x.startswith("{")][-1])
                 for rf in [d["roofline"]] + d.get("roofline_more", []):
                     bench_live[rf["kernel"]] = rf["avg_launch_us"]
+                    work[rf["kernel"]] = (rf.get("flops_per_launch"), rf.get("bytes_per_launch"))
             except Exception:
                 pass
         lines += ["", "## Bench roofline kernels: rocprof vs the bench's live HIP-event timing",
                   "", "| roofline kernel | rocprof avg of the 50 timed dispatches (us) | bench live avg (us) | in-graph avg, every "
-                  "launch of this kernel name (us) | in-graph estimate for this launch (us) |",
-                  "|---|---|---|---|---|"]
+                  "launch of this kernel name (us) | in-graph estimate for this launch (us) | in-graph fraction of the "
+                  "MFMA roof (2.5 PF) / of HBM (8 TB/s), algorithmic work |",
+                  "|---|---|---|---|---|---|"]
         for name in dict.fromkeys(n for _, n in pats):
             v = sorted(per.get(name, []))
             if len(v) < 60:
@@ -66,8 +68,11 @@ if os.path.exists(stats) and default_shape:
             loop = [x[1] for x in v[-50:]]
             graph = [x[1] for x in v[:-51]]
             # (with the fused MLP the row-LN kernel serves only out_proj, x2 per layer)
+            g = sum(graph) / len(graph)
+            fl, by = work.get(name, (None, None))
+            fr = (f"{fl / (g * 1e-6) / 2.5e15:.3f} / {by / (g * 1e-6) / 8e12:.3f}" if fl and by else "n/a")
             lines.append(f"| {name} | {sum(loop) / len(loop):.1f} | {bench_live.get(name, 'n/a')} | "
-                         f"{sum(graph) / len(graph):.1f} | {sum(graph) / len(graph):.1f} |")
+                         f"{g:.1f} | {g:.1f} | {fr} |")
     open(os.path.join(out, f"r{rr}_summary.md"), "w").write("\n".join(lines) + "\n")
 
 # each roofline kernel's last 50 dispatches are its bench.roofline timing loop (the row-LN
