@@ -3132,7 +3132,8 @@ hipError_t mlp_fused_launch(const mdg_gemm_desc& f1, const mdg_gemm_desc& f2, hi
     if (hipError_t e = hipGetLastError()) return e;
     return launch_split_reduce(f2, (const float*)part, a.nsplit, s);
   }
-  if (mlp_ws_mode() == 2 && f1.N % 128 == 0) {
+  // (H 64 KiB + the W1 ring 72 KiB + b1: F <= 6 144 for the wave-specialised kernel)
+  if (mlp_ws_mode() == 2 && (size_t)2 * 128 * 128 * 2 + (size_t)3 * kWs2Slot * 2 + (size_t)f1.N * 4 <= 160 * 1024) {
     hipLaunchKernelGGL((mlp_ws2_kernel<384>), dim3(tiles), dim3(kWsThreads), 160 * 1024, s, a);
     return hipGetLastError();
   }

@@ -152,6 +152,14 @@ def test_mlp_fused_opt_in_variants(knob):
     assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
 
 
+@pytest.mark.parametrize("F", [6144, 7168])
+def test_mlp_fused_wide_hidden(lib, F):
+    """Hidden widths at the wave-specialised kernel's LDS limit (F = 6 144: H + W1 ring + b1 =
+    160 KiB) and past it (7 168: the launcher takes the lock-step kernel, whose limit is 8 192):
+    still bit-identical to fc1 then fc2."""
+    _mlp_fused_vs_unfused(lib, 8292, 4146, True, F=F)
+
+
 def test_mlp_ws2_window_equals_lockstep():
     """The round-6 wave-specialised MLP (the default) in the bench's whole inference window (B = 16,
     two concurrent lanes, hipGraph, 49 Euler steps: 2 x 250-tile launches per layer): the samples
@@ -173,10 +181,10 @@ def test_mlp_ws2_window_equals_lockstep():
     assert sums[0][0] == sums[0][1] == sums[1][0] == sums[1][1], sums
 
 
-def _mlp_fused_vs_unfused(lib, M, TL, with_ln):
+def _mlp_fused_vs_unfused(lib, M, TL, with_ln, F=1536):
     from mdgen_finetune_amd import _lib
 
-    C, F = 384, 1536
+    C = 384
     g = torch.Generator(device="cuda").manual_seed(M + TL)
     xn = torch.randn(M, C, device="cuda", generator=g).to(torch.bfloat16)
     W1 = (torch.randn(F, C, device="cuda", generator=g) / math.sqrt(C)).to(torch.bfloat16)
