@@ -172,7 +172,7 @@ def test_mlp_ws2_window_equals_lockstep():
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sums = []
     for env in ({"MDG_MLP_WS": "0"}, {}):
-        r = subprocess.run([sys.executable, "tools/dbg_ws2.py", "2", "1", "16", "50"], env=dict(os.environ, **env),
+        r = subprocess.run([sys.executable, "tools/window_probe.py", "2", "1", "16", "50"], env=dict(os.environ, **env),
                            cwd=root, capture_output=True, text=True, timeout=300)
         assert r.returncode == 0, r.stderr[-2000:]
         lines = [ln for ln in r.stdout.splitlines() if ln.startswith("lanes=")]

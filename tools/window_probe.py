@@ -1,5 +1,5 @@
 """Finite / checksum probe of the inference window (the bench's model and inputs) for A/B of
-MLP kernel variants: python tools/dbg_ws2.py LANES GRAPH(0|1) [B] [NUM_STEPS]"""
+MLP kernel variants: python tools/window_probe.py LANES GRAPH(0|1) [B] [NUM_STEPS]"""
 import os
 import sys
 
